@@ -1,0 +1,605 @@
+/*
+ * amx_oracle.c -- CPU restatement of the reference's mastering hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity oracle: it may be linked,
+ * loaded or executed only by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg, as the checker.  The product path (libamx.so + amx/) never
+ * calls it.
+ *
+ * Pinning: the per-chunk stages (analog, EQ, width, int16 conversions, crossover,
+ * compressor, overlay) are checked bit-for-bit against golden vectors produced by
+ * running the reference's own audio_mastering_engine.py (tests/golden/, generator
+ * tests/golden/make_golden.py).  The ffmpeg stages (loudnorm measurement/linear
+ * gain, alimiter) have NO reference code or fixtures in /root/reference and no
+ * ffmpeg binary exists here: their restatement below follows the published
+ * libebur128 / FFmpeg af_loudnorm.c / af_alimiter.c algorithms and is
+ * "parity unpinned" beyond the EBU Tech 3341/3342 known answers in the tests.
+ *
+ * Floating-point operation ORDER follows the reference exactly (scipy's
+ * _linear_filter / _sosfilt inner loops, numpy dtype promotion, CPython audioop).
+ * Build with -ffp-contract=off so no FMA contraction changes rounding.
+ * All citations are audio_mastering_engine.py:<line> unless noted.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <float.h>
+
+#define EXPORT __attribute__((visibility("default")))
+
+/* ---------------------------------------------------------------- filters */
+
+/* scipy.signal.lfilter DF-II-transposed inner loop for a 2nd-order ba filter,
+ * zero initial state, a[0] == 1 (butter output).  Order of operations is
+ * scipy's _linear_filter:  y = Z0 + b0*x;  Z0 = Z1 + x*b1 - y*a1;  Z1 = x*b2 - y*a2.
+ * Used by apply_shelf_filter (:286). */
+typedef struct { double z0, z1; } lf_state;
+
+static inline double lf_step(const double *b, const double *a, lf_state *s, double x) {
+    double y = s->z0 + b[0] * x;
+    s->z0 = (s->z1 + x * b[1]) - y * a[1];
+    s->z1 = x * b[2] - y * a[2];
+    return y;
+}
+
+/* scipy.signal.sosfilt (_sosfilt) inner loop, one section:
+ *   x_new = b0*x + zi0;  zi0 = b1*x - a1*x_new + zi1;  zi1 = b2*x - a2*x_new.
+ * sos rows are [b0 b1 b2 a0 a1 a2] with a0 == 1.  Used at :296 and :303. */
+static inline double sos_step(const double *sec, double *zi, double x) {
+    double xn = sec[0] * x + zi[0];
+    zi[0] = (sec[1] * x - sec[4] * xn) + zi[1];
+    zi[1] = sec[2] * x - sec[5] * xn;
+    return xn;
+}
+
+/* float_array_to_audio_segment (:254-257) for float32 arrays:
+ * np.clip(x,-1,1) * 32767 in float32, .astype(int16) truncates toward zero. */
+static inline int16_t f32_to_s16(float x) {
+    float v = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
+    v = v * 32767.0f;
+    return (int16_t)v;
+}
+/* same for float64 arrays (analog character :266, crossover bands :305) */
+static inline int16_t f64_to_s16(double x) {
+    double v = x < -1.0 ? -1.0 : (x > 1.0 ? 1.0 : x);
+    v = v * 32767.0;
+    return (int16_t)v;
+}
+
+/* ------------------------------------------------------- analog character */
+/* apply_analog_character (:258-266).  x = s16/32768 (f32, :253); tanh(x*drive)
+ * in float32 -- taken from `tanh_lut` (65536 float32 values indexed by s16+32768,
+ * built from numpy's own float32 tanh by the caller); then two shelf filters
+ * whose lfilter runs along axis -1, i.e. ACROSS THE TWO CHANNELS of each frame
+ * (:264-265): a length-2 sequence per frame, zero state per frame.
+ * Both shelves have gain_db > 0, so :288 applies:  x + (y - x)*(g - 1). */
+EXPORT void orc_analog(const int16_t *in, int64_t n, const float *tanh_lut,
+                       const double *b_lo, const double *a_lo, double g_lo,
+                       const double *b_hi, const double *a_hi, double g_hi,
+                       int16_t *out) {
+    const double glo1 = g_lo - 1.0, ghi1 = g_hi - 1.0;
+    for (int64_t i = 0; i < n; i++) {
+        double x0 = (double)tanh_lut[(int)in[2 * i] + 32768];
+        double x1 = (double)tanh_lut[(int)in[2 * i + 1] + 32768];
+        lf_state s = {0.0, 0.0};
+        double y0 = lf_step(b_lo, a_lo, &s, x0);
+        double y1 = lf_step(b_lo, a_lo, &s, x1);
+        double u0 = x0 + (y0 - x0) * glo1;
+        double u1 = x1 + (y1 - x1) * glo1;
+        lf_state t = {0.0, 0.0};
+        double v0 = lf_step(b_hi, a_hi, &t, u0);
+        double v1 = lf_step(b_hi, a_hi, &t, u1);
+        double w0 = u0 + (v0 - u0) * ghi1;
+        double w1 = u1 + (v1 - u1) * ghi1;
+        out[2 * i] = f64_to_s16(w0);
+        out[2 * i + 1] = f64_to_s16(w1);
+    }
+}
+
+/* ------------------------------------------------------------------- EQ */
+/* _apply_eq_to_channel (:277-282): four stages in order, each skipped when its
+ * gain is 0 (:284, :291).  kind: 0 = skipped, 1 = shelf (ba, lfilter, :283-289),
+ * 2 = peak (4 SOS band-pass, sosfilt, :290-298).
+ * coef layout per stage: kind 1 -> b[3], a[3];  kind 2 -> sos[4][6].
+ * Numpy dtype promotion: the channel enters as float32; the first ACTIVE stage
+ * sees a float32 input, later stages float64.  That matters only for the
+ * negative-gain shelf, where `samples * gain` (:289) is a float32 product when
+ * `samples` is float32 (NEP 50: the Python float is cast to float32).
+ * The final float64 result is stored back into the float32 column (:274). */
+typedef struct {
+    int kind[4];
+    double gain_db[4];
+    double g[4];          /* 10**(gain_db/20) as computed by Python */
+    double coef[4][24];
+} orc_eq_t;
+
+EXPORT void orc_eq_channel(const float *in, int64_t n, int stride, const orc_eq_t *eq,
+                           float *out) {
+    lf_state ls[4];
+    double zs[4][4][2];
+    memset(ls, 0, sizeof(ls));
+    memset(zs, 0, sizeof(zs));
+    for (int64_t i = 0; i < n; i++) {
+        float xf = in[i * stride];
+        double x = (double)xf;
+        int first = 1;
+        for (int st = 0; st < 4; st++) {
+            int k = eq->kind[st];
+            if (k == 0) continue;
+            const double *c = eq->coef[st];
+            if (k == 1) {
+                double y = lf_step(c, c + 3, &ls[st], x);
+                double g = eq->g[st];
+                if (eq->gain_db[st] > 0) {
+                    x = x + (y - x) * (g - 1.0);
+                } else {
+                    double xg = first ? (double)(xf * (float)g) : x * g;
+                    x = xg + (y - xg);
+                }
+            } else {
+                double y = x;
+                for (int s = 0; s < 4; s++) y = sos_step(c + 6 * s, zs[st][s], y);
+                x = x + y * (eq->g[st] - 1.0);
+            }
+            first = 0;
+        }
+        out[i * stride] = first ? xf : (float)x;
+    }
+}
+
+/* apply_stereo_width (:267-271), float32 M/S with clip. */
+EXPORT void orc_width(float *lr, int64_t n, float w) {
+    for (int64_t i = 0; i < n; i++) {
+        float l = lr[2 * i], r = lr[2 * i + 1];
+        float mid = (l + r) / 2.0f, side = (l - r) / 2.0f;
+        side = side * w;
+        float nl = mid + side, nr = mid - side;
+        lr[2 * i] = nl < -1.0f ? -1.0f : (nl > 1.0f ? 1.0f : nl);
+        lr[2 * i + 1] = nr < -1.0f ? -1.0f : (nr > 1.0f ? 1.0f : nr);
+    }
+}
+
+EXPORT void orc_f32_to_s16(const float *x, int64_t n, int16_t *out) {
+    for (int64_t i = 0; i < n; i++) out[i] = f32_to_s16(x[i]);
+}
+
+/* ------------------------------------------------------------ crossover */
+/* apply_multiband_compressor (:300-305): x = s16/32768 (float32, :253);
+ * low = sosfilt(butter(4,250,'lowpass',sos), x, axis=0); high likewise at 4 kHz
+ * 'highpass' (2 SOS each, float64); mid = x - low - high; each band -> int16. */
+EXPORT void orc_crossover(const int16_t *p16, int64_t n, const double *lo_sos,
+                          const double *hi_sos, int16_t *lo, int16_t *mid, int16_t *hi) {
+    for (int c = 0; c < 2; c++) {
+        double zl[2][2] = {{0, 0}, {0, 0}}, zh[2][2] = {{0, 0}, {0, 0}};
+        for (int64_t i = 0; i < n; i++) {
+            float xf = (float)p16[2 * i + c] / 32768.0f;
+            double x = (double)xf;
+            double l = x, h = x;
+            for (int s = 0; s < 2; s++) l = sos_step(lo_sos + 6 * s, zl[s], l);
+            for (int s = 0; s < 2; s++) h = sos_step(hi_sos + 6 * s, zh[s], h);
+            double m = (x - l) - h;
+            lo[2 * i + c] = f64_to_s16(l);
+            mid[2 * i + c] = f64_to_s16(m);
+            hi[2 * i + c] = f64_to_s16(h);
+        }
+    }
+}
+
+/* ----------------------------------------------------------- compressor */
+/* CPython audioop.mul's clamp (Modules/audioop.c fbound): > max -> max,
+ * < min+1 -> min, then floor. */
+static inline int16_t audioop_mul16(int v, double factor) {
+    double val = (double)v * factor;
+    if (val > 32767.0) val = 32767.0;
+    else if (val < -32768.0 + 1.0) val = -32768.0;
+    return (int16_t)(int)floor(val);
+}
+
+/* pydub.effects.compress_dynamic_range (pydub 0.25.1, called at :306-308),
+ * restated:  thresh_rms = 32768 * 10**(T/20); look_frames = int(5*(fs/1000.0));
+ * per frame i: rms of frames [max(i-L,0), i) via audioop.rms (double sum of
+ * squares -- exact integer here -- / sample count, sqrt, truncating (unsigned)),
+ * over = max(20*log(rms/thr,10), 0) (0 if rms==0; math.log(x,10) = log(x)/log(10)),
+ * max_att = (1 - 1/ratio)*over; inc = max_att/(5*fs/1000.0), dec = max_att/(50*fs/1000.0);
+ * attack if rms > thr and att <= max_att (capped at max_att) else release (floored at 0);
+ * if att != 0 the frame is audioop.mul'ed by 10**(-att/20).
+ * If att_trace != NULL the per-frame attenuation is written there. */
+EXPORT void orc_compress(const int16_t *in, int64_t n, int fs, double threshold, double ratio,
+                         int16_t *out, double *att_trace) {
+    const double thr = 32768.0 * pow(10.0, threshold / 20.0);
+    const int64_t L = (int64_t)(5.0 * (fs / 1000.0));
+    const double A = 5.0 * (fs / 1000.0), R = 50.0 * (fs / 1000.0);
+    const double k = 1.0 - (1.0 / ratio);
+    const double ln10 = log(10.0);
+    int64_t S = 0;   /* exact sum of squares of the window */
+    double att = 0.0;
+    for (int64_t i = 0; i < n; i++) {
+        if (i > 0) {
+            int64_t a = in[2 * (i - 1)], b = in[2 * (i - 1) + 1];
+            S += a * a + b * b;
+        }
+        if (i - L - 1 >= 0) {
+            int64_t a = in[2 * (i - L - 1)], b = in[2 * (i - L - 1) + 1];
+            S -= a * a + b * b;
+        }
+        int64_t lo = i - L < 0 ? 0 : i - L;
+        int64_t cnt = 2 * (i - lo);
+        unsigned int rms = cnt ? (unsigned int)sqrt((double)S / (double)cnt) : 0u;
+        double over = 0.0;
+        if (rms != 0) {
+            double db = 20 * (log((double)rms / thr) / ln10);
+            over = db > 0 ? db : (db == 0 ? db : 0.0);
+        }
+        double m = k * over;
+        double inc = m / A, dec = m / R;
+        if ((double)rms > thr && att <= m) {
+            att += inc;
+            att = att < m ? att : m;
+        } else {
+            att -= dec;
+            att = att > 0 ? att : 0.0;
+        }
+        if (att_trace) att_trace[i] = att;
+        if (att != 0.0) {
+            double f = pow(10.0, (-att) / 20.0);
+            out[2 * i] = audioop_mul16(in[2 * i], f);
+            out[2 * i + 1] = audioop_mul16(in[2 * i + 1], f);
+        } else {
+            out[2 * i] = in[2 * i];
+            out[2 * i + 1] = in[2 * i + 1];
+        }
+    }
+}
+
+/* --------------------------------------------------------------- overlay */
+/* pydub AudioSegment.__len__ / __getitem__ ms rounding used by overlay (:309):
+ * int(round(1000*(n/fs)) * (fs/1000.0)) frames (round = half-to-even). */
+EXPORT int64_t orc_overlay_len(int64_t n, int fs) {
+    double ms = nearbyint(1000.0 * ((double)n / (double)fs));
+    return (int64_t)(ms * (fs / 1000.0));
+}
+
+static inline int16_t sat16(int v) { return (int16_t)(v > 32767 ? 32767 : (v < -32768 ? -32768 : v)); }
+
+/* low.overlay(mid).overlay(high) (:309): audioop.add (saturating) over the common
+ * length; seg1 is first ms-rounded (zero-padded or truncated).  Returns out frames. */
+EXPORT int64_t orc_overlay3(const int16_t *lo, const int16_t *mid, const int16_t *hi,
+                            int64_t n, int fs, int16_t *out) {
+    int64_t n1 = orc_overlay_len(n, fs);
+    int64_t n2 = orc_overlay_len(n1, fs);
+    int64_t nn = n1 < n ? n1 : n;
+    for (int64_t i = 0; i < 2 * nn; i++) out[i] = sat16((int)lo[i] + (int)mid[i]);
+    for (int64_t i = 2 * nn; i < 2 * n1; i++) out[i] = 0;
+    /* second overlay on the n1-frame intermediate (ms-rounded again to n2) */
+    for (int64_t i = 2 * n1; i < 2 * n2; i++) out[i] = 0;
+    int64_t m = n2 < n ? n2 : n;
+    for (int64_t i = 0; i < 2 * m; i++) out[i] = sat16((int)out[i] + (int)hi[i]);
+    return n2;
+}
+
+/* ------------------------------------------------------- chunk composition */
+typedef struct {
+    int fs;
+    int analog_on;
+    double an_b_lo[3], an_a_lo[3], an_g_lo, an_b_hi[3], an_a_hi[3], an_g_hi;
+    const float *tanh_lut;
+    orc_eq_t eq;
+    int width_on;
+    float width;
+    int mb_on;
+    double xlo[12], xhi[12];
+    double thr_db[3], ratio[3];
+} orc_chunk_t;
+
+/* the chunk body, audio_mastering_engine.py:189-197, on an s16 stereo chunk.
+ * `out` must hold max(n, overlay_len(n)) + 8 frames.  Returns output frames. */
+EXPORT int64_t orc_chunk(const orc_chunk_t *p, const int16_t *in16, int64_t n, int16_t *out) {
+    int16_t *a16 = (int16_t *)malloc(sizeof(int16_t) * 2 * (n + 1));
+    float *f = (float *)malloc(sizeof(float) * 2 * (n + 1));
+    const int16_t *src = in16;
+    if (p->analog_on) {
+        orc_analog(in16, n, p->tanh_lut, p->an_b_lo, p->an_a_lo, p->an_g_lo,
+                   p->an_b_hi, p->an_a_hi, p->an_g_hi, a16);
+        src = a16;
+    }
+    for (int64_t i = 0; i < 2 * n; i++) f[i] = (float)src[i] / 32768.0f;
+    orc_eq_channel(f, n, 2, &p->eq, f);
+    orc_eq_channel(f + 1, n, 2, &p->eq, f + 1);
+    if (p->width_on) orc_width(f, n, p->width);
+    int64_t nout = n;
+    if (!p->mb_on) {
+        orc_f32_to_s16(f, 2 * n, out);
+    } else {
+        int16_t *p16 = a16;
+        orc_f32_to_s16(f, 2 * n, p16);
+        int16_t *b = (int16_t *)malloc(sizeof(int16_t) * 12 * (n + 1));
+        int16_t *lo = b, *mi = b + 2 * (n + 1), *hi = b + 4 * (n + 1);
+        int16_t *loc = b + 6 * (n + 1), *mic = b + 8 * (n + 1), *hic = b + 10 * (n + 1);
+        orc_crossover(p16, n, p->xlo, p->xhi, lo, mi, hi);
+        orc_compress(lo, n, p->fs, p->thr_db[0], p->ratio[0], loc, NULL);
+        orc_compress(mi, n, p->fs, p->thr_db[1], p->ratio[1], mic, NULL);
+        orc_compress(hi, n, p->fs, p->thr_db[2], p->ratio[2], hic, NULL);
+        nout = orc_overlay3(loc, mic, hic, n, p->fs, out);
+        free(b);
+    }
+    free(a16);
+    free(f);
+    return nout;
+}
+
+/* ========================================================================
+ * ffmpeg stages -- restated from the published FFmpeg sources (not in the
+ * container).  PARITY UNPINNED: no ffmpeg binary and no reference fixtures.
+ * ======================================================================== */
+
+/* ---------------------------------------------------- libebur128 (ffmpeg) */
+static double hist_energies[1000], hist_bounds[1001];
+static int hist_init_done = 0;
+EXPORT void orc_ebur128_tables(double *energies, double *bounds) {
+    if (!hist_init_done) {
+        hist_bounds[0] = pow(10.0, (-70.0 + 0.691) / 10.0);
+        for (int i = 0; i < 1000; ++i)
+            hist_energies[i] = pow(10.0, ((double)i / 10.0 - 69.95 + 0.691) / 10.0);
+        for (int i = 1; i < 1001; ++i)
+            hist_bounds[i] = pow(10.0, ((double)i / 10.0 - 70.0 + 0.691) / 10.0);
+        hist_init_done = 1;
+    }
+    if (energies) memcpy(energies, hist_energies, sizeof(hist_energies));
+    if (bounds) memcpy(bounds, hist_bounds, sizeof(hist_bounds));
+}
+
+static size_t find_hist_index(double energy) {
+    size_t lo = 0, hi = 1000, mid;
+    do {
+        mid = (lo + hi) / 2;
+        if (energy >= hist_bounds[mid]) lo = mid; else hi = mid;
+    } while (hi - lo != 1);
+    return lo;
+}
+
+/* K-weighting coefficients (libebur128 ebur128_init_filter): b[5], a[5]. */
+EXPORT void orc_kweight_coefs(int fs, double *b, double *a) {
+    double f0 = 1681.974450955533, G = 3.999843853973347, Q = 0.7071752369554196;
+    double K = tan(M_PI * f0 / (double)fs);
+    double Vh = pow(10.0, G / 20.0);
+    double Vb = pow(Vh, 0.4996667741545416);
+    double pb[3] = {0.0, 0.0, 0.0}, pa[3] = {1.0, 0.0, 0.0};
+    double rb[3] = {1.0, -2.0, 1.0}, ra[3] = {1.0, 0.0, 0.0};
+    double a0 = 1.0 + K / Q + K * K;
+    pb[0] = (Vh + Vb * K / Q + K * K) / a0;
+    pb[1] = 2.0 * (K * K - Vh) / a0;
+    pb[2] = (Vh - Vb * K / Q + K * K) / a0;
+    pa[1] = 2.0 * (K * K - 1.0) / a0;
+    pa[2] = (1.0 - K / Q + K * K) / a0;
+    f0 = 38.13547087602444;
+    Q = 0.5003270373238773;
+    K = tan(M_PI * f0 / (double)fs);
+    ra[1] = 2.0 * (K * K - 1.0) / (1.0 + K / Q + K * K);
+    ra[2] = (1.0 - K / Q + K * K) / (1.0 + K / Q + K * K);
+    b[0] = pb[0] * rb[0];
+    b[1] = pb[0] * rb[1] + pb[1] * rb[0];
+    b[2] = pb[0] * rb[2] + pb[1] * rb[1] + pb[2] * rb[0];
+    b[3] = pb[1] * rb[2] + pb[2] * rb[1];
+    b[4] = pb[2] * rb[2];
+    a[0] = pa[0] * ra[0];
+    a[1] = pa[0] * ra[1] + pa[1] * ra[0];
+    a[2] = pa[0] * ra[2] + pa[1] * ra[1] + pa[2] * ra[0];
+    a[3] = pa[1] * ra[2] + pa[2] * ra[1];
+    a[4] = pa[2] * ra[2];
+}
+
+/* Streaming libebur128 (MODE_I | MODE_LRA | MODE_SAMPLE_PEAK) over an s16 track
+ * fed as doubles x/32768 (what loudnorm receives, at the native rate here --
+ * ffmpeg's loudnorm pass 1 resamples to 192 kHz first: not reproduced).
+ * Outputs the gating-block histogram, the short-term (LRA) histogram, per
+ * channel sample peak and the number of gating blocks. */
+EXPORT void orc_ebur128(const int16_t *x, int64_t n, int fs, int channels,
+                        uint64_t *hist, uint64_t *st_hist, double *peak,
+                        int64_t *n_blocks) {
+    orc_ebur128_tables(NULL, NULL);
+    double b[5], a[5];
+    orc_kweight_coefs(fs, b, a);
+    const size_t h100 = (size_t)((fs + 5) / 10);
+    size_t ring_frames = (size_t)fs * 3000 / 1000;
+    if (ring_frames % h100) ring_frames = (ring_frames + h100) - (ring_frames % h100);
+    double *ring = (double *)calloc(ring_frames * channels, sizeof(double));
+    double v[8][5];
+    memset(v, 0, sizeof(v));
+    memset(hist, 0, 1000 * sizeof(uint64_t));
+    memset(st_hist, 0, 1000 * sizeof(uint64_t));
+    for (int c = 0; c < channels; c++) peak[c] = 0.0;
+    size_t idx = 0;               /* audio_data_index, in samples */
+    size_t needed = h100 * 4;
+    size_t st_counter = 0;
+    int64_t nb = 0;
+    int64_t pos = 0;
+    while (pos < n) {
+        size_t take = (size_t)(n - pos) >= needed ? needed : (size_t)(n - pos);
+        /* sample peak */
+        for (int c = 0; c < channels; c++) {
+            double mx = 0.0;
+            for (size_t i = 0; i < take; i++) {
+                double s = (double)x[(pos + i) * channels + c] * (1.0 / 32768.0);
+                if (s > mx) mx = s; else if (-s > mx) mx = -1.0 * s;
+            }
+            if (mx > peak[c]) peak[c] = mx;
+        }
+        /* K filter (4th-order DF-II as in libebur128) */
+        for (int c = 0; c < channels; c++) {
+            for (size_t i = 0; i < take; i++) {
+                double s = (double)x[(pos + i) * channels + c] * (1.0 / 32768.0);
+                v[c][0] = s - a[1] * v[c][1] - a[2] * v[c][2] - a[3] * v[c][3] - a[4] * v[c][4];
+                ring[idx + i * channels + c] = b[0] * v[c][0] + b[1] * v[c][1] + b[2] * v[c][2] +
+                                               b[3] * v[c][3] + b[4] * v[c][4];
+                v[c][4] = v[c][3]; v[c][3] = v[c][2]; v[c][2] = v[c][1]; v[c][1] = v[c][0];
+            }
+            for (int k = 1; k < 5; k++) v[c][k] = fabs(v[c][k]) < DBL_MIN ? 0.0 : v[c][k];
+        }
+        pos += (int64_t)take;
+        idx += take * channels;
+        st_counter += take;
+        if (take == needed) {
+            /* gating block of 4*h100 frames (ebur128_calc_gating_block) */
+            for (int pass = 0; pass < 2; pass++) {
+                size_t fpb = pass == 0 ? h100 * 4 : h100 * 30;
+                if (pass == 1 && st_counter != h100 * 30) continue;
+                double sum = 0.0;
+                for (int c = 0; c < channels; c++) {
+                    double cs = 0.0;
+                    if (idx < fpb * channels) {
+                        for (size_t i = 0; i < idx / channels; ++i)
+                            cs += ring[i * channels + c] * ring[i * channels + c];
+                        for (size_t i = ring_frames - (fpb - idx / channels); i < ring_frames; ++i)
+                            cs += ring[i * channels + c] * ring[i * channels + c];
+                    } else {
+                        for (size_t i = idx / channels - fpb; i < idx / channels; ++i)
+                            cs += ring[i * channels + c] * ring[i * channels + c];
+                    }
+                    sum += cs;
+                }
+                sum /= (double)fpb;
+                if (pass == 0) {
+                    nb++;
+                    if (sum >= hist_bounds[0]) ++hist[find_hist_index(sum)];
+                } else {
+                    if (sum >= hist_bounds[0]) ++st_hist[find_hist_index(sum)];
+                    st_counter = h100 * 20;
+                }
+            }
+            needed = h100;
+            if (idx == ring_frames * channels) idx = 0;
+        } else {
+            needed -= take;
+        }
+    }
+    *n_blocks = nb;
+    free(ring);
+}
+
+/* ------------------------------------------------------------ alimiter */
+/* FFmpeg af_alimiter.c filter_frame(), restated for interleaved doubles with
+ * asc (auto release) off -- the reference passes only
+ * level_in=1:level_out=1:limit=0.98:attack=5:release=50 (:223), so
+ * asc=0, level (auto level)=1, latency=0.  Input s16 -> double x/32768,
+ * output double -> s16 llrint(x*32768) clipped.  Output is the input delayed
+ * by buffer_size/channels - 1 frames (no latency compensation). */
+EXPORT void orc_alimiter(const int16_t *x, int64_t n, int fs, int channels,
+                         double level_in, double level_out, double limit,
+                         double attack_ms, double release_ms, int auto_level,
+                         int16_t *out) {
+    double attack = attack_ms / 1000.0, release = release_ms / 1000.0;
+    int buffer_size = (int)(fs * attack * channels);
+    buffer_size -= buffer_size % channels;
+    int max_size = (int)((int64_t)fs * 100 / 1000) * channels; /* av_rescale(sr,100,1000)*ch */
+    if (max_size < buffer_size + channels) max_size = buffer_size + channels;
+    double *buffer = (double *)calloc((size_t)max_size, sizeof(double));
+    double *nextdelta = (double *)calloc((size_t)max_size, sizeof(double));
+    int *nextpos = (int *)malloc(sizeof(int) * (size_t)max_size);
+    for (int i = 0; i < max_size; i++) nextpos[i] = -1;
+    double att = 1.0, delta = 0.0;
+    int pos = 0, nextiter = 0, nextlen = 0;
+    double level = auto_level ? 1 / limit : 1;
+    for (int64_t nn = 0; nn < n; nn++) {
+        const int16_t *src = x + nn * channels;
+        double dst[8];
+        double peak = 0;
+        for (int c = 0; c < channels; c++) {
+            double sample = ((double)src[c] * (1.0 / 32768.0)) * level_in;
+            buffer[pos + c] = sample;
+            peak = fmax(peak, fabs(sample));
+        }
+        if (peak > limit) {
+            double patt = fmin(limit / peak, 1.);
+            double rdelta = (1.0 - patt) / (fs * release);
+            double d = (limit / peak - att) / buffer_size * channels;
+            int found = 0, i;
+            if (d < delta) {
+                delta = d;
+                nextpos[0] = pos;
+                nextpos[1] = -1;
+                nextdelta[0] = rdelta;
+                nextlen = 1;
+                nextiter = 0;
+            } else {
+                for (i = nextiter; i < nextiter + nextlen; i++) {
+                    int j = i % buffer_size;
+                    double ppeak = 0, pdelta;
+                    for (int c = 0; c < channels; c++) ppeak = fmax(ppeak, fabs(buffer[nextpos[j] + c]));
+                    pdelta = (limit / peak - limit / ppeak) /
+                             (((buffer_size - nextpos[j] + pos) % buffer_size) / channels);
+                    if (pdelta < nextdelta[j]) {
+                        nextdelta[j] = pdelta;
+                        found = 1;
+                        break;
+                    }
+                }
+                if (found) {
+                    nextlen = i - nextiter + 1;
+                    nextpos[(nextiter + nextlen) % buffer_size] = pos;
+                    nextdelta[(nextiter + nextlen) % buffer_size] = rdelta;
+                    nextpos[(nextiter + nextlen + 1) % buffer_size] = -1;
+                    nextlen++;
+                }
+            }
+        }
+        double *buf = &buffer[(pos + channels) % buffer_size];
+        peak = 0;
+        for (int c = 0; c < channels; c++) peak = fmax(peak, fabs(buf[c]));
+        att += delta;
+        for (int c = 0; c < channels; c++) dst[c] = buf[c] * att;
+        if ((pos + channels) % buffer_size == nextpos[nextiter]) {
+            delta = nextdelta[nextiter];
+            att = limit / peak;
+            nextlen -= 1;
+            nextpos[nextiter] = -1;
+            nextiter = (nextiter + 1) % buffer_size;
+        }
+        if (att > 1.) {
+            att = 1.;
+            delta = 0.;
+            nextiter = 0;
+            nextlen = 0;
+            nextpos[0] = -1;
+        }
+        if (att <= 0.) {
+            att = 0.0000000000001;
+            delta = (1.0 - att) / (fs * release);
+        }
+        if (att != 1. && (1. - att) < 0.0000000000001) att = 1.;
+        if (delta != 0. && fabs(delta) < 0.00000000000001) delta = 0.;
+        for (int c = 0; c < channels; c++) {
+            double v = dst[c];
+            v = v < -limit ? -limit : (v > limit ? limit : v);
+            v = v * level * level_out;
+            double q = (double)llrint(v * 32768.0);
+            out[nn * channels + c] = (int16_t)(q > 32767 ? 32767 : (q < -32768 ? -32768 : q));
+        }
+        pos = (pos + channels) % buffer_size;
+    }
+    free(buffer);
+    free(nextdelta);
+    free(nextpos);
+}
+
+/* loudnorm LINEAR mode (af_loudnorm.c, pass 2 at :240 when the measured values
+ * allow it): dst = src * 10^((I_target - I_measured)/20) on doubles x/32768,
+ * then s16 via llrint(x*32768) clipped. */
+EXPORT void orc_linear_gain(const int16_t *x, int64_t n_samples, double gain, int16_t *out) {
+    for (int64_t i = 0; i < n_samples; i++) {
+        double v = ((double)x[i] * (1.0 / 32768.0)) * gain;
+        double q = (double)llrint(v * 32768.0);
+        out[i] = (int16_t)(q > 32767 ? 32767 : (q < -32768 ? -32768 : q));
+    }
+}
+
+/* A.1: ffmpeg's f32 -> s16 conversion, clip(lrintf(x*32768)); mono duplicated. */
+EXPORT void orc_quantize(const float *x, int64_t n, int channels, int16_t *out) {
+    for (int64_t i = 0; i < n; i++) {
+        for (int c = 0; c < 2; c++) {
+            float v = x[i * channels + (channels == 1 ? 0 : c)] * 32768.0f;
+            long q = lrintf(v);
+            out[2 * i + c] = (int16_t)(q > 32767 ? 32767 : (q < -32768 ? -32768 : q));
+        }
+    }
+}

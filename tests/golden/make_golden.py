@@ -1,0 +1,167 @@
+"""Generate golden vectors for the per-chunk mastering chain from the REFERENCE itself.
+
+Runs ONLY in the build container, where /root/reference exists (it refuses to
+run anywhere else).  It imports the reference's own
+``audio_mastering_engine.py`` with three ``sys.modules`` stand-ins:
+
+* ``pydub`` / ``pydub.effects`` -> ``pydub_restated.py`` (pydub 0.25.1 restated;
+  pydub is not installed in this image),
+* ``ai_tagger`` -> an empty module (the AI tagger is out of scope).
+
+and then runs the reference's chunk body, audio_mastering_engine.py:189-197,
+through the reference functions (``apply_analog_character``,
+``audio_segment_to_float_array``, ``apply_eq_to_samples``,
+``apply_stereo_width``, ``float_array_to_audio_segment``,
+``apply_multiband_compressor``) on numpy 2.2.6 / scipy 1.15.3.  Every
+intermediate is stored as a small ``.npz`` (no pickles) under tests/golden/.
+
+Usage:  python tests/golden/make_golden.py
+"""
+import importlib.util
+import json
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference/audio_mastering_engine.py"
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(HERE, "..", "..", "audio-mastering-engine_amd"))
+
+import pydub_restated  # noqa: E402
+from amx import synth  # noqa: E402
+
+RECORD = []
+
+
+def _recording_compressor(seg, threshold=-20.0, ratio=4.0, attack=5.0, release=50.0):
+    out = pydub_restated.compress_dynamic_range(seg, threshold=threshold, ratio=ratio,
+                                                attack=attack, release=release)
+    RECORD.append((np.frombuffer(seg._data, dtype=np.int16).copy(),
+                   np.frombuffer(out._data, dtype=np.int16).copy()))
+    return out
+
+
+def load_reference():
+    if not os.path.exists(REF):
+        raise SystemExit("make_golden.py needs the reference at %s; refusing to run" % REF)
+    pyd = types.ModuleType("pydub")
+    pyd.AudioSegment = pydub_restated.AudioSegment
+    eff = types.ModuleType("pydub.effects")
+    eff.compress_dynamic_range = _recording_compressor
+    pyd.effects = eff
+    sys.modules["pydub"] = pyd
+    sys.modules["pydub.effects"] = eff
+    sys.modules["ai_tagger"] = types.ModuleType("ai_tagger")
+    spec = importlib.util.spec_from_file_location("ref_ame", REF)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def reference_chunk(ame, x16, fs, channels, settings):
+    """audio_mastering_engine.py:189-197, called through the reference functions."""
+    RECORD.clear()
+    rec = {}
+    chunk = pydub_restated.AudioSegment(data=x16.tobytes(), sample_width=2,
+                                        frame_rate=fs, channels=channels)
+    if chunk.channels == 1:
+        chunk = chunk.set_channels(2)
+    rec["in16"] = np.frombuffer(chunk._data, dtype=np.int16).reshape(-1, 2).copy()
+    if settings.get("analog_character", 0) > 0:
+        chunk = ame.apply_analog_character(chunk, settings.get("analog_character"))
+        rec["analog16"] = np.frombuffer(chunk._data, dtype=np.int16).reshape(-1, 2).copy()
+    chunk_samples = ame.audio_segment_to_float_array(chunk)
+    processed = ame.apply_eq_to_samples(chunk_samples, chunk.frame_rate, settings)
+    rec["eq32"] = np.array(processed, dtype=processed.dtype, copy=True)
+    if settings.get("width", 1.0) != 1.0:
+        processed = ame.apply_stereo_width(processed, settings.get("width"))
+        rec["width32"] = np.array(processed, copy=True)
+    pchunk = ame.float_array_to_audio_segment(processed, chunk)
+    rec["p16"] = np.frombuffer(pchunk._data, dtype=np.int16).reshape(-1, 2).copy()
+    out = pchunk
+    if settings.get("multiband"):
+        out = ame.apply_multiband_compressor(pchunk, settings)
+        for name, (bi, bo) in zip(("low", "mid", "high"), RECORD):
+            rec[name + "16"] = bi.reshape(-1, 2)
+            rec[name + "c16"] = bo.reshape(-1, 2)
+    rec["out16"] = np.frombuffer(out._data, dtype=np.int16).reshape(-1, 2).copy()
+    return rec
+
+
+MB = dict(multiband=True, low_thresh=-25.0, low_ratio=6.0, mid_thresh=-20.0,
+          mid_ratio=3.0, high_thresh=-15.0, high_ratio=4.0)
+
+
+def cases(ame):
+    P = ame.EQ_PRESETS
+    vc = P["Vocal Clarity"]
+    out = []
+    # (name, fs, n_frames, channels, signal, settings)
+    out.append(("c2_vocal_48k", 48000, 12000, 2, "music", dict(vc, lufs=-14.0)))
+    out.append(("c3_vocal_mb_48k", 48000, 12345, 2, "music",
+                dict(vc, lufs=-14.0, width=1.3, analog_character=40.0, **MB)))
+    out.append(("c1_mono_bt_441k", 44100, 11025, 1, "music",
+                dict(bass_boost=3.0, treble_boost=3.0, lufs=None)))
+    out.append(("c1_mono_btneg_441k", 44100, 9999, 1, "music",
+                dict(bass_boost=-3.0, treble_boost=-3.0, lufs=None)))
+    out.append(("c5_mb_96k", 96000, 24011, 2, "music",
+                dict(vc, lufs=-14.0, width=1.3, analog_character=40.0, **MB)))
+    for i, (pname, pv) in enumerate(sorted(P.items())):
+        fs = (44100, 48000, 96000)[i % 3]
+        out.append(("preset_%d_%s" % (i, pname.split()[0].lower().replace("-", "")), fs,
+                    6000 + 777 * i, 2, "music", dict(pv)))
+    out.append(("analog100_w0_48k", 48000, 7000, 2, "music",
+                dict(analog_character=100.0, width=0.0, mid_cut=6.0)))
+    out.append(("analog1_w2_mb_48k", 48000, 9000, 2, "music",
+                dict(analog_character=1.0, width=2.0, presence_boost=-6.0, treble_boost=6.0, **MB)))
+    out.append(("square_fullscale_mb_48k", 48000, 6000, 2, "square",
+                dict(bass_boost=6.0, width=1.5, **MB)))
+    out.append(("silence_mb_48k", 48000, 4000, 2, "silence", dict(vc, **MB)))
+    out.append(("dc_48k", 48000, 4000, 2, "dc", dict(bass_boost=2.0, analog_character=50.0)))
+    out.append(("mb_edges_48k", 48000, 8000, 2, "music",
+                dict(bass_boost=1.0, multiband=True, low_thresh=0.0, low_ratio=1.0,
+                     mid_thresh=-40.0, mid_ratio=10.0, high_thresh=-30.0, high_ratio=1.5)))
+    out.append(("eq_only_mid_96k", 96000, 9600, 2, "music", dict(mid_cut=4.5, width=0.7)))
+    out.append(("passthrough_48k", 48000, 3000, 2, "music", dict()))
+    out.append(("odd_len_mb_441k", 44100, 4411, 2, "music",
+                dict(treble_boost=-1.0, analog_character=70.0, **MB)))
+    return out
+
+
+def make_signal(kind, n, fs, channels, seed):
+    if kind == "music":
+        return synth.to_s16(synth.music_like(n, fs, channels, seed=seed, peak_dbfs=-3.0))
+    if kind == "square":
+        return synth.to_s16(synth.square(n, fs, channels, amp=1.0))
+    if kind == "silence":
+        return np.zeros((n, channels), dtype=np.int16)
+    if kind == "dc":
+        return np.full((n, channels), 12000, dtype=np.int16)
+    raise ValueError(kind)
+
+
+def main():
+    ame = load_reference()
+    man = {}
+    for seed, (name, fs, n, ch, kind, settings) in enumerate(cases(ame)):
+        x16 = make_signal(kind, n, fs, ch, seed)
+        rec = reference_chunk(ame, x16, fs, ch, settings)
+        rec["x16"] = x16
+        meta = dict(name=name, fs=fs, n=n, channels=ch, signal=kind, seed=seed,
+                    settings=settings)
+        rec["meta"] = np.array(json.dumps(meta))
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **rec)
+        man[name] = {k: [list(v.shape), str(v.dtype)] for k, v in rec.items() if k != "meta"}
+        print(name, {k: v.shape for k, v in rec.items()})
+    with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
+        json.dump(dict(generator="tests/golden/make_golden.py",
+                       reference="audio_mastering_engine.py:189-197 via reference functions",
+                       numpy=np.__version__, scipy=__import__("scipy").__version__,
+                       cases=man), f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
