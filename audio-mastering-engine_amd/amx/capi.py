@@ -1,0 +1,174 @@
+"""ctypes binding of libamx.so (include/amx.h).
+
+The product's only compute path: every per-sample stage runs in the HIP kernels
+behind this ABI.  If the library is missing this module raises -- there is no
+CPU fallback.
+"""
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libamx.so")
+
+c_double_p = ctypes.POINTER(ctypes.c_double)
+c_float_p = ctypes.POINTER(ctypes.c_float)
+
+AMX_OK, AMX_EINVAL, AMX_EHIP, AMX_ENOMEM, AMX_ERANGE = 0, -1, -2, -3, -4
+ABI_VERSION = 1
+
+
+class AmxError(RuntimeError):
+    pass
+
+
+class ChainDesc(ctypes.Structure):
+    _fields_ = [
+        ("sample_rate", ctypes.c_int32), ("channels_in", ctypes.c_int32),
+        ("input_s16", ctypes.c_int32), ("pad0_", ctypes.c_int32),
+        ("analog_on", ctypes.c_int32), ("analog_drive", ctypes.c_float),
+        ("tanh_lut", c_float_p),
+        ("analog_lo_ba", ctypes.c_double * 6), ("analog_lo_gain", ctypes.c_double),
+        ("analog_hi_ba", ctypes.c_double * 6), ("analog_hi_gain", ctypes.c_double),
+        ("eq_kind", ctypes.c_int32 * 4), ("eq_gain_db", ctypes.c_double * 4),
+        ("eq_gain", ctypes.c_double * 4), ("eq_coef", (ctypes.c_double * 24) * 4),
+        ("width_on", ctypes.c_int32), ("width", ctypes.c_float),
+        ("multiband_on", ctypes.c_int32),
+        ("xover_lo_sos", ctypes.c_double * 12), ("xover_hi_sos", ctypes.c_double * 12),
+        ("comp_threshold_db", ctypes.c_double * 3), ("comp_ratio", ctypes.c_double * 3),
+        ("comp_m_table", c_double_p * 3),
+    ]
+
+
+class Chunk(ctypes.Structure):
+    _fields_ = [("track", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("in_offset", ctypes.c_int64), ("frames", ctypes.c_int64)]
+
+
+class FinalDesc(ctypes.Structure):
+    _fields_ = [("limit", ctypes.c_double), ("attack_ms", ctypes.c_double),
+                ("release_ms", ctypes.c_double), ("level_in", ctypes.c_double),
+                ("level_out", ctypes.c_double), ("auto_level", ctypes.c_int32),
+                ("pad_", ctypes.c_int32)]
+
+
+class PlanInfo(ctypes.Structure):
+    _fields_ = [("workspace_bytes", ctypes.c_int64), ("out_frames", ctypes.c_int64),
+                ("n_tracks", ctypes.c_int32), ("n_chunks", ctypes.c_int32),
+                ("n_segments", ctypes.c_int64), ("seg_frames", ctypes.c_int32),
+                ("scan_levels_eq", ctypes.c_int32), ("scan_levels_xover", ctypes.c_int32),
+                ("scan_levels_kw", ctypes.c_int32), ("eq_dim", ctypes.c_int32),
+                ("hop_frames", ctypes.c_int32)]
+
+
+class TrackSpan(ctypes.Structure):
+    _fields_ = [("out_offset", ctypes.c_int64), ("out_frames", ctypes.c_int64),
+                ("track_frame0", ctypes.c_int64), ("track_frames_total", ctypes.c_int64)]
+
+
+# every symbol include/amx.h declares (checked by the CPU test suite)
+EXPORTS = ("amx_abi_version", "amx_last_error", "amx_plan_create", "amx_plan_free",
+           "amx_plan_get_info", "amx_plan_track_span", "amx_run_chunks", "amx_loudness_pass1",
+           "amx_kw_propagate", "amx_loudness_pass2", "amx_loudness_histograms",
+           "amx_limiter_geometry", "amx_finalize")
+
+_lib = None
+
+
+def load(path=None):
+    """Load libamx.so (built in-tree by __graft_entry__.build()); raise if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise AmxError("libamx.so not found at %s -- build it with "
+                       "`python -c 'import __graft_entry__ as g; g.build()'`" % p)
+    L = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    vp = ctypes.c_void_p
+    L.amx_abi_version.restype = ctypes.c_int
+    L.amx_last_error.restype = ctypes.c_char_p
+    L.amx_plan_create.argtypes = [ctypes.POINTER(ChainDesc), ctypes.POINTER(Chunk), ctypes.c_int32,
+                                  ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                  ctypes.c_int32, ctypes.POINTER(vp)]
+    L.amx_plan_free.argtypes = [vp]
+    L.amx_plan_free.restype = None
+    L.amx_plan_get_info.argtypes = [vp, ctypes.POINTER(PlanInfo)]
+    L.amx_plan_track_span.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(TrackSpan)]
+    L.amx_run_chunks.argtypes = [vp, vp, vp, vp, vp]
+    L.amx_loudness_pass1.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.amx_kw_propagate.argtypes = [vp, ctypes.c_int64, c_double_p, c_double_p]
+    L.amx_loudness_pass2.argtypes = [vp, vp, vp, vp, ctypes.c_int64, vp, vp]
+    L.amx_loudness_histograms.argtypes = [vp, vp, ctypes.c_int64, vp, vp, vp, vp]
+    L.amx_limiter_geometry.argtypes = [vp, ctypes.POINTER(FinalDesc), ctypes.POINTER(ctypes.c_int32),
+                                       ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]
+    L.amx_finalize.argtypes = [vp, ctypes.POINTER(FinalDesc), vp, vp, ctypes.c_int32, vp, vp, vp,
+                               vp, vp]
+    if L.amx_abi_version() != ABI_VERSION:
+        raise AmxError("libamx ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != AMX_OK:
+        msg = load().amx_last_error()
+        raise AmxError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (or None)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class Plan:
+    """Owns an amx_plan*; see include/amx.h for the call contract."""
+
+    def __init__(self, desc, chunks, track_frame0=None, track_total=None, seg_frames=256):
+        L = load()
+        arr = (Chunk * max(1, len(chunks)))()
+        for i, (t, off, n) in enumerate(chunks):
+            arr[i].track, arr[i].in_offset, arr[i].frames = int(t), int(off), int(n)
+        nt = (max(c[0] for c in chunks) + 1) if chunks else 0
+        f0 = (ctypes.c_int64 * max(1, nt))(*(track_frame0 or [0] * nt)) if track_frame0 else None
+        tt = (ctypes.c_int64 * max(1, nt))(*track_total) if track_total else None
+        h = ctypes.c_void_p()
+        self._desc = desc  # keep tables referenced by pointer alive
+        check(L.amx_plan_create(ctypes.byref(desc), arr, len(chunks), f0, tt, int(seg_frames),
+                                ctypes.byref(h)), "amx_plan_create")
+        self.h = h
+        info = PlanInfo()
+        check(L.amx_plan_get_info(h, ctypes.byref(info)), "amx_plan_get_info")
+        self.info = info
+
+    def span(self, track):
+        s = TrackSpan()
+        check(load().amx_plan_track_span(self.h, int(track), ctypes.byref(s)), "amx_plan_track_span")
+        return s
+
+    def kw_propagate(self, frames, state8):
+        import numpy as np
+        a = np.ascontiguousarray(state8, np.float64).reshape(8)
+        out = np.zeros(8, np.float64)
+        check(load().amx_kw_propagate(self.h, int(frames), a.ctypes.data_as(c_double_p),
+                                      out.ctypes.data_as(c_double_p)), "amx_kw_propagate")
+        return out
+
+    def limiter_geometry(self, fd):
+        bs, halo, sd = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        check(load().amx_limiter_geometry(self.h, ctypes.byref(fd), ctypes.byref(bs),
+                                          ctypes.byref(halo), ctypes.byref(sd)),
+              "amx_limiter_geometry")
+        return bs.value, halo.value, sd.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().amx_plan_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

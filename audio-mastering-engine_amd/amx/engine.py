@@ -1,0 +1,201 @@
+"""GPU mastering engine: the host side of the drop-in path.
+
+``MasteringJob`` owns one amx plan (tracks laid back to back, or one rank's
+contiguous run of chunks of chunk-sharded tracks), torch-allocated device
+buffers and the call sequence of process_audio_with_ffmpeg_pipeline
+(audio_mastering_engine.py:171-226):
+
+  chunk chain (:185-204) + concat (:205-214)    -> amx_run_chunks
+  loudnorm pass 1 measurement (:229-237)         -> amx_loudness_pass1/pass2/histograms
+                                                    + amx/loudness.py host arithmetic
+  loudnorm pass 2 linear gain (:240) + alimiter (:223) -> amx_finalize
+
+PyTorch only owns device memory and the stream; every per-sample operation is a
+HIP kernel in libamx.so.  There is no CPU fallback: if the library or a GPU is
+missing, construction raises.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import capi, design, loudness
+from .chunking import plan_tracks, packet_frames
+from .settings import ALIMITER, LOUDNORM_LRA, LOUDNORM_TP
+
+
+class DynamicModeUnsupported(NotImplementedError):
+    """loudnorm would run in dynamic mode (192 kHz AGC); SURVEY.md §8f row 1."""
+
+
+def final_desc(params=ALIMITER):
+    fd = capi.FinalDesc()
+    fd.limit = params["limit"]
+    fd.attack_ms = params["attack"]
+    fd.release_ms = params["release"]
+    fd.level_in = params["level_in"]
+    fd.level_out = params["level_out"]
+    fd.auto_level = 1
+    return fd
+
+
+class MasteringJob:
+    def __init__(self, sample_rate, channels_in, settings, track_frames, *, quantum=None,
+                 input_s16=False, seg_frames=256, device=None, chunks=None, track_frame0=None,
+                 track_total=None, limiter=ALIMITER):
+        if not torch.cuda.is_available():
+            raise RuntimeError("amx needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.device = torch.device(device or "cuda")
+        self.fs = int(sample_rate)
+        self.settings = dict(settings)
+        self.channels_in = int(channels_in)
+        self.input_s16 = bool(input_s16)
+        self.desc, self._keep = design.chain_desc(self.fs, self.channels_in, self.settings)
+        self.desc.input_s16 = 1 if input_s16 else 0
+        if quantum is None:
+            quantum = packet_frames(self.channels_in * (2 if input_s16 else 4))
+        self.track_frames = [int(n) for n in track_frames]
+        self.chunks = chunks if chunks is not None else plan_tracks(self.track_frames, self.fs, quantum)
+        self.plan = capi.Plan(self.desc, self.chunks, track_frame0, track_total, seg_frames)
+        info = self.plan.info
+        self.info = info
+        self.n_tracks = info.n_tracks
+        dev = self.device
+        self.ws = torch.empty(max(1, info.workspace_bytes), dtype=torch.uint8, device=dev)
+        self.out = torch.empty((max(1, info.out_frames), 2), dtype=torch.int16, device=dev)
+        self.y = torch.empty_like(self.out)
+        T = max(1, self.n_tracks)
+        self.spans = [self.plan.span(t) for t in range(self.n_tracks)]
+        self.hop = info.hop_frames
+        self.max_hops = max([s.track_frames_total // self.hop + 1 for s in self.spans] + [1])
+        self.kw_tail = torch.zeros((T, 2, 4), dtype=torch.float64, device=dev)
+        self.kw_carry = torch.zeros((T, 2, 4), dtype=torch.float64, device=dev)
+        self.peak = torch.zeros((T, 2), dtype=torch.float64, device=dev)
+        self.hops = torch.zeros((T, self.max_hops, 2), dtype=torch.float64, device=dev)
+        self.hist = torch.zeros((T, 1000), dtype=torch.int64, device=dev)
+        self.st_hist = torch.zeros((T, 1000), dtype=torch.int64, device=dev)
+        self.gains = torch.full((T,), -1.0, dtype=torch.float64, device=dev)
+        self.fd = final_desc(limiter)
+        self.limit = limiter["limit"]
+        self.bs, self.halo_frames, self.state_doubles = self.plan.limiter_geometry(self.fd)
+        self.halo = torch.zeros((T, max(1, self.halo_frames), 2), dtype=torch.int16, device=dev)
+        self.lim_state = torch.zeros((T, self.state_doubles), dtype=torch.float64, device=dev)
+        self.report = {}
+
+    # ------------------------------------------------------------ device steps
+    @staticmethod
+    def _s(stream):
+        import ctypes
+        s = stream if stream is not None else torch.cuda.current_stream()
+        return ctypes.c_void_p(s.cuda_stream)
+
+    def run_chunks(self, d_in, stream=None):
+        want = torch.int16 if self.input_s16 else torch.float32
+        if d_in.dtype != want or not d_in.is_contiguous() or d_in.device.type != "cuda":
+            raise TypeError("d_in must be a contiguous %s CUDA tensor" % want)
+        need = max((off + n for (_, off, n) in self.chunks), default=0)
+        if d_in.numel() < need * self.channels_in:
+            raise ValueError("d_in holds %d samples, plan needs %d" % (d_in.numel(), need * self.channels_in))
+        L = capi.load()
+        capi.check(L.amx_run_chunks(self.plan.h, capi.ptr(d_in), capi.ptr(self.out),
+                                    capi.ptr(self.ws), self._s(stream)), "amx_run_chunks")
+
+    def loudness_pass1(self, stream=None):
+        capi.check(capi.load().amx_loudness_pass1(self.plan.h, capi.ptr(self.out), capi.ptr(self.kw_tail),
+                                                  capi.ptr(self.peak), capi.ptr(self.ws), self._s(stream)),
+                   "amx_loudness_pass1")
+
+    def loudness_pass2(self, stream=None, carry=True):
+        capi.check(capi.load().amx_loudness_pass2(self.plan.h, capi.ptr(self.out),
+                                                  capi.ptr(self.kw_carry) if carry else None,
+                                                  capi.ptr(self.hops), int(self.max_hops),
+                                                  capi.ptr(self.ws), self._s(stream)),
+                   "amx_loudness_pass2")
+
+    def histograms(self, stream=None):
+        capi.check(capi.load().amx_loudness_histograms(self.plan.h, capi.ptr(self.hops), int(self.max_hops),
+                                                       capi.ptr(self.hist), capi.ptr(self.st_hist),
+                                                       capi.ptr(self.ws), self._s(stream)),
+                   "amx_loudness_histograms")
+
+    def finalize(self, fast, stream=None):
+        capi.check(capi.load().amx_finalize(self.plan.h, self.fd, capi.ptr(self.out), capi.ptr(self.gains),
+                                            1 if fast else 0, capi.ptr(self.halo), capi.ptr(self.y),
+                                            capi.ptr(self.lim_state), capi.ptr(self.ws), self._s(stream)),
+                   "amx_finalize")
+
+    # ------------------------------------------------------------ host decisions
+    def measure(self):
+        """loudnorm pass-1 statistics per track from the device histograms (syncs)."""
+        hist = self.hist.cpu().numpy().view(np.uint64)
+        st = self.st_hist.cpu().numpy().view(np.uint64)
+        peaks = self.peak.cpu().numpy()
+        return [loudness.measure(hist[t], st[t], peaks[t]) for t in range(self.n_tracks)]
+
+    def decide_gains(self, stats):
+        lufs = self.settings.get("lufs")
+        gains, modes = [], []
+        for st in stats:
+            if lufs is None:
+                modes.append("off")
+                gains.append(-1.0)
+                continue
+            mode, g = loudness.linear_gain(st, float(lufs), LOUDNORM_TP, LOUDNORM_LRA)
+            if mode == "dynamic":
+                raise DynamicModeUnsupported(
+                    "loudnorm would use dynamic mode for these measurements %s; only linear "
+                    "mode is implemented (DESIGN.md: next rows)" % (st,))
+            modes.append(mode)
+            gains.append(g if mode == "linear" else -1.0)
+        return gains, modes
+
+    def fast_ok(self, gains):
+        peaks = self.peak.cpu().numpy()
+        for t in range(self.n_tracks):
+            m = float(peaks[t].max()) if peaks.shape[1] else 0.0
+            if loudness.max_after_gain(m, gains[t]) * self.fd.level_in > self.limit:
+                return False
+        return True
+
+    def run(self, d_in, stream=None):
+        """Whole pipeline for whole tracks on this GPU; returns y (int16 [frames, 2])."""
+        self.run_chunks(d_in, stream)
+        self.loudness_pass1(stream)
+        lufs = self.settings.get("lufs")
+        stats = None
+        if lufs is not None:
+            self.loudness_pass2(stream, carry=False)
+            self.histograms(stream)
+            stats = self.measure()
+            gains, modes = self.decide_gains(stats)
+        else:
+            gains, modes = [-1.0] * self.n_tracks, ["off"] * self.n_tracks
+        self.gains.copy_(torch.tensor(gains, dtype=torch.float64))
+        fast = self.fast_ok(gains)
+        self.finalize(fast, stream)
+        self.report = {"stats": stats, "modes": modes, "gains": gains, "limiter_fast": fast,
+                       "chunks": len(self.chunks), "segments": self.info.n_segments}
+        return self.y[:self.info.out_frames]
+
+    def track_output(self, t):
+        s = self.spans[t]
+        return self.y[s.out_offset:s.out_offset + s.out_frames]
+
+
+def master_array(x, sample_rate, settings, *, quantum=None, seg_frames=256):
+    """In-memory twin of master_audio: float32 [frames, C] (C = 1/2,
+    any device) -> int16 [frames', 2] CUDA tensor (the 16-bit WAV the reference
+    writes) and a report dict."""
+    x = torch.as_tensor(x)
+    if x.dim() == 1:
+        x = x.reshape(-1, 1)
+    if x.dtype == torch.int16:
+        s16 = True
+    else:
+        s16 = False
+        x = x.to(torch.float32)
+    x = x.contiguous().to("cuda")
+    job = MasteringJob(sample_rate, x.shape[1], settings, [x.shape[0]], quantum=quantum,
+                       input_s16=s16, seg_frames=seg_frames)
+    y = job.run(x)
+    return y, job.report

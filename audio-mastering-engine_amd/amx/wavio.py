@@ -1,0 +1,114 @@
+"""Minimal RIFF/WAVE reader/writer (PCM 8/16/24/32 and IEEE float 32/64).
+
+Host I/O for master_audio(): the reference reads any format ffmpeg decodes and
+writes 16-bit PCM (:178, :223); this build reads WAV and writes s16 WAV.
+"""
+import struct
+
+import numpy as np
+
+
+class WavInfo:
+    def __init__(self, fs, channels, fmt_tag, bits):
+        self.sample_rate, self.channels, self.fmt_tag, self.bits = fs, channels, fmt_tag, bits
+
+    @property
+    def block_align(self):
+        return self.channels * self.bits // 8
+
+
+def read_wav_native(path):
+    """Returns (array [frames, channels] in the file's own sample type, WavInfo).
+
+    PCM 8 -> uint8, 16 -> int16, 24 -> int32 (sign-extended 24-bit value),
+    32 -> int32; IEEE float -> float32/float64."""
+    with open(path, "rb") as f:
+        data = f.read()
+    if data[:4] != b"RIFF" or data[8:12] != b"WAVE":
+        raise ValueError("not a RIFF/WAVE file: %s" % path)
+    pos, fmt, payload = 12, None, None
+    while pos + 8 <= len(data):
+        cid, size = data[pos:pos + 4], struct.unpack("<I", data[pos + 4:pos + 8])[0]
+        body = data[pos + 8:pos + 8 + size]
+        if cid == b"fmt ":
+            tag, ch, fs, _, _, bits = struct.unpack("<HHIIHH", body[:16])
+            if tag == 0xFFFE and len(body) >= 26:
+                tag = struct.unpack("<H", body[24:26])[0]
+            fmt = WavInfo(fs, ch, tag, bits)
+        elif cid == b"data":
+            payload = body
+        pos += 8 + size + (size & 1)
+    if fmt is None or payload is None:
+        raise ValueError("WAV without fmt/data chunk: %s" % path)
+    n = len(payload) // fmt.block_align
+    raw = payload[:n * fmt.block_align]
+    if fmt.fmt_tag == 3:
+        x = np.frombuffer(raw, dtype={32: "<f4", 64: "<f8"}[fmt.bits])
+    elif fmt.fmt_tag == 1:
+        if fmt.bits == 16:
+            x = np.frombuffer(raw, "<i2")
+        elif fmt.bits == 8:
+            x = np.frombuffer(raw, "u1")
+        elif fmt.bits == 24:
+            b = np.frombuffer(raw, "u1").reshape(-1, 3).astype(np.int32)
+            v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
+            x = np.where(v >= 1 << 23, v - (1 << 24), v).astype(np.int32)
+        elif fmt.bits == 32:
+            x = np.frombuffer(raw, "<i4")
+        else:
+            raise ValueError("unsupported PCM bit depth %d" % fmt.bits)
+    else:
+        raise ValueError("unsupported WAV format tag %d" % fmt.fmt_tag)
+    return x.reshape(n, fmt.channels), fmt
+
+
+def to_s16(x, fmt):
+    """ffmpeg's conversion of the decoded samples to s16 for the segment WAVs (:178),
+    libswresample audioconvert.c: u8 (v-0x80)<<8; s32 >>16 (24-bit PCM decodes to
+    s32 = v<<8); float/double av_clip_int16(lrint(x*32768))."""
+    if fmt.fmt_tag == 3:
+        if x.dtype == np.float64:
+            return np.clip(np.rint(x * 32768.0), -32768, 32767).astype(np.int16)
+        y = np.rint(x.astype(np.float32) * np.float32(32768.0))
+        return np.clip(y, -32768, 32767).astype(np.int16)
+    if fmt.bits == 16:
+        return x.astype(np.int16)
+    if fmt.bits == 8:
+        return ((x.astype(np.int32) - 0x80) << 8).astype(np.int16)
+    if fmt.bits == 24:
+        return ((x.astype(np.int64) << 8) >> 16).astype(np.int16)
+    return (x.astype(np.int64) >> 16).astype(np.int16)
+
+
+def read_wav(path):
+    """Returns (float32 array [frames, channels], WavInfo)."""
+    x, fmt = read_wav_native(path)
+    if fmt.fmt_tag == 3:
+        return x.astype(np.float32), fmt
+    scale = {8: 128.0, 16: 32768.0, 24: float(1 << 23), 32: float(1 << 31)}[fmt.bits]
+    off = 128.0 if fmt.bits == 8 else 0.0
+    return ((x.astype(np.float64) - off) / scale).astype(np.float32), fmt
+
+
+def write_wav_s16(path, x16, fs):
+    x16 = np.ascontiguousarray(x16, dtype="<i2")
+    ch = 1 if x16.ndim == 1 else x16.shape[1]
+    raw = x16.tobytes()
+    hdr = b"RIFF" + struct.pack("<I", 36 + len(raw)) + b"WAVE"
+    hdr += b"fmt " + struct.pack("<IHHIIHH", 16, 1, ch, fs, fs * ch * 2, ch * 2, 16)
+    hdr += b"data" + struct.pack("<I", len(raw))
+    with open(path, "wb") as f:
+        f.write(hdr)
+        f.write(raw)
+
+
+def write_wav_f32(path, x, fs):
+    x = np.ascontiguousarray(x, dtype="<f4")
+    ch = 1 if x.ndim == 1 else x.shape[1]
+    raw = x.tobytes()
+    hdr = b"RIFF" + struct.pack("<I", 36 + len(raw)) + b"WAVE"
+    hdr += b"fmt " + struct.pack("<IHHIIHH", 16, 3, ch, fs, fs * ch * 4, ch * 4, 32)
+    hdr += b"data" + struct.pack("<I", len(raw))
+    with open(path, "wb") as f:
+        f.write(hdr)
+        f.write(raw)

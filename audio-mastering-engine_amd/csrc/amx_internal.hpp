@@ -1,0 +1,130 @@
+// amx_internal.hpp -- device-visible plan structures shared by amx_kernels.hip
+// (CDNA4 kernels) and amx_plan.cpp (host plan construction + C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define AMX_MAX_EQ_DIM 20
+#define AMX_XO_DIM 8      // crossover: 2 low-pass + 2 high-pass SOS sections
+#define AMX_KW_DIM 4      // K-weighting 4th-order DF-II state (v1..v4)
+#define AMX_BLOCK 256
+#define AMX_HIST_BINS 1000
+
+// One EQ stage of _apply_eq_to_channel (audio_mastering_engine.py:277-282).
+struct EqStageDev {
+    int32_t kind;    // 0 skipped, 1 shelf (lfilter ba, :283-289), 2 peak (4 SOS, :290-298)
+    int32_t neg;     // shelf with gain_db < 0 (:289)
+    double g;        // 10**(gain_db/20)
+    double gm1;      // g - 1
+    float gf;        // float32(g): the float32 product of :289 on a float32 input
+    float pad_;
+    double c[24];    // shelf: b0 b1 b2 a0 a1 a2 ; peak: 4 x [b0 b1 b2 a0 a1 a2]
+};
+
+struct ChainDev {
+    int32_t fs, chin;
+    int32_t in_s16, pad0_;
+    int32_t analog_on, has_lut;
+    int32_t eq_mask, eq_dim;
+    int32_t width_on, mb_on;
+    float width, drive;
+    double an_lo[6];
+    double an_glo1;   // analog low shelf g - 1
+    double an_hi[6];
+    double an_ghi1;
+    EqStageDev st[4];
+    double xlo[12], xhi[12];
+    // compressor (pydub compress_dynamic_range, :306-308)
+    int32_t look;          // int(5 ms * fs)
+    int32_t rthr[3];       // smallest integer rms with rms > thresh_rms
+    double kb[5], ka[5];   // K-weighting (libebur128) b, a
+};
+
+// A ~30 s chunk (ffmpeg segment, :178).  loc_off indexes chunk-local scratch.
+struct ChunkDev {
+    int64_t in_off;    // first input frame in d_in
+    int64_t loc_off;   // offset in per-frame scratch arrays (sum of previous chunk lengths)
+    int64_t out_off;   // offset in d_out (frames)
+    int64_t n;         // input frames
+    int64_t out_n;     // output frames (n, or pydub overlay ms-rounded length when multiband)
+    int32_t seg0, nseg;
+    int32_t track, pad_;
+};
+
+// IIR / envelope segment: `len` frames from chunk-local frame `pos`.
+struct SegDev {
+    int64_t pos;
+    int32_t chunk;
+    int32_t len;
+    int32_t first;     // global index of the first segment of the same chunk
+    int32_t last;      // 1 if last segment of its chunk
+};
+
+// K-weighting segment over a track span of d_out.
+struct KwSegDev {
+    int64_t out_pos;     // frame in d_out
+    int64_t tframe;      // frame in the whole-track timeline
+    int32_t track;
+    int32_t len;
+    int32_t first;       // global index of the span's first segment (the scan stream)
+    int32_t last;        // 1 if last segment of its span
+};
+
+struct SpanDev {
+    int64_t out_off, out_n, tframe0, ttotal;
+    int32_t kseg0, nkseg;
+};
+
+// ---------------------------------------------------------------- launchers
+namespace amx {
+struct Launch {
+    const ChainDev *cd;
+    const ChunkDev *chunks;
+    const SegDev *segs;
+    int32_t n_chunks, n_seg, L;
+    hipStream_t stream;
+};
+hipError_t launch_front1_lut(const Launch &l, int mask, const float *in, const float *lut,
+                             int16_t *a16, const double *G, double *e);
+hipError_t launch_scan(const double *e, double *s, const int32_t *seg_first,
+                       const int32_t *seg_stream, int n_seg, int D, int lanes,
+                       const double *Mp, int levels, const double *carry, hipStream_t st);
+hipError_t launch_front2(const Launch &l, int mask, const int16_t *a16, const double *s_eq,
+                         int16_t *dst, int to_out, const double *Gx, double *e_x);
+hipError_t launch_xover2(const Launch &l, const int16_t *p16, const double *s_x,
+                         int16_t *bands, int64_t nloc);
+hipError_t launch_rms(const Launch &l, const int16_t *bands, uint16_t *r, int64_t nloc);
+hipError_t launch_env(const Launch &l, const uint16_t *r, const double *tabs, double *att,
+                      double *guess, double *endv, int64_t nloc, int warm);
+hipError_t launch_fix(const Launch &l, const uint16_t *r, const double *tabs, double *att,
+                      double *guess, double *endv, int64_t nloc);
+hipError_t launch_apply_n1(const Launch &l, const int16_t *bands, const double *att,
+                           int16_t *out, int64_t nloc, int64_t max_chunk_out,
+                           const int64_t *n1tab);
+// loudness
+hipError_t launch_kw1(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L,
+                      const int16_t *x, const double *G, double *e, unsigned long long *peak,
+                      hipStream_t st);
+hipError_t launch_kw2(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L, int hop,
+                      const int16_t *x, const double *s, double *parts, int64_t *part_hop,
+                      hipStream_t st);
+hipError_t launch_hops(const SpanDev *spans, int n_tracks, const KwSegDev *ks, int L, int hop,
+                       const double *parts, const int64_t *part_hop, double *hops,
+                       int64_t max_hops, hipStream_t st);
+hipError_t launch_hist(const SpanDev *spans, int n_tracks, int hop, const double *hops,
+                       int64_t max_hops, const double *bounds, unsigned long long *hist,
+                       unsigned long long *st_hist, hipStream_t st);
+// finalize
+hipError_t launch_final_fast(const SpanDev *spans, int n_tracks, int64_t max_span,
+                             const int16_t *x, const int16_t *halo, int halo_frames,
+                             const double *gains, double level_in, double level,
+                             double level_out, double limit, int16_t *y, hipStream_t st);
+hipError_t launch_final_general(const SpanDev *spans, int n_tracks, const int16_t *x,
+                                const int16_t *halo, int halo_frames, const double *gains,
+                                int fs, double level_in, double level, double level_out,
+                                double limit, double release, int buffer_size,
+                                double *state, int64_t state_doubles, int16_t *y,
+                                hipStream_t st);
+hipError_t launch_kw_tail(const SpanDev *spans, int n_tracks, const double *s, const double *e,
+                          const double *P, double *tail, hipStream_t st);
+}  // namespace amx

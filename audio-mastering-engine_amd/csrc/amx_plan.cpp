@@ -1,0 +1,721 @@
+// amx_plan.cpp -- host side of libamx.so: plan construction (state-space models,
+// scan matrices, segment tables, compressor tables) and the C ABI of include/amx.h.
+#include "../../include/amx.h"
+#include "amx_internal.hpp"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdarg>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+#define HIPCHK(x)                                                                      \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) return fail(AMX_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+// ------------------------------------------------------------ dense helpers
+using Mat = std::vector<double>;  // row-major D x D
+
+Mat matmul(const Mat &a, const Mat &b, int D) {
+    Mat c((size_t)D * D, 0.0);
+    for (int i = 0; i < D; i++)
+        for (int k = 0; k < D; k++) {
+            double v = a[(size_t)i * D + k];
+            if (v == 0.0) continue;
+            for (int j = 0; j < D; j++) c[(size_t)i * D + j] += v * b[(size_t)k * D + j];
+        }
+    return c;
+}
+Mat matpow(const Mat &a, int64_t p, int D) {
+    Mat r((size_t)D * D, 0.0), b = a;
+    for (int i = 0; i < D; i++) r[(size_t)i * D + i] = 1.0;
+    while (p > 0) {
+        if (p & 1) r = matmul(r, b, D);
+        b = matmul(b, b, D);
+        p >>= 1;
+    }
+    return r;
+}
+double norm_inf(const Mat &a, int D) {
+    double m = 0.0;
+    for (int i = 0; i < D; i++) {
+        double s = 0.0;
+        for (int j = 0; j < D; j++) s += std::fabs(a[(size_t)i * D + j]);
+        m = s > m ? s : m;
+    }
+    return m;
+}
+
+// A linear time-invariant model s' = A s + B x of a chain, derived by stepping a
+// host copy of the chain from unit states / a unit input.
+struct Lti {
+    int D = 0;
+    Mat A;
+    std::vector<double> B;
+    template <class Step>
+    void derive(int dim, Step step) {
+        D = dim;
+        A.assign((size_t)D * D, 0.0);
+        B.assign(D, 0.0);
+        std::vector<double> s(D);
+        for (int k = 0; k < D; k++) {
+            std::fill(s.begin(), s.end(), 0.0);
+            s[k] = 1.0;
+            step(s.data(), 0.0);
+            for (int i = 0; i < D; i++) A[(size_t)i * D + k] = s[i];
+        }
+        std::fill(s.begin(), s.end(), 0.0);
+        step(s.data(), 1.0);
+        for (int i = 0; i < D; i++) B[i] = s[i];
+    }
+    // G[n][d] = (A^{L-1-n} B)[d]
+    std::vector<double> gemv_table(int L) const {
+        std::vector<double> G((size_t)L * D);
+        std::vector<double> v = B, t(D);
+        for (int n = L - 1; n >= 0; n--) {
+            for (int d = 0; d < D; d++) G[(size_t)n * D + d] = v[d];
+            for (int i = 0; i < D; i++) {
+                double acc = 0.0;
+                for (int k = 0; k < D; k++) acc += A[(size_t)i * D + k] * v[k];
+                t[i] = acc;
+            }
+            v = t;
+        }
+        return G;
+    }
+    // powers M^(2^l), l < levels, of M = A^L; levels chosen so that the neglected
+    // tail ||M^(2^levels)|| <= tol (the scan looks back 2^levels - 1 segments).
+    int scan_powers(int L, double tol, int max_levels, std::vector<double> &out) const {
+        Mat M = matpow(A, L, D);
+        std::vector<Mat> pw;
+        Mat cur = M;
+        int levels = 0;
+        while (norm_inf(cur, D) > tol) {
+            pw.push_back(cur);
+            cur = matmul(cur, cur, D);
+            levels++;
+            if (levels > max_levels) return -1;
+        }
+        out.clear();
+        for (auto &m : pw) out.insert(out.end(), m.begin(), m.end());
+        return levels;
+    }
+};
+
+// host step functions (same math as the device chains, no rounding claims)
+void shelf_step_h(const double *c, double *z, double &x, int neg, double gm1) {
+    double y = z[0] + c[0] * x;
+    z[0] = (z[1] + x * c[1]) - y * c[4];
+    z[1] = x * c[2] - y * c[5];
+    x = neg ? y : x + (y - x) * gm1;
+}
+double sos_step_h(const double *c, double *z, double x) {
+    double y = c[0] * x + z[0];
+    z[0] = (c[1] * x - c[4] * y) + z[1];
+    z[1] = c[2] * x - c[5] * y;
+    return y;
+}
+
+void *align_up(size_t &off, size_t bytes) {
+    size_t o = (off + 255) & ~(size_t)255;
+    off = o + bytes;
+    return reinterpret_cast<void *>(o);
+}
+
+}  // namespace
+
+struct amx_plan {
+    amx_chain_desc desc;
+    ChainDev cd;
+    int L = 256, Lkw = 512, hop = 0;
+    int mask = 0, D = 0;
+    int lev_eq = 0, lev_x = 0, lev_kw = 0;
+    int mb = 0, warm = 512;
+    int n_tracks = 0, n_chunks = 0, n_seg = 0, n_kseg = 0;
+    int64_t nloc = 0, out_frames = 0, max_chunk_out = 0, max_span = 0;
+    std::vector<ChunkDev> chunks;
+    std::vector<SegDev> segs;
+    std::vector<KwSegDev> ksegs;
+    std::vector<SpanDev> spans;
+    std::vector<int64_t> n1tab;
+    Lti kw_model;
+    std::vector<double> tail_pow;  // per span: A_kw^{len_last} (16 doubles)
+    // device constant tables
+    ChainDev *d_cd = nullptr;
+    ChunkDev *d_chunks = nullptr;
+    SegDev *d_segs = nullptr;
+    KwSegDev *d_ksegs = nullptr;
+    SpanDev *d_spans = nullptr;
+    int32_t *d_seg_first = nullptr, *d_seg_stream = nullptr;
+    int32_t *d_kseg_first = nullptr, *d_kseg_stream = nullptr;
+    int64_t *d_n1 = nullptr;
+    double *d_G = nullptr, *d_Mp = nullptr, *d_Gx = nullptr, *d_Mpx = nullptr;
+    double *d_Gkw = nullptr, *d_Mpkw = nullptr, *d_tabs = nullptr, *d_bounds = nullptr;
+    double *d_tailpow = nullptr;
+    float *d_lut = nullptr;
+    // workspace offsets
+    size_t ws_bytes = 0;
+    size_t o_a16, o_e, o_s, o_p16, o_ex, o_sx, o_bands, o_r, o_att, o_guess, o_end;
+    size_t o_ekw, o_skw, o_parts, o_phop;
+};
+
+namespace {
+
+template <class T>
+int upload(T **dst, const T *src, size_t n) {
+    if (n == 0) n = 1;
+    HIPCHK(hipMalloc((void **)dst, n * sizeof(T)));
+    if (src) HIPCHK(hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+    return AMX_OK;
+}
+template <class T>
+T *wsp(void *ws, size_t off) {
+    return reinterpret_cast<T *>(reinterpret_cast<char *>(ws) + off);
+}
+
+int64_t overlay_len(int64_t n, int fs) {
+    // pydub: int(round(1000*(n/fs)) * (fs/1000.0)), Python round = half-to-even
+    double ms = std::nearbyint(1000.0 * ((double)n / (double)fs));
+    return (int64_t)(ms * (fs / 1000.0));
+}
+
+}  // namespace
+
+extern "C" {
+
+int amx_abi_version(void) { return AMX_ABI_VERSION; }
+const char *amx_last_error(void) { return g_err.c_str(); }
+
+int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t n_chunks,
+                    const int64_t *track_frame0, const int64_t *track_total_frames,
+                    int32_t seg_frames, amx_plan **out) {
+    if (!desc || !out || (n_chunks > 0 && !chunks) || n_chunks < 0)
+        return fail(AMX_EINVAL, "amx_plan_create: null argument");
+    if (desc->sample_rate <= 0) return fail(AMX_EINVAL, "sample_rate must be > 0");
+    if (desc->channels_in != 1 && desc->channels_in != 2)
+        return fail(AMX_EINVAL, "channels_in must be 1 or 2");
+    *out = nullptr;
+    amx_plan *p = new (std::nothrow) amx_plan();
+    if (!p) return fail(AMX_ENOMEM, "out of memory");
+    p->desc = *desc;
+    const int fs = desc->sample_rate;
+    p->L = seg_frames > 0 ? seg_frames : 256;
+    p->hop = (fs + 5) / 10;                    // libebur128 samples_in_100ms
+    p->Lkw = 512 < p->hop ? 512 : p->hop;
+    ChainDev &cd = p->cd;
+    memset(&cd, 0, sizeof cd);
+    cd.fs = fs;
+    cd.chin = desc->channels_in;
+    cd.in_s16 = desc->input_s16 ? 1 : 0;
+    cd.analog_on = desc->analog_on ? 1 : 0;
+    cd.has_lut = desc->tanh_lut ? 1 : 0;
+    cd.drive = desc->analog_drive;
+    for (int k = 0; k < 6; k++) {
+        cd.an_lo[k] = desc->analog_lo_ba[k];
+        cd.an_hi[k] = desc->analog_hi_ba[k];
+    }
+    cd.an_glo1 = desc->analog_lo_gain - 1.0;
+    cd.an_ghi1 = desc->analog_hi_gain - 1.0;
+    // EQ stages and the compact state model
+    int mask = 0, D = 0;
+    for (int s = 0; s < 4; s++) {
+        int kind = desc->eq_kind[s];
+        int want = (s == 0 || s == 3) ? 1 : 2;
+        if (kind != 0 && kind != want) {
+            delete p;
+            return fail(AMX_EINVAL, "eq stage %d: kind %d not supported at this position", s, kind);
+        }
+        EqStageDev &st = cd.st[s];
+        st.kind = kind;
+        if (!kind) continue;
+        mask |= 1 << s;
+        D += kind == 1 ? 2 : 8;
+        st.neg = desc->eq_gain_db[s] < 0 ? 1 : 0;
+        st.g = desc->eq_gain[s];
+        st.gm1 = desc->eq_gain[s] - 1.0;
+        st.gf = (float)desc->eq_gain[s];
+        for (int k = 0; k < 24; k++) st.c[k] = desc->eq_coef[s][k];
+    }
+    cd.eq_mask = mask;
+    cd.eq_dim = D;
+    p->mask = mask;
+    p->D = D;
+    cd.width_on = desc->width_on ? 1 : 0;
+    cd.width = desc->width;
+    cd.mb_on = p->mb = desc->multiband_on ? 1 : 0;
+    for (int k = 0; k < 12; k++) {
+        cd.xlo[k] = desc->xover_lo_sos[k];
+        cd.xhi[k] = desc->xover_hi_sos[k];
+    }
+    cd.look = (int32_t)(5.0 * (fs / 1000.0));
+    // K-weighting coefficients (libebur128 ebur128_init_filter)
+    {
+        double f0 = 1681.974450955533, G = 3.999843853973347, Q = 0.7071752369554196;
+        double K = std::tan(M_PI * f0 / (double)fs);
+        double Vh = std::pow(10.0, G / 20.0);
+        double Vb = std::pow(Vh, 0.4996667741545416);
+        double pb[3] = {0.0, 0.0, 0.0}, pa[3] = {1.0, 0.0, 0.0};
+        double rb[3] = {1.0, -2.0, 1.0}, ra[3] = {1.0, 0.0, 0.0};
+        double a0 = 1.0 + K / Q + K * K;
+        pb[0] = (Vh + Vb * K / Q + K * K) / a0;
+        pb[1] = 2.0 * (K * K - Vh) / a0;
+        pb[2] = (Vh - Vb * K / Q + K * K) / a0;
+        pa[1] = 2.0 * (K * K - 1.0) / a0;
+        pa[2] = (1.0 - K / Q + K * K) / a0;
+        f0 = 38.13547087602444;
+        Q = 0.5003270373238773;
+        K = std::tan(M_PI * f0 / (double)fs);
+        ra[1] = 2.0 * (K * K - 1.0) / (1.0 + K / Q + K * K);
+        ra[2] = (1.0 - K / Q + K * K) / (1.0 + K / Q + K * K);
+        cd.kb[0] = pb[0] * rb[0];
+        cd.kb[1] = pb[0] * rb[1] + pb[1] * rb[0];
+        cd.kb[2] = pb[0] * rb[2] + pb[1] * rb[1] + pb[2] * rb[0];
+        cd.kb[3] = pb[1] * rb[2] + pb[2] * rb[1];
+        cd.kb[4] = pb[2] * rb[2];
+        cd.ka[0] = pa[0] * ra[0];
+        cd.ka[1] = pa[0] * ra[1] + pa[1] * ra[0];
+        cd.ka[2] = pa[0] * ra[2] + pa[1] * ra[1] + pa[2] * ra[0];
+        cd.ka[3] = pa[1] * ra[2] + pa[2] * ra[1];
+        cd.ka[4] = pa[2] * ra[2];
+    }
+    // compressor tables (pydub compress_dynamic_range, exact C math == CPython math)
+    std::vector<double> tabs;
+    if (p->mb) {
+        tabs.assign((size_t)3 * 3 * 32769, 0.0);
+        const double A = 5.0 * (fs / 1000.0), R = 50.0 * (fs / 1000.0);
+        for (int b = 0; b < 3; b++) {
+            double thr = 32768.0 * std::pow(10.0, desc->comp_threshold_db[b] / 20.0);
+            double ratio = desc->comp_ratio[b];
+            if (ratio == 0.0) {
+                delete p;
+                return fail(AMX_EINVAL, "compressor ratio must be non-zero");
+            }
+            int rthr = 0;
+            while (rthr <= 32768 && !((double)rthr > thr)) rthr++;
+            cd.rthr[b] = rthr;
+            double k = 1.0 - (1.0 / ratio);
+            double ln10 = std::log(10.0);
+            double *mt = &tabs[(size_t)b * 3 * 32769];
+            for (int r = 0; r <= 32768; r++) {
+                double m;
+                if (desc->comp_m_table[b]) {
+                    m = desc->comp_m_table[b][r];
+                } else {
+                    double over = 0.0;
+                    if (r != 0) {
+                        double db = 20 * (std::log((double)r / thr) / ln10);
+                        over = (0 > db) ? 0.0 : db;
+                    }
+                    m = k * over;
+                }
+                mt[r] = m;
+                mt[32769 + r] = m / A;
+                mt[2 * 32769 + r] = m / R;
+            }
+        }
+    }
+    // ------------------------------------------------ chunks, tracks, segments
+    int n_tracks = 0;
+    for (int c = 0; c < n_chunks; c++) {
+        if (chunks[c].frames < 0 || chunks[c].in_offset < 0 || chunks[c].track < 0) {
+            delete p;
+            return fail(AMX_EINVAL, "chunk %d: negative field", c);
+        }
+        if (c > 0 && chunks[c].track < chunks[c - 1].track) {
+            delete p;
+            return fail(AMX_EINVAL, "chunks must be ordered by track");
+        }
+        n_tracks = chunks[c].track + 1 > n_tracks ? chunks[c].track + 1 : n_tracks;
+    }
+    p->n_tracks = n_tracks;
+    p->n_chunks = n_chunks;
+    int64_t loc = 0, outo = 0;
+    std::vector<int32_t> seg_first, seg_stream;
+    p->spans.assign(n_tracks, SpanDev{});
+    std::vector<int> track_seen(n_tracks, 0);
+    for (int c = 0; c < n_chunks; c++) {
+        ChunkDev ch{};
+        ch.in_off = chunks[c].in_offset;
+        ch.loc_off = loc;
+        ch.out_off = outo;
+        ch.n = chunks[c].frames;
+        int64_t n1 = ch.n, n2 = ch.n;
+        if (p->mb && ch.n > 0) {
+            n1 = overlay_len(ch.n, fs);
+            n2 = overlay_len(n1, fs);
+        }
+        ch.out_n = n2;
+        ch.track = chunks[c].track;
+        ch.seg0 = (int32_t)p->segs.size();
+        int64_t ns = (ch.n + p->L - 1) / p->L;
+        ch.nseg = (int32_t)ns;
+        for (int64_t k = 0; k < ns; k++) {
+            SegDev s{};
+            s.pos = k * p->L;
+            s.chunk = c;
+            s.len = (int32_t)((ch.n - s.pos) < p->L ? (ch.n - s.pos) : p->L);
+            s.first = ch.seg0;
+            s.last = (k == ns - 1) ? 1 : 0;
+            p->segs.push_back(s);
+            seg_first.push_back(ch.seg0);
+            seg_stream.push_back(c);
+        }
+        SpanDev &sp = p->spans[ch.track];
+        if (!track_seen[ch.track]) {
+            sp.out_off = outo;
+            track_seen[ch.track] = 1;
+        }
+        sp.out_n += n2;
+        p->chunks.push_back(ch);
+        p->n1tab.push_back(n1);
+        p->max_chunk_out = n2 > p->max_chunk_out ? n2 : p->max_chunk_out;
+        loc += ch.n;
+        outo += n2;
+    }
+    p->nloc = loc;
+    p->out_frames = outo;
+    p->n_seg = (int)p->segs.size();
+    // K-weighting segments per track span
+    std::vector<int32_t> kfirst, kstream;
+    for (int t = 0; t < n_tracks; t++) {
+        SpanDev &sp = p->spans[t];
+        sp.tframe0 = track_frame0 ? track_frame0[t] : 0;
+        sp.ttotal = track_total_frames ? track_total_frames[t] : sp.out_n;
+        sp.kseg0 = (int32_t)p->ksegs.size();
+        int64_t nk = (sp.out_n + p->Lkw - 1) / p->Lkw;
+        sp.nkseg = (int32_t)nk;
+        for (int64_t k = 0; k < nk; k++) {
+            KwSegDev s{};
+            s.out_pos = sp.out_off + k * p->Lkw;
+            s.tframe = sp.tframe0 + k * p->Lkw;
+            s.track = t;
+            s.len = (int32_t)((sp.out_n - k * p->Lkw) < p->Lkw ? (sp.out_n - k * p->Lkw) : p->Lkw);
+            s.first = sp.kseg0;
+            s.last = (k == nk - 1) ? 1 : 0;
+            p->ksegs.push_back(s);
+            kfirst.push_back(sp.kseg0);
+            kstream.push_back(t);
+        }
+        p->max_span = sp.out_n > p->max_span ? sp.out_n : p->max_span;
+    }
+    p->n_kseg = (int)p->ksegs.size();
+
+    // ------------------------------------------------------- LTI models
+    const double tol = 1e-22;
+    std::vector<double> G, Mp, Gx, Mpx, Gkw, Mpkw;
+    if (D > 0) {
+        Lti eq;
+        eq.derive(D, [&](double *z, double x) {
+            int o = 0;
+            for (int s = 0; s < 4; s++) {
+                const EqStageDev &st = cd.st[s];
+                if (st.kind == 1) {
+                    shelf_step_h(st.c, z + o, x, st.neg, st.gm1);
+                    o += 2;
+                } else if (st.kind == 2) {
+                    double b = x;
+                    for (int k = 0; k < 4; k++) b = sos_step_h(st.c + 6 * k, z + o + 2 * k, b);
+                    x = x + b * st.gm1;
+                    o += 8;
+                }
+            }
+        });
+        G = eq.gemv_table(p->L);
+        p->lev_eq = eq.scan_powers(p->L, tol, 7, Mp);
+        if (p->lev_eq < 0) {
+            delete p;
+            return fail(AMX_ERANGE, "EQ decays too slowly for %d-frame segments; raise seg_frames", p->L);
+        }
+    }
+    if (p->mb) {
+        Lti xo;
+        xo.derive(AMX_XO_DIM, [&](double *z, double x) {
+            double l = sos_step_h(cd.xlo, z, x);
+            sos_step_h(cd.xlo + 6, z + 2, l);
+            double h = sos_step_h(cd.xhi, z + 4, x);
+            sos_step_h(cd.xhi + 6, z + 6, h);
+        });
+        Gx = xo.gemv_table(p->L);
+        p->lev_x = xo.scan_powers(p->L, tol, 7, Mpx);
+        if (p->lev_x < 0) {
+            delete p;
+            return fail(AMX_ERANGE, "crossover decays too slowly for %d-frame segments", p->L);
+        }
+    }
+    {
+        Lti &kw = p->kw_model;
+        const double *a = cd.ka;
+        kw.derive(AMX_KW_DIM, [&](double *v, double x) {
+            double v0 = x - a[1] * v[0] - a[2] * v[1] - a[3] * v[2] - a[4] * v[3];
+            v[3] = v[2];
+            v[2] = v[1];
+            v[1] = v[0];
+            v[0] = v0;
+        });
+        Gkw = kw.gemv_table(p->Lkw);
+        p->lev_kw = kw.scan_powers(p->Lkw, tol, 7, Mpkw);
+        if (p->lev_kw < 0) {
+            delete p;
+            return fail(AMX_ERANGE, "K-weighting decays too slowly for %d-frame segments", p->Lkw);
+        }
+        p->tail_pow.assign((size_t)n_tracks * 16, 0.0);
+        for (int t = 0; t < n_tracks; t++) {
+            const SpanDev &sp = p->spans[t];
+            if (sp.nkseg == 0) continue;
+            int len_last = p->ksegs[sp.kseg0 + sp.nkseg - 1].len;
+            Mat P = matpow(kw.A, len_last, AMX_KW_DIM);
+            for (int k = 0; k < 16; k++) p->tail_pow[(size_t)t * 16 + k] = P[k];
+        }
+    }
+    // histogram boundaries (libebur128 init_histogram)
+    double bounds[1001];
+    bounds[0] = std::pow(10.0, (-70.0 + 0.691) / 10.0);
+    for (int i = 1; i < 1001; ++i) bounds[i] = std::pow(10.0, ((double)i / 10.0 - 70.0 + 0.691) / 10.0);
+
+    // ------------------------------------------------------- upload
+    int rc = AMX_OK;
+#define UP(dst, src, n)                          \
+    if ((rc = upload(&dst, src, n)) != AMX_OK) { \
+        amx_plan_free(p);                        \
+        return rc;                               \
+    }
+    UP(p->d_cd, &p->cd, 1);
+    UP(p->d_chunks, p->chunks.data(), p->chunks.size());
+    UP(p->d_segs, p->segs.data(), p->segs.size());
+    UP(p->d_ksegs, p->ksegs.data(), p->ksegs.size());
+    UP(p->d_spans, p->spans.data(), p->spans.size());
+    UP(p->d_seg_first, seg_first.data(), seg_first.size());
+    UP(p->d_seg_stream, seg_stream.data(), seg_stream.size());
+    UP(p->d_kseg_first, kfirst.data(), kfirst.size());
+    UP(p->d_kseg_stream, kstream.data(), kstream.size());
+    UP(p->d_n1, p->n1tab.data(), p->n1tab.size());
+    UP(p->d_G, G.data(), G.size());
+    UP(p->d_Mp, Mp.data(), Mp.size());
+    UP(p->d_Gx, Gx.data(), Gx.size());
+    UP(p->d_Mpx, Mpx.data(), Mpx.size());
+    UP(p->d_Gkw, Gkw.data(), Gkw.size());
+    UP(p->d_Mpkw, Mpkw.data(), Mpkw.size());
+    UP(p->d_tabs, tabs.data(), tabs.size());
+    UP(p->d_bounds, bounds, 1001);
+    UP(p->d_tailpow, p->tail_pow.data(), p->tail_pow.size());
+    if (desc->tanh_lut) UP(p->d_lut, desc->tanh_lut, 65536);
+#undef UP
+    // ------------------------------------------------------- workspace layout
+    size_t off = 0;
+    const size_t nseg = (size_t)p->n_seg, nl = (size_t)p->nloc, nk = (size_t)p->n_kseg;
+    p->o_a16 = (size_t)align_up(off, nl * 4);
+    p->o_e = (size_t)align_up(off, nseg * 2 * (D ? D : 1) * 8);
+    p->o_s = (size_t)align_up(off, nseg * 2 * (D ? D : 1) * 8);
+    if (p->mb) {
+        p->o_p16 = (size_t)align_up(off, nl * 4);
+        p->o_ex = (size_t)align_up(off, nseg * 2 * AMX_XO_DIM * 8);
+        p->o_sx = (size_t)align_up(off, nseg * 2 * AMX_XO_DIM * 8);
+        p->o_bands = (size_t)align_up(off, 3 * nl * 4);
+        p->o_r = (size_t)align_up(off, 3 * nl * 2);
+        p->o_att = (size_t)align_up(off, 3 * nl * 8);
+        p->o_guess = (size_t)align_up(off, 3 * nseg * 8);
+        p->o_end = (size_t)align_up(off, 3 * nseg * 8);
+    }
+    p->o_ekw = (size_t)align_up(off, nk * 2 * AMX_KW_DIM * 8);
+    p->o_skw = (size_t)align_up(off, nk * 2 * AMX_KW_DIM * 8);
+    p->o_parts = (size_t)align_up(off, nk * 4 * 8);
+    p->o_phop = (size_t)align_up(off, nk * 8);
+    p->ws_bytes = (off + 255) & ~(size_t)255;
+    *out = p;
+    return AMX_OK;
+}
+
+void amx_plan_free(amx_plan *p) {
+    if (!p) return;
+    void *ptrs[] = {p->d_cd,    p->d_chunks,     p->d_segs,       p->d_ksegs,        p->d_spans,
+                    p->d_seg_first, p->d_seg_stream, p->d_kseg_first, p->d_kseg_stream, p->d_n1,
+                    p->d_G,     p->d_Mp,         p->d_Gx,         p->d_Mpx,          p->d_Gkw,
+                    p->d_Mpkw,  p->d_tabs,       p->d_bounds,     p->d_tailpow,      p->d_lut};
+    for (void *q : ptrs)
+        if (q) (void)hipFree(q);
+    delete p;
+}
+
+int amx_plan_get_info(const amx_plan *p, amx_plan_info *info) {
+    if (!p || !info) return fail(AMX_EINVAL, "null argument");
+    memset(info, 0, sizeof *info);
+    info->workspace_bytes = (int64_t)p->ws_bytes;
+    info->out_frames = p->out_frames;
+    info->n_tracks = p->n_tracks;
+    info->n_chunks = p->n_chunks;
+    info->n_segments = p->n_seg;
+    info->seg_frames = p->L;
+    info->scan_levels_eq = p->lev_eq;
+    info->scan_levels_xover = p->lev_x;
+    info->scan_levels_kw = p->lev_kw;
+    info->eq_dim = p->D;
+    info->hop_frames = p->hop;
+    return AMX_OK;
+}
+
+int amx_plan_track_span(const amx_plan *p, int32_t track, amx_track_span *span) {
+    if (!p || !span || track < 0 || track >= p->n_tracks) return fail(AMX_EINVAL, "bad track");
+    const SpanDev &s = p->spans[track];
+    span->out_offset = s.out_off;
+    span->out_frames = s.out_n;
+    span->track_frame0 = s.tframe0;
+    span->track_frames_total = s.ttotal;
+    return AMX_OK;
+}
+
+int amx_run_chunks(amx_plan *p, const float *d_in, int16_t *d_out, void *d_ws, void *stream) {
+    if (!p || (p->nloc > 0 && (!d_in || !d_out || !d_ws))) return fail(AMX_EINVAL, "null argument");
+    if (p->n_seg == 0) return AMX_OK;
+    hipStream_t st = (hipStream_t)stream;
+    amx::Launch l{p->d_cd, p->d_chunks, p->d_segs, p->n_chunks, p->n_seg, p->L, st};
+    int16_t *a16 = wsp<int16_t>(d_ws, p->o_a16);
+    double *e = wsp<double>(d_ws, p->o_e), *s = wsp<double>(d_ws, p->o_s);
+    HIPCHK(amx::launch_front1_lut(l, p->mask, d_in, p->d_lut, a16, p->d_G, e));
+    if (p->D > 0)
+        HIPCHK(amx::launch_scan(e, s, p->d_seg_first, p->d_seg_stream, p->n_seg, p->D, 2, p->d_Mp,
+                                p->lev_eq, nullptr, st));
+    if (!p->mb) {
+        HIPCHK(amx::launch_front2(l, p->mask, a16, s, d_out, 1, nullptr, nullptr));
+        return AMX_OK;
+    }
+    int16_t *p16 = wsp<int16_t>(d_ws, p->o_p16);
+    double *ex = wsp<double>(d_ws, p->o_ex), *sx = wsp<double>(d_ws, p->o_sx);
+    HIPCHK(amx::launch_front2(l, p->mask, a16, s, p16, 0, p->d_Gx, ex));
+    HIPCHK(amx::launch_scan(ex, sx, p->d_seg_first, p->d_seg_stream, p->n_seg, AMX_XO_DIM, 2,
+                            p->d_Mpx, p->lev_x, nullptr, st));
+    int16_t *bands = wsp<int16_t>(d_ws, p->o_bands);
+    uint16_t *r = wsp<uint16_t>(d_ws, p->o_r);
+    double *att = wsp<double>(d_ws, p->o_att);
+    double *guess = wsp<double>(d_ws, p->o_guess), *endv = wsp<double>(d_ws, p->o_end);
+    HIPCHK(amx::launch_xover2(l, p16, sx, bands, p->nloc));
+    HIPCHK(amx::launch_rms(l, bands, r, p->nloc));
+    HIPCHK(amx::launch_env(l, r, p->d_tabs, att, guess, endv, p->nloc, p->warm));
+    HIPCHK(amx::launch_fix(l, r, p->d_tabs, att, guess, endv, p->nloc));
+    HIPCHK(amx::launch_apply_n1(l, bands, att, d_out, p->nloc, p->max_chunk_out, p->d_n1));
+    return AMX_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, double *d_kw_tail, double *d_peak,
+                       void *d_ws, void *stream) {
+    if (!p || !d_kw_tail || !d_peak || (p->n_kseg > 0 && (!d_out || !d_ws)))
+        return fail(AMX_EINVAL, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(d_peak, 0, sizeof(double) * 2 * (size_t)p->n_tracks, st));
+    if (p->n_kseg == 0) {
+        HIPCHK(hipMemsetAsync(d_kw_tail, 0, sizeof(double) * 8 * (size_t)p->n_tracks, st));
+        return AMX_OK;
+    }
+    double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
+    HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e,
+                           reinterpret_cast<unsigned long long *>(d_peak), st));
+    HIPCHK(amx::launch_scan(e, s, p->d_kseg_first, p->d_kseg_stream, p->n_kseg, AMX_KW_DIM, 2,
+                            p->d_Mpkw, p->lev_kw, nullptr, st));
+    HIPCHK(amx::launch_kw_tail(p->d_spans, p->n_tracks, s, e, p->d_tailpow, d_kw_tail, st));
+    return AMX_OK;
+}
+
+int amx_kw_propagate(const amx_plan *p, int64_t frames, const double *in8, double *out8) {
+    if (!p || !in8 || !out8 || frames < 0) return fail(AMX_EINVAL, "bad argument");
+    Mat P = matpow(p->kw_model.A, frames, AMX_KW_DIM);
+    for (int c = 0; c < 2; c++)
+        for (int i = 0; i < AMX_KW_DIM; i++) {
+            double acc = 0.0;
+            for (int k = 0; k < AMX_KW_DIM; k++) acc += P[(size_t)i * AMX_KW_DIM + k] * in8[c * 4 + k];
+            out8[c * 4 + i] = acc;
+        }
+    return AMX_OK;
+}
+
+int amx_loudness_pass2(amx_plan *p, const int16_t *d_out, const double *d_kw_carry,
+                       double *d_hops, int64_t max_hops, void *d_ws, void *stream) {
+    if (!p || !d_hops || max_hops <= 0 || (p->n_kseg > 0 && (!d_out || !d_ws)))
+        return fail(AMX_EINVAL, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(d_hops, 0, sizeof(double) * 2 * (size_t)max_hops * p->n_tracks, st));
+    if (p->n_kseg == 0) return AMX_OK;
+    double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
+    double *parts = wsp<double>(d_ws, p->o_parts);
+    int64_t *phop = wsp<int64_t>(d_ws, p->o_phop);
+    HIPCHK(amx::launch_scan(e, s, p->d_kseg_first, p->d_kseg_stream, p->n_kseg, AMX_KW_DIM, 2,
+                            p->d_Mpkw, p->lev_kw, d_kw_carry, st));
+    HIPCHK(amx::launch_kw2(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, p->hop, d_out, s, parts, phop, st));
+    HIPCHK(amx::launch_hops(p->d_spans, p->n_tracks, p->d_ksegs, p->Lkw, p->hop, parts, phop, d_hops,
+                            max_hops, st));
+    return AMX_OK;
+}
+
+int amx_loudness_histograms(amx_plan *p, const double *d_hops, int64_t max_hops, uint64_t *d_hist,
+                            uint64_t *d_st_hist, void *d_ws, void *stream) {
+    (void)d_ws;
+    if (!p || !d_hops || !d_hist || !d_st_hist || max_hops <= 0)
+        return fail(AMX_EINVAL, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(d_hist, 0, sizeof(uint64_t) * AMX_HIST_BINS * (size_t)p->n_tracks, st));
+    HIPCHK(hipMemsetAsync(d_st_hist, 0, sizeof(uint64_t) * AMX_HIST_BINS * (size_t)p->n_tracks, st));
+    HIPCHK(amx::launch_hist(p->d_spans, p->n_tracks, p->hop, d_hops, max_hops, p->d_bounds,
+                            reinterpret_cast<unsigned long long *>(d_hist),
+                            reinterpret_cast<unsigned long long *>(d_st_hist), st));
+    return AMX_OK;
+}
+
+int amx_limiter_geometry(const amx_plan *p, const amx_final_desc *fd, int32_t *buffer_size,
+                         int32_t *halo_frames, int64_t *state_doubles) {
+    if (!p || !fd) return fail(AMX_EINVAL, "null argument");
+    const int channels = 2;
+    double attack = fd->attack_ms / 1000.0;
+    int bs = (int)(p->cd.fs * attack * channels);   // af_alimiter config_input
+    bs -= bs % channels;
+    if (bs <= 0) return fail(AMX_EINVAL, "Attack is too small.");
+    if (buffer_size) *buffer_size = bs;
+    if (halo_frames) *halo_frames = bs / channels - 1;
+    if (state_doubles) *state_doubles = 8 + 3 * (int64_t)bs;
+    return AMX_OK;
+}
+
+int amx_finalize(amx_plan *p, const amx_final_desc *fd, const int16_t *d_x,
+                 const double *d_gains, int32_t fast, const int16_t *d_halo, int16_t *d_y,
+                 double *d_lim_state, void *d_ws, void *stream) {
+    (void)d_ws;
+    if (!p || !fd || !d_gains || (p->out_frames > 0 && (!d_x || !d_y)))
+        return fail(AMX_EINVAL, "null argument");
+    if (p->out_frames == 0) return AMX_OK;
+    int32_t bs = 0, halo = 0;
+    int64_t sd = 0;
+    int rc = amx_limiter_geometry(p, fd, &bs, &halo, &sd);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const double level = fd->auto_level ? 1 / fd->limit : 1;
+    if (fast) {
+        HIPCHK(amx::launch_final_fast(p->d_spans, p->n_tracks, p->max_span, d_x, d_halo, halo,
+                                      d_gains, fd->level_in, level, fd->level_out, fd->limit,
+                                      d_y, st));
+    } else {
+        if (!d_lim_state) return fail(AMX_EINVAL, "general limiter needs d_lim_state");
+        HIPCHK(amx::launch_final_general(p->d_spans, p->n_tracks, d_x, d_halo, halo, d_gains,
+                                         p->cd.fs, fd->level_in, level, fd->level_out, fd->limit,
+                                         fd->release_ms / 1000.0, bs, d_lim_state, sd, d_y, st));
+    }
+    return AMX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,194 @@
+/*
+ * amx.h -- C ABI of libamx.so, the MI355X-native mastering DSP hot path.
+ *
+ * Drop-in boundary for the reference's per-chunk mastering pipeline
+ * (theouterlimitz/Audio-Mastering-Engine, audio_mastering_engine.py):
+ *
+ *   reference interface                                  | replaced by
+ *   -----------------------------------------------------+-------------------------------
+ *   chunk loop :185-204 (AudioSegment -> analog :192,    | amx_run_chunks()
+ *     float :193, EQ :194, width :195, int16 :196,       |
+ *     multiband :197) + ffmpeg concat :205-214           |
+ *   normalize_loudness_on_disk_with_ffmpeg :227-246      | amx_loudness_pass1/pass2(),
+ *     (ffmpeg loudnorm pass 1 measurement :229-237)      | amx_loudness_histograms()
+ *   loudnorm pass 2 (linear mode) :240-242 +             | amx_finalize()
+ *     final alimiter :223                                |
+ *   process_audio_with_ffmpeg_pipeline :171-226          | host: amx/engine.py master_audio()
+ *
+ * Conventions:
+ *  - every function returns AMX_OK (0) or a negative AMX_E* code; amx_last_error()
+ *    returns a thread-local message for the last failure on the calling thread;
+ *  - the caller owns every device pointer it passes (input, output, workspace);
+ *    the plan owns only its small constant tables;
+ *  - device calls are asynchronous on the given hipStream_t (passed as void*);
+ *    they never allocate, copy synchronously or synchronise, so they may be
+ *    captured into a hipGraph;
+ *  - one plan per stream/thread; plans are not shared across threads;
+ *  - no torch types cross this ABI; multi-GPU exchange (RCCL all-reduce of the
+ *    loudness partials, K-filter carry all-gather) is done by the host between
+ *    calls, on buffers this ABI fills and consumes.
+ */
+#ifndef AMX_H
+#define AMX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AMX_OK 0
+#define AMX_EINVAL -1     /* bad argument / settings */
+#define AMX_EHIP -2       /* HIP runtime error */
+#define AMX_ENOMEM -3     /* host allocation failed */
+#define AMX_ERANGE -4     /* a size or filter is outside what the plan supports */
+
+#define AMX_ABI_VERSION 1
+
+#if defined(__GNUC__)
+#define AMX_API __attribute__((visibility("default")))
+#else
+#define AMX_API
+#endif
+
+/* Filter coefficients and parameters of the chain.  The host designs them with
+ * the same calls the reference makes (scipy.signal.butter at :285, :296,
+ * :301-302), so the device sees the reference's exact numbers. */
+typedef struct amx_chain_desc {
+    int32_t sample_rate;
+    int32_t channels_in;          /* 1 or 2; mono is duplicated to stereo (:190) */
+    int32_t input_s16;            /* 0: d_in is float32 (quantised on device like ffmpeg's
+                                     f32->s16 segment split, A.1); 1: d_in is int16 already */
+    int32_t pad0_;
+    /* analog character (:258-266), applied if analog_on */
+    int32_t analog_on;
+    float analog_drive;           /* float32(1 + 0.5*cf) */
+    const float *tanh_lut;        /* 65536 float32: tanh(float32(s/32768)*drive) for
+                                     s = -32768..32767 (numpy's float32 tanh); NULL ->
+                                     device computes correctly-rounded float32 tanh */
+    double analog_lo_ba[6];       /* butter(2,120/(fs/2),'low'):  b0 b1 b2 a0 a1 a2 */
+    double analog_lo_gain;        /* 10**(cf/20) */
+    double analog_hi_ba[6];       /* butter(2,12000/(fs/2),'high') */
+    double analog_hi_gain;        /* 10**(1.5cf/20) */
+    /* 4-stage EQ (:277-282): stage order low shelf 250 Hz, peak 1 kHz, peak 4 kHz,
+     * high shelf 8 kHz.  kind 0 = skipped (gain 0), 1 = shelf (ba in coef[0..5]),
+     * 2 = peak (4 SOS rows [b0 b1 b2 a0 a1 a2] in coef[0..23]). */
+    int32_t eq_kind[4];
+    double eq_gain_db[4];
+    double eq_gain[4];            /* 10**(gain_db/20) */
+    double eq_coef[4][24];
+    /* stereo width (:267-271) */
+    int32_t width_on;
+    float width;
+    /* multiband (:299-309) */
+    int32_t multiband_on;
+    double xover_lo_sos[12];      /* butter(4,250,'lowpass',fs,sos) */
+    double xover_hi_sos[12];      /* butter(4,4000,'highpass',fs,sos) */
+    double comp_threshold_db[3];  /* low, mid, high */
+    double comp_ratio[3];
+    const double *comp_m_table[3];/* optional override of max_attenuation(rms), rms=0..32768;
+                                     NULL -> the plan tabulates it with the C library's
+                                     log/pow, which is what CPython's math uses (pydub) */
+} amx_chain_desc;
+
+/* One ~30 s chunk of one track (the ffmpeg segment split, :178). */
+typedef struct amx_chunk {
+    int32_t track;                /* track index within the plan */
+    int32_t pad_;
+    int64_t in_offset;            /* first input frame of the chunk in d_in */
+    int64_t frames;               /* chunk length in frames */
+} amx_chunk;
+
+/* Loudness / finalize parameters (af_loudnorm linear mode + af_alimiter, :223). */
+typedef struct amx_final_desc {
+    double limit;                 /* 0.98 */
+    double attack_ms;             /* 5 */
+    double release_ms;            /* 50 */
+    double level_in, level_out;   /* 1, 1 */
+    int32_t auto_level;           /* 1 (alimiter default) */
+    int32_t pad_;
+} amx_final_desc;
+
+typedef struct amx_plan amx_plan;
+
+typedef struct amx_plan_info {
+    int64_t workspace_bytes;      /* caller-allocated device scratch for all calls */
+    int64_t out_frames;           /* total output frames over all tracks of the plan */
+    int32_t n_tracks;
+    int32_t n_chunks;
+    int64_t n_segments;           /* IIR segments over all chunks */
+    int32_t seg_frames;           /* frames per IIR segment */
+    int32_t scan_levels_eq;
+    int32_t scan_levels_xover;
+    int32_t scan_levels_kw;
+    int32_t eq_dim;
+    int32_t hop_frames;           /* libebur128 samples_in_100ms */
+} amx_plan_info;
+
+/* Per-track output span of this plan inside the full track timeline (for chunk
+ * sharding over ranks: a rank holds a contiguous run of chunks of a track). */
+typedef struct amx_track_span {
+    int64_t out_offset;           /* first output frame of this plan's part, in the plan's d_out */
+    int64_t out_frames;           /* frames this plan produces for the track */
+    int64_t track_frame0;         /* index of that first frame in the WHOLE track timeline */
+    int64_t track_frames_total;   /* output frames of the whole track (all ranks) */
+} amx_track_span;
+
+AMX_API int amx_abi_version(void);
+AMX_API const char *amx_last_error(void);
+
+/* Build a plan (host only: designs nothing, derives scan matrices and segment
+ * tables from the given coefficients, uploads small constant tables).
+ * track_frame0/track_total may be NULL for a plan that holds whole tracks. */
+AMX_API int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t n_chunks,
+                    const int64_t *track_frame0, const int64_t *track_total_frames,
+                    int32_t seg_frames, amx_plan **out);
+AMX_API void amx_plan_free(amx_plan *plan);
+AMX_API int amx_plan_get_info(const amx_plan *plan, amx_plan_info *info);
+AMX_API int amx_plan_track_span(const amx_plan *plan, int32_t track, amx_track_span *span);
+
+/* Per-chunk chain: d_in float32 [frames, channels_in] -> d_out int16 [out_frames, 2]
+ * (tracks back to back, chunks concatenated = the ffmpeg concat of :210-212). */
+AMX_API int amx_run_chunks(amx_plan *plan, const float *d_in, int16_t *d_out, void *d_ws, void *stream);
+
+/* Loudness pass 1 over d_out (libebur128 restated, ffmpeg loudnorm :229):
+ * K-filter zero-state GEMV per segment + exact scan + sample peak.
+ * d_kw_tail [n_tracks][2][4]: K-filter state at each span end assuming the span
+ * started from rest (what the NEXT rank of a chunk-sharded track needs, see
+ * amx_kw_propagate); d_peak [n_tracks][2]: max |x| per channel (zeroed here). */
+AMX_API int amx_loudness_pass1(amx_plan *plan, const int16_t *d_out, double *d_kw_tail, double *d_peak,
+                       void *d_ws, void *stream);
+/* Host helper for chunk-sharded tracks: out8 = A^frames * in8 (per channel 4x4 K-filter
+ * transition), so carry(r+1) = A^{len_r} carry(r) + tail(r). */
+AMX_API int amx_kw_propagate(const amx_plan *plan, int64_t frames, const double *in8, double *out8);
+/* Loudness pass 2: K-filter from the exact state (d_kw_carry [n_tracks][2][4] = state
+ * entering each span, NULL = rest), squared and summed per 100 ms hop on the
+ * WHOLE-track hop grid: d_hops [n_tracks][max_hops][2] (zeroed here; hops a span only
+ * partly covers hold partial sums -- sum them over ranks, e.g. RCCL all-reduce). */
+AMX_API int amx_loudness_pass2(amx_plan *plan, const int16_t *d_out, const double *d_kw_carry,
+                       double *d_hops, int64_t max_hops, void *d_ws, void *stream);
+/* Gating-block (400 ms / 100 ms hop) and short-term (3 s / 1 s) histograms from
+ * whole-track hop energies.  d_hist, d_st_hist [n_tracks][1000] uint64 (zeroed here). */
+AMX_API int amx_loudness_histograms(amx_plan *plan, const double *d_hops, int64_t max_hops,
+                            uint64_t *d_hist, uint64_t *d_st_hist, void *d_ws, void *stream);
+
+/* alimiter geometry: ring size in samples (fs*attack*channels), the frame delay
+ * (ring frames - 1 = halo frames a span needs from its predecessor) and the state
+ * doubles per track for the general path. */
+AMX_API int amx_limiter_geometry(const amx_plan *plan, const amx_final_desc *fd, int32_t *buffer_size,
+                         int32_t *halo_frames, int64_t *state_doubles);
+/* Finalize: loudnorm linear gain (d_gains[t] <= 0 -> no normalisation, :216) then
+ * alimiter (:223) -> d_y int16 [out_frames, 2] (same frame indexing as d_x).
+ * d_halo [n_tracks][halo_frames][2]: the input frames preceding each span (ignored
+ * for spans that start their track).  fast != 0: host proved max|gained sample| <=
+ * limit, so the limiter never engages and is an exact delay + level.  Otherwise the
+ * sequential limiter runs; d_lim_state [n_tracks][state_doubles] carries its state
+ * in (span not starting the track) and out (span end). */
+AMX_API int amx_finalize(amx_plan *plan, const amx_final_desc *fd, const int16_t *d_x,
+                 const double *d_gains, int32_t fast, const int16_t *d_halo, int16_t *d_y,
+                 double *d_lim_state, void *d_ws, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AMX_H */

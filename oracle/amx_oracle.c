@@ -603,3 +603,54 @@ EXPORT void orc_quantize(const float *x, int64_t n, int channels, int16_t *out) 
         }
     }
 }
+
+/* libebur128 gated loudness / relative threshold / loudness range from
+ * histograms (ebur128_gated_loudness, ff_ebur128_relative_threshold,
+ * ff_ebur128_loudness_range_multiple), single state.  out[0]=I, out[1]=LRA,
+ * out[2]=threshold (LUFS). */
+EXPORT void orc_loudness_stats(const uint64_t *hist, const uint64_t *st_hist, double *out) {
+    orc_ebur128_tables(NULL, NULL);
+    const double gate = pow(10.0, -10.0 / 10.0);
+    double rel = 0.0;
+    uint64_t cnt = 0;
+    for (int j = 0; j < 1000; ++j) { rel += hist[j] * hist_energies[j]; cnt += hist[j]; }
+    double I = -HUGE_VAL, thr = -70.0;
+    if (cnt) {
+        rel /= (double)cnt;
+        rel *= gate;
+        thr = 10 * log10(rel) - 0.691;
+        size_t start;
+        if (rel < hist_bounds[0]) start = 0;
+        else { start = find_hist_index(rel); if (rel > hist_energies[start]) ++start; }
+        double g = 0.0;
+        uint64_t above = 0;
+        for (size_t j = start; j < 1000; ++j) { g += hist[j] * hist_energies[j]; above += hist[j]; }
+        if (above) I = 10 * log10(g / (double)above) - 0.691;
+    }
+    /* LRA */
+    double lra = 0.0, stl_size = 0.0, stl_power = 0.0;
+    for (int j = 0; j < 1000; ++j) { stl_size += st_hist[j]; stl_power += st_hist[j] * hist_energies[j]; }
+    if (stl_size) {
+        stl_power /= stl_size;
+        double stl_int = pow(10.0, -20.0 / 10.0) * stl_power;
+        size_t index;
+        if (stl_int < hist_bounds[0]) index = 0;
+        else { index = find_hist_index(stl_int); if (stl_int > hist_energies[index]) ++index; }
+        stl_size = 0;
+        for (size_t j = index; j < 1000; ++j) stl_size += st_hist[j];
+        if (stl_size) {
+            size_t plo = (size_t)((stl_size - 1) * 0.1 + 0.5);
+            size_t phi = (size_t)((stl_size - 1) * 0.95 + 0.5);
+            stl_size = 0;
+            size_t j = index;
+            while (stl_size <= plo) stl_size += st_hist[j++];
+            double l_en = hist_energies[j - 1];
+            while (stl_size <= phi) stl_size += st_hist[j++];
+            double h_en = hist_energies[j - 1];
+            lra = (10 * log10(h_en) - 0.691) - (10 * log10(l_en) - 0.691);
+        }
+    }
+    out[0] = I;
+    out[1] = lra;
+    out[2] = thr;
+}

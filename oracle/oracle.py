@@ -301,3 +301,60 @@ def linear_gain(x16, gain):
     out = np.empty_like(x16)
     lib().orc_linear_gain(_p(x16, _i16p), _i64(x16.size), ctypes.c_double(gain), _p(out, _i16p))
     return out
+
+
+def loudness_stats(hist, st_hist):
+    out = np.zeros(3, np.float64)
+    h = np.ascontiguousarray(hist, np.uint64)
+    s = np.ascontiguousarray(st_hist, np.uint64)
+    lib().orc_loudness_stats(_p(h, _u64p), _p(s, _u64p), _p(out, _f64p))
+    return float(out[0]), float(out[1]), float(out[2])
+
+
+def loudnorm_measure(x16, fs):
+    """pass-1 JSON 'input_*' strings (native-rate restatement, see amx_oracle.c)."""
+    hist, st, peak, _ = ebur128(x16, fs)
+    I, lra, thr = loudness_stats(hist, st)
+    tp = float(peak.max()) if peak.size else 0.0
+    tp_db = 20.0 * np.log10(tp) if tp > 0 else -np.inf
+    f = lambda v: "%.2f" % v
+    return {"input_i": f(I), "input_tp": f(tp_db), "input_lra": f(lra), "input_thresh": f(thr)}
+
+
+def loudnorm_linear_gain(stats, target_i, target_tp=-1.5, target_lra=11.0):
+    if stats["input_i"] == "-inf":
+        return "skip", None
+    mi, mtp = float(stats["input_i"]), float(stats["input_tp"])
+    mlra, mth = float(stats["input_lra"]), float(stats["input_thresh"])
+    off = target_i - mi
+    if mtp != 99 and mth != -70 and mlra != 0 and mi != 0:
+        if mtp + off <= target_tp and mlra <= target_lra:
+            return "linear", 10.0 ** (off / 20.0)
+    return "dynamic", None
+
+
+def pipeline(x, fs, settings, chunks):
+    """Whole process_audio_with_ffmpeg_pipeline (:171-226) on CPU.
+
+    x: int16 [n, C] (already the ffmpeg s16 conversion) ; chunks: [(start, n)].
+    Returns (int16 output [n', 2], info dict)."""
+    x = np.asarray(x)
+    if x.ndim == 1:
+        x = x.reshape(-1, 1)
+    if x.shape[1] == 1:
+        x = np.repeat(x, 2, axis=1)
+    outs = [chunk(x[s:s + n], fs, settings) for s, n in chunks]
+    cat = np.concatenate(outs, axis=0) if outs else np.zeros((0, 2), np.int16)
+    info = {"concat": cat}
+    y = cat
+    lufs = settings.get("lufs")
+    if lufs is not None:
+        st = loudnorm_measure(cat, fs)
+        mode, g = loudnorm_linear_gain(st, float(lufs))
+        info.update(stats=st, mode=mode, gain=g)
+        if mode == "linear":
+            y = linear_gain(cat, g)
+        elif mode == "dynamic":
+            raise NotImplementedError("dynamic loudnorm")
+    info["normalized"] = y
+    return alimiter(y, fs), info

@@ -1,0 +1,119 @@
+"""CPU: host logic of the product (design, chunk plan, WAV I/O, C-ABI exports,
+drop-in call surface)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def test_libamx_builds_and_exports_every_header_symbol():
+    import re
+    from amx import build, capi
+    build.build()
+    lib = ctypes.CDLL(capi.LIB_PATH)
+    with open(os.path.join(ROOT, "include", "amx.h")) as f:
+        declared = set(re.findall(r"AMX_API\s+[\w\s\*]*?\b(amx_\w+)\s*\(", f.read()))
+    assert declared == set(capi.EXPORTS), declared ^ set(capi.EXPORTS)
+    for sym in declared:
+        assert hasattr(lib, sym), sym
+    L = capi.load()
+    assert L.amx_abi_version() == capi.ABI_VERSION
+
+
+def test_struct_sizes_match_header():
+    """ctypes mirrors of the ABI structs have the C sizes (compiled probe)."""
+    import subprocess
+    import tempfile
+    from amx import capi
+    src = r'''
+#include <stdio.h>
+#include "amx.h"
+int main(){printf("%zu %zu %zu %zu %zu\n", sizeof(amx_chain_desc), sizeof(amx_chunk),
+  sizeof(amx_final_desc), sizeof(amx_plan_info), sizeof(amx_track_span));return 0;}'''
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "p.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "p")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        sizes = [int(v) for v in subprocess.run([exe], capture_output=True, text=True).stdout.split()]
+    assert sizes == [ctypes.sizeof(capi.ChainDesc), ctypes.sizeof(capi.Chunk),
+                     ctypes.sizeof(capi.FinalDesc), ctypes.sizeof(capi.PlanInfo),
+                     ctypes.sizeof(capi.TrackSpan)]
+
+
+def test_design_uses_reference_coefficients():
+    from scipy.signal import butter
+    from amx import design
+    s = dict(bass_boost=-1.0, mid_cut=2.0, presence_boost=2.5, treble_boost=1.0,
+             analog_character=40.0, width=1.3, multiband=True, low_thresh=-25.0, low_ratio=6.0,
+             mid_thresh=-20.0, mid_ratio=3.0, high_thresh=-15.0, high_ratio=4.0)
+    d, keep = design.chain_desc(48000, 2, s)
+    b, a = butter(2, 250 / 24000.0, btype='low')
+    assert list(d.eq_coef[0])[:6] == list(b) + list(a)
+    assert list(d.eq_kind) == [1, 2, 2, 1]
+    assert d.eq_gain[1] == 10 ** (-2.0 / 20.0)
+    lo = butter(4, 250, btype='lowpass', fs=48000, output='sos')
+    assert list(d.xover_lo_sos) == list(lo.reshape(-1))
+    assert d.width == np.float32(1.3) and d.analog_on == 1
+    lut = np.ctypeslib.as_array(d.tanh_lut, shape=(65536,))
+    x = np.arange(-32768, 32768, dtype=np.int16).astype(np.float32) / 32768
+    np.testing.assert_array_equal(lut, np.tanh(x * (1.0 + 0.4 * 0.5)))
+    d0, _ = design.chain_desc(48000, 2, dict())
+    assert list(d0.eq_kind) == [0, 0, 0, 0] and d0.width_on == 0 and d0.multiband_on == 0
+    with pytest.raises(TypeError):
+        design.chain_desc(48000, 2, dict(multiband=True))
+
+
+def test_chunk_bounds_follow_segment_rule():
+    from amx.chunking import chunk_bounds, packet_frames
+    fs = 48000
+    q = packet_frames(8)
+    assert q == 512
+    n = fs * 301 + 77
+    b = chunk_bounds(n, fs, q)
+    assert sum(m for _, m in b) == n and b[0][0] == 0
+    for k, (s, m) in enumerate(b[1:], start=1):
+        assert s % q == 0 and s >= k * 30 * fs and s - q < k * 30 * fs
+    assert len(b) == 11
+    assert chunk_bounds(0, fs, q) == []
+    assert chunk_bounds(100, fs, q) == [(0, 100)]
+
+
+def test_wav_roundtrip_and_ffmpeg_s16_rules(tmp_path):
+    from amx import wavio
+    rng = np.random.default_rng(0)
+    x16 = rng.integers(-32768, 32767, size=(1000, 2)).astype(np.int16)
+    p = str(tmp_path / "a.wav")
+    wavio.write_wav_s16(p, x16, 44100)
+    nat, info = wavio.read_wav_native(p)
+    assert info.sample_rate == 44100 and info.channels == 2 and info.bits == 16
+    np.testing.assert_array_equal(wavio.to_s16(nat, info), x16)
+    xf = rng.uniform(-1.2, 1.2, size=(500, 1)).astype(np.float32)
+    p2 = str(tmp_path / "b.wav")
+    wavio.write_wav_f32(p2, xf, 48000)
+    nat2, info2 = wavio.read_wav_native(p2)
+    exp = np.clip(np.rint(xf * np.float32(32768)), -32768, 32767).astype(np.int16)
+    np.testing.assert_array_equal(wavio.to_s16(nat2, info2), exp)
+
+
+def test_settings_presets():
+    from amx.settings import EQ_PRESETS, apply_preset
+    assert EQ_PRESETS["Vocal Clarity"] == {"bass_boost": -1.0, "mid_cut": 2.0,
+                                           "presence_boost": 2.5, "treble_boost": 1.0}
+    s = apply_preset({}, "Lo-Fi Haze")
+    assert s["treble_boost"] == -4.0
+    assert apply_preset(s, "None")["bass_boost"] == 0
+
+
+def test_dropin_errors_like_reference(tmp_path):
+    import audio_mastering_engine as ame
+    with pytest.raises(ValueError, match="Input or output file not specified."):
+        ame.master_audio({"input_file": None, "output_file": "x.wav"})
+    msgs, prog, art, tag = [], [], [], []
+    ame.process_audio({"input_file": "", "output_file": ""}, msgs.append,
+                      lambda a, b: prog.append((a, b)), art.append, tag.append)
+    assert msgs[-1] == "Error: Input or output file not specified."
+    assert prog == [(0, 1)] and art == [None] and tag == ["Processing failed."]

@@ -1,0 +1,169 @@
+"""CPU: the oracle against the reference's golden vectors and known answers.
+
+The golden vectors (tests/golden/*.npz) were produced by running the reference's
+own audio_mastering_engine.py functions (tests/golden/make_golden.py); the
+oracle must reproduce every intermediate bit for bit."""
+import audioop
+import glob
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+FILES = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def test_golden_present():
+    assert len(FILES) >= 15
+
+
+@pytest.mark.parametrize("path", FILES, ids=lambda p: os.path.basename(p)[:-4])
+def test_oracle_matches_reference_golden(oracle_mod, path):
+    O = oracle_mod
+    d = np.load(path)
+    meta = json.loads(str(d["meta"]))
+    s, fs = meta["settings"], meta["fs"]
+    x = d["in16"]
+    if "analog16" in d:
+        a = O.analog(x, fs, s["analog_character"])
+        np.testing.assert_array_equal(a, d["analog16"])
+        x = a
+    e = O.eq(x.astype(np.float32) / 32768, fs, s)
+    np.testing.assert_array_equal(e, d["eq32"])
+    if "width32" in d:
+        e = O.width(e, s["width"])
+        np.testing.assert_array_equal(e, d["width32"])
+    np.testing.assert_array_equal(O.f32_to_s16(e), d["p16"])
+    if s.get("multiband"):
+        for got, k in zip(O.crossover(d["p16"], fs), ("low16", "mid16", "high16")):
+            np.testing.assert_array_equal(got, d[k])
+        for b in ("low", "mid", "high"):
+            np.testing.assert_array_equal(
+                O.compress(d[b + "16"], fs, s[b + "_thresh"], s[b + "_ratio"]), d[b + "c16"])
+        np.testing.assert_array_equal(O.overlay3(d["lowc16"], d["midc16"], d["highc16"], fs),
+                                      d["out16"])
+    x16 = d["x16"] if d["x16"].shape[1] == 2 else np.repeat(d["x16"], 2, axis=1)
+    np.testing.assert_array_equal(O.chunk(x16, fs, s), d["out16"])
+
+
+def test_audioop_known_answers(oracle_mod):
+    """SURVEY.md §4 known answers, and the oracle's audioop restatements."""
+    import struct
+    pack = lambda v: struct.pack("<%dh" % len(v), *v)
+    got = audioop.mul(pack([-3, 3, -1, 1, 32767, -32768, 5, -5]), 2, 0.5)
+    assert list(struct.unpack("<8h", got)) == [-2, 1, -1, 0, 16383, -16384, 2, -3]
+    assert struct.unpack("<h", audioop.add(pack([32767]), pack([32000]), 2))[0] == 32767
+    assert audioop.rms(pack([3, 4, 0, 0]), 2) == 2
+    assert audioop.rms(b"", 2) == 0
+    assert math.log(1000, 10) == 2.9999999999999996 != math.log10(1000)
+
+
+def test_compressor_matches_pydub_restatement(oracle_mod):
+    """C compressor == the Python pydub 0.25.1 restatement (tests/golden/pydub_restated.py)
+    on randomised bands, thresholds and ratios (incl. ratio 1 and threshold 0)."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import pydub_restated as P
+    rng = np.random.default_rng(7)
+    for trial in range(12):
+        fs = [44100, 48000, 96000, 22050][trial % 4]
+        n = int(rng.integers(1, 2500))
+        amp = [200, 3000, 20000, 32767][trial % 4]
+        env = np.abs(np.sin(np.linspace(0, rng.uniform(1, 20), n)))[:, None]
+        x = np.clip(rng.normal(0, amp, (n, 2)) * env, -32768, 32767).astype(np.int16)
+        thr = float(rng.choice([-40.0, -25.0, -12.5, 0.0, -60.0]))
+        ratio = float(rng.choice([1.0, 1.5, 4.0, 10.0, 6.0]))
+        seg = P.AudioSegment(data=x.tobytes(), sample_width=2, frame_rate=fs, channels=2)
+        ref = np.frombuffer(P.compress_dynamic_range(seg, thr, ratio)._data, np.int16).reshape(-1, 2)
+        np.testing.assert_array_equal(oracle_mod.compress(x, fs, thr, ratio), ref)
+
+
+def test_overlay_lengths(oracle_mod):
+    """pydub ms rounding (SURVEY.md A.10 examples)."""
+    assert oracle_mod.overlay_len(1234567, 48000) == 1234560
+    assert oracle_mod.overlay_len(1234590, 48000) == 1234608
+    assert oracle_mod.overlay_len(1323008, 44100) == 1323000
+
+
+def _sine(fs, seconds, dbfs, freq=1000.0):
+    t = np.arange(int(fs * seconds)) / fs
+    s = 10 ** (dbfs / 20.0) * np.sin(2 * np.pi * freq * t)
+    return np.clip(np.rint(np.repeat(s[:, None], 2, 1) * 32768), -32768, 32767).astype(np.int16)
+
+
+@pytest.mark.parametrize("fs", [44100, 48000, 96000])
+def test_ebu3341_integrated(oracle_mod, fs):
+    """EBU Tech 3341 case 1: stereo 1 kHz sine at -23 dBFS -> -23.0 +- 0.1 LUFS.
+    Checks the oracle's libebur128 restatement AND the product's host arithmetic."""
+    from amx import loudness as L
+    hist, st, peak, nb = oracle_mod.ebur128(_sine(fs, 20.0, -23.0), fs)
+    i_prod = L.integrated_loudness(hist)
+    i_orc = oracle_mod.loudness_stats(hist, st)[0]
+    assert i_prod == i_orc
+    assert abs(i_prod - (-23.0)) <= 0.1
+
+
+def test_ebu3342_lra(oracle_mod):
+    """EBU Tech 3342 case 1: 20 s at -20 dBFS then 20 s at -30 dBFS sine -> LRA 10 +- 1."""
+    from amx import loudness as L
+    fs = 48000
+    x = np.concatenate([_sine(fs, 20.0, -20.0), _sine(fs, 20.0, -30.0)])
+    hist, st, peak, nb = oracle_mod.ebur128(x, fs)
+    lra = L.loudness_range(st)
+    assert lra == oracle_mod.loudness_stats(hist, st)[1]
+    assert abs(lra - 10.0) <= 1.0
+
+
+def test_host_loudness_arithmetic_matches_oracle(oracle_mod):
+    from amx import loudness as L
+    rng = np.random.default_rng(3)
+    for _ in range(25):
+        hist = np.zeros(1000, np.uint64)
+        st = np.zeros(1000, np.uint64)
+        k = int(rng.integers(0, 60))
+        for idx in rng.integers(100, 999, size=k):
+            hist[idx] += np.uint64(rng.integers(1, 50))
+        for idx in rng.integers(100, 999, size=int(rng.integers(0, 40))):
+            st[idx] += np.uint64(rng.integers(1, 20))
+        I, lra, thr = oracle_mod.loudness_stats(hist, st)
+        assert L.integrated_loudness(hist) == I or (math.isinf(I) and math.isinf(L.integrated_loudness(hist)))
+        assert L.loudness_range(st) == lra
+        assert L.relative_threshold(hist) == thr
+
+
+def test_linear_mode_decision():
+    from amx import loudness as L
+    st = {"input_i": "-24.00", "input_tp": "-12.00", "input_lra": "7.00", "input_thresh": "-34.00"}
+    mode, g = L.linear_gain(st, -14.0)
+    assert mode == "linear" and g == 10.0 ** (10.0 / 20.0)
+    st2 = dict(st, input_tp="-11.00")             # TP + offset > -1.5 -> dynamic
+    assert L.linear_gain(st2, -14.0)[0] == "dynamic"
+    st3 = dict(st, input_lra="0.00")              # measured_LRA == 0 -> dynamic
+    assert L.linear_gain(st3, -14.0)[0] == "dynamic"
+    assert L.linear_gain(dict(st, input_i="-inf"), -14.0)[0] == "skip"
+
+
+def test_alimiter_below_limit_is_delay_and_level(oracle_mod):
+    fs = 48000
+    rng = np.random.default_rng(1)
+    x = rng.integers(-20000, 20000, size=(5000, 2)).astype(np.int16)
+    y = oracle_mod.alimiter(x, fs)
+    B = int(fs * 0.005 * 2) // 2
+    assert np.all(y[:B - 1] == 0)
+    v = ((x[:-(B - 1)].astype(np.float64) / 32768.0) * (1 / 0.98)) * 1.0
+    np.testing.assert_array_equal(y[B - 1:], np.clip(np.rint(v * 32768.0), -32768, 32767).astype(np.int16))
+
+
+def test_alimiter_limits_peaks(oracle_mod):
+    fs = 48000
+    t = np.arange(fs) / fs
+    s = np.sin(2 * np.pi * 100 * t) * (0.5 + 0.5 * (t > 0.5))
+    x = np.clip(np.rint(np.repeat(s[:, None], 2, 1) * 32767), -32768, 32767).astype(np.int16)
+    y = oracle_mod.alimiter(x, fs)
+    # output never exceeds limit * level = 1.0 full scale and is attenuated where loud
+    assert np.abs(y.astype(np.int32)).max() <= 32768
+    assert np.abs(y[-fs // 4:].astype(np.int32)).max() < np.abs(x[-fs // 4:].astype(np.int32)).max() / 0.98
