@@ -15,6 +15,7 @@ c_float_p = ctypes.POINTER(ctypes.c_float)
 
 AMX_OK, AMX_EINVAL, AMX_EHIP, AMX_ENOMEM, AMX_ERANGE = 0, -1, -2, -3, -4
 ABI_VERSION = 1
+STAGES = ("front1", "scan_eq", "front2", "scan_xo", "xover", "rms", "env", "fix", "apply")
 
 
 class AmxError(RuntimeError):
@@ -67,7 +68,8 @@ class TrackSpan(ctypes.Structure):
 
 # every symbol include/amx.h declares (checked by the CPU test suite)
 EXPORTS = ("amx_abi_version", "amx_last_error", "amx_plan_create", "amx_plan_free",
-           "amx_plan_get_info", "amx_plan_track_span", "amx_run_chunks", "amx_loudness_pass1",
+           "amx_plan_get_info", "amx_plan_track_span", "amx_run_chunks", "amx_run_stage",
+           "amx_loudness_pass1",
            "amx_kw_propagate", "amx_loudness_pass2", "amx_loudness_histograms",
            "amx_limiter_geometry", "amx_finalize")
 
@@ -95,6 +97,7 @@ def load(path=None):
     L.amx_plan_get_info.argtypes = [vp, ctypes.POINTER(PlanInfo)]
     L.amx_plan_track_span.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(TrackSpan)]
     L.amx_run_chunks.argtypes = [vp, vp, vp, vp, vp]
+    L.amx_run_stage.argtypes = [vp, ctypes.c_int32, vp, vp, vp, vp]
     L.amx_loudness_pass1.argtypes = [vp, vp, vp, vp, vp, vp]
     L.amx_kw_propagate.argtypes = [vp, ctypes.c_int64, c_double_p, c_double_p]
     L.amx_loudness_pass2.argtypes = [vp, vp, vp, vp, ctypes.c_int64, vp, vp]

@@ -1,0 +1,158 @@
+"""Chunk-sharded multi-GPU mastering: one process per GPU, torch.distributed
+(backend "nccl" = RCCL over xGMI on ROCm; "gloo" for CPU tests).
+
+A track is cut into ~30 s chunks exactly as on one GPU (the ffmpeg segment rule,
+audio_mastering_engine.py:178); rank r owns a contiguous run of chunks.  The chunk
+chain needs no communication (all DSP state resets per chunk, :185-204).  The
+exchange steps are the track-level ones:
+
+1. K-filter carry (loudnorm measurement is continuous over the concatenated
+   track): all-gather each rank's zero-start tail state (8 doubles), then
+   carry(r) = sum_{q<r} A^{len_q+...} tail(q), chained on the host.
+2. Loudness partials: RCCL all-reduce(SUM) of the whole-track 100 ms hop energy
+   array (a hop spanning a rank boundary gets exactly two non-zero addends, so the
+   sum is order-independent and bit-identical for any world size) and
+   all-reduce(MAX) of the sample peaks.  Every rank then derives the same
+   histograms, statistics and gain.
+3. Limiter: all-gather of each rank's last B-1 frames (the look-ahead halo).  If
+   the limiter can engage (peaks above the limit) its state is handed rank to rank
+   with send/recv (sequential, rare path).
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .chunking import chunk_bounds, packet_frames
+from .engine import MasteringJob
+
+
+def overlay_len(n, fs):
+    ms = round(1000 * (n / fs))
+    return int(ms * (fs / 1000.0))
+
+
+def chunk_out_frames(n, fs, multiband):
+    if not multiband or n == 0:
+        return n
+    return overlay_len(overlay_len(n, fs), fs)
+
+
+def shard_ranges(n_chunks, world):
+    """Contiguous chunk ranges [(c0, c1)] per rank; the first n % world get one more."""
+    base, extra = divmod(n_chunks, world)
+    out, c = [], 0
+    for r in range(world):
+        k = base + (1 if r < extra else 0)
+        out.append((c, c + k))
+        c += k
+    return out
+
+
+def carry_from_tails(tails, span_frames, rank, propagate):
+    """K-filter state entering `rank`'s span: c_0 = 0, c_{q+1} = A^{len_q} c_q + tail_q.
+
+    tails: [world][8] zero-start end states; propagate(frames, state8) -> A^frames state8."""
+    c = np.zeros(8)
+    for q in range(rank):
+        c = propagate(span_frames[q], c) + np.asarray(tails[q], np.float64).reshape(8)
+    return c
+
+
+class ShardedTrack:
+    """This rank's part of one chunk-sharded track."""
+
+    def __init__(self, sample_rate, channels_in, settings, track_frames, rank, world, *,
+                 quantum=None, input_s16=False, seg_frames=256, group=None):
+        self.rank, self.world, self.group = rank, world, group
+        fs = int(sample_rate)
+        if quantum is None:
+            quantum = packet_frames(channels_in * (2 if input_s16 else 4))
+        self.bounds = chunk_bounds(track_frames, fs, quantum)
+        if len(self.bounds) < world:
+            raise ValueError("track has %d chunks for %d ranks" % (len(self.bounds), world))
+        mb = bool(settings.get("multiband"))
+        self.out_n = [chunk_out_frames(n, fs, mb) for _, n in self.bounds]
+        self.ranges = shard_ranges(len(self.bounds), world)
+        c0, c1 = self.ranges[rank]
+        self.in0 = self.bounds[c0][0]
+        self.local_frames = sum(n for _, n in self.bounds[c0:c1])
+        self.span_frames = [sum(self.out_n[a:b]) for a, b in self.ranges]
+        self.tframe0 = sum(self.out_n[:c0])
+        self.ttotal = sum(self.out_n)
+        chunks = [(0, s - self.in0, n) for s, n in self.bounds[c0:c1]]
+        self.job = MasteringJob(fs, channels_in, settings, [self.local_frames], chunks=chunks,
+                                track_frame0=[self.tframe0], track_total=[self.ttotal],
+                                input_s16=input_s16, seg_frames=seg_frames)
+        self.halo_all = None
+
+    # -------------------------------------------------------------- exchanges
+    def exchange_carry(self):
+        job = self.job
+        tails = [torch.empty_like(job.kw_tail) for _ in range(self.world)]
+        dist.all_gather(tails, job.kw_tail.contiguous(), group=self.group)
+        host = [t.reshape(-1)[:8].cpu().numpy() for t in tails]
+        c = carry_from_tails(host, self.span_frames, self.rank, job.plan.kw_propagate)
+        job.kw_carry.copy_(torch.from_numpy(c).reshape(job.kw_carry.shape))
+
+    def reduce_loudness(self):
+        dist.all_reduce(self.job.hops, op=dist.ReduceOp.SUM, group=self.group)
+        dist.all_reduce(self.job.peak, op=dist.ReduceOp.MAX, group=self.group)
+
+    def exchange_halo(self):
+        job = self.job
+        h = job.halo_frames
+        n = self.span_frames[self.rank]
+        mine = job.out[max(0, n - h):n]
+        if mine.shape[0] < h:
+            mine = torch.cat([torch.zeros((h - mine.shape[0], 2), dtype=mine.dtype, device=mine.device), mine])
+        allh = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(allh, mine.contiguous(), group=self.group)
+        if self.rank > 0:
+            job.halo[0, :h].copy_(allh[self.rank - 1])
+
+    def limiter_sequential(self):
+        job = self.job
+        if self.rank > 0:
+            dist.recv(job.lim_state, src=self.rank - 1, group=self.group)
+        job.finalize(False)
+        if self.rank < self.world - 1:
+            dist.send(job.lim_state, dst=self.rank + 1, group=self.group)
+
+    # -------------------------------------------------------------- the step
+    def step(self, d_in):
+        """One pass of the whole path over this rank's chunks (input resident)."""
+        job = self.job
+        job.run_chunks(d_in)
+        job.loudness_pass1()
+        lufs = job.settings.get("lufs")
+        if self.world > 1:
+            self.exchange_carry()
+        if lufs is not None:
+            job.loudness_pass2(carry=self.world > 1)
+        if self.world > 1:
+            if lufs is None:
+                dist.all_reduce(job.peak, op=dist.ReduceOp.MAX, group=self.group)
+            else:
+                self.reduce_loudness()
+        stats = None
+        if lufs is not None:
+            job.histograms()
+            stats = job.measure()
+            gains, modes = job.decide_gains(stats)
+        else:
+            job._fetch(False)
+            gains, modes = [-1.0], ["off"]
+        job.set_gains(gains)
+        if self.world > 1:
+            self.exchange_halo()
+        fast = job.fast_ok(gains)
+        if fast:
+            job.finalize(True)
+        elif self.world > 1:
+            job.lim_state.zero_()
+            self.limiter_sequential()
+        else:
+            job.lim_state.zero_()
+            job.finalize(False)
+        job.report = {"stats": stats, "modes": modes, "gains": gains, "limiter_fast": fast}
+        return job.y[:job.info.out_frames]

@@ -97,8 +97,20 @@ class MasteringJob:
         if d_in.numel() < need * self.channels_in:
             raise ValueError("d_in holds %d samples, plan needs %d" % (d_in.numel(), need * self.channels_in))
         L = capi.load()
-        capi.check(L.amx_run_chunks(self.plan.h, capi.ptr(d_in), capi.ptr(self.out),
-                                    capi.ptr(self.ws), self._s(stream)), "amx_run_chunks")
+        ev = getattr(self, "stage_events", None)
+        if ev is None:
+            capi.check(L.amx_run_chunks(self.plan.h, capi.ptr(d_in), capi.ptr(self.out),
+                                        capi.ptr(self.ws), self._s(stream)), "amx_run_chunks")
+            return
+        # per-stage timing: events recorded on the stream the kernels run on
+        for s in range(len(capi.STAGES)):
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            capi.check(L.amx_run_stage(self.plan.h, s, capi.ptr(d_in), capi.ptr(self.out),
+                                       capi.ptr(self.ws), self._s(stream)), "amx_run_stage")
+            b.record(stream)
+            ev.append((capi.STAGES[s], a, b))
 
     def loudness_pass1(self, stream=None):
         capi.check(capi.load().amx_loudness_pass1(self.plan.h, capi.ptr(self.out), capi.ptr(self.kw_tail),
@@ -125,12 +137,32 @@ class MasteringJob:
                    "amx_finalize")
 
     # ------------------------------------------------------------ host decisions
+    def _fetch(self, with_hist=True):
+        """One stream sync: histograms + peaks into pinned host buffers."""
+        if not hasattr(self, "_h_hist"):
+            self._h_hist = torch.empty(self.hist.shape, dtype=torch.int64, pin_memory=True)
+            self._h_st = torch.empty(self.st_hist.shape, dtype=torch.int64, pin_memory=True)
+            self._h_peak = torch.empty(self.peak.shape, dtype=torch.float64, pin_memory=True)
+            self._h_gains = torch.empty(self.gains.shape, dtype=torch.float64, pin_memory=True)
+        if with_hist:
+            self._h_hist.copy_(self.hist, non_blocking=True)
+            self._h_st.copy_(self.st_hist, non_blocking=True)
+        self._h_peak.copy_(self.peak, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        self._peaks = self._h_peak.numpy().copy()
+
     def measure(self):
         """loudnorm pass-1 statistics per track from the device histograms (syncs)."""
-        hist = self.hist.cpu().numpy().view(np.uint64)
-        st = self.st_hist.cpu().numpy().view(np.uint64)
-        peaks = self.peak.cpu().numpy()
-        return [loudness.measure(hist[t], st[t], peaks[t]) for t in range(self.n_tracks)]
+        self._fetch(True)
+        hist = self._h_hist.numpy().view(np.uint64)
+        st = self._h_st.numpy().view(np.uint64)
+        return [loudness.measure(hist[t], st[t], self._peaks[t]) for t in range(self.n_tracks)]
+
+    def set_gains(self, gains):
+        if not hasattr(self, "_h_gains"):
+            self._fetch(False)
+        self._h_gains.copy_(torch.tensor(gains, dtype=torch.float64))
+        self.gains.copy_(self._h_gains, non_blocking=True)
 
     def decide_gains(self, stats):
         lufs = self.settings.get("lufs")
@@ -150,7 +182,10 @@ class MasteringJob:
         return gains, modes
 
     def fast_ok(self, gains):
-        peaks = self.peak.cpu().numpy()
+        if getattr(self, "_peaks", None) is None:
+            self._fetch(False)
+        peaks = self._peaks
+        self._peaks = None
         for t in range(self.n_tracks):
             m = float(peaks[t].max()) if peaks.shape[1] else 0.0
             if loudness.max_after_gain(m, gains[t]) * self.fd.level_in > self.limit:
@@ -169,8 +204,9 @@ class MasteringJob:
             stats = self.measure()
             gains, modes = self.decide_gains(stats)
         else:
+            self._fetch(False)
             gains, modes = [-1.0] * self.n_tracks, ["off"] * self.n_tracks
-        self.gains.copy_(torch.tensor(gains, dtype=torch.float64))
+        self.set_gains(gains)
         fast = self.fast_ok(gains)
         self.finalize(fast, stream)
         self.report = {"stats": stats, "modes": modes, "gains": gains, "limiter_fast": fast,
@@ -198,4 +234,5 @@ def master_array(x, sample_rate, settings, *, quantum=None, seg_frames=256):
     job = MasteringJob(sample_rate, x.shape[1], settings, [x.shape[0]], quantum=quantum,
                        input_s16=s16, seg_frames=seg_frames)
     y = job.run(x)
+    job.report["job"] = job
     return y, job.report

@@ -46,9 +46,15 @@ def energy_to_loudness(e):
     return 10 * math.log10(e) - 0.691 if e > 0 else -math.inf
 
 
+def _nz(hist):
+    """Indices of non-empty bins, ascending (adding an empty bin's 0.0 is exact,
+    so summing only these keeps libebur128's sequential double sums bit-identical)."""
+    return [int(j) for j in np.flatnonzero(np.asarray(hist))]
+
+
 def relative_threshold_energy(hist):
     rel, count = 0.0, 0
-    for j in range(1000):
+    for j in _nz(hist):
         h = int(hist[j])
         rel += h * HIST_ENERGIES[j]
         count += h
@@ -70,7 +76,9 @@ def integrated_loudness(hist):
         if rel > HIST_ENERGIES[start]:
             start += 1
     gated, above = 0.0, 0
-    for j in range(start, 1000):
+    for j in _nz(hist):
+        if j < start:
+            continue
         h = int(hist[j])
         gated += h * HIST_ENERGIES[j]
         above += h
@@ -92,7 +100,7 @@ def loudness_range(st_hist):
     """ff_ebur128_loudness_range_multiple (one state)."""
     hist = [int(v) for v in st_hist]
     stl_size, stl_power = 0.0, 0.0
-    for j in range(1000):
+    for j in _nz(hist):
         stl_size += hist[j]
         stl_power += hist[j] * HIST_ENERGIES[j]
     if not stl_size:

@@ -65,3 +65,40 @@ def to_s16(x):
     """
     y = np.rint(np.asarray(x, dtype=np.float32) * np.float32(32768.0))
     return np.clip(y, -32768, 32767).astype(np.int16)
+
+
+def mix_like(n_frames, sample_rate, channels=2, seed=0, peak_dbfs=-3.0):
+    """A "mixed" program signal with a modest peak-to-loudness ratio (~9-11 dB):
+    a bass line of partials in 110-240 Hz, mid/high partials and 1/f noise, slow
+    section-scale (9-14 s period, ~4 dB) and 0.2-0.6 Hz level changes.  After the reference's EQ presets it stays in
+    loudnorm's linear mode at -14 LUFS (TP + offset <= -1.5 dBTP, LRA in (0, 11]),
+    which is the mode the build implements."""
+    rng = np.random.default_rng(SEED_BASE + 1000 + int(seed))
+    n = int(n_frames)
+    if n == 0:
+        return np.zeros((0, channels), np.float32)
+    t = np.arange(n, dtype=np.float64) / float(sample_rate)
+    # section-scale level changes (LRA > 0) plus a faster 0.2-0.6 Hz swell
+    env = 1.0 - 0.35 * 0.5 * (1.0 + np.sin(2 * np.pi * t / rng.uniform(9.0, 14.0) + rng.uniform(0, 6.3)))
+    env *= 1.0 - 0.1 * 0.5 * (1.0 + np.sin(2 * np.pi * rng.uniform(0.2, 0.6) * t + rng.uniform(0, 6.3)))
+    out = np.zeros((n, channels))
+    bass = rng.uniform(110.0, 240.0, size=4)
+    mids = np.exp(rng.uniform(np.log(400.0), np.log(min(9000.0, 0.45 * sample_rate)), size=5))
+    for c in range(channels):
+        sig = np.zeros(n)
+        for f in bass:
+            sig += rng.uniform(0.6, 1.0) * np.sin(2 * np.pi * f * t + rng.uniform(0, 6.3))
+        for f in mids:
+            sig += rng.uniform(0.1, 0.3) * np.sin(2 * np.pi * f * t + rng.uniform(0, 6.3))
+        w = rng.standard_normal(n)
+        spec = np.fft.rfft(w)
+        fr = np.fft.rfftfreq(n, 1.0 / sample_rate)
+        fr[0] = fr[1] if len(fr) > 1 else 1.0
+        pink = np.fft.irfft(spec / np.sqrt(fr), n)
+        pink /= (np.abs(pink).max() + 1e-12)
+        out[:, c] = sig + 0.3 * pink
+    out *= env[:, None]
+    peak = np.abs(out).max()
+    if peak > 0:
+        out *= (10.0 ** (peak_dbfs / 20.0)) / peak
+    return out.astype(np.float32)

@@ -82,7 +82,9 @@ def master_audio(settings, status_callback=None, progress_callback=None):
         job.report["stats"] = stats
     status("Applying final limiting and exporting...")                        # :221
     progress(num_chunks + 3, total_steps)                                     # :222
-    job.gains.copy_(torch.tensor(gains, dtype=torch.float64))
+    if settings.get("lufs") is None:
+        job._fetch(False)
+    job.set_gains(gains)
     job.finalize(job.fast_ok(gains))
     y = job.y[:job.info.out_frames].cpu().numpy()
     wavio.write_wav_s16(output_file, y, fs)

@@ -37,7 +37,7 @@ struct ChainDev {
     // compressor (pydub compress_dynamic_range, :306-308)
     int32_t look;          // int(5 ms * fs)
     int32_t rthr[3];       // smallest integer rms with rms > thresh_rms
-    double kb[5], ka[5];   // K-weighting (libebur128) b, a
+    double kw1[6], kw2[6]; // K-weighting as two DF-II-T biquads (libebur128 pb/pa, rb/ra)
 };
 
 // A ~30 s chunk (ffmpeg segment, :178).  loc_off indexes chunk-local scratch.

@@ -229,51 +229,61 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_front1(const ChainDev *__restrict
 
 // ------------------------------------------------------ Kogge-Stone affine scan
 // x_j = carry (j == first) or e_{j-1};   s_j = sum_{k<K} M^k x_{j-k}  (same stream)
-// One block = 256 consecutive entries of one lane; the first K-1 are halo.
+// One block = 256 consecutive entries of one lane; the first K-1 are halo.  Each
+// thread keeps its entry's D-vector in registers; LDS only publishes it per level.
+template <int D>
 __global__ void __launch_bounds__(AMX_BLOCK) k_scan(const double *__restrict__ e,
                                                     double *__restrict__ s,
                                                     const int32_t *__restrict__ seg_first,
                                                     const int32_t *__restrict__ seg_stream,
-                                                    int n_seg, int D, int lanes,
+                                                    int n_seg, int lanes,
                                                     const double *__restrict__ Mp, int levels,
                                                     const double *__restrict__ carry) {
-    extern __shared__ double lds[];
+    __shared__ double lds[AMX_BLOCK * D];
     const int K = 1 << levels;
     const int HALO = K - 1;
     const int OUT = blockDim.x - HALO;
     const int lane = blockIdx.y;
     const int t = threadIdx.x;
     const int64_t j = (int64_t)blockIdx.x * OUT - HALO + t;
-    double *A = lds, *B = lds + blockDim.x * D;
+    double v[D], nb[D];
     int first = 0x7fffffff;
-    if (j >= 0 && j < n_seg) first = seg_first[j];
+    const bool in = j >= 0 && j < n_seg;
+    if (in) first = seg_first[j];
+#pragma unroll
     for (int d = 0; d < D; d++) {
-        double v = 0.0;
-        if (j >= 0 && j < n_seg) {
-            if (j == first) v = carry ? carry[((int64_t)seg_stream[j] * lanes + lane) * D + d] : 0.0;
-            else v = e[((j - 1) * lanes + lane) * D + d];
+        double x = 0.0;
+        if (in) {
+            if (j == first) x = carry ? carry[((int64_t)seg_stream[j] * lanes + lane) * D + d] : 0.0;
+            else x = e[((j - 1) * lanes + lane) * D + d];
         }
-        A[t * D + d] = v;
+        v[d] = x;
     }
-    __syncthreads();
     for (int l = 0; l < levels; l++) {
         const int off = 1 << l;
-        const double *M = Mp + (int64_t)l * D * D;
-        const bool use = (t - off >= 0) && (j - off >= first) && (j < n_seg);
-        for (int i = 0; i < D; i++) {
-            double acc = A[t * D + i];
-            if (use) {
-                const double *mi = M + i * D;
-                const double *src = A + (t - off) * D;
-                for (int k = 0; k < D; k++) acc = fma(mi[k], src[k], acc);
-            }
-            B[t * D + i] = acc;
+#pragma unroll
+        for (int d = 0; d < D; d++) lds[t * D + d] = v[d];
+        __syncthreads();
+        const bool use = (t - off >= 0) && (j - off >= first) && in;
+        if (use) {
+#pragma unroll
+            for (int d = 0; d < D; d++) nb[d] = lds[(t - off) * D + d];
         }
         __syncthreads();
-        double *tmp = A; A = B; B = tmp;
+        if (use) {
+            const double *M = Mp + (int64_t)l * D * D;
+#pragma unroll
+            for (int i = 0; i < D; i++) {
+                double acc = v[i];
+#pragma unroll
+                for (int k = 0; k < D; k++) acc = fma(M[i * D + k], nb[k], acc);
+                v[i] = acc;
+            }
+        }
     }
-    if (t >= HALO && j >= 0 && j < n_seg)
-        for (int d = 0; d < D; d++) s[(j * lanes + lane) * D + d] = A[t * D + d];
+    if (t >= HALO && in)
+#pragma unroll
+        for (int d = 0; d < D; d++) s[(j * lanes + lane) * D + d] = v[d];
 }
 
 // ------------------------------------------- pass 2: EQ from true state -> int16
@@ -645,8 +655,6 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_kw2(const ChainDev *__restrict__ 
     for (int c = 0; c < 2; c++)
 #pragma unroll
         for (int d = 0; d < 4; d++) v[c][d] = st[c * 4 + d];
-    const double b0 = cd.kb[0], b1 = cd.kb[1], b2 = cd.kb[2], b3 = cd.kb[3], b4 = cd.kb[4];
-    const double a1 = cd.ka[1], a2 = cd.ka[2], a3 = cd.ka[3], a4 = cd.ka[4];
     const int64_t h0 = sg.tframe / hop;
     int64_t next_b = (h0 + 1) * hop;   // next hop boundary (whole-track frame)
     double acc[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
@@ -658,9 +666,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_kw2(const ChainDev *__restrict__ 
 #pragma unroll
         for (int c = 0; c < 2; c++) {
             double xs = (double)(c ? hi16(p) : lo16(p)) * (1.0 / 32768.0);
-            double v0 = xs - a1 * v[c][0] - a2 * v[c][1] - a3 * v[c][2] - a4 * v[c][3];
-            double y = b0 * v0 + b1 * v[c][0] + b2 * v[c][1] + b3 * v[c][2] + b4 * v[c][3];
-            v[c][3] = v[c][2]; v[c][2] = v[c][1]; v[c][1] = v[c][0]; v[c][0] = v0;
+            double u = sos_step(cd.kw1, v[c][0], v[c][1], xs);
+            double y = sos_step(cd.kw2, v[c][2], v[c][3], u);
             acc[piece][c] = fma(y, y, acc[piece][c]);
         }
     }
@@ -896,6 +903,7 @@ __global__ void k_final_general(const SpanDev *__restrict__ spans, int n_tracks,
 
 // ================================================================ launchers
 static inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + AMX_BLOCK - 1) / AMX_BLOCK)); }
+static inline bool empty(dim3 g) { return g.x == 0 || g.y == 0 || g.z == 0; }
 
 template <int MASK>
 static hipError_t front1_t(const Launch &l, const float *in, const float *lut, uint32_t *a16,
@@ -940,18 +948,29 @@ hipError_t launch_front2(const Launch &l, int mask, const int16_t *a16, const do
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_scan(const double *e, double *s, const int32_t *seg_first,
-                       const int32_t *seg_stream, int n_seg, int D, int lanes,
-                       const double *Mp, int levels, const double *carry, hipStream_t st) {
-    if (n_seg <= 0 || D <= 0) return hipSuccess;
+template <int D>
+static hipError_t scan_t(const double *e, double *s, const int32_t *seg_first,
+                         const int32_t *seg_stream, int n_seg, int lanes, const double *Mp,
+                         int levels, const double *carry, hipStream_t st) {
     const int K = 1 << levels;
     const int OUT = AMX_BLOCK - (K - 1);
     if (OUT <= 0) return hipErrorInvalidValue;
     dim3 grid((unsigned)((n_seg + OUT - 1) / OUT), (unsigned)lanes);
-    size_t shm = (size_t)2 * AMX_BLOCK * D * sizeof(double);
-    hipLaunchKernelGGL(k_scan, grid, dim3(AMX_BLOCK), shm, st, e, s, seg_first, seg_stream,
-                       n_seg, D, lanes, Mp, levels, carry);
+    hipLaunchKernelGGL(k_scan<D>, grid, dim3(AMX_BLOCK), 0, st, e, s, seg_first, seg_stream,
+                       n_seg, lanes, Mp, levels, carry);
     return hipGetLastError();
+}
+
+hipError_t launch_scan(const double *e, double *s, const int32_t *seg_first,
+                       const int32_t *seg_stream, int n_seg, int D, int lanes,
+                       const double *Mp, int levels, const double *carry, hipStream_t st) {
+    if (n_seg <= 0 || D <= 0) return hipSuccess;
+    switch (D) {
+#define SC(DD) case DD: return scan_t<DD>(e, s, seg_first, seg_stream, n_seg, lanes, Mp, levels, carry, st);
+        SC(2) SC(4) SC(8) SC(10) SC(12) SC(16) SC(18) SC(20)
+#undef SC
+    }
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_xover2(const Launch &l, const int16_t *p16, const double *s_x,
@@ -981,6 +1000,7 @@ hipError_t launch_env(const Launch &l, const uint16_t *r, const double *tabs, do
 
 hipError_t launch_fix(const Launch &l, const uint16_t *r, const double *tabs, double *att,
                       double *guess, double *endv, int64_t nloc) {
+    if (l.n_chunks <= 0) return hipSuccess;
     dim3 g((unsigned)l.n_chunks, 3);
     hipLaunchKernelGGL(k_fix, g, dim3(64), 0, l.stream, l.cd, l.chunks, l.segs, l.n_seg, r, tabs,
                        att, guess, endv, nloc);
@@ -992,6 +1012,7 @@ hipError_t launch_apply_n1(const Launch &l, const int16_t *bands, const double *
                            const int64_t *n1tab) {
     dim3 g = grid1(max_chunk_out);
     g.y = (unsigned)l.n_chunks;
+    if (empty(g)) return hipSuccess;
     hipLaunchKernelGGL(k_apply, g, dim3(AMX_BLOCK), 0, l.stream, l.chunks,
                        reinterpret_cast<const uint32_t *>(bands), att,
                        reinterpret_cast<uint32_t *>(out), nloc, n1tab);
@@ -1023,6 +1044,7 @@ hipError_t launch_hops(const SpanDev *spans, int n_tracks, const KwSegDev *ks, i
                        int64_t max_hops, hipStream_t st) {
     dim3 g = grid1(max_hops);
     g.y = (unsigned)n_tracks;
+    if (empty(g)) return hipSuccess;
     hipLaunchKernelGGL(k_hops, g, dim3(AMX_BLOCK), 0, st, spans, ks, L, hop, parts, part_hop,
                        hops, max_hops);
     return hipGetLastError();
@@ -1033,6 +1055,7 @@ hipError_t launch_hist(const SpanDev *spans, int n_tracks, int hop, const double
                        unsigned long long *st_hist, hipStream_t st) {
     dim3 g = grid1(max_hops);
     g.y = (unsigned)n_tracks;
+    if (empty(g)) return hipSuccess;
     hipLaunchKernelGGL(k_hist, g, dim3(AMX_BLOCK), 0, st, spans, hop, hops, max_hops, bounds,
                        hist, st_hist);
     return hipGetLastError();
@@ -1044,6 +1067,7 @@ hipError_t launch_final_fast(const SpanDev *spans, int n_tracks, int64_t max_spa
                              double level_out, double limit, int16_t *y, hipStream_t st) {
     dim3 g = grid1(max_span);
     g.y = (unsigned)n_tracks;
+    if (empty(g)) return hipSuccess;
     hipLaunchKernelGGL(k_final_fast, g, dim3(AMX_BLOCK), 0, st, spans,
                        reinterpret_cast<const uint32_t *>(x),
                        reinterpret_cast<const uint32_t *>(halo), halo_frames, gains, level_in,
@@ -1057,6 +1081,7 @@ hipError_t launch_final_general(const SpanDev *spans, int n_tracks, const int16_
                                 double limit, double release, int buffer_size,
                                 double *state, int64_t state_doubles, int16_t *y,
                                 hipStream_t st) {
+    if (n_tracks <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_final_general, dim3((n_tracks + 63) / 64), dim3(64), 0, st, spans,
                        n_tracks, reinterpret_cast<const uint32_t *>(x),
                        reinterpret_cast<const uint32_t *>(halo), halo_frames, gains, fs,

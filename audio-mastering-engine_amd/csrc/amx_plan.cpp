@@ -283,16 +283,15 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         K = std::tan(M_PI * f0 / (double)fs);
         ra[1] = 2.0 * (K * K - 1.0) / (1.0 + K / Q + K * K);
         ra[2] = (1.0 - K / Q + K * K) / (1.0 + K / Q + K * K);
-        cd.kb[0] = pb[0] * rb[0];
-        cd.kb[1] = pb[0] * rb[1] + pb[1] * rb[0];
-        cd.kb[2] = pb[0] * rb[2] + pb[1] * rb[1] + pb[2] * rb[0];
-        cd.kb[3] = pb[1] * rb[2] + pb[2] * rb[1];
-        cd.kb[4] = pb[2] * rb[2];
-        cd.ka[0] = pa[0] * ra[0];
-        cd.ka[1] = pa[0] * ra[1] + pa[1] * ra[0];
-        cd.ka[2] = pa[0] * ra[2] + pa[1] * ra[1] + pa[2] * ra[0];
-        cd.ka[3] = pa[1] * ra[2] + pa[2] * ra[1];
-        cd.ka[4] = pa[2] * ra[2];
+        // libebur128 multiplies the two sections into one 4th-order direct form II;
+        // its state (~1/(1-p)^2 ~ 1e5 x signal at 96 kHz) makes the A^L scan
+        // ill-conditioned, so the GPU runs the same two sections as DF-II-T biquads.
+        for (int k = 0; k < 3; k++) {
+            cd.kw1[k] = pb[k];
+            cd.kw1[3 + k] = pa[k];
+            cd.kw2[k] = rb[k];
+            cd.kw2[3 + k] = ra[k];
+        }
     }
     // compressor tables (pydub compress_dynamic_range, exact C math == CPython math)
     std::vector<double> tabs;
@@ -460,13 +459,9 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     }
     {
         Lti &kw = p->kw_model;
-        const double *a = cd.ka;
-        kw.derive(AMX_KW_DIM, [&](double *v, double x) {
-            double v0 = x - a[1] * v[0] - a[2] * v[1] - a[3] * v[2] - a[4] * v[3];
-            v[3] = v[2];
-            v[2] = v[1];
-            v[1] = v[0];
-            v[0] = v0;
+        kw.derive(AMX_KW_DIM, [&](double *z, double x) {
+            double y = sos_step_h(cd.kw1, z, x);
+            sos_step_h(cd.kw2, z + 2, y);
         });
         Gkw = kw.gemv_table(p->Lkw);
         p->lev_kw = kw.scan_powers(p->Lkw, tol, 7, Mpkw);
@@ -579,35 +574,66 @@ int amx_plan_track_span(const amx_plan *p, int32_t track, amx_track_span *span) 
     return AMX_OK;
 }
 
-int amx_run_chunks(amx_plan *p, const float *d_in, int16_t *d_out, void *d_ws, void *stream) {
+int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out, void *d_ws,
+                  void *stream) {
     if (!p || (p->nloc > 0 && (!d_in || !d_out || !d_ws))) return fail(AMX_EINVAL, "null argument");
+    if (stage < 0 || stage >= AMX_STAGE_COUNT) return fail(AMX_EINVAL, "bad stage %d", stage);
     if (p->n_seg == 0) return AMX_OK;
     hipStream_t st = (hipStream_t)stream;
     amx::Launch l{p->d_cd, p->d_chunks, p->d_segs, p->n_chunks, p->n_seg, p->L, st};
     int16_t *a16 = wsp<int16_t>(d_ws, p->o_a16);
     double *e = wsp<double>(d_ws, p->o_e), *s = wsp<double>(d_ws, p->o_s);
-    HIPCHK(amx::launch_front1_lut(l, p->mask, d_in, p->d_lut, a16, p->d_G, e));
-    if (p->D > 0)
-        HIPCHK(amx::launch_scan(e, s, p->d_seg_first, p->d_seg_stream, p->n_seg, p->D, 2, p->d_Mp,
-                                p->lev_eq, nullptr, st));
-    if (!p->mb) {
-        HIPCHK(amx::launch_front2(l, p->mask, a16, s, d_out, 1, nullptr, nullptr));
-        return AMX_OK;
+    int16_t *p16 = p->mb ? wsp<int16_t>(d_ws, p->o_p16) : nullptr;
+    double *ex = p->mb ? wsp<double>(d_ws, p->o_ex) : nullptr;
+    double *sx = p->mb ? wsp<double>(d_ws, p->o_sx) : nullptr;
+    int16_t *bands = p->mb ? wsp<int16_t>(d_ws, p->o_bands) : nullptr;
+    uint16_t *r = p->mb ? wsp<uint16_t>(d_ws, p->o_r) : nullptr;
+    double *att = p->mb ? wsp<double>(d_ws, p->o_att) : nullptr;
+    double *guess = p->mb ? wsp<double>(d_ws, p->o_guess) : nullptr;
+    double *endv = p->mb ? wsp<double>(d_ws, p->o_end) : nullptr;
+    switch (stage) {
+    case AMX_STAGE_FRONT1:
+        HIPCHK(amx::launch_front1_lut(l, p->mask, d_in, p->d_lut, a16, p->d_G, e));
+        break;
+    case AMX_STAGE_SCAN_EQ:
+        if (p->D > 0)
+            HIPCHK(amx::launch_scan(e, s, p->d_seg_first, p->d_seg_stream, p->n_seg, p->D, 2,
+                                    p->d_Mp, p->lev_eq, nullptr, st));
+        break;
+    case AMX_STAGE_FRONT2:
+        if (!p->mb) HIPCHK(amx::launch_front2(l, p->mask, a16, s, d_out, 1, nullptr, nullptr));
+        else HIPCHK(amx::launch_front2(l, p->mask, a16, s, p16, 0, p->d_Gx, ex));
+        break;
+    case AMX_STAGE_SCAN_XO:
+        if (p->mb)
+            HIPCHK(amx::launch_scan(ex, sx, p->d_seg_first, p->d_seg_stream, p->n_seg, AMX_XO_DIM, 2,
+                                    p->d_Mpx, p->lev_x, nullptr, st));
+        break;
+    case AMX_STAGE_XOVER:
+        if (p->mb) HIPCHK(amx::launch_xover2(l, p16, sx, bands, p->nloc));
+        break;
+    case AMX_STAGE_RMS:
+        if (p->mb) HIPCHK(amx::launch_rms(l, bands, r, p->nloc));
+        break;
+    case AMX_STAGE_ENV:
+        if (p->mb) HIPCHK(amx::launch_env(l, r, p->d_tabs, att, guess, endv, p->nloc, p->warm));
+        break;
+    case AMX_STAGE_FIX:
+        if (p->mb) HIPCHK(amx::launch_fix(l, r, p->d_tabs, att, guess, endv, p->nloc));
+        break;
+    case AMX_STAGE_APPLY:
+        if (p->mb)
+            HIPCHK(amx::launch_apply_n1(l, bands, att, d_out, p->nloc, p->max_chunk_out, p->d_n1));
+        break;
     }
-    int16_t *p16 = wsp<int16_t>(d_ws, p->o_p16);
-    double *ex = wsp<double>(d_ws, p->o_ex), *sx = wsp<double>(d_ws, p->o_sx);
-    HIPCHK(amx::launch_front2(l, p->mask, a16, s, p16, 0, p->d_Gx, ex));
-    HIPCHK(amx::launch_scan(ex, sx, p->d_seg_first, p->d_seg_stream, p->n_seg, AMX_XO_DIM, 2,
-                            p->d_Mpx, p->lev_x, nullptr, st));
-    int16_t *bands = wsp<int16_t>(d_ws, p->o_bands);
-    uint16_t *r = wsp<uint16_t>(d_ws, p->o_r);
-    double *att = wsp<double>(d_ws, p->o_att);
-    double *guess = wsp<double>(d_ws, p->o_guess), *endv = wsp<double>(d_ws, p->o_end);
-    HIPCHK(amx::launch_xover2(l, p16, sx, bands, p->nloc));
-    HIPCHK(amx::launch_rms(l, bands, r, p->nloc));
-    HIPCHK(amx::launch_env(l, r, p->d_tabs, att, guess, endv, p->nloc, p->warm));
-    HIPCHK(amx::launch_fix(l, r, p->d_tabs, att, guess, endv, p->nloc));
-    HIPCHK(amx::launch_apply_n1(l, bands, att, d_out, p->nloc, p->max_chunk_out, p->d_n1));
+    return AMX_OK;
+}
+
+int amx_run_chunks(amx_plan *p, const float *d_in, int16_t *d_out, void *d_ws, void *stream) {
+    for (int s = 0; s < AMX_STAGE_COUNT; s++) {
+        int rc = amx_run_stage(p, s, d_in, d_out, d_ws, stream);
+        if (rc) return rc;
+    }
     return AMX_OK;
 }
 

@@ -1,0 +1,162 @@
+"""Benchmark: mastered Msamples/s (48 kHz stereo f32) at N GPUs + HBM roofline.
+
+Workload (BASELINE.json configs[1], the metric's single-GPU config): per rank a
+5-minute stereo 48 kHz float32 program (synthetic, seeded), mastered with the
+"Vocal Clarity" EQ preset and loudness normalisation to -14 LUFS, i.e. the whole
+process_audio_with_ffmpeg_pipeline path (audio_mastering_engine.py:171-226):
+chunk chain + concat, loudnorm measurement + linear gain, alimiter.  At N GPUs the
+job is ONE track of N x 5 min, chunk-sharded over the ranks (weak scaling) with the
+RCCL all-reduce of the loudness partials.  Input is resident in HBM before timing;
+output (16-bit PCM, what the reference writes) stays in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "audio-mastering-engine_amd"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (spec)
+
+VOCAL = dict(bass_boost=-1.0, mid_cut=2.0, presence_boost=2.5, treble_boost=1.0)
+MB = dict(multiband=True, low_thresh=-25.0, low_ratio=6.0, mid_thresh=-20.0, mid_ratio=3.0,
+          high_thresh=-15.0, high_ratio=4.0)
+CONFIGS = {
+    "c2": dict(VOCAL, lufs=-14.0),
+    "c3": dict(VOCAL, lufs=-14.0, width=1.3, analog_character=40.0, **MB),
+}
+
+
+def stage_bytes(stage, frames, ch_in, mb):
+    """Algorithmic HBM bytes of one launch: what the stage must read
+    and write per frame, x frames.  int16 stereo frame = 4 B; f32 stereo = 8 B."""
+    fin = 4 * ch_in
+    per = {
+        "front1": fin + 4,              # f32 input -> s16 chain input
+        "front2": 4 + 4,                # s16 chain input -> s16 chunk output / P
+        "xover": 4 + 12,                # P -> 3 bands
+        "rms": 12 + 6,                  # 3 bands -> 3 x u16 rms
+        "env": 6 + 24,                  # rms -> 3 x f64 attenuation
+        "apply": 12 + 24 + 4,           # bands + attenuation -> output
+    }
+    return per.get(stage, 0) * frames
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--seconds", type=float, default=300.0)
+    ap.add_argument("--seg-frames", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from amx import synth
+    from amx.dist import ShardedTrack
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    fs = 48000
+    settings = CONFIGS[args.config]
+    per_rank = int(args.seconds * fs)
+    total = per_rank * world
+    track = ShardedTrack(fs, 2, settings, total, rank, world, quantum=512,
+                         seg_frames=args.seg_frames)
+    x = synth.mix_like(track.local_frames, fs, 2, seed=rank)
+    d_in = torch.from_numpy(x).cuda()
+    job = track.job
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        track.step(d_in)
+    barrier()
+    job.stage_events = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        track.step(d_in)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed * 1000.0 / args.steps
+    samples_total = sum(track.span_frames) * 2          # output channel-samples, all ranks
+    value = samples_total * args.steps / elapsed / 1e6
+
+    # per-stage device time (HIP events on the launch stream, timed region only)
+    per_stage = {}
+    for name, a, b in job.stage_events:
+        per_stage[name] = per_stage.get(name, 0.0) + a.elapsed_time(b)
+    per_stage = {k: v / args.steps for k, v in per_stage.items()}
+    job.stage_events = None
+    frames = track.local_frames
+    mb = bool(settings.get("multiband"))
+    candidates = {k: v for k, v in per_stage.items() if stage_bytes(k, frames, 2, mb) > 0}
+    dom = max(candidates, key=candidates.get)
+    dom_ms = candidates[dom]
+    dom_bytes = stage_bytes(dom, frames, 2, mb)
+    achieved = dom_bytes / (dom_ms / 1e3) / 1e9
+
+    line = {
+        "metric": "mastered Msamples/sec (48 kHz stereo f32) at 1/2/4/8 GPUs; % HBM roofline",
+        "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (amx.synth.mix_like, seeded per rank)",
+        "config": {"workload": "configs[1]: 5 min stereo 48 kHz f32 per GPU, EQ 'Vocal Clarity' + "
+                               "loudnorm -14 LUFS (linear) + alimiter; N GPUs = one N x 5 min track, "
+                               "chunk-sharded" if args.config == "c2" else
+                               "configs[2]: C2 + multiband + width 1.3 + analog 40",
+                   "settings": args.config, "seconds_per_gpu": args.seconds,
+                   "seg_frames": args.seg_frames, "parallelism": "chunk-shard x%d" % world},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "bytes_per_launch": int(dom_bytes), "avg_launch_ms": round(dom_ms, 4),
+                     "traffic": None},
+        "stages_ms": {k: round(v, 4) for k, v in per_stage.items()},
+        "limiter_fast": job.report.get("limiter_fast"),
+        "loudnorm": job.report.get("stats"),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        x16 = oracle.quantize(x)
+        c = [(s - track.in0, n) for s, n in track.bounds]
+        t0 = time.perf_counter()
+        ref, _ = oracle.pipeline(x16, fs, settings, c)
+        dt = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": round(x16.shape[0] * 2 / dt / 1e6, 3), "unit": "Msamples/s",
+                                "cores": 1, "kind": "port",
+                                "sample": "full workload: 1 pass of the %.0f s track through the C "
+                                          "oracle (oracle/amx_oracle.c), single thread" % args.seconds,
+                                "seconds": round(dt, 3)}
+        y = job.y[:job.info.out_frames].cpu().numpy()
+        d = np.abs(y.astype(np.int32) - ref.astype(np.int32))
+        line["parity_vs_oracle"] = {"max_abs_lsb": int(d.max()), "exact_frac": float((d == 0).mean())}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

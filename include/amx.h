@@ -151,6 +151,22 @@ AMX_API int amx_plan_track_span(const amx_plan *plan, int32_t track, amx_track_s
  * (tracks back to back, chunks concatenated = the ffmpeg concat of :210-212). */
 AMX_API int amx_run_chunks(amx_plan *plan, const float *d_in, int16_t *d_out, void *d_ws, void *stream);
 
+/* The same chain one stage at a time (amx_run_chunks == stages 0..AMX_STAGE_COUNT-1 in
+ * order), so a host can bracket individual kernels with events on its stream.
+ * Stages that the settings make unnecessary are no-ops. */
+#define AMX_STAGE_FRONT1 0   /* quantise + analog character + EQ zero-state GEMV */
+#define AMX_STAGE_SCAN_EQ 1  /* affine scan -> exact EQ segment start states */
+#define AMX_STAGE_FRONT2 2   /* EQ from true state + width -> int16 (+ crossover GEMV) */
+#define AMX_STAGE_SCAN_XO 3  /* crossover scan */
+#define AMX_STAGE_XOVER 4    /* crossover -> 3 int16 bands */
+#define AMX_STAGE_RMS 5      /* exact audioop.rms detector per frame */
+#define AMX_STAGE_ENV 6      /* speculative envelope per segment */
+#define AMX_STAGE_FIX 7      /* envelope hand-off verification / re-run */
+#define AMX_STAGE_APPLY 8    /* gains + overlay -> chunk output */
+#define AMX_STAGE_COUNT 9
+AMX_API int amx_run_stage(amx_plan *plan, int32_t stage, const float *d_in, int16_t *d_out,
+                          void *d_ws, void *stream);
+
 /* Loudness pass 1 over d_out (libebur128 restated, ffmpeg loudnorm :229):
  * K-filter zero-state GEMV per segment + exact scan + sample peak.
  * d_kw_tail [n_tracks][2][4]: K-filter state at each span end assuming the span
