@@ -9,7 +9,7 @@ import subprocess
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(PKG, "lib", "libamx.so")
-SOURCES = ["amx_kernels.hip", "amx_plan.cpp"]
+SOURCES = ["amx_chain.hip", "amx_dyn.hip", "amx_loud.hip", "amx_final.hip", "amx_plan.cpp"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-fvisibility=hidden", "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
 
@@ -18,7 +18,7 @@ def needs_build():
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = SOURCES + ["amx_internal.hpp"]
+    deps = SOURCES + ["amx_internal.hpp", "amx_dev.hpp"]
     hdr = os.path.join(PKG, "..", "include", "amx.h")
     return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in deps) or os.path.getmtime(hdr) > t
 

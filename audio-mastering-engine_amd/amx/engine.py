@@ -54,6 +54,11 @@ class MasteringJob:
         self.desc.input_s16 = 1 if input_s16 else 0
         if quantum is None:
             quantum = packet_frames(self.channels_in * (2 if input_s16 else 4))
+        # int16 frames are read as one dword per stereo frame; mono int16 is
+        # duplicated to stereo on the device before the chain (-ac 2, :190)
+        self._mono_s16 = self.input_s16 and self.channels_in == 1
+        if self._mono_s16:
+            self.desc.channels_in = 2
         self.track_frames = [int(n) for n in track_frames]
         self.chunks = chunks if chunks is not None else plan_tracks(self.track_frames, self.fs, quantum)
         self.plan = capi.Plan(self.desc, self.chunks, track_frame0, track_total, seg_frames)
@@ -96,6 +101,8 @@ class MasteringJob:
         need = max((off + n for (_, off, n) in self.chunks), default=0)
         if d_in.numel() < need * self.channels_in:
             raise ValueError("d_in holds %d samples, plan needs %d" % (d_in.numel(), need * self.channels_in))
+        if self._mono_s16:
+            d_in = d_in.reshape(-1, 1).expand(-1, 2).contiguous()
         L = capi.load()
         ev = getattr(self, "stage_events", None)
         if ev is None:

@@ -1,0 +1,199 @@
+// amx_dev.hpp -- device helpers shared by the libamx kernels (gfx950).
+#pragma once
+#include "amx_internal.hpp"
+#include <math.h>
+
+namespace amx {
+
+// ------------------------------------------------------------ helpers
+__device__ __forceinline__ int16_t q_f32_to_s16_ffmpeg(float x) {
+    // libswresample f32->s16: av_clip_int16(lrintf(x * 32768))   
+    float v = rintf(x * 32768.0f);
+    v = fminf(fmaxf(v, -32768.0f), 32767.0f);
+    return (int16_t)(int)v;
+}
+__device__ __forceinline__ int16_t f32_to_s16(float x) {
+    // float_array_to_audio_segment (:255-256) on float32 arrays
+    float v = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
+    v = v * 32767.0f;
+    return (int16_t)(int)v;
+}
+__device__ __forceinline__ int16_t f64_to_s16(double x) {
+    double v = x < -1.0 ? -1.0 : (x > 1.0 ? 1.0 : x);
+    v = v * 32767.0;
+    return (int16_t)(int)v;
+}
+__device__ __forceinline__ int16_t sat16(int v) {
+    return (int16_t)(v > 32767 ? 32767 : (v < -32768 ? -32768 : v));
+}
+__device__ __forceinline__ uint32_t pack2(int16_t a, int16_t b) {
+    return (uint32_t)(uint16_t)a | ((uint32_t)(uint16_t)b << 16);
+}
+__device__ __forceinline__ int16_t lo16(uint32_t v) { return (int16_t)(v & 0xffff); }
+__device__ __forceinline__ int16_t hi16(uint32_t v) { return (int16_t)(v >> 16); }
+
+// lfilter DF-II-T biquad step (scipy _linear_filter order, fused)
+__device__ __forceinline__ double lf_step(const double *c, double &z0, double &z1, double x) {
+    double y = fma(c[0], x, z0);
+    z0 = fma(-c[4], y, fma(c[1], x, z1));
+    z1 = fma(-c[5], y, c[2] * x);
+    return y;
+}
+// sosfilt section step (scipy _sosfilt order, fused)
+__device__ __forceinline__ double sos_step(const double *c, double &z0, double &z1, double x) {
+    double y = fma(c[0], x, z0);
+    z0 = fma(-c[4], y, fma(c[1], x, z1));
+    z1 = fma(-c[5], y, c[2] * x);
+    return y;
+}
+
+// analog character for one frame, exact reference op order (no FMA):
+// lfilter along the channel axis (:264-265) = a length-2 sequence per frame.
+__device__ __forceinline__ void analog_frame(const ChainDev &cd, const float *lut, int16_t l,
+                                             int16_t r, int16_t &ol, int16_t &orr) {
+    double x0, x1;
+    if (lut) {
+        x0 = (double)lut[(int)l + 32768];
+        x1 = (double)lut[(int)r + 32768];
+    } else {
+        float a = ((float)l / 32768.0f) * cd.drive, b = ((float)r / 32768.0f) * cd.drive;
+        x0 = (double)(float)tanh((double)a);
+        x1 = (double)(float)tanh((double)b);
+    }
+    const double *b1 = cd.an_lo, *b2 = cd.an_hi;
+    // first shelf (120 Hz low, +cf dB): y0 = 0 + b0*x0 ; Z0 = (0 + x0*b1) - y0*a1 ; y1 = Z0 + b0*x1
+    double y0 = 0.0 + b1[0] * x0;
+    double z0 = (0.0 + x0 * b1[1]) - y0 * b1[4];
+    double y1 = z0 + b1[0] * x1;
+    double u0 = x0 + (y0 - x0) * cd.an_glo1;
+    double u1 = x1 + (y1 - x1) * cd.an_glo1;
+    double v0 = 0.0 + b2[0] * u0;
+    double w = (0.0 + u0 * b2[1]) - v0 * b2[4];
+    double v1 = w + b2[0] * u1;
+    double o0 = u0 + (v0 - u0) * cd.an_ghi1;
+    double o1 = u1 + (v1 - u1) * cd.an_ghi1;
+    ol = f64_to_s16(o0);
+    orr = f64_to_s16(o1);
+}
+
+// --------------------------------------------------------------- EQ chain
+template <int MASK>
+struct EqDim {
+    static constexpr int v = ((MASK & 1) ? 2 : 0) + ((MASK & 2) ? 8 : 0) + ((MASK & 4) ? 8 : 0) +
+                             ((MASK & 8) ? 2 : 0);
+};
+
+// One channel: z holds the compact state (active stages in order).
+// Stage k is the first active stage (float32 input) iff no lower bit of MASK is set.
+template <int MASK>
+__device__ __forceinline__ float eq_chain(const ChainDev &cd, double *z, float xf) {
+    double x = (double)xf;
+    int o = 0;
+    if constexpr ((MASK & 1) != 0) {
+        const EqStageDev &s = cd.st[0];
+        double y = lf_step(s.c, z[o], z[o + 1], x);
+        if (!s.neg) x = x + (y - x) * s.gm1;
+        else { double xg = (double)(xf * s.gf); x = xg + (y - xg); }
+        o += 2;
+    }
+    if constexpr ((MASK & 2) != 0) {
+        const EqStageDev &s = cd.st[1];
+        double b = x;
+#pragma unroll
+        for (int k = 0; k < 4; k++) b = sos_step(s.c + 6 * k, z[o + 2 * k], z[o + 2 * k + 1], b);
+        x = x + b * s.gm1;
+        o += 8;
+    }
+    if constexpr ((MASK & 4) != 0) {
+        const EqStageDev &s = cd.st[2];
+        double b = x;
+#pragma unroll
+        for (int k = 0; k < 4; k++) b = sos_step(s.c + 6 * k, z[o + 2 * k], z[o + 2 * k + 1], b);
+        x = x + b * s.gm1;
+        o += 8;
+    }
+    if constexpr ((MASK & 8) != 0) {
+        const EqStageDev &s = cd.st[3];
+        double y = lf_step(s.c, z[o], z[o + 1], x);
+        if (!s.neg) x = x + (y - x) * s.gm1;
+        else if constexpr ((MASK & 7) == 0) { double xg = (double)(xf * s.gf); x = xg + (y - xg); }
+        else { double xg = x * s.g; x = xg + (y - xg); }
+        o += 2;
+    }
+    (void)o;
+    if constexpr (MASK == 0) return xf;
+    return (float)x;
+}
+// stage-1/2 "first" cases: a peak stage has no float32-sensitive op, and the
+// stage-0 shelf is always first; only stage 3 needs the (MASK & 7) test above.
+
+__device__ __forceinline__ void width_frame(float w, float &l, float &r) {
+    // apply_stereo_width (:269-270), float32, exact order
+    float mid = (l + r) / 2.0f, side = (l - r) / 2.0f;
+    side = side * w;
+    float nl = mid + side, nr = mid - side;
+    l = nl < -1.0f ? -1.0f : (nl > 1.0f ? 1.0f : nl);
+    r = nr < -1.0f ? -1.0f : (nr > 1.0f ? 1.0f : nr);
+}
+
+// ------------------------------------------------------- LDS tile stager
+// A workgroup owns AMX_BLOCK segments (one per thread).  Row r's frames live at
+// dword offset rb[r] (W dwords per frame).  Tiles of AMX_TF frames per row move
+// global <-> LDS cooperatively with dword accesses: consecutive lanes touch
+// consecutive dwords of a row, so each wave instruction covers 1-2 rows of
+// 64-128 contiguous bytes instead of 64 scattered cache lines.  The row pitch is
+// ROW+1 dwords so the per-thread row reads are LDS-bank-conflict free.
+#define AMX_TF AMX_TF_FRAMES
+template <int W>
+struct Tile {
+    static constexpr int ROW = AMX_TF * W;
+    static constexpr int PITCH = ROW + 1;
+    static constexpr int WORDS = AMX_BLOCK * PITCH;
+};
+
+// Row r holds frames n in [lo[r], hi[r]) at dword rb[r] + n*W (lo == nullptr -> 0).
+// Loads are issued unconditionally from a clamped in-range address and masked
+// afterwards: a load guarded by a per-element branch makes hipcc wait vmcnt(0)
+// after every element (cdna_hip_programming.md §5 "Three .s-level traps" (c)),
+// which serialises the tile into ROW dependent HBM round trips.
+template <int W>
+__device__ __forceinline__ void tile_load(uint32_t *lds, const uint32_t *__restrict__ src,
+                                          const int64_t *rb, const int *lo, const int *hi,
+                                          int k) {
+    constexpr int ROW = Tile<W>::ROW, PITCH = Tile<W>::PITCH;
+    uint32_t v[ROW];
+    bool ok[ROW];
+    const int c = threadIdx.x % ROW;              // column is fixed per thread
+    const int n = k + c / W;
+#pragma unroll
+    for (int m = 0; m < ROW; m++) {
+        const int r = threadIdx.x / ROW + m * (AMX_BLOCK / ROW);
+        const int l0 = lo ? lo[r] : 0, h0 = hi[r];
+        ok[m] = n >= l0 && n < h0;
+        const int nn = ok[m] ? n : (h0 > l0 ? l0 : 0);
+        v[m] = src[rb[r] + (int64_t)nn * W + (c % W)];
+    }
+#pragma unroll
+    for (int m = 0; m < ROW; m++) {
+        const int r = threadIdx.x / ROW + m * (AMX_BLOCK / ROW);
+        lds[r * PITCH + c] = ok[m] ? v[m] : 0u;
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void tile_store(const uint32_t *lds, uint32_t *__restrict__ dst,
+                                           const int64_t *rb, const int *hi, int k) {
+    constexpr int ROW = Tile<W>::ROW, PITCH = Tile<W>::PITCH;
+    const int c = threadIdx.x % ROW;
+    const int n = k + c / W;
+#pragma unroll
+    for (int m = 0; m < ROW; m++) {
+        const int r = threadIdx.x / ROW + m * (AMX_BLOCK / ROW);
+        if (n < hi[r]) dst[rb[r] + (int64_t)n * W + (c % W)] = lds[r * PITCH + c];
+    }
+}
+
+static inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + AMX_BLOCK - 1) / AMX_BLOCK)); }
+static inline bool empty(dim3 g) { return g.x == 0 || g.y == 0 || g.z == 0; }
+
+}  // namespace amx

@@ -1,0 +1,194 @@
+// amx_final.hip -- loudnorm linear gain (:240) + alimiter (:223).
+#include "amx_dev.hpp"
+
+namespace amx {
+
+// ----------------------------------------------------------------- finalize
+__device__ __forceinline__ int16_t clip_llrint(double v) {
+    double q = rint(v);
+    q = q > 32767.0 ? 32767.0 : (q < -32768.0 ? -32768.0 : q);
+    return (int16_t)(int)q;
+}
+__device__ __forceinline__ int16_t gain16(int16_t x, double g) {
+    // loudnorm linear mode: dst = src * gain on doubles x/32768 ; s16 llrint(x*32768)
+    if (g <= 0.0) return x;
+    double v = ((double)x * (1.0 / 32768.0)) * g;
+    return clip_llrint(v * 32768.0);
+}
+
+// limiter never engages (host-proven max|x| <= limit): att == 1, delta == 0 for
+// every frame, so out[n] = level-scaled input[n - (B-1)] (B = ring frames).
+__global__ void __launch_bounds__(AMX_BLOCK) k_final_fast(const SpanDev *__restrict__ spans,
+                                                          const uint32_t *__restrict__ x,
+                                                          const uint32_t *__restrict__ halo,
+                                                          int halo_frames,
+                                                          const double *__restrict__ gains,
+                                                          double level_in, double level,
+                                                          double level_out, double limit,
+                                                          uint32_t *__restrict__ y) {
+    const int t = blockIdx.y;
+    const SpanDev sp = spans[t];
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= sp.out_n) return;
+    const int64_t src = i - halo_frames;      // span-local source frame (delay B-1)
+    const int64_t tsrc = sp.tframe0 + src;   // whole-track source frame
+    uint32_t p = 0;
+    bool zero = tsrc < 0;
+    if (!zero) p = src >= 0 ? x[sp.out_off + src] : halo[(int64_t)t * halo_frames + (halo_frames + src)];
+    const double g = gains[t];
+    int16_t o[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        if (zero) { o[c] = 0; continue; }
+        int16_t v = gain16(c ? hi16(p) : lo16(p), g);
+        double smp = ((double)v * (1.0 / 32768.0)) * level_in;
+        double d = smp * 1.0;
+        d = d < -limit ? -limit : (d > limit ? limit : d);
+        d = d * level * level_out;
+        o[c] = clip_llrint(d * 32768.0);
+    }
+    y[sp.out_off + i] = pack2(o[0], o[1]);
+}
+
+// General alimiter (af_alimiter.c filter_frame, asc off), one thread per track
+// span, sequential.  State layout (doubles): [0] att [1] delta [2] pos [3] nextiter
+// [4] nextlen [5] valid  [8 .. 8+bs) buffer  [8+bs .. 8+2bs) nextdelta
+// [8+2bs .. 8+3bs) nextpos (stored as doubles).
+__global__ void k_final_general(const SpanDev *__restrict__ spans, int n_tracks,
+                                const uint32_t *__restrict__ x,
+                                const uint32_t *__restrict__ halo, int halo_frames,
+                                const double *__restrict__ gains, int fs, double level_in,
+                                double level, double level_out, double limit, double release,
+                                int bs, double *__restrict__ state, int64_t state_doubles,
+                                uint32_t *__restrict__ y) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_tracks) return;
+    const SpanDev sp = spans[t];
+    const int channels = 2;
+    double *S = state + (int64_t)t * state_doubles;
+    double *buffer = S + 8, *nextdelta = S + 8 + bs, *nextposd = S + 8 + 2 * bs;
+    double att, delta;
+    int pos, nextiter, nextlen;
+    if (sp.tframe0 == 0 || S[5] == 0.0) {
+        att = 1.0; delta = 0.0; pos = 0; nextiter = 0; nextlen = 0;
+        for (int k = 0; k < bs; k++) { buffer[k] = 0.0; nextdelta[k] = 0.0; nextposd[k] = -1.0; }
+        if (sp.tframe0 != 0) {
+            // no carried state: prime the ring with the halo (limiter assumed idle)
+            for (int h = 0; h < halo_frames; h++) {
+                uint32_t p = halo[(int64_t)t * halo_frames + h];
+                const double g = gains[t];
+                for (int c = 0; c < channels; c++)
+                    buffer[pos + c] = ((double)gain16(c ? hi16(p) : lo16(p), g) * (1.0 / 32768.0)) * level_in;
+                pos = (pos + channels) % bs;
+            }
+        }
+    } else {
+        att = S[0]; delta = S[1]; pos = (int)S[2]; nextiter = (int)S[3]; nextlen = (int)S[4];
+    }
+#define NEXTPOS(k) ((int)nextposd[(k)])
+    const double g = gains[t];
+    for (int64_t n = 0; n < sp.out_n; n++) {
+        uint32_t p = x[sp.out_off + n];
+        double dst[2];
+        double peak = 0;
+        for (int c = 0; c < channels; c++) {
+            double sample = ((double)gain16(c ? hi16(p) : lo16(p), g) * (1.0 / 32768.0)) * level_in;
+            buffer[pos + c] = sample;
+            peak = fmax(peak, fabs(sample));
+        }
+        if (peak > limit) {
+            double patt = fmin(limit / peak, 1.);
+            double rdelta = (1.0 - patt) / (fs * release);
+            double d = (limit / peak - att) / bs * channels;
+            int found = 0, i;
+            if (d < delta) {
+                delta = d;
+                nextposd[0] = pos;
+                nextposd[1] = -1;
+                nextdelta[0] = rdelta;
+                nextlen = 1;
+                nextiter = 0;
+            } else {
+                for (i = nextiter; i < nextiter + nextlen; i++) {
+                    int jx = i % bs;
+                    double ppeak = 0, pdelta;
+                    for (int c = 0; c < channels; c++) ppeak = fmax(ppeak, fabs(buffer[NEXTPOS(jx) + c]));
+                    pdelta = (limit / peak - limit / ppeak) /
+                             (((bs - NEXTPOS(jx) + pos) % bs) / channels);
+                    if (pdelta < nextdelta[jx]) {
+                        nextdelta[jx] = pdelta;
+                        found = 1;
+                        break;
+                    }
+                }
+                if (found) {
+                    nextlen = i - nextiter + 1;
+                    nextposd[(nextiter + nextlen) % bs] = pos;
+                    nextdelta[(nextiter + nextlen) % bs] = rdelta;
+                    nextposd[(nextiter + nextlen + 1) % bs] = -1;
+                    nextlen++;
+                }
+            }
+        }
+        const double *buf = &buffer[(pos + channels) % bs];
+        peak = 0;
+        for (int c = 0; c < channels; c++) peak = fmax(peak, fabs(buf[c]));
+        att += delta;
+        for (int c = 0; c < channels; c++) dst[c] = buf[c] * att;
+        if ((pos + channels) % bs == NEXTPOS(nextiter)) {
+            delta = nextdelta[nextiter];
+            att = limit / peak;
+            nextlen -= 1;
+            nextposd[nextiter] = -1;
+            nextiter = (nextiter + 1) % bs;
+        }
+        if (att > 1.) { att = 1.; delta = 0.; nextiter = 0; nextlen = 0; nextposd[0] = -1; }
+        if (att <= 0.) { att = 0.0000000000001; delta = (1.0 - att) / (fs * release); }
+        if (att != 1. && (1. - att) < 0.0000000000001) att = 1.;
+        if (delta != 0. && fabs(delta) < 0.00000000000001) delta = 0.;
+        int16_t o[2];
+        for (int c = 0; c < channels; c++) {
+            double v = dst[c];
+            v = v < -limit ? -limit : (v > limit ? limit : v);
+            v = v * level * level_out;
+            o[c] = clip_llrint(v * 32768.0);
+        }
+        y[sp.out_off + n] = pack2(o[0], o[1]);
+        pos = (pos + channels) % bs;
+    }
+#undef NEXTPOS
+    S[0] = att; S[1] = delta; S[2] = pos; S[3] = nextiter; S[4] = nextlen; S[5] = 1.0;
+}
+
+// ---------------------------------------------------------------- launchers
+hipError_t launch_final_fast(const SpanDev *spans, int n_tracks, int64_t max_span,
+                             const int16_t *x, const int16_t *halo, int halo_frames,
+                             const double *gains, double level_in, double level,
+                             double level_out, double limit, int16_t *y, hipStream_t st) {
+    dim3 g = grid1(max_span);
+    g.y = (unsigned)n_tracks;
+    if (empty(g)) return hipSuccess;
+    hipLaunchKernelGGL(k_final_fast, g, dim3(AMX_BLOCK), 0, st, spans,
+                       reinterpret_cast<const uint32_t *>(x),
+                       reinterpret_cast<const uint32_t *>(halo), halo_frames, gains, level_in,
+                       level, level_out, limit, reinterpret_cast<uint32_t *>(y));
+    return hipGetLastError();
+}
+
+hipError_t launch_final_general(const SpanDev *spans, int n_tracks, const int16_t *x,
+                                const int16_t *halo, int halo_frames, const double *gains,
+                                int fs, double level_in, double level, double level_out,
+                                double limit, double release, int buffer_size,
+                                double *state, int64_t state_doubles, int16_t *y,
+                                hipStream_t st) {
+    if (n_tracks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_final_general, dim3((n_tracks + 63) / 64), dim3(64), 0, st, spans,
+                       n_tracks, reinterpret_cast<const uint32_t *>(x),
+                       reinterpret_cast<const uint32_t *>(halo), halo_frames, gains, fs,
+                       level_in, level, level_out, limit, release, buffer_size, state,
+                       state_doubles, reinterpret_cast<uint32_t *>(y));
+    return hipGetLastError();
+}
+
+
+}  // namespace amx

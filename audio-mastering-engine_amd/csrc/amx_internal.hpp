@@ -9,6 +9,7 @@
 #define AMX_KW_DIM 4      // K-weighting 4th-order DF-II state (v1..v4)
 #define AMX_BLOCK 256
 #define AMX_HIST_BINS 1000
+#define AMX_TF_FRAMES 16  // LDS tile frames (AMX_TF in amx_dev.hpp)
 
 // One EQ stage of _apply_eq_to_channel (audio_mastering_engine.py:277-282).
 struct EqStageDev {
@@ -84,7 +85,7 @@ struct Launch {
     int32_t n_chunks, n_seg, L;
     hipStream_t stream;
 };
-hipError_t launch_front1_lut(const Launch &l, int mask, const float *in, const float *lut,
+hipError_t launch_front1_lut(const Launch &l, int mask, int win, const float *in, const float *lut,
                              int16_t *a16, const double *G, double *e);
 hipError_t launch_scan(const double *e, double *s, const int32_t *seg_first,
                        const int32_t *seg_stream, int n_seg, int D, int lanes,

@@ -210,14 +210,17 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     if (desc->sample_rate <= 0) return fail(AMX_EINVAL, "sample_rate must be > 0");
     if (desc->channels_in != 1 && desc->channels_in != 2)
         return fail(AMX_EINVAL, "channels_in must be 1 or 2");
+    if (desc->input_s16 && desc->channels_in != 2)
+        return fail(AMX_EINVAL, "int16 input must be stereo (duplicate mono on the host)");
     *out = nullptr;
     amx_plan *p = new (std::nothrow) amx_plan();
     if (!p) return fail(AMX_ENOMEM, "out of memory");
     p->desc = *desc;
     const int fs = desc->sample_rate;
     p->L = seg_frames > 0 ? seg_frames : 256;
+    p->L = (p->L + AMX_TF_FRAMES - 1) / AMX_TF_FRAMES * AMX_TF_FRAMES;   // whole LDS tiles
     p->hop = (fs + 5) / 10;                    // libebur128 samples_in_100ms
-    p->Lkw = 512 < p->hop ? 512 : p->hop;
+    p->Lkw = 512 < p->hop ? 512 : p->hop / AMX_TF_FRAMES * AMX_TF_FRAMES;
     ChainDev &cd = p->cd;
     memset(&cd, 0, sizeof cd);
     cd.fs = fs;
@@ -593,7 +596,8 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     double *endv = p->mb ? wsp<double>(d_ws, p->o_end) : nullptr;
     switch (stage) {
     case AMX_STAGE_FRONT1:
-        HIPCHK(amx::launch_front1_lut(l, p->mask, d_in, p->d_lut, a16, p->d_G, e));
+        HIPCHK(amx::launch_front1_lut(l, p->mask, (p->cd.chin == 2 && !p->cd.in_s16) ? 2 : 1, d_in,
+                                      p->d_lut, a16, p->d_G, e));
         break;
     case AMX_STAGE_SCAN_EQ:
         if (p->D > 0)
