@@ -49,17 +49,12 @@ __device__ __forceinline__ double sos_step(const double *c, double &z0, double &
 
 // analog character for one frame, exact reference op order (no FMA):
 // lfilter along the channel axis (:264-265) = a length-2 sequence per frame.
-__device__ __forceinline__ void analog_frame(const ChainDev &cd, const float *lut, int16_t l,
-                                             int16_t r, int16_t &ol, int16_t &orr) {
-    double x0, x1;
-    if (lut) {
-        x0 = (double)lut[(int)l + 32768];
-        x1 = (double)lut[(int)r + 32768];
-    } else {
-        float a = ((float)l / 32768.0f) * cd.drive, b = ((float)r / 32768.0f) * cd.drive;
-        x0 = (double)(float)tanh((double)a);
-        x1 = (double)(float)tanh((double)b);
-    }
+// tanh comes from the plan's 65536-entry table of numpy's float32 tanh over every
+// int16 input (design.py), so the result is the reference's own rounding.
+__device__ __forceinline__ void analog_frame(const ChainDev &cd, const float *__restrict__ lut,
+                                             int16_t l, int16_t r, int16_t &ol, int16_t &orr) {
+    const double x0 = (double)lut[(int)l + 32768];
+    const double x1 = (double)lut[(int)r + 32768];
     const double *b1 = cd.an_lo, *b2 = cd.an_hi;
     // first shelf (120 Hz low, +cf dB): y0 = 0 + b0*x0 ; Z0 = (0 + x0*b1) - y0*a1 ; y1 = Z0 + b0*x1
     double y0 = 0.0 + b1[0] * x0;
@@ -83,49 +78,58 @@ struct EqDim {
                              ((MASK & 8) ? 2 : 0);
 };
 
-// One channel: z holds the compact state (active stages in order).
-// Stage k is the first active stage (float32 input) iff no lower bit of MASK is set.
 template <int MASK>
-__device__ __forceinline__ float eq_chain(const ChainDev &cd, double *z, float xf) {
+struct EqQ {   // doubles of ChainDev::eqc used by the active stages
+    static constexpr int n = ((MASK & 1) ? 6 : 0) + ((MASK & 2) ? 21 : 0) + ((MASK & 4) ? 21 : 0) +
+                             ((MASK & 8) ? 6 : 0);
+};
+
+// DF-II-T biquad on packed coefficients q = b0 b1 b2 a1 a2 (FMA recursion)
+__device__ __forceinline__ double bq_step(const double *q, double &z0, double &z1, double x) {
+    const double y = fma(q[0], x, z0);
+    z0 = fma(-q[3], y, fma(q[1], x, z1));
+    z1 = fma(-q[4], y, q[2] * x);
+    return y;
+}
+
+// One channel of _apply_eq_to_channel (:277-282) over the active stages of MASK.
+// q = the stage coefficients (registers, ChainDev::eqc layout), z = compact state,
+// negm bit s = stage s is a negative-gain shelf (:289: x*g + (y - x*g)).  The first
+// active stage sees the float32 column, so a negative first shelf forms x*g as a
+// float32 product (NEP 50); later stages see float64.
+template <int MASK>
+__device__ __forceinline__ float eq_chain(int negm, const double *q, double *z, float xf) {
     double x = (double)xf;
-    int o = 0;
+    int o = 0, c = 0;
     if constexpr ((MASK & 1) != 0) {
-        const EqStageDev &s = cd.st[0];
-        double y = lf_step(s.c, z[o], z[o + 1], x);
-        if (!s.neg) x = x + (y - x) * s.gm1;
-        else { double xg = (double)(xf * s.gf); x = xg + (y - xg); }
+        const double y = bq_step(q + c, z[o], z[o + 1], x);
+        if (!(negm & 1)) x = x + (y - x) * q[c + 5];
+        else { const double xg = (double)(xf * (float)q[c + 5]); x = xg + (y - xg); }
         o += 2;
+        c += 6;
     }
-    if constexpr ((MASK & 2) != 0) {
-        const EqStageDev &s = cd.st[1];
-        double b = x;
 #pragma unroll
-        for (int k = 0; k < 4; k++) b = sos_step(s.c + 6 * k, z[o + 2 * k], z[o + 2 * k + 1], b);
-        x = x + b * s.gm1;
-        o += 8;
-    }
-    if constexpr ((MASK & 4) != 0) {
-        const EqStageDev &s = cd.st[2];
-        double b = x;
+    for (int s = 1; s <= 2; s++) {
+        if ((MASK >> s) & 1) {
+            double b = x;
 #pragma unroll
-        for (int k = 0; k < 4; k++) b = sos_step(s.c + 6 * k, z[o + 2 * k], z[o + 2 * k + 1], b);
-        x = x + b * s.gm1;
-        o += 8;
+            for (int k = 0; k < 4; k++) b = bq_step(q + c + 5 * k, z[o + 2 * k], z[o + 2 * k + 1], b);
+            x = x + b * q[c + 20];
+            o += 8;
+            c += 21;
+        }
     }
     if constexpr ((MASK & 8) != 0) {
-        const EqStageDev &s = cd.st[3];
-        double y = lf_step(s.c, z[o], z[o + 1], x);
-        if (!s.neg) x = x + (y - x) * s.gm1;
-        else if constexpr ((MASK & 7) == 0) { double xg = (double)(xf * s.gf); x = xg + (y - xg); }
-        else { double xg = x * s.g; x = xg + (y - xg); }
+        const double y = bq_step(q + c, z[o], z[o + 1], x);
+        if (!(negm & 8)) x = x + (y - x) * q[c + 5];
+        else if constexpr ((MASK & 7) == 0) { const double xg = (double)(xf * (float)q[c + 5]); x = xg + (y - xg); }
+        else { const double xg = x * q[c + 5]; x = xg + (y - xg); }
         o += 2;
     }
     (void)o;
     if constexpr (MASK == 0) return xf;
     return (float)x;
 }
-// stage-1/2 "first" cases: a peak stage has no float32-sensitive op, and the
-// stage-0 shelf is always first; only stage 3 needs the (MASK & 7) test above.
 
 __device__ __forceinline__ void width_frame(float w, float &l, float &r) {
     // apply_stereo_width (:269-270), float32, exact order
@@ -144,53 +148,66 @@ __device__ __forceinline__ void width_frame(float w, float &l, float &r) {
 // 64-128 contiguous bytes instead of 64 scattered cache lines.  The row pitch is
 // ROW+1 dwords so the per-thread row reads are LDS-bank-conflict free.
 #define AMX_TF AMX_TF_FRAMES
-template <int W>
+template <int W, int ROWS = AMX_BLOCK>
 struct Tile {
     static constexpr int ROW = AMX_TF * W;
     static constexpr int PITCH = ROW + 1;
-    static constexpr int WORDS = AMX_BLOCK * PITCH;
+    static constexpr int WORDS = ROWS * PITCH;
+    static constexpr int ITER = ROWS * ROW / AMX_BLOCK;   // dwords per thread per tile
+    static constexpr int RSTEP = AMX_BLOCK / ROW;         // rows covered per iteration
 };
 
-// Row r holds frames n in [lo[r], hi[r]) at dword rb[r] + n*W (lo == nullptr -> 0).
-// Loads are issued unconditionally from a clamped in-range address and masked
-// afterwards: a load guarded by a per-element branch makes hipcc wait vmcnt(0)
-// after every element (cdna_hip_programming.md §5 "Three .s-level traps" (c)),
-// which serialises the tile into ROW dependent HBM round trips.
-template <int W>
+// Row r (< ROWS) holds frames n in [lo[r], hi[r]) at dword rb[r] + n*W (lo == nullptr
+// -> 0).  Loads are issued unconditionally from a clamped in-range address and
+// masked afterwards: a load guarded by a per-element branch makes hipcc wait
+// vmcnt(0) after every element (cdna_hip_programming.md §5 "Three .s-level traps"
+// (c)), which serialises the tile into dependent HBM round trips.
+template <int W, int ROWS = AMX_BLOCK>
 __device__ __forceinline__ void tile_load(uint32_t *lds, const uint32_t *__restrict__ src,
                                           const int64_t *rb, const int *lo, const int *hi,
                                           int k) {
-    constexpr int ROW = Tile<W>::ROW, PITCH = Tile<W>::PITCH;
-    uint32_t v[ROW];
-    bool ok[ROW];
-    const int c = threadIdx.x % ROW;              // column is fixed per thread
+    using T = Tile<W, ROWS>;
+    uint32_t v[T::ITER];
+    bool ok[T::ITER];
+    const int c = threadIdx.x % T::ROW;              // column is fixed per thread
     const int n = k + c / W;
 #pragma unroll
-    for (int m = 0; m < ROW; m++) {
-        const int r = threadIdx.x / ROW + m * (AMX_BLOCK / ROW);
+    for (int m = 0; m < T::ITER; m++) {
+        const int r = threadIdx.x / T::ROW + m * T::RSTEP;
         const int l0 = lo ? lo[r] : 0, h0 = hi[r];
         ok[m] = n >= l0 && n < h0;
         const int nn = ok[m] ? n : (h0 > l0 ? l0 : 0);
         v[m] = src[rb[r] + (int64_t)nn * W + (c % W)];
     }
 #pragma unroll
-    for (int m = 0; m < ROW; m++) {
-        const int r = threadIdx.x / ROW + m * (AMX_BLOCK / ROW);
-        lds[r * PITCH + c] = ok[m] ? v[m] : 0u;
+    for (int m = 0; m < T::ITER; m++) {
+        const int r = threadIdx.x / T::ROW + m * T::RSTEP;
+        lds[r * T::PITCH + c] = ok[m] ? v[m] : 0u;
     }
 }
 
-template <int W>
+template <int W, int ROWS = AMX_BLOCK>
 __device__ __forceinline__ void tile_store(const uint32_t *lds, uint32_t *__restrict__ dst,
                                            const int64_t *rb, const int *hi, int k) {
-    constexpr int ROW = Tile<W>::ROW, PITCH = Tile<W>::PITCH;
-    const int c = threadIdx.x % ROW;
+    using T = Tile<W, ROWS>;
+    const int c = threadIdx.x % T::ROW;
     const int n = k + c / W;
 #pragma unroll
-    for (int m = 0; m < ROW; m++) {
-        const int r = threadIdx.x / ROW + m * (AMX_BLOCK / ROW);
-        if (n < hi[r]) dst[rb[r] + (int64_t)n * W + (c % W)] = lds[r * PITCH + c];
+    for (int m = 0; m < T::ITER; m++) {
+        const int r = threadIdx.x / T::ROW + m * T::RSTEP;
+        if (n < hi[r]) dst[rb[r] + (int64_t)n * W + (c % W)] = lds[r * T::PITCH + c];
     }
+}
+
+// the other lane of an even/odd lane pair (channel pairs, DPP quad_perm [1,0,3,2])
+__device__ __forceinline__ float pair_swap(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ double pair_swap(double v) {
+    const int64_t b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), 0xB1, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0xB1, 0xF, 0xF, false);
+    return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
 }
 
 static inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + AMX_BLOCK - 1) / AMX_BLOCK)); }

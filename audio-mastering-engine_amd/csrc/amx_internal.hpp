@@ -10,6 +10,8 @@
 #define AMX_BLOCK 256
 #define AMX_HIST_BINS 1000
 #define AMX_TF_FRAMES 16  // LDS tile frames (AMX_TF in amx_dev.hpp)
+#define AMX_SCAN_S 16     // segments per scan block
+#define AMX_EQC 64        // compact EQ coefficient block (see ChainDev::eqc)
 
 // One EQ stage of _apply_eq_to_channel (audio_mastering_engine.py:277-282).
 struct EqStageDev {
@@ -39,6 +41,10 @@ struct ChainDev {
     int32_t look;          // int(5 ms * fs)
     int32_t rthr[3];       // smallest integer rms with rms > thresh_rms
     double kw1[6], kw2[6]; // K-weighting as two DF-II-T biquads (libebur128 pb/pa, rb/ra)
+    // Active EQ stages packed in order for register-resident use (amx_dev.hpp eq_chain):
+    //   shelf: b0 b1 b2 a1 a2 gx     (gx = g-1, or the negative-gain factor g / f32(g))
+    //   peak : 4 x [b0 b1 b2 a1 a2] gm1
+    double eqc[AMX_EQC];
 };
 
 // A ~30 s chunk (ffmpeg segment, :178).  loc_off indexes chunk-local scratch.
@@ -71,6 +77,14 @@ struct KwSegDev {
     int32_t last;        // 1 if last segment of its span
 };
 
+// A block of up to AMX_SCAN_S consecutive segments of one stream (amx_scan.hip).
+struct ScanBlk {
+    int32_t seg0, nseg;
+    int32_t first;       // index of the stream's first block
+    int32_t last;        // 1 if the stream's last block
+    int32_t stream, pad_;
+};
+
 struct SpanDev {
     int64_t out_off, out_n, tframe0, ttotal;
     int32_t kseg0, nkseg;
@@ -85,11 +99,16 @@ struct Launch {
     int32_t n_chunks, n_seg, L;
     hipStream_t stream;
 };
-hipError_t launch_front1_lut(const Launch &l, int mask, int win, const float *in, const float *lut,
-                             int16_t *a16, const double *G, double *e);
-hipError_t launch_scan(const double *e, double *s, const int32_t *seg_first,
-                       const int32_t *seg_stream, int n_seg, int D, int lanes,
-                       const double *Mp, int levels, const double *carry, hipStream_t st);
+struct ScanPlan {
+    int D, n_blk, levels;
+    const ScanBlk *blks;
+    const double *M;     // A^L, D x D row-major
+    const double *Mbp;   // (A^{L S})^(2^l), l < levels
+};
+hipError_t launch_front1(const Launch &l, int D, int win, bool analog, const float *in,
+                         const float *lut, int16_t *a16, const double *G, double *e);
+hipError_t launch_scan(const ScanPlan &p, const double *e, double *s, const double *carry,
+                       double *eb, double *bst, hipStream_t st);
 hipError_t launch_front2(const Launch &l, int mask, const int16_t *a16, const double *s_eq,
                          int16_t *dst, int to_out, const double *Gx, double *e_x);
 hipError_t launch_xover2(const Launch &l, const int16_t *p16, const double *s_x,

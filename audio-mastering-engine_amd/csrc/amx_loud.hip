@@ -37,6 +37,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_kw1(const KwSegDev *__restrict__ 
         tile_load<1>(s_in, x, rb, rlo, rhi, k);
         __syncthreads();
         const uint32_t *row = s_in + t * Tile<1>::PITCH;
+#pragma unroll 4
         for (int f = 0; f < AMX_TF; f++) {
             const uint32_t p = row[f];
             const int a = lo16(p), b = hi16(p);
@@ -74,8 +75,9 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_kw1(const KwSegDev *__restrict__ 
 }
 
 // K-weighting pass 2: filter from the true state (two DF-II-T biquads, see
-// amx_plan.cpp), y^2 summed per 100 ms hop piece.  parts[j][piece][ch],
-// part_hop[j] = whole-track hop index of piece 0 (a segment spans <= 2 hops).
+// amx_plan.cpp), y^2 summed per 100 ms hop piece.  One thread per (segment,
+// channel), lanes 2i / 2i+1 = L / R of row i.  parts[j][piece][ch], part_hop[j] =
+// whole-track hop index of piece 0 (a segment spans <= 2 hops).
 __global__ void __launch_bounds__(AMX_BLOCK) k_kw2(const ChainDev *__restrict__ cdp,
                                                    const KwSegDev *__restrict__ ks, int n_kseg,
                                                    int L, int hop,
@@ -83,54 +85,58 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_kw2(const ChainDev *__restrict__ 
                                                    const double *__restrict__ s,
                                                    double *__restrict__ parts,
                                                    int64_t *__restrict__ part_hop) {
-    __shared__ uint32_t s_in[Tile<1>::WORDS];
-    __shared__ int64_t rb[AMX_BLOCK];
-    __shared__ int rl[AMX_BLOCK];
+    constexpr int ROWS = AMX_BLOCK / 2;
+    using T = Tile<1, ROWS>;
+    __shared__ uint32_t s_in[T::WORDS];
+    __shared__ int64_t rb[ROWS];
+    __shared__ int rl[ROWS];
+    __shared__ double s_c[12];
     const ChainDev &cd = *cdp;
-    const int t = threadIdx.x;
-    const int j = blockIdx.x * AMX_BLOCK + t;
+    const int t = threadIdx.x, row = t >> 1, chn = t & 1;
+    const int j = blockIdx.x * ROWS + row;
     const bool valid = j < n_kseg;
     const KwSegDev sg = ks[valid ? j : n_kseg - 1];
-    rb[t] = valid ? sg.out_pos : 0;
-    rl[t] = valid ? sg.len : 0;
-    double v[2][4];
-    const double *st = s + (int64_t)(valid ? j : 0) * 2 * AMX_KW_DIM;
+    if (chn == 0) {
+        rb[row] = valid ? sg.out_pos : 0;
+        rl[row] = valid ? sg.len : 0;
+    }
+    if (t < 6) s_c[t] = cd.kw1[t];
+    else if (t < 12) s_c[t] = cd.kw2[t - 6];
+    double v[4];
+    const double *st = s + ((int64_t)(valid ? j : 0) * 2 + chn) * AMX_KW_DIM;
 #pragma unroll
-    for (int c = 0; c < 2; c++)
-#pragma unroll
-        for (int d = 0; d < 4; d++) v[c][d] = valid ? st[c * 4 + d] : 0.0;
+    for (int d = 0; d < 4; d++) v[d] = valid ? st[d] : 0.0;
     const int len = valid ? sg.len : 0;
     const int64_t h0 = sg.tframe / hop;
     const int64_t split = (h0 + 1) * hop - sg.tframe;   // first frame of piece 1
-    double acc[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+    double acc0 = 0.0, acc1 = 0.0;
     __syncthreads();
-    for (int k = 0; k < L; k += AMX_TF) {
-        tile_load<1>(s_in, x, rb, nullptr, rl, k);
-        __syncthreads();
-        const uint32_t *row = s_in + t * Tile<1>::PITCH;
-        for (int f = 0; f < AMX_TF; f++) {
-            const uint32_t p = row[f];
-            const int n = k + f;
-            const int piece = n >= split ? 1 : 0;
-            const bool act = n < len;
+    double c1[5], c2[5];
 #pragma unroll
-            for (int c = 0; c < 2; c++) {
-                const double xs = (double)(c ? hi16(p) : lo16(p)) * (1.0 / 32768.0);
-                const double u = sos_step(cd.kw1, v[c][0], v[c][1], xs);
-                const double y = act ? sos_step(cd.kw2, v[c][2], v[c][3], u) : 0.0;
-                if (piece) acc[1][c] = fma(y, y, acc[1][c]);
-                else acc[0][c] = fma(y, y, acc[0][c]);
-            }
+    for (int i = 0; i < 3; i++) { c1[i] = s_c[i]; c2[i] = s_c[6 + i]; }
+    c1[3] = s_c[4]; c1[4] = s_c[5];
+    c2[3] = s_c[10]; c2[4] = s_c[11];
+    for (int k = 0; k < L; k += AMX_TF) {
+        tile_load<1, ROWS>(s_in, x, rb, nullptr, rl, k);
+        __syncthreads();
+        const uint32_t *rp = s_in + row * T::PITCH;
+#pragma unroll 4
+        for (int f = 0; f < AMX_TF; f++) {
+            const uint32_t p = rp[f];
+            const int n = k + f;
+            const double xs = (double)(chn ? hi16(p) : lo16(p)) * (1.0 / 32768.0);
+            const double u = bq_step(c1, v[0], v[1], xs);
+            const double y = n < len ? bq_step(c2, v[2], v[3], u) : 0.0;
+            if (n >= split) acc1 = fma(y, y, acc1);
+            else acc0 = fma(y, y, acc0);
         }
         __syncthreads();
     }
     if (valid) {
         double *o = parts + (int64_t)j * 4;
-        o[0] = acc[0][0];
-        o[1] = acc[0][1];
-        o[2] = acc[1][0];
-        o[3] = acc[1][1];
-        part_hop[j] = h0;
+        o[chn] = acc0;
+        o[2 + chn] = acc1;
+        if (chn == 0) part_hop[j] = h0;
     }
 }
 
@@ -217,7 +223,8 @@ hipError_t launch_kw2(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L,
                       const int16_t *x, const double *s, double *parts, int64_t *part_hop,
                       hipStream_t st) {
     if (n_kseg <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_kw2, grid1(n_kseg), dim3(AMX_BLOCK), 0, st, cd, ks, n_kseg, L, hop,
+    const dim3 grid((unsigned)((n_kseg + AMX_BLOCK / 2 - 1) / (AMX_BLOCK / 2)));
+    hipLaunchKernelGGL(k_kw2, grid, dim3(AMX_BLOCK), 0, st, cd, ks, n_kseg, L, hop,
                        reinterpret_cast<const uint32_t *>(x), s, parts, part_hop);
     return hipGetLastError();
 }

@@ -147,11 +147,12 @@ struct amx_plan {
     int mask = 0, D = 0;
     int lev_eq = 0, lev_x = 0, lev_kw = 0;
     int mb = 0, warm = 512;
-    int n_tracks = 0, n_chunks = 0, n_seg = 0, n_kseg = 0;
+    int n_tracks = 0, n_chunks = 0, n_seg = 0, n_kseg = 0, n_blk = 0, n_kblk = 0;
     int64_t nloc = 0, out_frames = 0, max_chunk_out = 0, max_span = 0;
     std::vector<ChunkDev> chunks;
     std::vector<SegDev> segs;
     std::vector<KwSegDev> ksegs;
+    std::vector<ScanBlk> blks, kblks;
     std::vector<SpanDev> spans;
     std::vector<int64_t> n1tab;
     Lti kw_model;
@@ -162,17 +163,22 @@ struct amx_plan {
     SegDev *d_segs = nullptr;
     KwSegDev *d_ksegs = nullptr;
     SpanDev *d_spans = nullptr;
-    int32_t *d_seg_first = nullptr, *d_seg_stream = nullptr;
-    int32_t *d_kseg_first = nullptr, *d_kseg_stream = nullptr;
+    ScanBlk *d_blks = nullptr, *d_kblks = nullptr;
     int64_t *d_n1 = nullptr;
-    double *d_G = nullptr, *d_Mp = nullptr, *d_Gx = nullptr, *d_Mpx = nullptr;
-    double *d_Gkw = nullptr, *d_Mpkw = nullptr, *d_tabs = nullptr, *d_bounds = nullptr;
+    double *d_G = nullptr, *d_M = nullptr, *d_Mp = nullptr;
+    double *d_Gx = nullptr, *d_Mx = nullptr, *d_Mpx = nullptr;
+    double *d_Gkw = nullptr, *d_Mkw = nullptr, *d_Mpkw = nullptr;
+    double *d_tabs = nullptr, *d_bounds = nullptr;
     double *d_tailpow = nullptr;
     float *d_lut = nullptr;
     // workspace offsets
     size_t ws_bytes = 0;
     size_t o_a16, o_e, o_s, o_p16, o_ex, o_sx, o_bands, o_r, o_att, o_guess, o_end;
     size_t o_ekw, o_skw, o_parts, o_phop;
+    size_t o_eb, o_bst, o_ebx, o_bstx, o_ebk, o_bstk;
+    amx::ScanPlan scan_eq() const { return {D, n_blk, lev_eq, d_blks, d_M, d_Mp}; }
+    amx::ScanPlan scan_xo() const { return {AMX_XO_DIM, mb ? n_blk : 0, lev_x, d_blks, d_Mx, d_Mpx}; }
+    amx::ScanPlan scan_kw() const { return {AMX_KW_DIM, n_kblk, lev_kw, d_kblks, d_Mkw, d_Mpkw}; }
 };
 
 namespace {
@@ -187,6 +193,20 @@ int upload(T **dst, const T *src, size_t n) {
 template <class T>
 T *wsp(void *ws, size_t off) {
     return reinterpret_cast<T *>(reinterpret_cast<char *>(ws) + off);
+}
+
+// blocks of AMX_SCAN_S segments over each stream's run [j0, j0 + n) of segments
+void add_blocks(std::vector<ScanBlk> &out, int32_t j0, int32_t n, int32_t stream) {
+    const int32_t first = (int32_t)out.size();
+    for (int32_t q = 0; q < n; q += AMX_SCAN_S) {
+        ScanBlk b{};
+        b.seg0 = j0 + q;
+        b.nseg = (n - q) < AMX_SCAN_S ? (n - q) : AMX_SCAN_S;
+        b.first = first;
+        b.last = (q + AMX_SCAN_S >= n) ? 1 : 0;
+        b.stream = stream;
+        out.push_back(b);
+    }
 }
 
 int64_t overlay_len(int64_t n, int fs) {
@@ -212,6 +232,8 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         return fail(AMX_EINVAL, "channels_in must be 1 or 2");
     if (desc->input_s16 && desc->channels_in != 2)
         return fail(AMX_EINVAL, "int16 input must be stereo (duplicate mono on the host)");
+    if (desc->analog_on && !desc->tanh_lut)
+        return fail(AMX_EINVAL, "analog character needs the float32 tanh table (tanh_lut)");
     *out = nullptr;
     amx_plan *p = new (std::nothrow) amx_plan();
     if (!p) return fail(AMX_ENOMEM, "out of memory");
@@ -220,7 +242,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     p->L = seg_frames > 0 ? seg_frames : 256;
     p->L = (p->L + AMX_TF_FRAMES - 1) / AMX_TF_FRAMES * AMX_TF_FRAMES;   // whole LDS tiles
     p->hop = (fs + 5) / 10;                    // libebur128 samples_in_100ms
-    p->Lkw = 512 < p->hop ? 512 : p->hop / AMX_TF_FRAMES * AMX_TF_FRAMES;
+    p->Lkw = 128 < p->hop ? 128 : p->hop / AMX_TF_FRAMES * AMX_TF_FRAMES;
     ChainDev &cd = p->cd;
     memset(&cd, 0, sizeof cd);
     cd.fs = fs;
@@ -254,6 +276,28 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         st.gm1 = desc->eq_gain[s] - 1.0;
         st.gf = (float)desc->eq_gain[s];
         for (int k = 0; k < 24; k++) st.c[k] = desc->eq_coef[s][k];
+    }
+    {   // compact register-resident coefficients (amx_dev.hpp eq_chain)
+        int c = 0;
+        for (int s = 0; s < 4; s++) {
+            const EqStageDev &st = cd.st[s];
+            if (!st.kind) continue;
+            const double *k = st.c;
+            int nsec = st.kind == 1 ? 1 : 4;
+            for (int q = 0; q < nsec; q++) {
+                cd.eqc[c++] = k[6 * q + 0];
+                cd.eqc[c++] = k[6 * q + 1];
+                cd.eqc[c++] = k[6 * q + 2];
+                cd.eqc[c++] = k[6 * q + 4];
+                cd.eqc[c++] = k[6 * q + 5];
+            }
+            if (st.kind == 2) cd.eqc[c++] = st.gm1;
+            else if (!st.neg) cd.eqc[c++] = st.gm1;
+            else {
+                const bool first = (mask & ((1 << s) - 1)) == 0;   // stage sees the float32 column
+                cd.eqc[c++] = first ? (double)st.gf : st.g;
+            }
+        }
     }
     cd.eq_mask = mask;
     cd.eq_dim = D;
@@ -348,7 +392,6 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     p->n_tracks = n_tracks;
     p->n_chunks = n_chunks;
     int64_t loc = 0, outo = 0;
-    std::vector<int32_t> seg_first, seg_stream;
     p->spans.assign(n_tracks, SpanDev{});
     std::vector<int> track_seen(n_tracks, 0);
     for (int c = 0; c < n_chunks; c++) {
@@ -367,6 +410,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         ch.seg0 = (int32_t)p->segs.size();
         int64_t ns = (ch.n + p->L - 1) / p->L;
         ch.nseg = (int32_t)ns;
+        add_blocks(p->blks, ch.seg0, (int32_t)ns, c);
         for (int64_t k = 0; k < ns; k++) {
             SegDev s{};
             s.pos = k * p->L;
@@ -375,8 +419,6 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             s.first = ch.seg0;
             s.last = (k == ns - 1) ? 1 : 0;
             p->segs.push_back(s);
-            seg_first.push_back(ch.seg0);
-            seg_stream.push_back(c);
         }
         SpanDev &sp = p->spans[ch.track];
         if (!track_seen[ch.track]) {
@@ -394,7 +436,6 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     p->out_frames = outo;
     p->n_seg = (int)p->segs.size();
     // K-weighting segments per track span
-    std::vector<int32_t> kfirst, kstream;
     for (int t = 0; t < n_tracks; t++) {
         SpanDev &sp = p->spans[t];
         sp.tframe0 = track_frame0 ? track_frame0[t] : 0;
@@ -402,6 +443,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         sp.kseg0 = (int32_t)p->ksegs.size();
         int64_t nk = (sp.out_n + p->Lkw - 1) / p->Lkw;
         sp.nkseg = (int32_t)nk;
+        add_blocks(p->kblks, sp.kseg0, (int32_t)nk, t);
         for (int64_t k = 0; k < nk; k++) {
             KwSegDev s{};
             s.out_pos = sp.out_off + k * p->Lkw;
@@ -411,16 +453,16 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             s.first = sp.kseg0;
             s.last = (k == nk - 1) ? 1 : 0;
             p->ksegs.push_back(s);
-            kfirst.push_back(sp.kseg0);
-            kstream.push_back(t);
         }
         p->max_span = sp.out_n > p->max_span ? sp.out_n : p->max_span;
     }
     p->n_kseg = (int)p->ksegs.size();
+    p->n_blk = (int)p->blks.size();
+    p->n_kblk = (int)p->kblks.size();
 
     // ------------------------------------------------------- LTI models
     const double tol = 1e-22;
-    std::vector<double> G, Mp, Gx, Mpx, Gkw, Mpkw;
+    std::vector<double> G, M, Mp, Gx, Mx, Mpx, Gkw, Mkw, Mpkw;
     if (D > 0) {
         Lti eq;
         eq.derive(D, [&](double *z, double x) {
@@ -439,7 +481,8 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             }
         });
         G = eq.gemv_table(p->L);
-        p->lev_eq = eq.scan_powers(p->L, tol, 7, Mp);
+        M = matpow(eq.A, p->L, D);
+        p->lev_eq = eq.scan_powers(p->L * AMX_SCAN_S, tol, 7, Mp);
         if (p->lev_eq < 0) {
             delete p;
             return fail(AMX_ERANGE, "EQ decays too slowly for %d-frame segments; raise seg_frames", p->L);
@@ -454,7 +497,8 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             sos_step_h(cd.xhi + 6, z + 6, h);
         });
         Gx = xo.gemv_table(p->L);
-        p->lev_x = xo.scan_powers(p->L, tol, 7, Mpx);
+        Mx = matpow(xo.A, p->L, AMX_XO_DIM);
+        p->lev_x = xo.scan_powers(p->L * AMX_SCAN_S, tol, 7, Mpx);
         if (p->lev_x < 0) {
             delete p;
             return fail(AMX_ERANGE, "crossover decays too slowly for %d-frame segments", p->L);
@@ -467,7 +511,8 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             sos_step_h(cd.kw2, z + 2, y);
         });
         Gkw = kw.gemv_table(p->Lkw);
-        p->lev_kw = kw.scan_powers(p->Lkw, tol, 7, Mpkw);
+        Mkw = matpow(kw.A, p->Lkw, AMX_KW_DIM);
+        p->lev_kw = kw.scan_powers(p->Lkw * AMX_SCAN_S, tol, 7, Mpkw);
         if (p->lev_kw < 0) {
             delete p;
             return fail(AMX_ERANGE, "K-weighting decays too slowly for %d-frame segments", p->Lkw);
@@ -498,16 +543,17 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     UP(p->d_segs, p->segs.data(), p->segs.size());
     UP(p->d_ksegs, p->ksegs.data(), p->ksegs.size());
     UP(p->d_spans, p->spans.data(), p->spans.size());
-    UP(p->d_seg_first, seg_first.data(), seg_first.size());
-    UP(p->d_seg_stream, seg_stream.data(), seg_stream.size());
-    UP(p->d_kseg_first, kfirst.data(), kfirst.size());
-    UP(p->d_kseg_stream, kstream.data(), kstream.size());
+    UP(p->d_blks, p->blks.data(), p->blks.size());
+    UP(p->d_kblks, p->kblks.data(), p->kblks.size());
     UP(p->d_n1, p->n1tab.data(), p->n1tab.size());
     UP(p->d_G, G.data(), G.size());
+    UP(p->d_M, M.data(), M.size());
     UP(p->d_Mp, Mp.data(), Mp.size());
     UP(p->d_Gx, Gx.data(), Gx.size());
+    UP(p->d_Mx, Mx.data(), Mx.size());
     UP(p->d_Mpx, Mpx.data(), Mpx.size());
     UP(p->d_Gkw, Gkw.data(), Gkw.size());
+    UP(p->d_Mkw, Mkw.data(), Mkw.size());
     UP(p->d_Mpkw, Mpkw.data(), Mpkw.size());
     UP(p->d_tabs, tabs.data(), tabs.size());
     UP(p->d_bounds, bounds, 1001);
@@ -530,6 +576,15 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         p->o_guess = (size_t)align_up(off, 3 * nseg * 8);
         p->o_end = (size_t)align_up(off, 3 * nseg * 8);
     }
+    const size_t nb = (size_t)p->n_blk, nkb = (size_t)p->n_kblk;
+    p->o_eb = (size_t)align_up(off, nb * 2 * (D ? D : 1) * 8);
+    p->o_bst = (size_t)align_up(off, nb * 2 * (D ? D : 1) * 8);
+    if (p->mb) {
+        p->o_ebx = (size_t)align_up(off, nb * 2 * AMX_XO_DIM * 8);
+        p->o_bstx = (size_t)align_up(off, nb * 2 * AMX_XO_DIM * 8);
+    }
+    p->o_ebk = (size_t)align_up(off, nkb * 2 * AMX_KW_DIM * 8);
+    p->o_bstk = (size_t)align_up(off, nkb * 2 * AMX_KW_DIM * 8);
     p->o_ekw = (size_t)align_up(off, nk * 2 * AMX_KW_DIM * 8);
     p->o_skw = (size_t)align_up(off, nk * 2 * AMX_KW_DIM * 8);
     p->o_parts = (size_t)align_up(off, nk * 4 * 8);
@@ -541,10 +596,10 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
 
 void amx_plan_free(amx_plan *p) {
     if (!p) return;
-    void *ptrs[] = {p->d_cd,    p->d_chunks,     p->d_segs,       p->d_ksegs,        p->d_spans,
-                    p->d_seg_first, p->d_seg_stream, p->d_kseg_first, p->d_kseg_stream, p->d_n1,
-                    p->d_G,     p->d_Mp,         p->d_Gx,         p->d_Mpx,          p->d_Gkw,
-                    p->d_Mpkw,  p->d_tabs,       p->d_bounds,     p->d_tailpow,      p->d_lut};
+    void *ptrs[] = {p->d_cd,  p->d_chunks, p->d_segs, p->d_ksegs, p->d_spans,  p->d_blks,
+                    p->d_kblks, p->d_n1,   p->d_G,    p->d_M,     p->d_Mp,     p->d_Gx,
+                    p->d_Mx,  p->d_Mpx,    p->d_Gkw,  p->d_Mkw,   p->d_Mpkw,   p->d_tabs,
+                    p->d_bounds, p->d_tailpow, p->d_lut};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     delete p;
@@ -596,13 +651,13 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     double *endv = p->mb ? wsp<double>(d_ws, p->o_end) : nullptr;
     switch (stage) {
     case AMX_STAGE_FRONT1:
-        HIPCHK(amx::launch_front1_lut(l, p->mask, (p->cd.chin == 2 && !p->cd.in_s16) ? 2 : 1, d_in,
-                                      p->d_lut, a16, p->d_G, e));
+        HIPCHK(amx::launch_front1(l, p->D, (p->cd.chin == 2 && !p->cd.in_s16) ? 2 : 1,
+                                  p->cd.analog_on != 0, d_in, p->d_lut, a16, p->d_G, e));
         break;
     case AMX_STAGE_SCAN_EQ:
         if (p->D > 0)
-            HIPCHK(amx::launch_scan(e, s, p->d_seg_first, p->d_seg_stream, p->n_seg, p->D, 2,
-                                    p->d_Mp, p->lev_eq, nullptr, st));
+            HIPCHK(amx::launch_scan(p->scan_eq(), e, s, nullptr, wsp<double>(d_ws, p->o_eb),
+                                    wsp<double>(d_ws, p->o_bst), st));
         break;
     case AMX_STAGE_FRONT2:
         if (!p->mb) HIPCHK(amx::launch_front2(l, p->mask, a16, s, d_out, 1, nullptr, nullptr));
@@ -610,8 +665,8 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
         break;
     case AMX_STAGE_SCAN_XO:
         if (p->mb)
-            HIPCHK(amx::launch_scan(ex, sx, p->d_seg_first, p->d_seg_stream, p->n_seg, AMX_XO_DIM, 2,
-                                    p->d_Mpx, p->lev_x, nullptr, st));
+            HIPCHK(amx::launch_scan(p->scan_xo(), ex, sx, nullptr, wsp<double>(d_ws, p->o_ebx),
+                                    wsp<double>(d_ws, p->o_bstx), st));
         break;
     case AMX_STAGE_XOVER:
         if (p->mb) HIPCHK(amx::launch_xover2(l, p16, sx, bands, p->nloc));
@@ -658,8 +713,8 @@ int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, double *d_kw_tail, dou
     double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
     HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e,
                            reinterpret_cast<unsigned long long *>(d_peak), st));
-    HIPCHK(amx::launch_scan(e, s, p->d_kseg_first, p->d_kseg_stream, p->n_kseg, AMX_KW_DIM, 2,
-                            p->d_Mpkw, p->lev_kw, nullptr, st));
+    HIPCHK(amx::launch_scan(p->scan_kw(), e, s, nullptr, wsp<double>(d_ws, p->o_ebk),
+                            wsp<double>(d_ws, p->o_bstk), st));
     HIPCHK(amx::launch_kw_tail(p->d_spans, p->n_tracks, s, e, p->d_tailpow, d_kw_tail, st));
     return AMX_OK;
 }
@@ -686,8 +741,8 @@ int amx_loudness_pass2(amx_plan *p, const int16_t *d_out, const double *d_kw_car
     double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
     double *parts = wsp<double>(d_ws, p->o_parts);
     int64_t *phop = wsp<int64_t>(d_ws, p->o_phop);
-    HIPCHK(amx::launch_scan(e, s, p->d_kseg_first, p->d_kseg_stream, p->n_kseg, AMX_KW_DIM, 2,
-                            p->d_Mpkw, p->lev_kw, d_kw_carry, st));
+    HIPCHK(amx::launch_scan(p->scan_kw(), e, s, d_kw_carry, wsp<double>(d_ws, p->o_ebk),
+                            wsp<double>(d_ws, p->o_bstk), st));
     HIPCHK(amx::launch_kw2(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, p->hop, d_out, s, parts, phop, st));
     HIPCHK(amx::launch_hops(p->d_spans, p->n_tracks, p->d_ksegs, p->Lkw, p->hop, parts, phop, d_hops,
                             max_hops, st));
