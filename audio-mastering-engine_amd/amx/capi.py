@@ -14,7 +14,10 @@ c_double_p = ctypes.POINTER(ctypes.c_double)
 c_float_p = ctypes.POINTER(ctypes.c_float)
 
 AMX_OK, AMX_EINVAL, AMX_EHIP, AMX_ENOMEM, AMX_ERANGE = 0, -1, -2, -3, -4
-ABI_VERSION = 1
+ABI_VERSION = 2
+CTL_FAST = 1
+MODES = ("off", "skip", "linear", "dynamic")
+STATS = 16
 STAGES = ("front1", "scan_eq", "front2", "scan_xo", "xover", "rms", "env", "fix", "apply")
 
 
@@ -52,6 +55,12 @@ class FinalDesc(ctypes.Structure):
                 ("pad_", ctypes.c_int32)]
 
 
+class DecideDesc(ctypes.Structure):
+    _fields_ = [("lufs_on", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("target_i", ctypes.c_double), ("target_tp", ctypes.c_double),
+                ("target_lra", ctypes.c_double)]
+
+
 class PlanInfo(ctypes.Structure):
     _fields_ = [("workspace_bytes", ctypes.c_int64), ("out_frames", ctypes.c_int64),
                 ("n_tracks", ctypes.c_int32), ("n_chunks", ctypes.c_int32),
@@ -71,7 +80,8 @@ EXPORTS = ("amx_abi_version", "amx_last_error", "amx_plan_create", "amx_plan_fre
            "amx_plan_get_info", "amx_plan_track_span", "amx_run_chunks", "amx_run_stage",
            "amx_loudness_pass1",
            "amx_kw_propagate", "amx_loudness_pass2", "amx_loudness_histograms",
-           "amx_limiter_geometry", "amx_finalize")
+           "amx_limiter_geometry", "amx_loudness_decide", "amx_kw_carry_setup", "amx_kw_carry",
+           "amx_finalize")
 
 _lib = None
 
@@ -104,8 +114,12 @@ def load(path=None):
     L.amx_loudness_histograms.argtypes = [vp, vp, ctypes.c_int64, vp, vp, vp, vp]
     L.amx_limiter_geometry.argtypes = [vp, ctypes.POINTER(FinalDesc), ctypes.POINTER(ctypes.c_int32),
                                        ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]
-    L.amx_finalize.argtypes = [vp, ctypes.POINTER(FinalDesc), vp, vp, ctypes.c_int32, vp, vp, vp,
-                               vp, vp]
+    L.amx_loudness_decide.argtypes = [vp, ctypes.POINTER(DecideDesc), ctypes.POINTER(FinalDesc),
+                                      vp, vp, vp, vp, vp, vp, vp]
+    L.amx_kw_carry_setup.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]
+    L.amx_kw_carry.argtypes = [vp, vp, vp, vp]
+    L.amx_finalize.argtypes = [vp, ctypes.POINTER(FinalDesc), vp, vp, vp, ctypes.c_int32, vp, vp,
+                               vp, vp, vp]
     if L.amx_abi_version() != ABI_VERSION:
         raise AmxError("libamx ABI version mismatch")
     _lib = L
@@ -128,7 +142,7 @@ def ptr(t):
 class Plan:
     """Owns an amx_plan*; see include/amx.h for the call contract."""
 
-    def __init__(self, desc, chunks, track_frame0=None, track_total=None, seg_frames=256):
+    def __init__(self, desc, chunks, track_frame0=None, track_total=None, seg_frames=128):
         L = load()
         arr = (Chunk * max(1, len(chunks)))()
         for i, (t, off, n) in enumerate(chunks):
@@ -157,6 +171,11 @@ class Plan:
         check(load().amx_kw_propagate(self.h, int(frames), a.ctypes.data_as(c_double_p),
                                       out.ctypes.data_as(c_double_p)), "amx_kw_propagate")
         return out
+
+    def kw_carry_setup(self, frames_after):
+        n = len(frames_after)
+        arr = (ctypes.c_int64 * max(1, n))(*[int(f) for f in frames_after])
+        check(load().amx_kw_carry_setup(self.h, n, arr), "amx_kw_carry_setup")
 
     def limiter_geometry(self, fd):
         bs, halo, sd = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()

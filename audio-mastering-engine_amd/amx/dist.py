@@ -8,7 +8,8 @@ exchange steps are the track-level ones:
 
 1. K-filter carry (loudnorm measurement is continuous over the concatenated
    track): all-gather each rank's zero-start tail state (8 doubles), then
-   carry(r) = sum_{q<r} A^{len_q+...} tail(q), chained on the host.
+   carry(r) = sum_{q<r} A^{frames between span q and span r} tail(q) on the device
+   (amx_kw_carry; the transition matrices are host-computed once per job).
 2. Loudness partials: RCCL all-reduce(SUM) of the whole-track 100 ms hop energy
    array (a hop spanning a rank boundary gets exactly two non-zero addends, so the
    sum is order-independent and bit-identical for any world size) and
@@ -17,6 +18,11 @@ exchange steps are the track-level ones:
 3. Limiter: all-gather of each rank's last B-1 frames (the look-ahead halo).  If
    the limiter can engage (peaks above the limit) its state is handed rank to rank
    with send/recv (sequential, rare path).
+
+Everything before the limiter runs on the stream without a host round trip; at
+N > 1 the host reads the one-word limiter decision (identical on every rank, it is
+computed from all-reduced data) to choose between the idle path and the
+sequential rank-to-rank chain.
 """
 import numpy as np
 import torch
@@ -62,7 +68,7 @@ class ShardedTrack:
     """This rank's part of one chunk-sharded track."""
 
     def __init__(self, sample_rate, channels_in, settings, track_frames, rank, world, *,
-                 quantum=None, input_s16=False, seg_frames=256, group=None):
+                 quantum=None, input_s16=False, seg_frames=128, group=None):
         self.rank, self.world, self.group = rank, world, group
         fs = int(sample_rate)
         if quantum is None:
@@ -84,15 +90,19 @@ class ShardedTrack:
                                 track_frame0=[self.tframe0], track_total=[self.ttotal],
                                 input_s16=input_s16, seg_frames=seg_frames)
         self.halo_all = None
+        if world > 1:
+            frames_after = [sum(self.span_frames[q + 1:rank]) for q in range(rank)]
+            self.job.plan.kw_carry_setup(frames_after)
+            self.tails_all = torch.zeros((world, 2, 4), dtype=torch.float64, device=self.job.device)
 
     # -------------------------------------------------------------- exchanges
     def exchange_carry(self):
         job = self.job
-        tails = [torch.empty_like(job.kw_tail) for _ in range(self.world)]
-        dist.all_gather(tails, job.kw_tail.contiguous(), group=self.group)
-        host = [t.reshape(-1)[:8].cpu().numpy() for t in tails]
-        c = carry_from_tails(host, self.span_frames, self.rank, job.plan.kw_propagate)
-        job.kw_carry.copy_(torch.from_numpy(c).reshape(job.kw_carry.shape))
+        dist.all_gather_into_tensor(self.tails_all, job.kw_tail.reshape(1, 2, 4).contiguous(),
+                                    group=self.group)
+        from . import capi
+        capi.check(capi.load().amx_kw_carry(job.plan.h, capi.ptr(self.tails_all), capi.ptr(job.kw_carry),
+                                            job._s(None)), "amx_kw_carry")
 
     def reduce_loudness(self):
         dist.all_reduce(self.job.hops, op=dist.ReduceOp.SUM, group=self.group)
@@ -121,38 +131,31 @@ class ShardedTrack:
     # -------------------------------------------------------------- the step
     def step(self, d_in):
         """One pass of the whole path over this rank's chunks (input resident)."""
+        from . import capi
         job = self.job
         job.run_chunks(d_in)
-        job.loudness_pass1()
-        lufs = job.settings.get("lufs")
+        job.timed("loud1", job.loudness_pass1)
+        lufs_on = job.dd.lufs_on
         if self.world > 1:
             self.exchange_carry()
-        if lufs is not None:
-            job.loudness_pass2(carry=self.world > 1)
+        if lufs_on:
+            job.timed("loud2", lambda: job.loudness_pass2(carry=self.world > 1))
         if self.world > 1:
-            if lufs is None:
-                dist.all_reduce(job.peak, op=dist.ReduceOp.MAX, group=self.group)
-            else:
-                self.reduce_loudness()
-        stats = None
-        if lufs is not None:
-            job.histograms()
-            stats = job.measure()
-            gains, modes = job.decide_gains(stats)
+            if lufs_on:
+                dist.all_reduce(job.hops, op=dist.ReduceOp.SUM, group=self.group)
+            dist.all_reduce(job.peak, op=dist.ReduceOp.MAX, group=self.group)
+        if lufs_on:
+            job.timed("hist", job.histograms)
+        job.timed("decide", job.decide)
+        if self.world == 1:
+            job.timed("final", lambda: job.finalize(None))
         else:
-            job._fetch(False)
-            gains, modes = [-1.0], ["off"]
-        job.set_gains(gains)
-        if self.world > 1:
             self.exchange_halo()
-        fast = job.fast_ok(gains)
-        if fast:
-            job.finalize(True)
-        elif self.world > 1:
-            job.lim_state.zero_()
-            self.limiter_sequential()
-        else:
-            job.lim_state.zero_()
-            job.finalize(False)
-        job.report = {"stats": stats, "modes": modes, "gains": gains, "limiter_fast": fast}
+            fast = bool(int(job.ctl[0].item()) & capi.CTL_FAST)   # same word on every rank
+            if fast:
+                job.timed("final", lambda: job.finalize(True))
+            else:
+                job.lim_state.zero_()
+                self.limiter_sequential()
+        job.report = {"chunks": len(job.chunks), "segments": job.info.n_segments}
         return job.y[:job.info.out_frames]

@@ -41,7 +41,7 @@ def final_desc(params=ALIMITER):
 
 class MasteringJob:
     def __init__(self, sample_rate, channels_in, settings, track_frames, *, quantum=None,
-                 input_s16=False, seg_frames=256, device=None, chunks=None, track_frame0=None,
+                 input_s16=False, seg_frames=128, device=None, chunks=None, track_frame0=None,
                  track_total=None, limiter=ALIMITER):
         if not torch.cuda.is_available():
             raise RuntimeError("amx needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -80,6 +80,14 @@ class MasteringJob:
         self.hist = torch.zeros((T, 1000), dtype=torch.int64, device=dev)
         self.st_hist = torch.zeros((T, 1000), dtype=torch.int64, device=dev)
         self.gains = torch.full((T,), -1.0, dtype=torch.float64, device=dev)
+        self.stats = torch.zeros((T, capi.STATS), dtype=torch.float64, device=dev)
+        self.ctl = torch.zeros((T,), dtype=torch.int32, device=dev)
+        self.dd = capi.DecideDesc()
+        lufs = self.settings.get("lufs")
+        self.dd.lufs_on = 0 if lufs is None else 1
+        self.dd.target_i = 0.0 if lufs is None else float(lufs)
+        self.dd.target_tp = LOUDNORM_TP
+        self.dd.target_lra = LOUDNORM_LRA
         self.fd = final_desc(limiter)
         self.limit = limiter["limit"]
         self.bs, self.halo_frames, self.state_doubles = self.plan.limiter_geometry(self.fd)
@@ -119,6 +127,20 @@ class MasteringJob:
             b.record(stream)
             ev.append((capi.STAGES[s], a, b))
 
+    def timed(self, name, fn, stream=None):
+        """Run fn() between two HIP events on the launch stream when stage timing is on
+        (self.stage_events is a list), else just run it."""
+        ev = getattr(self, "stage_events", None)
+        if ev is None:
+            return fn()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        r = fn()
+        b.record(stream)
+        ev.append((name, a, b))
+        return r
+
     def loudness_pass1(self, stream=None):
         capi.check(capi.load().amx_loudness_pass1(self.plan.h, capi.ptr(self.out), capi.ptr(self.kw_tail),
                                                   capi.ptr(self.peak), capi.ptr(self.ws), self._s(stream)),
@@ -137,87 +159,58 @@ class MasteringJob:
                                                        capi.ptr(self.ws), self._s(stream)),
                    "amx_loudness_histograms")
 
-    def finalize(self, fast, stream=None):
+    def decide(self, stream=None):
+        """loudnorm statistics, mode, gain and limiter path on the device (no sync)."""
+        lufs_on = self.dd.lufs_on
+        capi.check(capi.load().amx_loudness_decide(
+            self.plan.h, self.dd, self.fd, capi.ptr(self.hist) if lufs_on else None,
+            capi.ptr(self.st_hist) if lufs_on else None, capi.ptr(self.peak), capi.ptr(self.stats),
+            capi.ptr(self.gains), capi.ptr(self.ctl), self._s(stream)), "amx_loudness_decide")
+
+    def finalize(self, fast=None, stream=None):
+        """fast None: each track takes the limiter path amx_loudness_decide chose."""
+        ctl = capi.ptr(self.ctl) if fast is None else None
         capi.check(capi.load().amx_finalize(self.plan.h, self.fd, capi.ptr(self.out), capi.ptr(self.gains),
-                                            1 if fast else 0, capi.ptr(self.halo), capi.ptr(self.y),
+                                            ctl, 1 if fast else 0, capi.ptr(self.halo), capi.ptr(self.y),
                                             capi.ptr(self.lim_state), capi.ptr(self.ws), self._s(stream)),
                    "amx_finalize")
 
-    # ------------------------------------------------------------ host decisions
-    def _fetch(self, with_hist=True):
-        """One stream sync: histograms + peaks into pinned host buffers."""
-        if not hasattr(self, "_h_hist"):
-            self._h_hist = torch.empty(self.hist.shape, dtype=torch.int64, pin_memory=True)
-            self._h_st = torch.empty(self.st_hist.shape, dtype=torch.int64, pin_memory=True)
-            self._h_peak = torch.empty(self.peak.shape, dtype=torch.float64, pin_memory=True)
-            self._h_gains = torch.empty(self.gains.shape, dtype=torch.float64, pin_memory=True)
-        if with_hist:
-            self._h_hist.copy_(self.hist, non_blocking=True)
-            self._h_st.copy_(self.st_hist, non_blocking=True)
-        self._h_peak.copy_(self.peak, non_blocking=True)
-        torch.cuda.current_stream().synchronize()
-        self._peaks = self._h_peak.numpy().copy()
-
-    def measure(self):
-        """loudnorm pass-1 statistics per track from the device histograms (syncs)."""
-        self._fetch(True)
-        hist = self._h_hist.numpy().view(np.uint64)
-        st = self._h_st.numpy().view(np.uint64)
-        return [loudness.measure(hist[t], st[t], self._peaks[t]) for t in range(self.n_tracks)]
-
-    def set_gains(self, gains):
-        if not hasattr(self, "_h_gains"):
-            self._fetch(False)
-        self._h_gains.copy_(torch.tensor(gains, dtype=torch.float64))
-        self.gains.copy_(self._h_gains, non_blocking=True)
-
-    def decide_gains(self, stats):
-        lufs = self.settings.get("lufs")
-        gains, modes = [], []
-        for st in stats:
-            if lufs is None:
-                modes.append("off")
-                gains.append(-1.0)
-                continue
-            mode, g = loudness.linear_gain(st, float(lufs), LOUDNORM_TP, LOUDNORM_LRA)
-            if mode == "dynamic":
+    # ------------------------------------------------------------ report
+    def fetch_report(self, raise_dynamic=True):
+        """Synchronise and read the device decision back: loudnorm statistics as the
+        JSON strings ffmpeg prints, mode, gain, limiter path.  Raises
+        DynamicModeUnsupported when loudnorm would have used dynamic mode."""
+        st = self.stats.cpu().numpy()
+        stats, modes, gains, fast = [], [], [], []
+        for t in range(self.n_tracks):
+            row = st[t]
+            mode = capi.MODES[int(row[8])]
+            modes.append(mode)
+            gains.append(float(row[9]))
+            fast.append(bool(row[10]))
+            if self.dd.lufs_on:
+                stats.append({"input_i": loudness._fmt(row[4]), "input_tp": loudness._fmt(row[5]),
+                              "input_lra": loudness._fmt(row[6]), "input_thresh": loudness._fmt(row[7])})
+            if mode == "dynamic" and raise_dynamic:
                 raise DynamicModeUnsupported(
                     "loudnorm would use dynamic mode for these measurements %s; only linear "
-                    "mode is implemented (DESIGN.md: next rows)" % (st,))
-            modes.append(mode)
-            gains.append(g if mode == "linear" else -1.0)
-        return gains, modes
-
-    def fast_ok(self, gains):
-        if getattr(self, "_peaks", None) is None:
-            self._fetch(False)
-        peaks = self._peaks
-        self._peaks = None
-        for t in range(self.n_tracks):
-            m = float(peaks[t].max()) if peaks.shape[1] else 0.0
-            if loudness.max_after_gain(m, gains[t]) * self.fd.level_in > self.limit:
-                return False
-        return True
+                    "mode is implemented (DESIGN.md: next rows)" % (stats[-1],))
+        self.report.update({"stats": stats if self.dd.lufs_on else None, "modes": modes,
+                            "gains": gains, "limiter_fast": all(fast)})
+        return self.report
 
     def run(self, d_in, stream=None):
-        """Whole pipeline for whole tracks on this GPU; returns y (int16 [frames, 2])."""
+        """Whole pipeline for whole tracks on this GPU, fully on the stream (no host
+        round trip); returns y (int16 [frames, 2]).  fetch_report() reads the
+        loudness decision afterwards."""
         self.run_chunks(d_in, stream)
         self.loudness_pass1(stream)
-        lufs = self.settings.get("lufs")
-        stats = None
-        if lufs is not None:
+        if self.dd.lufs_on:
             self.loudness_pass2(stream, carry=False)
             self.histograms(stream)
-            stats = self.measure()
-            gains, modes = self.decide_gains(stats)
-        else:
-            self._fetch(False)
-            gains, modes = [-1.0] * self.n_tracks, ["off"] * self.n_tracks
-        self.set_gains(gains)
-        fast = self.fast_ok(gains)
-        self.finalize(fast, stream)
-        self.report = {"stats": stats, "modes": modes, "gains": gains, "limiter_fast": fast,
-                       "chunks": len(self.chunks), "segments": self.info.n_segments}
+        self.decide(stream)
+        self.finalize(None, stream)
+        self.report = {"chunks": len(self.chunks), "segments": self.info.n_segments}
         return self.y[:self.info.out_frames]
 
     def track_output(self, t):
@@ -225,7 +218,7 @@ class MasteringJob:
         return self.y[s.out_offset:s.out_offset + s.out_frames]
 
 
-def master_array(x, sample_rate, settings, *, quantum=None, seg_frames=256):
+def master_array(x, sample_rate, settings, *, quantum=None, seg_frames=128):
     """In-memory twin of master_audio: float32 [frames, C] (C = 1/2,
     any device) -> int16 [frames', 2] CUDA tensor (the 16-bit WAV the reference
     writes) and a report dict."""
@@ -241,5 +234,6 @@ def master_array(x, sample_rate, settings, *, quantum=None, seg_frames=256):
     job = MasteringJob(sample_rate, x.shape[1], settings, [x.shape[0]], quantum=quantum,
                        input_s16=s16, seg_frames=seg_frames)
     y = job.run(x)
+    job.fetch_report()
     job.report["job"] = job
     return y, job.report

@@ -69,23 +69,18 @@ def master_audio(settings, status_callback=None, progress_callback=None):
     progress(num_chunks + 1, total_steps)                                     # :206
     status("Concatenation complete.")                                         # :213
     job.loudness_pass1()
-    gains = [-1.0]
     if settings.get("lufs") is not None:                                      # :216
         status("Normalizing final loudness...")                               # :217
         progress(num_chunks + 2, total_steps)                                 # :218
         job.loudness_pass2(carry=False)
         job.histograms()
-        stats = job.measure()
-        gains, modes = job.decide_gains(stats)
-        if modes[0] == "skip":
-            logging.warning("Measured loudness is -inf (silent audio). Skipping normalization.")
-        job.report["stats"] = stats
+    job.decide()
+    report = job.fetch_report()          # raises DynamicModeUnsupported before any output
+    if report["modes"][0] == "skip":
+        logging.warning("Measured loudness is -inf (silent audio). Skipping normalization.")
     status("Applying final limiting and exporting...")                        # :221
     progress(num_chunks + 3, total_steps)                                     # :222
-    if settings.get("lufs") is None:
-        job._fetch(False)
-    job.set_gains(gains)
-    job.finalize(job.fast_ok(gains))
+    job.finalize(None)
     y = job.y[:job.info.out_frames].cpu().numpy()
     wavio.write_wav_s16(output_file, y, fs)
     progress(total_steps, total_steps)                                        # :224

@@ -16,38 +16,57 @@ __device__ __forceinline__ int16_t gain16(int16_t x, double g) {
     return clip_llrint(v * 32768.0);
 }
 
-// limiter never engages (host-proven max|x| <= limit): att == 1, delta == 0 for
-// every frame, so out[n] = level-scaled input[n - (B-1)] (B = ring frames).
+// limiter never engages (proved from the sample peak: max|gained x| <= limit):
+// att == 1, delta == 0 for every frame, so out[n] = level-scaled input[n - (B-1)]
+// (B = ring frames).  A workgroup covers AMX_BLOCK * FPT frames of one track span;
+// thread k handles frames k, k + AMX_BLOCK, ... so every load and store instruction
+// of a wave is one contiguous 256-B run, with FPT independent loads in flight.
+// ctl (nullable): per-track decision word of k_decide; this kernel only runs the
+// tracks whose AMX_CTL_FAST bit is set.
+#define AMX_FINAL_FPT 8
 __global__ void __launch_bounds__(AMX_BLOCK) k_final_fast(const SpanDev *__restrict__ spans,
                                                           const uint32_t *__restrict__ x,
                                                           const uint32_t *__restrict__ halo,
                                                           int halo_frames,
                                                           const double *__restrict__ gains,
+                                                          const int32_t *__restrict__ ctl,
                                                           double level_in, double level,
                                                           double level_out, double limit,
                                                           uint32_t *__restrict__ y) {
     const int t = blockIdx.y;
+    if (ctl && !(ctl[t] & AMX_CTL_FAST)) return;
     const SpanDev sp = spans[t];
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= sp.out_n) return;
-    const int64_t src = i - halo_frames;      // span-local source frame (delay B-1)
-    const int64_t tsrc = sp.tframe0 + src;   // whole-track source frame
-    uint32_t p = 0;
-    bool zero = tsrc < 0;
-    if (!zero) p = src >= 0 ? x[sp.out_off + src] : halo[(int64_t)t * halo_frames + (halo_frames + src)];
+    const int64_t i0 = (int64_t)blockIdx.x * (AMX_BLOCK * AMX_FINAL_FPT) + threadIdx.x;
+    if (i0 >= sp.out_n) return;
     const double g = gains[t];
-    int16_t o[2];
+    uint32_t p[AMX_FINAL_FPT];
 #pragma unroll
-    for (int c = 0; c < 2; c++) {
-        if (zero) { o[c] = 0; continue; }
-        int16_t v = gain16(c ? hi16(p) : lo16(p), g);
-        double smp = ((double)v * (1.0 / 32768.0)) * level_in;
-        double d = smp * 1.0;
-        d = d < -limit ? -limit : (d > limit ? limit : d);
-        d = d * level * level_out;
-        o[c] = clip_llrint(d * 32768.0);
+    for (int m = 0; m < AMX_FINAL_FPT; m++) {
+        const int64_t i = i0 + (int64_t)m * AMX_BLOCK;
+        const int64_t src = i - halo_frames;      // span-local source frame (delay B-1)
+        const int64_t cs = src < 0 ? 0 : (src >= sp.out_n ? sp.out_n - 1 : src);
+        // one unconditional load from a selected address (see tile_load): frames
+        // before the span come from the halo, frames before the track are silence
+        const uint32_t *a = src < 0 ? halo + (int64_t)t * halo_frames + (halo_frames + src)
+                                    : x + sp.out_off + cs;
+        const uint32_t v = *a;
+        p[m] = (sp.tframe0 + src < 0) ? 0u : v;
     }
-    y[sp.out_off + i] = pack2(o[0], o[1]);
+#pragma unroll
+    for (int m = 0; m < AMX_FINAL_FPT; m++) {
+        const int64_t i = i0 + (int64_t)m * AMX_BLOCK;
+        int16_t o[2];
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            int16_t v = gain16(c ? hi16(p[m]) : lo16(p[m]), g);
+            double smp = ((double)v * (1.0 / 32768.0)) * level_in;
+            double d = smp * 1.0;
+            d = d < -limit ? -limit : (d > limit ? limit : d);
+            d = d * level * level_out;
+            o[c] = clip_llrint(d * 32768.0);
+        }
+        if (i < sp.out_n) y[sp.out_off + i] = pack2(o[0], o[1]);
+    }
 }
 
 // General alimiter (af_alimiter.c filter_frame, asc off), one thread per track
@@ -60,9 +79,10 @@ __global__ void k_final_general(const SpanDev *__restrict__ spans, int n_tracks,
                                 const double *__restrict__ gains, int fs, double level_in,
                                 double level, double level_out, double limit, double release,
                                 int bs, double *__restrict__ state, int64_t state_doubles,
-                                uint32_t *__restrict__ y) {
+                                const int32_t *__restrict__ ctl, uint32_t *__restrict__ y) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_tracks) return;
+    if (ctl && (ctl[t] & AMX_CTL_FAST)) return;
     const SpanDev sp = spans[t];
     const int channels = 2;
     double *S = state + (int64_t)t * state_doubles;
@@ -163,15 +183,16 @@ __global__ void k_final_general(const SpanDev *__restrict__ spans, int n_tracks,
 // ---------------------------------------------------------------- launchers
 hipError_t launch_final_fast(const SpanDev *spans, int n_tracks, int64_t max_span,
                              const int16_t *x, const int16_t *halo, int halo_frames,
-                             const double *gains, double level_in, double level,
-                             double level_out, double limit, int16_t *y, hipStream_t st) {
-    dim3 g = grid1(max_span);
-    g.y = (unsigned)n_tracks;
+                             const double *gains, const int32_t *ctl, double level_in,
+                             double level, double level_out, double limit, int16_t *y,
+                             hipStream_t st) {
+    const int64_t per = (int64_t)AMX_BLOCK * AMX_FINAL_FPT;
+    dim3 g((unsigned)((max_span + per - 1) / per), (unsigned)n_tracks);
     if (empty(g)) return hipSuccess;
     hipLaunchKernelGGL(k_final_fast, g, dim3(AMX_BLOCK), 0, st, spans,
                        reinterpret_cast<const uint32_t *>(x),
-                       reinterpret_cast<const uint32_t *>(halo), halo_frames, gains, level_in,
-                       level, level_out, limit, reinterpret_cast<uint32_t *>(y));
+                       reinterpret_cast<const uint32_t *>(halo), halo_frames, gains, ctl,
+                       level_in, level, level_out, limit, reinterpret_cast<uint32_t *>(y));
     return hipGetLastError();
 }
 
@@ -179,14 +200,14 @@ hipError_t launch_final_general(const SpanDev *spans, int n_tracks, const int16_
                                 const int16_t *halo, int halo_frames, const double *gains,
                                 int fs, double level_in, double level, double level_out,
                                 double limit, double release, int buffer_size,
-                                double *state, int64_t state_doubles, int16_t *y,
-                                hipStream_t st) {
+                                double *state, int64_t state_doubles, const int32_t *ctl,
+                                int16_t *y, hipStream_t st) {
     if (n_tracks <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_final_general, dim3((n_tracks + 63) / 64), dim3(64), 0, st, spans,
                        n_tracks, reinterpret_cast<const uint32_t *>(x),
                        reinterpret_cast<const uint32_t *>(halo), halo_frames, gains, fs,
                        level_in, level, level_out, limit, release, buffer_size, state,
-                       state_doubles, reinterpret_cast<uint32_t *>(y));
+                       state_doubles, ctl, reinterpret_cast<uint32_t *>(y));
     return hipGetLastError();
 }
 

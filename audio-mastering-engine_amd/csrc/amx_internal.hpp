@@ -11,6 +11,8 @@
 #define AMX_HIST_BINS 1000
 #define AMX_TF_FRAMES 16  // LDS tile frames (AMX_TF in amx_dev.hpp)
 #define AMX_SCAN_S 16     // segments per scan block
+#define AMX_CTL_FAST 1    // k_decide control word: limiter provably idle
+#define AMX_STATS 16      // doubles per track written by k_decide
 #define AMX_EQC 64        // compact EQ coefficient block (see ChainDev::eqc)
 
 // One EQ stage of _apply_eq_to_channel (audio_mastering_engine.py:277-282).
@@ -137,14 +139,26 @@ hipError_t launch_hist(const SpanDev *spans, int n_tracks, int hop, const double
 // finalize
 hipError_t launch_final_fast(const SpanDev *spans, int n_tracks, int64_t max_span,
                              const int16_t *x, const int16_t *halo, int halo_frames,
-                             const double *gains, double level_in, double level,
-                             double level_out, double limit, int16_t *y, hipStream_t st);
+                             const double *gains, const int32_t *ctl, double level_in,
+                             double level, double level_out, double limit, int16_t *y,
+                             hipStream_t st);
 hipError_t launch_final_general(const SpanDev *spans, int n_tracks, const int16_t *x,
                                 const int16_t *halo, int halo_frames, const double *gains,
                                 int fs, double level_in, double level, double level_out,
                                 double limit, double release, int buffer_size,
-                                double *state, int64_t state_doubles, int16_t *y,
-                                hipStream_t st);
+                                double *state, int64_t state_doubles, const int32_t *ctl,
+                                int16_t *y, hipStream_t st);
+struct DecideArgs {
+    int n_tracks, lufs_on;
+    const unsigned long long *hist, *st_hist;
+    const double *peak, *energies, *bounds;
+    double target_i, target_tp, target_lra, level_in, limit;
+    double *stats, *gains;
+    int32_t *ctl;
+};
+hipError_t launch_decide(const DecideArgs &a, hipStream_t st);
+hipError_t launch_kw_carry(const double *tails, const double *P, int n_prev, double *carry,
+                           hipStream_t st);
 hipError_t launch_kw_tail(const SpanDev *spans, int n_tracks, const double *s, const double *e,
                           const double *P, double *tail, hipStream_t st);
 }  // namespace amx

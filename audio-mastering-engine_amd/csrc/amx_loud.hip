@@ -280,5 +280,176 @@ hipError_t launch_kw_tail(const SpanDev *spans, int n_tracks, const double *s, c
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ decision
+// loudnorm pass-1 statistics and the pass-2 linear-mode decision (af_loudnorm
+// init, audio_mastering_engine.py:229-242), the gain, and whether the final
+// alimiter can engage -- on the device, so a step needs no host round trip.
+// The arithmetic is amx/loudness.py's (libebur128 loop orders): one wave per track;
+// non-empty histogram bins are compacted in ascending order (adding an empty bin's
+// 0.0 is exact) and lane 0 runs the sequential double sums over them.
+
+// "%.2f" then float(): the exact decimal rounding (half-even on exact ties) of v
+__device__ double round2(double v) {
+    if (!isfinite(v)) return v;
+    const double p = v * 100.0;
+    const double err = fma(v, 100.0, -p);        // v*100 == p + err exactly
+    double k = rint(p);
+    if (fabs(p - k) == 0.5 && err != 0.0) k = err > 0.0 ? floor(p) + 1.0 : floor(p);
+    return k / 100.0;
+}
+
+__device__ __forceinline__ double lufs_of(double e) { return 10 * log10(e) - 0.691; }
+
+__device__ int compact_bins(const unsigned long long *h, short *nz) {
+    const int lane = threadIdx.x;
+    int n = 0;
+    for (int base = 0; base < AMX_HIST_BINS; base += 64) {
+        const int j = base + lane;
+        const unsigned long long v = j < AMX_HIST_BINS ? h[j] : 0ull;
+        const unsigned long long m = __ballot(v != 0ull);
+        const int pos = __popcll(m & ((1ull << lane) - 1ull));
+        if (v) nz[n + pos] = (short)j;
+        n += __popcll(m);
+    }
+    __syncthreads();
+    return n;
+}
+
+__global__ void __launch_bounds__(64) k_decide(DecideArgs a) {
+    __shared__ short nz[AMX_HIST_BINS];
+    const int t = blockIdx.x;
+    const unsigned long long *H = a.hist + (int64_t)t * AMX_HIST_BINS;
+    const unsigned long long *S = a.st_hist + (int64_t)t * AMX_HIST_BINS;
+    const double *E = a.energies;
+    double I = -INFINITY, thr = -70.0, lra = 0.0;
+    if (a.lufs_on) {
+        const int n = compact_bins(H, nz);
+        if (threadIdx.x == 0) {
+            double rel = 0.0;
+            unsigned long long cnt = 0;
+            for (int q = 0; q < n; q++) {
+                const int j = nz[q];
+                rel += (double)H[j] * E[j];
+                cnt += H[j];
+            }
+            if (cnt) {
+                rel /= (double)cnt;
+                rel *= 0.1;                            // pow(10, -10/10)
+                thr = lufs_of(rel);
+                int start;
+                if (rel < a.bounds[0]) start = 0;
+                else {
+                    start = find_bin(a.bounds, rel);
+                    if (rel > E[start]) ++start;
+                }
+                double g = 0.0;
+                unsigned long long above = 0;
+                for (int q = 0; q < n; q++) {
+                    const int j = nz[q];
+                    if (j < start) continue;
+                    g += (double)H[j] * E[j];
+                    above += H[j];
+                }
+                if (above) I = lufs_of(g / (double)above);
+            }
+        }
+        __syncthreads();
+        const int m = compact_bins(S, nz);
+        if (threadIdx.x == 0) {
+            double size = 0.0, power = 0.0;
+            for (int q = 0; q < m; q++) {
+                const int j = nz[q];
+                size += (double)S[j];
+                power += (double)S[j] * E[j];
+            }
+            if (size != 0.0) {
+                power /= size;
+                const double integ = 0.01 * power;      // pow(10, -20/10)
+                int index;
+                if (integ < a.bounds[0]) index = 0;
+                else {
+                    index = find_bin(a.bounds, integ);
+                    if (integ > E[index]) ++index;
+                }
+                size = 0.0;
+                int q0 = 0;
+                while (q0 < m && nz[q0] < index) q0++;
+                for (int q = q0; q < m; q++) size += (double)S[nz[q]];
+                if (size != 0.0) {
+                    const double plo = (double)(int64_t)((size - 1) * 0.1 + 0.5);
+                    const double phi = (double)(int64_t)((size - 1) * 0.95 + 0.5);
+                    double acc = 0.0;
+                    int q = q0, last = index;
+                    while (acc <= plo) { last = nz[q]; acc += (double)S[nz[q]]; q++; }
+                    const double l_en = E[last];
+                    while (acc <= phi) { last = nz[q]; acc += (double)S[nz[q]]; q++; }
+                    const double h_en = E[last];
+                    lra = lufs_of(h_en) - lufs_of(l_en);
+                }
+            }
+        }
+    }
+    if (threadIdx.x != 0) return;
+    const double pk = fmax(a.peak[2 * t], a.peak[2 * t + 1]);
+    const double tp = pk > 0.0 ? 20.0 * log10(pk) : -INFINITY;
+    const double si = round2(I), stp = round2(tp), slra = round2(lra), sthr = round2(thr);
+    int mode = 0;                                   // 0 off, 1 skip, 2 linear, 3 dynamic
+    double gain = -1.0;
+    if (a.lufs_on) {
+        if (si == -INFINITY) mode = 1;
+        else {
+            const double offset = a.target_i - si;
+            const double offset_tp = stp + offset;
+            if (stp != 99 && sthr != -70 && slra != 0 && si != 0 && offset_tp <= a.target_tp &&
+                slra <= a.target_lra) {
+                mode = 2;
+                gain = pow(10.0, offset / 20.0);
+            } else {
+                mode = 3;
+            }
+        }
+    }
+    // max |sample| after the gain stage (llrint(x*g) clipped), the limiter's input
+    const double m16 = rint(pk * 32768.0);
+    double amax = m16 / 32768.0;
+    if (gain > 0.0) amax = fmin(rint(((m16 * (1.0 / 32768.0)) * gain) * 32768.0), 32768.0) / 32768.0;
+    const bool fast = amax * a.level_in <= a.limit;
+    double *o = a.stats + (int64_t)t * AMX_STATS;
+    o[0] = I; o[1] = lra; o[2] = thr; o[3] = tp;
+    o[4] = si; o[5] = stp; o[6] = slra; o[7] = sthr;
+    o[8] = (double)mode; o[9] = gain; o[10] = fast ? 1.0 : 0.0; o[11] = pk;
+    a.gains[t] = gain;
+    a.ctl[t] = (fast ? AMX_CTL_FAST : 0) | (mode << 4);
+}
+
+hipError_t launch_decide(const DecideArgs &a, hipStream_t st) {
+    if (a.n_tracks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_decide, dim3(a.n_tracks), dim3(64), 0, st, a);
+    return hipGetLastError();
+}
+
+// K-filter state entering this rank's span from the other ranks' zero-start tails:
+// carry = sum_q P_q tail_q (P_q = A^{frames between span q's end and this span},
+// host-computed), per channel; one thread per (channel, row).
+__global__ void k_kw_carry(const double *__restrict__ tails, const double *__restrict__ P,
+                           int n_prev, double *__restrict__ carry) {
+    const int c = threadIdx.x / AMX_KW_DIM, i = threadIdx.x % AMX_KW_DIM;
+    if (c >= 2) return;
+    double acc = 0.0;
+    for (int q = 0; q < n_prev; q++) {
+        const double *Pq = P + (int64_t)q * AMX_KW_DIM * AMX_KW_DIM;
+        const double *tq = tails + ((int64_t)q * 2 + c) * AMX_KW_DIM;
+#pragma unroll
+        for (int k = 0; k < AMX_KW_DIM; k++) acc = fma(Pq[i * AMX_KW_DIM + k], tq[k], acc);
+    }
+    carry[c * AMX_KW_DIM + i] = acc;
+}
+
+hipError_t launch_kw_carry(const double *tails, const double *P, int n_prev, double *carry,
+                           hipStream_t st) {
+    hipLaunchKernelGGL(k_kw_carry, dim3(1), dim3(64), 0, st, tails, P, n_prev, carry);
+    return hipGetLastError();
+}
+
 }  // namespace amx
 

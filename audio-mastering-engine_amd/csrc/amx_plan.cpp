@@ -168,7 +168,9 @@ struct amx_plan {
     double *d_G = nullptr, *d_M = nullptr, *d_Mp = nullptr;
     double *d_Gx = nullptr, *d_Mx = nullptr, *d_Mpx = nullptr;
     double *d_Gkw = nullptr, *d_Mkw = nullptr, *d_Mpkw = nullptr;
-    double *d_tabs = nullptr, *d_bounds = nullptr;
+    double *d_tabs = nullptr, *d_bounds = nullptr, *d_energies = nullptr;
+    double *d_carryP = nullptr;
+    int n_prev = 0;
     double *d_tailpow = nullptr;
     float *d_lut = nullptr;
     // workspace offsets
@@ -527,9 +529,10 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         }
     }
     // histogram boundaries (libebur128 init_histogram)
-    double bounds[1001];
+    double bounds[1001], energies[1000];
     bounds[0] = std::pow(10.0, (-70.0 + 0.691) / 10.0);
     for (int i = 1; i < 1001; ++i) bounds[i] = std::pow(10.0, ((double)i / 10.0 - 70.0 + 0.691) / 10.0);
+    for (int i = 0; i < 1000; ++i) energies[i] = std::pow(10.0, ((double)i / 10.0 - 69.95 + 0.691) / 10.0);
 
     // ------------------------------------------------------- upload
     int rc = AMX_OK;
@@ -557,6 +560,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     UP(p->d_Mpkw, Mpkw.data(), Mpkw.size());
     UP(p->d_tabs, tabs.data(), tabs.size());
     UP(p->d_bounds, bounds, 1001);
+    UP(p->d_energies, energies, 1000);
     UP(p->d_tailpow, p->tail_pow.data(), p->tail_pow.size());
     if (desc->tanh_lut) UP(p->d_lut, desc->tanh_lut, 65536);
 #undef UP
@@ -599,7 +603,7 @@ void amx_plan_free(amx_plan *p) {
     void *ptrs[] = {p->d_cd,  p->d_chunks, p->d_segs, p->d_ksegs, p->d_spans,  p->d_blks,
                     p->d_kblks, p->d_n1,   p->d_G,    p->d_M,     p->d_Mp,     p->d_Gx,
                     p->d_Mx,  p->d_Mpx,    p->d_Gkw,  p->d_Mkw,   p->d_Mpkw,   p->d_tabs,
-                    p->d_bounds, p->d_tailpow, p->d_lut};
+                    p->d_bounds, p->d_tailpow, p->d_lut, p->d_energies, p->d_carryP};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     delete p;
@@ -777,9 +781,59 @@ int amx_limiter_geometry(const amx_plan *p, const amx_final_desc *fd, int32_t *b
     return AMX_OK;
 }
 
+int amx_loudness_decide(amx_plan *p, const amx_decide_desc *dd, const amx_final_desc *fd,
+                        const uint64_t *d_hist, const uint64_t *d_st_hist, const double *d_peak,
+                        double *d_stats, double *d_gains, int32_t *d_ctl, void *stream) {
+    if (!p || !dd || !fd || !d_peak || !d_stats || !d_gains || !d_ctl ||
+        (dd->lufs_on && (!d_hist || !d_st_hist)))
+        return fail(AMX_EINVAL, "null argument");
+    amx::DecideArgs a{};
+    a.n_tracks = p->n_tracks;
+    a.lufs_on = dd->lufs_on ? 1 : 0;
+    a.hist = reinterpret_cast<const unsigned long long *>(d_hist);
+    a.st_hist = reinterpret_cast<const unsigned long long *>(d_st_hist);
+    a.peak = d_peak;
+    a.energies = p->d_energies;
+    a.bounds = p->d_bounds;
+    a.target_i = dd->target_i;
+    a.target_tp = dd->target_tp;
+    a.target_lra = dd->target_lra;
+    a.level_in = fd->level_in;
+    a.limit = fd->limit;
+    a.stats = d_stats;
+    a.gains = d_gains;
+    a.ctl = d_ctl;
+    HIPCHK(amx::launch_decide(a, (hipStream_t)stream));
+    return AMX_OK;
+}
+
+int amx_kw_carry_setup(amx_plan *p, int32_t n_prev, const int64_t *frames_after) {
+    if (!p || n_prev < 0 || (n_prev > 0 && !frames_after)) return fail(AMX_EINVAL, "bad argument");
+    std::vector<double> P((size_t)(n_prev > 0 ? n_prev : 1) * 16, 0.0);
+    for (int q = 0; q < n_prev; q++) {
+        if (frames_after[q] < 0) return fail(AMX_EINVAL, "frames_after[%d] < 0", q);
+        Mat m = matpow(p->kw_model.A, frames_after[q], AMX_KW_DIM);
+        for (int k = 0; k < 16; k++) P[(size_t)q * 16 + k] = m[k];
+    }
+    if (p->d_carryP) (void)hipFree(p->d_carryP);
+    p->d_carryP = nullptr;
+    int rc = upload(&p->d_carryP, P.data(), P.size());
+    if (rc) return rc;
+    p->n_prev = n_prev;
+    return AMX_OK;
+}
+
+int amx_kw_carry(amx_plan *p, const double *d_tails, double *d_carry, void *stream) {
+    if (!p || !d_carry || (p->n_prev > 0 && !d_tails)) return fail(AMX_EINVAL, "null argument");
+    if (!p->d_carryP) return fail(AMX_EINVAL, "amx_kw_carry: call amx_kw_carry_setup first");
+    HIPCHK(amx::launch_kw_carry(d_tails, p->d_carryP, p->n_prev, d_carry, (hipStream_t)stream));
+    return AMX_OK;
+}
+
 int amx_finalize(amx_plan *p, const amx_final_desc *fd, const int16_t *d_x,
-                 const double *d_gains, int32_t fast, const int16_t *d_halo, int16_t *d_y,
-                 double *d_lim_state, void *d_ws, void *stream) {
+                 const double *d_gains, const int32_t *d_ctl, int32_t fast,
+                 const int16_t *d_halo, int16_t *d_y, double *d_lim_state, void *d_ws,
+                 void *stream) {
     (void)d_ws;
     if (!p || !fd || !d_gains || (p->out_frames > 0 && (!d_x || !d_y)))
         return fail(AMX_EINVAL, "null argument");
@@ -790,15 +844,17 @@ int amx_finalize(amx_plan *p, const amx_final_desc *fd, const int16_t *d_x,
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     const double level = fd->auto_level ? 1 / fd->limit : 1;
-    if (fast) {
+    if (d_ctl || fast) {
         HIPCHK(amx::launch_final_fast(p->d_spans, p->n_tracks, p->max_span, d_x, d_halo, halo,
-                                      d_gains, fd->level_in, level, fd->level_out, fd->limit,
-                                      d_y, st));
-    } else {
+                                      d_gains, d_ctl, fd->level_in, level, fd->level_out,
+                                      fd->limit, d_y, st));
+    }
+    if (d_ctl || !fast) {
         if (!d_lim_state) return fail(AMX_EINVAL, "general limiter needs d_lim_state");
         HIPCHK(amx::launch_final_general(p->d_spans, p->n_tracks, d_x, d_halo, halo, d_gains,
                                          p->cd.fs, fd->level_in, level, fd->level_out, fd->limit,
-                                         fd->release_ms / 1000.0, bs, d_lim_state, sd, d_y, st));
+                                         fd->release_ms / 1000.0, bs, d_lim_state, sd, d_ctl,
+                                         d_y, st));
     }
     return AMX_OK;
 }

@@ -43,7 +43,7 @@ extern "C" {
 #define AMX_ENOMEM -3     /* host allocation failed */
 #define AMX_ERANGE -4     /* a size or filter is outside what the plan supports */
 
-#define AMX_ABI_VERSION 1
+#define AMX_ABI_VERSION 2
 
 #if defined(__GNUC__)
 #define AMX_API __attribute__((visibility("default")))
@@ -193,16 +193,45 @@ AMX_API int amx_loudness_histograms(amx_plan *plan, const double *d_hops, int64_
  * doubles per track for the general path. */
 AMX_API int amx_limiter_geometry(const amx_plan *plan, const amx_final_desc *fd, int32_t *buffer_size,
                          int32_t *halo_frames, int64_t *state_doubles);
+/* Loudnorm decision on the device (af_loudnorm pass-1 statistics + pass-2 mode,
+ * :229-242): per track, from the histograms and sample peak:
+ *   d_stats [n_tracks][16] doubles: I, LRA, thresh, TP(dB), the same four after
+ *     ffmpeg's "%.2f" print + parse, mode (0 off, 1 skip = silent, 2 linear,
+ *     3 dynamic = unsupported), gain, limiter-idle flag, sample peak;
+ *   d_gains [n_tracks]: the linear gain, or -1 (no normalisation);
+ *   d_ctl [n_tracks] int32: bit 0 = limiter provably idle (AMX_CTL_FAST), bits 4..7
+ *     mode -- consumed by amx_finalize without a host round trip.
+ * lufs_on = 0 (settings lufs None, :216) only computes the limiter flag. */
+typedef struct amx_decide_desc {
+    int32_t lufs_on, pad_;
+    double target_i;              /* settings['lufs'] */
+    double target_tp;             /* loudnorm TP=-1.5 (:229) */
+    double target_lra;            /* loudnorm LRA=11 */
+} amx_decide_desc;
+#define AMX_CTL_FAST 1
+AMX_API int amx_loudness_decide(amx_plan *plan, const amx_decide_desc *dd, const amx_final_desc *fd,
+                                const uint64_t *d_hist, const uint64_t *d_st_hist, const double *d_peak,
+                                double *d_stats, double *d_gains, int32_t *d_ctl, void *stream);
+
+/* Chunk-sharded tracks: K-filter state entering this plan's (single) span from the
+ * zero-start tails of the n_prev spans before it.  Setup (host, once): frames_after[q]
+ * = frames between the end of span q and the start of this span.  Then, on the
+ * stream: d_carry [2][4] = sum_q A^{frames_after[q]} d_tails[q] (d_tails [n_prev][2][4]). */
+AMX_API int amx_kw_carry_setup(amx_plan *plan, int32_t n_prev, const int64_t *frames_after);
+AMX_API int amx_kw_carry(amx_plan *plan, const double *d_tails, double *d_carry, void *stream);
+
 /* Finalize: loudnorm linear gain (d_gains[t] <= 0 -> no normalisation, :216) then
  * alimiter (:223) -> d_y int16 [out_frames, 2] (same frame indexing as d_x).
  * d_halo [n_tracks][halo_frames][2]: the input frames preceding each span (ignored
- * for spans that start their track).  fast != 0: host proved max|gained sample| <=
- * limit, so the limiter never engages and is an exact delay + level.  Otherwise the
- * sequential limiter runs; d_lim_state [n_tracks][state_doubles] carries its state
+ * for spans that start their track).  Limiter path per track: with d_ctl (from
+ * amx_loudness_decide) each track takes the path its AMX_CTL_FAST bit selects, on the
+ * device; with d_ctl NULL, fast != 0 selects the idle path for every track.  The idle
+ * path (max|gained sample| <= limit) is an exact delay + level; otherwise the
+ * sequential limiter runs, and d_lim_state [n_tracks][state_doubles] carries its state
  * in (span not starting the track) and out (span end). */
 AMX_API int amx_finalize(amx_plan *plan, const amx_final_desc *fd, const int16_t *d_x,
-                 const double *d_gains, int32_t fast, const int16_t *d_halo, int16_t *d_y,
-                 double *d_lim_state, void *d_ws, void *stream);
+                 const double *d_gains, const int32_t *d_ctl, int32_t fast, const int16_t *d_halo,
+                 int16_t *d_y, double *d_lim_state, void *d_ws, void *stream);
 
 #ifdef __cplusplus
 }
