@@ -68,9 +68,12 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_front1(const ChainDev *__restrict
 #pragma unroll
     for (int d = 0; d < D; d++) { e0[d] = 0.0; e1[d] = 0.0; }
     __syncthreads();
+    TileRegs<WIN> R;
+    tile_fetch<WIN>(R, in, rb_in, nullptr, rl, 0);
     for (int k = 0; k < L; k += AMX_TF) {
-        tile_load<WIN>(s_in, in, rb_in, nullptr, rl, k);
+        tile_put<WIN>(s_in, R, nullptr, rl, k);
         __syncthreads();
+        if (k + AMX_TF < L) tile_fetch<WIN>(R, in, rb_in, nullptr, rl, k + AMX_TF);
         const uint32_t *row = s_in + t * Tile<WIN>::PITCH;
         uint32_t *orow = s_out + t * Tile<1>::PITCH;
 #pragma unroll 2
@@ -104,13 +107,15 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_front1(const ChainDev *__restrict
 
 // ------------------------------------------- pass 2: EQ from true state -> int16
 // One thread per (segment, channel): lanes 2i / 2i+1 are the L / R channel of row
-// i, so the recursion's dependent FMA chains spread over twice the lanes.  The
-// stage coefficients live in VGPRs (copied once through LDS: scalar registers
-// cannot hold ~54 doubles without spilling).  Width couples the channels: the
-// pair exchanges its float32 EQ output with one DPP swap per frame.
+// i.  The EQ runs stage-major over sub-tiles of AMX_EQ_F frames (eq_tile), so only
+// one stage's coefficients and a few frames are live: ~90 VGPRs, 5 waves/SIMD to
+// cover the fp64 recursion latency.  Width couples the channels: the pair
+// exchanges its float32 EQ output with one DPP swap per frame.  Tiles are fetched
+// one ahead (tile_fetch / tile_put).
 // MB: also accumulate the crossover's zero-state end state (GEMV) for its scan.
+#define AMX_EQ_F 8
 template <int MASK, bool MB>
-__global__ void __launch_bounds__(AMX_BLOCK) k_front2(const ChainDev *__restrict__ cdp,
+__global__ void __launch_bounds__(AMX_BLOCK, MB ? 4 : 5) k_front2(const ChainDev *__restrict__ cdp,
                                                       const ChunkDev *__restrict__ chunks,
                                                       const SegDev *__restrict__ segs, int n_seg,
                                                       int L, const uint32_t *__restrict__ a16,
@@ -118,18 +123,16 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_front2(const ChainDev *__restrict
                                                       uint32_t *__restrict__ dst, int to_out,
                                                       const double *__restrict__ Gx,
                                                       double *__restrict__ e_x) {
-    constexpr int D = EqDim<MASK>::v, NQ = EqQ<MASK>::n;
+    constexpr int D = EqDim<MASK>::v;
     constexpr int ROWS = AMX_BLOCK / 2;
     using T = Tile<1, ROWS>;
     __shared__ uint32_t s_in[T::WORDS];
     __shared__ uint32_t s_out[T::WORDS];
     __shared__ int64_t rb_in[ROWS], rb_out[ROWS];
     __shared__ int rl[ROWS];
-    __shared__ double s_q[AMX_EQC];
     const ChainDev &cd = *cdp;
     const int t = threadIdx.x, row = t >> 1, chn = t & 1;
     const int j = blockIdx.x * ROWS + row;
-    if (t < AMX_EQC) s_q[t] = cd.eqc[t];
     bool need_x = false;
     if (chn == 0) {
         rb_in[row] = 0;
@@ -154,6 +157,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_front2(const ChainDev *__restrict
             for (int d = 0; d < D; d++) z[d] = s[d];
         }
     }
+    EqState est;
+    eq_state_load<MASK>(est, z);
     double xv[MB ? AMX_XO_DIM : 1];
 #pragma unroll
     for (int d = 0; d < (MB ? AMX_XO_DIM : 1); d++) xv[d] = 0.0;
@@ -161,33 +166,45 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_front2(const ChainDev *__restrict
     const float w = cd.width;
     const int won = cd.width_on;
     __syncthreads();
-    double q[NQ > 0 ? NQ : 1];
-#pragma unroll
-    for (int i = 0; i < NQ; i++) q[i] = s_q[i];
+    TileRegs<1, ROWS> R;
+    tile_fetch<1, ROWS>(R, a16, rb_in, nullptr, rl, 0);
     for (int k = 0; k < L; k += AMX_TF) {
-        tile_load<1, ROWS>(s_in, a16, rb_in, nullptr, rl, k);
+        tile_put<1, ROWS>(s_in, R, nullptr, rl, k);
         __syncthreads();
+        if (k + AMX_TF < L) tile_fetch<1, ROWS>(R, a16, rb_in, nullptr, rl, k + AMX_TF);
         const uint32_t *rp = s_in + row * T::PITCH;
         uint32_t *op = s_out + row * T::PITCH;
-#pragma unroll 4
-        for (int f = 0; f < AMX_TF; f++) {
-            const uint32_t p = rp[f];
-            float x = (float)(chn ? hi16(p) : lo16(p)) / 32768.0f;
-            x = eq_chain<MASK>(negm, q, z, x);
-            if (won) {
-                const float o = pair_swap(x);
-                float l = chn ? o : x, r = chn ? x : o;
-                width_frame(w, l, r);
-                x = chn ? r : l;
-            }
-            const int16_t qv = f32_to_s16(x);
-            const int other = __builtin_amdgcn_update_dpp(0, (int)qv, 0xB1, 0xF, 0xF, false);
-            if (chn == 0) op[f] = pack2(qv, (int16_t)other);
-            if constexpr (MB) {
-                const double *g = Gx + (int64_t)(k + f) * AMX_XO_DIM;
-                const double xd = (double)((float)qv / 32768.0f);
+#pragma unroll 1
+        for (int f0 = 0; f0 < AMX_TF; f0 += AMX_EQ_F) {
+            float xf[AMX_EQ_F];
+            double x[AMX_EQ_F];
 #pragma unroll
-                for (int d = 0; d < AMX_XO_DIM; d++) xv[d] = fma(g[d], xd, xv[d]);
+            for (int f = 0; f < AMX_EQ_F; f++) {
+                const uint32_t p = rp[f0 + f];
+                xf[f] = (float)(chn ? hi16(p) : lo16(p)) / 32768.0f;
+                x[f] = (double)xf[f];
+            }
+            // cd.pad0_ == 0: the offset makes the coefficient address depend on the
+            // loop, so the scalar loads stay per tile (no hoisting, no SGPR spill)
+            eq_tile<MASK, AMX_EQ_F>(negm, cd.eqc + (f0 & cd.pad0_), est, x, xf);
+#pragma unroll 2
+            for (int f = 0; f < AMX_EQ_F; f++) {
+                float v = MASK ? (float)x[f] : xf[f];
+                if (won) {
+                    const float o = pair_swap(v);
+                    float l = chn ? o : v, r = chn ? v : o;
+                    width_frame(w, l, r);
+                    v = chn ? r : l;
+                }
+                const int16_t qv = f32_to_s16(v);
+                const int other = __builtin_amdgcn_update_dpp(0, (int)qv, 0xB1, 0xF, 0xF, false);
+                if (chn == 0) op[f0 + f] = pack2(qv, (int16_t)other);
+                if constexpr (MB) {
+                    const double *g = Gx + (int64_t)(k + f0 + f) * AMX_XO_DIM;
+                    const double xd = (double)((float)qv / 32768.0f);
+#pragma unroll
+                    for (int d = 0; d < AMX_XO_DIM; d++) xv[d] = fma(g[d], xd, xv[d]);
+                }
             }
         }
         __syncthreads();

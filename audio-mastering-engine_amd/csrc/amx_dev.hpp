@@ -131,6 +131,91 @@ __device__ __forceinline__ float eq_chain(int negm, const double *q, double *z, 
     return (float)x;
 }
 
+// Stage-major form of eq_chain over F frames of one channel (amx_chain.hip k_front2):
+// each stage runs over all F frames before the next, so only that stage's
+// coefficients are live, as SGPR operands of the FMAs.  The two peak stages share
+// one loop body (`#pragma unroll 1`) over a per-iteration coefficient address, with
+// their 8-double states swapped between iterations; otherwise the compiler hoists
+// and merges every stage's scalar loads (~54 doubles > the SGPR file) and spills.
+// Inside a stage the unrolled section x frame grid is one basic block, so section
+// k+1 of frame f overlaps section k of frame f+1.
+struct EqState {
+    double s0[2], pa[8], pb[8], s3[2];
+};
+
+template <int MASK>
+__device__ __forceinline__ void eq_state_load(EqState &st, const double *z) {
+    int o = 0;
+    if constexpr ((MASK & 1) != 0) { st.s0[0] = z[0]; st.s0[1] = z[1]; o = 2; }
+    if constexpr ((MASK & 2) != 0) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) st.pa[i] = z[o + i];
+        o += 8;
+    }
+    if constexpr ((MASK & 4) != 0) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            if constexpr ((MASK & 2) != 0) st.pb[i] = z[o + i];
+            else st.pa[i] = z[o + i];
+        }
+        o += 8;
+    }
+    if constexpr ((MASK & 8) != 0) { st.s3[0] = z[o]; st.s3[1] = z[o + 1]; }
+}
+
+template <int MASK, int F>
+__device__ __forceinline__ void eq_tile(int negm, const double *__restrict__ sq, EqState &st,
+                                        double *x, const float *xf) {
+    constexpr int NP = ((MASK >> 1) & 1) + ((MASK >> 2) & 1);
+    int c = 0;
+    if constexpr ((MASK & 1) != 0) {
+        double q[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) q[i] = sq[i];
+#pragma unroll
+        for (int f = 0; f < F; f++) {
+            const double y = bq_step(q, st.s0[0], st.s0[1], x[f]);
+            if (!(negm & 1)) x[f] = x[f] + (y - x[f]) * q[5];
+            else { const double xg = (double)(xf[f] * (float)q[5]); x[f] = xg + (y - xg); }
+        }
+        c = 6;
+    }
+    if constexpr (NP > 0) {
+#pragma unroll 1
+        for (int sidx = 0; sidx < NP; sidx++) {
+            const double *q = sq + c + 21 * sidx;
+            double b[F];
+#pragma unroll
+            for (int f = 0; f < F; f++) b[f] = x[f];
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+#pragma unroll
+                for (int f = 0; f < F; f++)
+                    b[f] = bq_step(q + 5 * k, st.pa[2 * k], st.pa[2 * k + 1], b[f]);
+            const double gm1 = q[20];
+#pragma unroll
+            for (int f = 0; f < F; f++) x[f] = x[f] + b[f] * gm1;
+            if constexpr (NP == 2) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) { const double tmp = st.pa[i]; st.pa[i] = st.pb[i]; st.pb[i] = tmp; }
+            }
+        }
+        c += 21 * NP;
+    }
+    if constexpr ((MASK & 8) != 0) {
+        double q[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) q[i] = sq[c + i];
+#pragma unroll
+        for (int f = 0; f < F; f++) {
+            const double y = bq_step(q, st.s3[0], st.s3[1], x[f]);
+            if (!(negm & 8)) x[f] = x[f] + (y - x[f]) * q[5];
+            else if constexpr ((MASK & 7) == 0) { const double xg = (double)(xf[f] * (float)q[5]); x[f] = xg + (y - xg); }
+            else { const double xg = x[f] * q[5]; x[f] = xg + (y - xg); }
+        }
+    }
+}
+
 __device__ __forceinline__ void width_frame(float w, float &l, float &r) {
     // apply_stereo_width (:269-270), float32, exact order
     float mid = (l + r) / 2.0f, side = (l - r) / 2.0f;
@@ -183,6 +268,46 @@ __device__ __forceinline__ void tile_load(uint32_t *lds, const uint32_t *__restr
     for (int m = 0; m < T::ITER; m++) {
         const int r = threadIdx.x / T::ROW + m * T::RSTEP;
         lds[r * T::PITCH + c] = ok[m] ? v[m] : 0u;
+    }
+}
+
+// Split form of tile_load for software pipelining: tile_fetch issues the global
+// loads of tile k into registers (no wait), tile_put masks and writes them to LDS.
+// Fetching tile k+1 before computing tile k keeps its HBM latency off the
+// critical path (the loads are only waited for at the next tile_put).
+template <int W, int ROWS = AMX_BLOCK>
+struct TileRegs {
+    uint32_t v[Tile<W, ROWS>::ITER];
+};
+
+template <int W, int ROWS = AMX_BLOCK>
+__device__ __forceinline__ void tile_fetch(TileRegs<W, ROWS> &R, const uint32_t *__restrict__ src,
+                                           const int64_t *rb, const int *lo, const int *hi,
+                                           int k) {
+    using T = Tile<W, ROWS>;
+    const int c = threadIdx.x % T::ROW;
+    const int n = k + c / W;
+#pragma unroll
+    for (int m = 0; m < T::ITER; m++) {
+        const int r = threadIdx.x / T::ROW + m * T::RSTEP;
+        const int l0 = lo ? lo[r] : 0, h0 = hi[r];
+        const bool ok = n >= l0 && n < h0;
+        const int nn = ok ? n : (h0 > l0 ? l0 : 0);
+        R.v[m] = src[rb[r] + (int64_t)nn * W + (c % W)];
+    }
+}
+
+template <int W, int ROWS = AMX_BLOCK>
+__device__ __forceinline__ void tile_put(uint32_t *lds, const TileRegs<W, ROWS> &R,
+                                         const int *lo, const int *hi, int k) {
+    using T = Tile<W, ROWS>;
+    const int c = threadIdx.x % T::ROW;
+    const int n = k + c / W;
+#pragma unroll
+    for (int m = 0; m < T::ITER; m++) {
+        const int r = threadIdx.x / T::ROW + m * T::RSTEP;
+        const int l0 = lo ? lo[r] : 0, h0 = hi[r];
+        lds[r * T::PITCH + c] = (n >= l0 && n < h0) ? R.v[m] : 0u;
     }
 }
 
