@@ -300,7 +300,10 @@ __device__ double round2(double v) {
 
 __device__ __forceinline__ double lufs_of(double e) { return 10 * log10(e) - 0.691; }
 
-__device__ int compact_bins(const unsigned long long *h, short *nz) {
+// Non-empty bins of h in ascending order -> nz (index), nc (count as double, exact
+// below 2^53) and np (count * energy, the product libebur128 adds); returns how many.
+__device__ int compact_bins(const unsigned long long *h, const double *E, short *nz, double *nc,
+                            double *np) {
     const int lane = threadIdx.x;
     int n = 0;
     for (int base = 0; base < AMX_HIST_BINS; base += 64) {
@@ -308,7 +311,11 @@ __device__ int compact_bins(const unsigned long long *h, short *nz) {
         const unsigned long long v = j < AMX_HIST_BINS ? h[j] : 0ull;
         const unsigned long long m = __ballot(v != 0ull);
         const int pos = __popcll(m & ((1ull << lane) - 1ull));
-        if (v) nz[n + pos] = (short)j;
+        if (v) {
+            nz[n + pos] = (short)j;
+            nc[n + pos] = (double)v;
+            np[n + pos] = (double)v * E[j];
+        }
         n += __popcll(m);
     }
     __syncthreads();
@@ -317,23 +324,22 @@ __device__ int compact_bins(const unsigned long long *h, short *nz) {
 
 __global__ void __launch_bounds__(64) k_decide(DecideArgs a) {
     __shared__ short nz[AMX_HIST_BINS];
+    __shared__ double nc[AMX_HIST_BINS], np[AMX_HIST_BINS];
     const int t = blockIdx.x;
     const unsigned long long *H = a.hist + (int64_t)t * AMX_HIST_BINS;
     const unsigned long long *S = a.st_hist + (int64_t)t * AMX_HIST_BINS;
     const double *E = a.energies;
     double I = -INFINITY, thr = -70.0, lra = 0.0;
     if (a.lufs_on) {
-        const int n = compact_bins(H, nz);
+        const int n = compact_bins(H, E, nz, nc, np);
         if (threadIdx.x == 0) {
-            double rel = 0.0;
-            unsigned long long cnt = 0;
+            double rel = 0.0, cnt = 0.0;
             for (int q = 0; q < n; q++) {
-                const int j = nz[q];
-                rel += (double)H[j] * E[j];
-                cnt += H[j];
+                rel += np[q];
+                cnt += nc[q];                          // exact: integer-valued < 2^53
             }
-            if (cnt) {
-                rel /= (double)cnt;
+            if (cnt != 0.0) {
+                rel /= cnt;
                 rel *= 0.1;                            // pow(10, -10/10)
                 thr = lufs_of(rel);
                 int start;
@@ -342,25 +348,22 @@ __global__ void __launch_bounds__(64) k_decide(DecideArgs a) {
                     start = find_bin(a.bounds, rel);
                     if (rel > E[start]) ++start;
                 }
-                double g = 0.0;
-                unsigned long long above = 0;
+                double g = 0.0, above = 0.0;
                 for (int q = 0; q < n; q++) {
-                    const int j = nz[q];
-                    if (j < start) continue;
-                    g += (double)H[j] * E[j];
-                    above += H[j];
+                    if (nz[q] < start) continue;
+                    g += np[q];
+                    above += nc[q];
                 }
-                if (above) I = lufs_of(g / (double)above);
+                if (above != 0.0) I = lufs_of(g / above);
             }
         }
         __syncthreads();
-        const int m = compact_bins(S, nz);
+        const int m = compact_bins(S, E, nz, nc, np);
         if (threadIdx.x == 0) {
             double size = 0.0, power = 0.0;
             for (int q = 0; q < m; q++) {
-                const int j = nz[q];
-                size += (double)S[j];
-                power += (double)S[j] * E[j];
+                size += nc[q];
+                power += np[q];
             }
             if (size != 0.0) {
                 power /= size;
@@ -374,15 +377,15 @@ __global__ void __launch_bounds__(64) k_decide(DecideArgs a) {
                 size = 0.0;
                 int q0 = 0;
                 while (q0 < m && nz[q0] < index) q0++;
-                for (int q = q0; q < m; q++) size += (double)S[nz[q]];
+                for (int q = q0; q < m; q++) size += nc[q];
                 if (size != 0.0) {
                     const double plo = (double)(int64_t)((size - 1) * 0.1 + 0.5);
                     const double phi = (double)(int64_t)((size - 1) * 0.95 + 0.5);
                     double acc = 0.0;
                     int q = q0, last = index;
-                    while (acc <= plo) { last = nz[q]; acc += (double)S[nz[q]]; q++; }
+                    while (acc <= plo) { last = nz[q]; acc += nc[q]; q++; }
                     const double l_en = E[last];
-                    while (acc <= phi) { last = nz[q]; acc += (double)S[nz[q]]; q++; }
+                    while (acc <= phi) { last = nz[q]; acc += nc[q]; q++; }
                     const double h_en = E[last];
                     lra = lufs_of(h_en) - lufs_of(l_en);
                 }
