@@ -113,16 +113,23 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_front1(const ChainDev *__restrict
 // exchanges its float32 EQ output with one DPP swap per frame.  Tiles are fetched
 // one ahead (tile_fetch / tile_put).
 // MB: also accumulate the crossover's zero-state end state (GEMV) for its scan.
+// KW (no multiband, K-filter segments == these segments): also the loudness pass-1
+// work on the output just produced -- the K filter's zero-state end state (GEMV
+// over Gkw, right-aligned for a span's final partial segment like k_kw1) and the
+// per-(segment, channel) sample peak -- so the track is not read again for it.
 #define AMX_EQ_F 8
-template <int MASK, bool MB>
-__global__ void __launch_bounds__(AMX_BLOCK, MB ? 4 : 5) k_front2(const ChainDev *__restrict__ cdp,
+template <int MASK, bool MB, bool KW>
+__global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const ChainDev *__restrict__ cdp,
                                                       const ChunkDev *__restrict__ chunks,
                                                       const SegDev *__restrict__ segs, int n_seg,
                                                       int L, const uint32_t *__restrict__ a16,
                                                       const double *__restrict__ s_eq,
                                                       uint32_t *__restrict__ dst, int to_out,
                                                       const double *__restrict__ Gx,
-                                                      double *__restrict__ e_x) {
+                                                      double *__restrict__ e_x,
+                                                      const double *__restrict__ Gkw,
+                                                      double *__restrict__ e_kw,
+                                                      uint32_t *__restrict__ pk) {
     constexpr int D = EqDim<MASK>::v;
     constexpr int ROWS = AMX_BLOCK / 2;
     using T = Tile<1, ROWS>;
@@ -162,6 +169,13 @@ __global__ void __launch_bounds__(AMX_BLOCK, MB ? 4 : 5) k_front2(const ChainDev
     double xv[MB ? AMX_XO_DIM : 1];
 #pragma unroll
     for (int d = 0; d < (MB ? AMX_XO_DIM : 1); d++) xv[d] = 0.0;
+    double kv[KW ? AMX_KW_DIM : 1];
+#pragma unroll
+    for (int d = 0; d < (KW ? AMX_KW_DIM : 1); d++) kv[d] = 0.0;
+    int kmax = 0;
+    const int klen = (j < n_seg) ? segs[j].len : 0;
+    const int kshift = L - klen;                          // != 0 only on a span's last segment
+    const bool kuni = __ballot(kshift != 0 && klen > 0) == 0ull;
     const int negm = (cd.st[0].neg ? 1 : 0) | (cd.st[3].neg ? 8 : 0);
     const float w = cd.width;
     const int won = cd.width_on;
@@ -205,6 +219,21 @@ __global__ void __launch_bounds__(AMX_BLOCK, MB ? 4 : 5) k_front2(const ChainDev
 #pragma unroll
                     for (int d = 0; d < AMX_XO_DIM; d++) xv[d] = fma(g[d], xd, xv[d]);
                 }
+                if constexpr (KW) {
+                    const int n = k + f0 + f;
+                    const bool act = n < klen;
+                    kmax = max(kmax, act ? abs((int)qv) : 0);
+                    const double xs = act ? (double)qv * (1.0 / 32768.0) : 0.0;
+                    if (kuni) {
+                        const double *g = Gkw + (int64_t)n * AMX_KW_DIM;     // wave-uniform row
+#pragma unroll
+                        for (int d = 0; d < AMX_KW_DIM; d++) kv[d] = fma(g[d], xs, kv[d]);
+                    } else {
+                        const double *g = Gkw + (int64_t)min(n + kshift, L - 1) * AMX_KW_DIM;
+#pragma unroll
+                        for (int d = 0; d < AMX_KW_DIM; d++) kv[d] = fma(g[d], xs, kv[d]);
+                    }
+                }
             }
         }
         __syncthreads();
@@ -215,6 +244,14 @@ __global__ void __launch_bounds__(AMX_BLOCK, MB ? 4 : 5) k_front2(const ChainDev
             double *o = e_x + ((int64_t)j * 2 + chn) * AMX_XO_DIM;
 #pragma unroll
             for (int d = 0; d < AMX_XO_DIM; d++) o[d] = xv[d];
+        }
+    }
+    if constexpr (KW) {
+        if (j < n_seg) {
+            double *o = e_kw + ((int64_t)j * 2 + chn) * AMX_KW_DIM;
+#pragma unroll
+            for (int d = 0; d < AMX_KW_DIM; d++) o[d] = kv[d];
+            pk[(int64_t)j * 2 + chn] = (uint32_t)kmax;
         }
     }
 }
@@ -330,27 +367,34 @@ hipError_t launch_front1(const Launch &l, int D, int win, bool analog, const flo
     return hipErrorInvalidValue;
 }
 
-template <int MASK, bool MB>
+template <int MASK, bool MB, bool KW>
 static hipError_t front2_t(const Launch &l, const uint32_t *a16, const double *s_eq,
-                           uint32_t *dst, int to_out, const double *Gx, double *e_x) {
+                           uint32_t *dst, int to_out, const double *Gx, double *e_x,
+                           const double *Gkw, double *e_kw, uint32_t *pk) {
     const int rows = AMX_BLOCK / 2;
     dim3 grid((unsigned)((l.n_seg + rows - 1) / rows));
-    hipLaunchKernelGGL((k_front2<MASK, MB>), grid, dim3(AMX_BLOCK), 0, l.stream, l.cd, l.chunks,
-                       l.segs, l.n_seg, l.L, a16, s_eq, dst, to_out, Gx, e_x);
+    hipLaunchKernelGGL((k_front2<MASK, MB, KW>), grid, dim3(AMX_BLOCK), 0, l.stream, l.cd,
+                       l.chunks, l.segs, l.n_seg, l.L, a16, s_eq, dst, to_out, Gx, e_x, Gkw, e_kw,
+                       pk);
     return hipGetLastError();
 }
 
 #define AMX_MASK_CASES(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
 
 hipError_t launch_front2(const Launch &l, int mask, const int16_t *a16, const double *s_eq,
-                         int16_t *dst, int to_out, const double *Gx, double *e_x) {
+                         int16_t *dst, int to_out, const double *Gx, double *e_x,
+                         const double *Gkw, double *e_kw, uint32_t *pk) {
     if (l.n_seg <= 0) return hipSuccess;
     const uint32_t *a = reinterpret_cast<const uint32_t *>(a16);
     uint32_t *d = reinterpret_cast<uint32_t *>(dst);
-    const bool mb = Gx != nullptr;
+    const bool mb = Gx != nullptr, kw = Gkw != nullptr;
+    if (mb && kw) return hipErrorInvalidValue;
     switch (mask) {
-#define C2(M) case M: return mb ? front2_t<M, true>(l, a, s_eq, d, to_out, Gx, e_x) \
-                                : front2_t<M, false>(l, a, s_eq, d, to_out, Gx, e_x);
+#define C2(M)                                                                           \
+    case M:                                                                             \
+        return mb ? front2_t<M, true, false>(l, a, s_eq, d, to_out, Gx, e_x, Gkw, e_kw, pk) \
+             : kw ? front2_t<M, false, true>(l, a, s_eq, d, to_out, Gx, e_x, Gkw, e_kw, pk) \
+                  : front2_t<M, false, false>(l, a, s_eq, d, to_out, Gx, e_x, Gkw, e_kw, pk);
         AMX_MASK_CASES(C2)
 #undef C2
     }

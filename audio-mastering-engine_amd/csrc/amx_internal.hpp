@@ -102,17 +102,18 @@ struct Launch {
     hipStream_t stream;
 };
 struct ScanPlan {
-    int D, n_blk, levels;
+    int D, n_blk, K;
     const ScanBlk *blks;
     const double *M;     // A^L, D x D row-major
-    const double *Mbp;   // (A^{L S})^(2^l), l < levels
+    const double *Mbk;   // (A^{L S})^k, k = 1 .. K-1
 };
 hipError_t launch_front1(const Launch &l, int D, int win, bool analog, const float *in,
                          const float *lut, int16_t *a16, const double *G, double *e);
 hipError_t launch_scan(const ScanPlan &p, const double *e, double *s, const double *carry,
-                       double *eb, double *bst, hipStream_t st);
+                       double *eb, hipStream_t st);
 hipError_t launch_front2(const Launch &l, int mask, const int16_t *a16, const double *s_eq,
-                         int16_t *dst, int to_out, const double *Gx, double *e_x);
+                         int16_t *dst, int to_out, const double *Gx, double *e_x,
+                         const double *Gkw, double *e_kw, uint32_t *pk);
 hipError_t launch_xover2(const Launch &l, const int16_t *p16, const double *s_x,
                          int16_t *bands, int64_t nloc);
 hipError_t launch_rms(const Launch &l, const int16_t *bands, uint16_t *r, int64_t nloc);
@@ -159,6 +160,8 @@ struct DecideArgs {
 hipError_t launch_decide(const DecideArgs &a, hipStream_t st);
 hipError_t launch_kw_carry(const double *tails, const double *P, int n_prev, double *carry,
                            hipStream_t st);
+hipError_t launch_peak_reduce(const SpanDev *spans, int n_tracks, const uint32_t *pk,
+                              unsigned long long *peak, hipStream_t st);
 hipError_t launch_kw_tail(const SpanDev *spans, int n_tracks, const double *s, const double *e,
                           const double *P, double *tail, hipStream_t st);
 }  // namespace amx

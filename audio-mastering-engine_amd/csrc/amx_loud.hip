@@ -116,9 +116,12 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_kw2(const ChainDev *__restrict__ 
     for (int i = 0; i < 3; i++) { c1[i] = s_c[i]; c2[i] = s_c[6 + i]; }
     c1[3] = s_c[4]; c1[4] = s_c[5];
     c2[3] = s_c[10]; c2[4] = s_c[11];
+    TileRegs<1, ROWS> R;
+    tile_fetch<1, ROWS>(R, x, rb, nullptr, rl, 0);
     for (int k = 0; k < L; k += AMX_TF) {
-        tile_load<1, ROWS>(s_in, x, rb, nullptr, rl, k);
+        tile_put<1, ROWS>(s_in, R, nullptr, rl, k);
         __syncthreads();
+        if (k + AMX_TF < L) tile_fetch<1, ROWS>(R, x, rb, nullptr, rl, k + AMX_TF);
         const uint32_t *rp = s_in + row * T::PITCH;
 #pragma unroll 4
         for (int f = 0; f < AMX_TF; f++) {
@@ -140,7 +143,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_kw2(const ChainDev *__restrict__ 
     }
 }
 
-// per-hop deterministic sum of the segment pieces (segment order)
+// per-hop sum of the segment pieces: one wave per hop, lanes over the hop's
+// segments, then a fixed butterfly (deterministic for a given segment grid)
 __global__ void __launch_bounds__(AMX_BLOCK) k_hops(const SpanDev *__restrict__ spans,
                                                     const KwSegDev *__restrict__ ks, int L,
                                                     int hop, const double *__restrict__ parts,
@@ -149,24 +153,32 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_hops(const SpanDev *__restrict__ 
     const int t = blockIdx.y;
     const SpanDev sp = spans[t];
     if (sp.nkseg == 0) return;
+    const int lane = threadIdx.x & 63;
     const int64_t hfirst = sp.tframe0 / hop;
     const int64_t hlast = (sp.tframe0 + sp.out_n - 1) / hop;
-    const int64_t h = hfirst + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (h > hlast || h >= max_hops) return;
+    const int64_t h = hfirst + (int64_t)blockIdx.x * (AMX_BLOCK / 64) + (threadIdx.x >> 6);
+    if (h > hlast || h >= max_hops) return;          // wave-uniform
     // span-local frame range of hop h
     int64_t a = h * hop - sp.tframe0, bnd = (h + 1) * hop - sp.tframe0;
     if (a < 0) a = 0;
     if (bnd > sp.out_n) bnd = sp.out_n;
     const int64_t j0 = a / L, j1 = (bnd - 1) / L;
     double s0 = 0.0, s1 = 0.0;
-    for (int64_t jj = j0; jj <= j1; jj++) {
+    for (int64_t jj = j0 + lane; jj <= j1; jj += 64) {
         const int64_t j = sp.kseg0 + jj;
         const int pc = part_hop[j] == h ? 0 : 1;
         s0 += parts[j * 4 + 2 * pc];
         s1 += parts[j * 4 + 2 * pc + 1];
     }
-    hops[((int64_t)t * max_hops + h) * 2] = s0;
-    hops[((int64_t)t * max_hops + h) * 2 + 1] = s1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s0 += __shfl_xor(s0, o);
+        s1 += __shfl_xor(s1, o);
+    }
+    if (lane == 0) {
+        hops[((int64_t)t * max_hops + h) * 2] = s0;
+        hops[((int64_t)t * max_hops + h) * 2 + 1] = s1;
+    }
 }
 
 __device__ __forceinline__ int find_bin(const double *bounds, double energy) {
@@ -232,8 +244,8 @@ hipError_t launch_kw2(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L,
 hipError_t launch_hops(const SpanDev *spans, int n_tracks, const KwSegDev *ks, int L, int hop,
                        const double *parts, const int64_t *part_hop, double *hops,
                        int64_t max_hops, hipStream_t st) {
-    dim3 g = grid1(max_hops);
-    g.y = (unsigned)n_tracks;
+    const int wpb = AMX_BLOCK / 64;   // hops per workgroup (one wave each)
+    dim3 g((unsigned)((max_hops + wpb - 1) / wpb), (unsigned)n_tracks);
     if (empty(g)) return hipSuccess;
     hipLaunchKernelGGL(k_hops, g, dim3(AMX_BLOCK), 0, st, spans, ks, L, hop, parts, part_hop,
                        hops, max_hops);
@@ -251,6 +263,44 @@ hipError_t launch_hist(const SpanDev *spans, int n_tracks, int hop, const double
     return hipGetLastError();
 }
 
+
+// Sample peak per track from the per-(segment, channel) maxima k_front2 wrote
+// when it ran the loudness pass-1 work fused (pk[j][ch] = max |x|).
+__global__ void __launch_bounds__(AMX_BLOCK) k_peak_reduce(const SpanDev *__restrict__ spans,
+                                                           const uint32_t *__restrict__ pk,
+                                                           unsigned long long *__restrict__ peak) {
+    __shared__ int red[2][AMX_BLOCK / 64];
+    const int t = blockIdx.x;
+    const SpanDev sp = spans[t];
+    int m0 = 0, m1 = 0;
+    for (int q = threadIdx.x; q < sp.nkseg; q += AMX_BLOCK) {
+        const int64_t j = (int64_t)sp.kseg0 + q;
+        m0 = max(m0, (int)pk[j * 2]);
+        m1 = max(m1, (int)pk[j * 2 + 1]);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        m0 = max(m0, __shfl_xor(m0, o));
+        m1 = max(m1, __shfl_xor(m1, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = m0;
+        red[1][threadIdx.x >> 6] = m1;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        int m = 0;
+        for (int w = 0; w < AMX_BLOCK / 64; w++) m = max(m, red[threadIdx.x][w]);
+        const double p = (double)m * (1.0 / 32768.0);
+        peak[2 * t + threadIdx.x] = (unsigned long long)__double_as_longlong(p);
+    }
+}
+
+hipError_t launch_peak_reduce(const SpanDev *spans, int n_tracks, const uint32_t *pk,
+                              unsigned long long *peak, hipStream_t st) {
+    if (n_tracks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_peak_reduce, dim3(n_tracks), dim3(AMX_BLOCK), 0, st, spans, pk, peak);
+    return hipGetLastError();
+}
 
 // K-filter state at each span end from rest: P_t * s_last + e_last (per lane)
 __global__ void k_kw_tail(const SpanDev *__restrict__ spans, int n_tracks,
@@ -304,17 +354,25 @@ __device__ __forceinline__ double lufs_of(double e) { return 10 * log10(e) - 0.6
 // below 2^53) and np (count * energy, the product libebur128 adds); returns how many.
 __device__ int compact_bins(const unsigned long long *h, const double *E, short *nz, double *nc,
                             double *np) {
+    constexpr int NB = (AMX_HIST_BINS + 63) / 64;
     const int lane = threadIdx.x;
+    unsigned long long v[NB];
+#pragma unroll
+    for (int c = 0; c < NB; c++) {                 // every load in flight before the first use
+        const int j = c * 64 + lane;
+        v[c] = h[j < AMX_HIST_BINS ? j : AMX_HIST_BINS - 1];
+        if (j >= AMX_HIST_BINS) v[c] = 0ull;
+    }
     int n = 0;
-    for (int base = 0; base < AMX_HIST_BINS; base += 64) {
-        const int j = base + lane;
-        const unsigned long long v = j < AMX_HIST_BINS ? h[j] : 0ull;
-        const unsigned long long m = __ballot(v != 0ull);
+#pragma unroll
+    for (int c = 0; c < NB; c++) {
+        const int j = c * 64 + lane;
+        const unsigned long long m = __ballot(v[c] != 0ull);
         const int pos = __popcll(m & ((1ull << lane) - 1ull));
-        if (v) {
+        if (v[c]) {
             nz[n + pos] = (short)j;
-            nc[n + pos] = (double)v;
-            np[n + pos] = (double)v * E[j];
+            nc[n + pos] = (double)v[c];
+            np[n + pos] = (double)v[c] * E[j];
         }
         n += __popcll(m);
     }

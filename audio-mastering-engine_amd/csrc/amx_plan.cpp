@@ -99,6 +99,21 @@ struct Lti {
         }
         return G;
     }
+    // window powers Mb^k, k = 1 .. K-1, of Mb = A^LS; K = the first k with
+    // ||Mb^k|| <= tol (the block scan sums the previous K-1 blocks' contributions).
+    int window_powers(int64_t LS, double tol, int max_k, std::vector<double> &out) const {
+        Mat Mb = matpow(A, LS, D);
+        Mat cur = Mb;
+        out.clear();
+        int K = 1;
+        while (norm_inf(cur, D) > tol) {
+            out.insert(out.end(), cur.begin(), cur.end());
+            cur = matmul(cur, Mb, D);
+            K++;
+            if (K > max_k) return -1;
+        }
+        return K;
+    }
     // powers M^(2^l), l < levels, of M = A^L; levels chosen so that the neglected
     // tail ||M^(2^levels)|| <= tol (the scan looks back 2^levels - 1 segments).
     int scan_powers(int L, double tol, int max_levels, std::vector<double> &out) const {
@@ -147,6 +162,7 @@ struct amx_plan {
     int mask = 0, D = 0;
     int lev_eq = 0, lev_x = 0, lev_kw = 0;
     int mb = 0, warm = 512;
+    int fuse_kw = 0;        // loudness pass-1 GEMV + peak run inside k_front2
     int n_tracks = 0, n_chunks = 0, n_seg = 0, n_kseg = 0, n_blk = 0, n_kblk = 0;
     int64_t nloc = 0, out_frames = 0, max_chunk_out = 0, max_span = 0;
     std::vector<ChunkDev> chunks;
@@ -177,7 +193,7 @@ struct amx_plan {
     size_t ws_bytes = 0;
     size_t o_a16, o_e, o_s, o_p16, o_ex, o_sx, o_bands, o_r, o_att, o_guess, o_end;
     size_t o_ekw, o_skw, o_parts, o_phop;
-    size_t o_eb, o_bst, o_ebx, o_bstx, o_ebk, o_bstk;
+    size_t o_eb, o_ebx, o_ebk, o_pk;
     amx::ScanPlan scan_eq() const { return {D, n_blk, lev_eq, d_blks, d_M, d_Mp}; }
     amx::ScanPlan scan_xo() const { return {AMX_XO_DIM, mb ? n_blk : 0, lev_x, d_blks, d_Mx, d_Mpx}; }
     amx::ScanPlan scan_kw() const { return {AMX_KW_DIM, n_kblk, lev_kw, d_kblks, d_Mkw, d_Mpkw}; }
@@ -459,6 +475,14 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         p->max_span = sp.out_n > p->max_span ? sp.out_n : p->max_span;
     }
     p->n_kseg = (int)p->ksegs.size();
+    // the K-filter segment grid equals the chain's when there is no multiband
+    // (output frames == input frames) and every chunk but a span's last is whole
+    // segments long: k_front2 then does loudness pass 1 on the output it writes
+    p->fuse_kw = (!p->mb && p->Lkw == p->L && p->n_kseg == p->n_seg) ? 1 : 0;
+    for (int c = 0; c < n_chunks && p->fuse_kw; c++) {
+        const bool span_last = (c == n_chunks - 1) || (chunks[c + 1].track != chunks[c].track);
+        if (!span_last && (p->chunks[c].n % p->L) != 0) p->fuse_kw = 0;
+    }
     p->n_blk = (int)p->blks.size();
     p->n_kblk = (int)p->kblks.size();
 
@@ -484,7 +508,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         });
         G = eq.gemv_table(p->L);
         M = matpow(eq.A, p->L, D);
-        p->lev_eq = eq.scan_powers(p->L * AMX_SCAN_S, tol, 7, Mp);
+        p->lev_eq = eq.window_powers((int64_t)p->L * AMX_SCAN_S, tol, 16, Mp);
         if (p->lev_eq < 0) {
             delete p;
             return fail(AMX_ERANGE, "EQ decays too slowly for %d-frame segments; raise seg_frames", p->L);
@@ -500,7 +524,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         });
         Gx = xo.gemv_table(p->L);
         Mx = matpow(xo.A, p->L, AMX_XO_DIM);
-        p->lev_x = xo.scan_powers(p->L * AMX_SCAN_S, tol, 7, Mpx);
+        p->lev_x = xo.window_powers((int64_t)p->L * AMX_SCAN_S, tol, 16, Mpx);
         if (p->lev_x < 0) {
             delete p;
             return fail(AMX_ERANGE, "crossover decays too slowly for %d-frame segments", p->L);
@@ -514,7 +538,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         });
         Gkw = kw.gemv_table(p->Lkw);
         Mkw = matpow(kw.A, p->Lkw, AMX_KW_DIM);
-        p->lev_kw = kw.scan_powers(p->Lkw * AMX_SCAN_S, tol, 7, Mpkw);
+        p->lev_kw = kw.window_powers((int64_t)p->Lkw * AMX_SCAN_S, tol, 16, Mpkw);
         if (p->lev_kw < 0) {
             delete p;
             return fail(AMX_ERANGE, "K-weighting decays too slowly for %d-frame segments", p->Lkw);
@@ -582,14 +606,12 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     }
     const size_t nb = (size_t)p->n_blk, nkb = (size_t)p->n_kblk;
     p->o_eb = (size_t)align_up(off, nb * 2 * (D ? D : 1) * 8);
-    p->o_bst = (size_t)align_up(off, nb * 2 * (D ? D : 1) * 8);
     if (p->mb) {
         p->o_ebx = (size_t)align_up(off, nb * 2 * AMX_XO_DIM * 8);
-        p->o_bstx = (size_t)align_up(off, nb * 2 * AMX_XO_DIM * 8);
     }
     p->o_ebk = (size_t)align_up(off, nkb * 2 * AMX_KW_DIM * 8);
-    p->o_bstk = (size_t)align_up(off, nkb * 2 * AMX_KW_DIM * 8);
     p->o_ekw = (size_t)align_up(off, nk * 2 * AMX_KW_DIM * 8);
+    p->o_pk = (size_t)align_up(off, nk * 2 * 4);
     p->o_skw = (size_t)align_up(off, nk * 2 * AMX_KW_DIM * 8);
     p->o_parts = (size_t)align_up(off, nk * 4 * 8);
     p->o_phop = (size_t)align_up(off, nk * 8);
@@ -660,17 +682,22 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
         break;
     case AMX_STAGE_SCAN_EQ:
         if (p->D > 0)
-            HIPCHK(amx::launch_scan(p->scan_eq(), e, s, nullptr, wsp<double>(d_ws, p->o_eb),
-                                    wsp<double>(d_ws, p->o_bst), st));
+            HIPCHK(amx::launch_scan(p->scan_eq(), e, s, nullptr, wsp<double>(d_ws, p->o_eb), st));
         break;
     case AMX_STAGE_FRONT2:
-        if (!p->mb) HIPCHK(amx::launch_front2(l, p->mask, a16, s, d_out, 1, nullptr, nullptr));
-        else HIPCHK(amx::launch_front2(l, p->mask, a16, s, p16, 0, p->d_Gx, ex));
+        if (p->mb)
+            HIPCHK(amx::launch_front2(l, p->mask, a16, s, p16, 0, p->d_Gx, ex, nullptr, nullptr,
+                                      nullptr));
+        else if (p->fuse_kw)
+            HIPCHK(amx::launch_front2(l, p->mask, a16, s, d_out, 1, nullptr, nullptr, p->d_Gkw,
+                                      wsp<double>(d_ws, p->o_ekw), wsp<uint32_t>(d_ws, p->o_pk)));
+        else
+            HIPCHK(amx::launch_front2(l, p->mask, a16, s, d_out, 1, nullptr, nullptr, nullptr,
+                                      nullptr, nullptr));
         break;
     case AMX_STAGE_SCAN_XO:
         if (p->mb)
-            HIPCHK(amx::launch_scan(p->scan_xo(), ex, sx, nullptr, wsp<double>(d_ws, p->o_ebx),
-                                    wsp<double>(d_ws, p->o_bstx), st));
+            HIPCHK(amx::launch_scan(p->scan_xo(), ex, sx, nullptr, wsp<double>(d_ws, p->o_ebx), st));
         break;
     case AMX_STAGE_XOVER:
         if (p->mb) HIPCHK(amx::launch_xover2(l, p16, sx, bands, p->nloc));
@@ -715,10 +742,13 @@ int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, double *d_kw_tail, dou
         return AMX_OK;
     }
     double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
-    HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e,
-                           reinterpret_cast<unsigned long long *>(d_peak), st));
-    HIPCHK(amx::launch_scan(p->scan_kw(), e, s, nullptr, wsp<double>(d_ws, p->o_ebk),
-                            wsp<double>(d_ws, p->o_bstk), st));
+    if (p->fuse_kw)   // GEMV + per-segment peaks already made by k_front2 (amx_run_chunks)
+        HIPCHK(amx::launch_peak_reduce(p->d_spans, p->n_tracks, wsp<uint32_t>(d_ws, p->o_pk),
+                                       reinterpret_cast<unsigned long long *>(d_peak), st));
+    else
+        HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e,
+                               reinterpret_cast<unsigned long long *>(d_peak), st));
+    HIPCHK(amx::launch_scan(p->scan_kw(), e, s, nullptr, wsp<double>(d_ws, p->o_ebk), st));
     HIPCHK(amx::launch_kw_tail(p->d_spans, p->n_tracks, s, e, p->d_tailpow, d_kw_tail, st));
     return AMX_OK;
 }
@@ -745,8 +775,7 @@ int amx_loudness_pass2(amx_plan *p, const int16_t *d_out, const double *d_kw_car
     double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
     double *parts = wsp<double>(d_ws, p->o_parts);
     int64_t *phop = wsp<int64_t>(d_ws, p->o_phop);
-    HIPCHK(amx::launch_scan(p->scan_kw(), e, s, d_kw_carry, wsp<double>(d_ws, p->o_ebk),
-                            wsp<double>(d_ws, p->o_bstk), st));
+    HIPCHK(amx::launch_scan(p->scan_kw(), e, s, d_kw_carry, wsp<double>(d_ws, p->o_ebk), st));
     HIPCHK(amx::launch_kw2(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, p->hop, d_out, s, parts, phop, st));
     HIPCHK(amx::launch_hops(p->d_spans, p->n_tracks, p->d_ksegs, p->Lkw, p->hop, parts, phop, d_hops,
                             max_hops, st));

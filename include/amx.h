@@ -118,7 +118,7 @@ typedef struct amx_plan_info {
     int32_t n_chunks;
     int64_t n_segments;           /* IIR segments over all chunks */
     int32_t seg_frames;           /* frames per IIR segment */
-    int32_t scan_levels_eq;
+    int32_t scan_levels_eq;       /* scan window K (blocks of 16 segments) per filter */
     int32_t scan_levels_xover;
     int32_t scan_levels_kw;
     int32_t eq_dim;
