@@ -32,11 +32,12 @@ __device__ __forceinline__ void decode_in(const ChainDev &cd, const uint32_t *ro
 }
 
 // ------------------------------------------------ pass 1: quantise/analog + GEMV
-// One thread per (segment, channel), lanes 2i / 2i+1 = L / R of row i: both decode
-// the frame (the analog stage filters across the channel pair, :264-265) and each
-// accumulates its own channel's GEMV.  The GEMV row G[n] is the same for every
-// lane (wave-uniform -> scalar loads, SGPR operands); the frame loop is unrolled by
-// 2 only, so at most two G rows are live in SGPRs.  Tiles are fetched one ahead.
+// One thread per segment (both channels): frames stream through LDS tiles (fetched
+// one ahead); the GEMV row G[n] is the same for every lane (wave-uniform -> scalar
+// loads, SGPR operands), each used by both channels' FMAs.  The frame loop is
+// unrolled by 2 only, so at most two G rows (2 x D doubles) are live in SGPRs: a
+// full unroll spills SGPRs to VGPR lanes.  (A thread per (segment, channel) halves
+// the reuse of each scalar-loaded G value and measured 35 % slower.)
 template <int D, int WIN, bool AN>
 __global__ void __launch_bounds__(AMX_BLOCK) k_front1(const ChainDev *__restrict__ cdp,
                                                       const ChunkDev *__restrict__ chunks,
@@ -46,65 +47,62 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_front1(const ChainDev *__restrict
                                                       uint32_t *__restrict__ a16,
                                                       const double *__restrict__ G,
                                                       double *__restrict__ e) {
-    constexpr int ROWS = AMX_BLOCK / 2;
-    using TI = Tile<WIN, ROWS>;
-    using TO = Tile<1, ROWS>;
-    __shared__ uint32_t s_in[TI::WORDS];
-    __shared__ uint32_t s_out[TO::WORDS];
-    __shared__ int64_t rb_in[ROWS], rb_out[ROWS];
-    __shared__ int rl[ROWS];
+    __shared__ uint32_t s_in[Tile<WIN>::WORDS];
+    __shared__ uint32_t s_out[Tile<1>::WORDS];
+    __shared__ int64_t rb_in[AMX_BLOCK], rb_out[AMX_BLOCK];
+    __shared__ int rl[AMX_BLOCK];
     const ChainDev &cd = *cdp;
-    const int t = threadIdx.x, row = t >> 1, chn = t & 1;
-    const int j = blockIdx.x * ROWS + row;
+    const int t = threadIdx.x;
+    const int j = blockIdx.x * AMX_BLOCK + t;
     bool need_e = false;
-    if (chn == 0) {
-        rb_in[row] = 0;
-        rb_out[row] = 0;
-        rl[row] = 0;
-    }
+    rb_in[t] = 0;
+    rb_out[t] = 0;
+    rl[t] = 0;
     if (j < n_seg) {
         const SegDev sg = segs[j];
         const ChunkDev ch = chunks[sg.chunk];
-        if (chn == 0) {
-            rb_in[row] = (ch.in_off + sg.pos) * WIN;
-            rb_out[row] = ch.loc_off + sg.pos;
-            rl[row] = sg.len;
-        }
+        rb_in[t] = (ch.in_off + sg.pos) * WIN;
+        rb_out[t] = ch.loc_off + sg.pos;
+        rl[t] = sg.len;
         need_e = !sg.last;
     }
-    double ev[D > 0 ? D : 1];
+    double e0[D > 0 ? D : 1], e1[D > 0 ? D : 1];
 #pragma unroll
-    for (int d = 0; d < D; d++) ev[d] = 0.0;
+    for (int d = 0; d < D; d++) { e0[d] = 0.0; e1[d] = 0.0; }
     __syncthreads();
-    TileRegs<WIN, ROWS> R;
-    tile_fetch<WIN, ROWS>(R, in, rb_in, nullptr, rl, 0);
+    TileRegs<WIN> R;
+    tile_fetch<WIN>(R, in, rb_in, nullptr, rl, 0);
     for (int k = 0; k < L; k += AMX_TF) {
-        tile_put<WIN, ROWS>(s_in, R, nullptr, rl, k);
+        tile_put<WIN>(s_in, R, nullptr, rl, k);
         __syncthreads();
-        if (k + AMX_TF < L) tile_fetch<WIN, ROWS>(R, in, rb_in, nullptr, rl, k + AMX_TF);
-        const uint32_t *rp = s_in + row * TI::PITCH;
-        uint32_t *op = s_out + row * TO::PITCH;
+        if (k + AMX_TF < L) tile_fetch<WIN>(R, in, rb_in, nullptr, rl, k + AMX_TF);
+        const uint32_t *row = s_in + t * Tile<WIN>::PITCH;
+        uint32_t *orow = s_out + t * Tile<1>::PITCH;
 #pragma unroll 2
         for (int f = 0; f < AMX_TF; f++) {
             int16_t l, r;
-            decode_in(cd, rp, f, WIN, l, r);
+            decode_in(cd, row, f, WIN, l, r);
             if constexpr (AN) analog_frame(cd, lut, l, r, l, r);
-            if (chn == 0) op[f] = pack2(l, r);
+            orow[f] = pack2(l, r);
             if constexpr (D > 0) {
                 const double *g = G + (int64_t)(k + f) * D;   // wave-uniform row
-                const double x = (double)((float)(chn ? r : l) / 32768.0f);
+                const double x0 = (double)((float)l / 32768.0f);
+                const double x1 = (double)((float)r / 32768.0f);
 #pragma unroll
-                for (int d = 0; d < D; d++) ev[d] = fma(g[d], x, ev[d]);
+                for (int d = 0; d < D; d++) {
+                    e0[d] = fma(g[d], x0, e0[d]);
+                    e1[d] = fma(g[d], x1, e1[d]);
+                }
             }
         }
         __syncthreads();
-        tile_store<1, ROWS>(s_out, a16, rb_out, rl, k);
+        tile_store<1>(s_out, a16, rb_out, rl, k);
     }
     if constexpr (D > 0) {
         if (need_e) {
-            double *o = e + ((int64_t)j * 2 + chn) * D;
+            double *o = e + (int64_t)j * 2 * D;
 #pragma unroll
-            for (int d = 0; d < D; d++) o[d] = ev[d];
+            for (int d = 0; d < D; d++) { o[d] = e0[d]; o[D + d] = e1[d]; }
         }
     }
 }
@@ -344,10 +342,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_xover2(const ChainDev *__restrict
 template <int D, int WIN, bool AN>
 static hipError_t front1_t(const Launch &l, const uint32_t *in, const float *lut, uint32_t *a16,
                            const double *G, double *e) {
-    const int rows = AMX_BLOCK / 2;
-    dim3 grid((unsigned)((l.n_seg + rows - 1) / rows));
-    hipLaunchKernelGGL((k_front1<D, WIN, AN>), grid, dim3(AMX_BLOCK), 0, l.stream, l.cd, l.chunks,
-                       l.segs, l.n_seg, l.L, in, lut, a16, G, e);
+    hipLaunchKernelGGL((k_front1<D, WIN, AN>), grid1(l.n_seg), dim3(AMX_BLOCK), 0, l.stream, l.cd,
+                       l.chunks, l.segs, l.n_seg, l.L, in, lut, a16, G, e);
     return hipGetLastError();
 }
 

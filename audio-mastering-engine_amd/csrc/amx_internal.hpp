@@ -160,7 +160,7 @@ struct DecideArgs {
 hipError_t launch_decide(const DecideArgs &a, hipStream_t st);
 hipError_t launch_kw_carry(const double *tails, const double *P, int n_prev, double *carry,
                            hipStream_t st);
-hipError_t launch_peak_reduce(const SpanDev *spans, int n_tracks, const uint32_t *pk,
+hipError_t launch_peak_reduce(const KwSegDev *ks, int n_kseg, const uint32_t *pk,
                               unsigned long long *peak, hipStream_t st);
 hipError_t launch_kw_tail(const SpanDev *spans, int n_tracks, const double *s, const double *e,
                           const double *P, double *tail, hipStream_t st);

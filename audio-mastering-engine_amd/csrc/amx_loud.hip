@@ -152,12 +152,18 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_hops(const SpanDev *__restrict__ 
                                                     double *__restrict__ hops, int64_t max_hops) {
     const int t = blockIdx.y;
     const SpanDev sp = spans[t];
-    if (sp.nkseg == 0) return;
     const int lane = threadIdx.x & 63;
     const int64_t hfirst = sp.tframe0 / hop;
-    const int64_t hlast = (sp.tframe0 + sp.out_n - 1) / hop;
-    const int64_t h = hfirst + (int64_t)blockIdx.x * (AMX_BLOCK / 64) + (threadIdx.x >> 6);
-    if (h > hlast || h >= max_hops) return;          // wave-uniform
+    const int64_t hlast = sp.nkseg ? (sp.tframe0 + sp.out_n - 1) / hop : hfirst - 1;
+    const int64_t h = (int64_t)blockIdx.x * (AMX_BLOCK / 64) + (threadIdx.x >> 6);
+    if (h >= max_hops) return;                       // wave-uniform
+    if (h < hfirst || h > hlast) {                   // hops of other ranks' spans: 0
+        if (lane == 0) {
+            hops[((int64_t)t * max_hops + h) * 2] = 0.0;
+            hops[((int64_t)t * max_hops + h) * 2 + 1] = 0.0;
+        }
+        return;
+    }
     // span-local frame range of hop h
     int64_t a = h * hop - sp.tframe0, bnd = (h + 1) * hop - sp.tframe0;
     if (a < 0) a = 0;
@@ -190,33 +196,44 @@ __device__ __forceinline__ int find_bin(const double *bounds, double energy) {
     return lo;
 }
 
-// gating blocks (400 ms every 100 ms) and short-term blocks (3 s every 1 s)
-__global__ void __launch_bounds__(AMX_BLOCK) k_hist(const SpanDev *__restrict__ spans, int hop,
-                                                    const double *__restrict__ hops,
-                                                    int64_t max_hops,
-                                                    const double *__restrict__ bounds,
-                                                    unsigned long long *__restrict__ hist,
-                                                    unsigned long long *__restrict__ st_hist) {
-    const int t = blockIdx.y;
+// gating blocks (400 ms every 100 ms) and short-term blocks (3 s every 1 s): one
+// workgroup per track, histograms in LDS, written whole (no zeroing pass needed)
+#define AMX_HIST_THREADS 1024
+__global__ void __launch_bounds__(AMX_HIST_THREADS) k_hist(const SpanDev *__restrict__ spans,
+                                                           int hop,
+                                                           const double *__restrict__ hops,
+                                                           int64_t max_hops,
+                                                           const double *__restrict__ bounds,
+                                                           unsigned long long *__restrict__ hist,
+                                                           unsigned long long *__restrict__ st_hist) {
+    __shared__ unsigned int h[AMX_HIST_BINS], sh[AMX_HIST_BINS];
+    __shared__ double bd[AMX_HIST_BINS + 1];
+    const int t = blockIdx.x;
     const SpanDev sp = spans[t];
+    for (int i = threadIdx.x; i < AMX_HIST_BINS; i += AMX_HIST_THREADS) { h[i] = 0u; sh[i] = 0u; }
+    for (int i = threadIdx.x; i <= AMX_HIST_BINS; i += AMX_HIST_THREADS) bd[i] = bounds[i];
+    __syncthreads();
     int64_t nh = sp.ttotal / hop;
     if (nh > max_hops) nh = max_hops;
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const double *H = hops + (int64_t)t * max_hops * 2;
-    if (k + 4 <= nh) {
+    for (int64_t k = threadIdx.x; k + 4 <= nh; k += AMX_HIST_THREADS) {
         double c0 = ((H[2 * k] + H[2 * (k + 1)]) + H[2 * (k + 2)]) + H[2 * (k + 3)];
         double c1 = ((H[2 * k + 1] + H[2 * (k + 1) + 1]) + H[2 * (k + 2) + 1]) + H[2 * (k + 3) + 1];
         double en = (c0 + c1) / (double)(4 * (int64_t)hop);
-        if (en >= bounds[0]) atomicAdd(hist + (int64_t)t * AMX_HIST_BINS + find_bin(bounds, en), 1ull);
+        if (en >= bd[0]) atomicAdd(&h[find_bin(bd, en)], 1u);
     }
     // short-term block m ends at hop 30 + 10 m
-    const int64_t end = 30 + 10 * k;
-    if (end <= nh) {
+    for (int64_t m = threadIdx.x; 30 + 10 * m <= nh; m += AMX_HIST_THREADS) {
+        const int64_t end = 30 + 10 * m;
         double c0 = 0.0, c1 = 0.0;
-        for (int64_t h = end - 30; h < end; h++) { c0 += H[2 * h]; c1 += H[2 * h + 1]; }
+        for (int64_t q = end - 30; q < end; q++) { c0 += H[2 * q]; c1 += H[2 * q + 1]; }
         double en = (c0 + c1) / (double)(30 * (int64_t)hop);
-        if (en >= bounds[0])
-            atomicAdd(st_hist + (int64_t)t * AMX_HIST_BINS + find_bin(bounds, en), 1ull);
+        if (en >= bd[0]) atomicAdd(&sh[find_bin(bd, en)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < AMX_HIST_BINS; i += AMX_HIST_THREADS) {
+        hist[(int64_t)t * AMX_HIST_BINS + i] = h[i];
+        st_hist[(int64_t)t * AMX_HIST_BINS + i] = sh[i];
     }
 }
 
@@ -255,50 +272,45 @@ hipError_t launch_hops(const SpanDev *spans, int n_tracks, const KwSegDev *ks, i
 hipError_t launch_hist(const SpanDev *spans, int n_tracks, int hop, const double *hops,
                        int64_t max_hops, const double *bounds, unsigned long long *hist,
                        unsigned long long *st_hist, hipStream_t st) {
-    dim3 g = grid1(max_hops);
-    g.y = (unsigned)n_tracks;
-    if (empty(g)) return hipSuccess;
-    hipLaunchKernelGGL(k_hist, g, dim3(AMX_BLOCK), 0, st, spans, hop, hops, max_hops, bounds,
-                       hist, st_hist);
+    if (n_tracks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hist, dim3(n_tracks), dim3(AMX_HIST_THREADS), 0, st, spans, hop, hops,
+                       max_hops, bounds, hist, st_hist);
     return hipGetLastError();
 }
 
 
 // Sample peak per track from the per-(segment, channel) maxima k_front2 wrote
-// when it ran the loudness pass-1 work fused (pk[j][ch] = max |x|).
-__global__ void __launch_bounds__(AMX_BLOCK) k_peak_reduce(const SpanDev *__restrict__ spans,
+// when it ran the loudness pass-1 work fused (pk[j][ch] = max |x|): one thread per
+// segment, a wave max, one atomicMax per wave when the wave is one track (the
+// peak buffer is zeroed by amx_loudness_pass1 first).
+__global__ void __launch_bounds__(AMX_BLOCK) k_peak_reduce(const KwSegDev *__restrict__ ks,
+                                                           int n_kseg,
                                                            const uint32_t *__restrict__ pk,
                                                            unsigned long long *__restrict__ peak) {
-    __shared__ int red[2][AMX_BLOCK / 64];
-    const int t = blockIdx.x;
-    const SpanDev sp = spans[t];
-    int m0 = 0, m1 = 0;
-    for (int q = threadIdx.x; q < sp.nkseg; q += AMX_BLOCK) {
-        const int64_t j = (int64_t)sp.kseg0 + q;
-        m0 = max(m0, (int)pk[j * 2]);
-        m1 = max(m1, (int)pk[j * 2 + 1]);
+    const int j = blockIdx.x * AMX_BLOCK + threadIdx.x;
+    const bool valid = j < n_kseg;
+    const int track = ks[valid ? j : n_kseg - 1].track;
+    int m0 = valid ? (int)pk[(int64_t)j * 2] : 0;
+    int m1 = valid ? (int)pk[(int64_t)j * 2 + 1] : 0;
+    const int t0 = __shfl(track, 0);
+    const bool same = __ballot(track != t0) == 0ull;
+    if (same) {
+        for (int o = 32; o > 0; o >>= 1) {
+            m0 = max(m0, __shfl_xor(m0, o));
+            m1 = max(m1, __shfl_xor(m1, o));
+        }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        m0 = max(m0, __shfl_xor(m0, o));
-        m1 = max(m1, __shfl_xor(m1, o));
-    }
-    if ((threadIdx.x & 63) == 0) {
-        red[0][threadIdx.x >> 6] = m0;
-        red[1][threadIdx.x >> 6] = m1;
-    }
-    __syncthreads();
-    if (threadIdx.x < 2) {
-        int m = 0;
-        for (int w = 0; w < AMX_BLOCK / 64; w++) m = max(m, red[threadIdx.x][w]);
-        const double p = (double)m * (1.0 / 32768.0);
-        peak[2 * t + threadIdx.x] = (unsigned long long)__double_as_longlong(p);
+    if (valid && (!same || (threadIdx.x & 63) == 0)) {
+        const double p0 = (double)m0 * (1.0 / 32768.0), p1 = (double)m1 * (1.0 / 32768.0);
+        atomicMax(peak + 2 * track, (unsigned long long)__double_as_longlong(p0));
+        atomicMax(peak + 2 * track + 1, (unsigned long long)__double_as_longlong(p1));
     }
 }
 
-hipError_t launch_peak_reduce(const SpanDev *spans, int n_tracks, const uint32_t *pk,
+hipError_t launch_peak_reduce(const KwSegDev *ks, int n_kseg, const uint32_t *pk,
                               unsigned long long *peak, hipStream_t st) {
-    if (n_tracks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_peak_reduce, dim3(n_tracks), dim3(AMX_BLOCK), 0, st, spans, pk, peak);
+    if (n_kseg <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_peak_reduce, grid1(n_kseg), dim3(AMX_BLOCK), 0, st, ks, n_kseg, pk, peak);
     return hipGetLastError();
 }
 
@@ -350,103 +362,112 @@ __device__ double round2(double v) {
 
 __device__ __forceinline__ double lufs_of(double e) { return 10 * log10(e) - 0.691; }
 
-// Non-empty bins of h in ascending order -> nz (index), nc (count as double, exact
-// below 2^53) and np (count * energy, the product libebur128 adds); returns how many.
-__device__ int compact_bins(const unsigned long long *h, const double *E, short *nz, double *nc,
-                            double *np) {
-    constexpr int NB = (AMX_HIST_BINS + 63) / 64;
-    const int lane = threadIdx.x;
-    unsigned long long v[NB];
+// Wave-parallel histogram arithmetic: lane l owns bins [16 l, 16 l + 16).  Counts
+// are integers (exact in double), so count sums and prefix walks are exact in any
+// order; the energy sums use a fixed lane order + butterfly (deterministic; they
+// differ from libebur128's sequential order only in the last bits, far below the
+// "%.2f" the statistics are printed with).
+#define AMX_BPL 16
+__device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
-    for (int c = 0; c < NB; c++) {                 // every load in flight before the first use
-        const int j = c * 64 + lane;
-        v[c] = h[j < AMX_HIST_BINS ? j : AMX_HIST_BINS - 1];
-        if (j >= AMX_HIST_BINS) v[c] = 0ull;
-    }
-    int n = 0;
-#pragma unroll
-    for (int c = 0; c < NB; c++) {
-        const int j = c * 64 + lane;
-        const unsigned long long m = __ballot(v[c] != 0ull);
-        const int pos = __popcll(m & ((1ull << lane) - 1ull));
-        if (v[c]) {
-            nz[n + pos] = (short)j;
-            nc[n + pos] = (double)v[c];
-            np[n + pos] = (double)v[c] * E[j];
-        }
-        n += __popcll(m);
-    }
-    __syncthreads();
-    return n;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
 }
 
 __global__ void __launch_bounds__(64) k_decide(DecideArgs a) {
-    __shared__ short nz[AMX_HIST_BINS];
-    __shared__ double nc[AMX_HIST_BINS], np[AMX_HIST_BINS];
-    const int t = blockIdx.x;
+    const int t = blockIdx.x, lane = threadIdx.x;
     const unsigned long long *H = a.hist + (int64_t)t * AMX_HIST_BINS;
     const unsigned long long *S = a.st_hist + (int64_t)t * AMX_HIST_BINS;
     const double *E = a.energies;
     double I = -INFINITY, thr = -70.0, lra = 0.0;
     if (a.lufs_on) {
-        const int n = compact_bins(H, E, nz, nc, np);
-        if (threadIdx.x == 0) {
-            double rel = 0.0, cnt = 0.0;
-            for (int q = 0; q < n; q++) {
-                rel += np[q];
-                cnt += nc[q];                          // exact: integer-valued < 2^53
-            }
-            if (cnt != 0.0) {
-                rel /= cnt;
-                rel *= 0.1;                            // pow(10, -10/10)
-                thr = lufs_of(rel);
-                int start;
-                if (rel < a.bounds[0]) start = 0;
-                else {
-                    start = find_bin(a.bounds, rel);
-                    if (rel > E[start]) ++start;
-                }
-                double g = 0.0, above = 0.0;
-                for (int q = 0; q < n; q++) {
-                    if (nz[q] < start) continue;
-                    g += np[q];
-                    above += nc[q];
-                }
-                if (above != 0.0) I = lufs_of(g / above);
-            }
+        double hc[AMX_BPL], sc[AMX_BPL], en[AMX_BPL];
+#pragma unroll
+        for (int q = 0; q < AMX_BPL; q++) {      // all loads in flight before use
+            const int j = lane * AMX_BPL + q;
+            const int jj = j < AMX_HIST_BINS ? j : AMX_HIST_BINS - 1;
+            const bool ok = j < AMX_HIST_BINS;
+            hc[q] = ok ? (double)H[jj] : 0.0;
+            sc[q] = ok ? (double)S[jj] : 0.0;
+            en[q] = E[jj];
         }
-        __syncthreads();
-        const int m = compact_bins(S, E, nz, nc, np);
-        if (threadIdx.x == 0) {
-            double size = 0.0, power = 0.0;
-            for (int q = 0; q < m; q++) {
-                size += nc[q];
-                power += np[q];
+        // integrated loudness with the relative gate (ebur128_gated_loudness)
+        double rel = 0.0, cnt = 0.0;
+#pragma unroll
+        for (int q = 0; q < AMX_BPL; q++) { rel += hc[q] * en[q]; cnt += hc[q]; }
+        rel = wave_sum(rel);
+        cnt = wave_sum(cnt);
+        if (cnt != 0.0) {
+            rel /= cnt;
+            rel *= 0.1;                                // pow(10, -10/10)
+            thr = lufs_of(rel);
+            int start;
+            if (rel < a.bounds[0]) start = 0;
+            else {
+                start = find_bin(a.bounds, rel);
+                if (rel > E[start]) ++start;
             }
-            if (size != 0.0) {
-                power /= size;
-                const double integ = 0.01 * power;      // pow(10, -20/10)
-                int index;
-                if (integ < a.bounds[0]) index = 0;
-                else {
-                    index = find_bin(a.bounds, integ);
-                    if (integ > E[index]) ++index;
+            double g = 0.0, above = 0.0;
+#pragma unroll
+            for (int q = 0; q < AMX_BPL; q++) {
+                const bool in = lane * AMX_BPL + q >= start;
+                g += in ? hc[q] * en[q] : 0.0;
+                above += in ? hc[q] : 0.0;
+            }
+            g = wave_sum(g);
+            above = wave_sum(above);
+            if (above != 0.0) I = lufs_of(g / above);
+        }
+        // loudness range (ebur128_loudness_range) on the short-term histogram
+        double size = 0.0, power = 0.0;
+#pragma unroll
+        for (int q = 0; q < AMX_BPL; q++) { size += sc[q]; power += sc[q] * en[q]; }
+        size = wave_sum(size);
+        power = wave_sum(power);
+        if (size != 0.0) {
+            power /= size;
+            const double integ = 0.01 * power;         // pow(10, -20/10)
+            int index;
+            if (integ < a.bounds[0]) index = 0;
+            else {
+                index = find_bin(a.bounds, integ);
+                if (integ > E[index]) ++index;
+            }
+            double mine = 0.0;                         // this lane's counts at bins >= index
+            double cum[AMX_BPL];
+#pragma unroll
+            for (int q = 0; q < AMX_BPL; q++) {
+                mine += lane * AMX_BPL + q >= index ? sc[q] : 0.0;
+                cum[q] = mine;
+            }
+            // exclusive prefix of the lane totals (exact integer arithmetic)
+            double incl = mine;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const double up = __shfl_up(incl, o);
+                if (lane >= o) incl += up;
+            }
+            const double before = incl - mine;
+            const double tot = __shfl(incl, 63);
+            if (tot != 0.0) {
+                const double plo = (double)(int64_t)((tot - 1) * 0.1 + 0.5);
+                const double phi = (double)(int64_t)((tot - 1) * 0.95 + 0.5);
+                // the walk stops at the first bin whose cumulative count exceeds p
+                int jl = 0x7fffffff, jh = 0x7fffffff;
+#pragma unroll
+                for (int q = AMX_BPL - 1; q >= 0; q--) {
+                    const int j = lane * AMX_BPL + q;
+                    const double c = before + cum[q];
+                    const bool nz = j >= index && sc[q] != 0.0;
+                    if (nz && c > plo) jl = j;
+                    if (nz && c > phi) jh = j;
                 }
-                size = 0.0;
-                int q0 = 0;
-                while (q0 < m && nz[q0] < index) q0++;
-                for (int q = q0; q < m; q++) size += nc[q];
-                if (size != 0.0) {
-                    const double plo = (double)(int64_t)((size - 1) * 0.1 + 0.5);
-                    const double phi = (double)(int64_t)((size - 1) * 0.95 + 0.5);
-                    double acc = 0.0;
-                    int q = q0, last = index;
-                    while (acc <= plo) { last = nz[q]; acc += nc[q]; q++; }
-                    const double l_en = E[last];
-                    while (acc <= phi) { last = nz[q]; acc += nc[q]; q++; }
-                    const double h_en = E[last];
-                    lra = lufs_of(h_en) - lufs_of(l_en);
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    jl = min(jl, __shfl_xor(jl, o));
+                    jh = min(jh, __shfl_xor(jh, o));
                 }
+                lra = lufs_of(E[jh]) - lufs_of(E[jl]);
             }
         }
     }

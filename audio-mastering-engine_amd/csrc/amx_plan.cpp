@@ -743,7 +743,7 @@ int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, double *d_kw_tail, dou
     }
     double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
     if (p->fuse_kw)   // GEMV + per-segment peaks already made by k_front2 (amx_run_chunks)
-        HIPCHK(amx::launch_peak_reduce(p->d_spans, p->n_tracks, wsp<uint32_t>(d_ws, p->o_pk),
+        HIPCHK(amx::launch_peak_reduce(p->d_ksegs, p->n_kseg, wsp<uint32_t>(d_ws, p->o_pk),
                                        reinterpret_cast<unsigned long long *>(d_peak), st));
     else
         HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e,
@@ -770,8 +770,10 @@ int amx_loudness_pass2(amx_plan *p, const int16_t *d_out, const double *d_kw_car
     if (!p || !d_hops || max_hops <= 0 || (p->n_kseg > 0 && (!d_out || !d_ws)))
         return fail(AMX_EINVAL, "null argument");
     hipStream_t st = (hipStream_t)stream;
-    HIPCHK(hipMemsetAsync(d_hops, 0, sizeof(double) * 2 * (size_t)max_hops * p->n_tracks, st));
-    if (p->n_kseg == 0) return AMX_OK;
+    if (p->n_kseg == 0) {
+        HIPCHK(hipMemsetAsync(d_hops, 0, sizeof(double) * 2 * (size_t)max_hops * p->n_tracks, st));
+        return AMX_OK;
+    }
     double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
     double *parts = wsp<double>(d_ws, p->o_parts);
     int64_t *phop = wsp<int64_t>(d_ws, p->o_phop);
@@ -788,8 +790,6 @@ int amx_loudness_histograms(amx_plan *p, const double *d_hops, int64_t max_hops,
     if (!p || !d_hops || !d_hist || !d_st_hist || max_hops <= 0)
         return fail(AMX_EINVAL, "null argument");
     hipStream_t st = (hipStream_t)stream;
-    HIPCHK(hipMemsetAsync(d_hist, 0, sizeof(uint64_t) * AMX_HIST_BINS * (size_t)p->n_tracks, st));
-    HIPCHK(hipMemsetAsync(d_st_hist, 0, sizeof(uint64_t) * AMX_HIST_BINS * (size_t)p->n_tracks, st));
     HIPCHK(amx::launch_hist(p->d_spans, p->n_tracks, p->hop, d_hops, max_hops, p->d_bounds,
                             reinterpret_cast<unsigned long long *>(d_hist),
                             reinterpret_cast<unsigned long long *>(d_st_hist), st));
