@@ -126,7 +126,7 @@ hipError_t launch_apply_n1(const Launch &l, const int16_t *bands, const double *
                            const int64_t *n1tab);
 // loudness
 hipError_t launch_kw1(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L,
-                      const int16_t *x, const double *G, double *e, unsigned long long *peak,
+                      const int16_t *x, const double *G, double *e, uint32_t *pk,
                       hipStream_t st);
 hipError_t launch_kw2(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L, int hop,
                       const int16_t *x, const double *s, double *parts, int64_t *part_hop,
@@ -160,8 +160,8 @@ struct DecideArgs {
 hipError_t launch_decide(const DecideArgs &a, hipStream_t st);
 hipError_t launch_kw_carry(const double *tails, const double *P, int n_prev, double *carry,
                            hipStream_t st);
-hipError_t launch_peak_reduce(const KwSegDev *ks, int n_kseg, const uint32_t *pk,
-                              unsigned long long *peak, hipStream_t st);
+hipError_t launch_peak_reduce(const SpanDev *spans, int n_tracks, int64_t max_nkseg,
+                              const uint32_t *pk, unsigned long long *peak, hipStream_t st);
 hipError_t launch_kw_tail(const SpanDev *spans, int n_tracks, const double *s, const double *e,
                           const double *P, double *tail, hipStream_t st);
 }  // namespace amx

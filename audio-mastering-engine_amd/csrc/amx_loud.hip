@@ -8,12 +8,13 @@
 
 namespace amx {
 
-// K-weighting pass 1: zero-state end state GEMV + sample peak
+// K-weighting pass 1: zero-state end state GEMV + per-(segment, channel) peak
+// (reduced per track by k_peak_reduce)
 __global__ void __launch_bounds__(AMX_BLOCK) k_kw1(const KwSegDev *__restrict__ ks, int n_kseg,
                                                    int L, const uint32_t *__restrict__ x,
                                                    const double *__restrict__ G,
                                                    double *__restrict__ e,
-                                                   unsigned long long *__restrict__ peak) {
+                                                   uint32_t *__restrict__ pk) {
     __shared__ uint32_t s_in[Tile<1>::WORDS];
     __shared__ int64_t rb[AMX_BLOCK];
     __shared__ int rlo[AMX_BLOCK], rhi[AMX_BLOCK];
@@ -58,19 +59,9 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_kw1(const KwSegDev *__restrict__ 
 #pragma unroll
         for (int d = 0; d < AMX_KW_DIM; d++) { o[d] = e0[d]; o[AMX_KW_DIM + d] = e1[d]; }
     }
-    // sample peak: wave max first, one atomic per wave when the wave is one track
-    const int t0 = __shfl(sg.track, 0);
-    const bool same = __ballot(sg.track != t0) == 0ull;
-    if (same) {
-        for (int o = 32; o > 0; o >>= 1) {
-            m0 = max(m0, __shfl_xor(m0, o));
-            m1 = max(m1, __shfl_xor(m1, o));
-        }
-    }
-    if (valid && (!same || (threadIdx.x & 63) == 0)) {
-        const double p0 = (double)m0 * (1.0 / 32768.0), p1 = (double)m1 * (1.0 / 32768.0);
-        atomicMax(peak + 2 * sg.track, (unsigned long long)__double_as_longlong(p0));
-        atomicMax(peak + 2 * sg.track + 1, (unsigned long long)__double_as_longlong(p1));
+    if (valid) {
+        pk[(int64_t)j * 2] = (uint32_t)m0;
+        pk[(int64_t)j * 2 + 1] = (uint32_t)m1;
     }
 }
 
@@ -239,12 +230,12 @@ __global__ void __launch_bounds__(AMX_HIST_THREADS) k_hist(const SpanDev *__rest
 
 // ================================================================ launchers
 hipError_t launch_kw1(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L,
-                      const int16_t *x, const double *G, double *e, unsigned long long *peak,
+                      const int16_t *x, const double *G, double *e, uint32_t *pk,
                       hipStream_t st) {
     (void)cd;
     if (n_kseg <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_kw1, grid1(n_kseg), dim3(AMX_BLOCK), 0, st, ks, n_kseg, L,
-                       reinterpret_cast<const uint32_t *>(x), G, e, peak);
+                       reinterpret_cast<const uint32_t *>(x), G, e, pk);
     return hipGetLastError();
 }
 
@@ -280,37 +271,53 @@ hipError_t launch_hist(const SpanDev *spans, int n_tracks, int hop, const double
 
 
 // Sample peak per track from the per-(segment, channel) maxima k_front2 wrote
-// when it ran the loudness pass-1 work fused (pk[j][ch] = max |x|): one thread per
-// segment, a wave max, one atomicMax per wave when the wave is one track (the
-// peak buffer is zeroed by amx_loudness_pass1 first).
-__global__ void __launch_bounds__(AMX_BLOCK) k_peak_reduce(const KwSegDev *__restrict__ ks,
-                                                           int n_kseg,
-                                                           const uint32_t *__restrict__ pk,
-                                                           unsigned long long *__restrict__ peak) {
-    const int j = blockIdx.x * AMX_BLOCK + threadIdx.x;
-    const bool valid = j < n_kseg;
-    const int track = ks[valid ? j : n_kseg - 1].track;
-    int m0 = valid ? (int)pk[(int64_t)j * 2] : 0;
-    int m1 = valid ? (int)pk[(int64_t)j * 2 + 1] : 0;
-    const int t0 = __shfl(track, 0);
-    const bool same = __ballot(track != t0) == 0ull;
-    if (same) {
-        for (int o = 32; o > 0; o >>= 1) {
-            m0 = max(m0, __shfl_xor(m0, o));
-            m1 = max(m1, __shfl_xor(m1, o));
-        }
+// when it ran the loudness pass-1 work fused (pk[j][ch] = max |x|).  grid.y =
+// track, each workgroup reduces a contiguous run of that track's segments in LDS
+// and issues one atomicMax per channel (the peak buffer is zeroed by
+// amx_loudness_pass1 first): same-address atomics serialise, so there are few.
+#define AMX_PEAK_THREADS 1024
+#define AMX_PEAK_PER_THREAD 8
+__global__ void __launch_bounds__(AMX_PEAK_THREADS) k_peak_reduce(const SpanDev *__restrict__ spans,
+                                                                  const uint32_t *__restrict__ pk,
+                                                                  unsigned long long *__restrict__ peak) {
+    __shared__ int red[2][AMX_PEAK_THREADS / 64];
+    const int t = blockIdx.y;
+    const SpanDev sp = spans[t];
+    const int64_t q0 = (int64_t)blockIdx.x * AMX_PEAK_THREADS * AMX_PEAK_PER_THREAD;
+    if (q0 >= sp.nkseg) return;                      // block-uniform
+    int m0 = 0, m1 = 0;
+#pragma unroll
+    for (int i = 0; i < AMX_PEAK_PER_THREAD; i++) {
+        const int64_t q = q0 + threadIdx.x + (int64_t)i * AMX_PEAK_THREADS;
+        const bool ok = q < sp.nkseg;
+        const int64_t j = (int64_t)sp.kseg0 + (ok ? q : 0);
+        const uint32_t a0 = pk[j * 2], a1 = pk[j * 2 + 1];
+        m0 = max(m0, ok ? (int)a0 : 0);
+        m1 = max(m1, ok ? (int)a1 : 0);
     }
-    if (valid && (!same || (threadIdx.x & 63) == 0)) {
-        const double p0 = (double)m0 * (1.0 / 32768.0), p1 = (double)m1 * (1.0 / 32768.0);
-        atomicMax(peak + 2 * track, (unsigned long long)__double_as_longlong(p0));
-        atomicMax(peak + 2 * track + 1, (unsigned long long)__double_as_longlong(p1));
+    for (int o = 32; o > 0; o >>= 1) {
+        m0 = max(m0, __shfl_xor(m0, o));
+        m1 = max(m1, __shfl_xor(m1, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = m0;
+        red[1][threadIdx.x >> 6] = m1;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        int m = 0;
+        for (int w = 0; w < AMX_PEAK_THREADS / 64; w++) m = max(m, red[threadIdx.x][w]);
+        const double p = (double)m * (1.0 / 32768.0);
+        atomicMax(peak + 2 * t + threadIdx.x, (unsigned long long)__double_as_longlong(p));
     }
 }
 
-hipError_t launch_peak_reduce(const KwSegDev *ks, int n_kseg, const uint32_t *pk,
-                              unsigned long long *peak, hipStream_t st) {
-    if (n_kseg <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_peak_reduce, grid1(n_kseg), dim3(AMX_BLOCK), 0, st, ks, n_kseg, pk, peak);
+hipError_t launch_peak_reduce(const SpanDev *spans, int n_tracks, int64_t max_nkseg,
+                              const uint32_t *pk, unsigned long long *peak, hipStream_t st) {
+    const int64_t per = (int64_t)AMX_PEAK_THREADS * AMX_PEAK_PER_THREAD;
+    dim3 g((unsigned)((max_nkseg + per - 1) / per), (unsigned)n_tracks);
+    if (empty(g)) return hipSuccess;
+    hipLaunchKernelGGL(k_peak_reduce, g, dim3(AMX_PEAK_THREADS), 0, st, spans, pk, peak);
     return hipGetLastError();
 }
 

@@ -164,6 +164,7 @@ struct amx_plan {
     int mb = 0, warm = 512;
     int fuse_kw = 0;        // loudness pass-1 GEMV + peak run inside k_front2
     int n_tracks = 0, n_chunks = 0, n_seg = 0, n_kseg = 0, n_blk = 0, n_kblk = 0;
+    int64_t max_nkseg = 0;
     int64_t nloc = 0, out_frames = 0, max_chunk_out = 0, max_span = 0;
     std::vector<ChunkDev> chunks;
     std::vector<SegDev> segs;
@@ -473,6 +474,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             p->ksegs.push_back(s);
         }
         p->max_span = sp.out_n > p->max_span ? sp.out_n : p->max_span;
+        p->max_nkseg = sp.nkseg > p->max_nkseg ? sp.nkseg : p->max_nkseg;
     }
     p->n_kseg = (int)p->ksegs.size();
     // the K-filter segment grid equals the chain's when there is no multiband
@@ -742,12 +744,11 @@ int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, double *d_kw_tail, dou
         return AMX_OK;
     }
     double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
-    if (p->fuse_kw)   // GEMV + per-segment peaks already made by k_front2 (amx_run_chunks)
-        HIPCHK(amx::launch_peak_reduce(p->d_ksegs, p->n_kseg, wsp<uint32_t>(d_ws, p->o_pk),
-                                       reinterpret_cast<unsigned long long *>(d_peak), st));
-    else
-        HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e,
-                               reinterpret_cast<unsigned long long *>(d_peak), st));
+    uint32_t *pk = wsp<uint32_t>(d_ws, p->o_pk);
+    if (!p->fuse_kw)  // else the GEMV + per-segment peaks were made by k_front2 (amx_run_chunks)
+        HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e, pk, st));
+    HIPCHK(amx::launch_peak_reduce(p->d_spans, p->n_tracks, p->max_nkseg, pk,
+                                   reinterpret_cast<unsigned long long *>(d_peak), st));
     HIPCHK(amx::launch_scan(p->scan_kw(), e, s, nullptr, wsp<double>(d_ws, p->o_ebk), st));
     HIPCHK(amx::launch_kw_tail(p->d_spans, p->n_tracks, s, e, p->d_tailpow, d_kw_tail, st));
     return AMX_OK;

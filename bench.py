@@ -141,6 +141,10 @@ def main():
                      "bytes_per_launch": int(dom_bytes), "avg_launch_ms": round(dom_ms, 4),
                      "traffic": None},
         "stages_ms": {k: round(v, 4) for k, v in per_stage.items()},
+        "plan": {"segments": int(job.info.n_segments), "seg_frames": int(job.info.seg_frames),
+                 "scan_window_eq": int(job.info.scan_levels_eq),
+                 "scan_window_xover": int(job.info.scan_levels_xover),
+                 "scan_window_kw": int(job.info.scan_levels_kw)},
         "limiter_fast": report.get("limiter_fast"),
         "loudnorm": report.get("stats"),
         "loudnorm_mode": report.get("modes"),
