@@ -40,6 +40,7 @@ class ChainDesc(ctypes.Structure):
         ("xover_lo_sos", ctypes.c_double * 12), ("xover_hi_sos", ctypes.c_double * 12),
         ("comp_threshold_db", ctypes.c_double * 3), ("comp_ratio", ctypes.c_double * 3),
         ("comp_m_table", c_double_p * 3),
+        ("env_warm_frames", ctypes.c_int32), ("env_rounds", ctypes.c_int32),
     ]
 
 

@@ -46,6 +46,10 @@ def chain_desc(fs, channels_in, settings):
     keep = []
     d.sample_rate = int(fs)
     d.channels_in = int(channels_in)
+    # compressor envelope work split (amx_dyn.hip); exact for any value -- the
+    # underscore keys exist so the tests can force the fix-up paths
+    d.env_warm_frames = int(settings.get("_env_warm", -1))
+    d.env_rounds = int(settings.get("_env_rounds", -1))
     ac = settings.get("analog_character", 0)
     if ac > 0:                                                    # :192
         cf = ac / 100.0

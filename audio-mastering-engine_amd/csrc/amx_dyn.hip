@@ -1,172 +1,111 @@
 // amx_dyn.hip -- multiband compressor dynamics (pydub compress_dynamic_range,
 // audio_mastering_engine.py:306-308) and the overlay (:309).
+//
+// Per band b and frame i:
+//   r_i   = audioop.rms of frames [max(i-look, 0), i)          (exact integer sums)
+//   m_i   = (1 - 1/ratio) * max(20 log10(r_i / thr), 0)        (host tables, C libm)
+//   att  <- (r_i > thr and att <= m_i) ? min(att + m_i/A, m_i) : max(att - m_i/R, 0)
+//   out_i = audioop.mul(frame_i, 10^(-att/20))   if att != 0
+//
+// r is embarrassingly parallel (k_rms: block prefix sums).  The envelope is a
+// sequential nonlinear recurrence; it is parallelised by exact speculation:
+//   round 0 (k_env0): every envelope segment of Le frames runs from att = 0 started
+//     W frames earlier (the trajectories of this recurrence coincide after clamp
+//     events, so the warm-up usually lands exactly on the true state) and writes its
+//     gained output, its start guess s_j and end state e_j;
+//   rounds 1..R (k_envfix): segment j takes its true start from the end of the
+//     nearest earlier segment that has any over-threshold frame (below-threshold
+//     frames hold the state: m = 0 makes both steps the identity), and if it differs
+//     from s_j re-runs both trajectories in lockstep until they coincide, rewriting
+//     the gained output up to there;
+//   k_envseq: a final in-order walk per (chunk, band) fixes whatever is still
+//     inconsistent, so the result is exact whatever the signal; it costs one parallel
+//     consistency scan when the rounds already converged.
+// Every value is produced by the reference's own operation sequence from the true
+// start state, so the envelope is bit-exact, not approximate.
 #include "amx_dev.hpp"
 
 namespace amx {
 
-// --------------------------------------------- compressor RMS detector (exact)
-// r_i = audioop.rms of frames [max(i-look,0), i) of the band, both channels:
-// (unsigned)sqrt(S / count) with S the exact integer sum of squares.
+#define AMX_TAB 32769
+
+// ----------------------------------------- compressor RMS detector (exact)
+// One workgroup = AMX_RMS_F frames of one (chunk, band); squares of the window
+// [base - look, base + AMX_RMS_F) are prefix-summed in LDS (exact int64), so
+// S_i = P(i) - P(max(i - look, 0)) with no sequential sliding window.
+#define AMX_RMS_F 1024
+#define AMX_RMS_MAXLOOK 1024
 __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ cdp,
                                                    const ChunkDev *__restrict__ chunks,
-                                                   const SegDev *__restrict__ segs, int n_seg,
                                                    const uint32_t *__restrict__ bands,
                                                    uint16_t *__restrict__ rr, int64_t nloc) {
-    int j = blockIdx.x * blockDim.x + threadIdx.x;
-    int b = blockIdx.y;
-    if (j >= n_seg) return;
+    constexpr int N = AMX_RMS_F + AMX_RMS_MAXLOOK;
+    constexpr int PER = N / AMX_BLOCK;                 // 8 values per thread
+    __shared__ long long P[N];
+    __shared__ long long wsum[AMX_BLOCK / 64];
     const int look = cdp->look;
-    const SegDev sg = segs[j];
-    const ChunkDev ch = chunks[sg.chunk];
+    const int c = blockIdx.y, b = blockIdx.z;
+    const ChunkDev ch = chunks[c];
+    const int64_t base = (int64_t)blockIdx.x * AMX_RMS_F;
+    if (base >= ch.n) return;                          // block-uniform
     const uint32_t *x = bands + b * nloc + ch.loc_off;
     uint16_t *r = rr + b * nloc + ch.loc_off;
-    const int64_t p0 = sg.pos;
-    int64_t lo = p0 - look < 0 ? 0 : p0 - look;
-    int64_t S = 0;
-    for (int64_t f = lo; f < p0; f++) {
-        uint32_t v = x[f];
-        int64_t a = lo16(v), c = hi16(v);
-        S += a * a + c * c;
+    // LDS slot k holds frame base - look + k (frames before the chunk count as 0)
+    const int64_t f0 = base - look;
+    const int t = threadIdx.x;
+    long long v[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int k = t * PER + q;
+        const int64_t f = f0 + k;
+        const bool ok = f >= 0 && f < ch.n && k < AMX_RMS_F + look;
+        const uint32_t u = x[ok ? f : 0];
+        const long long a = lo16(u), d = hi16(u);
+        v[q] = ok ? a * a + d * d : 0;
     }
-    for (int n = 0; n < sg.len; n++) {
-        int64_t i = p0 + n;
-        int64_t wlo = i - look < 0 ? 0 : i - look;
-        int64_t cnt = 2 * (i - wlo);
-        uint32_t rms = cnt ? (uint32_t)sqrt((double)S / (double)cnt) : 0u;
+    // block inclusive scan: per-thread serial, wave scan of totals, cross-wave
+    long long run = 0;
+#pragma unroll
+    for (int q = 0; q < PER; q++) { run += v[q]; v[q] = run; }
+    long long incl = run;
+    const int lane = t & 63, w = t >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long up = __shfl_up(incl, o);
+        if (lane >= o) incl += up;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    long long wpre = 0;
+    for (int q = 0; q < w; q++) wpre += wsum[q];
+    const long long excl = wpre + incl - run;
+#pragma unroll
+    for (int q = 0; q < PER; q++) P[t * PER + q] = excl + v[q];
+    __syncthreads();
+    // frame i = base + n uses slots [n, n + look) -> P[n + look - 1] - P[n - 1]
+    for (int n = t; n < AMX_RMS_F; n += AMX_BLOCK) {
+        const int64_t i = base + n;
+        if (i >= ch.n) break;
+        const int64_t wlo = i - look < 0 ? 0 : i - look;
+        const int64_t cnt = 2 * (i - wlo);
+        const long long S = P[n + look - 1] - (n > 0 ? P[n - 1] : 0);
+        const uint32_t rms = cnt ? (uint32_t)sqrt((double)S / (double)cnt) : 0u;
         r[i] = (uint16_t)(rms > 65535u ? 65535u : rms);
-        // slide: add frame i, drop frame i-look
-        uint32_t v = x[i];
-        int64_t a = lo16(v), c = hi16(v);
-        S += a * a + c * c;
-        if (i - look >= 0) {
-            uint32_t u = x[i - look];
-            int64_t a2 = lo16(u), c2 = hi16(u);
-            S -= a2 * a2 + c2 * c2;
-        }
     }
 }
 
-// pydub envelope step (compress_dynamic_range inner loop), exact.
+// --------------------------------------------------------- envelope helpers
+struct EnvTab {
+    const double *m, *inc, *dec;
+    int rthr;
+};
+
+// pydub envelope step, exact, branch-free (both candidates, then select)
 __device__ __forceinline__ double env_step(double att, bool over, double m, double inc,
                                            double dec) {
-    if (over && att <= m) {
-        att = att + inc;
-        att = (m < att) ? m : att;          // min(attenuation, max_attenuation)
-    } else {
-        att = att - dec;
-        att = (0.0 > att) ? 0.0 : att;      // max(attenuation, 0)
-    }
-    return att;
-}
-
-#define AMX_TAB 32769
-// speculative envelope: guess from a warm-up started at att = 0
-__global__ void __launch_bounds__(AMX_BLOCK) k_env(const ChainDev *__restrict__ cdp,
-                                                   const ChunkDev *__restrict__ chunks,
-                                                   const SegDev *__restrict__ segs, int n_seg,
-                                                   const uint16_t *__restrict__ rr,
-                                                   const double *__restrict__ tabs,
-                                                   double *__restrict__ att_out,
-                                                   double *__restrict__ guess,
-                                                   double *__restrict__ endv, int64_t nloc,
-                                                   int warm) {
-    int j = blockIdx.x * blockDim.x + threadIdx.x;
-    int b = blockIdx.y;
-    if (j >= n_seg) return;
-    const SegDev sg = segs[j];
-    const ChunkDev ch = chunks[sg.chunk];
-    const uint16_t *r = rr + b * nloc + ch.loc_off;
-    double *ao = att_out + b * nloc + ch.loc_off;
-    const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
-    const double *it = mt + AMX_TAB, *dt = mt + 2 * AMX_TAB;
-    const int rthr = cdp->rthr[b];
-    double att = 0.0;
-    int64_t w0 = sg.pos - warm;
-    if (w0 < 0) w0 = 0;
-    for (int64_t f = w0; f < sg.pos; f++) {
-        int rv = r[f];
-        att = env_step(att, rv >= rthr, mt[rv], it[rv], dt[rv]);
-    }
-    guess[(int64_t)b * n_seg + j] = att;
-    for (int n = 0; n < sg.len; n++) {
-        int rv = r[sg.pos + n];
-        att = env_step(att, rv >= rthr, mt[rv], it[rv], dt[rv]);
-        ao[sg.pos + n] = att;
-    }
-    endv[(int64_t)b * n_seg + j] = att;
-}
-
-// verification / fix-up: one wave per (chunk, band).  Walks the chunk's segment
-// hand-offs; each mismatch (guess_j != end_{j-1}) is re-run from the exact start
-// until the new trajectory coincides with the stored one.
-__global__ void __launch_bounds__(64) k_fix(const ChainDev *__restrict__ cdp,
-                                            const ChunkDev *__restrict__ chunks,
-                                            const SegDev *__restrict__ segs, int n_seg,
-                                            const uint16_t *__restrict__ rr,
-                                            const double *__restrict__ tabs,
-                                            double *__restrict__ att_arr,
-                                            double *__restrict__ guess,
-                                            double *__restrict__ endv, int64_t nloc) {
-    const int c = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
-    const ChunkDev ch = chunks[c];
-    const uint16_t *r = rr + b * nloc + ch.loc_off;
-    double *aa = att_arr + b * nloc + ch.loc_off;
-    double *gs = guess + (int64_t)b * n_seg;
-    double *en = endv + (int64_t)b * n_seg;
-    const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
-    const double *it = mt + AMX_TAB, *dt = mt + 2 * AMX_TAB;
-    const int rthr = cdp->rthr[b];
-    const int s0 = ch.seg0, s1 = ch.seg0 + ch.nseg;
-    int cur = s0 + 1;
-    while (true) {
-        int found = 0x7fffffff;
-        for (int base = cur; base < s1; base += 64) {
-            int jj = base + lane;
-            bool bad = false;
-            if (jj < s1) bad = !(gs[jj] == en[jj - 1]);
-            unsigned long long m = __ballot(bad);
-            if (m) { found = base + __ffsll((long long)m) - 1; break; }
-        }
-        if (found >= s1) break;
-        const SegDev sg = segs[found];
-        double att = en[found - 1];
-        bool coincided = false;
-        for (int base = 0; base < sg.len && !coincided; base += 64) {
-            const int n = base + lane;
-            const bool valid = n < sg.len;
-            const int64_t f = sg.pos + n;
-            int rv = valid ? (int)r[f] : 0;
-            double mv = mt[rv], iv = it[rv], dv = dt[rv];
-            bool over = valid && rv >= rthr;
-            double old = valid ? aa[f] : 0.0;
-            double nv;
-            if (__ballot(over) == 0ull) {
-                nv = att;                       // below threshold: state held
-            } else {
-                nv = 0.0;
-                const int cnt = sg.len - base < 64 ? sg.len - base : 64;
-                for (int k = 0; k < cnt; k++) {
-                    double mk = __shfl(mv, k), ik = __shfl(iv, k), dk = __shfl(dv, k);
-                    int ok = __shfl((int)over, k);
-                    att = env_step(att, ok != 0, mk, ik, dk);
-                    if (lane == k) nv = att;
-                }
-            }
-            unsigned long long same = __ballot(valid && nv == old);
-            if (same) {
-                int k = __ffsll((long long)same) - 1;
-                if (valid && lane < k) aa[f] = nv;
-                coincided = true;
-            } else if (valid) {
-                aa[f] = nv;
-            }
-        }
-        if (!coincided && lane == 0) en[found] = att;
-        if (lane == 0) gs[found] = en[found - 1];
-        __threadfence_block();
-        __syncthreads();
-        cur = found + 1;
-    }
+    const double up = fmin(att + inc, m);          // attenuation += inc; min(., max_att)
+    const double dn = fmax(att - dec, 0.0);        // attenuation -= dec; max(., 0)
+    return (over && att <= m) ? up : dn;
 }
 
 // audioop.mul clamp + floor (CPython Modules/audioop.c fbound)
@@ -177,39 +116,266 @@ __device__ __forceinline__ int mul16(int v, double f) {
     return (int)floor(val);
 }
 
-// gains + overlay (:306-309) -> chunk output (pydub ms-rounded length)
-__global__ void __launch_bounds__(AMX_BLOCK) k_apply(const ChunkDev *__restrict__ chunks,
-                                                     const uint32_t *__restrict__ bands,
-                                                     const double *__restrict__ att,
-                                                     uint32_t *__restrict__ out, int64_t nloc,
-                                                     const int64_t *__restrict__ n2tab) {
+// the gained frame for attenuation att (:306-308 output, audioop.mul)
+__device__ __forceinline__ uint32_t gain_frame(uint32_t v, double att) {
+    if (att == 0.0) return v;
+    const double f = exp10(-att / 20.0);
+    return pack2((int16_t)mul16(lo16(v), f), (int16_t)mul16(hi16(v), f));
+}
+
+#define AMX_ENV_B 8   // frames per batch: table gathers issued ahead of the chain
+
+// run the envelope over frames [f0, f1) of r from att; optionally write gained output
+template <bool OUT>
+__device__ __forceinline__ double env_run(const EnvTab &T, const uint16_t *r, int64_t f0,
+                                          int64_t f1, double att, bool &any_over,
+                                          const uint32_t *x, uint32_t *g) {
+    for (int64_t f = f0; f < f1; f += AMX_ENV_B) {
+        double m[AMX_ENV_B], inc[AMX_ENV_B], dec[AMX_ENV_B];
+        bool ov[AMX_ENV_B];
+        uint32_t xv[AMX_ENV_B];
+#pragma unroll
+        for (int q = 0; q < AMX_ENV_B; q++) {
+            const bool ok = f + q < f1;
+            const int rl = r[ok ? f + q : f0];         // clamped, unconditional (tile_load)
+            const int rv = ok ? rl : 0;
+            ov[q] = ok && rv >= T.rthr;
+            m[q] = T.m[rv];
+            inc[q] = T.inc[rv];
+            dec[q] = T.dec[rv];
+            if (OUT) xv[q] = x[ok ? f + q : f0];
+        }
+#pragma unroll
+        for (int q = 0; q < AMX_ENV_B; q++) {
+            if (f + q >= f1) break;
+            att = env_step(att, ov[q], m[q], inc[q], dec[q]);
+            any_over |= ov[q];
+            if (OUT) g[f + q] = gain_frame(xv[q], att);
+        }
+    }
+    return att;
+}
+
+// ------------------------------------------------------- round 0: speculation
+// One thread per (envelope segment, band).  s = state at the segment start from a
+// warm-up of W frames begun at rest; e = state at the segment end; act = the
+// segment has an over-threshold frame (else its transfer is the identity).
+__global__ void __launch_bounds__(AMX_BLOCK) k_env0(const ChainDev *__restrict__ cdp,
+                                                    const ChunkDev *__restrict__ chunks,
+                                                    const SegDev *__restrict__ es, int n_es,
+                                                    const uint16_t *__restrict__ rr,
+                                                    const uint32_t *__restrict__ bands,
+                                                    const double *__restrict__ tabs,
+                                                    uint32_t *__restrict__ gained,
+                                                    double *__restrict__ sv,
+                                                    double *__restrict__ ev,
+                                                    int *__restrict__ act, int64_t nloc,
+                                                    int warm) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = blockIdx.y;
+    if (j >= n_es) return;
+    const SegDev sg = es[j];
+    const ChunkDev ch = chunks[sg.chunk];
+    const uint16_t *r = rr + b * nloc + ch.loc_off;
+    const uint32_t *x = bands + b * nloc + ch.loc_off;
+    uint32_t *g = gained + b * nloc + ch.loc_off;
+    const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
+    const EnvTab T{mt, mt + AMX_TAB, mt + 2 * AMX_TAB, cdp->rthr[b]};
+    int64_t w0 = sg.pos - warm;
+    if (w0 < 0) w0 = 0;
+    bool any = false, dummy = false;
+    double att = env_run<false>(T, r, w0, sg.pos, 0.0, dummy, nullptr, nullptr);
+    sv[(int64_t)b * n_es + j] = att;
+    att = env_run<true>(T, r, sg.pos, sg.pos + sg.len, att, any, x, g);
+    ev[(int64_t)b * n_es + j] = att;
+    act[(int64_t)b * n_es + j] = any ? 1 : 0;
+}
+
+// prev[j] = the nearest earlier active segment of the same chunk (or -1): the
+// segment whose end state is segment j's true start.  One wave per (chunk, band).
+__global__ void __launch_bounds__(64) k_env_prev(const ChunkDev *__restrict__ chunks,
+                                                 const int *__restrict__ eseg0,
+                                                 const int *__restrict__ neseg, int n_es,
+                                                 const int *__restrict__ act,
+                                                 int *__restrict__ prev) {
+    const int c = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
+    const int s0 = eseg0[c], s1 = s0 + neseg[c];
+    const int *A = act + (int64_t)b * n_es;
+    int *P = prev + (int64_t)b * n_es;
+    int carry = -1;                                    // last active index before the batch
+    for (int base = s0; base < s1; base += 64) {
+        const int j = base + lane;
+        const bool a = j < s1 && A[j] != 0;
+        // inclusive max-scan of (a ? j : -1); prev[j] = exclusive value
+        int v = a ? j : -1;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int up = __shfl_up(v, o);
+            if (lane >= o) v = max(v, up);
+        }
+        int excl = __shfl_up(v, 1);
+        if (lane == 0) excl = -1;
+        excl = max(excl, carry);
+        if (j < s1) P[j] = excl;
+        carry = max(carry, __shfl(v, 63));
+    }
+}
+
+// re-run segment j from the new start `ns` while re-running the stored trajectory
+// from `os` in lockstep; rewrite the gained output until the two coincide.
+// Returns the segment's end state (old end if they coincided).
+__device__ double env_rerun(const EnvTab &T, const uint16_t *r, const uint32_t *x, uint32_t *g,
+                            int64_t f0, int64_t f1, double os, double ns, double old_end) {
+    double a = os, c = ns;
+    for (int64_t f = f0; f < f1; f += AMX_ENV_B) {
+        double m[AMX_ENV_B], inc[AMX_ENV_B], dec[AMX_ENV_B];
+        bool ov[AMX_ENV_B];
+        uint32_t xv[AMX_ENV_B];
+#pragma unroll
+        for (int q = 0; q < AMX_ENV_B; q++) {
+            const bool ok = f + q < f1;
+            const int rl = r[ok ? f + q : f0];         // clamped, unconditional (tile_load)
+            const int rv = ok ? rl : 0;
+            ov[q] = ok && rv >= T.rthr;
+            m[q] = T.m[rv];
+            inc[q] = T.inc[rv];
+            dec[q] = T.dec[rv];
+            xv[q] = x[ok ? f + q : f0];
+        }
+#pragma unroll
+        for (int q = 0; q < AMX_ENV_B; q++) {
+            if (f + q >= f1) return c;
+            a = env_step(a, ov[q], m[q], inc[q], dec[q]);
+            c = env_step(c, ov[q], m[q], inc[q], dec[q]);
+            if (a == c) return old_end;                // identical from here on
+            g[f + q] = gain_frame(xv[q], c);
+        }
+    }
+    return c;
+}
+
+// ------------------------------------------------ rounds: parallel fix-up
+// Reads e_in (previous round), writes e_out; s is updated in place (segment-owned).
+__global__ void __launch_bounds__(AMX_BLOCK) k_envfix(const ChainDev *__restrict__ cdp,
+                                                      const ChunkDev *__restrict__ chunks,
+                                                      const SegDev *__restrict__ es, int n_es,
+                                                      const uint16_t *__restrict__ rr,
+                                                      const uint32_t *__restrict__ bands,
+                                                      const double *__restrict__ tabs,
+                                                      uint32_t *__restrict__ gained,
+                                                      double *__restrict__ sv,
+                                                      const double *__restrict__ e_in,
+                                                      double *__restrict__ e_out,
+                                                      const int *__restrict__ act,
+                                                      const int *__restrict__ prev,
+                                                      int64_t nloc) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = blockIdx.y;
+    if (j >= n_es) return;
+    const int64_t k = (int64_t)b * n_es + j;
+    const int p = prev[k];
+    const double ns = p >= 0 ? e_in[(int64_t)b * n_es + p] : 0.0;
+    const double os = sv[k];
+    if (ns == os) { e_out[k] = e_in[k]; return; }
+    const SegDev sg = es[j];
+    const ChunkDev ch = chunks[sg.chunk];
+    const uint32_t *x = bands + b * nloc + ch.loc_off;
+    uint32_t *g = gained + b * nloc + ch.loc_off;
+    if (!act[k]) {
+        // identity transfer: the held state is the new start for every frame
+        for (int64_t f = sg.pos; f < sg.pos + sg.len; f++) g[f] = gain_frame(x[f], ns);
+        e_out[k] = ns;
+    } else {
+        const uint16_t *r = rr + b * nloc + ch.loc_off;
+        const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
+        const EnvTab T{mt, mt + AMX_TAB, mt + 2 * AMX_TAB, cdp->rthr[b]};
+        e_out[k] = env_rerun(T, r, x, g, sg.pos, sg.pos + sg.len, os, ns, e_in[k]);
+    }
+    sv[k] = ns;
+}
+
+// --------------------------------------- final in-order walk (exactness net)
+// One wave per (chunk, band): find the first segment whose start disagrees with
+// its predecessor's end (64 at a time), fix it on lane 0, continue after it.
+__global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
+                                               const ChunkDev *__restrict__ chunks,
+                                               const SegDev *__restrict__ es, int n_es,
+                                               const int *__restrict__ eseg0,
+                                               const int *__restrict__ neseg,
+                                               const uint16_t *__restrict__ rr,
+                                               const uint32_t *__restrict__ bands,
+                                               const double *__restrict__ tabs,
+                                               uint32_t *__restrict__ gained,
+                                               double *__restrict__ sv, double *__restrict__ ev,
+                                               const int *__restrict__ act,
+                                               const int *__restrict__ prev, int64_t nloc) {
+    const int c = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
+    const int s0 = eseg0[c], s1 = s0 + neseg[c];
+    const ChunkDev ch = chunks[c];
+    const uint16_t *r = rr + b * nloc + ch.loc_off;
+    const uint32_t *x = bands + b * nloc + ch.loc_off;
+    uint32_t *g = gained + b * nloc + ch.loc_off;
+    const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
+    const EnvTab T{mt, mt + AMX_TAB, mt + 2 * AMX_TAB, cdp->rthr[b]};
+    double *S = sv + (int64_t)b * n_es, *E = ev + (int64_t)b * n_es;
+    const int *A = act + (int64_t)b * n_es, *Pv = prev + (int64_t)b * n_es;
+    int cur = s0;
+    while (cur < s1) {
+        int found = s1;
+        for (int base = cur; base < s1; base += 64) {
+            const int j = base + lane;
+            bool bad = false;
+            if (j < s1) {
+                const int p = Pv[j];
+                const double ns = p >= 0 ? E[p] : 0.0;
+                bad = !(ns == S[j]);
+            }
+            const unsigned long long m = __ballot(bad);
+            if (m) { found = base + __ffsll((long long)m) - 1; break; }
+        }
+        if (found >= s1) break;
+        if (lane == 0) {
+            const SegDev sg = es[found];
+            const int p = Pv[found];
+            const double ns = p >= 0 ? E[p] : 0.0;
+            if (!A[found]) {
+                for (int64_t f = sg.pos; f < sg.pos + sg.len; f++) g[f] = gain_frame(x[f], ns);
+                E[found] = ns;
+            } else {
+                E[found] = env_rerun(T, r, x, g, sg.pos, sg.pos + sg.len, S[found], ns, E[found]);
+            }
+            S[found] = ns;
+        }
+        __threadfence_block();
+        cur = found + 1;
+    }
+}
+
+// ------------------------------------------------------------------- overlay
+// low.overlay(mid).overlay(high) (:309) of the gained bands -> chunk output with
+// pydub's ms-rounded lengths: n1 after the first overlay, n2 = out_n after the second.
+__global__ void __launch_bounds__(AMX_BLOCK) k_overlay(const ChunkDev *__restrict__ chunks,
+                                                       const uint32_t *__restrict__ gained,
+                                                       uint32_t *__restrict__ out, int64_t nloc,
+                                                       const int64_t *__restrict__ n1tab) {
     const int c = blockIdx.y;
     const ChunkDev ch = chunks[c];
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t n2 = ch.out_n;            // final (second overlay) length
+    const int64_t n2 = ch.out_n;
     if (i >= n2) return;
-    const int64_t n1 = n2tab[c];            // first overlay length
+    const int64_t n1 = n1tab[c];
     uint32_t res = 0;
     if (i < ch.n) {
-        int acc[3][2];
-#pragma unroll
-        for (int b = 0; b < 3; b++) {
-            uint32_t v = bands[b * nloc + ch.loc_off + i];
-            double a = att[b * nloc + ch.loc_off + i];
-            int l = lo16(v), r = hi16(v);
-            if (a != 0.0) {
-                double f = exp10(-a / 20.0);
-                l = mul16(l, f);
-                r = mul16(r, f);
-            }
-            acc[b][0] = l;
-            acc[b][1] = r;
-        }
+        const uint32_t v0 = gained[ch.loc_off + i];
+        const uint32_t v1 = gained[nloc + ch.loc_off + i];
+        const uint32_t v2 = gained[2 * nloc + ch.loc_off + i];
         int16_t o[2];
 #pragma unroll
         for (int k = 0; k < 2; k++) {
-            int s1 = i < n1 ? (int)sat16(acc[0][k] + acc[1][k]) : 0;
-            o[k] = sat16(s1 + acc[2][k]);
+            const int a0 = k ? hi16(v0) : lo16(v0), a1 = k ? hi16(v1) : lo16(v1);
+            const int a2 = k ? hi16(v2) : lo16(v2);
+            const int s1 = i < n1 ? (int)sat16(a0 + a1) : 0;
+            o[k] = sat16(s1 + a2);
         }
         res = pack2(o[0], o[1]);
     }
@@ -217,43 +383,59 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_apply(const ChunkDev *__restrict_
 }
 
 // ---------------------------------------------------------------- launchers
-hipError_t launch_rms(const Launch &l, const int16_t *bands, uint16_t *r, int64_t nloc) {
-    dim3 g = grid1(l.n_seg);
-    g.y = 3;
-    hipLaunchKernelGGL(k_rms, g, dim3(AMX_BLOCK), 0, l.stream, l.cd, l.chunks, l.segs, l.n_seg,
-                       reinterpret_cast<const uint32_t *>(bands), r, nloc);
-    return hipGetLastError();
-}
-
-hipError_t launch_env(const Launch &l, const uint16_t *r, const double *tabs, double *att,
-                      double *guess, double *endv, int64_t nloc, int warm) {
-    dim3 g = grid1(l.n_seg);
-    g.y = 3;
-    hipLaunchKernelGGL(k_env, g, dim3(AMX_BLOCK), 0, l.stream, l.cd, l.chunks, l.segs, l.n_seg,
-                       r, tabs, att, guess, endv, nloc, warm);
-    return hipGetLastError();
-}
-
-hipError_t launch_fix(const Launch &l, const uint16_t *r, const double *tabs, double *att,
-                      double *guess, double *endv, int64_t nloc) {
-    if (l.n_chunks <= 0) return hipSuccess;
-    dim3 g((unsigned)l.n_chunks, 3);
-    hipLaunchKernelGGL(k_fix, g, dim3(64), 0, l.stream, l.cd, l.chunks, l.segs, l.n_seg, r, tabs,
-                       att, guess, endv, nloc);
-    return hipGetLastError();
-}
-
-hipError_t launch_apply_n1(const Launch &l, const int16_t *bands, const double *att,
-                           int16_t *out, int64_t nloc, int64_t max_chunk_out,
-                           const int64_t *n1tab) {
-    dim3 g = grid1(max_chunk_out);
-    g.y = (unsigned)l.n_chunks;
+hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *r) {
+    if (d.look > AMX_RMS_MAXLOOK) return hipErrorInvalidValue;
+    dim3 g((unsigned)((d.max_chunk_n + AMX_RMS_F - 1) / AMX_RMS_F), (unsigned)d.n_chunks, 3);
     if (empty(g)) return hipSuccess;
-    hipLaunchKernelGGL(k_apply, g, dim3(AMX_BLOCK), 0, l.stream, l.chunks,
-                       reinterpret_cast<const uint32_t *>(bands), att,
-                       reinterpret_cast<uint32_t *>(out), nloc, n1tab);
+    hipLaunchKernelGGL(k_rms, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks,
+                       reinterpret_cast<const uint32_t *>(bands), r, d.nloc);
     return hipGetLastError();
 }
 
+hipError_t launch_env(const DynLaunch &d, const uint16_t *r, const int16_t *bands,
+                      int16_t *gained, double *sv, double *e0, double *e1, int *act, int *prev,
+                      int rounds) {
+    if (d.n_es <= 0) return hipSuccess;
+    const uint32_t *x = reinterpret_cast<const uint32_t *>(bands);
+    uint32_t *g = reinterpret_cast<uint32_t *>(gained);
+    dim3 grid = grid1(d.n_es);
+    grid.y = 3;
+    hipLaunchKernelGGL(k_env0, grid, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, d.es, d.n_es, r, x,
+                       d.tabs, g, sv, e0, act, d.nloc, d.warm);
+    hipLaunchKernelGGL(k_env_prev, dim3((unsigned)d.n_chunks, 3), dim3(64), 0, d.st, d.chunks,
+                       d.eseg0, d.neseg, d.n_es, act, prev);
+    double *ein = e0, *eout = e1;
+    for (int k = 0; k < rounds; k++) {
+        hipLaunchKernelGGL(k_envfix, grid, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, d.es, d.n_es,
+                           r, x, d.tabs, g, sv, ein, eout, act, prev, d.nloc);
+        double *tmp = ein;
+        ein = eout;
+        eout = tmp;
+    }
+    return hipGetLastError();
+}
+
+// ends: the array the last round wrote (e0 if rounds is even, else e1)
+hipError_t launch_envseq(const DynLaunch &d, const uint16_t *r, const int16_t *bands,
+                         int16_t *gained, double *sv, double *ends, const int *act,
+                         const int *prev) {
+    if (d.n_es <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_envseq, dim3((unsigned)d.n_chunks, 3), dim3(64), 0, d.st, d.cd, d.chunks,
+                       d.es, d.n_es, d.eseg0, d.neseg, r,
+                       reinterpret_cast<const uint32_t *>(bands), d.tabs,
+                       reinterpret_cast<uint32_t *>(gained), sv, ends, act, prev, d.nloc);
+    return hipGetLastError();
+}
+
+hipError_t launch_overlay(const DynLaunch &d, const int16_t *gained, int16_t *out,
+                          int64_t max_chunk_out, const int64_t *n1tab) {
+    dim3 g = grid1(max_chunk_out);
+    g.y = (unsigned)d.n_chunks;
+    if (empty(g)) return hipSuccess;
+    hipLaunchKernelGGL(k_overlay, g, dim3(AMX_BLOCK), 0, d.st, d.chunks,
+                       reinterpret_cast<const uint32_t *>(gained),
+                       reinterpret_cast<uint32_t *>(out), d.nloc, n1tab);
+    return hipGetLastError();
+}
 
 }  // namespace amx

@@ -116,14 +116,27 @@ hipError_t launch_front2(const Launch &l, int mask, const int16_t *a16, const do
                          const double *Gkw, double *e_kw, uint32_t *pk);
 hipError_t launch_xover2(const Launch &l, const int16_t *p16, const double *s_x,
                          int16_t *bands, int64_t nloc);
-hipError_t launch_rms(const Launch &l, const int16_t *bands, uint16_t *r, int64_t nloc);
-hipError_t launch_env(const Launch &l, const uint16_t *r, const double *tabs, double *att,
-                      double *guess, double *endv, int64_t nloc, int warm);
-hipError_t launch_fix(const Launch &l, const uint16_t *r, const double *tabs, double *att,
-                      double *guess, double *endv, int64_t nloc);
-hipError_t launch_apply_n1(const Launch &l, const int16_t *bands, const double *att,
-                           int16_t *out, int64_t nloc, int64_t max_chunk_out,
-                           const int64_t *n1tab);
+struct DynLaunch {
+    const ChainDev *cd;
+    const ChunkDev *chunks;
+    int n_chunks;
+    const SegDev *es;            // envelope segments (Le frames, per chunk)
+    int n_es;
+    const int *eseg0, *neseg;    // per chunk: first envelope segment, count
+    int64_t nloc, max_chunk_n;
+    int look, warm;
+    const double *tabs;
+    hipStream_t st;
+};
+hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *r);
+hipError_t launch_env(const DynLaunch &d, const uint16_t *r, const int16_t *bands,
+                      int16_t *gained, double *sv, double *e0, double *e1, int *act, int *prev,
+                      int rounds);
+hipError_t launch_envseq(const DynLaunch &d, const uint16_t *r, const int16_t *bands,
+                         int16_t *gained, double *sv, double *ends, const int *act,
+                         const int *prev);
+hipError_t launch_overlay(const DynLaunch &d, const int16_t *gained, int16_t *out,
+                          int64_t max_chunk_out, const int64_t *n1tab);
 // loudness
 hipError_t launch_kw1(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L,
                       const int16_t *x, const double *G, double *e, uint32_t *pk,

@@ -161,11 +161,15 @@ struct amx_plan {
     int L = 256, Lkw = 512, hop = 0;
     int mask = 0, D = 0;
     int lev_eq = 0, lev_x = 0, lev_kw = 0;
-    int mb = 0, warm = 512;
+    int mb = 0;
+    int Le = 1024, warm = 1024, rounds = 4;   // compressor envelope segments (amx_dyn.hip)
+    int n_es = 0;
+    std::vector<SegDev> esegs;
+    std::vector<int> eseg0, neseg;
     int fuse_kw = 0;        // loudness pass-1 GEMV + peak run inside k_front2
     int n_tracks = 0, n_chunks = 0, n_seg = 0, n_kseg = 0, n_blk = 0, n_kblk = 0;
     int64_t max_nkseg = 0;
-    int64_t nloc = 0, out_frames = 0, max_chunk_out = 0, max_span = 0;
+    int64_t nloc = 0, out_frames = 0, max_chunk_out = 0, max_span = 0, max_chunk_n = 0;
     std::vector<ChunkDev> chunks;
     std::vector<SegDev> segs;
     std::vector<KwSegDev> ksegs;
@@ -181,6 +185,8 @@ struct amx_plan {
     KwSegDev *d_ksegs = nullptr;
     SpanDev *d_spans = nullptr;
     ScanBlk *d_blks = nullptr, *d_kblks = nullptr;
+    SegDev *d_esegs = nullptr;
+    int *d_eseg0 = nullptr, *d_neseg = nullptr;
     int64_t *d_n1 = nullptr;
     double *d_G = nullptr, *d_M = nullptr, *d_Mp = nullptr;
     double *d_Gx = nullptr, *d_Mx = nullptr, *d_Mpx = nullptr;
@@ -192,7 +198,8 @@ struct amx_plan {
     float *d_lut = nullptr;
     // workspace offsets
     size_t ws_bytes = 0;
-    size_t o_a16, o_e, o_s, o_p16, o_ex, o_sx, o_bands, o_r, o_att, o_guess, o_end;
+    size_t o_a16, o_e, o_s, o_p16, o_ex, o_sx, o_bands, o_r, o_gain, o_esv, o_ee0, o_ee1, o_eact,
+        o_eprev;
     size_t o_ekw, o_skw, o_parts, o_phop;
     size_t o_eb, o_ebx, o_ebk, o_pk;
     amx::ScanPlan scan_eq() const { return {D, n_blk, lev_eq, d_blks, d_M, d_Mp}; }
@@ -258,6 +265,8 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     if (!p) return fail(AMX_ENOMEM, "out of memory");
     p->desc = *desc;
     const int fs = desc->sample_rate;
+    if (desc->env_warm_frames >= 0) p->warm = desc->env_warm_frames;
+    if (desc->env_rounds >= 0) p->rounds = desc->env_rounds;
     p->L = seg_frames > 0 ? seg_frames : 256;
     p->L = (p->L + AMX_TF_FRAMES - 1) / AMX_TF_FRAMES * AMX_TF_FRAMES;   // whole LDS tiles
     p->hop = (fs + 5) / 10;                    // libebur128 samples_in_100ms
@@ -430,6 +439,20 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         int64_t ns = (ch.n + p->L - 1) / p->L;
         ch.nseg = (int32_t)ns;
         add_blocks(p->blks, ch.seg0, (int32_t)ns, c);
+        if (p->mb) {   // envelope segments of the compressor (Le frames)
+            const int64_t ne = (ch.n + p->Le - 1) / p->Le;
+            p->eseg0.push_back((int)p->esegs.size());
+            p->neseg.push_back((int)ne);
+            for (int64_t k = 0; k < ne; k++) {
+                SegDev e{};
+                e.pos = k * p->Le;
+                e.chunk = c;
+                e.len = (int32_t)((ch.n - e.pos) < p->Le ? (ch.n - e.pos) : p->Le);
+                e.first = p->eseg0.back();
+                e.last = (k == ne - 1) ? 1 : 0;
+                p->esegs.push_back(e);
+            }
+        }
         for (int64_t k = 0; k < ns; k++) {
             SegDev s{};
             s.pos = k * p->L;
@@ -448,10 +471,12 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         p->chunks.push_back(ch);
         p->n1tab.push_back(n1);
         p->max_chunk_out = n2 > p->max_chunk_out ? n2 : p->max_chunk_out;
+        p->max_chunk_n = ch.n > p->max_chunk_n ? ch.n : p->max_chunk_n;
         loc += ch.n;
         outo += n2;
     }
     p->nloc = loc;
+    p->n_es = (int)p->esegs.size();
     p->out_frames = outo;
     p->n_seg = (int)p->segs.size();
     // K-weighting segments per track span
@@ -575,6 +600,9 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     UP(p->d_blks, p->blks.data(), p->blks.size());
     UP(p->d_kblks, p->kblks.data(), p->kblks.size());
     UP(p->d_n1, p->n1tab.data(), p->n1tab.size());
+    UP(p->d_esegs, p->esegs.data(), p->esegs.size());
+    UP(p->d_eseg0, p->eseg0.data(), p->eseg0.size());
+    UP(p->d_neseg, p->neseg.data(), p->neseg.size());
     UP(p->d_G, G.data(), G.size());
     UP(p->d_M, M.data(), M.size());
     UP(p->d_Mp, Mp.data(), Mp.size());
@@ -601,10 +629,14 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         p->o_ex = (size_t)align_up(off, nseg * 2 * AMX_XO_DIM * 8);
         p->o_sx = (size_t)align_up(off, nseg * 2 * AMX_XO_DIM * 8);
         p->o_bands = (size_t)align_up(off, 3 * nl * 4);
+        const size_t ne = (size_t)p->n_es;
         p->o_r = (size_t)align_up(off, 3 * nl * 2);
-        p->o_att = (size_t)align_up(off, 3 * nl * 8);
-        p->o_guess = (size_t)align_up(off, 3 * nseg * 8);
-        p->o_end = (size_t)align_up(off, 3 * nseg * 8);
+        p->o_gain = (size_t)align_up(off, 3 * nl * 4);
+        p->o_esv = (size_t)align_up(off, 3 * ne * 8);
+        p->o_ee0 = (size_t)align_up(off, 3 * ne * 8);
+        p->o_ee1 = (size_t)align_up(off, 3 * ne * 8);
+        p->o_eact = (size_t)align_up(off, 3 * ne * 4);
+        p->o_eprev = (size_t)align_up(off, 3 * ne * 4);
     }
     const size_t nb = (size_t)p->n_blk, nkb = (size_t)p->n_kblk;
     p->o_eb = (size_t)align_up(off, nb * 2 * (D ? D : 1) * 8);
@@ -627,7 +659,8 @@ void amx_plan_free(amx_plan *p) {
     void *ptrs[] = {p->d_cd,  p->d_chunks, p->d_segs, p->d_ksegs, p->d_spans,  p->d_blks,
                     p->d_kblks, p->d_n1,   p->d_G,    p->d_M,     p->d_Mp,     p->d_Gx,
                     p->d_Mx,  p->d_Mpx,    p->d_Gkw,  p->d_Mkw,   p->d_Mpkw,   p->d_tabs,
-                    p->d_bounds, p->d_tailpow, p->d_lut, p->d_energies, p->d_carryP};
+                    p->d_bounds, p->d_tailpow, p->d_lut, p->d_energies, p->d_carryP,
+                    p->d_esegs, p->d_eseg0, p->d_neseg};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     delete p;
@@ -674,9 +707,15 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     double *sx = p->mb ? wsp<double>(d_ws, p->o_sx) : nullptr;
     int16_t *bands = p->mb ? wsp<int16_t>(d_ws, p->o_bands) : nullptr;
     uint16_t *r = p->mb ? wsp<uint16_t>(d_ws, p->o_r) : nullptr;
-    double *att = p->mb ? wsp<double>(d_ws, p->o_att) : nullptr;
-    double *guess = p->mb ? wsp<double>(d_ws, p->o_guess) : nullptr;
-    double *endv = p->mb ? wsp<double>(d_ws, p->o_end) : nullptr;
+    int16_t *gained = p->mb ? wsp<int16_t>(d_ws, p->o_gain) : nullptr;
+    double *esv = p->mb ? wsp<double>(d_ws, p->o_esv) : nullptr;
+    double *ee0 = p->mb ? wsp<double>(d_ws, p->o_ee0) : nullptr;
+    double *ee1 = p->mb ? wsp<double>(d_ws, p->o_ee1) : nullptr;
+    int *eact = p->mb ? wsp<int>(d_ws, p->o_eact) : nullptr;
+    int *eprev = p->mb ? wsp<int>(d_ws, p->o_eprev) : nullptr;
+    amx::DynLaunch dl{p->d_cd,    p->d_chunks, p->n_chunks, p->d_esegs, p->n_es,
+                      p->d_eseg0, p->d_neseg,  p->nloc,     p->max_chunk_n, p->cd.look,
+                      p->warm,    p->d_tabs,   st};
     switch (stage) {
     case AMX_STAGE_FRONT1:
         HIPCHK(amx::launch_front1(l, p->D, (p->cd.chin == 2 && !p->cd.in_s16) ? 2 : 1,
@@ -705,17 +744,19 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
         if (p->mb) HIPCHK(amx::launch_xover2(l, p16, sx, bands, p->nloc));
         break;
     case AMX_STAGE_RMS:
-        if (p->mb) HIPCHK(amx::launch_rms(l, bands, r, p->nloc));
+        if (p->mb) HIPCHK(amx::launch_rms(dl, bands, r));
         break;
     case AMX_STAGE_ENV:
-        if (p->mb) HIPCHK(amx::launch_env(l, r, p->d_tabs, att, guess, endv, p->nloc, p->warm));
+        if (p->mb) HIPCHK(amx::launch_env(dl, r, bands, gained, esv, ee0, ee1, eact, eprev, p->rounds));
         break;
     case AMX_STAGE_FIX:
-        if (p->mb) HIPCHK(amx::launch_fix(l, r, p->d_tabs, att, guess, endv, p->nloc));
+        if (p->mb)
+            HIPCHK(amx::launch_envseq(dl, r, bands, gained, esv, (p->rounds & 1) ? ee1 : ee0, eact,
+                                      eprev));
         break;
     case AMX_STAGE_APPLY:
         if (p->mb)
-            HIPCHK(amx::launch_apply_n1(l, bands, att, d_out, p->nloc, p->max_chunk_out, p->d_n1));
+            HIPCHK(amx::launch_overlay(dl, gained, d_out, p->max_chunk_out, p->d_n1));
         break;
     }
     return AMX_OK;

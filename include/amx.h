@@ -64,8 +64,8 @@ typedef struct amx_chain_desc {
     int32_t analog_on;
     float analog_drive;           /* float32(1 + 0.5*cf) */
     const float *tanh_lut;        /* 65536 float32: tanh(float32(s/32768)*drive) for
-                                     s = -32768..32767 (numpy's float32 tanh); NULL ->
-                                     device computes correctly-rounded float32 tanh */
+                                     s = -32768..32767 (numpy's float32 tanh); required
+                                     when analog_on */
     double analog_lo_ba[6];       /* butter(2,120/(fs/2),'low'):  b0 b1 b2 a0 a1 a2 */
     double analog_lo_gain;        /* 10**(cf/20) */
     double analog_hi_ba[6];       /* butter(2,12000/(fs/2),'high') */
@@ -89,6 +89,10 @@ typedef struct amx_chain_desc {
     const double *comp_m_table[3];/* optional override of max_attenuation(rms), rms=0..32768;
                                      NULL -> the plan tabulates it with the C library's
                                      log/pow, which is what CPython's math uses (pydub) */
+    /* compressor envelope parallelisation (amx_dyn.hip); results are exact for any
+     * values, these only move work between the speculative and the fix-up passes */
+    int32_t env_warm_frames;      /* speculative warm-up per envelope segment; <0 -> 1024 */
+    int32_t env_rounds;           /* parallel fix-up rounds before the in-order walk; <0 -> 4 */
 } amx_chain_desc;
 
 /* One ~30 s chunk of one track (the ffmpeg segment split, :178). */
@@ -159,10 +163,10 @@ AMX_API int amx_run_chunks(amx_plan *plan, const float *d_in, int16_t *d_out, vo
 #define AMX_STAGE_FRONT2 2   /* EQ from true state + width -> int16 (+ crossover GEMV) */
 #define AMX_STAGE_SCAN_XO 3  /* crossover scan */
 #define AMX_STAGE_XOVER 4    /* crossover -> 3 int16 bands */
-#define AMX_STAGE_RMS 5      /* exact audioop.rms detector per frame */
-#define AMX_STAGE_ENV 6      /* speculative envelope per segment */
-#define AMX_STAGE_FIX 7      /* envelope hand-off verification / re-run */
-#define AMX_STAGE_APPLY 8    /* gains + overlay -> chunk output */
+#define AMX_STAGE_RMS 5      /* exact audioop.rms detector per frame (block prefix sums) */
+#define AMX_STAGE_ENV 6      /* envelope: speculation + parallel fix rounds + gained bands */
+#define AMX_STAGE_FIX 7      /* envelope: in-order exactness walk (no-op when converged) */
+#define AMX_STAGE_APPLY 8    /* overlay of the gained bands -> chunk output */
 #define AMX_STAGE_COUNT 9
 AMX_API int amx_run_stage(amx_plan *plan, int32_t stage, const float *d_in, int16_t *d_out,
                           void *d_ws, void *stream);

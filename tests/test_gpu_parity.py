@@ -77,6 +77,28 @@ def test_multichunk_chain_vs_oracle(gpu, oracle_mod, fs, settings, seconds, seg_
     _cmp(out, ref, "chain fs=%d" % fs)
 
 
+@pytest.mark.parametrize("warm,rounds", [(0, 0), (0, 1), (64, 2), (-1, -1)])
+@pytest.mark.parametrize("signal", ["music", "mix"])
+def test_compressor_fixup_paths(gpu, oracle_mod, warm, rounds, signal):
+    """The envelope is exact however the work is split between speculation, the
+    parallel fix-up rounds and the in-order walk (amx_dyn.hip): warm-up 0 and no
+    rounds leaves everything to the walk; the music signal has long held-state
+    (below-threshold) stretches between loud passages."""
+    from amx import synth
+    fs = 48000
+    n = int(fs * 9.7)
+    if signal == "music":
+        x = synth.music_like(n, fs, 2, seed=7, peak_dbfs=-3.0)
+    else:
+        x = synth.mix_like(n, fs, 2, seed=7)
+    x16 = oracle_mod.quantize(x)
+    settings = dict(C3, _env_warm=warm, _env_rounds=rounds)
+    chunks = [(0, n // 2 + 3), (n // 2 + 3, n - (n // 2 + 3))]
+    out, _ = _chunk_chain(x16, fs, settings, chunks)
+    ref = np.concatenate([oracle_mod.chunk(x16[s:s + m], fs, C3) for s, m in chunks])
+    _cmp(out, ref, "compressor warm=%d rounds=%d %s" % (warm, rounds, signal), exact_min=1.0, tol=0)
+
+
 def test_mono_and_f32_quantise(gpu, oracle_mod):
     import torch
     from amx import synth
