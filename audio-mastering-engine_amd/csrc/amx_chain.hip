@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_front1(const ChainDev *__restrict
 // work on the output just produced -- the K filter's zero-state end state (GEMV
 // over Gkw, right-aligned for a span's final partial segment like k_kw1) and the
 // per-(segment, channel) sample peak -- so the track is not read again for it.
-#define AMX_EQ_F 8
+#define AMX_EQ_F 4   // frames per stage-major sub-tile (must divide AMX_TF)
 template <int MASK, bool MB, bool KW>
 __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const ChainDev *__restrict__ cdp,
                                                       const ChunkDev *__restrict__ chunks,

@@ -172,11 +172,21 @@ __device__ __forceinline__ void eq_tile(int negm, const double *__restrict__ sq,
         double q[6];
 #pragma unroll
         for (int i = 0; i < 6; i++) q[i] = sq[i];
+        // the uniform branch is taken outside the frame loop, so the F frames stay
+        // one basic block (a per-frame branch splits the schedule at every frame)
+        if (!(negm & 1)) {
 #pragma unroll
-        for (int f = 0; f < F; f++) {
-            const double y = bq_step(q, st.s0[0], st.s0[1], x[f]);
-            if (!(negm & 1)) x[f] = x[f] + (y - x[f]) * q[5];
-            else { const double xg = (double)(xf[f] * (float)q[5]); x[f] = xg + (y - xg); }
+            for (int f = 0; f < F; f++) {
+                const double y = bq_step(q, st.s0[0], st.s0[1], x[f]);
+                x[f] = x[f] + (y - x[f]) * q[5];
+            }
+        } else {
+#pragma unroll
+            for (int f = 0; f < F; f++) {
+                const double y = bq_step(q, st.s0[0], st.s0[1], x[f]);
+                const double xg = (double)(xf[f] * (float)q[5]);
+                x[f] = xg + (y - xg);
+            }
         }
         c = 6;
     }
@@ -206,12 +216,24 @@ __device__ __forceinline__ void eq_tile(int negm, const double *__restrict__ sq,
         double q[6];
 #pragma unroll
         for (int i = 0; i < 6; i++) q[i] = sq[c + i];
+        if (!(negm & 8)) {
 #pragma unroll
-        for (int f = 0; f < F; f++) {
-            const double y = bq_step(q, st.s3[0], st.s3[1], x[f]);
-            if (!(negm & 8)) x[f] = x[f] + (y - x[f]) * q[5];
-            else if constexpr ((MASK & 7) == 0) { const double xg = (double)(xf[f] * (float)q[5]); x[f] = xg + (y - xg); }
-            else { const double xg = x[f] * q[5]; x[f] = xg + (y - xg); }
+            for (int f = 0; f < F; f++) {
+                const double y = bq_step(q, st.s3[0], st.s3[1], x[f]);
+                x[f] = x[f] + (y - x[f]) * q[5];
+            }
+        } else {
+#pragma unroll
+            for (int f = 0; f < F; f++) {
+                const double y = bq_step(q, st.s3[0], st.s3[1], x[f]);
+                if constexpr ((MASK & 7) == 0) {
+                    const double xg = (double)(xf[f] * (float)q[5]);
+                    x[f] = xg + (y - xg);
+                } else {
+                    const double xg = x[f] * q[5];
+                    x[f] = xg + (y - xg);
+                }
+            }
         }
     }
 }

@@ -35,10 +35,16 @@ namespace amx {
 // S_i = P(i) - P(max(i - look, 0)) with no sequential sliding window.
 #define AMX_RMS_F 1024
 #define AMX_RMS_MAXLOOK 1024
+// It also looks up m_i = max_attenuation(r_i) once per frame (consecutive frames
+// have similar r, so these gathers are cache friendly) for the envelope kernels,
+// which then stream (r, m) and derive inc = m/A, dec = m/R by IEEE division --
+// the same correctly rounded quotients the host tables hold.
 __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ cdp,
                                                    const ChunkDev *__restrict__ chunks,
                                                    const uint32_t *__restrict__ bands,
-                                                   uint16_t *__restrict__ rr, int64_t nloc) {
+                                                   const double *__restrict__ tabs,
+                                                   uint16_t *__restrict__ rr,
+                                                   double *__restrict__ mm, int64_t nloc) {
     constexpr int N = AMX_RMS_F + AMX_RMS_MAXLOOK;
     constexpr int PER = N / AMX_BLOCK;                 // 8 values per thread
     __shared__ long long P[N];
@@ -50,6 +56,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
     if (base >= ch.n) return;                          // block-uniform
     const uint32_t *x = bands + b * nloc + ch.loc_off;
     uint16_t *r = rr + b * nloc + ch.loc_off;
+    double *mo = mm + b * nloc + ch.loc_off;
+    const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
     // LDS slot k holds frame base - look + k (frames before the chunk count as 0)
     const int64_t f0 = base - look;
     const int t = threadIdx.x;
@@ -90,13 +98,16 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
         const int64_t cnt = 2 * (i - wlo);
         const long long S = P[n + look - 1] - (n > 0 ? P[n - 1] : 0);
         const uint32_t rms = cnt ? (uint32_t)sqrt((double)S / (double)cnt) : 0u;
-        r[i] = (uint16_t)(rms > 65535u ? 65535u : rms);
+        const uint32_t rc = rms > 32768u ? 32768u : rms;      // |sample| <= 32768
+        r[i] = (uint16_t)rc;
+        mo[i] = mt[rc];
     }
 }
 
 // --------------------------------------------------------- envelope helpers
 struct EnvTab {
-    const double *m, *inc, *dec;
+    const double *m;     // per-frame max_attenuation (k_rms)
+    double A, R;         // attack / release frames (pydub frame_count(ms=5 / 50))
     int rthr;
 };
 
@@ -137,12 +148,13 @@ __device__ __forceinline__ double env_run(const EnvTab &T, const uint16_t *r, in
 #pragma unroll
         for (int q = 0; q < AMX_ENV_B; q++) {
             const bool ok = f + q < f1;
-            const int rl = r[ok ? f + q : f0];         // clamped, unconditional (tile_load)
-            const int rv = ok ? rl : 0;
+            const int64_t fc = ok ? f + q : f0;        // clamped, unconditional (tile_load)
+            const int rv = r[fc];
+            const double mv = T.m[fc];
             ov[q] = ok && rv >= T.rthr;
-            m[q] = T.m[rv];
-            inc[q] = T.inc[rv];
-            dec[q] = T.dec[rv];
+            m[q] = ok ? mv : 0.0;
+            inc[q] = m[q] / T.A;
+            dec[q] = m[q] / T.R;
             if (OUT) xv[q] = x[ok ? f + q : f0];
         }
 #pragma unroll
@@ -165,7 +177,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_env0(const ChainDev *__restrict__
                                                     const SegDev *__restrict__ es, int n_es,
                                                     const uint16_t *__restrict__ rr,
                                                     const uint32_t *__restrict__ bands,
-                                                    const double *__restrict__ tabs,
+                                                    const double *__restrict__ mm,
                                                     uint32_t *__restrict__ gained,
                                                     double *__restrict__ sv,
                                                     double *__restrict__ ev,
@@ -179,8 +191,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_env0(const ChainDev *__restrict__
     const uint16_t *r = rr + b * nloc + ch.loc_off;
     const uint32_t *x = bands + b * nloc + ch.loc_off;
     uint32_t *g = gained + b * nloc + ch.loc_off;
-    const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
-    const EnvTab T{mt, mt + AMX_TAB, mt + 2 * AMX_TAB, cdp->rthr[b]};
+    const EnvTab T{mm + b * nloc + ch.loc_off, 5.0 * (cdp->fs / 1000.0), 50.0 * (cdp->fs / 1000.0),
+                   cdp->rthr[b]};
     int64_t w0 = sg.pos - warm;
     if (w0 < 0) w0 = 0;
     bool any = false, dummy = false;
@@ -234,12 +246,13 @@ __device__ double env_rerun(const EnvTab &T, const uint16_t *r, const uint32_t *
 #pragma unroll
         for (int q = 0; q < AMX_ENV_B; q++) {
             const bool ok = f + q < f1;
-            const int rl = r[ok ? f + q : f0];         // clamped, unconditional (tile_load)
-            const int rv = ok ? rl : 0;
+            const int64_t fc = ok ? f + q : f0;        // clamped, unconditional (tile_load)
+            const int rv = r[fc];
+            const double mv = T.m[fc];
             ov[q] = ok && rv >= T.rthr;
-            m[q] = T.m[rv];
-            inc[q] = T.inc[rv];
-            dec[q] = T.dec[rv];
+            m[q] = ok ? mv : 0.0;
+            inc[q] = m[q] / T.A;
+            dec[q] = m[q] / T.R;
             xv[q] = x[ok ? f + q : f0];
         }
 #pragma unroll
@@ -261,7 +274,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_envfix(const ChainDev *__restrict
                                                       const SegDev *__restrict__ es, int n_es,
                                                       const uint16_t *__restrict__ rr,
                                                       const uint32_t *__restrict__ bands,
-                                                      const double *__restrict__ tabs,
+                                                      const double *__restrict__ mm,
                                                       uint32_t *__restrict__ gained,
                                                       double *__restrict__ sv,
                                                       const double *__restrict__ e_in,
@@ -287,8 +300,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_envfix(const ChainDev *__restrict
         e_out[k] = ns;
     } else {
         const uint16_t *r = rr + b * nloc + ch.loc_off;
-        const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
-        const EnvTab T{mt, mt + AMX_TAB, mt + 2 * AMX_TAB, cdp->rthr[b]};
+        const EnvTab T{mm + b * nloc + ch.loc_off, 5.0 * (cdp->fs / 1000.0),
+                       50.0 * (cdp->fs / 1000.0), cdp->rthr[b]};
         e_out[k] = env_rerun(T, r, x, g, sg.pos, sg.pos + sg.len, os, ns, e_in[k]);
     }
     sv[k] = ns;
@@ -304,7 +317,7 @@ __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
                                                const int *__restrict__ neseg,
                                                const uint16_t *__restrict__ rr,
                                                const uint32_t *__restrict__ bands,
-                                               const double *__restrict__ tabs,
+                                               const double *__restrict__ mm,
                                                uint32_t *__restrict__ gained,
                                                double *__restrict__ sv, double *__restrict__ ev,
                                                const int *__restrict__ act,
@@ -315,8 +328,8 @@ __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
     const uint16_t *r = rr + b * nloc + ch.loc_off;
     const uint32_t *x = bands + b * nloc + ch.loc_off;
     uint32_t *g = gained + b * nloc + ch.loc_off;
-    const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
-    const EnvTab T{mt, mt + AMX_TAB, mt + 2 * AMX_TAB, cdp->rthr[b]};
+    const EnvTab T{mm + b * nloc + ch.loc_off, 5.0 * (cdp->fs / 1000.0), 50.0 * (cdp->fs / 1000.0),
+                   cdp->rthr[b]};
     double *S = sv + (int64_t)b * n_es, *E = ev + (int64_t)b * n_es;
     const int *A = act + (int64_t)b * n_es, *Pv = prev + (int64_t)b * n_es;
     int cur = s0;
@@ -383,16 +396,16 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_overlay(const ChunkDev *__restric
 }
 
 // ---------------------------------------------------------------- launchers
-hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *r) {
+hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *r, double *m) {
     if (d.look > AMX_RMS_MAXLOOK) return hipErrorInvalidValue;
     dim3 g((unsigned)((d.max_chunk_n + AMX_RMS_F - 1) / AMX_RMS_F), (unsigned)d.n_chunks, 3);
     if (empty(g)) return hipSuccess;
     hipLaunchKernelGGL(k_rms, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks,
-                       reinterpret_cast<const uint32_t *>(bands), r, d.nloc);
+                       reinterpret_cast<const uint32_t *>(bands), m, r, m, d.nloc);
     return hipGetLastError();
 }
 
-hipError_t launch_env(const DynLaunch &d, const uint16_t *r, const int16_t *bands,
+hipError_t launch_env(const DynLaunch &d, const uint16_t *r, const double *m, const int16_t *bands,
                       int16_t *gained, double *sv, double *e0, double *e1, int *act, int *prev,
                       int rounds) {
     if (d.n_es <= 0) return hipSuccess;
@@ -401,13 +414,13 @@ hipError_t launch_env(const DynLaunch &d, const uint16_t *r, const int16_t *band
     dim3 grid = grid1(d.n_es);
     grid.y = 3;
     hipLaunchKernelGGL(k_env0, grid, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, d.es, d.n_es, r, x,
-                       d.tabs, g, sv, e0, act, d.nloc, d.warm);
+                       m, g, sv, e0, act, d.nloc, d.warm);
     hipLaunchKernelGGL(k_env_prev, dim3((unsigned)d.n_chunks, 3), dim3(64), 0, d.st, d.chunks,
                        d.eseg0, d.neseg, d.n_es, act, prev);
     double *ein = e0, *eout = e1;
     for (int k = 0; k < rounds; k++) {
         hipLaunchKernelGGL(k_envfix, grid, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, d.es, d.n_es,
-                           r, x, d.tabs, g, sv, ein, eout, act, prev, d.nloc);
+                           r, x, m, g, sv, ein, eout, act, prev, d.nloc);
         double *tmp = ein;
         ein = eout;
         eout = tmp;
@@ -416,13 +429,14 @@ hipError_t launch_env(const DynLaunch &d, const uint16_t *r, const int16_t *band
 }
 
 // ends: the array the last round wrote (e0 if rounds is even, else e1)
-hipError_t launch_envseq(const DynLaunch &d, const uint16_t *r, const int16_t *bands,
+hipError_t launch_envseq(const DynLaunch &d, const uint16_t *r, const double *m,
+                         const int16_t *bands,
                          int16_t *gained, double *sv, double *ends, const int *act,
                          const int *prev) {
     if (d.n_es <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_envseq, dim3((unsigned)d.n_chunks, 3), dim3(64), 0, d.st, d.cd, d.chunks,
                        d.es, d.n_es, d.eseg0, d.neseg, r,
-                       reinterpret_cast<const uint32_t *>(bands), d.tabs,
+                       reinterpret_cast<const uint32_t *>(bands), m,
                        reinterpret_cast<uint32_t *>(gained), sv, ends, act, prev, d.nloc);
     return hipGetLastError();
 }

@@ -128,11 +128,12 @@ struct DynLaunch {
     const double *tabs;
     hipStream_t st;
 };
-hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *r);
-hipError_t launch_env(const DynLaunch &d, const uint16_t *r, const int16_t *bands,
+hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *r, double *m);
+hipError_t launch_env(const DynLaunch &d, const uint16_t *r, const double *m, const int16_t *bands,
                       int16_t *gained, double *sv, double *e0, double *e1, int *act, int *prev,
                       int rounds);
-hipError_t launch_envseq(const DynLaunch &d, const uint16_t *r, const int16_t *bands,
+hipError_t launch_envseq(const DynLaunch &d, const uint16_t *r, const double *m,
+                         const int16_t *bands,
                          int16_t *gained, double *sv, double *ends, const int *act,
                          const int *prev);
 hipError_t launch_overlay(const DynLaunch &d, const int16_t *gained, int16_t *out,

@@ -198,7 +198,7 @@ struct amx_plan {
     float *d_lut = nullptr;
     // workspace offsets
     size_t ws_bytes = 0;
-    size_t o_a16, o_e, o_s, o_p16, o_ex, o_sx, o_bands, o_r, o_gain, o_esv, o_ee0, o_ee1, o_eact,
+    size_t o_a16, o_e, o_s, o_p16, o_ex, o_sx, o_bands, o_r, o_m, o_gain, o_esv, o_ee0, o_ee1, o_eact,
         o_eprev;
     size_t o_ekw, o_skw, o_parts, o_phop;
     size_t o_eb, o_ebx, o_ebk, o_pk;
@@ -632,6 +632,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         const size_t ne = (size_t)p->n_es;
         p->o_r = (size_t)align_up(off, 3 * nl * 2);
         p->o_gain = (size_t)align_up(off, 3 * nl * 4);
+        p->o_m = (size_t)align_up(off, 3 * nl * 8);
         p->o_esv = (size_t)align_up(off, 3 * ne * 8);
         p->o_ee0 = (size_t)align_up(off, 3 * ne * 8);
         p->o_ee1 = (size_t)align_up(off, 3 * ne * 8);
@@ -708,6 +709,7 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     int16_t *bands = p->mb ? wsp<int16_t>(d_ws, p->o_bands) : nullptr;
     uint16_t *r = p->mb ? wsp<uint16_t>(d_ws, p->o_r) : nullptr;
     int16_t *gained = p->mb ? wsp<int16_t>(d_ws, p->o_gain) : nullptr;
+    double *mframe = p->mb ? wsp<double>(d_ws, p->o_m) : nullptr;
     double *esv = p->mb ? wsp<double>(d_ws, p->o_esv) : nullptr;
     double *ee0 = p->mb ? wsp<double>(d_ws, p->o_ee0) : nullptr;
     double *ee1 = p->mb ? wsp<double>(d_ws, p->o_ee1) : nullptr;
@@ -744,15 +746,17 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
         if (p->mb) HIPCHK(amx::launch_xover2(l, p16, sx, bands, p->nloc));
         break;
     case AMX_STAGE_RMS:
-        if (p->mb) HIPCHK(amx::launch_rms(dl, bands, r));
+        if (p->mb) HIPCHK(amx::launch_rms(dl, bands, r, mframe));
         break;
     case AMX_STAGE_ENV:
-        if (p->mb) HIPCHK(amx::launch_env(dl, r, bands, gained, esv, ee0, ee1, eact, eprev, p->rounds));
+        if (p->mb)
+            HIPCHK(amx::launch_env(dl, r, mframe, bands, gained, esv, ee0, ee1, eact, eprev,
+                                   p->rounds));
         break;
     case AMX_STAGE_FIX:
         if (p->mb)
-            HIPCHK(amx::launch_envseq(dl, r, bands, gained, esv, (p->rounds & 1) ? ee1 : ee0, eact,
-                                      eprev));
+            HIPCHK(amx::launch_envseq(dl, r, mframe, bands, gained, esv,
+                                      (p->rounds & 1) ? ee1 : ee0, eact, eprev));
         break;
     case AMX_STAGE_APPLY:
         if (p->mb)
