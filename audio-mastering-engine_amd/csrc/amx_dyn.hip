@@ -401,7 +401,7 @@ hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *r, dou
     dim3 g((unsigned)((d.max_chunk_n + AMX_RMS_F - 1) / AMX_RMS_F), (unsigned)d.n_chunks, 3);
     if (empty(g)) return hipSuccess;
     hipLaunchKernelGGL(k_rms, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks,
-                       reinterpret_cast<const uint32_t *>(bands), m, r, m, d.nloc);
+                       reinterpret_cast<const uint32_t *>(bands), d.tabs, r, m, d.nloc);
     return hipGetLastError();
 }
 
