@@ -134,7 +134,7 @@ class ShardedTrack:
         from . import capi
         job = self.job
         job.run_chunks(d_in)
-        job.timed("loud1", job.loudness_pass1)
+        job.timed("loud1", lambda: job.loudness_pass1(tail=self.world > 1))
         lufs_on = job.dd.lufs_on
         if self.world > 1:
             self.exchange_carry()

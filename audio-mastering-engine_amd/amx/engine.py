@@ -141,8 +141,11 @@ class MasteringJob:
         ev.append((name, a, b))
         return r
 
-    def loudness_pass1(self, stream=None):
-        capi.check(capi.load().amx_loudness_pass1(self.plan.h, capi.ptr(self.out), capi.ptr(self.kw_tail),
+    def loudness_pass1(self, stream=None, tail=True):
+        """tail: also the K-filter end state from rest (only a chunk-sharded track's
+        next rank needs it)."""
+        capi.check(capi.load().amx_loudness_pass1(self.plan.h, capi.ptr(self.out),
+                                                  capi.ptr(self.kw_tail) if tail else None,
                                                   capi.ptr(self.peak), capi.ptr(self.ws), self._s(stream)),
                    "amx_loudness_pass1")
 
@@ -204,7 +207,7 @@ class MasteringJob:
         round trip); returns y (int16 [frames, 2]).  fetch_report() reads the
         loudness decision afterwards."""
         self.run_chunks(d_in, stream)
-        self.loudness_pass1(stream)
+        self.loudness_pass1(stream, tail=False)
         if self.dd.lufs_on:
             self.loudness_pass2(stream, carry=False)
             self.histograms(stream)

@@ -176,8 +176,6 @@ __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const 
     for (int d = 0; d < (KW ? AMX_KW_DIM : 1); d++) kv[d] = 0.0;
     int kmax = 0;
     const int klen = (j < n_seg) ? segs[j].len : 0;
-    const int kshift = L - klen;                          // != 0 only on a span's last segment
-    const bool kuni = __ballot(kshift != 0 && klen > 0) == 0ull;
     const int negm = (cd.st[0].neg ? 1 : 0) | (cd.st[3].neg ? 8 : 0);
     const float w = cd.width;
     const int won = cd.width_on;
@@ -203,7 +201,7 @@ __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const 
             // cd.pad0_ == 0: the offset makes the coefficient address depend on the
             // loop, so the scalar loads stay per tile (no hoisting, no SGPR spill)
             eq_tile<MASK, AMX_EQ_F>(negm, cd.eqc + (f0 & cd.pad0_), est, x, xf);
-#pragma unroll 2
+#pragma unroll
             for (int f = 0; f < AMX_EQ_F; f++) {
                 float v = MASK ? (float)x[f] : xf[f];
                 if (won) {
@@ -222,19 +220,16 @@ __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const 
                     for (int d = 0; d < AMX_XO_DIM; d++) xv[d] = fma(g[d], xd, xv[d]);
                 }
                 if constexpr (KW) {
+                    // rows are used as if every segment were L long (a wave-uniform row:
+                    // scalar loads, SGPR operands); a span's partial last segment is
+                    // re-done right-aligned by k_peak_reduce (kw_fix)
                     const int n = k + f0 + f;
                     const bool act = n < klen;
                     kmax = max(kmax, act ? abs((int)qv) : 0);
                     const double xs = act ? (double)qv * (1.0 / 32768.0) : 0.0;
-                    if (kuni) {
-                        const double *g = Gkw + (int64_t)n * AMX_KW_DIM;     // wave-uniform row
+                    const double *g = Gkw + (int64_t)n * AMX_KW_DIM;
 #pragma unroll
-                        for (int d = 0; d < AMX_KW_DIM; d++) kv[d] = fma(g[d], xs, kv[d]);
-                    } else {
-                        const double *g = Gkw + (int64_t)min(n + kshift, L - 1) * AMX_KW_DIM;
-#pragma unroll
-                        for (int d = 0; d < AMX_KW_DIM; d++) kv[d] = fma(g[d], xs, kv[d]);
-                    }
+                    for (int d = 0; d < AMX_KW_DIM; d++) kv[d] = fma(g[d], xs, kv[d]);
                 }
             }
         }

@@ -31,17 +31,15 @@ __device__ __forceinline__ int16_t gain16(int16_t x, double g) {
 // and the gain stage's own clip is subsumed by the +-limit*2^15 clamp.
 #define AMX_FINAL_FPT 8
 template <bool UNIT>
-__global__ void __launch_bounds__(AMX_BLOCK) k_final_fast(const SpanDev *__restrict__ spans,
-                                                          const uint32_t *__restrict__ x,
-                                                          const uint32_t *__restrict__ halo,
-                                                          int halo_frames,
-                                                          const double *__restrict__ gains,
-                                                          const int32_t *__restrict__ ctl,
-                                                          double level_in, double level,
-                                                          double level_out, double limit,
-                                                          uint32_t *__restrict__ y) {
+__device__ __forceinline__ void final_fast_block(const SpanDev *__restrict__ spans,
+                                                 const uint32_t *__restrict__ x,
+                                                 const uint32_t *__restrict__ halo,
+                                                 int halo_frames,
+                                                 const double *__restrict__ gains,
+                                                 double level_in, double level,
+                                                 double level_out, double limit,
+                                                 uint32_t *__restrict__ y) {
     const int t = blockIdx.y;
-    if (ctl && !(ctl[t] & AMX_CTL_FAST)) return;
     const SpanDev sp = spans[t];
     const int64_t i0 = (int64_t)blockIdx.x * (AMX_BLOCK * AMX_FINAL_FPT) + threadIdx.x;
     if (i0 >= sp.out_n) return;
@@ -88,16 +86,13 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_final_fast(const SpanDev *__restr
 // span, sequential.  State layout (doubles): [0] att [1] delta [2] pos [3] nextiter
 // [4] nextlen [5] valid  [8 .. 8+bs) buffer  [8+bs .. 8+2bs) nextdelta
 // [8+2bs .. 8+3bs) nextpos (stored as doubles).
-__global__ void k_final_general(const SpanDev *__restrict__ spans, int n_tracks,
-                                const uint32_t *__restrict__ x,
-                                const uint32_t *__restrict__ halo, int halo_frames,
-                                const double *__restrict__ gains, int fs, double level_in,
-                                double level, double level_out, double limit, double release,
-                                int bs, double *__restrict__ state, int64_t state_doubles,
-                                const int32_t *__restrict__ ctl, uint32_t *__restrict__ y) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_tracks) return;
-    if (ctl && (ctl[t] & AMX_CTL_FAST)) return;
+__device__ void final_general_track(int t, const SpanDev *__restrict__ spans,
+                                    const uint32_t *__restrict__ x,
+                                    const uint32_t *__restrict__ halo, int halo_frames,
+                                    const double *__restrict__ gains, int fs, double level_in,
+                                    double level, double level_out, double limit, double release,
+                                    int bs, double *__restrict__ state, int64_t state_doubles,
+                                    uint32_t *__restrict__ y) {
     const SpanDev sp = spans[t];
     const int channels = 2;
     double *S = state + (int64_t)t * state_doubles;
@@ -195,43 +190,53 @@ __global__ void k_final_general(const SpanDev *__restrict__ spans, int n_tracks,
     S[0] = att; S[1] = delta; S[2] = pos; S[3] = nextiter; S[4] = nextlen; S[5] = 1.0;
 }
 
+// One launch for both limiter paths.  Columns blockIdx.x < gridDim.x - 1 are the
+// parallel idle-limiter pass of track blockIdx.y; the last column runs the
+// sequential general limiter for that track (thread 0).  With ctl (k_decide's
+// word) each track takes exactly one of them; without it `fast` picks for all.
+struct FinalArgs {
+    const SpanDev *spans;
+    const uint32_t *x, *halo;
+    int halo_frames, fs, bs, fast;
+    const double *gains;
+    const int32_t *ctl;
+    double level_in, level, level_out, limit, release;
+    double *state;
+    int64_t state_doubles;
+    uint32_t *y;
+};
+
+template <bool UNIT>
+__global__ void __launch_bounds__(AMX_BLOCK) k_final(FinalArgs a) {
+    const int t = blockIdx.y;
+    const bool fast = a.ctl ? (a.ctl[t] & AMX_CTL_FAST) != 0 : a.fast != 0;
+    if (blockIdx.x + 1 < gridDim.x) {
+        if (fast)
+            final_fast_block<UNIT>(a.spans, a.x, a.halo, a.halo_frames, a.gains, a.level_in,
+                                   a.level, a.level_out, a.limit, a.y);
+    } else if (!fast && threadIdx.x == 0) {
+        final_general_track(t, a.spans, a.x, a.halo, a.halo_frames, a.gains, a.fs, a.level_in,
+                            a.level, a.level_out, a.limit, a.release, a.bs, a.state,
+                            a.state_doubles, a.y);
+    }
+}
+
 // ---------------------------------------------------------------- launchers
-hipError_t launch_final_fast(const SpanDev *spans, int n_tracks, int64_t max_span,
-                             const int16_t *x, const int16_t *halo, int halo_frames,
-                             const double *gains, const int32_t *ctl, double level_in,
-                             double level, double level_out, double limit, int16_t *y,
-                             hipStream_t st) {
+hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, const int16_t *x,
+                        const int16_t *halo, int halo_frames, const double *gains,
+                        const int32_t *ctl, int fast, int fs, double level_in, double level,
+                        double level_out, double limit, double release, int buffer_size,
+                        double *state, int64_t state_doubles, int16_t *y, hipStream_t st) {
     const int64_t per = (int64_t)AMX_BLOCK * AMX_FINAL_FPT;
-    dim3 g((unsigned)((max_span + per - 1) / per), (unsigned)n_tracks);
-    if (empty(g)) return hipSuccess;
-    const bool unit = level_in == 1.0 && level_out == 1.0 && limit * 32768.0 <= 32767.0;
-    if (unit)
-        hipLaunchKernelGGL(k_final_fast<true>, g, dim3(AMX_BLOCK), 0, st, spans,
-                           reinterpret_cast<const uint32_t *>(x),
-                           reinterpret_cast<const uint32_t *>(halo), halo_frames, gains, ctl,
-                           level_in, level, level_out, limit, reinterpret_cast<uint32_t *>(y));
-    else
-        hipLaunchKernelGGL(k_final_fast<false>, g, dim3(AMX_BLOCK), 0, st, spans,
-                           reinterpret_cast<const uint32_t *>(x),
-                           reinterpret_cast<const uint32_t *>(halo), halo_frames, gains, ctl,
-                           level_in, level, level_out, limit, reinterpret_cast<uint32_t *>(y));
-    return hipGetLastError();
-}
-
-hipError_t launch_final_general(const SpanDev *spans, int n_tracks, const int16_t *x,
-                                const int16_t *halo, int halo_frames, const double *gains,
-                                int fs, double level_in, double level, double level_out,
-                                double limit, double release, int buffer_size,
-                                double *state, int64_t state_doubles, const int32_t *ctl,
-                                int16_t *y, hipStream_t st) {
+    dim3 g((unsigned)((max_span + per - 1) / per) + 1, (unsigned)n_tracks);
     if (n_tracks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_final_general, dim3((n_tracks + 63) / 64), dim3(64), 0, st, spans,
-                       n_tracks, reinterpret_cast<const uint32_t *>(x),
-                       reinterpret_cast<const uint32_t *>(halo), halo_frames, gains, fs,
-                       level_in, level, level_out, limit, release, buffer_size, state,
-                       state_doubles, ctl, reinterpret_cast<uint32_t *>(y));
+    FinalArgs a{spans, reinterpret_cast<const uint32_t *>(x), reinterpret_cast<const uint32_t *>(halo),
+                halo_frames, fs, buffer_size, fast, gains, ctl, level_in, level, level_out, limit,
+                release, state, state_doubles, reinterpret_cast<uint32_t *>(y)};
+    const bool unit = level_in == 1.0 && level_out == 1.0 && limit * 32768.0 <= 32767.0;
+    if (unit) hipLaunchKernelGGL(k_final<true>, g, dim3(AMX_BLOCK), 0, st, a);
+    else hipLaunchKernelGGL(k_final<false>, g, dim3(AMX_BLOCK), 0, st, a);
     return hipGetLastError();
 }
-
 
 }  // namespace amx

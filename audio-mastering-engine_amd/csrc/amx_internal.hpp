@@ -144,7 +144,7 @@ hipError_t launch_kw1(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L,
                       hipStream_t st);
 hipError_t launch_kw2(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L, int hop,
                       const int16_t *x, const double *s, double *parts, int64_t *part_hop,
-                      hipStream_t st);
+                      int aligned, hipStream_t st);
 hipError_t launch_hops(const SpanDev *spans, int n_tracks, const KwSegDev *ks, int L, int hop,
                        const double *parts, const int64_t *part_hop, double *hops,
                        int64_t max_hops, hipStream_t st);
@@ -152,17 +152,11 @@ hipError_t launch_hist(const SpanDev *spans, int n_tracks, int hop, const double
                        int64_t max_hops, const double *bounds, unsigned long long *hist,
                        unsigned long long *st_hist, hipStream_t st);
 // finalize
-hipError_t launch_final_fast(const SpanDev *spans, int n_tracks, int64_t max_span,
-                             const int16_t *x, const int16_t *halo, int halo_frames,
-                             const double *gains, const int32_t *ctl, double level_in,
-                             double level, double level_out, double limit, int16_t *y,
-                             hipStream_t st);
-hipError_t launch_final_general(const SpanDev *spans, int n_tracks, const int16_t *x,
-                                const int16_t *halo, int halo_frames, const double *gains,
-                                int fs, double level_in, double level, double level_out,
-                                double limit, double release, int buffer_size,
-                                double *state, int64_t state_doubles, const int32_t *ctl,
-                                int16_t *y, hipStream_t st);
+hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, const int16_t *x,
+                        const int16_t *halo, int halo_frames, const double *gains,
+                        const int32_t *ctl, int fast, int fs, double level_in, double level,
+                        double level_out, double limit, double release, int buffer_size,
+                        double *state, int64_t state_doubles, int16_t *y, hipStream_t st);
 struct DecideArgs {
     int n_tracks, lufs_on;
     const unsigned long long *hist, *st_hist;
@@ -175,7 +169,9 @@ hipError_t launch_decide(const DecideArgs &a, hipStream_t st);
 hipError_t launch_kw_carry(const double *tails, const double *P, int n_prev, double *carry,
                            hipStream_t st);
 hipError_t launch_peak_reduce(const SpanDev *spans, int n_tracks, int64_t max_nkseg,
-                              const uint32_t *pk, unsigned long long *peak, hipStream_t st);
+                              const uint32_t *pk, unsigned long long *peak, const KwSegDev *ks,
+                              int L, const int16_t *x, const double *G, double *e, int kw_fix,
+                              hipStream_t st);
 hipError_t launch_kw_tail(const SpanDev *spans, int n_tracks, const double *s, const double *e,
                           const double *P, double *tail, hipStream_t st);
 }  // namespace amx

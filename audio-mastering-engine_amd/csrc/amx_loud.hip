@@ -65,10 +65,82 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_kw1(const KwSegDev *__restrict__ 
     }
 }
 
+#define AMX_KW2_TILES 8   // segments of up to 128 frames (the plan's Lkw <= 128)
+#define AMX_KW2_PITCH (AMX_TF + 1)
 // K-weighting pass 2: filter from the true state (two DF-II-T biquads, see
 // amx_plan.cpp), y^2 summed per 100 ms hop piece.  One thread per (segment,
 // channel), lanes 2i / 2i+1 = L / R of row i.  parts[j][piece][ch], part_hop[j] =
 // whole-track hop index of piece 0 (a segment spans <= 2 hops).
+//
+// Loads: thread t moves column t % 16 of rows t / 16 + 16 m (m < 8) of every
+// 16-frame tile; the row pointers are formed once, so a tile costs 8 loads with
+// immediate offsets, all 8 tiles are issued up front (the recursion per tile is
+// too short to hide an HBM round trip), and only a workgroup holding a partial
+// (span-final) segment clamps addresses and masks frames (PART).
+// ALIGNED (the hop is a multiple of 16 frames and every segment starts on a
+// 16-frame boundary of the track): a segment's hop split falls on a tile
+// boundary, so the accumulator is picked once per tile instead of per frame;
+// each piece is still one sequential FMA chain in frame order.
+// The 1/32768 sample scaling is folded into the first biquad's numerator
+// (a power of two: the products, and so every rounding, are unchanged).
+template <bool ALIGNED, bool PART>
+__device__ __forceinline__ void kw2_run(const uint32_t *__restrict__ const *bp, const int *lm,
+                                        int c, int rg, uint32_t *s_in, int row, int chn, int L,
+                                        int len, int split, const double *c1, const double *c2,
+                                        double *v, double &acc0, double &acc1) {
+    uint32_t R[AMX_KW2_TILES][8];
+#pragma unroll
+    for (int q = 0; q < AMX_KW2_TILES; q++) {
+        if (q * AMX_TF >= L) break;
+#pragma unroll
+        for (int m = 0; m < 8; m++) {
+            if constexpr (PART) {
+                const bool ok = q * AMX_TF + c < lm[m];
+                R[q][m] = bp[m][ok ? q * AMX_TF : -c];     // frame 0 of the row: in range
+                R[q][m] = ok ? R[q][m] : 0u;
+            } else {
+                R[q][m] = bp[m][q * AMX_TF];
+            }
+        }
+    }
+    const uint32_t *rp = s_in + row * AMX_KW2_PITCH;
+    const int sh = chn ? 16 : 0;
+#pragma unroll
+    for (int q = 0; q < AMX_KW2_TILES; q++) {
+        const int k = q * AMX_TF;
+        if (k >= L) break;
+#pragma unroll
+        for (int m = 0; m < 8; m++) s_in[(rg + 16 * m) * AMX_KW2_PITCH + c] = R[q][m];
+        __syncthreads();
+        if constexpr (ALIGNED && !PART) {
+            const bool lo = k < split;
+            double a = lo ? acc0 : acc1;
+#pragma unroll
+            for (int f = 0; f < AMX_TF; f++) {
+                const double xs = (double)(int)(int16_t)(rp[f] >> sh);
+                const double u = bq_step(c1, v[0], v[1], xs);
+                const double y = bq_step(c2, v[2], v[3], u);
+                a = fma(y, y, a);
+            }
+            if (lo) acc0 = a;
+            else acc1 = a;
+        } else {
+#pragma unroll 4
+            for (int f = 0; f < AMX_TF; f++) {
+                const int n = k + f;
+                const double xs = (double)(int)(int16_t)(rp[f] >> sh);
+                const double u = bq_step(c1, v[0], v[1], xs);
+                double y = bq_step(c2, v[2], v[3], u);
+                if constexpr (PART) y = n < len ? y : 0.0;
+                if (n >= split) acc1 = fma(y, y, acc1);
+                else acc0 = fma(y, y, acc0);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <bool ALIGNED>
 __global__ void __launch_bounds__(AMX_BLOCK) k_kw2(const ChainDev *__restrict__ cdp,
                                                    const KwSegDev *__restrict__ ks, int n_kseg,
                                                    int L, int hop,
@@ -77,55 +149,43 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_kw2(const ChainDev *__restrict__ 
                                                    double *__restrict__ parts,
                                                    int64_t *__restrict__ part_hop) {
     constexpr int ROWS = AMX_BLOCK / 2;
-    using T = Tile<1, ROWS>;
-    __shared__ uint32_t s_in[T::WORDS];
+    __shared__ uint32_t s_in[ROWS * AMX_KW2_PITCH];
     __shared__ int64_t rb[ROWS];
     __shared__ int rl[ROWS];
-    __shared__ double s_c[12];
-    const ChainDev &cd = *cdp;
     const int t = threadIdx.x, row = t >> 1, chn = t & 1;
     const int j = blockIdx.x * ROWS + row;
     const bool valid = j < n_kseg;
     const KwSegDev sg = ks[valid ? j : n_kseg - 1];
+    const int len = valid ? sg.len : 0;
     if (chn == 0) {
         rb[row] = valid ? sg.out_pos : 0;
-        rl[row] = valid ? sg.len : 0;
+        rl[row] = len;
     }
-    if (t < 6) s_c[t] = cd.kw1[t];
-    else if (t < 12) s_c[t] = cd.kw2[t - 6];
+    double c1[5], c2[5];
+#pragma unroll
+    for (int i = 0; i < 3; i++) { c1[i] = cdp->kw1[i] * (1.0 / 32768.0); c2[i] = cdp->kw2[i]; }
+    c1[3] = cdp->kw1[4]; c1[4] = cdp->kw1[5];
+    c2[3] = cdp->kw2[4]; c2[4] = cdp->kw2[5];
     double v[4];
     const double *st = s + ((int64_t)(valid ? j : 0) * 2 + chn) * AMX_KW_DIM;
 #pragma unroll
     for (int d = 0; d < 4; d++) v[d] = valid ? st[d] : 0.0;
-    const int len = valid ? sg.len : 0;
     const int64_t h0 = sg.tframe / hop;
-    const int64_t split = (h0 + 1) * hop - sg.tframe;   // first frame of piece 1
-    double acc0 = 0.0, acc1 = 0.0;
-    __syncthreads();
-    double c1[5], c2[5];
+    const int split = (int)((h0 + 1) * hop - sg.tframe);   // first frame of piece 1
+    const int part = __syncthreads_or(len < L);
+    const int c = t & 15, rg = t >> 4;
+    const uint32_t *bp[8];
+    int lm[8];
 #pragma unroll
-    for (int i = 0; i < 3; i++) { c1[i] = s_c[i]; c2[i] = s_c[6 + i]; }
-    c1[3] = s_c[4]; c1[4] = s_c[5];
-    c2[3] = s_c[10]; c2[4] = s_c[11];
-    TileRegs<1, ROWS> R;
-    tile_fetch<1, ROWS>(R, x, rb, nullptr, rl, 0);
-    for (int k = 0; k < L; k += AMX_TF) {
-        tile_put<1, ROWS>(s_in, R, nullptr, rl, k);
-        __syncthreads();
-        if (k + AMX_TF < L) tile_fetch<1, ROWS>(R, x, rb, nullptr, rl, k + AMX_TF);
-        const uint32_t *rp = s_in + row * T::PITCH;
-#pragma unroll 4
-        for (int f = 0; f < AMX_TF; f++) {
-            const uint32_t p = rp[f];
-            const int n = k + f;
-            const double xs = (double)(chn ? hi16(p) : lo16(p)) * (1.0 / 32768.0);
-            const double u = bq_step(c1, v[0], v[1], xs);
-            const double y = n < len ? bq_step(c2, v[2], v[3], u) : 0.0;
-            if (n >= split) acc1 = fma(y, y, acc1);
-            else acc0 = fma(y, y, acc0);
-        }
-        __syncthreads();
+    for (int m = 0; m < 8; m++) {
+        bp[m] = x + rb[rg + 16 * m] + c;
+        lm[m] = rl[rg + 16 * m];
     }
+    double acc0 = 0.0, acc1 = 0.0;
+    if (part)
+        kw2_run<ALIGNED, true>(bp, lm, c, rg, s_in, row, chn, L, len, split, c1, c2, v, acc0, acc1);
+    else
+        kw2_run<ALIGNED, false>(bp, lm, c, rg, s_in, row, chn, L, len, split, c1, c2, v, acc0, acc1);
     if (valid) {
         double *o = parts + (int64_t)j * 4;
         o[chn] = acc0;
@@ -241,11 +301,16 @@ hipError_t launch_kw1(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L,
 
 hipError_t launch_kw2(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L, int hop,
                       const int16_t *x, const double *s, double *parts, int64_t *part_hop,
-                      hipStream_t st) {
+                      int aligned, hipStream_t st) {
     if (n_kseg <= 0) return hipSuccess;
+    if (L > AMX_KW2_TILES * AMX_TF || L % AMX_TF) return hipErrorInvalidValue;
     const dim3 grid((unsigned)((n_kseg + AMX_BLOCK / 2 - 1) / (AMX_BLOCK / 2)));
-    hipLaunchKernelGGL(k_kw2, grid, dim3(AMX_BLOCK), 0, st, cd, ks, n_kseg, L, hop,
-                       reinterpret_cast<const uint32_t *>(x), s, parts, part_hop);
+    if (aligned)
+        hipLaunchKernelGGL(k_kw2<true>, grid, dim3(AMX_BLOCK), 0, st, cd, ks, n_kseg, L, hop,
+                           reinterpret_cast<const uint32_t *>(x), s, parts, part_hop);
+    else
+        hipLaunchKernelGGL(k_kw2<false>, grid, dim3(AMX_BLOCK), 0, st, cd, ks, n_kseg, L, hop,
+                           reinterpret_cast<const uint32_t *>(x), s, parts, part_hop);
     return hipGetLastError();
 }
 
@@ -277,14 +342,52 @@ hipError_t launch_hist(const SpanDev *spans, int n_tracks, int hop, const double
 // amx_loudness_pass1 first): same-address atomics serialise, so there are few.
 #define AMX_PEAK_THREADS 1024
 #define AMX_PEAK_PER_THREAD 8
+// kw_fix: k_front2 accumulated the K-filter GEMV with the row of a full L-frame
+// segment (wave-uniform); a span's last segment shorter than L needs its rows
+// right-aligned (G[n + L - len], as k_kw1 does), so wave 0 of the span's first
+// workgroup redoes that one segment here (lanes split the frames, butterfly sum).
 __global__ void __launch_bounds__(AMX_PEAK_THREADS) k_peak_reduce(const SpanDev *__restrict__ spans,
                                                                   const uint32_t *__restrict__ pk,
-                                                                  unsigned long long *__restrict__ peak) {
+                                                                  unsigned long long *__restrict__ peak,
+                                                                  const KwSegDev *__restrict__ ks,
+                                                                  int L, const uint32_t *__restrict__ x,
+                                                                  const double *__restrict__ G,
+                                                                  double *__restrict__ e, int kw_fix) {
     __shared__ int red[2][AMX_PEAK_THREADS / 64];
     const int t = blockIdx.y;
     const SpanDev sp = spans[t];
     const int64_t q0 = (int64_t)blockIdx.x * AMX_PEAK_THREADS * AMX_PEAK_PER_THREAD;
     if (q0 >= sp.nkseg) return;                      // block-uniform
+    if (kw_fix && blockIdx.x == 0 && threadIdx.x < 64) {
+        const int64_t j = (int64_t)sp.kseg0 + sp.nkseg - 1;
+        const KwSegDev sg = ks[j];
+        if (sg.len < L) {                            // wave-uniform
+            double a[2 * AMX_KW_DIM];
+#pragma unroll
+            for (int d = 0; d < 2 * AMX_KW_DIM; d++) a[d] = 0.0;
+            const int sh = L - sg.len;
+            for (int n = threadIdx.x; n < sg.len; n += 64) {
+                const uint32_t p = x[sg.out_pos + n];
+                const double xa = (double)lo16(p) * (1.0 / 32768.0), xb = (double)hi16(p) * (1.0 / 32768.0);
+                const double *g = G + (int64_t)(n + sh) * AMX_KW_DIM;
+#pragma unroll
+                for (int d = 0; d < AMX_KW_DIM; d++) {
+                    a[d] = fma(g[d], xa, a[d]);
+                    a[AMX_KW_DIM + d] = fma(g[d], xb, a[AMX_KW_DIM + d]);
+                }
+            }
+#pragma unroll
+            for (int d = 0; d < 2 * AMX_KW_DIM; d++)
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) a[d] += __shfl_xor(a[d], o);
+            if (threadIdx.x < 2 * AMX_KW_DIM) {
+                double v = a[0];
+#pragma unroll
+                for (int d = 1; d < 2 * AMX_KW_DIM; d++) v = threadIdx.x == d ? a[d] : v;
+                e[j * 2 * AMX_KW_DIM + threadIdx.x] = v;
+            }
+        }
+    }
     int m0 = 0, m1 = 0;
 #pragma unroll
     for (int i = 0; i < AMX_PEAK_PER_THREAD; i++) {
@@ -313,11 +416,14 @@ __global__ void __launch_bounds__(AMX_PEAK_THREADS) k_peak_reduce(const SpanDev 
 }
 
 hipError_t launch_peak_reduce(const SpanDev *spans, int n_tracks, int64_t max_nkseg,
-                              const uint32_t *pk, unsigned long long *peak, hipStream_t st) {
+                              const uint32_t *pk, unsigned long long *peak, const KwSegDev *ks,
+                              int L, const int16_t *x, const double *G, double *e, int kw_fix,
+                              hipStream_t st) {
     const int64_t per = (int64_t)AMX_PEAK_THREADS * AMX_PEAK_PER_THREAD;
     dim3 g((unsigned)((max_nkseg + per - 1) / per), (unsigned)n_tracks);
     if (empty(g)) return hipSuccess;
-    hipLaunchKernelGGL(k_peak_reduce, g, dim3(AMX_PEAK_THREADS), 0, st, spans, pk, peak);
+    hipLaunchKernelGGL(k_peak_reduce, g, dim3(AMX_PEAK_THREADS), 0, st, spans, pk, peak, ks, L,
+                       reinterpret_cast<const uint32_t *>(x), G, e, kw_fix);
     return hipGetLastError();
 }
 
@@ -385,7 +491,12 @@ __global__ void __launch_bounds__(64) k_decide(DecideArgs a) {
     const int t = blockIdx.x, lane = threadIdx.x;
     const unsigned long long *H = a.hist + (int64_t)t * AMX_HIST_BINS;
     const unsigned long long *S = a.st_hist + (int64_t)t * AMX_HIST_BINS;
-    const double *E = a.energies;
+    // bin energies and boundaries staged in LDS: the bin searches and lookups below
+    // are dependent chains, each step an LDS read instead of an L2 round trip
+    __shared__ double E[AMX_HIST_BINS], B[AMX_HIST_BINS + 1];
+    for (int i = lane; i < AMX_HIST_BINS; i += 64) E[i] = a.energies[i];
+    for (int i = lane; i <= AMX_HIST_BINS; i += 64) B[i] = B[i];
+    __syncthreads();
     double I = -INFINITY, thr = -70.0, lra = 0.0;
     if (a.lufs_on) {
         double hc[AMX_BPL], sc[AMX_BPL], en[AMX_BPL];
@@ -409,9 +520,9 @@ __global__ void __launch_bounds__(64) k_decide(DecideArgs a) {
             rel *= 0.1;                                // pow(10, -10/10)
             thr = lufs_of(rel);
             int start;
-            if (rel < a.bounds[0]) start = 0;
+            if (rel < B[0]) start = 0;
             else {
-                start = find_bin(a.bounds, rel);
+                start = find_bin(B, rel);
                 if (rel > E[start]) ++start;
             }
             double g = 0.0, above = 0.0;
@@ -435,9 +546,9 @@ __global__ void __launch_bounds__(64) k_decide(DecideArgs a) {
             power /= size;
             const double integ = 0.01 * power;         // pow(10, -20/10)
             int index;
-            if (integ < a.bounds[0]) index = 0;
+            if (integ < B[0]) index = 0;
             else {
-                index = find_bin(a.bounds, integ);
+                index = find_bin(B, integ);
                 if (integ > E[index]) ++index;
             }
             double mine = 0.0;                         // this lane's counts at bins >= index

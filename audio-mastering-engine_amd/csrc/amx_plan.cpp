@@ -167,6 +167,8 @@ struct amx_plan {
     std::vector<SegDev> esegs;
     std::vector<int> eseg0, neseg;
     int fuse_kw = 0;        // loudness pass-1 GEMV + peak run inside k_front2
+    int kw_rest_states = 0;
+    int kw_aligned = 0;     // K-filter hop pieces split only at 16-frame tile boundaries // the last amx_loudness_pass1 left the K-filter start states from rest
     int n_tracks = 0, n_chunks = 0, n_seg = 0, n_kseg = 0, n_blk = 0, n_kblk = 0;
     int64_t max_nkseg = 0;
     int64_t nloc = 0, out_frames = 0, max_chunk_out = 0, max_span = 0, max_chunk_n = 0;
@@ -502,6 +504,10 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         p->max_nkseg = sp.nkseg > p->max_nkseg ? sp.nkseg : p->max_nkseg;
     }
     p->n_kseg = (int)p->ksegs.size();
+    // hop splits on 16-frame tile boundaries (k_kw2 picks the hop piece per tile)
+    p->kw_aligned = (p->hop % AMX_TF_FRAMES == 0 && p->Lkw % AMX_TF_FRAMES == 0) ? 1 : 0;
+    for (int t = 0; t < n_tracks; t++)
+        if (p->spans[t].tframe0 % AMX_TF_FRAMES) p->kw_aligned = 0;
     // the K-filter segment grid equals the chain's when there is no multiband
     // (output frames == input frames) and every chunk but a span's last is whole
     // segments long: k_front2 then does loudness pass 1 on the output it writes
@@ -780,12 +786,13 @@ extern "C" {
 
 int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, double *d_kw_tail, double *d_peak,
                        void *d_ws, void *stream) {
-    if (!p || !d_kw_tail || !d_peak || (p->n_kseg > 0 && (!d_out || !d_ws)))
+    if (!p || !d_peak || (p->n_kseg > 0 && (!d_out || !d_ws)))
         return fail(AMX_EINVAL, "null argument");
     hipStream_t st = (hipStream_t)stream;
     HIPCHK(hipMemsetAsync(d_peak, 0, sizeof(double) * 2 * (size_t)p->n_tracks, st));
+    p->kw_rest_states = 0;
     if (p->n_kseg == 0) {
-        HIPCHK(hipMemsetAsync(d_kw_tail, 0, sizeof(double) * 8 * (size_t)p->n_tracks, st));
+        if (d_kw_tail) HIPCHK(hipMemsetAsync(d_kw_tail, 0, sizeof(double) * 8 * (size_t)p->n_tracks, st));
         return AMX_OK;
     }
     double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
@@ -793,9 +800,12 @@ int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, double *d_kw_tail, dou
     if (!p->fuse_kw)  // else the GEMV + per-segment peaks were made by k_front2 (amx_run_chunks)
         HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e, pk, st));
     HIPCHK(amx::launch_peak_reduce(p->d_spans, p->n_tracks, p->max_nkseg, pk,
-                                   reinterpret_cast<unsigned long long *>(d_peak), st));
+                                   reinterpret_cast<unsigned long long *>(d_peak), p->d_ksegs,
+                                   p->Lkw, d_out, p->d_Gkw, e, p->fuse_kw, st));
     HIPCHK(amx::launch_scan(p->scan_kw(), e, s, nullptr, wsp<double>(d_ws, p->o_ebk), st));
-    HIPCHK(amx::launch_kw_tail(p->d_spans, p->n_tracks, s, e, p->d_tailpow, d_kw_tail, st));
+    p->kw_rest_states = 1;   // s = the start states from rest: pass 2 without a carry reuses them
+    if (d_kw_tail)
+        HIPCHK(amx::launch_kw_tail(p->d_spans, p->n_tracks, s, e, p->d_tailpow, d_kw_tail, st));
     return AMX_OK;
 }
 
@@ -823,8 +833,10 @@ int amx_loudness_pass2(amx_plan *p, const int16_t *d_out, const double *d_kw_car
     double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
     double *parts = wsp<double>(d_ws, p->o_parts);
     int64_t *phop = wsp<int64_t>(d_ws, p->o_phop);
-    HIPCHK(amx::launch_scan(p->scan_kw(), e, s, d_kw_carry, wsp<double>(d_ws, p->o_ebk), st));
-    HIPCHK(amx::launch_kw2(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, p->hop, d_out, s, parts, phop, st));
+    if (d_kw_carry || !p->kw_rest_states)
+        HIPCHK(amx::launch_scan(p->scan_kw(), e, s, d_kw_carry, wsp<double>(d_ws, p->o_ebk), st));
+    HIPCHK(amx::launch_kw2(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, p->hop, d_out, s, parts, phop,
+                           p->kw_aligned, st));
     HIPCHK(amx::launch_hops(p->d_spans, p->n_tracks, p->d_ksegs, p->Lkw, p->hop, parts, phop, d_hops,
                             max_hops, st));
     return AMX_OK;
@@ -919,18 +931,10 @@ int amx_finalize(amx_plan *p, const amx_final_desc *fd, const int16_t *d_x,
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     const double level = fd->auto_level ? 1 / fd->limit : 1;
-    if (d_ctl || fast) {
-        HIPCHK(amx::launch_final_fast(p->d_spans, p->n_tracks, p->max_span, d_x, d_halo, halo,
-                                      d_gains, d_ctl, fd->level_in, level, fd->level_out,
-                                      fd->limit, d_y, st));
-    }
-    if (d_ctl || !fast) {
-        if (!d_lim_state) return fail(AMX_EINVAL, "general limiter needs d_lim_state");
-        HIPCHK(amx::launch_final_general(p->d_spans, p->n_tracks, d_x, d_halo, halo, d_gains,
-                                         p->cd.fs, fd->level_in, level, fd->level_out, fd->limit,
-                                         fd->release_ms / 1000.0, bs, d_lim_state, sd, d_ctl,
-                                         d_y, st));
-    }
+    if ((d_ctl || !fast) && !d_lim_state) return fail(AMX_EINVAL, "general limiter needs d_lim_state");
+    HIPCHK(amx::launch_final(p->d_spans, p->n_tracks, p->max_span, d_x, d_halo, halo, d_gains, d_ctl,
+                             fast ? 1 : 0, p->cd.fs, fd->level_in, level, fd->level_out, fd->limit,
+                             fd->release_ms / 1000.0, bs, d_lim_state, sd, d_y, st));
     return AMX_OK;
 }
 

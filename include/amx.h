@@ -175,14 +175,16 @@ AMX_API int amx_run_stage(amx_plan *plan, int32_t stage, const float *d_in, int1
  * K-filter zero-state GEMV per segment + exact scan + sample peak.
  * d_kw_tail [n_tracks][2][4]: K-filter state at each span end assuming the span
  * started from rest (what the NEXT rank of a chunk-sharded track needs, see
- * amx_kw_propagate); d_peak [n_tracks][2]: max |x| per channel (zeroed here). */
+ * amx_kw_propagate; NULL = not wanted, e.g. one GPU); d_peak [n_tracks][2]: max |x|
+ * per channel (zeroed here). */
 AMX_API int amx_loudness_pass1(amx_plan *plan, const int16_t *d_out, double *d_kw_tail, double *d_peak,
                        void *d_ws, void *stream);
 /* Host helper for chunk-sharded tracks: out8 = A^frames * in8 (per channel 4x4 K-filter
  * transition), so carry(r+1) = A^{len_r} carry(r) + tail(r). */
 AMX_API int amx_kw_propagate(const amx_plan *plan, int64_t frames, const double *in8, double *out8);
 /* Loudness pass 2: K-filter from the exact state (d_kw_carry [n_tracks][2][4] = state
- * entering each span, NULL = rest), squared and summed per 100 ms hop on the
+ * entering each span, NULL = rest: then the start states amx_loudness_pass1 left are
+ * reused, so pass 1 must run first on the same d_ws), squared and summed per 100 ms hop on the
  * WHOLE-track hop grid: d_hops [n_tracks][max_hops][2] (zeroed here; hops a span only
  * partly covers hold partial sums -- sum them over ranks, e.g. RCCL all-reduce). */
 AMX_API int amx_loudness_pass2(amx_plan *plan, const int16_t *d_out, const double *d_kw_carry,
