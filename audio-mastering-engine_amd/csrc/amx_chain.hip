@@ -107,6 +107,146 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_front1(const ChainDev *__restrict
     }
 }
 
+// Stereo float32 input (the product path): two threads per segment, each holding
+// both channels' accumulators for half of the D state components (lanes 2i / 2i+1
+// = components [0, D/2) / [D/2, D) of row i), so a G value read once feeds two
+// FMAs and the launch has two waves per 64 segments.  The G rows of a tile go
+// through LDS (ds_read_b128; scalar loads thrash the scalar cache on the 20 KB
+// table).  Each lane quantises both samples (the analog stage couples the
+// channels).  Tile loads are 16 B per lane from row pointers formed once (lane
+// t: 16-B column t % 8 of rows t / 8 + 32 m), issued one tile ahead; only a
+// workgroup with a partial (chunk-final) segment clamps addresses (PART).
+#define AMX_F1_PITCH (2 * AMX_TF + 2)   // dwords per LDS row: 8-B aligned, conflict-free
+template <int D, bool AN, bool PART>
+__device__ __forceinline__ void front1s_run(const ChainDev &cd, const float *__restrict__ lut,
+                                            const uint32_t *__restrict__ const *ip,
+                                            const int *ilen, uint32_t *const *op,
+                                            int c4, int rg, uint32_t *s_in,
+                                            uint32_t *s_out, int row, int half, int L, int len,
+                                            const double *__restrict__ G, double *sG,
+                                            double *__restrict__ eo) {
+    constexpr int H = D / 2;
+    double a0[H > 0 ? H : 1], a1[H > 0 ? H : 1];
+#pragma unroll
+    for (int d = 0; d < H; d++) { a0[d] = 0.0; a1[d] = 0.0; }
+    constexpr int GQ = AMX_TF * D / 2;                  // 16-B pieces of a G tile
+    uint4 R[4], RG;
+    auto fetch = [&](int k) {
+        const int tt = threadIdx.x;
+        RG = tt < GQ ? *reinterpret_cast<const uint4 *>(G + (int64_t)k * D + 2 * tt)
+                     : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            if constexpr (PART) {
+                const bool ok = k + 2 * c4 < ilen[m];          // frames k + 2 c4, +1
+                R[m] = *reinterpret_cast<const uint4 *>(ip[m] + (ok ? 2 * k : -4 * c4));
+                if (!ok) R[m] = make_uint4(0u, 0u, 0u, 0u);
+            } else {
+                R[m] = *reinterpret_cast<const uint4 *>(ip[m] + 2 * k);
+            }
+        }
+    };
+    fetch(0);
+    const uint32_t *rp = s_in + row * AMX_F1_PITCH;
+    for (int k = 0; k < L; k += AMX_TF) {
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            uint32_t *w = s_in + (rg + 32 * m) * AMX_F1_PITCH + 4 * c4;
+            *reinterpret_cast<uint2 *>(w) = make_uint2(R[m].x, R[m].y);
+            *reinterpret_cast<uint2 *>(w + 2) = make_uint2(R[m].z, R[m].w);
+        }
+        if (threadIdx.x < GQ) reinterpret_cast<uint4 *>(sG)[threadIdx.x] = RG;
+        __syncthreads();
+        if (k + AMX_TF < L) fetch(k + AMX_TF);
+#pragma unroll 1
+        for (int f = 0; f < AMX_TF; f++) {
+            int16_t l = q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f]));
+            int16_t r = q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f + 1]));
+            if constexpr (AN) analog_frame(cd, lut, l, r, l, r);
+            if (half == 0) s_out[row * (AMX_TF + 1) + f] = pack2(l, r);
+            double x0 = (double)((float)l / 32768.0f), x1 = (double)((float)r / 32768.0f);
+            if constexpr (PART) {
+                x0 = k + f < len ? x0 : 0.0;
+                x1 = k + f < len ? x1 : 0.0;
+            }
+            const double *g = sG + f * D + half * H;
+#pragma unroll
+            for (int d = 0; d < H; d++) {
+                a0[d] = fma(g[d], x0, a0[d]);
+                a1[d] = fma(g[d], x1, a1[d]);
+            }
+        }
+        __syncthreads();
+        // s16 tile -> a16: lane t stores frames 2 (t % 8), +1 of rows t / 8 + 32 m
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const uint32_t *so = s_out + (rg + 32 * m) * (AMX_TF + 1) + 2 * c4;
+            const uint32_t w0 = so[0], w1 = so[1];
+            if constexpr (PART) {
+                if (k + 2 * c4 < ilen[m]) op[m][k] = w0;
+                if (k + 2 * c4 + 1 < ilen[m]) op[m][k + 1] = w1;
+            } else {
+                *reinterpret_cast<uint2 *>(op[m] + k) = make_uint2(w0, w1);
+            }
+        }
+    }
+    if (eo) {
+#pragma unroll
+        for (int d = 0; d < H; d++) { eo[d] = a0[d]; eo[D + d] = a1[d]; }
+    }
+}
+
+template <int D, bool AN>
+__global__ void __launch_bounds__(AMX_BLOCK, 4) k_front1s(const ChainDev *__restrict__ cdp,
+                                                          const ChunkDev *__restrict__ chunks,
+                                                          const SegDev *__restrict__ segs,
+                                                          int n_seg, int L,
+                                                          const uint32_t *__restrict__ in,
+                                                          const float *__restrict__ lut,
+                                                          uint32_t *__restrict__ a16,
+                                                          const double *__restrict__ G,
+                                                          double *__restrict__ e) {
+    constexpr int ROWS = AMX_BLOCK / 2;
+    constexpr int H = D / 2;
+    __shared__ uint32_t s_in[ROWS * AMX_F1_PITCH];
+    __shared__ uint32_t s_out[ROWS * (AMX_TF + 1)];
+    __shared__ __attribute__((aligned(16))) double sG[AMX_TF * (D > 0 ? D : 2)];
+    __shared__ int64_t rb_in[ROWS], rb_out[ROWS];
+    __shared__ int rl[ROWS];
+    static_assert(AMX_TF * D / 2 <= AMX_BLOCK, "one 16-B piece of the G tile per thread");
+    static_assert(D % 2 == 0, "state split in halves");
+    const ChainDev &cd = *cdp;
+    const int t = threadIdx.x, row = t >> 1, half = t & 1;
+    const int j = blockIdx.x * ROWS + row;
+    const bool valid = j < n_seg;
+    const SegDev sg = segs[valid ? j : n_seg - 1];
+    const ChunkDev ch = chunks[sg.chunk];
+    const int len = valid ? sg.len : 0;
+    if (half == 0) {
+        rb_in[row] = valid ? (ch.in_off + sg.pos) * 2 : 0;
+        rb_out[row] = valid ? ch.loc_off + sg.pos : 0;
+        rl[row] = len;
+    }
+    const int part = __syncthreads_or(len < L);
+    const int c4 = t & 7, rg = t >> 3;
+    const uint32_t *ip[4];
+    int ilen[4];
+    uint32_t *op[4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        ip[m] = in + rb_in[rg + 32 * m] + 4 * c4;
+        ilen[m] = rl[rg + 32 * m];
+        op[m] = a16 + rb_out[rg + 32 * m] + 2 * c4;
+    }
+    double *eo = (D > 0 && valid && !sg.last) ? e + (int64_t)j * 2 * D + half * H : nullptr;
+    if (part)
+        front1s_run<D, AN, true>(cd, lut, ip, ilen, op, c4, rg, s_in, s_out, row, half, L, len,
+                                 G, sG, eo);
+    else
+        front1s_run<D, AN, false>(cd, lut, ip, ilen, op, c4, rg, s_in, s_out, row, half, L, len,
+                                  G, sG, eo);
+}
+
 // ------------------------------------------- pass 2: EQ from true state -> int16
 // One thread per (segment, channel): lanes 2i / 2i+1 are the L / R channel of row
 // i.  The EQ runs stage-major over sub-tiles of AMX_EQ_F frames (eq_tile), so only
@@ -342,9 +482,24 @@ static hipError_t front1_t(const Launch &l, const uint32_t *in, const float *lut
     return hipGetLastError();
 }
 
+template <int D, bool AN>
+static hipError_t front1s_t(const Launch &l, const uint32_t *in, const float *lut, uint32_t *a16,
+                            const double *G, double *e) {
+    const int rows = AMX_BLOCK / 2;
+    dim3 grid((unsigned)((l.n_seg + rows - 1) / rows));
+    hipLaunchKernelGGL((k_front1s<D, AN>), grid, dim3(AMX_BLOCK), 0, l.stream, l.cd, l.chunks,
+                       l.segs, l.n_seg, l.L, in, lut, a16, G, e);
+    return hipGetLastError();
+}
+
 template <int D, int WIN>
 static hipError_t front1_an(const Launch &l, bool an, const uint32_t *in, const float *lut,
                             uint32_t *a16, const double *G, double *e) {
+    if constexpr (WIN == 2) {
+        if (l.L % AMX_TF) return hipErrorInvalidValue;
+        return an ? front1s_t<D, true>(l, in, lut, a16, G, e)
+                  : front1s_t<D, false>(l, in, lut, a16, G, e);
+    }
     return an ? front1_t<D, WIN, true>(l, in, lut, a16, G, e)
               : front1_t<D, WIN, false>(l, in, lut, a16, G, e);
 }
