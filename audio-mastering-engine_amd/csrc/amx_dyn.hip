@@ -43,7 +43,6 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
                                                    const ChunkDev *__restrict__ chunks,
                                                    const uint32_t *__restrict__ bands,
                                                    const double *__restrict__ tabs,
-                                                   uint16_t *__restrict__ rr,
                                                    double *__restrict__ mm, int64_t nloc) {
     constexpr int N = AMX_RMS_F + AMX_RMS_MAXLOOK;
     constexpr int PER = N / AMX_BLOCK;                 // 8 values per thread
@@ -55,7 +54,6 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
     const int64_t base = (int64_t)blockIdx.x * AMX_RMS_F;
     if (base >= ch.n) return;                          // block-uniform
     const uint32_t *x = bands + b * nloc + ch.loc_off;
-    uint16_t *r = rr + b * nloc + ch.loc_off;
     double *mo = mm + b * nloc + ch.loc_off;
     const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
     // LDS slot k holds frame base - look + k (frames before the chunk count as 0)
@@ -99,108 +97,217 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
         const long long S = P[n + look - 1] - (n > 0 ? P[n - 1] : 0);
         const uint32_t rms = cnt ? (uint32_t)sqrt((double)S / (double)cnt) : 0u;
         const uint32_t rc = rms > 32768u ? 32768u : rms;      // |sample| <= 32768
-        r[i] = (uint16_t)rc;
         mo[i] = mt[rc];
     }
 }
 
 // --------------------------------------------------------- envelope helpers
-struct EnvTab {
-    const double *m;     // per-frame max_attenuation (k_rms)
-    double A, R;         // attack / release frames (pydub frame_count(ms=5 / 50))
-    int rthr;
-};
+// The step needs only m: over-threshold <=> m != 0 for the reference's arithmetic
+// (m != 0 needs 20 log10(r/thr) > 0, i.e. r > thr; and when m == 0 both branches
+// return att unchanged: min(att + 0, 0) = 0 = att when att <= 0, max(att - 0, 0)
+// = att otherwise), so frames below the threshold -- and frames outside a chunk,
+// fed as m = 0 -- hold the state.
+
+// inc = m / A, dec = m / R exactly as IEEE division (pydub): with RCP the quotient
+// is formed as q = m (1/A) corrected by one FMA residual step -- the same correctly
+// rounded value (Markstein), checked on the host for every table m (ChainDev::env_rcp)
+template <bool RCP>
+__device__ __forceinline__ double env_div(double m, double a, double ra) {
+    if constexpr (RCP) {
+        const double q = m * ra;
+        return fma(fma(-q, a, m), ra, q);
+    } else {
+        return m / a;
+    }
+}
 
 // pydub envelope step, exact, branch-free (both candidates, then select)
-__device__ __forceinline__ double env_step(double att, bool over, double m, double inc,
-                                           double dec) {
+__device__ __forceinline__ double env_step3(double att, double m, double inc, double dec) {
     const double up = fmin(att + inc, m);          // attenuation += inc; min(., max_att)
     const double dn = fmax(att - dec, 0.0);        // attenuation -= dec; max(., 0)
-    return (over && att <= m) ? up : dn;
+    return (m != 0.0 && att <= m) ? up : dn;
 }
 
-// audioop.mul clamp + floor (CPython Modules/audioop.c fbound)
+template <bool RCP>
+__device__ __forceinline__ double env_step(const ChainDev &cd, double att, double m) {
+    return env_step3(att, m, env_div<RCP>(m, cd.env_A, cd.env_rA), env_div<RCP>(m, cd.env_R, cd.env_rR));
+}
+
+// audioop.mul clamp + floor (CPython Modules/audioop.c fbound), branch-free:
+// > 32767 -> 32767, < -32767 -> -32768, then floor
 __device__ __forceinline__ int mul16(int v, double f) {
-    double val = (double)v * f;
-    if (val > 32767.0) val = 32767.0;
-    else if (val < -32768.0 + 1.0) val = -32768.0;
-    return (int)floor(val);
+    const double val = fmin((double)v * f, 32767.0);
+    return (int)floor(val < -32768.0 + 1.0 ? -32768.0 : val);
 }
 
-// the gained frame for attenuation att (:306-308 output, audioop.mul)
-__device__ __forceinline__ uint32_t gain_frame(uint32_t v, double att) {
-    if (att == 0.0) return v;
-    const double f = exp10(-att / 20.0);
+// 10^x for the gain: ROCm device-libs' exp10 (ocml) operation for operation --
+// k = rint(x log2 10), r = x - k log10 2 (two-part), u = r ln 10 (two-part),
+// e^u by a degree-11 polynomial, scaled by 2^k -- so the values are those the
+// library gives; written out here so the constants are scalar operands of the
+// FMAs.  The library's overflow / underflow selects are left out: x = -att/20 is
+// finite and <= 0, and 2^k underflows to 0 by itself for very negative x.
+__device__ __forceinline__ double exp10_gain(const double *__restrict__ E, double x) {
+    const double k = rint(x * E[0]);
+    double r = fma(E[1], k, x);
+    r = fma(E[2], k, r);
+    double u = r * E[3];
+    u = fma(E[4], r, u);
+    double p = fma(E[5], u, E[6]);
+#pragma unroll
+    for (int i = 7; i < 15; i++) p = fma(u, p, E[i]);
+    p = fma(u, p, 1.0);
+    p = fma(u, p, 1.0);
+    return ldexp(p, (int)k);
+}
+
+// the gained frame for attenuation att (:306-308 output, audioop.mul).
+// att == 0 is the reference's "no change"; exp10(-0/20) == 1 and mul16(v, 1) == v,
+// so the branch-free form gives the same frame and keeps lanes converged.
+// -att / 20 is the IEEE quotient, formed by reciprocal multiply + one FMA residual
+// step (Markstein: exact for a correctly rounded 1/20; tests/test_host.py checks it
+// against division on random attenuations).
+__device__ __forceinline__ uint32_t gain_frame(const ChainDev &cd, uint32_t v, double att) {
+    const double q = -att * cd.exc[15];
+    const double f = exp10_gain(cd.exc, fma(fma(-q, 20.0, -att), cd.exc[15], q));
     return pack2((int16_t)mul16(lo16(v), f), (int16_t)mul16(hi16(v), f));
 }
 
-#define AMX_ENV_B 8   // frames per batch: table gathers issued ahead of the chain
+#define AMX_ENV_TF_ 16   // checkpoint spacing (frames)
 
-// run the envelope over frames [f0, f1) of r from att; optionally write gained output
-template <bool OUT>
-__device__ __forceinline__ double env_run(const EnvTab &T, const uint16_t *r, int64_t f0,
-                                          int64_t f1, double att, bool &any_over,
-                                          const uint32_t *x, uint32_t *g) {
-    for (int64_t f = f0; f < f1; f += AMX_ENV_B) {
-        double m[AMX_ENV_B], inc[AMX_ENV_B], dec[AMX_ENV_B];
-        bool ov[AMX_ENV_B];
-        uint32_t xv[AMX_ENV_B];
-#pragma unroll
-        for (int q = 0; q < AMX_ENV_B; q++) {
-            const bool ok = f + q < f1;
-            const int64_t fc = ok ? f + q : f0;        // clamped, unconditional (tile_load)
-            const int rv = r[fc];
-            const double mv = T.m[fc];
-            ov[q] = ok && rv >= T.rthr;
-            m[q] = ok ? mv : 0.0;
-            inc[q] = m[q] / T.A;
-            dec[q] = m[q] / T.R;
-            if (OUT) xv[q] = x[ok ? f + q : f0];
+// Wave-cooperative re-run of one segment's frames [f0, f1) (chunk-local; f0 a
+// multiple of 16) from the new start ns, with the stored trajectory from os re-run
+// in lockstep: every lane of the wave calls it with the same arguments.  Per
+// 64-frame window each lane loads and divides one frame (coalesced), the two
+// recurrences run on broadcast values (uniform across lanes), each lane keeps the
+// new state before its own frame, and the lanes on 16-frame boundaries rewrite
+// their checkpoint -- only up to the frame where the two trajectories coincide
+// (identical from there on, the old checkpoints stand).  Returns the segment's
+// end state (the old end if they coincided).
+template <bool RCP>
+__device__ double env_rerun_wave(const ChainDev &cd, const double *m, double *ckr, int64_t f0,
+                                 int64_t f1, double os, double ns, double old_end) {
+    const int lane = threadIdx.x & 63;
+    double a = os, c = ns;
+    for (int64_t base = f0; base < f1; base += 64) {
+        const int64_t fl = base + lane;
+        const bool ok = fl < f1;
+        const double ml = ok ? m[fl] : 0.0;
+        const double il = env_div<RCP>(ml, cd.env_A, cd.env_rA);
+        const double dl = env_div<RCP>(ml, cd.env_R, cd.env_rR);
+        const int n = (int)(f1 - base < 64 ? f1 - base : 64);
+        double mine = c;
+        int stop = n;
+        for (int q = 0; q < n; q++) {
+            mine = lane == q ? c : mine;                 // state before frame base + q
+            const double mq = __shfl(ml, q), iq = __shfl(il, q), dq = __shfl(dl, q);
+            a = env_step3(a, mq, iq, dq);
+            c = env_step3(c, mq, iq, dq);
+            if (a == c) { stop = q; break; }
         }
-#pragma unroll
-        for (int q = 0; q < AMX_ENV_B; q++) {
-            if (f + q >= f1) break;
-            att = env_step(att, ov[q], m[q], inc[q], dec[q]);
-            any_over |= ov[q];
-            if (OUT) g[f + q] = gain_frame(xv[q], att);
-        }
+        if (lane <= stop && lane < n && (lane & (AMX_ENV_TF_ - 1)) == 0)
+            ckr[fl / AMX_ENV_TF_] = mine;
+        if (stop < n) return old_end;
     }
-    return att;
+    return c;
 }
 
 // ------------------------------------------------------- round 0: speculation
-// One thread per (envelope segment, band).  s = state at the segment start from a
-// warm-up of W frames begun at rest; e = state at the segment end; act = the
-// segment has an over-threshold frame (else its transfer is the identity).
-__global__ void __launch_bounds__(AMX_BLOCK) k_env0(const ChainDev *__restrict__ cdp,
-                                                    const ChunkDev *__restrict__ chunks,
-                                                    const SegDev *__restrict__ es, int n_es,
-                                                    const uint16_t *__restrict__ rr,
-                                                    const uint32_t *__restrict__ bands,
-                                                    const double *__restrict__ mm,
-                                                    uint32_t *__restrict__ gained,
-                                                    double *__restrict__ sv,
-                                                    double *__restrict__ ev,
-                                                    int *__restrict__ act, int64_t nloc,
-                                                    int warm) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+// One lane per (envelope segment, band), a wave (= workgroup) per 64 consecutive
+// segments.  Each lane runs the attenuation recurrence over its segment from
+// att = 0 started W frames earlier (the warm-up: after a clamp event the trajectory
+// no longer depends on the start) and records its start guess s_j
+// (the state when its first frame begins), end state e_j, whether it has an
+// over-threshold frame, and a checkpoint -- the state before every 16th frame of
+// the chunk -- from which k_gain_overlay re-derives every frame's attenuation in
+// parallel.  No gains are computed here: this is the latency-bound sequential
+// part, kept to ~16 fp64 operations per frame.
+// Frames move in 16-frame tiles.  A lane's tile is one 128-B row of m (64 rows per
+// wave); the wave loads the 64 rows cooperatively -- lane l moves 16-B piece l % 8
+// of rows 8 i + l / 8, so each load instruction covers 8 whole lines instead of 64
+// lines' 16-B fragments -- stages them in LDS (padded rows, conflict-free b128
+// reads) and issues the next tile's loads before computing this one.  Frames
+// before the chunk or after the segment are fed as m = 0 (state held); the m
+// buffer is padded so those rows read in bounds.  W and Le are multiples of 16 and
+// chunk rows start 16-frame aligned, so the warm-up / main boundary is
+// tile-uniform, every vector is 16-B aligned and checkpoints fall on tile starts.
+#define AMX_ENV_TF 16
+#define AMX_ENV_MP 18      // m tile pitch in doubles (144 B)
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+template <bool RCP>
+__global__ void __launch_bounds__(64) k_env0(const ChainDev *__restrict__ cdp,
+                                             const ChunkDev *__restrict__ chunks,
+                                             const SegDev *__restrict__ es, int n_es,
+                                             const double *__restrict__ mm,
+                                             double *__restrict__ ck,
+                                             double *__restrict__ sv, double *__restrict__ ev,
+                                             int *__restrict__ act, int64_t nloc, int warm,
+                                             int Le) {
+    __shared__ __attribute__((aligned(16))) double sm[64 * AMX_ENV_MP];
+    const ChainDev &cd = *cdp;
+    const int lane = threadIdx.x;
+    const int j = blockIdx.x * 64 + lane;
     const int b = blockIdx.y;
-    if (j >= n_es) return;
-    const SegDev sg = es[j];
+    const bool valid = j < n_es;
+    const SegDev sg = es[valid ? j : n_es - 1];
     const ChunkDev ch = chunks[sg.chunk];
-    const uint16_t *r = rr + b * nloc + ch.loc_off;
-    const uint32_t *x = bands + b * nloc + ch.loc_off;
-    uint32_t *g = gained + b * nloc + ch.loc_off;
-    const EnvTab T{mm + b * nloc + ch.loc_off, 5.0 * (cdp->fs / 1000.0), 50.0 * (cdp->fs / 1000.0),
-                   cdp->rthr[b]};
-    int64_t w0 = sg.pos - warm;
-    if (w0 < 0) w0 = 0;
-    bool any = false, dummy = false;
-    double att = env_run<false>(T, r, w0, sg.pos, 0.0, dummy, nullptr, nullptr);
-    sv[(int64_t)b * n_es + j] = att;
-    att = env_run<true>(T, r, sg.pos, sg.pos + sg.len, att, any, x, g);
-    ev[(int64_t)b * n_es + j] = att;
-    act[(int64_t)b * n_es + j] = any ? 1 : 0;
+    const int64_t rowoff = b * nloc + ch.loc_off;       // this lane's chunk row
+    const int64_t start = sg.pos - warm;                // frame of step 0 (may be < 0)
+    const int64_t end = valid ? sg.pos + sg.len : sg.pos;
+    double *ckr = ck + rowoff / AMX_ENV_TF;             // checkpoint k: before frame 16 k
+    const int ntile = (warm + Le) / AMX_ENV_TF, nwarm = warm / AMX_ENV_TF;
+    const double *mrow[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int r = 8 * i + (lane >> 3);
+        mrow[i] = mm + __shfl(rowoff + start, r) + 2 * (lane & 7);
+    }
+    d2v M[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) M[i] = *reinterpret_cast<const d2v *>(mrow[i]);
+    double att = 0.0, s_spec = 0.0;
+    bool any = false;
+    for (int q = 0; q < ntile; q++) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int r = 8 * i + (lane >> 3);
+            *reinterpret_cast<d2v *>(sm + r * AMX_ENV_MP + 2 * (lane & 7)) = M[i];
+        }
+        __builtin_amdgcn_wave_barrier();
+        {
+            const int qn = (q + 1 < ntile ? q + 1 : q) * AMX_ENV_TF;   // last: re-read, unused
+#pragma unroll
+            for (int i = 0; i < 8; i++) M[i] = *reinterpret_cast<const d2v *>(mrow[i] + qn);
+        }
+        const int64_t f0 = start + (int64_t)q * AMX_ENV_TF;
+        const bool in = f0 >= 0 && f0 < end;           // whole tile in (else held)
+        double mv[AMX_ENV_TF];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const d2v v = *reinterpret_cast<const d2v *>(sm + lane * AMX_ENV_MP + 2 * i);
+            mv[2 * i] = in ? v.x : 0.0;
+            mv[2 * i + 1] = in ? v.y : 0.0;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (q == nwarm) s_spec = att;
+        if (q >= nwarm) {
+            if (in) ckr[f0 / AMX_ENV_TF] = att;
+            // the partial last tile of a chunk-final segment holds the state past the end
+            if (f0 + AMX_ENV_TF > end) {
+#pragma unroll
+                for (int f = 0; f < AMX_ENV_TF; f++) mv[f] = f0 + f < end ? mv[f] : 0.0;
+            }
+#pragma unroll
+            for (int f = 0; f < AMX_ENV_TF; f++) any |= mv[f] != 0.0;
+        }
+#pragma unroll
+        for (int f = 0; f < AMX_ENV_TF; f++) att = env_step<RCP>(cd, att, mv[f]);
+    }
+    if (valid) {
+        sv[(int64_t)b * n_es + j] = s_spec;
+        ev[(int64_t)b * n_es + j] = att;
+        act[(int64_t)b * n_es + j] = any ? 1 : 0;
+    }
 }
 
 // prev[j] = the nearest earlier active segment of the same chunk (or -1): the
@@ -233,103 +340,90 @@ __global__ void __launch_bounds__(64) k_env_prev(const ChunkDev *__restrict__ ch
     }
 }
 
-// re-run segment j from the new start `ns` while re-running the stored trajectory
-// from `os` in lockstep; rewrite the gained output until the two coincide.
-// Returns the segment's end state (old end if they coincided).
-__device__ double env_rerun(const EnvTab &T, const uint16_t *r, const uint32_t *x, uint32_t *g,
-                            int64_t f0, int64_t f1, double os, double ns, double old_end) {
-    double a = os, c = ns;
-    for (int64_t f = f0; f < f1; f += AMX_ENV_B) {
-        double m[AMX_ENV_B], inc[AMX_ENV_B], dec[AMX_ENV_B];
-        bool ov[AMX_ENV_B];
-        uint32_t xv[AMX_ENV_B];
-#pragma unroll
-        for (int q = 0; q < AMX_ENV_B; q++) {
-            const bool ok = f + q < f1;
-            const int64_t fc = ok ? f + q : f0;        // clamped, unconditional (tile_load)
-            const int rv = r[fc];
-            const double mv = T.m[fc];
-            ov[q] = ok && rv >= T.rthr;
-            m[q] = ok ? mv : 0.0;
-            inc[q] = m[q] / T.A;
-            dec[q] = m[q] / T.R;
-            xv[q] = x[ok ? f + q : f0];
-        }
-#pragma unroll
-        for (int q = 0; q < AMX_ENV_B; q++) {
-            if (f + q >= f1) return c;
-            a = env_step(a, ov[q], m[q], inc[q], dec[q]);
-            c = env_step(c, ov[q], m[q], inc[q], dec[q]);
-            if (a == c) return old_end;                // identical from here on
-            g[f + q] = gain_frame(xv[q], c);
-        }
+// the wave fixes segment sg of band b from the new start ns (all lanes, uniform args)
+template <bool RCP>
+__device__ __forceinline__ double env_fix_segment(const ChainDev &cd, const SegDev &sg,
+                                                  const ChunkDev &ch, int b, int64_t nloc,
+                                                  const double *mm, double *ck, bool active,
+                                                  double os, double ns, double old_end) {
+    double *ckr = ck + (b * nloc + ch.loc_off) / AMX_ENV_TF_;
+    if (!active) {
+        // identity transfer: the held state is every checkpoint of the segment
+        const int64_t k0 = sg.pos / AMX_ENV_TF_, k1 = (sg.pos + sg.len + AMX_ENV_TF_ - 1) / AMX_ENV_TF_;
+        for (int64_t k = k0 + (threadIdx.x & 63); k < k1; k += 64) ckr[k] = ns;
+        return ns;
     }
-    return c;
+    return env_rerun_wave<RCP>(cd, mm + b * nloc + ch.loc_off, ckr, sg.pos, sg.pos + sg.len, os, ns,
+                               old_end);
 }
 
 // ------------------------------------------------ rounds: parallel fix-up
-// Reads e_in (previous round), writes e_out; s is updated in place (segment-owned).
-__global__ void __launch_bounds__(AMX_BLOCK) k_envfix(const ChainDev *__restrict__ cdp,
-                                                      const ChunkDev *__restrict__ chunks,
-                                                      const SegDev *__restrict__ es, int n_es,
-                                                      const uint16_t *__restrict__ rr,
-                                                      const uint32_t *__restrict__ bands,
-                                                      const double *__restrict__ mm,
-                                                      uint32_t *__restrict__ gained,
-                                                      double *__restrict__ sv,
-                                                      const double *__restrict__ e_in,
-                                                      double *__restrict__ e_out,
-                                                      const int *__restrict__ act,
-                                                      const int *__restrict__ prev,
-                                                      int64_t nloc) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+// A wave per 64 segments: lanes whose start disagrees with the end of their
+// predecessor (previous round's ends e_in) are fixed one after another by the
+// whole wave; e_out gets every segment's end, s is updated in place.
+template <bool RCP>
+__global__ void __launch_bounds__(64) k_envfix(const ChainDev *__restrict__ cdp,
+                                               const ChunkDev *__restrict__ chunks,
+                                               const SegDev *__restrict__ es, int n_es,
+                                               const double *__restrict__ mm,
+                                               double *__restrict__ ck,
+                                               double *__restrict__ sv,
+                                               const double *__restrict__ e_in,
+                                               double *__restrict__ e_out,
+                                               const int *__restrict__ act,
+                                               const int *__restrict__ prev, int64_t nloc) {
+    const ChainDev &cd = *cdp;
+    const int lane = threadIdx.x;
+    const int j = blockIdx.x * 64 + lane;
     const int b = blockIdx.y;
-    if (j >= n_es) return;
-    const int64_t k = (int64_t)b * n_es + j;
-    const int p = prev[k];
-    const double ns = p >= 0 ? e_in[(int64_t)b * n_es + p] : 0.0;
-    const double os = sv[k];
-    if (ns == os) { e_out[k] = e_in[k]; return; }
-    const SegDev sg = es[j];
-    const ChunkDev ch = chunks[sg.chunk];
-    const uint32_t *x = bands + b * nloc + ch.loc_off;
-    uint32_t *g = gained + b * nloc + ch.loc_off;
-    if (!act[k]) {
-        // identity transfer: the held state is the new start for every frame
-        for (int64_t f = sg.pos; f < sg.pos + sg.len; f++) g[f] = gain_frame(x[f], ns);
-        e_out[k] = ns;
-    } else {
-        const uint16_t *r = rr + b * nloc + ch.loc_off;
-        const EnvTab T{mm + b * nloc + ch.loc_off, 5.0 * (cdp->fs / 1000.0),
-                       50.0 * (cdp->fs / 1000.0), cdp->rthr[b]};
-        e_out[k] = env_rerun(T, r, x, g, sg.pos, sg.pos + sg.len, os, ns, e_in[k]);
+    const bool valid = j < n_es;
+    const int64_t k = (int64_t)b * n_es + (valid ? j : 0);
+    double ns = 0.0, os = 0.0, en = 0.0;
+    bool need = false;
+    if (valid) {
+        const int p = prev[k];
+        ns = p >= 0 ? e_in[(int64_t)b * n_es + p] : 0.0;
+        os = sv[k];
+        en = e_in[k];
+        need = !(ns == os);
     }
-    sv[k] = ns;
+    unsigned long long work = __ballot(need);
+    while (work) {
+        const int w = __ffsll((long long)work) - 1;
+        work &= work - 1;
+        const int jw = blockIdx.x * 64 + w;
+        const SegDev sg = es[jw];
+        const ChunkDev ch = chunks[sg.chunk];
+        const double nsw = __shfl(ns, w), osw = __shfl(os, w), enw = __shfl(en, w);
+        const bool aw = act[(int64_t)b * n_es + jw] != 0;
+        const double r = env_fix_segment<RCP>(cd, sg, ch, b, nloc, mm, ck, aw, osw, nsw, enw);
+        if (lane == w) en = r;
+    }
+    if (valid) {
+        e_out[k] = en;
+        if (need) sv[k] = ns;
+    }
 }
 
 // --------------------------------------- final in-order walk (exactness net)
 // One wave per (chunk, band): find the first segment whose start disagrees with
-// its predecessor's end (64 at a time), fix it on lane 0, continue after it.
+// its predecessor's end (64 at a time) and fix it with the whole wave, continue
+// after it.
+template <bool RCP>
 __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
                                                const ChunkDev *__restrict__ chunks,
                                                const SegDev *__restrict__ es, int n_es,
                                                const int *__restrict__ eseg0,
                                                const int *__restrict__ neseg,
-                                               const uint16_t *__restrict__ rr,
-                                               const uint32_t *__restrict__ bands,
                                                const double *__restrict__ mm,
-                                               uint32_t *__restrict__ gained,
+                                               double *__restrict__ ck,
                                                double *__restrict__ sv, double *__restrict__ ev,
                                                const int *__restrict__ act,
                                                const int *__restrict__ prev, int64_t nloc) {
+    const ChainDev &cd = *cdp;
     const int c = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
     const int s0 = eseg0[c], s1 = s0 + neseg[c];
     const ChunkDev ch = chunks[c];
-    const uint16_t *r = rr + b * nloc + ch.loc_off;
-    const uint32_t *x = bands + b * nloc + ch.loc_off;
-    uint32_t *g = gained + b * nloc + ch.loc_off;
-    const EnvTab T{mm + b * nloc + ch.loc_off, 5.0 * (cdp->fs / 1000.0), 50.0 * (cdp->fs / 1000.0),
-                   cdp->rthr[b]};
     double *S = sv + (int64_t)b * n_es, *E = ev + (int64_t)b * n_es;
     const int *A = act + (int64_t)b * n_es, *Pv = prev + (int64_t)b * n_es;
     int cur = s0;
@@ -343,112 +437,173 @@ __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
                 const double ns = p >= 0 ? E[p] : 0.0;
                 bad = !(ns == S[j]);
             }
-            const unsigned long long m = __ballot(bad);
-            if (m) { found = base + __ffsll((long long)m) - 1; break; }
+            const unsigned long long mk = __ballot(bad);
+            if (mk) { found = base + __ffsll((long long)mk) - 1; break; }
         }
         if (found >= s1) break;
+        const SegDev sg = es[found];
+        const int p = Pv[found];
+        const double ns = p >= 0 ? E[p] : 0.0;
+        const double r = env_fix_segment<RCP>(cd, sg, ch, b, nloc, mm, ck, A[found] != 0, S[found],
+                                              ns, E[found]);
+        __syncthreads();                    // every lane has read E/S of `found`
         if (lane == 0) {
-            const SegDev sg = es[found];
-            const int p = Pv[found];
-            const double ns = p >= 0 ? E[p] : 0.0;
-            if (!A[found]) {
-                for (int64_t f = sg.pos; f < sg.pos + sg.len; f++) g[f] = gain_frame(x[f], ns);
-                E[found] = ns;
-            } else {
-                E[found] = env_rerun(T, r, x, g, sg.pos, sg.pos + sg.len, S[found], ns, E[found]);
-            }
+            E[found] = r;
             S[found] = ns;
         }
         __threadfence_block();
+        __syncthreads();
         cur = found + 1;
     }
 }
 
-// ------------------------------------------------------------------- overlay
-// low.overlay(mid).overlay(high) (:309) of the gained bands -> chunk output with
-// pydub's ms-rounded lengths: n1 after the first overlay, n2 = out_n after the second.
-__global__ void __launch_bounds__(AMX_BLOCK) k_overlay(const ChunkDev *__restrict__ chunks,
-                                                       const uint32_t *__restrict__ gained,
-                                                       uint32_t *__restrict__ out, int64_t nloc,
-                                                       const int64_t *__restrict__ n1tab) {
+// ------------------------------------------------------- gains + overlay
+// The compressor output (audioop.mul of each frame by 10^(-att/20), :306-308) of
+// all three bands and low.overlay(mid).overlay(high) (:309) with pydub's
+// ms-rounded lengths (n1 after the first overlay, n2 = out_n after the second).
+// A thread owns 16 consecutive output frames of a chunk: per band it re-runs the
+// recurrence from the checkpoint before its first frame (exact: the same operation
+// sequence from the same state) and applies the gain; the three gained samples are
+// summed with int16 saturation.  Loads and stores are 16-B vectors over
+// consecutive threads (coalesced); this is the parallel, throughput-bound half.
+template <bool RCP>
+__global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__restrict__ cdp,
+                                                            const ChunkDev *__restrict__ chunks,
+                                                            const double *__restrict__ mm,
+                                                            const double *__restrict__ ck,
+                                                            const uint32_t *__restrict__ bands,
+                                                            uint32_t *__restrict__ out,
+                                                            int64_t nloc,
+                                                            const int64_t *__restrict__ n1tab) {
+    const ChainDev &cd = *cdp;
     const int c = blockIdx.y;
     const ChunkDev ch = chunks[c];
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i0 = g * AMX_ENV_TF_;
     const int64_t n2 = ch.out_n;
-    if (i >= n2) return;
+    if (i0 >= n2) return;
     const int64_t n1 = n1tab[c];
-    uint32_t res = 0;
-    if (i < ch.n) {
-        const uint32_t v0 = gained[ch.loc_off + i];
-        const uint32_t v1 = gained[nloc + ch.loc_off + i];
-        const uint32_t v2 = gained[2 * nloc + ch.loc_off + i];
-        int16_t o[2];
+    const int64_t r0 = ch.loc_off + i0;                 // band 0 row of frame i0
+    double att[3];
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const int a0 = k ? hi16(v0) : lo16(v0), a1 = k ? hi16(v1) : lo16(v1);
-            const int a2 = k ? hi16(v2) : lo16(v2);
-            const int s1 = i < n1 ? (int)sat16(a0 + a1) : 0;
-            o[k] = sat16(s1 + a2);
+    for (int b = 0; b < 3; b++) att[b] = i0 < ch.n ? ck[(b * nloc + r0) / AMX_ENV_TF_] : 0.0;
+    uint32_t *op = out + ch.out_off + i0;
+    const bool vec = i0 + AMX_ENV_TF_ <= n2 && ((ch.out_off + i0) & 3) == 0;
+    // two halves of 8 frames: 3 bands x (8 m + 8 samples) in flight per half
+#pragma unroll 1
+    for (int h = 0; h < AMX_ENV_TF_; h += 8) {
+        const int64_t i = i0 + h;
+        d2v M[3][4];
+        u4v X[3][2];
+#pragma unroll
+        for (int b = 0; b < 3; b++) {
+            const d2v *mp = reinterpret_cast<const d2v *>(mm + b * nloc + r0 + h);
+            const u4v *xp = reinterpret_cast<const u4v *>(bands + b * nloc + r0 + h);
+#pragma unroll
+            for (int k = 0; k < 4; k++) M[b][k] = mp[k];
+#pragma unroll
+            for (int k = 0; k < 2; k++) X[b][k] = xp[k];
         }
-        res = pack2(o[0], o[1]);
+        uint32_t o[8];
+#pragma unroll
+        for (int f = 0; f < 8; f++) {
+            const bool in = i + f < ch.n;
+            int s[3][2];
+#pragma unroll
+            for (int b = 0; b < 3; b++) {
+                double mv = (f & 1) ? M[b][f >> 1].y : M[b][f >> 1].x;
+                mv = in ? mv : 0.0;
+                att[b] = env_step<RCP>(cd, att[b], mv);
+                const uint32_t gv = gain_frame(cd, X[b][f >> 2][f & 3], att[b]);
+                s[b][0] = lo16(gv);
+                s[b][1] = hi16(gv);
+            }
+            const bool in1 = i + f < n1;
+            int16_t q[2];
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int s1 = in1 ? (int)sat16(s[0][k] + s[1][k]) : 0;
+                q[k] = sat16(s1 + s[2][k]);
+            }
+            o[f] = in ? pack2(q[0], q[1]) : 0u;
+        }
+        if (vec) {
+            u4v *vp = reinterpret_cast<u4v *>(op + h);
+            vp[0] = u4v{o[0], o[1], o[2], o[3]};
+            vp[1] = u4v{o[4], o[5], o[6], o[7]};
+        } else {
+#pragma unroll
+            for (int f = 0; f < 8; f++)
+                if (i + f < n2) op[h + f] = o[f];
+        }
     }
-    out[ch.out_off + i] = res;
 }
 
 // ---------------------------------------------------------------- launchers
-hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *r, double *m) {
+hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, double *m) {
     if (d.look > AMX_RMS_MAXLOOK) return hipErrorInvalidValue;
     dim3 g((unsigned)((d.max_chunk_n + AMX_RMS_F - 1) / AMX_RMS_F), (unsigned)d.n_chunks, 3);
     if (empty(g)) return hipSuccess;
     hipLaunchKernelGGL(k_rms, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks,
-                       reinterpret_cast<const uint32_t *>(bands), d.tabs, r, m, d.nloc);
+                       reinterpret_cast<const uint32_t *>(bands), d.tabs, m, d.nloc);
     return hipGetLastError();
 }
 
-hipError_t launch_env(const DynLaunch &d, const uint16_t *r, const double *m, const int16_t *bands,
-                      int16_t *gained, double *sv, double *e0, double *e1, int *act, int *prev,
-                      int rounds) {
-    if (d.n_es <= 0) return hipSuccess;
-    const uint32_t *x = reinterpret_cast<const uint32_t *>(bands);
-    uint32_t *g = reinterpret_cast<uint32_t *>(gained);
-    dim3 grid = grid1(d.n_es);
-    grid.y = 3;
-    hipLaunchKernelGGL(k_env0, grid, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, d.es, d.n_es, r, x,
-                       m, g, sv, e0, act, d.nloc, d.warm);
+template <bool RCP>
+static void env_launch_t(const DynLaunch &d, const double *m, double *ck, double *sv, double *e0,
+                         double *e1, int *act, int *prev, int rounds) {
+    const dim3 gw((unsigned)((d.n_es + 63) / 64), 3);
+    hipLaunchKernelGGL(k_env0<RCP>, gw, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es, m, ck, sv,
+                       e0, act, d.nloc, d.warm, d.Le);
     hipLaunchKernelGGL(k_env_prev, dim3((unsigned)d.n_chunks, 3), dim3(64), 0, d.st, d.chunks,
                        d.eseg0, d.neseg, d.n_es, act, prev);
     double *ein = e0, *eout = e1;
     for (int k = 0; k < rounds; k++) {
-        hipLaunchKernelGGL(k_envfix, grid, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, d.es, d.n_es,
-                           r, x, m, g, sv, ein, eout, act, prev, d.nloc);
+        hipLaunchKernelGGL(k_envfix<RCP>, gw, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es, m,
+                           ck, sv, ein, eout, act, prev, d.nloc);
         double *tmp = ein;
         ein = eout;
         eout = tmp;
     }
+}
+
+hipError_t launch_env(const DynLaunch &d, const double *m, double *ck, double *sv, double *e0,
+                      double *e1, int *act, int *prev, int rounds) {
+    if (d.n_es <= 0) return hipSuccess;
+    if (d.warm % AMX_ENV_TF || d.Le % AMX_ENV_TF) return hipErrorInvalidValue;
+    if (d.rcp) env_launch_t<true>(d, m, ck, sv, e0, e1, act, prev, rounds);
+    else env_launch_t<false>(d, m, ck, sv, e0, e1, act, prev, rounds);
     return hipGetLastError();
 }
 
 // ends: the array the last round wrote (e0 if rounds is even, else e1)
-hipError_t launch_envseq(const DynLaunch &d, const uint16_t *r, const double *m,
-                         const int16_t *bands,
-                         int16_t *gained, double *sv, double *ends, const int *act,
-                         const int *prev) {
+hipError_t launch_envseq(const DynLaunch &d, const double *m, double *ck, double *sv, double *ends,
+                         const int *act, const int *prev) {
     if (d.n_es <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_envseq, dim3((unsigned)d.n_chunks, 3), dim3(64), 0, d.st, d.cd, d.chunks,
-                       d.es, d.n_es, d.eseg0, d.neseg, r,
-                       reinterpret_cast<const uint32_t *>(bands), m,
-                       reinterpret_cast<uint32_t *>(gained), sv, ends, act, prev, d.nloc);
+    const dim3 gr((unsigned)d.n_chunks, 3);
+    if (d.rcp)
+        hipLaunchKernelGGL(k_envseq<true>, gr, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es,
+                           d.eseg0, d.neseg, m, ck, sv, ends, act, prev, d.nloc);
+    else
+        hipLaunchKernelGGL(k_envseq<false>, gr, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es,
+                           d.eseg0, d.neseg, m, ck, sv, ends, act, prev, d.nloc);
     return hipGetLastError();
 }
 
-hipError_t launch_overlay(const DynLaunch &d, const int16_t *gained, int16_t *out,
-                          int64_t max_chunk_out, const int64_t *n1tab) {
-    dim3 g = grid1(max_chunk_out);
-    g.y = (unsigned)d.n_chunks;
+hipError_t launch_gain_overlay(const DynLaunch &d, const double *m, const double *ck,
+                               const int16_t *bands, int16_t *out, int64_t max_chunk_out,
+                               const int64_t *n1tab) {
+    dim3 g((unsigned)((max_chunk_out + AMX_ENV_TF_ * AMX_BLOCK - 1) / (AMX_ENV_TF_ * AMX_BLOCK)),
+           (unsigned)d.n_chunks);
     if (empty(g)) return hipSuccess;
-    hipLaunchKernelGGL(k_overlay, g, dim3(AMX_BLOCK), 0, d.st, d.chunks,
-                       reinterpret_cast<const uint32_t *>(gained),
-                       reinterpret_cast<uint32_t *>(out), d.nloc, n1tab);
+    const uint32_t *x = reinterpret_cast<const uint32_t *>(bands);
+    uint32_t *o = reinterpret_cast<uint32_t *>(out);
+    if (d.rcp)
+        hipLaunchKernelGGL(k_gain_overlay<true>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, m, ck,
+                           x, o, d.nloc, n1tab);
+    else
+        hipLaunchKernelGGL(k_gain_overlay<false>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, m, ck,
+                           x, o, d.nloc, n1tab);
     return hipGetLastError();
 }
 

@@ -47,6 +47,14 @@ struct ChainDev {
     //   shelf: b0 b1 b2 a1 a2 gx     (gx = g-1, or the negative-gain factor g / f32(g))
     //   peak : 4 x [b0 b1 b2 a1 a2] gm1
     double eqc[AMX_EQC];
+    // envelope divisions inc = m / A, dec = m / R (pydub frame counts): env_rcp = 1
+    // when the reciprocal-multiply with one FMA correction was checked on the host to
+    // equal the IEEE quotient for every table value m (amx_dyn.hip env_div)
+    double env_A, env_R, env_rA, env_rR;
+    int32_t env_rcp, pad1_;
+    // exp10 constants of the gain (amx_dyn.hip exp10_gain): read through the plan so
+    // they are scalar operands of the FMAs (a 64-bit literal is not encodable)
+    double exc[16];
 };
 
 // A ~30 s chunk (ffmpeg segment, :178).  loc_off indexes chunk-local scratch.
@@ -124,20 +132,18 @@ struct DynLaunch {
     int n_es;
     const int *eseg0, *neseg;    // per chunk: first envelope segment, count
     int64_t nloc, max_chunk_n;
-    int look, warm;
+    int look, warm, Le, rcp;
     const double *tabs;
     hipStream_t st;
 };
-hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *r, double *m);
-hipError_t launch_env(const DynLaunch &d, const uint16_t *r, const double *m, const int16_t *bands,
-                      int16_t *gained, double *sv, double *e0, double *e1, int *act, int *prev,
-                      int rounds);
-hipError_t launch_envseq(const DynLaunch &d, const uint16_t *r, const double *m,
-                         const int16_t *bands,
-                         int16_t *gained, double *sv, double *ends, const int *act,
-                         const int *prev);
-hipError_t launch_overlay(const DynLaunch &d, const int16_t *gained, int16_t *out,
-                          int64_t max_chunk_out, const int64_t *n1tab);
+hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, double *m);
+hipError_t launch_env(const DynLaunch &d, const double *m, double *ck, double *sv, double *e0,
+                      double *e1, int *act, int *prev, int rounds);
+hipError_t launch_envseq(const DynLaunch &d, const double *m, double *ck, double *sv, double *ends,
+                         const int *act, const int *prev);
+hipError_t launch_gain_overlay(const DynLaunch &d, const double *m, const double *ck,
+                               const int16_t *bands, int16_t *out, int64_t max_chunk_out,
+                               const int64_t *n1tab);
 // loudness
 hipError_t launch_kw1(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L,
                       const int16_t *x, const double *G, double *e, uint32_t *pk,

@@ -162,7 +162,7 @@ struct amx_plan {
     int mask = 0, D = 0;
     int lev_eq = 0, lev_x = 0, lev_kw = 0;
     int mb = 0;
-    int Le = 1024, warm = 1024, rounds = 4;   // compressor envelope segments (amx_dyn.hip)
+    int Le = 1024, warm = 2048, rounds = 4;   // compressor envelope segments (amx_dyn.hip)
     int n_es = 0;
     std::vector<SegDev> esegs;
     std::vector<int> eseg0, neseg;
@@ -267,7 +267,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     if (!p) return fail(AMX_ENOMEM, "out of memory");
     p->desc = *desc;
     const int fs = desc->sample_rate;
-    if (desc->env_warm_frames >= 0) p->warm = desc->env_warm_frames;
+    if (desc->env_warm_frames >= 0) p->warm = (desc->env_warm_frames + 15) / 16 * 16;
     if (desc->env_rounds >= 0) p->rounds = desc->env_rounds;
     p->L = seg_frames > 0 ? seg_frames : 256;
     p->L = (p->L + AMX_TF_FRAMES - 1) / AMX_TF_FRAMES * AMX_TF_FRAMES;   // whole LDS tiles
@@ -405,6 +405,31 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
                 mt[2 * 32769 + r] = m / R;
             }
         }
+        // the device forms m / A as q = m (1/A), q + (m - q A) (1/A) (two FMAs, exact
+        // to the IEEE quotient by Markstein's theorem for a correctly rounded 1/A);
+        // checked here for every m the tables can produce
+        {
+            static const double exc[16] = {
+                0x1.a934f0979a371p+1, -0x1.34413509f79ffp-2, 0x1.9dc1da994fd21p-59,
+                -0x1.f48ad494ea3e9p-53, 0x1.26bb1bbb55516p+1, 0x1.ade156a5dcb37p-26,
+                0x1.28af3fca7ab0cp-22, 0x1.71dee623fde64p-19, 0x1.a01997c89e6b0p-16,
+                0x1.a01a014761f6ep-13, 0x1.6c16c1852b7b0p-10, 0x1.1111111122322p-7,
+                0x1.55555555502a1p-5, 0x1.5555555555511p-3, 0x1.000000000000bp-1, 0.05};
+            for (int i = 0; i < 16; i++) cd.exc[i] = exc[i];
+        }
+        cd.env_A = A;
+        cd.env_R = R;
+        cd.env_rA = 1.0 / A;
+        cd.env_rR = 1.0 / R;
+        cd.env_rcp = 1;
+        for (size_t i = 0; i < (size_t)3 * 3 * 32769 && cd.env_rcp; i += 1) {
+            if (i % (3 * 32769) >= 32769) continue;
+            const double m = tabs[i];
+            const double qa = m * cd.env_rA, qr = m * cd.env_rR;
+            const double ca = std::fma(std::fma(-qa, A, m), cd.env_rA, qa);
+            const double cr = std::fma(std::fma(-qr, R, m), cd.env_rR, qr);
+            if (ca != m / A || cr != m / R) cd.env_rcp = 0;
+        }
     }
     // ------------------------------------------------ chunks, tracks, segments
     int n_tracks = 0;
@@ -474,7 +499,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         p->n1tab.push_back(n1);
         p->max_chunk_out = n2 > p->max_chunk_out ? n2 : p->max_chunk_out;
         p->max_chunk_n = ch.n > p->max_chunk_n ? ch.n : p->max_chunk_n;
-        loc += ch.n;
+        loc += (ch.n + 15) / 16 * 16;   // chunk rows of per-frame scratch start 16-frame aligned
         outo += n2;
     }
     p->nloc = loc;
@@ -636,9 +661,11 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         p->o_sx = (size_t)align_up(off, nseg * 2 * AMX_XO_DIM * 8);
         p->o_bands = (size_t)align_up(off, 3 * nl * 4);
         const size_t ne = (size_t)p->n_es;
-        p->o_r = (size_t)align_up(off, 3 * nl * 2);
-        p->o_gain = (size_t)align_up(off, 3 * nl * 4);
-        p->o_m = (size_t)align_up(off, 3 * nl * 8);
+        p->o_gain = (size_t)align_up(off, (3 * nl / 16 + 64) * 8);   // envelope checkpoints
+        // m rows are read whole-tile by k_env0, from W frames before a chunk to the
+        // 16-frame tile past its end: pad the buffer on both sides
+        const size_t mpad = (size_t)p->warm + 64;
+        p->o_m = (size_t)align_up(off, (3 * nl + 2 * mpad) * 8) + mpad * 8;
         p->o_esv = (size_t)align_up(off, 3 * ne * 8);
         p->o_ee0 = (size_t)align_up(off, 3 * ne * 8);
         p->o_ee1 = (size_t)align_up(off, 3 * ne * 8);
@@ -713,8 +740,7 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     double *ex = p->mb ? wsp<double>(d_ws, p->o_ex) : nullptr;
     double *sx = p->mb ? wsp<double>(d_ws, p->o_sx) : nullptr;
     int16_t *bands = p->mb ? wsp<int16_t>(d_ws, p->o_bands) : nullptr;
-    uint16_t *r = p->mb ? wsp<uint16_t>(d_ws, p->o_r) : nullptr;
-    int16_t *gained = p->mb ? wsp<int16_t>(d_ws, p->o_gain) : nullptr;
+    double *ck = p->mb ? wsp<double>(d_ws, p->o_gain) : nullptr;
     double *mframe = p->mb ? wsp<double>(d_ws, p->o_m) : nullptr;
     double *esv = p->mb ? wsp<double>(d_ws, p->o_esv) : nullptr;
     double *ee0 = p->mb ? wsp<double>(d_ws, p->o_ee0) : nullptr;
@@ -723,7 +749,7 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     int *eprev = p->mb ? wsp<int>(d_ws, p->o_eprev) : nullptr;
     amx::DynLaunch dl{p->d_cd,    p->d_chunks, p->n_chunks, p->d_esegs, p->n_es,
                       p->d_eseg0, p->d_neseg,  p->nloc,     p->max_chunk_n, p->cd.look,
-                      p->warm,    p->d_tabs,   st};
+                      p->warm,    p->Le,       p->cd.env_rcp, p->d_tabs, st};
     switch (stage) {
     case AMX_STAGE_FRONT1:
         HIPCHK(amx::launch_front1(l, p->D, (p->cd.chin == 2 && !p->cd.in_s16) ? 2 : 1,
@@ -752,21 +778,20 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
         if (p->mb) HIPCHK(amx::launch_xover2(l, p16, sx, bands, p->nloc));
         break;
     case AMX_STAGE_RMS:
-        if (p->mb) HIPCHK(amx::launch_rms(dl, bands, r, mframe));
+        if (p->mb) HIPCHK(amx::launch_rms(dl, bands, mframe));
         break;
     case AMX_STAGE_ENV:
         if (p->mb)
-            HIPCHK(amx::launch_env(dl, r, mframe, bands, gained, esv, ee0, ee1, eact, eprev,
-                                   p->rounds));
+            HIPCHK(amx::launch_env(dl, mframe, ck, esv, ee0, ee1, eact, eprev, p->rounds));
         break;
     case AMX_STAGE_FIX:
         if (p->mb)
-            HIPCHK(amx::launch_envseq(dl, r, mframe, bands, gained, esv,
+            HIPCHK(amx::launch_envseq(dl, mframe, ck, esv,
                                       (p->rounds & 1) ? ee1 : ee0, eact, eprev));
         break;
     case AMX_STAGE_APPLY:
         if (p->mb)
-            HIPCHK(amx::launch_overlay(dl, gained, d_out, p->max_chunk_out, p->d_n1));
+            HIPCHK(amx::launch_gain_overlay(dl, mframe, ck, bands, d_out, p->max_chunk_out, p->d_n1));
         break;
     }
     return AMX_OK;

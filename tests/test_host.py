@@ -117,3 +117,44 @@ def test_dropin_errors_like_reference(tmp_path):
                       lambda a, b: prog.append((a, b)), art.append, tag.append)
     assert msgs[-1] == "Error: Input or output file not specified."
     assert prog == [(0, 1)] and art == [None] and tag == ["Processing failed."]
+
+
+def test_reciprocal_division_is_ieee_quotient(tmp_path):
+    """The compressor kernels form m / A, m / R and -att / 20 as q = x (1/b) plus one
+    FMA residual step (amx_dyn.hip env_div, gain_frame).  Markstein's theorem makes
+    that the IEEE quotient for a correctly rounded 1/b; checked here on random and
+    edge operands with the C library's fma (the plan additionally checks every
+    compressor table value, amx_plan.cpp env_rcp)."""
+    import ctypes
+    import subprocess
+    import numpy as np
+    src = tmp_path / "mk.c"
+    src.write_text(r'''
+#include <math.h>
+#include <stdint.h>
+int64_t check(const double *x, int64_t n, double b) {
+    const double y = 1.0 / b;
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n; i++) {
+        const double q = x[i] * y;
+        const double c = fma(fma(-q, b, x[i]), y, q);
+        if (c != x[i] / b) bad++;
+    }
+    return bad;
+}
+''')
+    so = tmp_path / "mk.so"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-shared", "-fPIC", str(src), "-o", str(so), "-lm"],
+                   check=True)
+    lib = ctypes.CDLL(str(so))
+    lib.check.restype = ctypes.c_int64
+    lib.check.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_double]
+    rng = np.random.default_rng(7)
+    x = np.concatenate([rng.uniform(0, 200, 1_000_000), rng.uniform(0, 1e-6, 100_000),
+                        np.abs(rng.standard_normal(100_000)) * 30, -rng.uniform(0, 200, 100_000),
+                        np.arange(0, 5000, 0.125)])
+    x = np.ascontiguousarray(x, np.float64)
+    for fs in (44100, 48000, 96000, 22050, 192000):
+        for b in (5.0 * (fs / 1000.0), 50.0 * (fs / 1000.0)):
+            assert lib.check(x.ctypes.data, x.size, b) == 0, (fs, b)
+    assert lib.check(x.ctypes.data, x.size, 20.0) == 0
