@@ -27,25 +27,31 @@
 
 namespace amx {
 
+// clang vector types (HIP's double2 / uint4 structs defeat register promotion of arrays)
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+
 #define AMX_TAB 32769
 
 // ----------------------------------------- compressor RMS detector (exact)
 // One workgroup = AMX_RMS_F frames of one (chunk, band); squares of the window
-// [base - look, base + AMX_RMS_F) are prefix-summed in LDS (exact int64), so
-// S_i = P(i) - P(max(i - look, 0)) with no sequential sliding window.
-#define AMX_RMS_F 1024
+// [base - AMX_RMS_LOOKPAD, base + AMX_RMS_F) are prefix-summed in LDS (exact
+// int64), so S_i = P(i) - P(i - look) with no sequential sliding window.  Frames
+// before the chunk count as 0 (audioop.rms over the shorter window divides by the
+// frames present).  Loads are 16-B vectors (the LDS origin is 16-frame aligned),
+// and each thread's 16 table gathers m_i = max_attenuation(r_i) are all in flight
+// at once -- consecutive frames have similar r, so they hit the same lines.
+#define AMX_RMS_F 4096
 #define AMX_RMS_MAXLOOK 1024
-// It also looks up m_i = max_attenuation(r_i) once per frame (consecutive frames
-// have similar r, so these gathers are cache friendly) for the envelope kernels,
-// which then stream (r, m) and derive inc = m/A, dec = m/R by IEEE division --
-// the same correctly rounded quotients the host tables hold.
+#define AMX_RMS_LOOKPAD 1024
 __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ cdp,
                                                    const ChunkDev *__restrict__ chunks,
                                                    const uint32_t *__restrict__ bands,
                                                    const double *__restrict__ tabs,
                                                    double *__restrict__ mm, int64_t nloc) {
-    constexpr int N = AMX_RMS_F + AMX_RMS_MAXLOOK;
-    constexpr int PER = N / AMX_BLOCK;                 // 8 values per thread
+    constexpr int N = AMX_RMS_F + AMX_RMS_LOOKPAD;
+    constexpr int PER = N / AMX_BLOCK;                 // 20 slots per thread
+    constexpr int VEC = PER / 4;                       // as 5 16-B loads
     __shared__ long long P[N];
     __shared__ long long wsum[AMX_BLOCK / 64];
     const int look = cdp->look;
@@ -56,18 +62,21 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
     const uint32_t *x = bands + b * nloc + ch.loc_off;
     double *mo = mm + b * nloc + ch.loc_off;
     const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
-    // LDS slot k holds frame base - look + k (frames before the chunk count as 0)
-    const int64_t f0 = base - look;
+    const int64_t rowlen = (ch.n + 15) / 16 * 16;     // the chunk row (16-frame aligned)
+    // LDS slot k holds frame base - LOOKPAD + k
+    const int64_t f0 = base - AMX_RMS_LOOKPAD;
     const int t = threadIdx.x;
     long long v[PER];
 #pragma unroll
-    for (int q = 0; q < PER; q++) {
-        const int k = t * PER + q;
-        const int64_t f = f0 + k;
-        const bool ok = f >= 0 && f < ch.n && k < AMX_RMS_F + look;
-        const uint32_t u = x[ok ? f : 0];
-        const long long a = lo16(u), d = hi16(u);
-        v[q] = ok ? a * a + d * d : 0;
+    for (int q = 0; q < VEC; q++) {
+        const int64_t f = f0 + t * PER + 4 * q;
+        const bool ok = f >= 0 && f < rowlen;
+        const u4v u = *reinterpret_cast<const u4v *>(x + (ok ? f : 0));
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const long long a0 = lo16(u[e]), a1 = hi16(u[e]);
+            v[4 * q + e] = (ok && f + e < ch.n) ? a0 * a0 + a1 * a1 : 0;
+        }
     }
     // block inclusive scan: per-thread serial, wave scan of totals, cross-wave
     long long run = 0;
@@ -88,16 +97,26 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
 #pragma unroll
     for (int q = 0; q < PER; q++) P[t * PER + q] = excl + v[q];
     __syncthreads();
-    // frame i = base + n uses slots [n, n + look) -> P[n + look - 1] - P[n - 1]
-    for (int n = t; n < AMX_RMS_F; n += AMX_BLOCK) {
-        const int64_t i = base + n;
-        if (i >= ch.n) break;
+    // frame i = base + nn uses slots [nn + LOOKPAD - look, nn + LOOKPAD)
+    constexpr int OUT = AMX_RMS_F / AMX_BLOCK;
+    uint32_t rc[OUT];
+#pragma unroll
+    for (int k = 0; k < OUT; k++) {
+        const int nn = t + k * AMX_BLOCK;
+        const int64_t i = base + nn;
         const int64_t wlo = i - look < 0 ? 0 : i - look;
         const int64_t cnt = 2 * (i - wlo);
-        const long long S = P[n + look - 1] - (n > 0 ? P[n - 1] : 0);
+        const long long S = P[nn + AMX_RMS_LOOKPAD - 1] - P[nn + AMX_RMS_LOOKPAD - 1 - look];
         const uint32_t rms = cnt ? (uint32_t)sqrt((double)S / (double)cnt) : 0u;
-        const uint32_t rc = rms > 32768u ? 32768u : rms;      // |sample| <= 32768
-        mo[i] = mt[rc];
+        rc[k] = rms > 32768u ? 32768u : rms;                  // |sample| <= 32768
+    }
+    double mv[OUT];
+#pragma unroll
+    for (int k = 0; k < OUT; k++) mv[k] = mt[rc[k]];
+#pragma unroll
+    for (int k = 0; k < OUT; k++) {
+        const int64_t i = base + t + k * AMX_BLOCK;
+        if (i < ch.n) mo[i] = mv[k];
     }
 }
 
@@ -232,8 +251,6 @@ __device__ double env_rerun_wave(const ChainDev &cd, const double *m, double *ck
 // tile-uniform, every vector is 16-B aligned and checkpoints fall on tile starts.
 #define AMX_ENV_TF 16
 #define AMX_ENV_MP 18      // m tile pitch in doubles (144 B)
-typedef double d2v __attribute__((ext_vector_type(2)));
-typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 template <bool RCP>
 __global__ void __launch_bounds__(64) k_env0(const ChainDev *__restrict__ cdp,
                                              const ChunkDev *__restrict__ chunks,
@@ -461,11 +478,18 @@ __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
 // The compressor output (audioop.mul of each frame by 10^(-att/20), :306-308) of
 // all three bands and low.overlay(mid).overlay(high) (:309) with pydub's
 // ms-rounded lengths (n1 after the first overlay, n2 = out_n after the second).
-// A thread owns 16 consecutive output frames of a chunk: per band it re-runs the
+// A thread owns 16 consecutive frames of a chunk: per band it re-runs the
 // recurrence from the checkpoint before its first frame (exact: the same operation
 // sequence from the same state) and applies the gain; the three gained samples are
-// summed with int16 saturation.  Loads and stores are 16-B vectors over
-// consecutive threads (coalesced); this is the parallel, throughput-bound half.
+// summed with int16 saturation, band by band.
+// Memory: a wave owns 1024 consecutive frames.  Per band its m (8 KB) and samples
+// (4 KB) are read by 16-B pieces over consecutive lanes (every load instruction
+// one contiguous KiB) into LDS rows of 16 frames, the next band's pieces already in
+// flight; the output goes back the same way.  (Thread-owned 16-frame runs read
+// directly touch 64 lines per instruction and left the loads TA-bound.)
+#define AMX_GO_MP 18       // m row pitch in doubles (144 B: 16-B aligned, b128 conflict-free)
+#define AMX_GO_XP 20       // sample / output row pitch in dwords (80 B)
+#define AMX_GO_WAVES (AMX_BLOCK / 64)
 template <bool RCP>
 __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__restrict__ cdp,
                                                             const ChunkDev *__restrict__ chunks,
@@ -475,66 +499,115 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
                                                             uint32_t *__restrict__ out,
                                                             int64_t nloc,
                                                             const int64_t *__restrict__ n1tab) {
+    __shared__ __attribute__((aligned(16))) double sm_all[AMX_GO_WAVES][64 * AMX_GO_MP];
+    __shared__ __attribute__((aligned(16))) uint32_t sx_all[AMX_GO_WAVES][64 * AMX_GO_XP];
     const ChainDev &cd = *cdp;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = blockIdx.y;
     const ChunkDev ch = chunks[c];
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t i0 = g * AMX_ENV_TF_;
-    const int64_t n2 = ch.out_n;
-    if (i0 >= n2) return;
+    const int64_t wbase = ((int64_t)blockIdx.x * AMX_GO_WAVES + wv) * (64 * AMX_ENV_TF_);
+    const int64_t n = ch.n, n2 = ch.out_n;
+    if (wbase >= n2) return;                            // wave-uniform; no block barriers below
     const int64_t n1 = n1tab[c];
-    const int64_t r0 = ch.loc_off + i0;                 // band 0 row of frame i0
-    double att[3];
+    double *smw = sm_all[wv];
+    uint32_t *sxw = sx_all[wv];
+    const int64_t i0 = wbase + lane * AMX_ENV_TF_;      // this thread's first frame
+    // the chunk row holds (n + 15) / 16 * 16 frames; pieces past it re-read its start
+    const int64_t rowlen = (n + AMX_ENV_TF_ - 1) / AMX_ENV_TF_ * AMX_ENV_TF_;
+    // loader pieces: m piece p = 64 i + lane (i < 8) = frames 2p, 2p+1 of the wave;
+    // sample piece p = 64 i + lane (i < 4) = frames 4p .. 4p+3
+    int64_t mo[8], xo[4];
 #pragma unroll
-    for (int b = 0; b < 3; b++) att[b] = i0 < ch.n ? ck[(b * nloc + r0) / AMX_ENV_TF_] : 0.0;
-    uint32_t *op = out + ch.out_off + i0;
-    const bool vec = i0 + AMX_ENV_TF_ <= n2 && ((ch.out_off + i0) & 3) == 0;
-    // two halves of 8 frames: 3 bands x (8 m + 8 samples) in flight per half
-#pragma unroll 1
-    for (int h = 0; h < AMX_ENV_TF_; h += 8) {
-        const int64_t i = i0 + h;
-        d2v M[3][4];
-        u4v X[3][2];
+    for (int i = 0; i < 8; i++) {
+        const int64_t f = wbase + 2 * (64 * i + lane);
+        mo[i] = ch.loc_off + (f < rowlen ? f : 0);
+    }
 #pragma unroll
-        for (int b = 0; b < 3; b++) {
-            const d2v *mp = reinterpret_cast<const d2v *>(mm + b * nloc + r0 + h);
-            const u4v *xp = reinterpret_cast<const u4v *>(bands + b * nloc + r0 + h);
+    for (int i = 0; i < 4; i++) {
+        const int64_t f = wbase + 4 * (64 * i + lane);
+        xo[i] = ch.loc_off + (f < rowlen ? f : 0);
+    }
+    d2v Mp[8];
+    u4v Xp[4];
 #pragma unroll
-            for (int k = 0; k < 4; k++) M[b][k] = mp[k];
+    for (int i = 0; i < 8; i++) Mp[i] = *reinterpret_cast<const d2v *>(mm + mo[i]);
 #pragma unroll
-            for (int k = 0; k < 2; k++) X[b][k] = xp[k];
+    for (int i = 0; i < 4; i++) Xp[i] = *reinterpret_cast<const u4v *>(bands + xo[i]);
+    uint32_t acc[AMX_ENV_TF_];
+#pragma unroll
+    for (int f = 0; f < AMX_ENV_TF_; f++) acc[f] = 0u;
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+        // stage this band's pieces: m piece p -> row p / 8, doubles 2 (p % 8);
+        // sample piece p -> row p / 4, dwords 4 (p % 4)
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int p = 64 * i + lane;
+            *reinterpret_cast<d2v *>(smw + (p >> 3) * AMX_GO_MP + 2 * (p & 7)) = Mp[i];
         }
-        uint32_t o[8];
 #pragma unroll
-        for (int f = 0; f < 8; f++) {
-            const bool in = i + f < ch.n;
-            int s[3][2];
-#pragma unroll
-            for (int b = 0; b < 3; b++) {
-                double mv = (f & 1) ? M[b][f >> 1].y : M[b][f >> 1].x;
-                mv = in ? mv : 0.0;
-                att[b] = env_step<RCP>(cd, att[b], mv);
-                const uint32_t gv = gain_frame(cd, X[b][f >> 2][f & 3], att[b]);
-                s[b][0] = lo16(gv);
-                s[b][1] = hi16(gv);
-            }
-            const bool in1 = i + f < n1;
-            int16_t q[2];
-#pragma unroll
-            for (int k = 0; k < 2; k++) {
-                const int s1 = in1 ? (int)sat16(s[0][k] + s[1][k]) : 0;
-                q[k] = sat16(s1 + s[2][k]);
-            }
-            o[f] = in ? pack2(q[0], q[1]) : 0u;
+        for (int i = 0; i < 4; i++) {
+            const int p = 64 * i + lane;
+            *reinterpret_cast<u4v *>(sxw + (p >> 2) * AMX_GO_XP + 4 * (p & 3)) = Xp[i];
         }
-        if (vec) {
-            u4v *vp = reinterpret_cast<u4v *>(op + h);
-            vp[0] = u4v{o[0], o[1], o[2], o[3]};
-            vp[1] = u4v{o[4], o[5], o[6], o[7]};
+        __builtin_amdgcn_wave_barrier();
+        if (b < 2) {                                    // next band in flight
+            const int64_t bo = (int64_t)(b + 1) * nloc;
+#pragma unroll
+            for (int i = 0; i < 8; i++) Mp[i] = *reinterpret_cast<const d2v *>(mm + bo + mo[i]);
+#pragma unroll
+            for (int i = 0; i < 4; i++) Xp[i] = *reinterpret_cast<const u4v *>(bands + bo + xo[i]);
+        }
+        double mv[AMX_ENV_TF_];
+        uint32_t xv[AMX_ENV_TF_];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const d2v v = *reinterpret_cast<const d2v *>(smw + lane * AMX_GO_MP + 2 * k);
+            mv[2 * k] = v.x;
+            mv[2 * k + 1] = v.y;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const u4v v = *reinterpret_cast<const u4v *>(sxw + lane * AMX_GO_XP + 4 * k);
+            xv[4 * k] = v.x; xv[4 * k + 1] = v.y; xv[4 * k + 2] = v.z; xv[4 * k + 3] = v.w;
+        }
+        __builtin_amdgcn_wave_barrier();
+        double att = i0 < n ? ck[(b * nloc + ch.loc_off + i0) / AMX_ENV_TF_] : 0.0;
+#pragma unroll
+        for (int f = 0; f < AMX_ENV_TF_; f++) {
+            const int64_t i = i0 + f;
+            att = env_step<RCP>(cd, att, i < n ? mv[f] : 0.0);
+            const uint32_t gv = gain_frame(cd, xv[f], att);
+            const int g0 = lo16(gv), g1 = hi16(gv);
+            if (b == 0) {
+                acc[f] = gv;
+            } else if (b == 1) {
+                const bool in1 = i < n1;                // first overlay's length
+                acc[f] = in1 ? pack2(sat16(lo16(acc[f]) + g0), sat16(hi16(acc[f]) + g1)) : 0u;
+            } else {
+                acc[f] = i < n ? pack2(sat16(lo16(acc[f]) + g0), sat16(hi16(acc[f]) + g1)) : 0u;
+            }
+        }
+    }
+    // output through LDS: row lane = frames i0 .. i0+15, stored as 16-B pieces
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        *reinterpret_cast<u4v *>(sxw + lane * AMX_GO_XP + 4 * k) =
+            u4v{acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]};
+    __builtin_amdgcn_wave_barrier();
+    uint32_t *ob = out + ch.out_off + wbase;
+    const bool al = ((ch.out_off + wbase) & 3) == 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int p = 64 * i + lane;
+        const u4v v = *reinterpret_cast<const u4v *>(sxw + (p >> 2) * AMX_GO_XP + 4 * (p & 3));
+        const int64_t f = wbase + 4 * p;
+        if (al && f + 4 <= n2) {
+            *reinterpret_cast<u4v *>(ob + 4 * p) = v;
         } else {
 #pragma unroll
-            for (int f = 0; f < 8; f++)
-                if (i + f < n2) op[h + f] = o[f];
+            for (int q = 0; q < 4; q++)
+                if (f + q < n2) ob[4 * p + q] = v[q];
         }
     }
 }

@@ -664,7 +664,8 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         p->o_gain = (size_t)align_up(off, (3 * nl / 16 + 64) * 8);   // envelope checkpoints
         // m rows are read whole-tile by k_env0, from W frames before a chunk to the
         // 16-frame tile past its end: pad the buffer on both sides
-        const size_t mpad = (size_t)p->warm + 64;
+        // (and k_gain_overlay reads whole 1024-frame wave tiles)
+        const size_t mpad = (size_t)(p->warm > 1024 ? p->warm : 1024) + 64;
         p->o_m = (size_t)align_up(off, (3 * nl + 2 * mpad) * 8) + mpad * 8;
         p->o_esv = (size_t)align_up(off, 3 * ne * 8);
         p->o_ee0 = (size_t)align_up(off, 3 * ne * 8);
