@@ -140,11 +140,14 @@ __device__ __forceinline__ double env_div(double m, double a, double ra) {
     }
 }
 
-// pydub envelope step, exact, branch-free (both candidates, then select)
+// pydub envelope step, exact, branch-free (both candidates, then select).  The
+// reference's condition is (over and att <= m); over can be dropped: when m == 0
+// (not over) and att == 0 the attack branch gives min(0 + 0, 0) = 0 = att, and
+// att > 0 takes the release branch anyway.
 __device__ __forceinline__ double env_step3(double att, double m, double inc, double dec) {
     const double up = fmin(att + inc, m);          // attenuation += inc; min(., max_att)
     const double dn = fmax(att - dec, 0.0);        // attenuation -= dec; max(., 0)
-    return (m != 0.0 && att <= m) ? up : dn;
+    return att <= m ? up : dn;
 }
 
 template <bool RCP>
@@ -193,39 +196,55 @@ __device__ __forceinline__ uint32_t gain_frame(const ChainDev &cd, uint32_t v, d
 
 #define AMX_ENV_TF_ 16   // checkpoint spacing (frames)
 
+// lane i's value of a double, as a wave-uniform (scalar) operand
+__device__ __forceinline__ double lane_val(double v, int i) {
+    const long long x = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)x, i);
+    const int hi = __builtin_amdgcn_readlane((int)(x >> 32), i);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // Wave-cooperative re-run of one segment's frames [f0, f1) (chunk-local; f0 a
-// multiple of 16) from the new start ns, with the stored trajectory from os re-run
-// in lockstep: every lane of the wave calls it with the same arguments.  Per
-// 64-frame window each lane loads and divides one frame (coalesced), the two
-// recurrences run on broadcast values (uniform across lanes), each lane keeps the
-// new state before its own frame, and the lanes on 16-frame boundaries rewrite
-// their checkpoint -- only up to the frame where the two trajectories coincide
-// (identical from there on, the old checkpoints stand).  Returns the segment's
-// end state (the old end if they coincided).
+// multiple of 16) from the new start ns: every lane of the wave calls it with the
+// same arguments.  Per 64-frame window each lane loads and divides one frame
+// (coalesced; the next window's loads are in flight meanwhile) and the recurrence
+// runs on the lanes' values read out as scalar operands (v_readlane, no LDS round
+// trip); lanes 0, 16, 32, 48 keep the new state before their frame and rewrite that
+// checkpoint.  The stored checkpoints are the trajectory from the old start, so
+// at every 16-frame boundary the new state is compared with the stored one: once
+// they are equal the two trajectories are identical from there on, the remaining
+// checkpoints stand and the old end is the end.  Returns the segment's end state.
 template <bool RCP>
 __device__ double env_rerun_wave(const ChainDev &cd, const double *m, double *ckr, int64_t f0,
-                                 int64_t f1, double os, double ns, double old_end) {
+                                 int64_t f1, double ns, double old_end) {
     const int lane = threadIdx.x & 63;
-    double a = os, c = ns;
+    const bool ckl = (lane & (AMX_ENV_TF_ - 1)) == 0;
+    double c = ns;
+    double ml = f0 + lane < f1 ? m[f0 + lane] : 0.0;
+    double ol = ckl && f0 + lane < f1 ? ckr[(f0 + lane) / AMX_ENV_TF_] : 0.0;
     for (int64_t base = f0; base < f1; base += 64) {
-        const int64_t fl = base + lane;
-        const bool ok = fl < f1;
-        const double ml = ok ? m[fl] : 0.0;
+        const int64_t fn = base + 64 + lane;
+        const double mn = fn < f1 ? m[fn] : 0.0;
+        const double on = ckl && fn < f1 ? ckr[fn / AMX_ENV_TF_] : 0.0;
         const double il = env_div<RCP>(ml, cd.env_A, cd.env_rA);
         const double dl = env_div<RCP>(ml, cd.env_R, cd.env_rR);
-        const int n = (int)(f1 - base < 64 ? f1 - base : 64);
         double mine = c;
-        int stop = n;
-        for (int q = 0; q < n; q++) {
-            mine = lane == q ? c : mine;                 // state before frame base + q
-            const double mq = __shfl(ml, q), iq = __shfl(il, q), dq = __shfl(dl, q);
-            a = env_step3(a, mq, iq, dq);
-            c = env_step3(c, mq, iq, dq);
-            if (a == c) { stop = q; break; }
+        int stop = 4;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const bool same = base + 16 * t < f1 && c == lane_val(ol, 16 * t);
+            if (__builtin_amdgcn_readfirstlane((int)same)) { stop = t; break; }
+            mine = lane == 16 * t ? c : mine;            // state before frame base + 16 t
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const int i = 16 * t + q;
+                c = env_step3(c, lane_val(ml, i), lane_val(il, i), lane_val(dl, i));
+            }
         }
-        if (lane <= stop && lane < n && (lane & (AMX_ENV_TF_ - 1)) == 0)
-            ckr[fl / AMX_ENV_TF_] = mine;
-        if (stop < n) return old_end;
+        if (ckl && (lane >> 4) < stop && base + lane < f1) ckr[(base + lane) / AMX_ENV_TF_] = mine;
+        if (stop < 4) return old_end;
+        ml = mn;
+        ol = on;
     }
     return c;
 }
@@ -259,10 +278,11 @@ __global__ void __launch_bounds__(64) k_env0(const ChainDev *__restrict__ cdp,
                                              double *__restrict__ ck,
                                              double *__restrict__ sv, double *__restrict__ ev,
                                              int *__restrict__ act, int64_t nloc, int warm,
-                                             int Le) {
+                                             int Le, int *__restrict__ flags) {
     __shared__ __attribute__((aligned(16))) double sm[64 * AMX_ENV_MP];
     const ChainDev &cd = *cdp;
     const int lane = threadIdx.x;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && lane < AMX_ENV_MAX_ROUNDS) flags[lane] = 0;
     const int j = blockIdx.x * 64 + lane;
     const int b = blockIdx.y;
     const bool valid = j < n_es;
@@ -327,105 +347,120 @@ __global__ void __launch_bounds__(64) k_env0(const ChainDev *__restrict__ cdp,
     }
 }
 
-// prev[j] = the nearest earlier active segment of the same chunk (or -1): the
-// segment whose end state is segment j's true start.  One wave per (chunk, band).
-__global__ void __launch_bounds__(64) k_env_prev(const ChunkDev *__restrict__ chunks,
-                                                 const int *__restrict__ eseg0,
-                                                 const int *__restrict__ neseg, int n_es,
-                                                 const int *__restrict__ act,
-                                                 int *__restrict__ prev) {
-    const int c = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
-    const int s0 = eseg0[c], s1 = s0 + neseg[c];
-    const int *A = act + (int64_t)b * n_es;
-    int *P = prev + (int64_t)b * n_es;
-    int carry = -1;                                    // last active index before the batch
-    for (int base = s0; base < s1; base += 64) {
-        const int j = base + lane;
-        const bool a = j < s1 && A[j] != 0;
-        // inclusive max-scan of (a ? j : -1); prev[j] = exclusive value
-        int v = a ? j : -1;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int up = __shfl_up(v, o);
-            if (lane >= o) v = max(v, up);
-        }
-        int excl = __shfl_up(v, 1);
-        if (lane == 0) excl = -1;
-        excl = max(excl, carry);
-        if (j < s1) P[j] = excl;
-        carry = max(carry, __shfl(v, 63));
-    }
-}
-
-// the wave fixes segment sg of band b from the new start ns (all lanes, uniform args)
+// the wave fixes segment [pos, pos + len) of a chunk row from the new start ns (all
+// lanes, uniform arguments); returns the segment's end state
 template <bool RCP>
-__device__ __forceinline__ double env_fix_segment(const ChainDev &cd, const SegDev &sg,
-                                                  const ChunkDev &ch, int b, int64_t nloc,
-                                                  const double *mm, double *ck, bool active,
-                                                  double os, double ns, double old_end) {
-    double *ckr = ck + (b * nloc + ch.loc_off) / AMX_ENV_TF_;
+__device__ __forceinline__ double env_fix_segment(const ChainDev &cd, const double *mrow,
+                                                  double *ckr, int64_t pos, int len, bool active,
+                                                  double ns, double old_end) {
     if (!active) {
         // identity transfer: the held state is every checkpoint of the segment
-        const int64_t k0 = sg.pos / AMX_ENV_TF_, k1 = (sg.pos + sg.len + AMX_ENV_TF_ - 1) / AMX_ENV_TF_;
+        const int64_t k0 = pos / AMX_ENV_TF_, k1 = (pos + len + AMX_ENV_TF_ - 1) / AMX_ENV_TF_;
         for (int64_t k = k0 + (threadIdx.x & 63); k < k1; k += 64) ckr[k] = ns;
         return ns;
     }
-    return env_rerun_wave<RCP>(cd, mm + b * nloc + ch.loc_off, ckr, sg.pos, sg.pos + sg.len, os, ns,
-                               old_end);
+    return env_rerun_wave<RCP>(cd, mrow, ckr, pos, pos + len, ns, old_end);
 }
 
 // ------------------------------------------------ rounds: parallel fix-up
-// A wave per 64 segments: lanes whose start disagrees with the end of their
-// predecessor (previous round's ends e_in) are fixed one after another by the
-// whole wave; e_out gets every segment's end, s is updated in place.
+// A wave per 64 consecutive segments of one band, updating s and e in place.
+// Segment j's true start is the end of prev[j], the nearest earlier segment of its
+// chunk with an over-threshold frame (below-threshold frames hold the state), or 0.
+// Round 0 derives prev[j] (ballot of the act flags within the wave, a wave-uniform
+// look-back over earlier waves for the lanes of the wave's first chunk that have
+// none) and stores it for the later rounds and k_envseq.  Lanes whose start differs
+// from their stored start s_j are fixed in index order by the whole wave; a fixed
+// segment's new end is handed at once to the lanes of the same wave that start from
+// it, so a run of dependent segments within one wave settles in one round.  flags[r]
+// records that round r fixed anything: a round (and k_envseq) after a round that
+// fixed nothing has nothing to do and returns at once.  Waves of one round may read
+// a predecessor's end before or after another wave rewrites it; either is an end
+// of its segment from some start, and k_envseq checks every link at the end.
 template <bool RCP>
 __global__ void __launch_bounds__(64) k_envfix(const ChainDev *__restrict__ cdp,
                                                const ChunkDev *__restrict__ chunks,
                                                const SegDev *__restrict__ es, int n_es,
                                                const double *__restrict__ mm,
-                                               double *__restrict__ ck,
-                                               double *__restrict__ sv,
-                                               const double *__restrict__ e_in,
-                                               double *__restrict__ e_out,
+                                               double *__restrict__ ck, double *sv, double *ev,
                                                const int *__restrict__ act,
-                                               const int *__restrict__ prev, int64_t nloc) {
+                                               int *__restrict__ prev, int64_t nloc,
+                                               int *flags, int round, int fix) {
+    if (round > 0 && __builtin_amdgcn_readfirstlane(flags[round - 1]) == 0) return;
     const ChainDev &cd = *cdp;
     const int lane = threadIdx.x;
-    const int j = blockIdx.x * 64 + lane;
+    const int w0 = blockIdx.x * 64;
+    const int j = w0 + lane;
     const int b = blockIdx.y;
     const bool valid = j < n_es;
-    const int64_t k = (int64_t)b * n_es + (valid ? j : 0);
+    const int64_t bo = (int64_t)b * n_es;
+    const int jc = valid ? j : n_es - 1;
+    const SegDev sg = es[jc];
+    const bool a = valid && act[bo + jc] != 0;
+    int p;
+    if (round == 0) {
+        const unsigned long long am = __ballot(a);
+        const unsigned long long below = lane ? am & (~0ull >> (64 - lane)) : 0ull;
+        p = below ? w0 + 63 - __clzll((long long)below) : -1;
+        if (p < sg.first) p = -1;
+        const bool lb = valid && p < 0 && sg.first < w0;
+        if (__ballot(lb)) {
+            // the wave's first chunk: last active segment before w0 (uniform)
+            const int first0 = __shfl(sg.first, 0);
+            int last = -1;
+            for (int base = w0 - 64; base + 63 >= first0; base -= 64) {
+                const int jj = base + lane;
+                const unsigned long long mk = __ballot(jj >= first0 && act[bo + jj] != 0);
+                if (mk) { last = base + 63 - __clzll((long long)mk); break; }
+            }
+            if (lb) p = last;
+        }
+        if (!valid) p = -1;
+        if (valid) prev[bo + j] = p;
+    } else {
+        p = valid ? prev[bo + j] : -1;
+    }
+    if (!fix) return;
     double ns = 0.0, os = 0.0, en = 0.0;
     bool need = false;
     if (valid) {
-        const int p = prev[k];
-        ns = p >= 0 ? e_in[(int64_t)b * n_es + p] : 0.0;
-        os = sv[k];
-        en = e_in[k];
+        ns = p >= 0 ? ev[bo + p] : 0.0;
+        os = sv[bo + j];
+        en = ev[bo + j];
         need = !(ns == os);
     }
     unsigned long long work = __ballot(need);
+    if (!work) return;
+    if (lane == 0) flags[round] = 1;
+    const int64_t loc = chunks[sg.chunk].loc_off;
+    bool fixed = false;
     while (work) {
         const int w = __ffsll((long long)work) - 1;
-        work &= work - 1;
-        const int jw = blockIdx.x * 64 + w;
-        const SegDev sg = es[jw];
-        const ChunkDev ch = chunks[sg.chunk];
-        const double nsw = __shfl(ns, w), osw = __shfl(os, w), enw = __shfl(en, w);
-        const bool aw = act[(int64_t)b * n_es + jw] != 0;
-        const double r = env_fix_segment<RCP>(cd, sg, ch, b, nloc, mm, ck, aw, osw, nsw, enw);
-        if (lane == w) en = r;
+        const int64_t posw = __shfl(sg.pos, w), locw = __shfl(loc, w);
+        const int lenw = __shfl(sg.len, w);
+        const bool aw = __shfl((int)a, w) != 0;
+        const double nsw = __shfl(ns, w), enw = __shfl(en, w);
+        const int64_t ro = b * nloc + locw;
+        const double r = env_fix_segment<RCP>(cd, mm + ro, ck + ro / AMX_ENV_TF_, posw, lenw, aw,
+                                              nsw, enw);
+        if (lane == w) { en = r; fixed = true; }
+        // lanes starting from segment w0 + w take its new end now
+        if (lane > w && valid && p == w0 + w) {
+            ns = r;
+            need = !(ns == os);
+        }
+        work = __ballot(need) & (w == 63 ? 0ull : ~0ull << (w + 1));
     }
-    if (valid) {
-        e_out[k] = en;
-        if (need) sv[k] = ns;
+    if (fixed) {
+        ev[bo + j] = en;
+        sv[bo + j] = ns;
     }
 }
 
 // --------------------------------------- final in-order walk (exactness net)
 // One wave per (chunk, band): find the first segment whose start disagrees with
 // its predecessor's end (64 at a time) and fix it with the whole wave, continue
-// after it.
+// after it.  Nothing to do when the last round fixed nothing (flags[fl] == 0; fl < 0:
+// no rounds ran, always walk).
 template <bool RCP>
 __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
                                                const ChunkDev *__restrict__ chunks,
@@ -436,13 +471,16 @@ __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
                                                double *__restrict__ ck,
                                                double *__restrict__ sv, double *__restrict__ ev,
                                                const int *__restrict__ act,
-                                               const int *__restrict__ prev, int64_t nloc) {
+                                               const int *__restrict__ prev, int64_t nloc,
+                                               const int *__restrict__ flags, int fl) {
+    if (fl >= 0 && __builtin_amdgcn_readfirstlane(flags[fl]) == 0) return;
     const ChainDev &cd = *cdp;
     const int c = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
     const int s0 = eseg0[c], s1 = s0 + neseg[c];
     const ChunkDev ch = chunks[c];
     double *S = sv + (int64_t)b * n_es, *E = ev + (int64_t)b * n_es;
     const int *A = act + (int64_t)b * n_es, *Pv = prev + (int64_t)b * n_es;
+    const int64_t ro = b * nloc + ch.loc_off;
     int cur = s0;
     while (cur < s1) {
         int found = s1;
@@ -461,8 +499,8 @@ __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
         const SegDev sg = es[found];
         const int p = Pv[found];
         const double ns = p >= 0 ? E[p] : 0.0;
-        const double r = env_fix_segment<RCP>(cd, sg, ch, b, nloc, mm, ck, A[found] != 0, S[found],
-                                              ns, E[found]);
+        const double r = env_fix_segment<RCP>(cd, mm + ro, ck + ro / AMX_ENV_TF_, sg.pos, sg.len,
+                                              A[found] != 0, ns, E[found]);
         __syncthreads();                    // every lane has read E/S of `found`
         if (lane == 0) {
             E[found] = r;
@@ -623,43 +661,37 @@ hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, double *m) {
 }
 
 template <bool RCP>
-static void env_launch_t(const DynLaunch &d, const double *m, double *ck, double *sv, double *e0,
-                         double *e1, int *act, int *prev, int rounds) {
+static void env_launch_t(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
+                         int *act, int *prev, int *flags, int rounds) {
     const dim3 gw((unsigned)((d.n_es + 63) / 64), 3);
     hipLaunchKernelGGL(k_env0<RCP>, gw, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es, m, ck, sv,
-                       e0, act, d.nloc, d.warm, d.Le);
-    hipLaunchKernelGGL(k_env_prev, dim3((unsigned)d.n_chunks, 3), dim3(64), 0, d.st, d.chunks,
-                       d.eseg0, d.neseg, d.n_es, act, prev);
-    double *ein = e0, *eout = e1;
-    for (int k = 0; k < rounds; k++) {
+                       ev, act, d.nloc, d.warm, d.Le, flags);
+    // rounds == 0: only prev[] (everything is left to k_envseq)
+    for (int k = 0; k < (rounds > 0 ? rounds : 1); k++)
         hipLaunchKernelGGL(k_envfix<RCP>, gw, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es, m,
-                           ck, sv, ein, eout, act, prev, d.nloc);
-        double *tmp = ein;
-        ein = eout;
-        eout = tmp;
-    }
+                           ck, sv, ev, act, prev, d.nloc, flags, k, rounds > 0 ? 1 : 0);
 }
 
-hipError_t launch_env(const DynLaunch &d, const double *m, double *ck, double *sv, double *e0,
-                      double *e1, int *act, int *prev, int rounds) {
+hipError_t launch_env(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
+                      int *act, int *prev, int *flags, int rounds) {
     if (d.n_es <= 0) return hipSuccess;
     if (d.warm % AMX_ENV_TF || d.Le % AMX_ENV_TF) return hipErrorInvalidValue;
-    if (d.rcp) env_launch_t<true>(d, m, ck, sv, e0, e1, act, prev, rounds);
-    else env_launch_t<false>(d, m, ck, sv, e0, e1, act, prev, rounds);
+    if (rounds < 0 || rounds > AMX_ENV_MAX_ROUNDS) return hipErrorInvalidValue;
+    if (d.rcp) env_launch_t<true>(d, m, ck, sv, ev, act, prev, flags, rounds);
+    else env_launch_t<false>(d, m, ck, sv, ev, act, prev, flags, rounds);
     return hipGetLastError();
 }
 
-// ends: the array the last round wrote (e0 if rounds is even, else e1)
-hipError_t launch_envseq(const DynLaunch &d, const double *m, double *ck, double *sv, double *ends,
-                         const int *act, const int *prev) {
+hipError_t launch_envseq(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
+                         const int *act, const int *prev, const int *flags, int rounds) {
     if (d.n_es <= 0) return hipSuccess;
     const dim3 gr((unsigned)d.n_chunks, 3);
     if (d.rcp)
         hipLaunchKernelGGL(k_envseq<true>, gr, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es,
-                           d.eseg0, d.neseg, m, ck, sv, ends, act, prev, d.nloc);
+                           d.eseg0, d.neseg, m, ck, sv, ev, act, prev, d.nloc, flags, rounds - 1);
     else
         hipLaunchKernelGGL(k_envseq<false>, gr, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es,
-                           d.eseg0, d.neseg, m, ck, sv, ends, act, prev, d.nloc);
+                           d.eseg0, d.neseg, m, ck, sv, ev, act, prev, d.nloc, flags, rounds - 1);
     return hipGetLastError();
 }
 

@@ -13,6 +13,7 @@
 #define AMX_SCAN_S 16     // segments per scan block
 #define AMX_CTL_FAST 1    // k_decide control word: limiter provably idle
 #define AMX_STATS 16      // doubles per track written by k_decide
+#define AMX_ENV_MAX_ROUNDS 16  // k_envfix rounds (one flag word each)
 #define AMX_EQC 64        // compact EQ coefficient block (see ChainDev::eqc)
 
 // One EQ stage of _apply_eq_to_channel (audio_mastering_engine.py:277-282).
@@ -137,10 +138,10 @@ struct DynLaunch {
     hipStream_t st;
 };
 hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, double *m);
-hipError_t launch_env(const DynLaunch &d, const double *m, double *ck, double *sv, double *e0,
-                      double *e1, int *act, int *prev, int rounds);
-hipError_t launch_envseq(const DynLaunch &d, const double *m, double *ck, double *sv, double *ends,
-                         const int *act, const int *prev);
+hipError_t launch_env(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
+                      int *act, int *prev, int *flags, int rounds);
+hipError_t launch_envseq(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
+                         const int *act, const int *prev, const int *flags, int rounds);
 hipError_t launch_gain_overlay(const DynLaunch &d, const double *m, const double *ck,
                                const int16_t *bands, int16_t *out, int64_t max_chunk_out,
                                const int64_t *n1tab);

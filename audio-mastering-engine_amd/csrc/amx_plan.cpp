@@ -162,7 +162,7 @@ struct amx_plan {
     int mask = 0, D = 0;
     int lev_eq = 0, lev_x = 0, lev_kw = 0;
     int mb = 0;
-    int Le = 1024, warm = 2048, rounds = 4;   // compressor envelope segments (amx_dyn.hip)
+    int Le = 1024, warm = 2048, rounds = 2;   // compressor envelope segments (amx_dyn.hip)
     int n_es = 0;
     std::vector<SegDev> esegs;
     std::vector<int> eseg0, neseg;
@@ -200,7 +200,7 @@ struct amx_plan {
     float *d_lut = nullptr;
     // workspace offsets
     size_t ws_bytes = 0;
-    size_t o_a16, o_e, o_s, o_p16, o_ex, o_sx, o_bands, o_r, o_m, o_gain, o_esv, o_ee0, o_ee1, o_eact,
+    size_t o_a16, o_e, o_s, o_p16, o_ex, o_sx, o_bands, o_r, o_m, o_gain, o_esv, o_ee0, o_eflags, o_eact,
         o_eprev;
     size_t o_ekw, o_skw, o_parts, o_phop;
     size_t o_eb, o_ebx, o_ebk, o_pk;
@@ -269,6 +269,10 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     const int fs = desc->sample_rate;
     if (desc->env_warm_frames >= 0) p->warm = (desc->env_warm_frames + 15) / 16 * 16;
     if (desc->env_rounds >= 0) p->rounds = desc->env_rounds;
+    if (p->rounds > AMX_ENV_MAX_ROUNDS) {
+        delete p;
+        return fail(AMX_EINVAL, "env_rounds %d > %d", desc->env_rounds, AMX_ENV_MAX_ROUNDS);
+    }
     p->L = seg_frames > 0 ? seg_frames : 256;
     p->L = (p->L + AMX_TF_FRAMES - 1) / AMX_TF_FRAMES * AMX_TF_FRAMES;   // whole LDS tiles
     p->hop = (fs + 5) / 10;                    // libebur128 samples_in_100ms
@@ -669,7 +673,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         p->o_m = (size_t)align_up(off, (3 * nl + 2 * mpad) * 8) + mpad * 8;
         p->o_esv = (size_t)align_up(off, 3 * ne * 8);
         p->o_ee0 = (size_t)align_up(off, 3 * ne * 8);
-        p->o_ee1 = (size_t)align_up(off, 3 * ne * 8);
+        p->o_eflags = (size_t)align_up(off, AMX_ENV_MAX_ROUNDS * 4);
         p->o_eact = (size_t)align_up(off, 3 * ne * 4);
         p->o_eprev = (size_t)align_up(off, 3 * ne * 4);
     }
@@ -745,7 +749,7 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     double *mframe = p->mb ? wsp<double>(d_ws, p->o_m) : nullptr;
     double *esv = p->mb ? wsp<double>(d_ws, p->o_esv) : nullptr;
     double *ee0 = p->mb ? wsp<double>(d_ws, p->o_ee0) : nullptr;
-    double *ee1 = p->mb ? wsp<double>(d_ws, p->o_ee1) : nullptr;
+    int *eflags = p->mb ? wsp<int>(d_ws, p->o_eflags) : nullptr;
     int *eact = p->mb ? wsp<int>(d_ws, p->o_eact) : nullptr;
     int *eprev = p->mb ? wsp<int>(d_ws, p->o_eprev) : nullptr;
     amx::DynLaunch dl{p->d_cd,    p->d_chunks, p->n_chunks, p->d_esegs, p->n_es,
@@ -783,12 +787,11 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
         break;
     case AMX_STAGE_ENV:
         if (p->mb)
-            HIPCHK(amx::launch_env(dl, mframe, ck, esv, ee0, ee1, eact, eprev, p->rounds));
+            HIPCHK(amx::launch_env(dl, mframe, ck, esv, ee0, eact, eprev, eflags, p->rounds));
         break;
     case AMX_STAGE_FIX:
         if (p->mb)
-            HIPCHK(amx::launch_envseq(dl, mframe, ck, esv,
-                                      (p->rounds & 1) ? ee1 : ee0, eact, eprev));
+            HIPCHK(amx::launch_envseq(dl, mframe, ck, esv, ee0, eact, eprev, eflags, p->rounds));
         break;
     case AMX_STAGE_APPLY:
         if (p->mb)

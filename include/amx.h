@@ -92,7 +92,7 @@ typedef struct amx_chain_desc {
     /* compressor envelope parallelisation (amx_dyn.hip); results are exact for any
      * values, these only move work between the speculative and the fix-up passes */
     int32_t env_warm_frames;      /* speculative warm-up per envelope segment; <0 -> 1024 */
-    int32_t env_rounds;           /* parallel fix-up rounds before the in-order walk; <0 -> 4 */
+    int32_t env_rounds;           /* parallel fix-up rounds before the in-order walk (0..16); <0 -> 2 */
 } amx_chain_desc;
 
 /* One ~30 s chunk of one track (the ffmpeg segment split, :178). */
