@@ -64,6 +64,69 @@ def carry_from_tails(tails, span_frames, rank, propagate):
     return c
 
 
+# ------------------------------------------------------------------ collectives
+# Device-agnostic (CUDA tensors over RCCL on the GPU path, CPU tensors over gloo in
+# tests/test_dist.py), so the exchange steps are tested exactly as they run.
+
+def _staged(group, *ts):
+    """gloo with device tensors (multi-rank rehearsal on one GPU): host copies."""
+    if dist.get_backend(group) == "gloo" and any(t.is_cuda for t in ts):
+        return [t.cpu() for t in ts], True
+    return list(ts), False
+
+
+def gather_tails(tail, tails_all, group=None):
+    """Step 1: every rank's zero-start K-filter end state [2, 4] -> tails_all[world, 2, 4]
+    (rank order)."""
+    (a, b), st = _staged(group, tails_all, tail.reshape(1, 2, 4).contiguous())
+    dist.all_gather_into_tensor(a, b, group=group)
+    if st:
+        tails_all.copy_(a)
+    return tails_all
+
+
+def reduce_loudness(hops, peak, group=None):
+    """Step 2: whole-track hop energies summed over ranks (each hop has at most two
+    non-zero addends), sample peaks max-reduced.  hops None: loudnorm off."""
+    for t, op in ((hops, dist.ReduceOp.SUM), (peak, dist.ReduceOp.MAX)):
+        if t is None:
+            continue
+        (h,), st = _staged(group, t)
+        dist.all_reduce(h, op=op, group=group)
+        if st:
+            t.copy_(h)
+
+
+def gather_halo(out, n, h, rank, world, group=None):
+    """Step 3: every rank's last h frames of its span out[:n] (zero-padded in front when
+    the span is shorter) are all-gathered; returns the previous rank's (None on rank 0)."""
+    mine = out[max(0, n - h):n]
+    if mine.shape[0] < h:
+        mine = torch.cat([torch.zeros((h - mine.shape[0], 2), dtype=mine.dtype, device=mine.device), mine])
+    # one int32 word per stereo int16 frame: neither RCCL nor gloo reduces/gathers int16
+    (mine,), st = _staged(group, mine.contiguous().view(torch.int32))
+    allh = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allh, mine, group=group)
+    if rank == 0:
+        return None
+    prev = allh[rank - 1].view(torch.int16)
+    return prev.to(out.device) if st else prev
+
+
+def chain_state(state, run, rank, world, group=None):
+    """Sequential limiter path: receive the state from rank - 1, run(), pass it on."""
+    (s,), st = _staged(group, state)
+    if rank > 0:
+        dist.recv(s, src=rank - 1, group=group)
+        if st:
+            state.copy_(s)
+    run()
+    if rank < world - 1:
+        if st:
+            s.copy_(state)
+        dist.send(s, dst=rank + 1, group=group)
+
+
 class ShardedTrack:
     """This rank's part of one chunk-sharded track."""
 
@@ -98,35 +161,21 @@ class ShardedTrack:
     # -------------------------------------------------------------- exchanges
     def exchange_carry(self):
         job = self.job
-        dist.all_gather_into_tensor(self.tails_all, job.kw_tail.reshape(1, 2, 4).contiguous(),
-                                    group=self.group)
+        gather_tails(job.kw_tail, self.tails_all, self.group)
         from . import capi
         capi.check(capi.load().amx_kw_carry(job.plan.h, capi.ptr(self.tails_all), capi.ptr(job.kw_carry),
                                             job._s(None)), "amx_kw_carry")
 
-    def reduce_loudness(self):
-        dist.all_reduce(self.job.hops, op=dist.ReduceOp.SUM, group=self.group)
-        dist.all_reduce(self.job.peak, op=dist.ReduceOp.MAX, group=self.group)
-
     def exchange_halo(self):
         job = self.job
         h = job.halo_frames
-        n = self.span_frames[self.rank]
-        mine = job.out[max(0, n - h):n]
-        if mine.shape[0] < h:
-            mine = torch.cat([torch.zeros((h - mine.shape[0], 2), dtype=mine.dtype, device=mine.device), mine])
-        allh = [torch.empty_like(mine) for _ in range(self.world)]
-        dist.all_gather(allh, mine.contiguous(), group=self.group)
-        if self.rank > 0:
-            job.halo[0, :h].copy_(allh[self.rank - 1])
+        prev = gather_halo(job.out, self.span_frames[self.rank], h, self.rank, self.world, self.group)
+        if prev is not None:
+            job.halo[0, :h].copy_(prev)
 
     def limiter_sequential(self):
         job = self.job
-        if self.rank > 0:
-            dist.recv(job.lim_state, src=self.rank - 1, group=self.group)
-        job.finalize(False)
-        if self.rank < self.world - 1:
-            dist.send(job.lim_state, dst=self.rank + 1, group=self.group)
+        chain_state(job.lim_state, lambda: job.finalize(False), self.rank, self.world, self.group)
 
     # -------------------------------------------------------------- the step
     def step(self, d_in):
@@ -141,9 +190,7 @@ class ShardedTrack:
         if lufs_on:
             job.timed("loud2", lambda: job.loudness_pass2(carry=self.world > 1))
         if self.world > 1:
-            if lufs_on:
-                dist.all_reduce(job.hops, op=dist.ReduceOp.SUM, group=self.group)
-            dist.all_reduce(job.peak, op=dist.ReduceOp.MAX, group=self.group)
+            reduce_loudness(job.hops if lufs_on else None, job.peak, self.group)
         if lufs_on:
             job.timed("hist", job.histograms)
         job.timed("decide", job.decide)

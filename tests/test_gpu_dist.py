@@ -1,0 +1,84 @@
+"""N = 2 rehearsal of the chunk-sharded path on one GPU: two processes, both on
+cuda:0, exchanging over gloo (host-staged) instead of RCCL.  Every device kernel of
+the N > 1 path runs -- K-filter tails and carry, hop partials, all-reduced loudness,
+the limiter halo and, when the limiter can engage, the rank-to-rank sequential
+limiter -- and the concatenated rank outputs must equal the one-rank run of the
+same track bit for bit (the chunking, loudness decision and limiter are all
+track-level, so sharding must not change a sample)."""
+import datetime
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FS = 48000
+MB = dict(multiband=True, low_thresh=-25.0, low_ratio=6.0, mid_thresh=-20.0, mid_ratio=3.0,
+          high_thresh=-15.0, high_ratio=4.0)
+CASES = {
+    "c3_lufs": dict(bass_boost=-1.0, mid_cut=2.0, presence_boost=2.5, treble_boost=1.0,
+                    lufs=-14.0, width=1.3, analog_character=40.0, **MB),
+    "loud_limiter": dict(bass_boost=6.0, treble_boost=3.0),
+}
+
+
+def _track(seconds):
+    from amx import synth
+    n = int(FS * seconds)
+    return synth.mix_like(n, FS, 2, seed=3)
+
+
+def _worker(rank, world, port, case, seconds, outdir):
+    import torch
+    import torch.distributed as dist
+    from amx.dist import ShardedTrack
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))
+    try:
+        torch.cuda.set_device(0)
+        x = _track(seconds)
+        tr = ShardedTrack(FS, 2, CASES[case], x.shape[0], rank, world, quantum=512)
+        d_in = torch.from_numpy(np.ascontiguousarray(x[tr.in0:tr.in0 + tr.local_frames])).cuda()
+        y = tr.step(d_in)
+        torch.cuda.synchronize()
+        np.save(os.path.join(outdir, "y%d.npy" % rank), y.cpu().numpy())
+        fast = bool(int(tr.job.ctl[0].item()) & 1)
+        np.save(os.path.join(outdir, "fast%d.npy" % rank), np.array([fast]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_two_ranks_match_one(gpu, case):
+    import torch
+    import torch.multiprocessing as mp
+    from amx.dist import ShardedTrack
+    seconds = 75.0                                      # 3 chunks -> ranks own 2 + 1
+    x = _track(seconds)
+    one = ShardedTrack(FS, 2, CASES[case], x.shape[0], 0, 1, quantum=512)
+    y1 = one.step(torch.from_numpy(np.ascontiguousarray(x)).cuda()).cpu().numpy()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(2, _port(), case, seconds, d), nprocs=2, join=True)
+        parts = [np.load(os.path.join(d, "y%d.npy" % r)) for r in range(2)]
+        fast = [bool(np.load(os.path.join(d, "fast%d.npy" % r))[0]) for r in range(2)]
+    y2 = np.concatenate(parts)
+    assert fast[0] == fast[1]
+    # the loud case must exercise the rank-to-rank sequential limiter
+    assert fast[0] == (case != "loud_limiter"), "limiter fast path %s" % fast[0]
+    assert y2.shape == y1.shape
+    diff = np.abs(y2.astype(np.int32) - y1.astype(np.int32))
+    assert diff.max() == 0, "max |diff| %d LSB at %s (limiter fast path %s)" % (
+        diff.max(), np.argmax(diff.max(axis=1)), fast[0])
