@@ -262,14 +262,61 @@ __device__ double env_rerun_wave(const ChainDev &cd, const double *m, double *ck
 // Frames move in 16-frame tiles.  A lane's tile is one 128-B row of m (64 rows per
 // wave); the wave loads the 64 rows cooperatively -- lane l moves 16-B piece l % 8
 // of rows 8 i + l / 8, so each load instruction covers 8 whole lines instead of 64
-// lines' 16-B fragments -- stages them in LDS (padded rows, conflict-free b128
-// reads) and issues the next tile's loads before computing this one.  Frames
-// before the chunk or after the segment are fed as m = 0 (state held); the m
-// buffer is padded so those rows read in bounds.  W and Le are multiples of 16 and
-// chunk rows start 16-frame aligned, so the warm-up / main boundary is
-// tile-uniform, every vector is 16-B aligned and checkpoints fall on tile starts.
+// lines' 16-B fragments -- and stages them in LDS (padded rows, conflict-free b128
+// reads).  The loads run AMX_ENV_PF tiles ahead of the tile being computed (a ring
+// of register tiles): one tile is ~16 dependent steps, shorter than a miss to HBM,
+// so a one-tile lookahead left the wave waiting on every tile.  Frames before the
+// chunk or after the segment are fed as m = 0 (state held); the m buffer is padded
+// so those rows read in bounds.  W and Le are multiples of 16 AMX_ENV_PF and chunk
+// rows start 16-frame aligned, so the warm-up / main boundary is tile-uniform,
+// every vector is 16-B aligned and checkpoints fall on tile starts.
 #define AMX_ENV_TF 16
 #define AMX_ENV_MP 18      // m tile pitch in doubles (144 B)
+#define AMX_ENV_PF 4       // tiles in flight
+
+template <bool RCP>
+__device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, d2v (&M)[8],
+                                          const double *const (&mrow)[8], int q, int ntile,
+                                          int nwarm, int64_t start, int64_t end, double *ckr,
+                                          double &att, double &s_spec, bool &any) {
+    const int lane = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int r = 8 * i + (lane >> 3);
+        *reinterpret_cast<d2v *>(sm + r * AMX_ENV_MP + 2 * (lane & 7)) = M[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+    {
+        // refill this ring slot with tile q + PF (past the end: re-read, unused)
+        const int qn = (q + AMX_ENV_PF < ntile ? q + AMX_ENV_PF : q) * AMX_ENV_TF;
+#pragma unroll
+        for (int i = 0; i < 8; i++) M[i] = *reinterpret_cast<const d2v *>(mrow[i] + qn);
+    }
+    const int64_t f0 = start + (int64_t)q * AMX_ENV_TF;
+    const bool in = f0 >= 0 && f0 < end;           // whole tile in (else held)
+    double mv[AMX_ENV_TF];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const d2v v = *reinterpret_cast<const d2v *>(sm + lane * AMX_ENV_MP + 2 * i);
+        mv[2 * i] = in ? v.x : 0.0;
+        mv[2 * i + 1] = in ? v.y : 0.0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (q == nwarm) s_spec = att;
+    if (q >= nwarm) {
+        if (in) ckr[f0 / AMX_ENV_TF] = att;
+        // the partial last tile of a chunk-final segment holds the state past the end
+        if (f0 + AMX_ENV_TF > end) {
+#pragma unroll
+            for (int f = 0; f < AMX_ENV_TF; f++) mv[f] = f0 + f < end ? mv[f] : 0.0;
+        }
+#pragma unroll
+        for (int f = 0; f < AMX_ENV_TF; f++) any |= mv[f] != 0.0;
+    }
+#pragma unroll
+    for (int f = 0; f < AMX_ENV_TF; f++) att = env_step<RCP>(cd, att, mv[f]);
+}
+
 template <bool RCP>
 __global__ void __launch_bounds__(64) k_env0(const ChainDev *__restrict__ cdp,
                                              const ChunkDev *__restrict__ chunks,
@@ -299,46 +346,18 @@ __global__ void __launch_bounds__(64) k_env0(const ChainDev *__restrict__ cdp,
         const int r = 8 * i + (lane >> 3);
         mrow[i] = mm + __shfl(rowoff + start, r) + 2 * (lane & 7);
     }
-    d2v M[8];
+    d2v M[AMX_ENV_PF][8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) M[i] = *reinterpret_cast<const d2v *>(mrow[i]);
+    for (int u = 0; u < AMX_ENV_PF; u++)
+#pragma unroll
+        for (int i = 0; i < 8; i++) M[u][i] = *reinterpret_cast<const d2v *>(mrow[i] + u * AMX_ENV_TF);
     double att = 0.0, s_spec = 0.0;
     bool any = false;
-    for (int q = 0; q < ntile; q++) {
+    for (int q0 = 0; q0 < ntile; q0 += AMX_ENV_PF) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int r = 8 * i + (lane >> 3);
-            *reinterpret_cast<d2v *>(sm + r * AMX_ENV_MP + 2 * (lane & 7)) = M[i];
-        }
-        __builtin_amdgcn_wave_barrier();
-        {
-            const int qn = (q + 1 < ntile ? q + 1 : q) * AMX_ENV_TF;   // last: re-read, unused
-#pragma unroll
-            for (int i = 0; i < 8; i++) M[i] = *reinterpret_cast<const d2v *>(mrow[i] + qn);
-        }
-        const int64_t f0 = start + (int64_t)q * AMX_ENV_TF;
-        const bool in = f0 >= 0 && f0 < end;           // whole tile in (else held)
-        double mv[AMX_ENV_TF];
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const d2v v = *reinterpret_cast<const d2v *>(sm + lane * AMX_ENV_MP + 2 * i);
-            mv[2 * i] = in ? v.x : 0.0;
-            mv[2 * i + 1] = in ? v.y : 0.0;
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (q == nwarm) s_spec = att;
-        if (q >= nwarm) {
-            if (in) ckr[f0 / AMX_ENV_TF] = att;
-            // the partial last tile of a chunk-final segment holds the state past the end
-            if (f0 + AMX_ENV_TF > end) {
-#pragma unroll
-                for (int f = 0; f < AMX_ENV_TF; f++) mv[f] = f0 + f < end ? mv[f] : 0.0;
-            }
-#pragma unroll
-            for (int f = 0; f < AMX_ENV_TF; f++) any |= mv[f] != 0.0;
-        }
-#pragma unroll
-        for (int f = 0; f < AMX_ENV_TF; f++) att = env_step<RCP>(cd, att, mv[f]);
+        for (int u = 0; u < AMX_ENV_PF; u++)
+            env0_tile<RCP>(cd, sm, M[u], mrow, q0 + u, ntile, nwarm, start, end, ckr, att, s_spec,
+                           any);
     }
     if (valid) {
         sv[(int64_t)b * n_es + j] = s_spec;
@@ -675,7 +694,8 @@ static void env_launch_t(const DynLaunch &d, const double *m, double *ck, double
 hipError_t launch_env(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
                       int *act, int *prev, int *flags, int rounds) {
     if (d.n_es <= 0) return hipSuccess;
-    if (d.warm % AMX_ENV_TF || d.Le % AMX_ENV_TF) return hipErrorInvalidValue;
+    if (d.warm % (AMX_ENV_TF * AMX_ENV_PF) || d.Le % (AMX_ENV_TF * AMX_ENV_PF))
+        return hipErrorInvalidValue;
     if (rounds < 0 || rounds > AMX_ENV_MAX_ROUNDS) return hipErrorInvalidValue;
     if (d.rcp) env_launch_t<true>(d, m, ck, sv, ev, act, prev, flags, rounds);
     else env_launch_t<false>(d, m, ck, sv, ev, act, prev, flags, rounds);

@@ -267,7 +267,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     if (!p) return fail(AMX_ENOMEM, "out of memory");
     p->desc = *desc;
     const int fs = desc->sample_rate;
-    if (desc->env_warm_frames >= 0) p->warm = (desc->env_warm_frames + 15) / 16 * 16;
+    if (desc->env_warm_frames >= 0) p->warm = (desc->env_warm_frames + 63) / 64 * 64;   // whole ring of k_env0 tiles
     if (desc->env_rounds >= 0) p->rounds = desc->env_rounds;
     if (p->rounds > AMX_ENV_MAX_ROUNDS) {
         delete p;
