@@ -178,6 +178,16 @@ class ShardedTrack:
         chain_state(job.lim_state, lambda: job.finalize(False), self.rank, self.world, self.group)
 
     # -------------------------------------------------------------- the step
+    def capture(self, d_in):
+        """One rank: record the whole step as a hipGraph (MasteringJob.capture).  N > 1
+        steps read the limiter decision on the host between collectives and stay eager."""
+        if self.world != 1:
+            raise RuntimeError("graph capture is for the one-rank step")
+        return self.job.capture(d_in)
+
+    def replay(self):
+        return self.job.replay()
+
     def step(self, d_in):
         """One pass of the whole path over this rank's chunks (input resident)."""
         from . import capi

@@ -216,6 +216,27 @@ class MasteringJob:
         self.report = {"chunks": len(self.chunks), "segments": self.info.n_segments}
         return self.y[:self.info.out_frames]
 
+    def capture(self, d_in):
+        """Record run(d_in) as one hipGraph (torch.cuda.CUDAGraph over the HIP stream
+        capture): replay() then re-issues the whole pipeline -- every kernel, same
+        buffers -- with one launch, so the host's per-kernel launch cost is off the
+        critical path.  run() has no host round trip, so the captured graph is the
+        complete step."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self.run(d_in)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.run(d_in)
+        self._graph = g
+        return g
+
+    def replay(self):
+        self._graph.replay()
+        return self.y[:self.info.out_frames]
+
     def track_output(self, t):
         s = self.spans[t]
         return self.y[s.out_offset:s.out_offset + s.out_frames]

@@ -43,11 +43,33 @@ def stage_bytes(stage, frames, ch_in, mb):
         "loud2": 4,                     # K-filter recursion: reads the track once
         "final": 4 + 4,                 # gain + limiter: track in -> output
         "xover": 4 + 12,                # P -> 3 bands
-        "rms": 12 + 6,                  # 3 bands -> 3 x u16 rms
-        "env": 6 + 24,                  # rms -> 3 x f64 attenuation
-        "apply": 12 + 24 + 4,           # bands + attenuation -> output
+        "rms": 12 + 24,                 # 3 bands -> 3 x f64 max attenuation m
+        "env": 24 + 1.5,                # m once -> 3 x f64 checkpoint per 16 frames
+        "apply": 12 + 24 + 1.5 + 4,     # bands + m + checkpoints -> output
     }
     return per.get(stage, 0) * frames
+
+
+# kernels of each stage (rocprofv3 short names) for the PMC traffic lookup
+STAGE_KERNELS = {
+    "front1": ("k_front1s", "k_front1"), "front2": ("k_front2",), "xover": ("k_xover2",),
+    "rms": ("k_rms",), "env": ("k_env0", "k_envfix"), "apply": ("k_gain_overlay",),
+    "loud1": ("k_kw1", "k_peak_reduce"), "loud2": ("k_kw2", "k_hops"), "final": ("k_final",),
+}
+
+
+def stage_traffic(stage, config):
+    """HBM bytes per launch of `stage` from the committed PMC summary
+    (profiles/traffic_<config>.json, scripts/gpu_traffic.sh), or None."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                        "traffic_%s.json" % config)
+    try:
+        ks = json.load(open(path))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    names = STAGE_KERNELS.get(stage, ())
+    hit = [v["hbm_bytes"] for k, v in ks.items() if k in names]
+    return int(sum(hit)) if hit else None
 
 
 def main():
@@ -59,6 +81,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=300.0)
     ap.add_argument("--seg-frames", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no hipGraph replay at N=1")
     args = ap.parse_args()
 
     import numpy as np
@@ -90,10 +113,17 @@ def main():
 
     for _ in range(args.warmup):
         track.step(d_in)
+    # one rank: the step is replayed as one captured hipGraph (every kernel, same
+    # buffers); N > 1 ranks step eagerly (host-side limiter decision between collectives)
+    graph = world == 1 and not args.eager
+    if graph:
+        track.capture(d_in)
+        track.replay()
+    run = track.replay if graph else (lambda: track.step(d_in))
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        track.step(d_in)
+        run()
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -135,11 +165,14 @@ def main():
                                "chunk-sharded" if args.config == "c2" else
                                "configs[2]: C2 + multiband + width 1.3 + analog 40",
                    "settings": args.config, "seconds_per_gpu": args.seconds,
-                   "seg_frames": args.seg_frames, "parallelism": "chunk-shard x%d" % world},
+                   "seg_frames": args.seg_frames, "parallelism": "chunk-shard x%d" % world,
+                   "launch": "hipGraph replay" if graph else "eager"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "bytes_per_launch": int(dom_bytes), "avg_launch_ms": round(dom_ms, 4),
-                     "traffic": None},
+                     "traffic": stage_traffic(dom, args.config),
+                     "traffic_source": "profiles/traffic_%s.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
+                                       % args.config},
         "stages_ms": {k: round(v, 4) for k, v in per_stage.items()},
         "plan": {"segments": int(job.info.n_segments), "seg_frames": int(job.info.seg_frames),
                  "scan_window_eq": int(job.info.scan_levels_eq),

@@ -213,6 +213,28 @@ def test_deterministic(gpu):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("settings", [C2, C3], ids=["c2", "c3"])
+def test_graph_replay_matches_eager(gpu, oracle_mod, settings):
+    """The captured hipGraph of the whole pipeline (MasteringJob.capture, used by
+    bench.py) replays to the eager result and the oracle, also after the input
+    buffer's contents change (the graph holds pointers, not values)."""
+    import torch
+    from amx import synth
+    from amx.engine import MasteringJob
+    fs = 48000
+    n = fs * 12
+    xs = [synth.mix_like(n, fs, 2, seed=s) for s in (21, 22)]
+    job = MasteringJob(fs, 2, settings, [n])
+    d_in = torch.from_numpy(xs[0]).cuda()
+    eager = job.run(d_in).cpu().numpy()
+    job.capture(d_in)
+    np.testing.assert_array_equal(job.replay().cpu().numpy(), eager)
+    d_in.copy_(torch.from_numpy(xs[1]))
+    y = job.replay().cpu().numpy()
+    eager2 = MasteringJob(fs, 2, settings, [n]).run(torch.from_numpy(xs[1]).cuda()).cpu().numpy()
+    np.testing.assert_array_equal(y, eager2)
+
+
 @pytest.mark.slow
 def test_full_size_c3_5min(gpu, oracle_mod):
     """BASELINE config 3 at full size (5 min stereo 48 kHz) against the oracle."""
