@@ -9,18 +9,19 @@
 //
 // r is embarrassingly parallel (k_rms: block prefix sums).  The envelope is a
 // sequential nonlinear recurrence; it is parallelised by exact speculation:
-//   round 0 (k_env0): every envelope segment of Le frames runs from att = 0 started
-//     W frames earlier (the trajectories of this recurrence coincide after clamp
-//     events, so the warm-up usually lands exactly on the true state) and writes its
-//     gained output, its start guess s_j and end state e_j;
-//   rounds 1..R (k_envfix): segment j takes its true start from the end of the
-//     nearest earlier segment that has any over-threshold frame (below-threshold
-//     frames hold the state: m = 0 makes both steps the identity), and if it differs
-//     from s_j re-runs both trajectories in lockstep until they coincide, rewriting
-//     the gained output up to there;
+//   k_env0: every envelope segment of Le frames runs from att = 0 started W frames
+//     earlier (the trajectories of this recurrence coincide after clamp events, so
+//     the warm-up usually lands exactly on the true state) and writes its start guess
+//     s_j, end state e_j, an over-threshold flag and a checkpoint every 16 frames;
+//   k_envfix rounds: segment j takes its true start from the end of the nearest
+//     earlier segment that has any over-threshold frame (below-threshold frames hold
+//     the state: m = 0 makes both steps the identity), and if it differs from s_j the
+//     wave re-runs the segment from it, rewriting checkpoints until the new state
+//     meets a stored one (the trajectories have coincided);
 //   k_envseq: a final in-order walk per (chunk, band) fixes whatever is still
-//     inconsistent, so the result is exact whatever the signal; it costs one parallel
-//     consistency scan when the rounds already converged.
+//     inconsistent, so the result is exact whatever the signal;
+//   k_gain_overlay: every frame's attenuation from the checkpoint before it, the
+//     gain, and the 3-band overlay.
 // Every value is produced by the reference's own operation sequence from the true
 // start state, so the envelope is bit-exact, not approximate.
 #include "amx_dev.hpp"
