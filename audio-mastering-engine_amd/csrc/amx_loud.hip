@@ -487,28 +487,49 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+// bin search without a table walk: the largest b < 1000 with bounds[b] <= v (what
+// find_bin's bisection returns for v >= bounds[0]) is the number of the 1000 lower
+// bounds <= v, minus one; each lane counts its 16, the wave sums
+__device__ __forceinline__ int wave_find_bin(const double (&bd)[AMX_BPL], double v) {
+    int c = 0;
+#pragma unroll
+    for (int q = 0; q < AMX_BPL; q++) c += bd[q] <= v ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    return c - 1;
+}
+
+// the energy of bin j from the lane that owns it
+__device__ __forceinline__ double wave_bin_value(const double (&en)[AMX_BPL], int j) {
+    double v = 0.0;
+#pragma unroll
+    for (int q = 0; q < AMX_BPL; q++) v = (j % AMX_BPL) == q ? en[q] : v;
+    return __shfl(v, j / AMX_BPL);
+}
+
 __global__ void __launch_bounds__(64) k_decide(DecideArgs a) {
     const int t = blockIdx.x, lane = threadIdx.x;
     const unsigned long long *H = a.hist + (int64_t)t * AMX_HIST_BINS;
     const unsigned long long *S = a.st_hist + (int64_t)t * AMX_HIST_BINS;
-    // bin energies and boundaries staged in LDS: the bin searches and lookups below
-    // are dependent chains, each step an LDS read instead of an L2 round trip
-    __shared__ double E[AMX_HIST_BINS], B[AMX_HIST_BINS + 1];
-    for (int i = lane; i < AMX_HIST_BINS; i += 64) E[i] = a.energies[i];
-    for (int i = lane; i <= AMX_HIST_BINS; i += 64) B[i] = B[i];
-    __syncthreads();
     double I = -INFINITY, thr = -70.0, lra = 0.0;
     if (a.lufs_on) {
-        double hc[AMX_BPL], sc[AMX_BPL], en[AMX_BPL];
+        // lane l owns bins [16 l, 16 l + 16): counts, bin energies and lower bounds in
+        // registers, every load in flight before the first use (bins past 999 hold
+        // count 0 and bound +inf)
+        double hc[AMX_BPL], sc[AMX_BPL], en[AMX_BPL], bd[AMX_BPL];
 #pragma unroll
-        for (int q = 0; q < AMX_BPL; q++) {      // all loads in flight before use
+        for (int q = 0; q < AMX_BPL; q++) {
             const int j = lane * AMX_BPL + q;
             const int jj = j < AMX_HIST_BINS ? j : AMX_HIST_BINS - 1;
             const bool ok = j < AMX_HIST_BINS;
-            hc[q] = ok ? (double)H[jj] : 0.0;
-            sc[q] = ok ? (double)S[jj] : 0.0;
-            en[q] = E[jj];
+            const unsigned long long h = H[jj], sh = S[jj];
+            const double e = a.energies[jj], b = a.bounds[jj];
+            hc[q] = ok ? (double)h : 0.0;
+            sc[q] = ok ? (double)sh : 0.0;
+            en[q] = e;
+            bd[q] = ok ? b : INFINITY;
         }
+        const double b0 = __shfl(bd[0], 0);
         // integrated loudness with the relative gate (ebur128_gated_loudness)
         double rel = 0.0, cnt = 0.0;
 #pragma unroll
@@ -520,10 +541,10 @@ __global__ void __launch_bounds__(64) k_decide(DecideArgs a) {
             rel *= 0.1;                                // pow(10, -10/10)
             thr = lufs_of(rel);
             int start;
-            if (rel < B[0]) start = 0;
+            if (rel < b0) start = 0;
             else {
-                start = find_bin(B, rel);
-                if (rel > E[start]) ++start;
+                start = wave_find_bin(bd, rel);
+                if (rel > wave_bin_value(en, start)) ++start;
             }
             double g = 0.0, above = 0.0;
 #pragma unroll
@@ -546,10 +567,10 @@ __global__ void __launch_bounds__(64) k_decide(DecideArgs a) {
             power /= size;
             const double integ = 0.01 * power;         // pow(10, -20/10)
             int index;
-            if (integ < B[0]) index = 0;
+            if (integ < b0) index = 0;
             else {
-                index = find_bin(B, integ);
-                if (integ > E[index]) ++index;
+                index = wave_find_bin(bd, integ);
+                if (integ > wave_bin_value(en, index)) ++index;
             }
             double mine = 0.0;                         // this lane's counts at bins >= index
             double cum[AMX_BPL];
@@ -585,7 +606,7 @@ __global__ void __launch_bounds__(64) k_decide(DecideArgs a) {
                     jl = min(jl, __shfl_xor(jl, o));
                     jh = min(jh, __shfl_xor(jh, o));
                 }
-                lra = lufs_of(E[jh]) - lufs_of(E[jl]);
+                lra = lufs_of(wave_bin_value(en, jh)) - lufs_of(wave_bin_value(en, jl));
             }
         }
     }

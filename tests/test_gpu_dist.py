@@ -21,14 +21,19 @@ MB = dict(multiband=True, low_thresh=-25.0, low_ratio=6.0, mid_thresh=-20.0, mid
 CASES = {
     "c3_lufs": dict(bass_boost=-1.0, mid_cut=2.0, presence_boost=2.5, treble_boost=1.0,
                     lufs=-14.0, width=1.3, analog_character=40.0, **MB),
-    "loud_limiter": dict(bass_boost=6.0, treble_boost=3.0),
+    "loud_limiter": dict(width=1.5),       # no EQ stage (the EQ lowers the level): clips
 }
 
 
-def _track(seconds):
+# input gain per case: the loud case drives the chain into clipping, so the final
+# alimiter (limit 0.98) must engage and the ranks hand its state along
+GAIN = {"c3_lufs": 1.0, "loud_limiter": 4.0}
+
+
+def _track(seconds, case):
     from amx import synth
     n = int(FS * seconds)
-    return synth.mix_like(n, FS, 2, seed=3)
+    return (synth.mix_like(n, FS, 2, seed=3) * np.float32(GAIN[case])).astype(np.float32)
 
 
 def _worker(rank, world, port, case, seconds, outdir):
@@ -41,7 +46,7 @@ def _worker(rank, world, port, case, seconds, outdir):
                             timeout=datetime.timedelta(seconds=60))
     try:
         torch.cuda.set_device(0)
-        x = _track(seconds)
+        x = _track(seconds, case)
         tr = ShardedTrack(FS, 2, CASES[case], x.shape[0], rank, world, quantum=512)
         d_in = torch.from_numpy(np.ascontiguousarray(x[tr.in0:tr.in0 + tr.local_frames])).cuda()
         y = tr.step(d_in)
@@ -66,8 +71,10 @@ def test_two_ranks_match_one(gpu, case):
     import torch
     import torch.multiprocessing as mp
     from amx.dist import ShardedTrack
-    seconds = 75.0                                      # 3 chunks -> ranks own 2 + 1
-    x = _track(seconds)
+    # 3 chunks -> ranks own 2 + 1; the sequential-limiter case 2 chunks (that path walks
+    # every frame in order)
+    seconds = 75.0 if case != "loud_limiter" else 32.0
+    x = _track(seconds, case)
     one = ShardedTrack(FS, 2, CASES[case], x.shape[0], 0, 1, quantum=512)
     y1 = one.step(torch.from_numpy(np.ascontiguousarray(x)).cuda()).cpu().numpy()
     with tempfile.TemporaryDirectory() as d:
