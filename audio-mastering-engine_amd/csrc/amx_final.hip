@@ -82,112 +82,151 @@ __device__ __forceinline__ void final_fast_block(const SpanDev *__restrict__ spa
     }
 }
 
-// General alimiter (af_alimiter.c filter_frame, asc off), one thread per track
-// span, sequential.  State layout (doubles): [0] att [1] delta [2] pos [3] nextiter
-// [4] nextlen [5] valid  [8 .. 8+bs) buffer  [8+bs .. 8+2bs) nextdelta
-// [8+2bs .. 8+3bs) nextpos (stored as doubles).
-__device__ void final_general_track(int t, const SpanDev *__restrict__ spans,
-                                    const uint32_t *__restrict__ x,
-                                    const uint32_t *__restrict__ halo, int halo_frames,
-                                    const double *__restrict__ gains, int fs, double level_in,
-                                    double level, double level_out, double limit, double release,
-                                    int bs, double *__restrict__ state, int64_t state_doubles,
-                                    uint32_t *__restrict__ y) {
+// General alimiter (af_alimiter.c filter_frame, asc off), one wave per track span.
+// The recurrence is sequential and runs on lane 0 with the ring buffer, nextdelta
+// and nextpos in LDS (dynamic shared memory, 3 bs doubles); the wave loads, gains
+// and converts 64 frames at a time in parallel around it (coalesced loads and
+// stores, the per-sample gain stage off the sequential chain).  The operation
+// sequence per frame is the reference's.  State layout in `state` (doubles), for
+// the rank-to-rank hand-off: [0] att [1] delta [2] pos [3] nextiter [4] nextlen
+// [5] valid  [8 .. 8+bs) buffer  [8+bs .. 8+2bs) nextdelta  [8+2bs .. 8+3bs) nextpos.
+#define AMX_LIM_BATCH 64
+__device__ void final_general_wave(int t, const SpanDev *__restrict__ spans,
+                                   const uint32_t *__restrict__ x,
+                                   const uint32_t *__restrict__ halo, int halo_frames,
+                                   const double *__restrict__ gains, int fs, double level_in,
+                                   double level, double level_out, double limit, double release,
+                                   int bs, double *__restrict__ state, int64_t state_doubles,
+                                   uint32_t *__restrict__ y, double *lds) {
+    const int lane = threadIdx.x & 63;
     const SpanDev sp = spans[t];
     const int channels = 2;
     double *S = state + (int64_t)t * state_doubles;
-    double *buffer = S + 8, *nextdelta = S + 8 + bs, *nextposd = S + 8 + 2 * bs;
-    double att, delta;
-    int pos, nextiter, nextlen;
-    if (sp.tframe0 == 0 || S[5] == 0.0) {
-        att = 1.0; delta = 0.0; pos = 0; nextiter = 0; nextlen = 0;
-        for (int k = 0; k < bs; k++) { buffer[k] = 0.0; nextdelta[k] = 0.0; nextposd[k] = -1.0; }
-        if (sp.tframe0 != 0) {
-            // no carried state: prime the ring with the halo (limiter assumed idle)
-            for (int h = 0; h < halo_frames; h++) {
-                uint32_t p = halo[(int64_t)t * halo_frames + h];
-                const double g = gains[t];
-                for (int c = 0; c < channels; c++)
-                    buffer[pos + c] = ((double)gain16(c ? hi16(p) : lo16(p), g) * (1.0 / 32768.0)) * level_in;
+    double *buffer = lds, *nextdelta = lds + bs, *nextposd = lds + 2 * bs;
+    double *inb = lds + 3 * bs, *outb = inb + 2 * AMX_LIM_BATCH;
+    const double g = gains[t];
+    const bool fresh = sp.tframe0 == 0 || S[5] == 0.0;
+    for (int k = lane; k < bs; k += 64) {
+        buffer[k] = fresh ? 0.0 : S[8 + k];
+        nextdelta[k] = fresh ? 0.0 : S[8 + bs + k];
+        nextposd[k] = fresh ? -1.0 : S[8 + 2 * bs + k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    double att = 1.0, delta = 0.0;
+    int pos = 0, nextiter = 0, nextlen = 0;
+    if (lane == 0) {
+        if (fresh) {
+            if (sp.tframe0 != 0) {
+                // no carried state: prime the ring with the halo (limiter assumed idle)
+                for (int h = 0; h < halo_frames; h++) {
+                    uint32_t p = halo[(int64_t)t * halo_frames + h];
+                    for (int c = 0; c < channels; c++)
+                        buffer[pos + c] = ((double)gain16(c ? hi16(p) : lo16(p), g) * (1.0 / 32768.0)) * level_in;
+                    pos = (pos + channels) % bs;
+                }
+            }
+        } else {
+            att = S[0]; delta = S[1]; pos = (int)S[2]; nextiter = (int)S[3]; nextlen = (int)S[4];
+        }
+    }
+#define NEXTPOS(k) ((int)nextposd[(k)])
+    for (int64_t base = 0; base < sp.out_n; base += AMX_LIM_BATCH) {
+        const int nb = (int)(sp.out_n - base < AMX_LIM_BATCH ? sp.out_n - base : AMX_LIM_BATCH);
+        if (lane < nb) {
+            const uint32_t p = x[sp.out_off + base + lane];
+            for (int c = 0; c < channels; c++)
+                inb[2 * lane + c] = ((double)gain16(c ? hi16(p) : lo16(p), g) * (1.0 / 32768.0)) * level_in;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+            for (int k = 0; k < nb; k++) {
+                double dst[2];
+                double peak = 0;
+                for (int c = 0; c < channels; c++) {
+                    const double sample = inb[2 * k + c];
+                    buffer[pos + c] = sample;
+                    peak = fmax(peak, fabs(sample));
+                }
+                if (peak > limit) {
+                    double patt = fmin(limit / peak, 1.);
+                    double rdelta = (1.0 - patt) / (fs * release);
+                    double d = (limit / peak - att) / bs * channels;
+                    int found = 0, i;
+                    if (d < delta) {
+                        delta = d;
+                        nextposd[0] = pos;
+                        nextposd[1] = -1;
+                        nextdelta[0] = rdelta;
+                        nextlen = 1;
+                        nextiter = 0;
+                    } else {
+                        for (i = nextiter; i < nextiter + nextlen; i++) {
+                            int jx = i % bs;
+                            double ppeak = 0, pdelta;
+                            for (int c = 0; c < channels; c++) ppeak = fmax(ppeak, fabs(buffer[NEXTPOS(jx) + c]));
+                            pdelta = (limit / peak - limit / ppeak) /
+                                     (((bs - NEXTPOS(jx) + pos) % bs) / channels);
+                            if (pdelta < nextdelta[jx]) {
+                                nextdelta[jx] = pdelta;
+                                found = 1;
+                                break;
+                            }
+                        }
+                        if (found) {
+                            nextlen = i - nextiter + 1;
+                            nextposd[(nextiter + nextlen) % bs] = pos;
+                            nextdelta[(nextiter + nextlen) % bs] = rdelta;
+                            nextposd[(nextiter + nextlen + 1) % bs] = -1;
+                            nextlen++;
+                        }
+                    }
+                }
+                const double *buf = &buffer[(pos + channels) % bs];
+                peak = 0;
+                for (int c = 0; c < channels; c++) peak = fmax(peak, fabs(buf[c]));
+                att += delta;
+                for (int c = 0; c < channels; c++) dst[c] = buf[c] * att;
+                if ((pos + channels) % bs == NEXTPOS(nextiter)) {
+                    delta = nextdelta[nextiter];
+                    att = limit / peak;
+                    nextlen -= 1;
+                    nextposd[nextiter] = -1;
+                    nextiter = (nextiter + 1) % bs;
+                }
+                if (att > 1.) { att = 1.; delta = 0.; nextiter = 0; nextlen = 0; nextposd[0] = -1; }
+                if (att <= 0.) { att = 0.0000000000001; delta = (1.0 - att) / (fs * release); }
+                if (att != 1. && (1. - att) < 0.0000000000001) att = 1.;
+                if (delta != 0. && fabs(delta) < 0.00000000000001) delta = 0.;
+                for (int c = 0; c < channels; c++) outb[2 * k + c] = dst[c];
                 pos = (pos + channels) % bs;
             }
         }
-    } else {
-        att = S[0]; delta = S[1]; pos = (int)S[2]; nextiter = (int)S[3]; nextlen = (int)S[4];
-    }
-#define NEXTPOS(k) ((int)nextposd[(k)])
-    const double g = gains[t];
-    for (int64_t n = 0; n < sp.out_n; n++) {
-        uint32_t p = x[sp.out_off + n];
-        double dst[2];
-        double peak = 0;
-        for (int c = 0; c < channels; c++) {
-            double sample = ((double)gain16(c ? hi16(p) : lo16(p), g) * (1.0 / 32768.0)) * level_in;
-            buffer[pos + c] = sample;
-            peak = fmax(peak, fabs(sample));
-        }
-        if (peak > limit) {
-            double patt = fmin(limit / peak, 1.);
-            double rdelta = (1.0 - patt) / (fs * release);
-            double d = (limit / peak - att) / bs * channels;
-            int found = 0, i;
-            if (d < delta) {
-                delta = d;
-                nextposd[0] = pos;
-                nextposd[1] = -1;
-                nextdelta[0] = rdelta;
-                nextlen = 1;
-                nextiter = 0;
-            } else {
-                for (i = nextiter; i < nextiter + nextlen; i++) {
-                    int jx = i % bs;
-                    double ppeak = 0, pdelta;
-                    for (int c = 0; c < channels; c++) ppeak = fmax(ppeak, fabs(buffer[NEXTPOS(jx) + c]));
-                    pdelta = (limit / peak - limit / ppeak) /
-                             (((bs - NEXTPOS(jx) + pos) % bs) / channels);
-                    if (pdelta < nextdelta[jx]) {
-                        nextdelta[jx] = pdelta;
-                        found = 1;
-                        break;
-                    }
-                }
-                if (found) {
-                    nextlen = i - nextiter + 1;
-                    nextposd[(nextiter + nextlen) % bs] = pos;
-                    nextdelta[(nextiter + nextlen) % bs] = rdelta;
-                    nextposd[(nextiter + nextlen + 1) % bs] = -1;
-                    nextlen++;
-                }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (lane < nb) {
+            int16_t o[2];
+            for (int c = 0; c < channels; c++) {
+                double v = outb[2 * lane + c];
+                v = v < -limit ? -limit : (v > limit ? limit : v);
+                v = v * level * level_out;
+                o[c] = clip_llrint(v * 32768.0);
             }
+            y[sp.out_off + base + lane] = pack2(o[0], o[1]);
         }
-        const double *buf = &buffer[(pos + channels) % bs];
-        peak = 0;
-        for (int c = 0; c < channels; c++) peak = fmax(peak, fabs(buf[c]));
-        att += delta;
-        for (int c = 0; c < channels; c++) dst[c] = buf[c] * att;
-        if ((pos + channels) % bs == NEXTPOS(nextiter)) {
-            delta = nextdelta[nextiter];
-            att = limit / peak;
-            nextlen -= 1;
-            nextposd[nextiter] = -1;
-            nextiter = (nextiter + 1) % bs;
-        }
-        if (att > 1.) { att = 1.; delta = 0.; nextiter = 0; nextlen = 0; nextposd[0] = -1; }
-        if (att <= 0.) { att = 0.0000000000001; delta = (1.0 - att) / (fs * release); }
-        if (att != 1. && (1. - att) < 0.0000000000001) att = 1.;
-        if (delta != 0. && fabs(delta) < 0.00000000000001) delta = 0.;
-        int16_t o[2];
-        for (int c = 0; c < channels; c++) {
-            double v = dst[c];
-            v = v < -limit ? -limit : (v > limit ? limit : v);
-            v = v * level * level_out;
-            o[c] = clip_llrint(v * 32768.0);
-        }
-        y[sp.out_off + n] = pack2(o[0], o[1]);
-        pos = (pos + channels) % bs;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
 #undef NEXTPOS
-    S[0] = att; S[1] = delta; S[2] = pos; S[3] = nextiter; S[4] = nextlen; S[5] = 1.0;
+    if (lane == 0) {
+        S[0] = att; S[1] = delta; S[2] = pos; S[3] = nextiter; S[4] = nextlen; S[5] = 1.0;
+    }
+    for (int k = lane; k < bs; k += 64) {
+        S[8 + k] = buffer[k];
+        S[8 + bs + k] = nextdelta[k];
+        S[8 + 2 * bs + k] = nextposd[k];
+    }
 }
 
 // One launch for both limiter paths.  Columns blockIdx.x < gridDim.x - 1 are the
@@ -208,16 +247,17 @@ struct FinalArgs {
 
 template <bool UNIT>
 __global__ void __launch_bounds__(AMX_BLOCK) k_final(FinalArgs a) {
+    extern __shared__ double lim_lds[];                 // general path: 3 bs + 4 x 64 doubles
     const int t = blockIdx.y;
     const bool fast = a.ctl ? (a.ctl[t] & AMX_CTL_FAST) != 0 : a.fast != 0;
     if (blockIdx.x + 1 < gridDim.x) {
         if (fast)
             final_fast_block<UNIT>(a.spans, a.x, a.halo, a.halo_frames, a.gains, a.level_in,
                                    a.level, a.level_out, a.limit, a.y);
-    } else if (!fast && threadIdx.x == 0) {
-        final_general_track(t, a.spans, a.x, a.halo, a.halo_frames, a.gains, a.fs, a.level_in,
-                            a.level, a.level_out, a.limit, a.release, a.bs, a.state,
-                            a.state_doubles, a.y);
+    } else if (!fast && threadIdx.x < 64) {
+        final_general_wave(t, a.spans, a.x, a.halo, a.halo_frames, a.gains, a.fs, a.level_in,
+                           a.level, a.level_out, a.limit, a.release, a.bs, a.state,
+                           a.state_doubles, a.y, lim_lds);
     }
 }
 
@@ -234,8 +274,10 @@ hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, co
                 halo_frames, fs, buffer_size, fast, gains, ctl, level_in, level, level_out, limit,
                 release, state, state_doubles, reinterpret_cast<uint32_t *>(y)};
     const bool unit = level_in == 1.0 && level_out == 1.0 && limit * 32768.0 <= 32767.0;
-    if (unit) hipLaunchKernelGGL(k_final<true>, g, dim3(AMX_BLOCK), 0, st, a);
-    else hipLaunchKernelGGL(k_final<false>, g, dim3(AMX_BLOCK), 0, st, a);
+    const size_t lds = ((size_t)3 * buffer_size + 4 * AMX_LIM_BATCH) * sizeof(double);
+    if (lds > 64 * 1024) return hipErrorInvalidValue;   // bs <= 2645: attack <= 13.7 ms at 96 kHz
+    if (unit) hipLaunchKernelGGL(k_final<true>, g, dim3(AMX_BLOCK), lds, st, a);
+    else hipLaunchKernelGGL(k_final<false>, g, dim3(AMX_BLOCK), lds, st, a);
     return hipGetLastError();
 }
 

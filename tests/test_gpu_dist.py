@@ -25,9 +25,9 @@ CASES = {
 }
 
 
-# input gain per case: the loud case drives the chain into clipping, so the final
+# input gain per case: the loud case drives 0.1 % of the frames over the limit, so the final
 # alimiter (limit 0.98) must engage and the ranks hand its state along
-GAIN = {"c3_lufs": 1.0, "loud_limiter": 4.0}
+GAIN = {"c3_lufs": 1.0, "loud_limiter": 1.3}
 
 
 def _track(seconds, case):
