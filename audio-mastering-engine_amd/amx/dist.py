@@ -179,14 +179,61 @@ class ShardedTrack:
 
     # -------------------------------------------------------------- the step
     def capture(self, d_in):
-        """One rank: record the whole step as a hipGraph (MasteringJob.capture).  N > 1
-        steps read the limiter decision on the host between collectives and stay eager."""
-        if self.world != 1:
-            raise RuntimeError("graph capture is for the one-rank step")
-        return self.job.capture(d_in)
+        """Record the step's device work as hipGraphs (torch.cuda.CUDAGraph over HIP
+        stream capture).  One rank: the whole step (MasteringJob.capture).  N ranks: the
+        three stretches between collectives -- chunk chain + loudness pass 1, carry +
+        pass 2, histograms + decision -- each one graph; the collectives, the halo
+        exchange, the host's read of the limiter decision and the limiter stay eager.
+        replay() then issues a step with a handful of host calls."""
+        if self.world == 1:
+            return self.job.capture(d_in)
+        import torch
+        job = self.job
+        lufs_on = job.dd.lufs_on
+
+        def seg(*fns):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for fn in fns:
+                    fn()
+            return g
+
+        from . import capi
+
+        def carry():
+            capi.check(capi.load().amx_kw_carry(job.plan.h, capi.ptr(self.tails_all),
+                                                capi.ptr(job.kw_carry), job._s(None)), "amx_kw_carry")
+        torch.cuda.synchronize()
+        self._g = [seg(lambda: job.run_chunks(d_in), lambda: job.loudness_pass1(tail=True)),
+                   seg(carry, lambda: job.loudness_pass2(carry=True)) if lufs_on else seg(carry),
+                   seg(job.histograms, job.decide) if lufs_on else seg(job.decide)]
+        return self._g
 
     def replay(self):
-        return self.job.replay()
+        if self.world == 1:
+            return self.job.replay()
+        from . import capi
+        job = self.job
+        g1, g2, g3 = self._g
+        g1.replay()
+        gather_tails(job.kw_tail, self.tails_all, self.group)
+        g2.replay()
+        reduce_loudness(job.hops if job.dd.lufs_on else None, job.peak, self.group)
+        g3.replay()
+        self._finish(capi)
+        return job.y[:job.info.out_frames]
+
+    def _finish(self, capi):
+        """halo exchange, then the limiter path k_decide chose (the same word on every
+        rank: it is computed from all-reduced data)."""
+        job = self.job
+        self.exchange_halo()
+        fast = bool(int(job.ctl[0].item()) & capi.CTL_FAST)
+        if fast:
+            job.timed("final", lambda: job.finalize(True))
+        else:
+            job.lim_state.zero_()
+            self.limiter_sequential()
 
     def step(self, d_in):
         """One pass of the whole path over this rank's chunks (input resident)."""
@@ -207,12 +254,6 @@ class ShardedTrack:
         if self.world == 1:
             job.timed("final", lambda: job.finalize(None))
         else:
-            self.exchange_halo()
-            fast = bool(int(job.ctl[0].item()) & capi.CTL_FAST)   # same word on every rank
-            if fast:
-                job.timed("final", lambda: job.finalize(True))
-            else:
-                job.lim_state.zero_()
-                self.limiter_sequential()
+            self._finish(capi)
         job.report = {"chunks": len(job.chunks), "segments": job.info.n_segments}
         return job.y[:job.info.out_frames]

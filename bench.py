@@ -81,7 +81,11 @@ def main():
     ap.add_argument("--seconds", type=float, default=300.0)
     ap.add_argument("--seg-frames", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--eager", action="store_true", help="no hipGraph replay at N=1")
+    ap.add_argument("--eager", action="store_true", help="launch every kernel from the host")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL on ROCm); gloo only to rehearse N ranks on one GPU")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank on cuda:0 (rehearsal with --dist-backend gloo)")
     args = ap.parse_args()
 
     import numpy as np
@@ -94,8 +98,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(0 if args.one_device else local)
+        dist.init_process_group(args.dist_backend)
     fs = 48000
     settings = CONFIGS[args.config]
     per_rank = int(args.seconds * fs)
@@ -113,9 +117,9 @@ def main():
 
     for _ in range(args.warmup):
         track.step(d_in)
-    # one rank: the step is replayed as one captured hipGraph (every kernel, same
-    # buffers); N > 1 ranks step eagerly (host-side limiter decision between collectives)
-    graph = world == 1 and not args.eager
+    # the step's device work is replayed from captured hipGraphs (every kernel, same
+    # buffers): one graph at N = 1, the three stretches between collectives at N > 1
+    graph = not args.eager
     if graph:
         track.capture(d_in)
         track.replay()
@@ -166,7 +170,8 @@ def main():
                                "configs[2]: C2 + multiband + width 1.3 + analog 40",
                    "settings": args.config, "seconds_per_gpu": args.seconds,
                    "seg_frames": args.seg_frames, "parallelism": "chunk-shard x%d" % world,
-                   "launch": "hipGraph replay" if graph else "eager"},
+                   "launch": ("hipGraph replay" if world == 1 else "hipGraph segments + eager collectives")
+                             if graph else "eager"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "bytes_per_launch": int(dom_bytes), "avg_launch_ms": round(dom_ms, 4),

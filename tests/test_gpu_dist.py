@@ -51,7 +51,12 @@ def _worker(rank, world, port, case, seconds, outdir):
         d_in = torch.from_numpy(np.ascontiguousarray(x[tr.in0:tr.in0 + tr.local_frames])).cuda()
         y = tr.step(d_in)
         torch.cuda.synchronize()
-        np.save(os.path.join(outdir, "y%d.npy" % rank), y.cpu().numpy())
+        y_eager = y.cpu().numpy()
+        # the same step from captured graph segments (bench.py's timed path)
+        tr.capture(d_in)
+        y_graph = tr.replay().cpu().numpy()
+        np.testing.assert_array_equal(y_graph, y_eager)
+        np.save(os.path.join(outdir, "y%d.npy" % rank), y_eager)
         fast = bool(int(tr.job.ctl[0].item()) & 1)
         np.save(os.path.join(outdir, "fast%d.npy" % rank), np.array([fast]))
     finally:
