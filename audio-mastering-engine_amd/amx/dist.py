@@ -54,6 +54,29 @@ def shard_ranges(n_chunks, world):
     return out
 
 
+def shard_tracks(track_frames, world):
+    """A batch of whole tracks (C4: 64 tracks on 8 GPUs) split into contiguous runs,
+    one per rank, balanced by frames: [(t0, t1)].  Whole tracks need no exchange at
+    all -- loudness and the limiter are per track -- so each rank runs one
+    MasteringJob over its tracks."""
+    n = len(track_frames)
+    if n < world:
+        raise ValueError("%d tracks for %d ranks" % (n, world))
+    total = float(sum(track_frames))
+    out, t, acc = [], 0, 0.0
+    for r in range(world):
+        t0 = t
+        goal = total * (r + 1) / world
+        # take tracks while the next one's midpoint stays within this rank's share,
+        # leaving at least one track for every later rank
+        while t < n - (world - 1 - r) and (t == t0 or acc + track_frames[t] / 2.0 <= goal):
+            acc += track_frames[t]
+            t += 1
+        out.append((t0, t))
+    out[-1] = (out[-1][0], n)
+    return out
+
+
 def carry_from_tails(tails, span_frames, rank, propagate):
     """K-filter state entering `rank`'s span: c_0 = 0, c_{q+1} = A^{len_q} c_q + tail_q.
 

@@ -168,6 +168,18 @@ def test_shard_ranges(n_chunks, world):
     assert max(sizes) - min(sizes) <= 1 and sizes == sorted(sizes, reverse=True)
 
 
+@pytest.mark.parametrize("frames,world", [
+    ([11520000] * 64, 8), ([5, 1, 1, 1, 1, 5], 3), ([3, 3], 2), ([1] * 9, 8), ([100, 1, 1, 1], 2)])
+def test_shard_tracks(frames, world):
+    """C4 batches: contiguous whole-track runs, every rank non-empty, balanced."""
+    r = adist.shard_tracks(frames, world)
+    assert len(r) == world and r[0][0] == 0 and r[-1][1] == len(frames)
+    assert all(r[i][1] == r[i + 1][0] for i in range(world - 1))
+    assert all(b > a for a, b in r)
+    if len(set(frames)) == 1 and len(frames) % world == 0:
+        assert all(b - a == len(frames) // world for a, b in r)
+
+
 def test_shard_geometry_matches_one_gpu_timeline():
     """Rank spans tile the single-GPU output timeline: the per-chunk output lengths
     (pydub overlay rounding when multiband) summed per rank, in order."""

@@ -166,6 +166,30 @@ def test_pipeline_vs_oracle(gpu, oracle_mod, fs, settings, seconds, seed):
     _cmp(y.cpu().numpy(), ref, "pipeline fs=%d" % fs)
 
 
+def test_batch_of_tracks_vs_oracle(gpu, oracle_mod):
+    """C4 shape, scaled down: several tracks of different lengths in one plan (laid
+    back to back), each with its own loudness statistics, gain and limiter; every
+    track must equal the oracle's pipeline run on that track alone.  The silent
+    track takes loudnorm's skip path (:238)."""
+    import torch
+    from amx import synth
+    from amx.chunking import chunk_bounds
+    from amx.engine import MasteringJob
+    fs = 48000
+    xs = [synth.mix_like(int(fs * 31.0), fs, 2, seed=1),
+          synth.music_like(int(fs * 12.3), fs, 2, seed=2, peak_dbfs=-3.0),
+          np.zeros((int(fs * 5.0), 2), np.float32)]
+    job = MasteringJob(fs, 2, C3, [x.shape[0] for x in xs], quantum=512)
+    job.run(torch.from_numpy(np.ascontiguousarray(np.concatenate(xs))).cuda())
+    rep = job.fetch_report()
+    assert rep["modes"] == ["linear", "linear", "skip"], rep["modes"]
+    for t, x in enumerate(xs):
+        ref, info = oracle_mod.pipeline(oracle_mod.quantize(x), fs, C3, chunk_bounds(x.shape[0], fs, 512))
+        if t < 2:
+            assert rep["stats"][t] == info["stats"], (t, rep["stats"][t], info["stats"])
+        _cmp(job.track_output(t).cpu().numpy(), ref, "batch track %d" % t)
+
+
 def test_limiter_general_path(gpu, oracle_mod):
     """Loud square wave, no normalisation: alimiter engages (sequential kernel)."""
     import torch
