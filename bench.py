@@ -50,6 +50,23 @@ def stage_bytes(stage, frames, ch_in, mb):
     return per.get(stage, 0) * frames
 
 
+FP64_PEAK_TFS = 78.6   # MI355X fp64 vector, spec (half the 157.3 TF fp32 rate); measured 68
+
+
+def front2_flops(frames, settings, mb):
+    """fp64 FLOPs of one k_front2 launch, per channel-frame:
+    a 2nd-order section in DF-II-T is 9 (3 FMA + 1 mul + 1 FMA); a shelf adds its
+    3-op mix (:286-289), a peak is 4 sections + its 2-op mix (:290-298); the fused
+    GEMV is 2 D (K filter D = 4, crossover D = 8)."""
+    per = 0
+    for key, kind in (("bass_boost", "shelf"), ("mid_cut", "peak"), ("presence_boost", "peak"),
+                      ("treble_boost", "shelf")):
+        if float(settings.get(key, 0.0)) != 0.0:
+            per += 12 if kind == "shelf" else 38
+    per += 16 if mb else 8
+    return per * 2 * frames
+
+
 # kernels of each stage (rocprofv3 short names) for the PMC traffic lookup
 STAGE_KERNELS = {
     "front1": ("k_front1s", "k_front1"), "front2": ("k_front2",), "xover": ("k_xover2",),
@@ -157,6 +174,7 @@ def main():
     dom_ms = candidates[dom]
     dom_bytes = stage_bytes(dom, frames, 2, mb)
     achieved = dom_bytes / (dom_ms / 1e3) / 1e9
+    f2_flops = front2_flops(frames, settings, mb)
 
     line = {
         "metric": "mastered Msamples/sec (48 kHz stereo f32) at 1/2/4/8 GPUs; % HBM roofline",
@@ -178,6 +196,11 @@ def main():
                      "traffic": stage_traffic(dom, args.config),
                      "traffic_source": "profiles/traffic_%s.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
                                        % args.config},
+        "roofline_fp64": {"bound": "fp64", "kernel": "front2",
+                          "achieved": round(f2_flops / (per_stage["front2"] / 1e3) / 1e12, 2),
+                          "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                          "frac": round(f2_flops / (per_stage["front2"] / 1e3) / 1e12 / FP64_PEAK_TFS, 4),
+                          "flops_per_launch": int(f2_flops)},
         "stages_ms": {k: round(v, 4) for k, v in per_stage.items()},
         "plan": {"segments": int(job.info.n_segments), "seg_frames": int(job.info.seg_frames),
                  "scan_window_eq": int(job.info.scan_levels_eq),
