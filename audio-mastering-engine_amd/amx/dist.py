@@ -203,16 +203,29 @@ class ShardedTrack:
     # -------------------------------------------------------------- the step
     def capture(self, d_in):
         """Record the step's device work as hipGraphs (torch.cuda.CUDAGraph over HIP
-        stream capture).  One rank: the whole step (MasteringJob.capture).  N ranks: the
-        three stretches between collectives -- chunk chain + loudness pass 1, carry +
-        pass 2, histograms + decision -- each one graph; the collectives, the halo
-        exchange, the host's read of the limiter decision and the limiter stay eager.
-        replay() then issues a step with a handful of host calls."""
+        stream capture).  One rank: the whole step (MasteringJob.capture).  N ranks:
+        the stretches between the step's two collectives, each one graph:
+          G1  chunk chain, loudness pass 1, and packing this rank's exchange word --
+              K-filter tail (8 doubles), sample peaks (2), limiter halo (the span's
+              last B-1 frames as raw bytes) -- into one buffer;
+          all-gather of those buffers (everything every rank needs from the others
+              once the chunk chain is done, in ONE collective instead of three);
+          G2  unpack: carry from the tails (amx_kw_carry), peak = max over ranks, the
+              previous rank's halo; loudness pass 2;
+          all-reduce(SUM) of the hop energies (loudnorm on);
+          G3  histograms + decision;
+        then the host reads the limiter decision and launches the limiter (eager)."""
         if self.world == 1:
             return self.job.capture(d_in)
-        import torch
         job = self.job
         lufs_on = job.dd.lufs_on
+        rank, world = self.rank, self.world
+        h = job.halo_frames
+        n = self.span_frames[rank]
+        hw = (4 * h + 7) // 8                     # doubles holding the halo's bytes
+        self._xbuf = torch.zeros(10 + hw, dtype=torch.float64, device=job.device)
+        # flat [world * words]: all_gather_into_tensor's output, rank-major
+        self._xall = torch.zeros(world * (10 + hw), dtype=torch.float64, device=job.device)
 
         def seg(*fns):
             g = torch.cuda.CUDAGraph()
@@ -223,13 +236,30 @@ class ShardedTrack:
 
         from . import capi
 
-        def carry():
+        def pack():
+            xb = self._xbuf
+            xb[0:8].copy_(job.kw_tail.reshape(-1)[:8])
+            xb[8:10].copy_(job.peak.reshape(-1)[:2])
+            m = min(h, n)
+            if m > 0:                             # front zero padding stays zero
+                mine = job.out[n - m:n].contiguous().view(torch.uint8).reshape(-1)
+                xb.view(torch.uint8)[80 + 4 * (h - m):80 + 4 * h].copy_(mine)
+
+        def unpack():
+            xa = self._xall.view(world, -1)
+            self.tails_all.copy_(xa[:, 0:8].reshape(world, 2, 4))
             capi.check(capi.load().amx_kw_carry(job.plan.h, capi.ptr(self.tails_all),
                                                 capi.ptr(job.kw_carry), job._s(None)), "amx_kw_carry")
+            job.peak.reshape(-1)[:2].copy_(xa[:, 8:10].amax(0))
+            if rank > 0 and h > 0:
+                prev = xa[rank - 1].view(torch.uint8)[80:80 + 4 * h].view(torch.int16).reshape(h, 2)
+                job.halo[0, :h].copy_(prev)
+
         torch.cuda.synchronize()
-        self._g = [seg(lambda: job.run_chunks(d_in), lambda: job.loudness_pass1(tail=True)),
-                   seg(carry, lambda: job.loudness_pass2(carry=True)) if lufs_on else seg(carry),
-                   seg(job.histograms, job.decide) if lufs_on else seg(job.decide)]
+        g1 = seg(lambda: job.run_chunks(d_in), lambda: job.loudness_pass1(tail=True), pack)
+        g2 = seg(unpack, lambda: job.loudness_pass2(carry=True)) if lufs_on else seg(unpack)
+        g3 = seg(job.histograms, job.decide) if lufs_on else seg(job.decide)
+        self._g = [g1, g2, g3]
         return self._g
 
     def replay(self):
@@ -239,24 +269,31 @@ class ShardedTrack:
         job = self.job
         g1, g2, g3 = self._g
         g1.replay()
-        gather_tails(job.kw_tail, self.tails_all, self.group)
+        (a, b), st = _staged(self.group, self._xall, self._xbuf)
+        dist.all_gather_into_tensor(a, b, group=self.group)
+        if st:
+            self._xall.copy_(a)
         g2.replay()
-        reduce_loudness(job.hops if job.dd.lufs_on else None, job.peak, self.group)
+        if job.dd.lufs_on:
+            reduce_loudness(job.hops, None, self.group)
         g3.replay()
-        self._finish(capi)
+        self._limit(capi)
         return job.y[:job.info.out_frames]
 
-    def _finish(self, capi):
-        """halo exchange, then the limiter path k_decide chose (the same word on every
-        rank: it is computed from all-reduced data)."""
+    def _limit(self, capi):
+        """the limiter path k_decide chose (the same word on every rank: it is
+        computed from all-reduced data)"""
         job = self.job
-        self.exchange_halo()
         fast = bool(int(job.ctl[0].item()) & capi.CTL_FAST)
         if fast:
             job.timed("final", lambda: job.finalize(True))
         else:
             job.lim_state.zero_()
             self.limiter_sequential()
+
+    def _finish(self, capi):
+        self.exchange_halo()
+        self._limit(capi)
 
     def step(self, d_in):
         """One pass of the whole path over this rank's chunks (input resident)."""
