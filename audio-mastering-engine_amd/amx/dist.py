@@ -213,8 +213,9 @@ class ShardedTrack:
           G2  unpack: carry from the tails (amx_kw_carry), peak = max over ranks, the
               previous rank's halo; loudness pass 2;
           all-reduce(SUM) of the hop energies (loudnorm on);
-          G3  histograms + decision;
-        then the host reads the limiter decision and launches the limiter (eager)."""
+          G3  histograms + decision + the limiter on the device's decision;
+        then the host reads the decision and, only if the limiter can engage, re-runs
+        it as the sequential rank-to-rank chain."""
         if self.world == 1:
             return self.job.capture(d_in)
         job = self.job
@@ -258,7 +259,11 @@ class ShardedTrack:
         torch.cuda.synchronize()
         g1 = seg(lambda: job.run_chunks(d_in), lambda: job.loudness_pass1(tail=True), pack)
         g2 = seg(unpack, lambda: job.loudness_pass2(carry=True)) if lufs_on else seg(unpack)
-        g3 = seg(job.histograms, job.decide) if lufs_on else seg(job.decide)
+        # the limiter is launched on the device's own decision (k_decide's word): the
+        # idle path is then complete without a host round trip; when the limiter can
+        # engage, replay() re-runs it as the rank-to-rank sequential chain
+        fin = lambda: job.finalize(None)
+        g3 = seg(job.histograms, job.decide, fin) if lufs_on else seg(job.decide, fin)
         self._g = [g1, g2, g3]
         return self._g
 
@@ -277,7 +282,9 @@ class ShardedTrack:
         if job.dd.lufs_on:
             reduce_loudness(job.hops, None, self.group)
         g3.replay()
-        self._limit(capi)
+        if not (int(job.ctl[0].item()) & capi.CTL_FAST):
+            job.lim_state.zero_()
+            self.limiter_sequential()
         return job.y[:job.info.out_frames]
 
     def _limit(self, capi):
