@@ -30,6 +30,33 @@ __device__ __forceinline__ int16_t gain16(int16_t x, double g) {
 //   limiter(v) * 2^15 = rint(clamp(v, +-limit*2^15) * level) (one rounding in *level)
 // and the gain stage's own clip is subsumed by the +-limit*2^15 clamp.
 #define AMX_FINAL_FPT 8
+typedef uint32_t fu4v __attribute__((ext_vector_type(4)));
+
+// one stereo frame through the gain stage and the idle limiter
+template <bool UNIT>
+__device__ __forceinline__ uint32_t final_frame(uint32_t p, double g, double level_in,
+                                                double level, double level_out, double limit) {
+    int16_t o[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        if constexpr (UNIT) {
+            double v = (double)(c ? hi16(p) : lo16(p));
+            if (g > 0.0) v = rint(v * g);
+            const double l32 = limit * 32768.0;
+            v = v < -l32 ? -l32 : (v > l32 ? l32 : v);
+            o[c] = clip_llrint(v * level);
+        } else {
+            int16_t v = gain16(c ? hi16(p) : lo16(p), g);
+            double smp = ((double)v * (1.0 / 32768.0)) * level_in;
+            double d = smp * 1.0;
+            d = d < -limit ? -limit : (d > limit ? limit : d);
+            d = d * level * level_out;
+            o[c] = clip_llrint(d * 32768.0);
+        }
+    }
+    return pack2(o[0], o[1]);
+}
+
 template <bool UNIT>
 __device__ __forceinline__ void final_fast_block(const SpanDev *__restrict__ spans,
                                                  const uint32_t *__restrict__ x,
@@ -41,9 +68,44 @@ __device__ __forceinline__ void final_fast_block(const SpanDev *__restrict__ spa
                                                  uint32_t *__restrict__ y) {
     const int t = blockIdx.y;
     const SpanDev sp = spans[t];
-    const int64_t i0 = (int64_t)blockIdx.x * (AMX_BLOCK * AMX_FINAL_FPT) + threadIdx.x;
-    if (i0 >= sp.out_n) return;
+    const int64_t blk0 = (int64_t)blockIdx.x * (AMX_BLOCK * AMX_FINAL_FPT);
+    if (blk0 >= sp.out_n) return;                    // block-uniform
     const double g = gains[t];
+    const int h = halo_frames;
+    // Interior blocks (every source frame inside the span, whole block in range, the
+    // span 16-B aligned): thread t owns 4 consecutive frames per group, so every load
+    // and store instruction of a wave moves one contiguous KiB in 16-B pieces.  The
+    // delay h makes the source run start at word r = (-h) mod 4 of an aligned 4-frame
+    // vector: two aligned vectors are loaded and r selects the window (the neighbour
+    // lane loads the same lines, so HBM sees each byte once).
+    if (blk0 >= h + 3 && blk0 + AMX_BLOCK * AMX_FINAL_FPT <= sp.out_n && (sp.out_off & 3) == 0 &&
+        h >= 4) {
+        const int r = (4 - (h & 3)) & 3;
+        const uint32_t *xs = x + sp.out_off;
+        fu4v v0[AMX_FINAL_FPT / 4], v1[AMX_FINAL_FPT / 4];
+#pragma unroll
+        for (int m = 0; m < AMX_FINAL_FPT / 4; m++) {
+            const int64_t i = blk0 + 4 * threadIdx.x + (int64_t)m * 4 * AMX_BLOCK;
+            const int64_t base = i - h - r;          // aligned: i % 4 == 0, (h + r) % 4 == 0
+            v0[m] = *reinterpret_cast<const fu4v *>(xs + base);
+            v1[m] = *reinterpret_cast<const fu4v *>(xs + base + 4);
+        }
+#pragma unroll
+        for (int m = 0; m < AMX_FINAL_FPT / 4; m++) {
+            const int64_t i = blk0 + 4 * threadIdx.x + (int64_t)m * 4 * AMX_BLOCK;
+            uint32_t w[8] = {v0[m].x, v0[m].y, v0[m].z, v0[m].w, v1[m].x, v1[m].y, v1[m].z, v1[m].w};
+            fu4v o;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t p = r == 0 ? w[q] : (r == 1 ? w[q + 1] : (r == 2 ? w[q + 2] : w[q + 3]));
+                o[q] = final_frame<UNIT>(p, g, level_in, level, level_out, limit);
+            }
+            *reinterpret_cast<fu4v *>(y + sp.out_off + i) = o;
+        }
+        return;
+    }
+    // edge blocks: one frame per load, frames before the span from the halo
+    const int64_t i0 = blk0 + threadIdx.x;
     uint32_t p[AMX_FINAL_FPT];
 #pragma unroll
     for (int m = 0; m < AMX_FINAL_FPT; m++) {
@@ -60,25 +122,8 @@ __device__ __forceinline__ void final_fast_block(const SpanDev *__restrict__ spa
 #pragma unroll
     for (int m = 0; m < AMX_FINAL_FPT; m++) {
         const int64_t i = i0 + (int64_t)m * AMX_BLOCK;
-        int16_t o[2];
-#pragma unroll
-        for (int c = 0; c < 2; c++) {
-            if constexpr (UNIT) {
-                double v = (double)(c ? hi16(p[m]) : lo16(p[m]));
-                if (g > 0.0) v = rint(v * g);
-                const double l32 = limit * 32768.0;
-                v = v < -l32 ? -l32 : (v > l32 ? l32 : v);
-                o[c] = clip_llrint(v * level);
-            } else {
-                int16_t v = gain16(c ? hi16(p[m]) : lo16(p[m]), g);
-                double smp = ((double)v * (1.0 / 32768.0)) * level_in;
-                double d = smp * 1.0;
-                d = d < -limit ? -limit : (d > limit ? limit : d);
-                d = d * level * level_out;
-                o[c] = clip_llrint(d * 32768.0);
-            }
-        }
-        if (i < sp.out_n) y[sp.out_off + i] = pack2(o[0], o[1]);
+        const uint32_t o = final_frame<UNIT>(p[m], g, level_in, level, level_out, limit);
+        if (i < sp.out_n) y[sp.out_off + i] = o;
     }
 }
 
