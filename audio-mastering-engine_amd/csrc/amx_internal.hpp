@@ -175,10 +175,13 @@ struct DecideArgs {
 hipError_t launch_decide(const DecideArgs &a, hipStream_t st);
 hipError_t launch_kw_carry(const double *tails, const double *P, int n_prev, double *carry,
                            hipStream_t st);
+// per-track sample peak: partial maxima per block into part[track][block][2], the last
+// block of a track (counter cnt[track], zero between launches) writes peak[track][2]
+int peak_reduce_blocks(int64_t max_nkseg);
 hipError_t launch_peak_reduce(const SpanDev *spans, int n_tracks, int64_t max_nkseg,
-                              const uint32_t *pk, unsigned long long *peak, const KwSegDev *ks,
-                              int L, const int16_t *x, const double *G, double *e, int kw_fix,
-                              hipStream_t st);
+                              const uint32_t *pk, double *peak, unsigned int *cnt, int *part,
+                              const KwSegDev *ks, int L, const int16_t *x, const double *G,
+                              double *e, int kw_fix, hipStream_t st);
 hipError_t launch_kw_tail(const SpanDev *spans, int n_tracks, const double *s, const double *e,
                           const double *P, double *tail, hipStream_t st);
 }  // namespace amx

@@ -348,7 +348,9 @@ hipError_t launch_hist(const SpanDev *spans, int n_tracks, int hop, const double
 // workgroup redoes that one segment here (lanes split the frames, butterfly sum).
 __global__ void __launch_bounds__(AMX_PEAK_THREADS) k_peak_reduce(const SpanDev *__restrict__ spans,
                                                                   const uint32_t *__restrict__ pk,
-                                                                  unsigned long long *__restrict__ peak,
+                                                                  double *__restrict__ peak,
+                                                                  unsigned int *__restrict__ cnt,
+                                                                  int *__restrict__ part,
                                                                   const KwSegDev *__restrict__ ks,
                                                                   int L, const uint32_t *__restrict__ x,
                                                                   const double *__restrict__ G,
@@ -407,23 +409,51 @@ __global__ void __launch_bounds__(AMX_PEAK_THREADS) k_peak_reduce(const SpanDev 
         red[1][threadIdx.x >> 6] = m1;
     }
     __syncthreads();
-    if (threadIdx.x < 2) {
-        int m = 0;
-        for (int w = 0; w < AMX_PEAK_THREADS / 64; w++) m = max(m, red[threadIdx.x][w]);
-        const double p = (double)m * (1.0 / 32768.0);
-        atomicMax(peak + 2 * t + threadIdx.x, (unsigned long long)__double_as_longlong(p));
+    // the block's maxima go to its slot of `part`; the last block of the track to
+    // finish (counter) reduces the slots and writes the peak, then re-arms the
+    // counter -- no zeroing pass before, no atomics on the result
+    __shared__ bool last;
+    if (threadIdx.x == 0) {
+        int a = 0, b = 0;
+        for (int w = 0; w < AMX_PEAK_THREADS / 64; w++) {
+            a = max(a, red[0][w]);
+            b = max(b, red[1][w]);
+        }
+        const int nb = (int)((sp.nkseg + (int64_t)AMX_PEAK_THREADS * AMX_PEAK_PER_THREAD - 1) /
+                             ((int64_t)AMX_PEAK_THREADS * AMX_PEAK_PER_THREAD));
+        int *pt = part + ((int64_t)t * gridDim.x + blockIdx.x) * 2;
+        pt[0] = a;
+        pt[1] = b;
+        __threadfence();
+        last = atomicAdd(cnt + t, 1u) == (unsigned)(nb - 1);
+        if (last) {
+            __threadfence();
+            int ma = 0, mb = 0;
+            for (int k = 0; k < nb; k++) {
+                const volatile int *q = part + ((int64_t)t * gridDim.x + k) * 2;
+                ma = max(ma, q[0]);
+                mb = max(mb, q[1]);
+            }
+            peak[2 * t] = (double)ma * (1.0 / 32768.0);
+            peak[2 * t + 1] = (double)mb * (1.0 / 32768.0);
+            cnt[t] = 0u;
+        }
     }
 }
 
-hipError_t launch_peak_reduce(const SpanDev *spans, int n_tracks, int64_t max_nkseg,
-                              const uint32_t *pk, unsigned long long *peak, const KwSegDev *ks,
-                              int L, const int16_t *x, const double *G, double *e, int kw_fix,
-                              hipStream_t st) {
+int peak_reduce_blocks(int64_t max_nkseg) {
     const int64_t per = (int64_t)AMX_PEAK_THREADS * AMX_PEAK_PER_THREAD;
-    dim3 g((unsigned)((max_nkseg + per - 1) / per), (unsigned)n_tracks);
+    return (int)((max_nkseg + per - 1) / per);
+}
+
+hipError_t launch_peak_reduce(const SpanDev *spans, int n_tracks, int64_t max_nkseg,
+                              const uint32_t *pk, double *peak, unsigned int *cnt, int *part,
+                              const KwSegDev *ks, int L, const int16_t *x, const double *G,
+                              double *e, int kw_fix, hipStream_t st) {
+    dim3 g((unsigned)peak_reduce_blocks(max_nkseg), (unsigned)n_tracks);
     if (empty(g)) return hipSuccess;
-    hipLaunchKernelGGL(k_peak_reduce, g, dim3(AMX_PEAK_THREADS), 0, st, spans, pk, peak, ks, L,
-                       reinterpret_cast<const uint32_t *>(x), G, e, kw_fix);
+    hipLaunchKernelGGL(k_peak_reduce, g, dim3(AMX_PEAK_THREADS), 0, st, spans, pk, peak, cnt, part,
+                       ks, L, reinterpret_cast<const uint32_t *>(x), G, e, kw_fix);
     return hipGetLastError();
 }
 

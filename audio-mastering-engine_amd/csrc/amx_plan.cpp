@@ -198,6 +198,9 @@ struct amx_plan {
     int n_prev = 0;
     double *d_tailpow = nullptr;
     float *d_lut = nullptr;
+    unsigned int *d_pcnt = nullptr;   // k_peak_reduce's per-track block counter (self re-arming)
+    int *d_ppart = nullptr;           // its per-block partial maxima
+    int any_empty_span = 0;           // a span with no K segment: its peak is zeroed directly
     // workspace offsets
     size_t ws_bytes = 0;
     size_t o_a16, o_e, o_s, o_p16, o_ex, o_sx, o_bands, o_r, o_m, o_gain, o_esv, o_ee0, o_eflags, o_eact,
@@ -651,6 +654,13 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     UP(p->d_bounds, bounds, 1001);
     UP(p->d_energies, energies, 1000);
     UP(p->d_tailpow, p->tail_pow.data(), p->tail_pow.size());
+    {
+        std::vector<unsigned int> zero((size_t)(p->n_tracks > 0 ? p->n_tracks : 1), 0u);
+        UP(p->d_pcnt, zero.data(), zero.size());
+        const size_t nb = (size_t)amx::peak_reduce_blocks(p->max_nkseg);
+        UP(p->d_ppart, (const int *)nullptr, (size_t)(p->n_tracks > 0 ? p->n_tracks : 1) * (nb ? nb : 1) * 2);
+        for (const SpanDev &sp : p->spans) p->any_empty_span |= sp.nkseg == 0 ? 1 : 0;
+    }
     if (desc->tanh_lut) UP(p->d_lut, desc->tanh_lut, 65536);
 #undef UP
     // ------------------------------------------------------- workspace layout
@@ -699,7 +709,7 @@ void amx_plan_free(amx_plan *p) {
                     p->d_kblks, p->d_n1,   p->d_G,    p->d_M,     p->d_Mp,     p->d_Gx,
                     p->d_Mx,  p->d_Mpx,    p->d_Gkw,  p->d_Mkw,   p->d_Mpkw,   p->d_tabs,
                     p->d_bounds, p->d_tailpow, p->d_lut, p->d_energies, p->d_carryP,
-                    p->d_esegs, p->d_eseg0, p->d_neseg};
+                    p->d_esegs, p->d_eseg0, p->d_neseg, p->d_pcnt, p->d_ppart};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     delete p;
@@ -818,7 +828,10 @@ int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, double *d_kw_tail, dou
     if (!p || !d_peak || (p->n_kseg > 0 && (!d_out || !d_ws)))
         return fail(AMX_EINVAL, "null argument");
     hipStream_t st = (hipStream_t)stream;
-    HIPCHK(hipMemsetAsync(d_peak, 0, sizeof(double) * 2 * (size_t)p->n_tracks, st));
+    // k_peak_reduce writes every track's peak; only tracks without a K segment (empty
+    // spans) need the zero written here
+    if (p->any_empty_span || p->n_kseg == 0)
+        HIPCHK(hipMemsetAsync(d_peak, 0, sizeof(double) * 2 * (size_t)p->n_tracks, st));
     p->kw_rest_states = 0;
     if (p->n_kseg == 0) {
         if (d_kw_tail) HIPCHK(hipMemsetAsync(d_kw_tail, 0, sizeof(double) * 8 * (size_t)p->n_tracks, st));
@@ -828,9 +841,9 @@ int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, double *d_kw_tail, dou
     uint32_t *pk = wsp<uint32_t>(d_ws, p->o_pk);
     if (!p->fuse_kw)  // else the GEMV + per-segment peaks were made by k_front2 (amx_run_chunks)
         HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e, pk, st));
-    HIPCHK(amx::launch_peak_reduce(p->d_spans, p->n_tracks, p->max_nkseg, pk,
-                                   reinterpret_cast<unsigned long long *>(d_peak), p->d_ksegs,
-                                   p->Lkw, d_out, p->d_Gkw, e, p->fuse_kw, st));
+    HIPCHK(amx::launch_peak_reduce(p->d_spans, p->n_tracks, p->max_nkseg, pk, d_peak, p->d_pcnt,
+                                   p->d_ppart, p->d_ksegs, p->Lkw, d_out, p->d_Gkw, e, p->fuse_kw,
+                                   st));
     HIPCHK(amx::launch_scan(p->scan_kw(), e, s, nullptr, wsp<double>(d_ws, p->o_ebk), st));
     p->kw_rest_states = 1;   // s = the start states from rest: pass 2 without a carry reuses them
     if (d_kw_tail)
