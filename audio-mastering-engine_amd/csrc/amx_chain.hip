@@ -319,13 +319,15 @@ __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const 
     const int negm = (cd.st[0].neg ? 1 : 0) | (cd.st[3].neg ? 8 : 0);
     const float w = cd.width;
     const int won = cd.width_on;
-    __syncthreads();
+    // tiles are wave-local (tile_row LOCAL): a wave stages, computes and stores only
+    // its own 32 rows, so it never waits for the other waves of the workgroup
+    amx_wave_sync();
     TileRegs<1, ROWS> R;
-    tile_fetch<1, ROWS>(R, a16, rb_in, nullptr, rl, 0);
+    tile_fetch<1, ROWS, true>(R, a16, rb_in, nullptr, rl, 0);
     for (int k = 0; k < L; k += AMX_TF) {
-        tile_put<1, ROWS>(s_in, R, nullptr, rl, k);
-        __syncthreads();
-        if (k + AMX_TF < L) tile_fetch<1, ROWS>(R, a16, rb_in, nullptr, rl, k + AMX_TF);
+        tile_put<1, ROWS, true>(s_in, R, nullptr, rl, k);
+        amx_wave_sync();
+        if (k + AMX_TF < L) tile_fetch<1, ROWS, true>(R, a16, rb_in, nullptr, rl, k + AMX_TF);
         const uint32_t *rp = s_in + row * T::PITCH;
         uint32_t *op = s_out + row * T::PITCH;
 #pragma unroll 1
@@ -373,8 +375,9 @@ __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const 
                 }
             }
         }
-        __syncthreads();
-        tile_store<1, ROWS>(s_out, dst, rb_out, rl, k);
+        amx_wave_sync();
+        tile_store<1, ROWS, true>(s_out, dst, rb_out, rl, k);
+        amx_wave_sync();                    // s_in / s_out are rewritten by the next tile
     }
     if constexpr (MB) {
         if (need_x) {
@@ -441,9 +444,14 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_xover2(const ChainDev *__restrict
         c[5 * sc + 3] = s_c[6 * sc + 4];
         c[5 * sc + 4] = s_c[6 * sc + 5];
     }
+    // wave-local tiles (tile_row LOCAL), the next tile's loads in flight while this
+    // one is filtered
+    TileRegs<1, ROWS> R;
+    tile_fetch<1, ROWS, true>(R, p16, rb, nullptr, rl, 0);
     for (int k = 0; k < L; k += AMX_TF) {
-        tile_load<1, ROWS>(s_in, p16, rb, nullptr, rl, k);
-        __syncthreads();
+        tile_put<1, ROWS, true>(s_in, R, nullptr, rl, k);
+        amx_wave_sync();
+        if (k + AMX_TF < L) tile_fetch<1, ROWS, true>(R, p16, rb, nullptr, rl, k + AMX_TF);
         const uint32_t *rp = s_in + row * T::PITCH;
         const int o = row * T::PITCH;
 #pragma unroll 4
@@ -466,10 +474,11 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_xover2(const ChainDev *__restrict
                 s_hi[o + f] = pack2((int16_t)qh, (int16_t)oh);
             }
         }
-        __syncthreads();
-        tile_store<1, ROWS>(s_lo, bands, rb, rl, k);
-        tile_store<1, ROWS>(s_mi, bands + nloc, rb, rl, k);
-        tile_store<1, ROWS>(s_hi, bands + 2 * nloc, rb, rl, k);
+        amx_wave_sync();
+        tile_store<1, ROWS, true>(s_lo, bands, rb, rl, k);
+        tile_store<1, ROWS, true>(s_mi, bands + nloc, rb, rl, k);
+        tile_store<1, ROWS, true>(s_hi, bands + 2 * nloc, rb, rl, k);
+        amx_wave_sync();
     }
 }
 

@@ -262,14 +262,39 @@ struct Tile {
     static constexpr int WORDS = ROWS * PITCH;
     static constexpr int ITER = ROWS * ROW / AMX_BLOCK;   // dwords per thread per tile
     static constexpr int RSTEP = AMX_BLOCK / ROW;         // rows covered per iteration
+    static constexpr int RW = ROWS / (AMX_BLOCK / 64);    // rows per wave (LOCAL)
 };
+
+// Row of iteration m for this thread.  Block-wide (LOCAL false): thread t moves
+// column t % ROW of rows t / ROW + m RSTEP, so a tile needs a workgroup barrier.
+// Wave-local (LOCAL true): the wave moves exactly the RW rows it computes on
+// (rows RW w .. RW w + RW - 1, i.e. compute row = thread / (AMX_BLOCK / ROWS)), so
+// a wave only waits for itself (amx_wave_sync) and the waves of a workgroup run
+// their tiles independently.
+template <int W, int ROWS, bool LOCAL>
+__device__ __forceinline__ int tile_row(int m) {
+    using T = Tile<W, ROWS>;
+    if constexpr (LOCAL) {
+        static_assert(64 % T::ROW == 0 && T::RW * (AMX_BLOCK / 64) == ROWS, "wave-local tile rows");
+        return T::RW * (threadIdx.x >> 6) + (threadIdx.x & 63) / T::ROW + m * (64 / T::ROW);
+    } else {
+        return threadIdx.x / T::ROW + m * T::RSTEP;
+    }
+}
+
+// LDS hand-off among the lanes of one wave (its LDS operations execute in order;
+// this only keeps the compiler from moving them across)
+__device__ __forceinline__ void amx_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
 
 // Row r (< ROWS) holds frames n in [lo[r], hi[r]) at dword rb[r] + n*W (lo == nullptr
 // -> 0).  Loads are issued unconditionally from a clamped in-range address and
 // masked afterwards: a load guarded by a per-element branch makes hipcc wait
 // vmcnt(0) after every element (cdna_hip_programming.md §5 "Three .s-level traps"
 // (c)), which serialises the tile into dependent HBM round trips.
-template <int W, int ROWS = AMX_BLOCK>
+template <int W, int ROWS = AMX_BLOCK, bool LOCAL = false>
 __device__ __forceinline__ void tile_load(uint32_t *lds, const uint32_t *__restrict__ src,
                                           const int64_t *rb, const int *lo, const int *hi,
                                           int k) {
@@ -280,7 +305,7 @@ __device__ __forceinline__ void tile_load(uint32_t *lds, const uint32_t *__restr
     const int n = k + c / W;
 #pragma unroll
     for (int m = 0; m < T::ITER; m++) {
-        const int r = threadIdx.x / T::ROW + m * T::RSTEP;
+        const int r = tile_row<W, ROWS, LOCAL>(m);
         const int l0 = lo ? lo[r] : 0, h0 = hi[r];
         ok[m] = n >= l0 && n < h0;
         const int nn = ok[m] ? n : (h0 > l0 ? l0 : 0);
@@ -288,7 +313,7 @@ __device__ __forceinline__ void tile_load(uint32_t *lds, const uint32_t *__restr
     }
 #pragma unroll
     for (int m = 0; m < T::ITER; m++) {
-        const int r = threadIdx.x / T::ROW + m * T::RSTEP;
+        const int r = tile_row<W, ROWS, LOCAL>(m);
         lds[r * T::PITCH + c] = ok[m] ? v[m] : 0u;
     }
 }
@@ -302,7 +327,7 @@ struct TileRegs {
     uint32_t v[Tile<W, ROWS>::ITER];
 };
 
-template <int W, int ROWS = AMX_BLOCK>
+template <int W, int ROWS = AMX_BLOCK, bool LOCAL = false>
 __device__ __forceinline__ void tile_fetch(TileRegs<W, ROWS> &R, const uint32_t *__restrict__ src,
                                            const int64_t *rb, const int *lo, const int *hi,
                                            int k) {
@@ -311,7 +336,7 @@ __device__ __forceinline__ void tile_fetch(TileRegs<W, ROWS> &R, const uint32_t 
     const int n = k + c / W;
 #pragma unroll
     for (int m = 0; m < T::ITER; m++) {
-        const int r = threadIdx.x / T::ROW + m * T::RSTEP;
+        const int r = tile_row<W, ROWS, LOCAL>(m);
         const int l0 = lo ? lo[r] : 0, h0 = hi[r];
         const bool ok = n >= l0 && n < h0;
         const int nn = ok ? n : (h0 > l0 ? l0 : 0);
@@ -319,7 +344,7 @@ __device__ __forceinline__ void tile_fetch(TileRegs<W, ROWS> &R, const uint32_t 
     }
 }
 
-template <int W, int ROWS = AMX_BLOCK>
+template <int W, int ROWS = AMX_BLOCK, bool LOCAL = false>
 __device__ __forceinline__ void tile_put(uint32_t *lds, const TileRegs<W, ROWS> &R,
                                          const int *lo, const int *hi, int k) {
     using T = Tile<W, ROWS>;
@@ -327,13 +352,13 @@ __device__ __forceinline__ void tile_put(uint32_t *lds, const TileRegs<W, ROWS> 
     const int n = k + c / W;
 #pragma unroll
     for (int m = 0; m < T::ITER; m++) {
-        const int r = threadIdx.x / T::ROW + m * T::RSTEP;
+        const int r = tile_row<W, ROWS, LOCAL>(m);
         const int l0 = lo ? lo[r] : 0, h0 = hi[r];
         lds[r * T::PITCH + c] = (n >= l0 && n < h0) ? R.v[m] : 0u;
     }
 }
 
-template <int W, int ROWS = AMX_BLOCK>
+template <int W, int ROWS = AMX_BLOCK, bool LOCAL = false>
 __device__ __forceinline__ void tile_store(const uint32_t *lds, uint32_t *__restrict__ dst,
                                            const int64_t *rb, const int *hi, int k) {
     using T = Tile<W, ROWS>;
@@ -341,7 +366,7 @@ __device__ __forceinline__ void tile_store(const uint32_t *lds, uint32_t *__rest
     const int n = k + c / W;
 #pragma unroll
     for (int m = 0; m < T::ITER; m++) {
-        const int r = threadIdx.x / T::ROW + m * T::RSTEP;
+        const int r = tile_row<W, ROWS, LOCAL>(m);
         if (n < hi[r]) dst[rb[r] + (int64_t)n * W + (c % W)] = lds[r * T::PITCH + c];
     }
 }
