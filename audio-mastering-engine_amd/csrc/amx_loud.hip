@@ -72,8 +72,9 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_kw1(const KwSegDev *__restrict__ 
 // channel), lanes 2i / 2i+1 = L / R of row i.  parts[j][piece][ch], part_hop[j] =
 // whole-track hop index of piece 0 (a segment spans <= 2 hops).
 //
-// Loads: thread t moves column t % 16 of rows t / 16 + 16 m (m < 8) of every
-// 16-frame tile; the row pointers are formed once, so a tile costs 8 loads with
+// Loads: thread t of wave w moves column t % 16 of rows 32 w + (t % 64) / 16 + 4 m
+// (m < 8) of every 16-frame tile -- the wave's own rows, so tiles need no
+// workgroup barrier; the row pointers are formed once, so a tile costs 8 loads with
 // immediate offsets, all 8 tiles are issued up front (the recursion per tile is
 // too short to hide an HBM round trip), and only a workgroup holding a partial
 // (span-final) segment clamps addresses and masks frames (PART).
@@ -110,8 +111,8 @@ __device__ __forceinline__ void kw2_run(const uint32_t *__restrict__ const *bp, 
         const int k = q * AMX_TF;
         if (k >= L) break;
 #pragma unroll
-        for (int m = 0; m < 8; m++) s_in[(rg + 16 * m) * AMX_KW2_PITCH + c] = R[q][m];
-        __syncthreads();
+        for (int m = 0; m < 8; m++) s_in[(rg + 4 * m) * AMX_KW2_PITCH + c] = R[q][m];
+        amx_wave_sync();
         if constexpr (ALIGNED && !PART) {
             const bool lo = k < split;
             double a = lo ? acc0 : acc1;
@@ -136,7 +137,7 @@ __device__ __forceinline__ void kw2_run(const uint32_t *__restrict__ const *bp, 
                 else acc0 = fma(y, y, acc0);
             }
         }
-        __syncthreads();
+        amx_wave_sync();
     }
 }
 
@@ -173,13 +174,14 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_kw2(const ChainDev *__restrict__ 
     const int64_t h0 = sg.tframe / hop;
     const int split = (int)((h0 + 1) * hop - sg.tframe);   // first frame of piece 1
     const int part = __syncthreads_or(len < L);
-    const int c = t & 15, rg = t >> 4;
+    // wave-local rows: wave w moves (and computes on) rows 32 w .. 32 w + 31 only
+    const int c = t & 15, rg = 32 * (t >> 6) + ((t & 63) >> 4);
     const uint32_t *bp[8];
     int lm[8];
 #pragma unroll
     for (int m = 0; m < 8; m++) {
-        bp[m] = x + rb[rg + 16 * m] + c;
-        lm[m] = rl[rg + 16 * m];
+        bp[m] = x + rb[rg + 4 * m] + c;
+        lm[m] = rl[rg + 4 * m];
     }
     double acc0 = 0.0, acc1 = 0.0;
     if (part)
