@@ -158,11 +158,31 @@ __device__ __forceinline__ void front1s_run(const ChainDev &cd, const float *__r
         if (threadIdx.x < GQ) reinterpret_cast<uint4 *>(sG)[threadIdx.x] = RG;
         __syncthreads();
         if (k + AMX_TF < L) fetch(k + AMX_TF);
+        if constexpr (AN) {
+            // tanh table lookups for the whole tile first, all in flight together
+            // (one per frame per lane: lane `half` takes its own channel), written
+            // back over that channel's input word; the frame loop then reads both
+            // channels' tanh from the row (a per-frame lookup left an L2 round trip
+            // on every step of the loop)
+            uint32_t *rw = s_in + row * AMX_F1_PITCH + half;
+            float th[AMX_TF];
+#pragma unroll
+            for (int f = 0; f < AMX_TF; f++)
+                th[f] = lut[(int)q_f32_to_s16_ffmpeg(__uint_as_float(rw[2 * f])) + 32768];
+#pragma unroll
+            for (int f = 0; f < AMX_TF; f++) rw[2 * f] = __float_as_uint(th[f]);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
 #pragma unroll 1
         for (int f = 0; f < AMX_TF; f++) {
-            int16_t l = q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f]));
-            int16_t r = q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f + 1]));
-            if constexpr (AN) analog_frame(cd, lut, l, r, l, r);
+            int16_t l, r;
+            if constexpr (AN) {
+                analog_shelves(cd, __uint_as_float(rp[2 * f]), __uint_as_float(rp[2 * f + 1]), l, r);
+            } else {
+                l = q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f]));
+                r = q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f + 1]));
+            }
             if (half == 0) s_out[row * (AMX_TF + 1) + f] = pack2(l, r);
             double x0 = (double)((float)l / 32768.0f), x1 = (double)((float)r / 32768.0f);
             if constexpr (PART) {

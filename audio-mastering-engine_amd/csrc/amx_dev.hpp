@@ -51,10 +51,11 @@ __device__ __forceinline__ double sos_step(const double *c, double &z0, double &
 // lfilter along the channel axis (:264-265) = a length-2 sequence per frame.
 // tanh comes from the plan's 65536-entry table of numpy's float32 tanh over every
 // int16 input (design.py), so the result is the reference's own rounding.
-__device__ __forceinline__ void analog_frame(const ChainDev &cd, const float *__restrict__ lut,
-                                             int16_t l, int16_t r, int16_t &ol, int16_t &orr) {
-    const double x0 = (double)lut[(int)l + 32768];
-    const double x1 = (double)lut[(int)r + 32768];
+// the part after the tanh table: t0, t1 = tanh of the left / right sample
+__device__ __forceinline__ void analog_shelves(const ChainDev &cd, float t0, float t1, int16_t &ol,
+                                               int16_t &orr) {
+    const double x0 = (double)t0;
+    const double x1 = (double)t1;
     const double *b1 = cd.an_lo, *b2 = cd.an_hi;
     // first shelf (120 Hz low, +cf dB): y0 = 0 + b0*x0 ; Z0 = (0 + x0*b1) - y0*a1 ; y1 = Z0 + b0*x1
     double y0 = 0.0 + b1[0] * x0;
@@ -69,6 +70,11 @@ __device__ __forceinline__ void analog_frame(const ChainDev &cd, const float *__
     double o1 = u1 + (v1 - u1) * cd.an_ghi1;
     ol = f64_to_s16(o0);
     orr = f64_to_s16(o1);
+}
+
+__device__ __forceinline__ void analog_frame(const ChainDev &cd, const float *__restrict__ lut,
+                                             int16_t l, int16_t r, int16_t &ol, int16_t &orr) {
+    analog_shelves(cd, lut[(int)l + 32768], lut[(int)r + 32768], ol, orr);
 }
 
 // --------------------------------------------------------------- EQ chain
