@@ -556,7 +556,11 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
                                                             const uint32_t *__restrict__ bands,
                                                             uint32_t *__restrict__ out,
                                                             int64_t nloc,
-                                                            const int64_t *__restrict__ n1tab) {
+                                                            const int64_t *__restrict__ n1tab,
+                                                            const int *__restrict__ act,
+                                                            const int *__restrict__ eseg0,
+                                                            const int *__restrict__ neseg,
+                                                            int n_es, int seg_tiles) {
     __shared__ __attribute__((aligned(16))) double sm_all[AMX_GO_WAVES][64 * AMX_GO_MP];
     __shared__ __attribute__((aligned(16))) uint32_t sx_all[AMX_GO_WAVES][64 * AMX_GO_XP];
     const ChainDev &cd = *cdp;
@@ -585,10 +589,20 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
         const int64_t f = wbase + 4 * (64 * i + lane);
         xo[i] = ch.loc_off + (f < rowlen ? f : 0);
     }
+    // seg_tiles (Le == this wave's 1024 frames): a band whose envelope segment has no
+    // over-threshold frame (act == 0) has m = 0 on the whole tile -- its m is not read
+    bool mzero[3] = {false, false, false};
+    const int jt = (int)(wbase / (64 * AMX_ENV_TF_));
+    if (seg_tiles && jt < neseg[c]) {
+        const int js = eseg0[c] + jt;
+#pragma unroll
+        for (int b = 0; b < 3; b++) mzero[b] = act[(int64_t)b * n_es + js] == 0;
+    }
     d2v Mp[8];
     u4v Xp[4];
 #pragma unroll
-    for (int i = 0; i < 8; i++) Mp[i] = *reinterpret_cast<const d2v *>(mm + mo[i]);
+    for (int i = 0; i < 8; i++)
+        Mp[i] = mzero[0] ? d2v{0.0, 0.0} : *reinterpret_cast<const d2v *>(mm + mo[i]);
 #pragma unroll
     for (int i = 0; i < 4; i++) Xp[i] = *reinterpret_cast<const u4v *>(bands + xo[i]);
     uint32_t acc[AMX_ENV_TF_];
@@ -612,7 +626,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
         if (b < 2) {                                    // next band in flight
             const int64_t bo = (int64_t)(b + 1) * nloc;
 #pragma unroll
-            for (int i = 0; i < 8; i++) Mp[i] = *reinterpret_cast<const d2v *>(mm + bo + mo[i]);
+            for (int i = 0; i < 8; i++)
+                Mp[i] = mzero[b + 1] ? d2v{0.0, 0.0} : *reinterpret_cast<const d2v *>(mm + bo + mo[i]);
 #pragma unroll
             for (int i = 0; i < 4; i++) Xp[i] = *reinterpret_cast<const u4v *>(bands + bo + xo[i]);
         }
@@ -631,14 +646,29 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
         }
         __builtin_amdgcn_wave_barrier();
         double att = i0 < n ? ck[(b * nloc + ch.loc_off + i0) / AMX_ENV_TF_] : 0.0;
+        // a wave whose 1024 frames of this band start at att = 0 and have m = 0
+        // throughout holds att = 0: every frame passes unchanged (the reference's
+        // "att != 0" test), so the envelope steps and gains are skipped
+        bool busy = att != 0.0;
+#pragma unroll
+        for (int f = 0; f < AMX_ENV_TF_; f++) busy = busy || mv[f] != 0.0;
+        uint32_t gv[AMX_ENV_TF_];
+        if (__ballot(busy) == 0) {
+#pragma unroll
+            for (int f = 0; f < AMX_ENV_TF_; f++) gv[f] = xv[f];
+        } else {
+#pragma unroll
+            for (int f = 0; f < AMX_ENV_TF_; f++) {
+                att = env_step<RCP>(cd, att, i0 + f < n ? mv[f] : 0.0);
+                gv[f] = gain_frame(cd, xv[f], att);
+            }
+        }
 #pragma unroll
         for (int f = 0; f < AMX_ENV_TF_; f++) {
             const int64_t i = i0 + f;
-            att = env_step<RCP>(cd, att, i < n ? mv[f] : 0.0);
-            const uint32_t gv = gain_frame(cd, xv[f], att);
-            const int g0 = lo16(gv), g1 = hi16(gv);
+            const int g0 = lo16(gv[f]), g1 = hi16(gv[f]);
             if (b == 0) {
-                acc[f] = gv;
+                acc[f] = gv[f];
             } else if (b == 1) {
                 const bool in1 = i < n1;                // first overlay's length
                 acc[f] = in1 ? pack2(sat16(lo16(acc[f]) + g0), sat16(hi16(acc[f]) + g1)) : 0u;
@@ -718,18 +748,19 @@ hipError_t launch_envseq(const DynLaunch &d, const double *m, double *ck, double
 
 hipError_t launch_gain_overlay(const DynLaunch &d, const double *m, const double *ck,
                                const int16_t *bands, int16_t *out, int64_t max_chunk_out,
-                               const int64_t *n1tab) {
+                               const int64_t *n1tab, const int *act) {
     dim3 g((unsigned)((max_chunk_out + AMX_ENV_TF_ * AMX_BLOCK - 1) / (AMX_ENV_TF_ * AMX_BLOCK)),
            (unsigned)d.n_chunks);
     if (empty(g)) return hipSuccess;
     const uint32_t *x = reinterpret_cast<const uint32_t *>(bands);
     uint32_t *o = reinterpret_cast<uint32_t *>(out);
+    const int seg_tiles = (act && d.Le == 64 * AMX_ENV_TF_) ? 1 : 0;
     if (d.rcp)
         hipLaunchKernelGGL(k_gain_overlay<true>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, m, ck,
-                           x, o, d.nloc, n1tab);
+                           x, o, d.nloc, n1tab, act, d.eseg0, d.neseg, d.n_es, seg_tiles);
     else
         hipLaunchKernelGGL(k_gain_overlay<false>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, m, ck,
-                           x, o, d.nloc, n1tab);
+                           x, o, d.nloc, n1tab, act, d.eseg0, d.neseg, d.n_es, seg_tiles);
     return hipGetLastError();
 }
 

@@ -144,7 +144,7 @@ hipError_t launch_envseq(const DynLaunch &d, const double *m, double *ck, double
                          const int *act, const int *prev, const int *flags, int rounds);
 hipError_t launch_gain_overlay(const DynLaunch &d, const double *m, const double *ck,
                                const int16_t *bands, int16_t *out, int64_t max_chunk_out,
-                               const int64_t *n1tab);
+                               const int64_t *n1tab, const int *act);
 // loudness
 hipError_t launch_kw1(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L,
                       const int16_t *x, const double *G, double *e, uint32_t *pk,

@@ -805,7 +805,7 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
         break;
     case AMX_STAGE_APPLY:
         if (p->mb)
-            HIPCHK(amx::launch_gain_overlay(dl, mframe, ck, bands, d_out, p->max_chunk_out, p->d_n1));
+            HIPCHK(amx::launch_gain_overlay(dl, mframe, ck, bands, d_out, p->max_chunk_out, p->d_n1, eact));
         break;
     }
     return AMX_OK;
