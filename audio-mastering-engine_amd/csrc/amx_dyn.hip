@@ -299,23 +299,27 @@ __device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, d2v (&
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         const d2v v = *reinterpret_cast<const d2v *>(sm + lane * AMX_ENV_MP + 2 * i);
-        mv[2 * i] = in ? v.x : 0.0;
-        mv[2 * i + 1] = in ? v.y : 0.0;
+        mv[2 * i] = v.x;
+        mv[2 * i + 1] = v.y;
     }
     __builtin_amdgcn_wave_barrier();
     if (q == nwarm) s_spec = att;
-    if (q >= nwarm) {
-        if (in) ckr[f0 / AMX_ENV_TF] = att;
-        // the partial last tile of a chunk-final segment holds the state past the end
-        if (f0 + AMX_ENV_TF > end) {
+    // a tile outside the chunk / segment holds the state: it is skipped rather than
+    // fed zeros (the same state; no per-frame selects on the common path)
+    if (in) {
+        if (q >= nwarm) {
+            ckr[f0 / AMX_ENV_TF] = att;
+            // the partial last tile of a chunk-final segment holds the state past the end
+            if (f0 + AMX_ENV_TF > end) {
 #pragma unroll
-            for (int f = 0; f < AMX_ENV_TF; f++) mv[f] = f0 + f < end ? mv[f] : 0.0;
+                for (int f = 0; f < AMX_ENV_TF; f++) mv[f] = f0 + f < end ? mv[f] : 0.0;
+            }
+#pragma unroll
+            for (int f = 0; f < AMX_ENV_TF; f++) any |= mv[f] != 0.0;
         }
 #pragma unroll
-        for (int f = 0; f < AMX_ENV_TF; f++) any |= mv[f] != 0.0;
+        for (int f = 0; f < AMX_ENV_TF; f++) att = env_step<RCP>(cd, att, mv[f]);
     }
-#pragma unroll
-    for (int f = 0; f < AMX_ENV_TF; f++) att = env_step<RCP>(cd, att, mv[f]);
 }
 
 template <bool RCP>
