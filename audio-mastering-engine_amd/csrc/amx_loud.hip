@@ -539,109 +539,117 @@ __device__ __forceinline__ double wave_bin_value(const double (&en)[AMX_BPL], in
     return __shfl(v, j / AMX_BPL);
 }
 
-__global__ void __launch_bounds__(64) k_decide(DecideArgs a) {
-    const int t = blockIdx.x, lane = threadIdx.x;
-    const unsigned long long *H = a.hist + (int64_t)t * AMX_HIST_BINS;
-    const unsigned long long *S = a.st_hist + (int64_t)t * AMX_HIST_BINS;
+// two waves: wave 0 the integrated loudness (gating histogram), wave 1 the loudness
+// range (short-term histogram) -- independent chains of dependent reductions, run
+// side by side; wave 0's lane 0 then forms the statistics and the decision
+__global__ void __launch_bounds__(128) k_decide(DecideArgs a) {
+    const int t = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    __shared__ double s_lra;
     double I = -INFINITY, thr = -70.0, lra = 0.0;
     if (a.lufs_on) {
-        // lane l owns bins [16 l, 16 l + 16): counts, bin energies and lower bounds in
-        // registers, every load in flight before the first use (bins past 999 hold
-        // count 0 and bound +inf)
-        double hc[AMX_BPL], sc[AMX_BPL], en[AMX_BPL], bd[AMX_BPL];
+        // lane l owns bins [16 l, 16 l + 16): this wave's counts, the bin energies and
+        // lower bounds in registers, every load in flight before the first use (bins
+        // past 999 hold count 0 and bound +inf)
+        const unsigned long long *C = (wv == 0 ? a.hist : a.st_hist) + (int64_t)t * AMX_HIST_BINS;
+        double cc[AMX_BPL], en[AMX_BPL], bd[AMX_BPL];
 #pragma unroll
         for (int q = 0; q < AMX_BPL; q++) {
             const int j = lane * AMX_BPL + q;
             const int jj = j < AMX_HIST_BINS ? j : AMX_HIST_BINS - 1;
             const bool ok = j < AMX_HIST_BINS;
-            const unsigned long long h = H[jj], sh = S[jj];
+            const unsigned long long h = C[jj];
             const double e = a.energies[jj], b = a.bounds[jj];
-            hc[q] = ok ? (double)h : 0.0;
-            sc[q] = ok ? (double)sh : 0.0;
+            cc[q] = ok ? (double)h : 0.0;
             en[q] = e;
             bd[q] = ok ? b : INFINITY;
         }
         const double b0 = __shfl(bd[0], 0);
-        // integrated loudness with the relative gate (ebur128_gated_loudness)
-        double rel = 0.0, cnt = 0.0;
+        if (wv == 0) {
+            // integrated loudness with the relative gate (ebur128_gated_loudness)
+            double rel = 0.0, cnt = 0.0;
 #pragma unroll
-        for (int q = 0; q < AMX_BPL; q++) { rel += hc[q] * en[q]; cnt += hc[q]; }
-        rel = wave_sum(rel);
-        cnt = wave_sum(cnt);
-        if (cnt != 0.0) {
-            rel /= cnt;
-            rel *= 0.1;                                // pow(10, -10/10)
-            thr = lufs_of(rel);
-            int start;
-            if (rel < b0) start = 0;
-            else {
-                start = wave_find_bin(bd, rel);
-                if (rel > wave_bin_value(en, start)) ++start;
-            }
-            double g = 0.0, above = 0.0;
-#pragma unroll
-            for (int q = 0; q < AMX_BPL; q++) {
-                const bool in = lane * AMX_BPL + q >= start;
-                g += in ? hc[q] * en[q] : 0.0;
-                above += in ? hc[q] : 0.0;
-            }
-            g = wave_sum(g);
-            above = wave_sum(above);
-            if (above != 0.0) I = lufs_of(g / above);
-        }
-        // loudness range (ebur128_loudness_range) on the short-term histogram
-        double size = 0.0, power = 0.0;
-#pragma unroll
-        for (int q = 0; q < AMX_BPL; q++) { size += sc[q]; power += sc[q] * en[q]; }
-        size = wave_sum(size);
-        power = wave_sum(power);
-        if (size != 0.0) {
-            power /= size;
-            const double integ = 0.01 * power;         // pow(10, -20/10)
-            int index;
-            if (integ < b0) index = 0;
-            else {
-                index = wave_find_bin(bd, integ);
-                if (integ > wave_bin_value(en, index)) ++index;
-            }
-            double mine = 0.0;                         // this lane's counts at bins >= index
-            double cum[AMX_BPL];
-#pragma unroll
-            for (int q = 0; q < AMX_BPL; q++) {
-                mine += lane * AMX_BPL + q >= index ? sc[q] : 0.0;
-                cum[q] = mine;
-            }
-            // exclusive prefix of the lane totals (exact integer arithmetic)
-            double incl = mine;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const double up = __shfl_up(incl, o);
-                if (lane >= o) incl += up;
-            }
-            const double before = incl - mine;
-            const double tot = __shfl(incl, 63);
-            if (tot != 0.0) {
-                const double plo = (double)(int64_t)((tot - 1) * 0.1 + 0.5);
-                const double phi = (double)(int64_t)((tot - 1) * 0.95 + 0.5);
-                // the walk stops at the first bin whose cumulative count exceeds p
-                int jl = 0x7fffffff, jh = 0x7fffffff;
-#pragma unroll
-                for (int q = AMX_BPL - 1; q >= 0; q--) {
-                    const int j = lane * AMX_BPL + q;
-                    const double c = before + cum[q];
-                    const bool nz = j >= index && sc[q] != 0.0;
-                    if (nz && c > plo) jl = j;
-                    if (nz && c > phi) jh = j;
+            for (int q = 0; q < AMX_BPL; q++) { rel += cc[q] * en[q]; cnt += cc[q]; }
+            rel = wave_sum(rel);
+            cnt = wave_sum(cnt);
+            if (cnt != 0.0) {
+                rel /= cnt;
+                rel *= 0.1;                                // pow(10, -10/10)
+                thr = lufs_of(rel);
+                int start;
+                if (rel < b0) start = 0;
+                else {
+                    start = wave_find_bin(bd, rel);
+                    if (rel > wave_bin_value(en, start)) ++start;
                 }
+                double g = 0.0, above = 0.0;
 #pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    jl = min(jl, __shfl_xor(jl, o));
-                    jh = min(jh, __shfl_xor(jh, o));
+                for (int q = 0; q < AMX_BPL; q++) {
+                    const bool in = lane * AMX_BPL + q >= start;
+                    g += in ? cc[q] * en[q] : 0.0;
+                    above += in ? cc[q] : 0.0;
                 }
-                lra = lufs_of(wave_bin_value(en, jh)) - lufs_of(wave_bin_value(en, jl));
+                g = wave_sum(g);
+                above = wave_sum(above);
+                if (above != 0.0) I = lufs_of(g / above);
             }
+        } else {
+            // loudness range (ebur128_loudness_range) on the short-term histogram
+            double size = 0.0, power = 0.0;
+#pragma unroll
+            for (int q = 0; q < AMX_BPL; q++) { size += cc[q]; power += cc[q] * en[q]; }
+            size = wave_sum(size);
+            power = wave_sum(power);
+            if (size != 0.0) {
+                power /= size;
+                const double integ = 0.01 * power;         // pow(10, -20/10)
+                int index;
+                if (integ < b0) index = 0;
+                else {
+                    index = wave_find_bin(bd, integ);
+                    if (integ > wave_bin_value(en, index)) ++index;
+                }
+                double mine = 0.0;                         // this lane's counts at bins >= index
+                double cum[AMX_BPL];
+#pragma unroll
+                for (int q = 0; q < AMX_BPL; q++) {
+                    mine += lane * AMX_BPL + q >= index ? cc[q] : 0.0;
+                    cum[q] = mine;
+                }
+                // exclusive prefix of the lane totals (exact integer arithmetic)
+                double incl = mine;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const double up = __shfl_up(incl, o);
+                    if (lane >= o) incl += up;
+                }
+                const double before = incl - mine;
+                const double tot = __shfl(incl, 63);
+                if (tot != 0.0) {
+                    const double plo = (double)(int64_t)((tot - 1) * 0.1 + 0.5);
+                    const double phi = (double)(int64_t)((tot - 1) * 0.95 + 0.5);
+                    // the walk stops at the first bin whose cumulative count exceeds p
+                    int jl = 0x7fffffff, jh = 0x7fffffff;
+#pragma unroll
+                    for (int q = AMX_BPL - 1; q >= 0; q--) {
+                        const int j = lane * AMX_BPL + q;
+                        const double c = before + cum[q];
+                        const bool nz = j >= index && cc[q] != 0.0;
+                        if (nz && c > plo) jl = j;
+                        if (nz && c > phi) jh = j;
+                    }
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) {
+                        jl = min(jl, __shfl_xor(jl, o));
+                        jh = min(jh, __shfl_xor(jh, o));
+                    }
+                    lra = lufs_of(wave_bin_value(en, jh)) - lufs_of(wave_bin_value(en, jl));
+                }
+            }
+            if (lane == 0) s_lra = lra;
         }
     }
+    __syncthreads();
+    if (a.lufs_on) lra = s_lra;
     if (threadIdx.x != 0) return;
     const double pk = fmax(a.peak[2 * t], a.peak[2 * t + 1]);
     const double tp = pk > 0.0 ? 20.0 * log10(pk) : -INFINITY;
@@ -677,7 +685,7 @@ __global__ void __launch_bounds__(64) k_decide(DecideArgs a) {
 
 hipError_t launch_decide(const DecideArgs &a, hipStream_t st) {
     if (a.n_tracks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_decide, dim3(a.n_tracks), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(k_decide, dim3(a.n_tracks), dim3(128), 0, st, a);
     return hipGetLastError();
 }
 
