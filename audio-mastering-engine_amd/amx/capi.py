@@ -81,7 +81,7 @@ EXPORTS = ("amx_abi_version", "amx_last_error", "amx_plan_create", "amx_plan_fre
            "amx_plan_get_info", "amx_plan_track_span", "amx_run_chunks", "amx_run_stage",
            "amx_loudness_pass1",
            "amx_kw_propagate", "amx_loudness_pass2", "amx_loudness_histograms",
-           "amx_limiter_geometry", "amx_loudness_decide", "amx_kw_carry_setup", "amx_kw_carry",
+           "amx_limiter_geometry", "amx_limiter_prepare", "amx_loudness_decide", "amx_kw_carry_setup", "amx_kw_carry",
            "amx_finalize")
 
 _lib = None
@@ -115,6 +115,7 @@ def load(path=None):
     L.amx_loudness_histograms.argtypes = [vp, vp, ctypes.c_int64, vp, vp, vp, vp]
     L.amx_limiter_geometry.argtypes = [vp, ctypes.POINTER(FinalDesc), ctypes.POINTER(ctypes.c_int32),
                                        ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]
+    L.amx_limiter_prepare.argtypes = [vp, ctypes.POINTER(FinalDesc), ctypes.c_int32, ctypes.c_int32]
     L.amx_loudness_decide.argtypes = [vp, ctypes.POINTER(DecideDesc), ctypes.POINTER(FinalDesc),
                                       vp, vp, vp, vp, vp, vp, vp]
     L.amx_kw_carry_setup.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]
@@ -184,6 +185,12 @@ class Plan:
                                           ctypes.byref(halo), ctypes.byref(sd)),
               "amx_limiter_geometry")
         return bs.value, halo.value, sd.value
+
+    def limiter_prepare(self, fd, seg_frames=0, warm_frames=-1):
+        """General-path limiter segments (<= 0: the library default, 16384 frames) and
+        their warm-up (< 0: the library default, 3 releases + the ring)."""
+        check(load().amx_limiter_prepare(self.h, ctypes.byref(fd), int(seg_frames), int(warm_frames)),
+              "amx_limiter_prepare")
 
     def close(self):
         if getattr(self, "h", None):

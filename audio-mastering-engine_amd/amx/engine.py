@@ -42,7 +42,8 @@ def final_desc(params=ALIMITER):
 class MasteringJob:
     def __init__(self, sample_rate, channels_in, settings, track_frames, *, quantum=None,
                  input_s16=False, seg_frames=128, device=None, chunks=None, track_frame0=None,
-                 track_total=None, limiter=ALIMITER):
+                 track_total=None, limiter=ALIMITER, limiter_seg_frames=0,
+                 limiter_warm_frames=-1):
         if not torch.cuda.is_available():
             raise RuntimeError("amx needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.device = torch.device(device or "cuda")
@@ -93,6 +94,8 @@ class MasteringJob:
         self.bs, self.halo_frames, self.state_doubles = self.plan.limiter_geometry(self.fd)
         self.halo = torch.zeros((T, max(1, self.halo_frames), 2), dtype=torch.int16, device=dev)
         self.lim_state = torch.zeros((T, self.state_doubles), dtype=torch.float64, device=dev)
+        # general-path limiter segments: allocated now, never inside a graph capture
+        self.plan.limiter_prepare(self.fd, limiter_seg_frames, limiter_warm_frames)
         self.report = {}
 
     # ------------------------------------------------------------ device steps
@@ -242,7 +245,8 @@ class MasteringJob:
         return self.y[s.out_offset:s.out_offset + s.out_frames]
 
 
-def master_array(x, sample_rate, settings, *, quantum=None, seg_frames=128):
+def master_array(x, sample_rate, settings, *, quantum=None, seg_frames=128, limiter_seg_frames=0,
+                 limiter_warm_frames=-1):
     """In-memory twin of master_audio: float32 [frames, C] (C = 1/2,
     any device) -> int16 [frames', 2] CUDA tensor (the 16-bit WAV the reference
     writes) and a report dict."""
@@ -256,7 +260,8 @@ def master_array(x, sample_rate, settings, *, quantum=None, seg_frames=128):
         x = x.to(torch.float32)
     x = x.contiguous().to("cuda")
     job = MasteringJob(sample_rate, x.shape[1], settings, [x.shape[0]], quantum=quantum,
-                       input_s16=s16, seg_frames=seg_frames)
+                       input_s16=s16, seg_frames=seg_frames, limiter_seg_frames=limiter_seg_frames,
+                       limiter_warm_frames=limiter_warm_frames)
     y = job.run(x)
     job.fetch_report()
     job.report["job"] = job

@@ -127,202 +127,523 @@ __device__ __forceinline__ void final_fast_block(const SpanDev *__restrict__ spa
     }
 }
 
-// General alimiter (af_alimiter.c filter_frame, asc off), one wave per track span.
-// The recurrence is sequential and runs on lane 0 with the ring buffer, nextdelta
-// and nextpos in LDS (dynamic shared memory, 3 bs doubles); the wave loads, gains
-// and converts 64 frames at a time in parallel around it (coalesced loads and
-// stores, the per-sample gain stage off the sequential chain).  The operation
-// sequence per frame is the reference's.  State layout in `state` (doubles), for
-// the rank-to-rank hand-off: [0] att [1] delta [2] pos [3] nextiter [4] nextlen
-// [5] valid  [8 .. 8+bs) buffer  [8+bs .. 8+2bs) nextdelta  [8+2bs .. 8+3bs) nextpos.
+// ------------------------------------------------------------ general alimiter
+// af_alimiter.c filter_frame (asc off) for a track span where the limiter can
+// engage.  The recurrence is sequential; it is parallelised exactly:
+//  * Rest state.  After a release completes (the att > 1 reset) the state is
+//    att = 1, delta = 0, nextlen = nextiter = 0, nextpos[0] = -1 (entries past the
+//    list terminator are never read before they are rewritten), and the ring holds
+//    only the last B/2 input frames, which the input alone determines.  Call it
+//    IDLE.  From IDLE, frames whose peak is <= limit keep it IDLE and output the
+//    delayed input at att = 1: such stretches are skipped 64 frames per step (a
+//    wave ballot finds the next frame over the limit, lanes write the delayed
+//    outputs); only active stretches run frame by frame, the whole wave in step
+//    (the pending-peak list search 64 entries at a time), with the ring,
+//    nextdelta and nextpos in LDS.
+//  * Segments (parallel, one wave each).  The span is cut into segments of LS
+//    frames.  Segment 0 runs from the exact span start state.  Segment k > 0
+//    starts from IDLE W frames early (or from the exact span start when that is
+//    before the span), runs the warm-up without output, records its guess G_k of
+//    the state at its first frame, then runs the segment with output and records
+//    its end state E_k.  A release takes ~ release·fs frames, so the guess is
+//    exact unless the limiter stays active through the whole warm-up.
+//  * Walk (the last wave of the track to finish).  State equality is exact
+//    equality of the scalars and the live list (nextpos / nextdelta from nextiter
+//    to the terminator) at the same canonical ring positions.  If E_{k-1} == G_k,
+//    segment k ran from its true start and E_k is its true end; the walker checks
+//    64 boundaries per step.  At the first mismatch it re-runs segment k from the
+//    true state, rewriting its output, and compares the new end with G_{k+1}.
+// Output is bit-identical to the sequential filter (tests/test_gpu_parity.py).
+// State layout (doubles) of the hand-off `state` and of each G / E slot:
+// [0] att [1] delta [2] pos [3] nextiter [4] nextlen [5] valid, [8 .. 8+B) ring,
+// [8+B .. 8+2B) nextdelta, [8+2B .. 8+3B) nextpos.  Ring positions are canonical:
+// span frame f sits at (P0 + 2 f) mod B, so states of different waves compare.
 #define AMX_LIM_BATCH 64
-__device__ void final_general_wave(int t, const SpanDev *__restrict__ spans,
-                                   const uint32_t *__restrict__ x,
-                                   const uint32_t *__restrict__ halo, int halo_frames,
-                                   const double *__restrict__ gains, int fs, double level_in,
-                                   double level, double level_out, double limit, double release,
-                                   int bs, double *__restrict__ state, int64_t state_doubles,
-                                   uint32_t *__restrict__ y, double *lds) {
-    const int lane = threadIdx.x & 63;
-    const SpanDev sp = spans[t];
-    const int channels = 2;
-    double *S = state + (int64_t)t * state_doubles;
-    double *buffer = lds, *nextdelta = lds + bs, *nextposd = lds + 2 * bs;
-    double *inb = lds + 3 * bs, *outb = inb + 2 * AMX_LIM_BATCH;
-    const double g = gains[t];
-    const bool fresh = sp.tframe0 == 0 || S[5] == 0.0;
-    for (int k = lane; k < bs; k += 64) {
-        buffer[k] = fresh ? 0.0 : S[8 + k];
-        nextdelta[k] = fresh ? 0.0 : S[8 + bs + k];
-        nextposd[k] = fresh ? -1.0 : S[8 + 2 * bs + k];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    double att = 1.0, delta = 0.0;
-    int pos = 0, nextiter = 0, nextlen = 0;
-    if (lane == 0) {
-        if (fresh) {
-            if (sp.tframe0 != 0) {
-                // no carried state: prime the ring with the halo (limiter assumed idle)
-                for (int h = 0; h < halo_frames; h++) {
-                    uint32_t p = halo[(int64_t)t * halo_frames + h];
-                    for (int c = 0; c < channels; c++)
-                        buffer[pos + c] = ((double)gain16(c ? hi16(p) : lo16(p), g) * (1.0 / 32768.0)) * level_in;
-                    pos = (pos + channels) % bs;
-                }
-            }
-        } else {
-            att = S[0]; delta = S[1]; pos = (int)S[2]; nextiter = (int)S[3]; nextlen = (int)S[4];
-        }
-    }
-#define NEXTPOS(k) ((int)nextposd[(k)])
-    for (int64_t base = 0; base < sp.out_n; base += AMX_LIM_BATCH) {
-        const int nb = (int)(sp.out_n - base < AMX_LIM_BATCH ? sp.out_n - base : AMX_LIM_BATCH);
-        if (lane < nb) {
-            const uint32_t p = x[sp.out_off + base + lane];
-            for (int c = 0; c < channels; c++)
-                inb[2 * lane + c] = ((double)gain16(c ? hi16(p) : lo16(p), g) * (1.0 / 32768.0)) * level_in;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {
-            for (int k = 0; k < nb; k++) {
-                double dst[2];
-                double peak = 0;
-                for (int c = 0; c < channels; c++) {
-                    const double sample = inb[2 * k + c];
-                    buffer[pos + c] = sample;
-                    peak = fmax(peak, fabs(sample));
-                }
-                if (peak > limit) {
-                    double patt = fmin(limit / peak, 1.);
-                    double rdelta = (1.0 - patt) / (fs * release);
-                    double d = (limit / peak - att) / bs * channels;
-                    int found = 0, i;
-                    if (d < delta) {
-                        delta = d;
-                        nextposd[0] = pos;
-                        nextposd[1] = -1;
-                        nextdelta[0] = rdelta;
-                        nextlen = 1;
-                        nextiter = 0;
-                    } else {
-                        for (i = nextiter; i < nextiter + nextlen; i++) {
-                            int jx = i % bs;
-                            double ppeak = 0, pdelta;
-                            for (int c = 0; c < channels; c++) ppeak = fmax(ppeak, fabs(buffer[NEXTPOS(jx) + c]));
-                            pdelta = (limit / peak - limit / ppeak) /
-                                     (((bs - NEXTPOS(jx) + pos) % bs) / channels);
-                            if (pdelta < nextdelta[jx]) {
-                                nextdelta[jx] = pdelta;
-                                found = 1;
-                                break;
-                            }
-                        }
-                        if (found) {
-                            nextlen = i - nextiter + 1;
-                            nextposd[(nextiter + nextlen) % bs] = pos;
-                            nextdelta[(nextiter + nextlen) % bs] = rdelta;
-                            nextposd[(nextiter + nextlen + 1) % bs] = -1;
-                            nextlen++;
-                        }
-                    }
-                }
-                const double *buf = &buffer[(pos + channels) % bs];
-                peak = 0;
-                for (int c = 0; c < channels; c++) peak = fmax(peak, fabs(buf[c]));
-                att += delta;
-                for (int c = 0; c < channels; c++) dst[c] = buf[c] * att;
-                if ((pos + channels) % bs == NEXTPOS(nextiter)) {
-                    delta = nextdelta[nextiter];
-                    att = limit / peak;
-                    nextlen -= 1;
-                    nextposd[nextiter] = -1;
-                    nextiter = (nextiter + 1) % bs;
-                }
-                if (att > 1.) { att = 1.; delta = 0.; nextiter = 0; nextlen = 0; nextposd[0] = -1; }
-                if (att <= 0.) { att = 0.0000000000001; delta = (1.0 - att) / (fs * release); }
-                if (att != 1. && (1. - att) < 0.0000000000001) att = 1.;
-                if (delta != 0. && fabs(delta) < 0.00000000000001) delta = 0.;
-                for (int c = 0; c < channels; c++) outb[2 * k + c] = dst[c];
-                pos = (pos + channels) % bs;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (lane < nb) {
-            int16_t o[2];
-            for (int c = 0; c < channels; c++) {
-                double v = outb[2 * lane + c];
-                v = v < -limit ? -limit : (v > limit ? limit : v);
-                v = v * level * level_out;
-                o[c] = clip_llrint(v * 32768.0);
-            }
-            y[sp.out_off + base + lane] = pack2(o[0], o[1]);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
-#undef NEXTPOS
-    if (lane == 0) {
-        S[0] = att; S[1] = delta; S[2] = pos; S[3] = nextiter; S[4] = nextlen; S[5] = 1.0;
-    }
-    for (int k = lane; k < bs; k += 64) {
-        S[8 + k] = buffer[k];
-        S[8 + bs + k] = nextdelta[k];
-        S[8 + 2 * bs + k] = nextposd[k];
-    }
-}
 
-// One launch for both limiter paths.  Columns blockIdx.x < gridDim.x - 1 are the
-// parallel idle-limiter pass of track blockIdx.y; the last column runs the
-// sequential general limiter for that track (thread 0).  With ctl (k_decide's
-// word) each track takes exactly one of them; without it `fast` picks for all.
-struct FinalArgs {
+struct LimArgs {
     const SpanDev *spans;
     const uint32_t *x, *halo;
-    int halo_frames, fs, bs, fast;
+    int halo_frames, fs, bs, seg_frames, warm_frames, max_segs, fast;
     const double *gains;
     const int32_t *ctl;
     double level_in, level, level_out, limit, release;
-    double *state;
+    double *state;          // [tracks][state_doubles] hand-off state in / out
     int64_t state_doubles;
+    double *seg_state;      // [tracks][max_segs][2][state_doubles]: G_k, E_k
+    unsigned *cnt;          // [tracks] finished-block counters (re-armed by the walker)
+    uint32_t *y;
+};
+
+struct Lim {
+    const uint32_t *xs, *hl;    // span input (x + out_off), the track's halo row
+    uint32_t *ys;
+    int64_t n, tframe0;
+    double g, level_in, level, level_out, limit, release;
+    int fs, bs, halo, P0;
+    double *buffer, *nextdelta, *nextposd, *inb, *outb;   // LDS
+    double att, delta;          // scalar state, identical in every lane between batches
+    int nextiter, nextlen;
+};
+
+__device__ __forceinline__ double lim_sample(const Lim &L, uint32_t p, int c) {
+    return ((double)gain16(c ? hi16(p) : lo16(p), L.g) * (1.0 / 32768.0)) * L.level_in;
+}
+// ring position of span frame f (f >= -halo)
+__device__ __forceinline__ int lim_pos(const Lim &L, int64_t f) {
+    const int64_t q = ((int64_t)L.P0 + 2 * f) % L.bs;
+    return (int)(q < 0 ? q + L.bs : q);
+}
+__device__ __forceinline__ int16_t lim_out(const Lim &L, double v) {
+    v = v < -L.limit ? -L.limit : (v > L.limit ? L.limit : v);
+    v = v * L.level * L.level_out;
+    return clip_llrint(v * 32768.0);
+}
+__device__ __forceinline__ bool lim_is_idle(const Lim &L) {
+    return L.att == 1.0 && L.delta == 0.0 && L.nextlen == 0 && L.nextiter == 0 && L.nextposd[0] == -1.0;
+}
+// ring slots of span frames [max(lo, 0), hi) from the input, lanes in parallel
+__device__ void lim_reload(Lim &L, int64_t lo, int64_t hi) {
+    const int lane = threadIdx.x & 63;
+    if (lo < 0) lo = 0;
+    for (int64_t f = lo + lane; f < hi; f += 64) {
+        const uint32_t p = L.xs[f];
+        const int q = lim_pos(L, f);
+        L.buffer[q] = lim_sample(L, p, 0);
+        L.buffer[q + 1] = lim_sample(L, p, 1);
+    }
+    amx_wave_sync();
+}
+__device__ void lim_set_idle(Lim &L) {
+    for (int k = threadIdx.x & 63; k < L.bs; k += 64) {
+        L.nextdelta[k] = 0.0;
+        L.nextposd[k] = -1.0;
+    }
+    L.att = 1.0;
+    L.delta = 0.0;
+    L.nextiter = 0;
+    L.nextlen = 0;
+    amx_wave_sync();
+}
+// The span's start state, exactly as the sequential filter has it: carried in
+// `S` (valid), or fresh -- silence before the track, or the halo frames before a
+// span that starts inside it (limiter assumed idle there).
+__device__ void lim_init_span(Lim &L, const double *S) {
+    const int lane = threadIdx.x & 63;
+    const bool fresh = L.tframe0 == 0 || S[5] == 0.0;
+    for (int k = lane; k < L.bs; k += 64) {
+        L.buffer[k] = fresh ? 0.0 : S[8 + k];
+        L.nextdelta[k] = fresh ? 0.0 : S[8 + L.bs + k];
+        L.nextposd[k] = fresh ? -1.0 : S[8 + 2 * L.bs + k];
+    }
+    amx_wave_sync();
+    if (fresh) {
+        L.att = 1.0; L.delta = 0.0; L.nextiter = 0; L.nextlen = 0;
+        if (L.tframe0 != 0) {
+            for (int h = lane; h < L.halo; h += 64) {
+                const uint32_t p = L.hl[h];
+                L.buffer[2 * h] = lim_sample(L, p, 0);
+                L.buffer[2 * h + 1] = lim_sample(L, p, 1);
+            }
+        }
+    } else {
+        L.att = S[0]; L.delta = S[1]; L.nextiter = (int)S[3]; L.nextlen = (int)S[4];
+    }
+    amx_wave_sync();
+}
+__device__ __forceinline__ int lim_p0(const SpanDev &sp, const double *S, int halo, int bs) {
+    const bool fresh = sp.tframe0 == 0 || S[5] == 0.0;
+    return fresh ? (sp.tframe0 != 0 ? (2 * halo) % bs : 0) : (int)S[2];
+}
+__device__ __forceinline__ int lim_wrap(int v, int bs) { return v >= bs ? v - bs : v; }
+
+// The whole wave: frames 0..nb-1 of the batch in inb (first frame at ring
+// position pos), the reference's operation sequence per frame, every lane holding
+// the same scalars; dst to outb.  The pending-peak search (the first list entry
+// whose pdelta is below its nextdelta) evaluates 64 entries per step, one per
+// lane, each with the reference's own expression.  Stops after the first frame
+// that leaves the state IDLE (nowidle).  Returns the frames done.
+__device__ int lim_seq(Lim &L, int nb, int pos, bool &nowidle) {
+    const int lane = threadIdx.x & 63;
+    const int bs = L.bs, channels = 2;
+    const double limit = L.limit;
+    double att = L.att, delta = L.delta;
+    int nextiter = L.nextiter, nextlen = L.nextlen;
+    double *buffer = L.buffer, *nextdelta = L.nextdelta, *nextposd = L.nextposd;
+#define NEXTPOS(k) ((int)nextposd[(k)])
+    int k = 0;
+    nowidle = false;
+    while (k < nb) {
+        double dst[2];
+        double peak = 0;
+        for (int c = 0; c < channels; c++) {
+            const double sample = L.inb[2 * k + c];
+            if (lane == 0) buffer[pos + c] = sample;
+            peak = fmax(peak, fabs(sample));
+        }
+        amx_wave_sync();
+        if (peak > limit) {
+            double patt = fmin(limit / peak, 1.);
+            double rdelta = (1.0 - patt) / (L.fs * L.release);
+            double d = (limit / peak - att) / bs * channels;
+            if (d < delta) {
+                delta = d;
+                if (lane == 0) {
+                    nextposd[0] = pos;
+                    nextposd[1] = -1;
+                    nextdelta[0] = rdelta;
+                }
+                nextlen = 1;
+                nextiter = 0;
+            } else {
+                int i = -1;                          // the first entry found
+                double pfound = 0.0;
+                for (int b0 = 0; b0 < nextlen; b0 += 64) {
+                    const int e = b0 + lane;
+                    bool hit = false;
+                    double pdelta = 0.0;
+                    if (e < nextlen) {
+                        const int jx = (nextiter + e) % bs;
+                        const int np = NEXTPOS(jx);
+                        double ppeak = 0;
+                        for (int c = 0; c < channels; c++) ppeak = fmax(ppeak, fabs(buffer[np + c]));
+                        pdelta = (limit / peak - limit / ppeak) / (((bs - np + pos) % bs) / channels);
+                        hit = pdelta < nextdelta[jx];
+                    }
+                    const unsigned long long bal = __ballot(hit);
+                    if (bal) {
+                        const int l = __ffsll(bal) - 1;
+                        i = nextiter + b0 + l;
+                        pfound = __shfl(pdelta, l);
+                        break;
+                    }
+                }
+                if (i >= 0) {
+                    amx_wave_sync();
+                    if (lane == 0) nextdelta[i % bs] = pfound;
+                    nextlen = i - nextiter + 1;
+                    if (lane == 0) {
+                        nextposd[(nextiter + nextlen) % bs] = pos;
+                        nextdelta[(nextiter + nextlen) % bs] = rdelta;
+                        nextposd[(nextiter + nextlen + 1) % bs] = -1;
+                    }
+                    nextlen++;
+                }
+            }
+            amx_wave_sync();
+        }
+        const int bp = lim_wrap(pos + channels, bs);
+        const double *buf = &buffer[bp];
+        peak = 0;
+        for (int c = 0; c < channels; c++) peak = fmax(peak, fabs(buf[c]));
+        att += delta;
+        for (int c = 0; c < channels; c++) dst[c] = buf[c] * att;
+        if (bp == NEXTPOS(nextiter)) {
+            delta = nextdelta[nextiter];
+            att = limit / peak;
+            nextlen -= 1;
+            amx_wave_sync();
+            if (lane == 0) nextposd[nextiter] = -1;
+            nextiter = lim_wrap(nextiter + 1, bs);
+        }
+        if (att > 1.) {
+            att = 1.; delta = 0.; nextiter = 0; nextlen = 0;
+            amx_wave_sync();
+            if (lane == 0) nextposd[0] = -1;
+        }
+        if (att <= 0.) { att = 0.0000000000001; delta = (1.0 - att) / (L.fs * L.release); }
+        if (att != 1. && (1. - att) < 0.0000000000001) att = 1.;
+        if (delta != 0. && fabs(delta) < 0.00000000000001) delta = 0.;
+        if (lane == 0)
+            for (int c = 0; c < channels; c++) L.outb[2 * k + c] = dst[c];
+        pos = bp;
+        k++;
+        amx_wave_sync();
+        if (att == 1.0 && delta == 0.0 && nextlen == 0 && nextiter == 0 && nextposd[0] == -1.0) {
+            nowidle = true;
+            break;
+        }
+    }
+#undef NEXTPOS
+    L.att = att; L.delta = delta; L.nextiter = nextiter; L.nextlen = nextlen;
+    return k;
+}
+
+// Runs span frames [f, fend) from the state in L (idle: it is IDLE), writing the
+// output when OUT.
+template <bool OUT>
+__device__ void lim_run(Lim &L, int64_t f, int64_t fend, bool idle) {
+    const int lane = threadIdx.x & 63;
+    while (f < fend) {
+        if (idle) {
+            int64_t tgt = fend;
+            for (int64_t b = f; b < fend; b += 64) {
+                const int64_t i = b + lane;
+                bool over = false;
+                if (i < fend) {
+                    const uint32_t q = L.xs[i];
+                    over = fmax(fabs(lim_sample(L, q, 0)), fabs(lim_sample(L, q, 1))) > L.limit;
+                }
+                const unsigned long long bal = __ballot(over);
+                const int64_t stop = bal ? b + (__ffsll(bal) - 1) : min(b + 64, fend);
+                if (OUT && i < stop) {                // delayed input at att = 1
+                    const int64_t src = i - L.halo;
+                    double v0, v1;
+                    if (src >= 0) {
+                        const uint32_t q = L.xs[src];
+                        v0 = lim_sample(L, q, 0);
+                        v1 = lim_sample(L, q, 1);
+                    } else {
+                        const int r = lim_pos(L, src);
+                        v0 = L.buffer[r];
+                        v1 = L.buffer[r + 1];
+                    }
+                    L.ys[i] = pack2(lim_out(L, v0 * 1.0), lim_out(L, v1 * 1.0));
+                }
+                if (bal) { tgt = stop; break; }
+            }
+            f = tgt;
+            if (tgt == fend) break;
+            lim_reload(L, f - L.halo, f);
+            idle = false;
+        } else {
+            const int nb = (int)min((int64_t)AMX_LIM_BATCH, fend - f);
+            if (lane < nb) {
+                const uint32_t q = L.xs[f + lane];
+                L.inb[2 * lane] = lim_sample(L, q, 0);
+                L.inb[2 * lane + 1] = lim_sample(L, q, 1);
+            }
+            amx_wave_sync();
+            bool nowidle = false;
+            const int kd = lim_seq(L, nb, lim_pos(L, f), nowidle);
+            amx_wave_sync();
+            if (OUT && lane < kd)
+                L.ys[f + lane] = pack2(lim_out(L, L.outb[2 * lane]), lim_out(L, L.outb[2 * lane + 1]));
+            amx_wave_sync();
+            f += kd;
+            idle = nowidle;
+        }
+    }
+}
+
+__device__ void lim_store(const Lim &L, double *E, int64_t f_end, bool with_ring) {
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) {
+        E[0] = L.att; E[1] = L.delta; E[2] = lim_pos(L, f_end); E[3] = L.nextiter; E[4] = L.nextlen;
+        E[5] = 1.0;
+    }
+    for (int k = lane; k < L.bs; k += 64) {
+        if (with_ring) E[8 + k] = L.buffer[k];
+        E[8 + L.bs + k] = L.nextdelta[k];
+        E[8 + 2 * L.bs + k] = L.nextposd[k];
+    }
+}
+__device__ void lim_load(Lim &L, const double *E) {
+    for (int k = threadIdx.x & 63; k < L.bs; k += 64) {
+        L.nextdelta[k] = E[8 + L.bs + k];
+        L.nextposd[k] = E[8 + 2 * L.bs + k];
+    }
+    L.att = E[0]; L.delta = E[1]; L.nextiter = (int)E[3]; L.nextlen = (int)E[4];
+    amx_wave_sync();
+}
+// state equality: scalars, then the live list from nextiter to its terminator
+// (A, B: slot layout; either may be LDS-backed through the nd / np pointers)
+__device__ bool lim_equal(double a_att, double a_delta, int a_it, int a_len, const double *a_nd,
+                          const double *a_np, const double *B, int bs) {
+    if (!(a_att == B[0] && a_delta == B[1] && a_it == (int)B[3] && a_len == (int)B[4])) return false;
+    const double *b_nd = B + 8 + bs, *b_np = B + 8 + 2 * bs;
+    bool ok = true;
+    for (int i = threadIdx.x & 63; i <= a_len; i += 64) {
+        const int j = (a_it + i) % bs;
+        ok = ok && a_np[j] == b_np[j] && (i == a_len || a_nd[j] == b_nd[j]);
+    }
+    return __ballot(!ok) == 0ull;
+}
+
+// grid (min(max_segs, 2048), tracks), one wave per block; block b runs segments
+// b, b + gridDim.x, ... of its track, the last block to finish walks them.
+__global__ void __launch_bounds__(64) k_limiter(LimArgs a) {
+    extern __shared__ double lim_lds[];               // 3 B + 4 x 64 doubles
+    const int t = blockIdx.y;
+    const int lane = threadIdx.x;
+    const bool fast = a.ctl ? (a.ctl[t] & AMX_CTL_FAST) != 0 : a.fast != 0;
+    if (fast) return;                                  // block-uniform: every block of t returns
+    const SpanDev sp = a.spans[t];
+    Lim L;
+    L.xs = a.x + sp.out_off;
+    L.hl = a.halo + (int64_t)t * a.halo_frames;
+    L.ys = a.y + sp.out_off;
+    L.n = sp.out_n;
+    L.tframe0 = sp.tframe0;
+    L.g = a.gains[t];
+    L.level_in = a.level_in; L.level = a.level; L.level_out = a.level_out;
+    L.limit = a.limit; L.release = a.release;
+    L.fs = a.fs; L.bs = a.bs; L.halo = a.halo_frames;
+    L.buffer = lim_lds; L.nextdelta = lim_lds + a.bs; L.nextposd = lim_lds + 2 * a.bs;
+    L.inb = lim_lds + 3 * a.bs; L.outb = L.inb + 2 * AMX_LIM_BATCH;
+    double *S = a.state + (int64_t)t * a.state_doubles;
+    L.P0 = lim_p0(sp, S, a.halo_frames, a.bs);
+    const int LS = a.seg_frames;
+    const int nseg = (int)((sp.out_n + LS - 1) / LS);
+    const int64_t sd = a.state_doubles;
+    double *slots = a.seg_state + (int64_t)t * a.max_segs * 2 * sd;
+#define GSLOT(k) (slots + (int64_t)(k) * 2 * sd)
+#define ESLOT(k) (slots + (int64_t)(k) * 2 * sd + sd)
+
+    // 1. segments: warm-up (no output) -> G_k, segment (output) -> E_k
+    for (int s = blockIdx.x; s < nseg; s += gridDim.x) {
+        const int64_t seg0 = (int64_t)s * LS;
+        const int64_t fend = min(sp.out_n, seg0 + LS);
+        if (s > 0) {
+            const int64_t w0 = seg0 - a.warm_frames;
+            if (w0 <= 0) {
+                lim_init_span(L, S);
+                lim_run<false>(L, 0, seg0, lim_is_idle(L));
+            } else {
+                lim_set_idle(L);
+                lim_reload(L, w0 - L.halo, w0);
+                lim_run<false>(L, w0, seg0, true);
+            }
+            lim_store(L, GSLOT(s), seg0, false);
+        } else {
+            lim_init_span(L, S);
+        }
+        lim_run<true>(L, seg0, fend, lim_is_idle(L));
+        lim_store(L, ESLOT(s), fend, false);
+        amx_wave_sync();
+    }
+
+    // 2. the last block of the track walks
+    __threadfence();
+    unsigned old = 0;
+    if (lane == 0) old = atomicAdd(a.cnt + t, 1u);
+    old = __shfl(old, 0);
+    if (old != gridDim.x - 1) return;
+    __threadfence();
+    if (lane == 0) a.cnt[t] = 0u;
+    lim_init_span(L, S);                               // ring content before the span
+    bool in_lds = false;                               // true end of segment k-1 is in L
+    int k = 1;
+    while (k < nseg) {
+        if (!in_lds) {
+            // first boundary k' >= k with E_{k'-1} != G_{k'}
+            int kk = nseg;
+            for (int b = k; b < nseg && kk == nseg; b += 64) {
+                const int j = b + lane;
+                int st = 0;                            // 0 equal, 1 differs, 2 compare lists
+                if (j < nseg) {
+                    const double *E = ESLOT(j - 1), *G = GSLOT(j);
+                    if (!(E[0] == G[0] && E[1] == G[1] && E[3] == G[3] && E[4] == G[4])) st = 1;
+                    else if (E[4] != 0.0) st = 2;
+                    else {
+                        const int it = (int)E[3];
+                        st = E[8 + 2 * a.bs + it] == G[8 + 2 * a.bs + it] ? 0 : 1;
+                    }
+                }
+                unsigned long long m = __ballot(st == 2);
+                while (m) {
+                    const int l = __ffsll(m) - 1;
+                    const double *E = ESLOT(b + l - 1);
+                    const bool eq = lim_equal(E[0], E[1], (int)E[3], (int)E[4], E + 8 + a.bs,
+                                              E + 8 + 2 * a.bs, GSLOT(b + l), a.bs);
+                    if (lane == l) st = eq ? 0 : 1;
+                    m &= m - 1;
+                }
+                const unsigned long long d = __ballot(st == 1);
+                if (d) kk = b + __ffsll(d) - 1;
+            }
+            if (kk >= nseg) break;
+            k = kk;
+            lim_load(L, ESLOT(k - 1));
+        } else if (lim_equal(L.att, L.delta, L.nextiter, L.nextlen, L.nextdelta, L.nextposd,
+                             GSLOT(k), a.bs)) {
+            in_lds = false;                            // segment k ran from its true start
+            k++;
+            continue;
+        }
+        // re-run segment k from the true state in L
+        const int64_t seg0 = (int64_t)k * LS;
+        lim_reload(L, seg0 - L.halo, seg0);
+        lim_run<true>(L, seg0, min(sp.out_n, seg0 + LS), lim_is_idle(L));
+        in_lds = true;
+        k++;
+    }
+    // hand-off state at the span end: the walker's own run, else the last segment's
+    if (!in_lds && nseg > 0) lim_load(L, ESLOT(nseg - 1));
+    lim_reload(L, sp.out_n - a.bs / 2, sp.out_n);
+    lim_store(L, S, sp.out_n, true);
+#undef GSLOT
+#undef ESLOT
+}
+
+// The idle-limiter pass: blocks (x, t) of the tracks whose limiter is provably idle
+// (k_decide's AMX_CTL_FAST bit, or `fast` for every track without ctl).
+struct FinalArgs {
+    const SpanDev *spans;
+    const uint32_t *x, *halo;
+    int halo_frames, fast;
+    const double *gains;
+    const int32_t *ctl;
+    double level_in, level, level_out, limit;
     uint32_t *y;
 };
 
 template <bool UNIT>
 __global__ void __launch_bounds__(AMX_BLOCK) k_final(FinalArgs a) {
-    extern __shared__ double lim_lds[];                 // general path: 3 bs + 4 x 64 doubles
     const int t = blockIdx.y;
     const bool fast = a.ctl ? (a.ctl[t] & AMX_CTL_FAST) != 0 : a.fast != 0;
-    if (blockIdx.x + 1 < gridDim.x) {
-        if (fast)
-            final_fast_block<UNIT>(a.spans, a.x, a.halo, a.halo_frames, a.gains, a.level_in,
-                                   a.level, a.level_out, a.limit, a.y);
-    } else if (!fast && threadIdx.x < 64) {
-        final_general_wave(t, a.spans, a.x, a.halo, a.halo_frames, a.gains, a.fs, a.level_in,
-                           a.level, a.level_out, a.limit, a.release, a.bs, a.state,
-                           a.state_doubles, a.y, lim_lds);
-    }
+    if (fast)
+        final_fast_block<UNIT>(a.spans, a.x, a.halo, a.halo_frames, a.gains, a.level_in,
+                               a.level, a.level_out, a.limit, a.y);
 }
 
 // ---------------------------------------------------------------- launchers
+size_t limiter_lds_bytes(int buffer_size) {
+    return ((size_t)3 * buffer_size + 4 * AMX_LIM_BATCH) * sizeof(double);
+}
+
 hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, const int16_t *x,
                         const int16_t *halo, int halo_frames, const double *gains,
                         const int32_t *ctl, int fast, int fs, double level_in, double level,
                         double level_out, double limit, double release, int buffer_size,
-                        double *state, int64_t state_doubles, int16_t *y, hipStream_t st) {
-    const int64_t per = (int64_t)AMX_BLOCK * AMX_FINAL_FPT;
-    dim3 g((unsigned)((max_span + per - 1) / per) + 1, (unsigned)n_tracks);
+                        double *state, int64_t state_doubles, const LimScratch &ls, int16_t *y,
+                        hipStream_t st) {
     if (n_tracks <= 0) return hipSuccess;
-    FinalArgs a{spans, reinterpret_cast<const uint32_t *>(x), reinterpret_cast<const uint32_t *>(halo),
-                halo_frames, fs, buffer_size, fast, gains, ctl, level_in, level, level_out, limit,
-                release, state, state_doubles, reinterpret_cast<uint32_t *>(y)};
+    const int64_t per = (int64_t)AMX_BLOCK * AMX_FINAL_FPT;
     const bool unit = level_in == 1.0 && level_out == 1.0 && limit * 32768.0 <= 32767.0;
-    const size_t lds = ((size_t)3 * buffer_size + 4 * AMX_LIM_BATCH) * sizeof(double);
-    if (lds > 64 * 1024) return hipErrorInvalidValue;   // bs <= 2645: attack <= 13.7 ms at 96 kHz
-    if (unit) hipLaunchKernelGGL(k_final<true>, g, dim3(AMX_BLOCK), lds, st, a);
-    else hipLaunchKernelGGL(k_final<false>, g, dim3(AMX_BLOCK), lds, st, a);
+    const bool general = ctl != nullptr || !fast;
+    if (ctl != nullptr || fast) {
+        dim3 g((unsigned)((max_span + per - 1) / per), (unsigned)n_tracks);
+        FinalArgs a{spans, reinterpret_cast<const uint32_t *>(x), reinterpret_cast<const uint32_t *>(halo),
+                    halo_frames, fast, gains, ctl, level_in, level, level_out, limit,
+                    reinterpret_cast<uint32_t *>(y)};
+        if (g.x > 0) {
+            if (unit) hipLaunchKernelGGL(k_final<true>, g, dim3(AMX_BLOCK), 0, st, a);
+            else hipLaunchKernelGGL(k_final<false>, g, dim3(AMX_BLOCK), 0, st, a);
+        }
+    }
+    if (general) {
+        const size_t lds = limiter_lds_bytes(buffer_size);
+        if (lds > 64 * 1024) return hipErrorInvalidValue;   // B <= 2645: attack <= 13.7 ms at 96 kHz
+        if (!ls.seg_state || !ls.cnt || ls.buffer_size != buffer_size ||
+            ls.max_segs < 1)
+            return hipErrorInvalidValue;
+        LimArgs a{};
+        a.spans = spans;
+        a.x = reinterpret_cast<const uint32_t *>(x);
+        a.halo = reinterpret_cast<const uint32_t *>(halo);
+        a.halo_frames = halo_frames; a.fs = fs; a.bs = buffer_size;
+        a.seg_frames = ls.seg_frames; a.warm_frames = ls.warm_frames; a.max_segs = ls.max_segs;
+        a.fast = fast;
+        a.gains = gains; a.ctl = ctl;
+        a.level_in = level_in; a.level = level; a.level_out = level_out; a.limit = limit;
+        a.release = release;
+        a.state = state; a.state_doubles = state_doubles;
+        a.seg_state = ls.seg_state; a.cnt = ls.cnt;
+        a.y = reinterpret_cast<uint32_t *>(y);
+        dim3 g((unsigned)(ls.max_segs < AMX_LIM_MAX_BLOCKS ? ls.max_segs : AMX_LIM_MAX_BLOCKS),
+               (unsigned)n_tracks);
+        hipLaunchKernelGGL(k_limiter, g, dim3(64), lds, st, a);
+    }
     return hipGetLastError();
 }
 

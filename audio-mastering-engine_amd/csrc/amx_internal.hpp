@@ -159,11 +159,23 @@ hipError_t launch_hist(const SpanDev *spans, int n_tracks, int hop, const double
                        int64_t max_hops, const double *bounds, unsigned long long *hist,
                        unsigned long long *st_hist, hipStream_t st);
 // finalize
+// general alimiter scratch (plan-owned, amx_limiter_prepare): per segment of
+// seg_frames frames the guessed start state G and the end state E (warm-up of
+// warm_frames frames from rest), finished-block counters
+#define AMX_LIM_SEG_DEFAULT 16384
+#define AMX_LIM_MAX_BLOCKS 2048
+struct LimScratch {
+    double *seg_state = nullptr;   // [tracks][max_segs][2][state_doubles]
+    unsigned *cnt = nullptr;       // [tracks], zero between launches
+    int seg_frames = 0, warm_frames = 0, max_segs = 0, buffer_size = 0;
+};
+size_t limiter_lds_bytes(int buffer_size);
 hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, const int16_t *x,
                         const int16_t *halo, int halo_frames, const double *gains,
                         const int32_t *ctl, int fast, int fs, double level_in, double level,
                         double level_out, double limit, double release, int buffer_size,
-                        double *state, int64_t state_doubles, int16_t *y, hipStream_t st);
+                        double *state, int64_t state_doubles, const LimScratch &ls, int16_t *y,
+                        hipStream_t st);
 struct DecideArgs {
     int n_tracks, lufs_on;
     const unsigned long long *hist, *st_hist;

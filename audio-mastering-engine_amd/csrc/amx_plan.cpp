@@ -3,6 +3,8 @@
 #include "../../include/amx.h"
 #include "amx_internal.hpp"
 
+#include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdarg>
@@ -201,6 +203,7 @@ struct amx_plan {
     unsigned int *d_pcnt = nullptr;   // k_peak_reduce's per-track block counter (self re-arming)
     int *d_ppart = nullptr;           // its per-block partial maxima
     int any_empty_span = 0;           // a span with no K segment: its peak is zeroed directly
+    amx::LimScratch lim;              // general alimiter segments (amx_limiter_prepare)
     // workspace offsets
     size_t ws_bytes = 0;
     size_t o_a16, o_e, o_s, o_p16, o_ex, o_sx, o_bands, o_r, o_m, o_gain, o_esv, o_ee0, o_eflags, o_eact,
@@ -709,7 +712,8 @@ void amx_plan_free(amx_plan *p) {
                     p->d_kblks, p->d_n1,   p->d_G,    p->d_M,     p->d_Mp,     p->d_Gx,
                     p->d_Mx,  p->d_Mpx,    p->d_Gkw,  p->d_Mkw,   p->d_Mpkw,   p->d_tabs,
                     p->d_bounds, p->d_tailpow, p->d_lut, p->d_energies, p->d_carryP,
-                    p->d_esegs, p->d_eseg0, p->d_neseg, p->d_pcnt, p->d_ppart};
+                    p->d_esegs, p->d_eseg0, p->d_neseg, p->d_pcnt, p->d_ppart,
+                    p->lim.seg_state, p->lim.cnt};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     delete p;
@@ -910,6 +914,46 @@ int amx_limiter_geometry(const amx_plan *p, const amx_final_desc *fd, int32_t *b
     return AMX_OK;
 }
 
+int amx_limiter_prepare(amx_plan *p, const amx_final_desc *fd, int32_t seg_frames,
+                        int32_t warm_frames) {
+    if (!p || !fd) return fail(AMX_EINVAL, "null argument");
+    int32_t bs = 0, halo = 0;
+    int64_t sd = 0;
+    int rc = amx_limiter_geometry(p, fd, &bs, &halo, &sd);
+    if (rc) return rc;
+    if (seg_frames <= 0) seg_frames = p->lim.seg_frames > 0 ? p->lim.seg_frames : AMX_LIM_SEG_DEFAULT;
+    if (seg_frames < 64 || seg_frames < bs / 2)
+        return fail(AMX_EINVAL, "limiter segments of %d frames: need >= 64 and >= the ring (%d frames)",
+                    seg_frames, bs / 2);
+    if (amx::limiter_lds_bytes(bs) > 64 * 1024) return fail(AMX_EINVAL, "Attack is too large.");
+    const int64_t max_segs64 = p->max_span > 0 ? (p->max_span + seg_frames - 1) / seg_frames : 1;
+    if (max_segs64 > INT32_MAX / 2) return fail(AMX_EINVAL, "limiter: too many segments");
+    const int max_segs = (int)max_segs64;
+    if (warm_frames < 0) {
+        // three releases plus the ring: a limiter that rested anywhere in the
+        // warm-up has forgotten everything before it
+        const double rel = p->cd.fs * (fd->release_ms / 1000.0);
+        warm_frames = (int)std::min(1e9, std::ceil(3.0 * rel)) + bs / 2;
+    }
+    p->lim.warm_frames = warm_frames;
+    if (p->lim.seg_state && p->lim.buffer_size == bs && p->lim.seg_frames == seg_frames &&
+        p->lim.max_segs == max_segs)
+        return AMX_OK;
+    const int T = p->n_tracks > 0 ? p->n_tracks : 1;
+    if (p->lim.seg_state) (void)hipFree(p->lim.seg_state);
+    if (p->lim.cnt) (void)hipFree(p->lim.cnt);
+    p->lim = amx::LimScratch{};
+    p->lim.warm_frames = warm_frames;
+    HIPCHK(hipMalloc(&p->lim.seg_state, (size_t)T * max_segs * 2 * sd * sizeof(double)));
+    HIPCHK(hipMalloc(&p->lim.cnt, (size_t)T * sizeof(unsigned)));
+    HIPCHK(hipMemset(p->lim.cnt, 0, (size_t)T * sizeof(unsigned)));
+    HIPCHK(hipDeviceSynchronize());
+    p->lim.seg_frames = seg_frames;
+    p->lim.max_segs = max_segs;
+    p->lim.buffer_size = bs;
+    return AMX_OK;
+}
+
 int amx_loudness_decide(amx_plan *p, const amx_decide_desc *dd, const amx_final_desc *fd,
                         const uint64_t *d_hist, const uint64_t *d_st_hist, const double *d_peak,
                         double *d_stats, double *d_gains, int32_t *d_ctl, void *stream) {
@@ -974,9 +1018,15 @@ int amx_finalize(amx_plan *p, const amx_final_desc *fd, const int16_t *d_x,
     hipStream_t st = (hipStream_t)stream;
     const double level = fd->auto_level ? 1 / fd->limit : 1;
     if ((d_ctl || !fast) && !d_lim_state) return fail(AMX_EINVAL, "general limiter needs d_lim_state");
+    if ((d_ctl || !fast) && (!p->lim.seg_state || p->lim.buffer_size != bs)) {
+        // not captured into a graph: amx_limiter_prepare allocates (callers that
+        // capture call it first)
+        rc = amx_limiter_prepare(p, fd, 0, -1);
+        if (rc) return rc;
+    }
     HIPCHK(amx::launch_final(p->d_spans, p->n_tracks, p->max_span, d_x, d_halo, halo, d_gains, d_ctl,
                              fast ? 1 : 0, p->cd.fs, fd->level_in, level, fd->level_out, fd->limit,
-                             fd->release_ms / 1000.0, bs, d_lim_state, sd, d_y, st));
+                             fd->release_ms / 1000.0, bs, d_lim_state, sd, p->lim, d_y, st));
     return AMX_OK;
 }
 

@@ -199,6 +199,16 @@ AMX_API int amx_loudness_histograms(amx_plan *plan, const double *d_hops, int64_
  * doubles per track for the general path. */
 AMX_API int amx_limiter_geometry(const amx_plan *plan, const amx_final_desc *fd, int32_t *buffer_size,
                          int32_t *halo_frames, int64_t *state_doubles);
+/* General-path alimiter scratch, plan-owned.  The span is cut into segments of
+ * seg_frames frames (<= 0: 16384, or the last value set; >= 64 and >= the ring
+ * frames); each segment warms up from the limiter's rest state over warm_frames
+ * frames before it (< 0: 3 releases + the ring), runs in parallel, and an in-order
+ * walk re-runs any segment whose guessed start state differs from the true one
+ * (amx_final.hip).  Allocates device memory: call it before capturing
+ * amx_finalize into a graph (amx_finalize calls it itself otherwise).  Replaces
+ * no reference line: it sizes the parallel form of the alimiter at :223. */
+AMX_API int amx_limiter_prepare(amx_plan *plan, const amx_final_desc *fd, int32_t seg_frames,
+                                int32_t warm_frames);
 /* Loudnorm decision on the device (af_loudnorm pass-1 statistics + pass-2 mode,
  * :229-242): per track, from the histograms and sample peak:
  *   d_stats [n_tracks][16] doubles: I, LRA, thresh, TP(dB), the same four after

@@ -205,6 +205,58 @@ def test_limiter_general_path(gpu, oracle_mod):
     _cmp(y.cpu().numpy(), ref, "limiter general", exact_min=1.0, tol=0)
 
 
+def _bursts(n, fs, seed):
+    """Quiet music with loud square bursts of random length (2 ms - 400 ms) at
+    random places: limiting episodes of every length, some spanning segment
+    boundaries, some back to back."""
+    from amx import synth
+    rng = np.random.default_rng(seed)
+    x = synth.music_like(n, fs, 2, seed=seed, peak_dbfs=-12.0)
+    t = 0
+    while True:
+        t += int(rng.integers(fs // 100, fs // 2))
+        ln = int(rng.integers(fs // 500, fs * 2 // 5))
+        if t + ln >= n:
+            break
+        x[t:t + ln] = synth.square(ln, fs, 2, freq=float(rng.uniform(60, 900)), amp=float(rng.uniform(0.9, 1.0)))
+        t += ln
+    return x
+
+
+@pytest.mark.parametrize("fs,signal,seconds,lseg,warm", [
+    (48000, "music", 20.0, 512, -1), (48000, "music", 20.0, 0, -1), (48000, "music", 20.0, 2048, 0),
+    (48000, "bursts", 20.0, 512, -1), (48000, "bursts", 20.0, 4096, 0), (48000, "bursts", 20.0, 1024, 300),
+    (96000, "bursts", 8.0, 512, -1), (96000, "bursts", 8.0, 1024, 0), (44100, "square", 2.0, 256, -1),
+    (44100, "square", 2.0, 256, 0), (48000, "square", 0.3, 512, -1),
+])
+def test_limiter_segments_vs_oracle(gpu, oracle_mod, fs, signal, seconds, lseg, warm):
+    """General alimiter (:223) run as warmed-up segments + in-order check and repair:
+    bit-exact to the sequential oracle for loud music (frequent short episodes),
+    square bursts (episodes of every length across segment boundaries), a
+    continuous square (the limiter never rests) and a span shorter than one
+    segment.  lseg 0 / warm -1 = the library defaults; warm 0 (segments guess the
+    rest state at their first frame) and a short warm-up make most guesses wrong,
+    so the walker's re-runs and state comparisons carry the result."""
+    import torch
+    from amx import synth
+    from amx.chunking import chunk_bounds
+    from amx.engine import master_array
+    n = int(fs * seconds)
+    if signal == "music":
+        x = synth.music_like(n, fs, 2, seed=7, peak_dbfs=3.0)
+    elif signal == "square":
+        x = synth.square(n, fs, 2, freq=110.0, amp=1.0)
+    else:
+        x = _bursts(n, fs, seed=int(seconds * 10) + fs)
+    settings = dict(lufs=None)       # no EQ: the EQ shelves here pull the peaks under the limit
+    y, rep = master_array(torch.from_numpy(x), fs, settings, quantum=512, limiter_seg_frames=lseg,
+                          limiter_warm_frames=warm)
+    assert rep["limiter_fast"] is False
+    ref, _ = oracle_mod.pipeline(oracle_mod.quantize(x), fs, settings, chunk_bounds(n, fs, 512))
+    _cmp(y.cpu().numpy(), ref, "limiter %s fs=%d lseg=%d warm=%d" % (signal, fs, lseg, warm),
+         exact_min=1.0, tol=0)
+
+
 def test_silence_skips_normalisation(gpu, oracle_mod):
     import torch
     from amx.engine import master_array
