@@ -459,14 +459,11 @@ __device__ bool lim_equal(double a_att, double a_delta, int a_it, int a_len, con
     return __ballot(!ok) == 0ull;
 }
 
-// grid (min(max_segs, 2048), tracks), one wave per block; block b runs segments
-// b, b + gridDim.x, ... of its track, the last block to finish walks them.
-__global__ void __launch_bounds__(64) k_limiter(LimArgs a) {
-    extern __shared__ double lim_lds[];               // 3 B + 4 x 64 doubles
+// Wave 0 of general block bx of nbx (columns of k_final): runs segments bx,
+// bx + nbx, ... of track blockIdx.y; the last block to finish walks them.
+__device__ void limiter_block(const LimArgs &a, int bx, int nbx, double *lim_lds) {
     const int t = blockIdx.y;
     const int lane = threadIdx.x;
-    const bool fast = a.ctl ? (a.ctl[t] & AMX_CTL_FAST) != 0 : a.fast != 0;
-    if (fast) return;                                  // block-uniform: every block of t returns
     const SpanDev sp = a.spans[t];
     Lim L;
     L.xs = a.x + sp.out_off;
@@ -490,7 +487,7 @@ __global__ void __launch_bounds__(64) k_limiter(LimArgs a) {
 #define ESLOT(k) (slots + (int64_t)(k) * 2 * sd + sd)
 
     // 1. segments: warm-up (no output) -> G_k, segment (output) -> E_k
-    for (int s = blockIdx.x; s < nseg; s += gridDim.x) {
+    for (int s = bx; s < nseg; s += nbx) {
         const int64_t seg0 = (int64_t)s * LS;
         const int64_t fend = min(sp.out_n, seg0 + LS);
         if (s > 0) {
@@ -517,7 +514,7 @@ __global__ void __launch_bounds__(64) k_limiter(LimArgs a) {
     unsigned old = 0;
     if (lane == 0) old = atomicAdd(a.cnt + t, 1u);
     old = __shfl(old, 0);
-    if (old != gridDim.x - 1) return;
+    if (old != (unsigned)nbx - 1) return;
     __threadfence();
     if (lane == 0) a.cnt[t] = 0u;
     lim_init_span(L, S);                               // ring content before the span
@@ -575,25 +572,28 @@ __global__ void __launch_bounds__(64) k_limiter(LimArgs a) {
 #undef ESLOT
 }
 
-// The idle-limiter pass: blocks (x, t) of the tracks whose limiter is provably idle
-// (k_decide's AMX_CTL_FAST bit, or `fast` for every track without ctl).
+// One launch for both limiter paths of every track: columns x < fast_cols are
+// the idle-limiter pass, the gen_cols after them the general limiter (wave 0 of
+// each, limiter_block).  With ctl (k_decide's word) each track takes exactly one
+// of them; without it `fast` picks for all.
 struct FinalArgs {
-    const SpanDev *spans;
-    const uint32_t *x, *halo;
-    int halo_frames, fast;
-    const double *gains;
-    const int32_t *ctl;
-    double level_in, level, level_out, limit;
-    uint32_t *y;
+    LimArgs lim;
+    int fast_cols, gen_cols;
 };
 
 template <bool UNIT>
-__global__ void __launch_bounds__(AMX_BLOCK) k_final(FinalArgs a) {
+__global__ void __launch_bounds__(AMX_BLOCK) k_final(FinalArgs fa) {
+    extern __shared__ double lim_lds[];               // general columns: 3 B + 4 x 64 doubles
+    const LimArgs &a = fa.lim;
     const int t = blockIdx.y;
     const bool fast = a.ctl ? (a.ctl[t] & AMX_CTL_FAST) != 0 : a.fast != 0;
-    if (fast)
-        final_fast_block<UNIT>(a.spans, a.x, a.halo, a.halo_frames, a.gains, a.level_in,
-                               a.level, a.level_out, a.limit, a.y);
+    if ((int)blockIdx.x < fa.fast_cols) {
+        if (fast)
+            final_fast_block<UNIT>(a.spans, a.x, a.halo, a.halo_frames, a.gains, a.level_in,
+                                   a.level, a.level_out, a.limit, a.y);
+    } else if (!fast && threadIdx.x < 64) {
+        limiter_block(a, (int)blockIdx.x - fa.fast_cols, fa.gen_cols, lim_lds);
+    }
 }
 
 // ---------------------------------------------------------------- launchers
@@ -611,39 +611,32 @@ hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, co
     const int64_t per = (int64_t)AMX_BLOCK * AMX_FINAL_FPT;
     const bool unit = level_in == 1.0 && level_out == 1.0 && limit * 32768.0 <= 32767.0;
     const bool general = ctl != nullptr || !fast;
-    if (ctl != nullptr || fast) {
-        dim3 g((unsigned)((max_span + per - 1) / per), (unsigned)n_tracks);
-        FinalArgs a{spans, reinterpret_cast<const uint32_t *>(x), reinterpret_cast<const uint32_t *>(halo),
-                    halo_frames, fast, gains, ctl, level_in, level, level_out, limit,
-                    reinterpret_cast<uint32_t *>(y)};
-        if (g.x > 0) {
-            if (unit) hipLaunchKernelGGL(k_final<true>, g, dim3(AMX_BLOCK), 0, st, a);
-            else hipLaunchKernelGGL(k_final<false>, g, dim3(AMX_BLOCK), 0, st, a);
-        }
-    }
+    FinalArgs fa{};
+    LimArgs &a = fa.lim;
+    a.spans = spans;
+    a.x = reinterpret_cast<const uint32_t *>(x);
+    a.halo = reinterpret_cast<const uint32_t *>(halo);
+    a.halo_frames = halo_frames; a.fs = fs; a.bs = buffer_size; a.fast = fast;
+    a.gains = gains; a.ctl = ctl;
+    a.level_in = level_in; a.level = level; a.level_out = level_out; a.limit = limit;
+    a.release = release;
+    a.state = state; a.state_doubles = state_doubles;
+    a.y = reinterpret_cast<uint32_t *>(y);
+    fa.fast_cols = (ctl != nullptr || fast) ? (int)((max_span + per - 1) / per) : 0;
+    size_t lds = 0;
     if (general) {
-        const size_t lds = limiter_lds_bytes(buffer_size);
+        lds = limiter_lds_bytes(buffer_size);
         if (lds > 64 * 1024) return hipErrorInvalidValue;   // B <= 2645: attack <= 13.7 ms at 96 kHz
-        if (!ls.seg_state || !ls.cnt || ls.buffer_size != buffer_size ||
-            ls.max_segs < 1)
+        if (!ls.seg_state || !ls.cnt || ls.buffer_size != buffer_size || ls.max_segs < 1)
             return hipErrorInvalidValue;
-        LimArgs a{};
-        a.spans = spans;
-        a.x = reinterpret_cast<const uint32_t *>(x);
-        a.halo = reinterpret_cast<const uint32_t *>(halo);
-        a.halo_frames = halo_frames; a.fs = fs; a.bs = buffer_size;
         a.seg_frames = ls.seg_frames; a.warm_frames = ls.warm_frames; a.max_segs = ls.max_segs;
-        a.fast = fast;
-        a.gains = gains; a.ctl = ctl;
-        a.level_in = level_in; a.level = level; a.level_out = level_out; a.limit = limit;
-        a.release = release;
-        a.state = state; a.state_doubles = state_doubles;
         a.seg_state = ls.seg_state; a.cnt = ls.cnt;
-        a.y = reinterpret_cast<uint32_t *>(y);
-        dim3 g((unsigned)(ls.max_segs < AMX_LIM_MAX_BLOCKS ? ls.max_segs : AMX_LIM_MAX_BLOCKS),
-               (unsigned)n_tracks);
-        hipLaunchKernelGGL(k_limiter, g, dim3(64), lds, st, a);
+        fa.gen_cols = ls.max_segs < AMX_LIM_MAX_BLOCKS ? ls.max_segs : AMX_LIM_MAX_BLOCKS;
     }
+    dim3 g((unsigned)(fa.fast_cols + fa.gen_cols), (unsigned)n_tracks);
+    if (g.x == 0) return hipSuccess;
+    if (unit) hipLaunchKernelGGL(k_final<true>, g, dim3(AMX_BLOCK), lds, st, fa);
+    else hipLaunchKernelGGL(k_final<false>, g, dim3(AMX_BLOCK), lds, st, fa);
     return hipGetLastError();
 }
 
