@@ -98,6 +98,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=300.0)
     ap.add_argument("--seg-frames", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true", help="skip the double-buffered host rate")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from the host")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm); gloo only to rehearse N ranks on one GPU")
@@ -173,6 +174,29 @@ def main():
         host_incl = {"value": round(samples_total / e2e / 1e6, 3), "unit": "Msamples/s",
                      "ms_per_step": round(e2e * 1e3, 4),
                      "what": "pinned H2D of the f32 input + the step + D2H of the int16 output"}
+        # the same, double-buffered (amx.stream_io.TrackStream): H2D of track i+1, the
+        # step of track i and D2H of track i-1 overlap on three streams; for f32 input
+        # and for an s16 WAV input (half the H2D bytes)
+        if not args.no_pipeline:
+            from amx.stream_io import TrackStream
+            host_incl["pipelined"] = {}
+            del h_in
+            for kind, s16 in (("f32", False), ("s16", True)):
+                ts = TrackStream(fs, 2, settings, per_rank, depth=2, input_s16=s16, quantum=512,
+                                 seg_frames=args.seg_frames)
+                hi = ts.pinned_input()
+                hi.copy_(torch.from_numpy(synth.to_s16(x)) if s16 else torch.from_numpy(x))
+                outs = [ts.pinned_output() for _ in range(2)]
+                n_tr = max(4, args.steps)
+                ts.run([hi] * 2, outs)                        # warm-up
+                t1 = time.perf_counter()
+                ts.run([hi] * n_tr, [outs[i % 2] for i in range(n_tr)])
+                e2p = (time.perf_counter() - t1) / n_tr
+                host_incl["pipelined"][kind] = {
+                    "value": round(samples_total / e2p / 1e6, 3), "ms_per_track": round(e2p * 1e3, 4),
+                    "tracks": n_tr, "h2d_bytes": int(hi.numel() * hi.element_size()),
+                    "d2h_bytes": int(outs[0].numel() * 2)}
+                del ts, hi, outs
 
     # per-stage device time: the same K steps again with HIP events bracketing each
     # stage on the launch stream (kept out of the timed region above)

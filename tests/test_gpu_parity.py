@@ -325,3 +325,33 @@ def test_full_size_c3_5min(gpu, oracle_mod):
     ref, info = oracle_mod.pipeline(oracle_mod.quantize(x), fs, C3, chunk_bounds(n, fs, 512))
     assert rep["stats"][0] == info["stats"]
     _cmp(y.cpu().numpy(), ref, "C3 5 min")
+
+
+@pytest.mark.parametrize("s16", [False, True])
+def test_track_stream_matches_single_jobs(gpu, s16):
+    """Double-buffered host pipeline (amx.stream_io.TrackStream, §8f row 2): five
+    tracks through two resident jobs on three streams give, track by track, the
+    output and loudnorm statistics of a single job run on that track alone."""
+    import torch
+    from amx import synth
+    from amx.engine import MasteringJob
+    from amx.stream_io import TrackStream
+    fs, n = 48000, 48000 * 7
+    xs = [synth.mix_like(n, fs, 2, seed=40 + i) for i in range(5)]
+    if s16:
+        xs = [synth.to_s16(x) for x in xs]
+    ts = TrackStream(fs, 2, C3, n, depth=2, input_s16=s16, quantum=512)
+    h_ins = []
+    for x in xs:
+        h = ts.pinned_input()
+        h.copy_(torch.from_numpy(x))
+        h_ins.append(h)
+    outs = [ts.pinned_output() for _ in xs]
+    stats = [ts.pinned_stats() for _ in xs]
+    ts.run(h_ins, outs, stats)
+    for i, x in enumerate(xs):
+        job = MasteringJob(fs, 2, C3, [n], quantum=512, input_s16=s16)
+        y = job.run(torch.from_numpy(x).cuda())
+        torch.cuda.synchronize()
+        assert torch.equal(y.cpu(), outs[i]), "track %d output" % i
+        assert torch.equal(job.stats.cpu(), stats[i]), "track %d stats" % i
