@@ -164,6 +164,7 @@ struct LimArgs {
     const SpanDev *spans;
     const uint32_t *x, *halo;
     int halo_frames, fs, bs, seg_frames, warm_frames, max_segs, fast;
+    int64_t warm_cap;
     const double *gains;
     const int32_t *ctl;
     double level_in, level, level_out, limit, release;
@@ -368,6 +369,35 @@ __device__ int lim_seq(Lim &L, int nb, int pos, bool &nowidle) {
     return k;
 }
 
+// Warm-up start for the segment at seg0: the latest frame w0 <= seg0 whose R
+// frames before it are all at or under the limit (then the limiter has almost
+// surely come to rest by w0), found by scanning back 64 frames per ballot; at
+// most `cap` frames back.  Returns <= 0 when the scan reaches the span start.
+__device__ int64_t lim_warm_start(const Lim &L, int64_t seg0, int64_t R, int64_t cap) {
+    const int lane = threadIdx.x & 63;
+    int64_t w0 = seg0;
+    const int64_t floor_ = seg0 - cap;
+    int64_t b = w0;                                   // scan [.., b) downwards
+    while (true) {
+        if (w0 <= 0) return 0;
+        if (w0 <= floor_) return w0;
+        if (b <= w0 - R || b <= 0) return w0;          // [w0 - R, w0) is clean
+        const int64_t i = b - 64 + lane;
+        bool over = false;
+        if (i >= 0 && i >= w0 - R) {
+            const uint32_t q = L.xs[i];
+            over = fmax(fabs(lim_sample(L, q, 0)), fabs(lim_sample(L, q, 1))) > L.limit;
+        }
+        const unsigned long long bal = __ballot(over);
+        if (bal) {
+            w0 = b - 64 + (63 - __clzll(bal));          // the latest frame over the limit
+            b = w0;
+        } else {
+            b -= 64;
+        }
+    }
+}
+
 // Runs span frames [f, fend) from the state in L (idle: it is IDLE), writing the
 // output when OUT.
 template <bool OUT>
@@ -491,7 +521,7 @@ __device__ void limiter_block(const LimArgs &a, int bx, int nbx, double *lim_lds
         const int64_t seg0 = (int64_t)s * LS;
         const int64_t fend = min(sp.out_n, seg0 + LS);
         if (s > 0) {
-            const int64_t w0 = seg0 - a.warm_frames;
+            const int64_t w0 = lim_warm_start(L, seg0, a.warm_frames, a.warm_cap);
             if (w0 <= 0) {
                 lim_init_span(L, S);
                 lim_run<false>(L, 0, seg0, lim_is_idle(L));
@@ -630,6 +660,7 @@ hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, co
         if (!ls.seg_state || !ls.cnt || ls.buffer_size != buffer_size || ls.max_segs < 1)
             return hipErrorInvalidValue;
         a.seg_frames = ls.seg_frames; a.warm_frames = ls.warm_frames; a.max_segs = ls.max_segs;
+        a.warm_cap = ls.warm_cap;
         a.seg_state = ls.seg_state; a.cnt = ls.cnt;
         fa.gen_cols = ls.max_segs < AMX_LIM_MAX_BLOCKS ? ls.max_segs : AMX_LIM_MAX_BLOCKS;
     }

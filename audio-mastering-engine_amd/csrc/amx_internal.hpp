@@ -168,6 +168,7 @@ struct LimScratch {
     double *seg_state = nullptr;   // [tracks][max_segs][2][state_doubles]
     unsigned *cnt = nullptr;       // [tracks], zero between launches
     int seg_frames = 0, warm_frames = 0, max_segs = 0, buffer_size = 0;
+    int64_t warm_cap = 0;          // furthest warm-up start before a segment, frames
 };
 size_t limiter_lds_bytes(int buffer_size);
 hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, const int16_t *x,

@@ -936,14 +936,19 @@ int amx_limiter_prepare(amx_plan *p, const amx_final_desc *fd, int32_t seg_frame
         warm_frames = (int)std::min(1e9, std::ceil(3.0 * rel)) + bs / 2;
     }
     p->lim.warm_frames = warm_frames;
+    // warm-ups reach back over active stretches up to 10 s (longer ones are left to
+    // the in-order repair); warm_frames 0 disables the search (tests)
+    p->lim.warm_cap = warm_frames > 0 ? (int64_t)p->cd.fs * 10 : 0;
     if (p->lim.seg_state && p->lim.buffer_size == bs && p->lim.seg_frames == seg_frames &&
         p->lim.max_segs == max_segs)
         return AMX_OK;
     const int T = p->n_tracks > 0 ? p->n_tracks : 1;
     if (p->lim.seg_state) (void)hipFree(p->lim.seg_state);
     if (p->lim.cnt) (void)hipFree(p->lim.cnt);
+    const int64_t cap = p->lim.warm_cap;
     p->lim = amx::LimScratch{};
     p->lim.warm_frames = warm_frames;
+    p->lim.warm_cap = cap;
     HIPCHK(hipMalloc(&p->lim.seg_state, (size_t)T * max_segs * 2 * sd * sizeof(double)));
     HIPCHK(hipMalloc(&p->lim.cnt, (size_t)T * sizeof(unsigned)));
     HIPCHK(hipMemset(p->lim.cnt, 0, (size_t)T * sizeof(unsigned)));
