@@ -133,6 +133,28 @@ def _worker(rank, world, port, spans):
             st.mul_(10.0).add_(rank + 1)
         adist.chain_state(st, run, rank, world)
         assert order[0] == ([0.0] * 3 if rank == 0 else [float(sum((q + 1) * 10 ** (rank - 1 - q) for q in range(rank)))] * 3)
+
+        # 5. speculative hand-off: every rank runs from rest first; a rank re-runs only
+        # when the state it receives is not the rest state.  Toy limiter on the real
+        # state layout (B = 4): rank 0 ends at rest when `rest0`, else with att = 0.5;
+        # ranks > 0 end at rest.
+        bs = 4
+        for rest0 in (True, False):
+            sv = torch.zeros(8 + 3 * bs, dtype=torch.float64)
+            seen = []
+
+            def lim_run():
+                seen.append(float(sv[0]))
+                sv.zero_()
+                sv[5] = 1.0
+                sv[8 + 2 * bs:] = -1.0
+                sv[0] = 1.0 if (rank > 0 or rest0) else 0.5
+            adist.chain_state_speculative(sv, lim_run, lambda v: adist.is_rest_state(v, bs), rank, world)
+            if rank == 0:
+                assert seen == [0.0]                      # one run, from nothing carried
+            else:
+                assert seen == ([0.0] if rest0 else [0.0, 0.5])   # re-run from the received state
+            assert adist.is_rest_state(sv, bs) == (rank > 0 or rest0)
     finally:
         dist.destroy_process_group()
 

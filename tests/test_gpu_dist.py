@@ -22,17 +22,22 @@ CASES = {
     "c3_lufs": dict(bass_boost=-1.0, mid_cut=2.0, presence_boost=2.5, treble_boost=1.0,
                     lufs=-14.0, width=1.3, analog_character=40.0, **MB),
     "loud_limiter": dict(width=1.5),       # no EQ stage (the EQ lowers the level): clips
+    # a full-scale square: the limiter never comes to rest, so rank 1's first run (from
+    # rest) is wrong and it must re-run from the state rank 0 hands it
+    "square_limiter": dict(),
 }
 
 
 # input gain per case: the loud case drives 0.1 % of the frames over the limit, so the final
 # alimiter (limit 0.98) must engage and the ranks hand its state along
-GAIN = {"c3_lufs": 1.0, "loud_limiter": 1.3}
+GAIN = {"c3_lufs": 1.0, "loud_limiter": 1.3, "square_limiter": 1.0}
 
 
 def _track(seconds, case):
     from amx import synth
     n = int(FS * seconds)
+    if case == "square_limiter":
+        return synth.square(n, FS, 2, freq=110.0, amp=1.0)
     return (synth.mix_like(n, FS, 2, seed=3) * np.float32(GAIN[case])).astype(np.float32)
 
 
@@ -78,7 +83,7 @@ def test_two_ranks_match_one(gpu, case):
     from amx.dist import ShardedTrack
     # 3 chunks -> ranks own 2 + 1; the sequential-limiter case 2 chunks (that path walks
     # every frame in order)
-    seconds = 75.0 if case != "loud_limiter" else 32.0
+    seconds = 75.0 if case == "c3_lufs" else 32.0
     x = _track(seconds, case)
     one = ShardedTrack(FS, 2, CASES[case], x.shape[0], 0, 1, quantum=512)
     y1 = one.step(torch.from_numpy(np.ascontiguousarray(x)).cuda()).cpu().numpy()
@@ -89,7 +94,7 @@ def test_two_ranks_match_one(gpu, case):
     y2 = np.concatenate(parts)
     assert fast[0] == fast[1]
     # the loud case must exercise the rank-to-rank sequential limiter
-    assert fast[0] == (case != "loud_limiter"), "limiter fast path %s" % fast[0]
+    assert fast[0] == (case == "c3_lufs"), "limiter fast path %s" % fast[0]
     assert y2.shape == y1.shape
     diff = np.abs(y2.astype(np.int32) - y1.astype(np.int32))
     assert diff.max() == 0, "max |diff| %d LSB at %s (limiter fast path %s)" % (
