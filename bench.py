@@ -267,6 +267,27 @@ def main():
                                 "sample": "full workload: 1 pass of the %.0f s track through the C "
                                           "oracle (oracle/amx_oracle.c), single thread" % args.seconds,
                                 "seconds": round(dt, 3)}
+        # all-cores variant: the chunks are independent (:185-204), so a
+        # thread pool runs the oracle's chunk chain on them at once (ctypes releases the
+        # GIL); loudness, gain and the alimiter stay serial, as in the reference
+        threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1,
+                             len(c)))
+        from concurrent.futures import ThreadPoolExecutor
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            outs = list(ex.map(lambda sn: oracle.chunk(x16[sn[0]:sn[0] + sn[1]], fs, settings), c))
+        cat = np.concatenate(outs, axis=0)
+        yy = cat
+        if settings.get("lufs") is not None:
+            mode, g = oracle.loudnorm_linear_gain(oracle.loudnorm_measure(cat, fs), float(settings["lufs"]))
+            if mode == "linear":
+                yy = oracle.linear_gain(cat, g)
+        ref_p = oracle.alimiter(yy, fs)
+        dtp = time.perf_counter() - t0
+        line["cpu_baseline"]["all_cores"] = {
+            "value": round(x16.shape[0] * 2 / dtp / 1e6, 3), "cores": threads, "seconds": round(dtp, 3),
+            "what": "chunk chains on a thread pool, loudness + alimiter serial",
+            "same_output": bool(np.array_equal(ref_p, ref))}
         y = job.y[:job.info.out_frames].cpu().numpy()
         d = np.abs(y.astype(np.int32) - ref.astype(np.int32))
         line["parity_vs_oracle"] = {"max_abs_lsb": int(d.max()), "exact_frac": float((d == 0).mean())}
