@@ -257,6 +257,30 @@ def test_limiter_segments_vs_oracle(gpu, oracle_mod, fs, signal, seconds, lseg, 
          exact_min=1.0, tol=0)
 
 
+def test_batch_general_limiter_vs_oracle(gpu, oracle_mod):
+    """Several tracks in one plan with settings lufs None: two loud tracks of
+    different lengths take the general limiter (per-track segment slots and
+    counters in the same launch), a quiet one the idle path; each equals the
+    oracle's pipeline on that track alone."""
+    import torch
+    from amx import synth
+    from amx.chunking import chunk_bounds
+    from amx.engine import MasteringJob
+    fs = 48000
+    settings = dict(lufs=None)
+    xs = [_bursts(int(fs * 9.0), fs, seed=5), synth.music_like(int(fs * 4.0), fs, 2, seed=6, peak_dbfs=-9.0),
+          synth.music_like(int(fs * 13.7), fs, 2, seed=7, peak_dbfs=3.0)]
+    job = MasteringJob(fs, 2, settings, [x.shape[0] for x in xs], quantum=512, limiter_seg_frames=2048)
+    job.run(torch.from_numpy(np.ascontiguousarray(np.concatenate(xs))).cuda())
+    rep = job.fetch_report()
+    fast = [bool(int(v) & 1) for v in job.ctl.cpu().tolist()]
+    assert fast == [False, True, False], fast
+    for t, x in enumerate(xs):
+        ref, _ = oracle_mod.pipeline(oracle_mod.quantize(x), fs, settings, chunk_bounds(x.shape[0], fs, 512))
+        _cmp(job.track_output(t).cpu().numpy(), ref, "batch general limiter track %d" % t,
+             exact_min=1.0, tol=0)
+
+
 def test_silence_skips_normalisation(gpu, oracle_mod):
     import torch
     from amx.engine import master_array
