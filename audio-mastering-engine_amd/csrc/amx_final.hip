@@ -257,13 +257,25 @@ __device__ __forceinline__ int lim_p0(const SpanDev &sp, const double *S, int ha
 }
 __device__ __forceinline__ int lim_wrap(int v, int bs) { return v >= bs ? v - bs : v; }
 
-// The whole wave: frames 0..nb-1 of the batch in inb (first frame at ring
-// position pos), the reference's operation sequence per frame, every lane holding
-// the same scalars; dst to outb.  The pending-peak search (the first list entry
-// whose pdelta is below its nextdelta) evaluates 64 entries per step, one per
-// lane, each with the reference's own expression.  Stops after the first frame
-// that leaves the state IDLE (nowidle).  Returns the frames done.
-__device__ int lim_seq(Lim &L, int nb, int pos, bool &nowidle) {
+__device__ __forceinline__ double lim_readlane(double v, int k) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, k);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// The whole wave, frames f .. f+nb-1 (first frame at ring position pos): the
+// reference's operation sequence per frame, every lane holding the same scalars.
+// Lane k holds frame f+k's samples (s0, s1) and the delayed samples the ring
+// returns for it (d0, d1: frame f+k-halo -- the ring only ever holds input
+// samples), read by the wave with readlane, so a frame without list work makes no
+// LDS round trip; `head` caches nextpos[nextiter].  The ring is still written
+// (the list search reads it).  The pending-peak search evaluates 64 entries per
+// step, one per lane, each with the reference's own expression.  Lane k keeps
+// frame k's dst in o0, o1.  Stops after the first frame that leaves the state
+// IDLE (nowidle).  Returns the frames done.
+__device__ int lim_seq(Lim &L, int nb, int pos, double s0v, double s1v, double d0v, double d1v,
+                       double &o0, double &o1, bool &nowidle) {
     const int lane = threadIdx.x & 63;
     const int bs = L.bs, channels = 2;
     const double limit = L.limit;
@@ -271,18 +283,18 @@ __device__ int lim_seq(Lim &L, int nb, int pos, bool &nowidle) {
     int nextiter = L.nextiter, nextlen = L.nextlen;
     double *buffer = L.buffer, *nextdelta = L.nextdelta, *nextposd = L.nextposd;
 #define NEXTPOS(k) ((int)nextposd[(k)])
+    int head = NEXTPOS(nextiter);
     int k = 0;
     nowidle = false;
     while (k < nb) {
-        double dst[2];
-        double peak = 0;
-        for (int c = 0; c < channels; c++) {
-            const double sample = L.inb[2 * k + c];
-            if (lane == 0) buffer[pos + c] = sample;
-            peak = fmax(peak, fabs(sample));
+        const double x0 = lim_readlane(s0v, k), x1 = lim_readlane(s1v, k);
+        if (lane == 0) {
+            buffer[pos] = x0;
+            buffer[pos + 1] = x1;
         }
-        amx_wave_sync();
+        double peak = fmax(fmax(0.0, fabs(x0)), fabs(x1));
         if (peak > limit) {
+            amx_wave_sync();
             double patt = fmin(limit / peak, 1.);
             double rdelta = (1.0 - patt) / (L.fs * L.release);
             double d = (limit / peak - att) / bs * channels;
@@ -331,40 +343,46 @@ __device__ int lim_seq(Lim &L, int nb, int pos, bool &nowidle) {
                 }
             }
             amx_wave_sync();
+            head = NEXTPOS(nextiter);
         }
         const int bp = lim_wrap(pos + channels, bs);
-        const double *buf = &buffer[bp];
-        peak = 0;
-        for (int c = 0; c < channels; c++) peak = fmax(peak, fabs(buf[c]));
+        const double b0 = lim_readlane(d0v, k), b1 = lim_readlane(d1v, k);
+        peak = fmax(fmax(0.0, fabs(b0)), fabs(b1));
         att += delta;
-        for (int c = 0; c < channels; c++) dst[c] = buf[c] * att;
-        if (bp == NEXTPOS(nextiter)) {
+        const double dst0 = b0 * att, dst1 = b1 * att;
+        if (bp == head) {
+            amx_wave_sync();
             delta = nextdelta[nextiter];
             att = limit / peak;
             nextlen -= 1;
             amx_wave_sync();
             if (lane == 0) nextposd[nextiter] = -1;
             nextiter = lim_wrap(nextiter + 1, bs);
+            amx_wave_sync();
+            head = NEXTPOS(nextiter);
         }
         if (att > 1.) {
             att = 1.; delta = 0.; nextiter = 0; nextlen = 0;
             amx_wave_sync();
             if (lane == 0) nextposd[0] = -1;
+            head = -1;
         }
         if (att <= 0.) { att = 0.0000000000001; delta = (1.0 - att) / (L.fs * L.release); }
         if (att != 1. && (1. - att) < 0.0000000000001) att = 1.;
         if (delta != 0. && fabs(delta) < 0.00000000000001) delta = 0.;
-        if (lane == 0)
-            for (int c = 0; c < channels; c++) L.outb[2 * k + c] = dst[c];
+        if (lane == k) {
+            o0 = dst0;
+            o1 = dst1;
+        }
         pos = bp;
         k++;
-        amx_wave_sync();
-        if (att == 1.0 && delta == 0.0 && nextlen == 0 && nextiter == 0 && nextposd[0] == -1.0) {
+        if (att == 1.0 && delta == 0.0 && nextlen == 0 && nextiter == 0 && head == -1) {
             nowidle = true;
             break;
         }
     }
 #undef NEXTPOS
+    amx_wave_sync();
     L.att = att; L.delta = delta; L.nextiter = nextiter; L.nextlen = nextlen;
     return k;
 }
@@ -437,18 +455,26 @@ __device__ void lim_run(Lim &L, int64_t f, int64_t fend, bool idle) {
             idle = false;
         } else {
             const int nb = (int)min((int64_t)AMX_LIM_BATCH, fend - f);
+            double s0 = 0.0, s1 = 0.0, d0 = 0.0, d1 = 0.0;
             if (lane < nb) {
                 const uint32_t q = L.xs[f + lane];
-                L.inb[2 * lane] = lim_sample(L, q, 0);
-                L.inb[2 * lane + 1] = lim_sample(L, q, 1);
+                s0 = lim_sample(L, q, 0);
+                s1 = lim_sample(L, q, 1);
+                const int64_t src = f + lane - L.halo;
+                if (src >= 0) {
+                    const uint32_t qd = L.xs[src];
+                    d0 = lim_sample(L, qd, 0);
+                    d1 = lim_sample(L, qd, 1);
+                } else {                             // before the span: the initial ring
+                    const int r = lim_pos(L, src);
+                    d0 = L.buffer[r];
+                    d1 = L.buffer[r + 1];
+                }
             }
-            amx_wave_sync();
             bool nowidle = false;
-            const int kd = lim_seq(L, nb, lim_pos(L, f), nowidle);
-            amx_wave_sync();
-            if (OUT && lane < kd)
-                L.ys[f + lane] = pack2(lim_out(L, L.outb[2 * lane]), lim_out(L, L.outb[2 * lane + 1]));
-            amx_wave_sync();
+            double o0 = 0.0, o1 = 0.0;
+            const int kd = lim_seq(L, nb, lim_pos(L, f), s0, s1, d0, d1, o0, o1, nowidle);
+            if (OUT && lane < kd) L.ys[f + lane] = pack2(lim_out(L, o0), lim_out(L, o1));
             f += kd;
             idle = nowidle;
         }
@@ -612,7 +638,7 @@ struct FinalArgs {
 };
 
 template <bool UNIT>
-__global__ void __launch_bounds__(AMX_BLOCK) k_final(FinalArgs fa) {
+__global__ void __launch_bounds__(AMX_BLOCK, 8) k_final(FinalArgs fa) {
     extern __shared__ double lim_lds[];               // general columns: 3 B + 4 x 64 doubles
     const LimArgs &a = fa.lim;
     const int t = blockIdx.y;
