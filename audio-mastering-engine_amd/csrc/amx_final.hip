@@ -319,7 +319,10 @@ __device__ int lim_seq(Lim &L, int nb, int pos, double s0v, double s1v, double d
                         const int np = NEXTPOS(jx);
                         double ppeak = 0;
                         for (int c = 0; c < channels; c++) ppeak = fmax(ppeak, fabs(buffer[np + c]));
-                        pdelta = (limit / peak - limit / ppeak) / (((bs - np + pos) % bs) / channels);
+                        const int dist = ((bs - np + pos) % bs) / channels;
+                        // equal peaks: the reference's (A - A) / dist is exactly +0 (dist >
+                        // 0), so a steady over-limit stretch needs no division here
+                        pdelta = (ppeak == peak && dist > 0) ? 0.0 : (limit / peak - limit / ppeak) / dist;
                         hit = pdelta < nextdelta[jx];
                     }
                     const unsigned long long bal = __ballot(hit);
