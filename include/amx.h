@@ -243,8 +243,10 @@ AMX_API int amx_kw_carry(amx_plan *plan, const double *d_tails, double *d_carry,
  * amx_loudness_decide) each track takes the path its AMX_CTL_FAST bit selects, on the
  * device; with d_ctl NULL, fast != 0 selects the idle path for every track.  The idle
  * path (max|gained sample| <= limit) is an exact delay + level; otherwise the
- * sequential limiter runs, and d_lim_state [n_tracks][state_doubles] carries its state
- * in (span not starting the track) and out (span end). */
+ * general limiter runs (parallel segments + in-order repair, bit-identical to the
+ * sequential filter; scratch from amx_limiter_prepare), and d_lim_state
+ * [n_tracks][state_doubles] carries its state in (span not starting the track) and out
+ * (span end). */
 AMX_API int amx_finalize(amx_plan *plan, const amx_final_desc *fd, const int16_t *d_x,
                  const double *d_gains, const int32_t *d_ctl, int32_t fast, const int16_t *d_halo,
                  int16_t *d_y, double *d_lim_state, void *d_ws, void *stream);
