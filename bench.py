@@ -29,7 +29,11 @@ MB = dict(multiband=True, low_thresh=-25.0, low_ratio=6.0, mid_thresh=-20.0, mid
 CONFIGS = {
     "c2": dict(VOCAL, lufs=-14.0),
     "c3": dict(VOCAL, lufs=-14.0, width=1.3, analog_character=40.0, **MB),
+    "c5": dict(VOCAL, lufs=-14.0, width=1.3, analog_character=40.0, **MB),
 }
+# sample rate and default length per config (BASELINE.json configs; C5 = 60 min at 96 kHz)
+CONFIG_FS = {"c2": 48000, "c3": 48000, "c5": 96000}
+CONFIG_SECONDS = {"c2": 300.0, "c3": 300.0, "c5": 3600.0}
 
 
 def stage_bytes(stage, frames, ch_in, mb):
@@ -95,7 +99,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--seconds", type=float, default=300.0)
+    ap.add_argument("--seconds", type=float, default=None, help="per GPU (default: the config's)")
     ap.add_argument("--seg-frames", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true", help="skip the double-buffered host rate")
@@ -118,7 +122,9 @@ def main():
     if world > 1:
         torch.cuda.set_device(0 if args.one_device else local)
         dist.init_process_group(args.dist_backend)
-    fs = 48000
+    fs = CONFIG_FS[args.config]
+    if args.seconds is None:
+        args.seconds = CONFIG_SECONDS[args.config]
     settings = CONFIGS[args.config]
     per_rank = int(args.seconds * fs)
     total = per_rank * world
@@ -228,7 +234,9 @@ def main():
         "config": {"workload": "configs[1]: 5 min stereo 48 kHz f32 per GPU, EQ 'Vocal Clarity' + "
                                "loudnorm -14 LUFS (linear) + alimiter; N GPUs = one N x 5 min track, "
                                "chunk-sharded" if args.config == "c2" else
-                               "configs[2]: C2 + multiband + width 1.3 + analog 40",
+                               ("configs[2]: C2 + multiband + width 1.3 + analog 40" if args.config == "c3"
+                                else "configs[4]: 60 min stereo 96 kHz f32 per GPU, C3 settings"),
+                   "sample_rate": fs,
                    "settings": args.config, "seconds_per_gpu": args.seconds,
                    "seg_frames": args.seg_frames, "parallelism": "chunk-shard x%d" % world,
                    "launch": ("hipGraph replay" if world == 1 else "hipGraph segments + eager collectives")
