@@ -101,6 +101,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--seconds", type=float, default=None, help="per GPU (default: the config's)")
     ap.add_argument("--seg-frames", type=int, default=128)
+    ap.add_argument("--env-warm", type=int, default=None,
+                    help="compressor envelope warm-up frames (default: the plan's, 2048)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true", help="skip the double-buffered host rate")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from the host")
@@ -126,6 +128,8 @@ def main():
     if args.seconds is None:
         args.seconds = CONFIG_SECONDS[args.config]
     settings = CONFIGS[args.config]
+    if args.env_warm is not None:
+        settings = dict(settings, _env_warm=int(args.env_warm))
     per_rank = int(args.seconds * fs)
     total = per_rank * world
     track = ShardedTrack(fs, 2, settings, total, rank, world, quantum=512,
