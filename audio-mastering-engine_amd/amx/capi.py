@@ -82,7 +82,8 @@ EXPORTS = ("amx_abi_version", "amx_last_error", "amx_plan_create", "amx_plan_fre
            "amx_loudness_pass1",
            "amx_kw_propagate", "amx_loudness_pass2", "amx_loudness_histograms",
            "amx_limiter_geometry", "amx_limiter_prepare", "amx_loudness_decide", "amx_kw_carry_setup", "amx_kw_carry",
-           "amx_finalize")
+           "amx_finalize", "amx_env_counters", "amx_pcm_to_s16")
+PCM_FORMATS = {"u8": 0, "s16": 1, "s24": 2, "s32": 3, "f32": 4, "f64": 5}
 
 _lib = None
 
@@ -110,6 +111,8 @@ def load(path=None):
     L.amx_run_chunks.argtypes = [vp, vp, vp, vp, vp]
     L.amx_run_stage.argtypes = [vp, ctypes.c_int32, vp, vp, vp, vp]
     L.amx_loudness_pass1.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.amx_pcm_to_s16.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, vp, vp]
+    L.amx_env_counters.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]
     L.amx_kw_propagate.argtypes = [vp, ctypes.c_int64, c_double_p, c_double_p]
     L.amx_loudness_pass2.argtypes = [vp, vp, vp, vp, ctypes.c_int64, vp, vp]
     L.amx_loudness_histograms.argtypes = [vp, vp, ctypes.c_int64, vp, vp, vp, vp]
@@ -139,6 +142,13 @@ def ptr(t):
     if t is None:
         return None
     return ctypes.c_void_p(t.data_ptr())
+
+
+def ptr_stream(stream=None):
+    """hipStream_t of a torch stream (default: the current one) for the C ABI."""
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
 
 
 class Plan:

@@ -159,15 +159,18 @@ def is_rest_state(s, bs):
                 and s[8 + 2 * bs] == -1.0)
 
 
-def chain_state_speculative(state, run, is_rest, rank, world, group=None):
+def chain_state_speculative(state, run, is_rest, rank, world, group=None, first_run_done=False):
     """Limiter hand-off with the ranks' work in parallel.  Every rank first runs its
     span from the rest state (state zeroed = nothing carried: the span's ring comes
     from the halo and the limiter is assumed at rest), all at once.  Then the true
     end states travel rank to rank: a rank whose received state is the rest state
     already has its exact output and end state; otherwise it re-runs from the
-    received state.  Only the small state messages stay sequential."""
-    state.zero_()
-    run()
+    received state.  Only the small state messages stay sequential.
+    first_run_done: the from-rest run already happened (the N > 1 graph runs it on
+    the device's own decision), so only the hand-off and re-runs remain."""
+    if not first_run_done:
+        state.zero_()
+        run()
     if world == 1:
         return
     (s,), st = _staged(group, state)
@@ -296,9 +299,16 @@ class ShardedTrack:
         # the limiter is launched on the device's own decision (k_decide's word): the
         # idle path is then complete without a host round trip; when the limiter can
         # engage, replay() re-runs it as the rank-to-rank sequential chain
-        fin = lambda: job.finalize(None)
+        # the limiter state is zeroed in the graph, so when the device picks the general
+        # limiter the in-graph run IS the speculative from-rest run of
+        # chain_state_speculative: replay() then only hands the end states along
+        def fin():
+            job.lim_state.zero_()
+            job.finalize(None)
         g3 = seg(job.histograms, job.decide, fin) if lufs_on else seg(job.decide, fin)
         self._g = [g1, g2, g3]
+        self._ctl_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self._ctl_ev = torch.cuda.Event()
         return self._g
 
     def replay(self):
@@ -316,9 +326,18 @@ class ShardedTrack:
         if job.dd.lufs_on:
             reduce_loudness(job.hops, None, self.group)
         g3.replay()
-        if not (int(job.ctl[0].item()) & capi.CTL_FAST):
-            job.lim_state.zero_()
-            self.limiter_sequential()
+        # The one host read of the step: RCCL operations are enqueued by the host, so
+        # only the host can decide whether the limiter's rank-to-rank hand-off runs.
+        # The word is the same on every rank (computed from all-reduced data); when it
+        # says "idle" (the common case) the step is already complete on the device.
+        # Only this 4-byte copy is waited for, on the launch stream.
+        self._ctl_host.copy_(job.ctl[:1], non_blocking=True)
+        self._ctl_ev.record()
+        self._ctl_ev.synchronize()
+        if not (int(self._ctl_host[0]) & capi.CTL_FAST):
+            chain_state_speculative(job.lim_state, lambda: job.finalize(False),
+                                    lambda v: is_rest_state(v, job.bs), self.rank, self.world,
+                                    self.group, first_run_done=True)
         return job.y[:job.info.out_frames]
 
     def _limit(self, capi):
@@ -358,3 +377,45 @@ class ShardedTrack:
             self._finish(capi)
         job.report = {"chunks": len(job.chunks), "segments": job.info.n_segments}
         return job.y[:job.info.out_frames]
+
+
+class ShardedBatch:
+    """This rank's share of a batch of whole tracks (BASELINE configs[3], C4: 64 tracks
+    over 8 GPUs).  Tracks are dealt to ranks as contiguous runs balanced by frames
+    (shard_tracks); loudness and the limiter are per track, so a batch needs no
+    exchange at all: each rank runs one MasteringJob over its tracks, laid back to
+    back in its input buffer, every track chunked exactly as on its own
+    (audio_mastering_engine.py:178)."""
+
+    def __init__(self, sample_rate, channels_in, settings, track_frames, rank, world, *,
+                 quantum=None, input_s16=False, seg_frames=128):
+        self.rank, self.world = rank, world
+        fs = int(sample_rate)
+        if quantum is None:
+            quantum = packet_frames(channels_in * (2 if input_s16 else 4))
+        self.track_frames = [int(n) for n in track_frames]
+        self.ranges = shard_tracks(self.track_frames, world)
+        t0, t1 = self.ranges[rank]
+        self.tracks = list(range(t0, t1))
+        mine = self.track_frames[t0:t1]
+        self.local_frames = sum(mine)
+        self.in0 = sum(self.track_frames[:t0])
+        mb = bool(settings.get("multiband"))
+        self.track_bounds = [chunk_bounds(n, fs, quantum) for n in self.track_frames]
+        out_t = [sum(chunk_out_frames(n, fs, mb) for _, n in b) for b in self.track_bounds]
+        self.span_frames = [sum(out_t[a:b]) for a, b in self.ranges]
+        self.job = MasteringJob(fs, channels_in, settings, mine, quantum=quantum,
+                                input_s16=input_s16, seg_frames=seg_frames)
+
+    def step(self, d_in):
+        """One pass of the whole path over this rank's tracks (input resident)."""
+        y = self.job.run(d_in)
+        self.job.report = {"chunks": len(self.job.chunks), "segments": self.job.info.n_segments,
+                           "tracks": len(self.tracks)}
+        return y
+
+    def capture(self, d_in):
+        return self.job.capture(d_in)
+
+    def replay(self):
+        return self.job.replay()

@@ -55,11 +55,6 @@ class MasteringJob:
         self.desc.input_s16 = 1 if input_s16 else 0
         if quantum is None:
             quantum = packet_frames(self.channels_in * (2 if input_s16 else 4))
-        # int16 frames are read as one dword per stereo frame; mono int16 is
-        # duplicated to stereo on the device before the chain (-ac 2, :190)
-        self._mono_s16 = self.input_s16 and self.channels_in == 1
-        if self._mono_s16:
-            self.desc.channels_in = 2
         self.track_frames = [int(n) for n in track_frames]
         self.chunks = chunks if chunks is not None else plan_tracks(self.track_frames, self.fs, quantum)
         self.plan = capi.Plan(self.desc, self.chunks, track_frame0, track_total, seg_frames)
@@ -112,8 +107,6 @@ class MasteringJob:
         need = max((off + n for (_, off, n) in self.chunks), default=0)
         if d_in.numel() < need * self.channels_in:
             raise ValueError("d_in holds %d samples, plan needs %d" % (d_in.numel(), need * self.channels_in))
-        if self._mono_s16:
-            d_in = d_in.reshape(-1, 1).expand(-1, 2).contiguous()
         L = capi.load()
         ev = getattr(self, "stage_events", None)
         if ev is None:
@@ -181,6 +174,18 @@ class MasteringJob:
                                             capi.ptr(self.lim_state), capi.ptr(self.ws), self._s(stream)),
                    "amx_finalize")
 
+    def env_counters(self):
+        """Compressor fix-up diagnostics of the last step (amx_env_counters), per round:
+        segments re-run, longest chain of dependent re-runs in one wave, waves with
+        work, longest round-0 look-back (64-segment steps).  Synchronous."""
+        import ctypes
+        n = 16 * 4
+        buf = (ctypes.c_int32 * n)()
+        capi.check(capi.load().amx_env_counters(self.plan.h, capi.ptr(self.ws), buf, n), "amx_env_counters")
+        rows = [list(buf[4 * r:4 * r + 4]) for r in range(16)]
+        keys = ("reruns", "max_chain", "waves", "lookback")
+        return [dict(zip(keys, r)) for r in rows if any(r)]
+
     # ------------------------------------------------------------ report
     def fetch_report(self, raise_dynamic=True):
         """Synchronise and read the device decision back: loudnorm statistics as the
@@ -210,12 +215,12 @@ class MasteringJob:
         round trip); returns y (int16 [frames, 2]).  fetch_report() reads the
         loudness decision afterwards."""
         self.run_chunks(d_in, stream)
-        self.loudness_pass1(stream, tail=False)
+        self.timed("loud1", lambda: self.loudness_pass1(stream, tail=False), stream)
         if self.dd.lufs_on:
-            self.loudness_pass2(stream, carry=False)
-            self.histograms(stream)
-        self.decide(stream)
-        self.finalize(None, stream)
+            self.timed("loud2", lambda: self.loudness_pass2(stream, carry=False), stream)
+            self.timed("hist", lambda: self.histograms(stream), stream)
+        self.timed("decide", lambda: self.decide(stream), stream)
+        self.timed("final", lambda: self.finalize(None, stream), stream)
         self.report = {"chunks": len(self.chunks), "segments": self.info.n_segments}
         return self.y[:self.info.out_frames]
 

@@ -70,6 +70,12 @@ class TrackStream:
         for h in h_outs:
             if not h.is_pinned() or tuple(h.shape) != (self.out_frames, 2) or h.dtype != torch.int16:
                 raise ValueError("outputs must be pinned int16 [%d, 2] tensors" % self.out_frames)
+        if h_stats is None:
+            # statistics rows always come back: the mode word is checked below
+            shape = (len(h_ins),) + tuple(self.jobs[0].stats.shape)
+            if getattr(self, "_rows", None) is None or self._rows.shape[0] < shape[0]:
+                self._rows = torch.empty(shape, dtype=torch.float64).pin_memory()
+            h_stats = [self._rows[i] for i in range(len(h_ins))]
         cur = torch.cuda.current_stream()
         for s in (self.s_in, self.s_comp, self.s_out):
             s.wait_stream(cur)
@@ -101,4 +107,10 @@ class TrackStream:
         for s in (self.s_in, self.s_comp, self.s_out):
             cur.wait_stream(s)
         torch.cuda.synchronize()
+        # the device decided each track's loudnorm mode; a track that needs dynamic mode
+        # must not pass as mastered (its gain would silently be "none")
+        for i, r in enumerate(h_stats):
+            if int(r.reshape(-1, r.shape[-1])[:, 8].max()) == 3:
+                from .engine import DynamicModeUnsupported
+                raise DynamicModeUnsupported("track %d: loudnorm would use dynamic mode" % i)
         return h_outs

@@ -17,11 +17,10 @@ class WavInfo:
         return self.channels * self.bits // 8
 
 
-def read_wav_native(path):
-    """Returns (array [frames, channels] in the file's own sample type, WavInfo).
+PCM_CODE = {(1, 8): "u8", (1, 16): "s16", (1, 24): "s24", (1, 32): "s32", (3, 32): "f32", (3, 64): "f64"}
 
-    PCM 8 -> uint8, 16 -> int16, 24 -> int32 (sign-extended 24-bit value),
-    32 -> int32; IEEE float -> float32/float64."""
+
+def _parse(path):
     with open(path, "rb") as f:
         data = f.read()
     if data[:4] != b"RIFF" or data[8:12] != b"WAVE":
@@ -40,6 +39,29 @@ def read_wav_native(path):
         pos += 8 + size + (size & 1)
     if fmt is None or payload is None:
         raise ValueError("WAV without fmt/data chunk: %s" % path)
+    if fmt.block_align <= 0:
+        raise ValueError("WAV with a zero block size: %s" % path)
+    return fmt, payload
+
+
+def read_wav_raw(path):
+    """(payload bytes as a uint8 array of whole frames, WavInfo, PCM code) -- the
+    file's samples untouched, for the device decode (amx_pcm_to_s16)."""
+    fmt, payload = _parse(path)
+    code = PCM_CODE.get((fmt.fmt_tag, fmt.bits))
+    if code is None:
+        raise ValueError("unsupported WAV format tag %d / %d bits" % (fmt.fmt_tag, fmt.bits))
+    n = len(payload) // fmt.block_align
+    raw = np.frombuffer(payload, np.uint8, count=n * fmt.block_align)
+    return raw, fmt, code
+
+
+def read_wav_native(path):
+    """Returns (array [frames, channels] in the file's own sample type, WavInfo).
+
+    PCM 8 -> uint8, 16 -> int16, 24 -> int32 (sign-extended 24-bit value),
+    32 -> int32; IEEE float -> float32/float64."""
+    fmt, payload = _parse(path)
     n = len(payload) // fmt.block_align
     raw = payload[:n * fmt.block_align]
     if fmt.fmt_tag == 3:
@@ -108,6 +130,39 @@ def write_wav_f32(path, x, fs):
     raw = x.tobytes()
     hdr = b"RIFF" + struct.pack("<I", 36 + len(raw)) + b"WAVE"
     hdr += b"fmt " + struct.pack("<IHHIIHH", 16, 3, ch, fs, fs * ch * 4, ch * 4, 32)
+    hdr += b"data" + struct.pack("<I", len(raw))
+    with open(path, "wb") as f:
+        f.write(hdr)
+        f.write(raw)
+
+
+def write_wav_pcm(path, x, fs, code):
+    """Test helper: write x (float in [-1, 1] or the native integer samples) as a WAV
+    of the given PCM code (u8 / s16 / s24 / s32 / f32 / f64)."""
+    x = np.asarray(x)
+    ch = 1 if x.ndim == 1 else x.shape[1]
+    tag, bits = {"u8": (1, 8), "s16": (1, 16), "s24": (1, 24), "s32": (1, 32),
+                 "f32": (3, 32), "f64": (3, 64)}[code]
+    if code == "f32":
+        raw = np.ascontiguousarray(x, "<f4").tobytes()
+    elif code == "f64":
+        raw = np.ascontiguousarray(x, "<f8").tobytes()
+    elif code == "u8":
+        raw = np.ascontiguousarray(x, "u1").tobytes()
+    elif code == "s16":
+        raw = np.ascontiguousarray(x, "<i2").tobytes()
+    elif code == "s32":
+        raw = np.ascontiguousarray(x, "<i4").tobytes()
+    else:
+        v = np.ascontiguousarray(x, np.int32).reshape(-1)
+        b = np.empty((v.size, 3), np.uint8)
+        b[:, 0] = v & 0xFF
+        b[:, 1] = (v >> 8) & 0xFF
+        b[:, 2] = (v >> 16) & 0xFF
+        raw = b.tobytes()
+    ba = ch * bits // 8
+    hdr = b"RIFF" + struct.pack("<I", 36 + len(raw)) + b"WAVE"
+    hdr += b"fmt " + struct.pack("<IHHIIHH", 16, tag, ch, fs, fs * ba, ba, bits)
     hdr += b"data" + struct.pack("<I", len(raw))
     with open(path, "wb") as f:
         f.write(hdr)

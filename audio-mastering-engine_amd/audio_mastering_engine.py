@@ -9,16 +9,22 @@ Mirrors audio_mastering_engine.py's call surface for the hot path:
   ``n+3``, ``n+4``), same ``ValueError`` for missing files, writes a 16-bit WAV.
 * ``process_audio_with_ffmpeg_pipeline`` -- alias of ``master_audio``.
 * ``process_audio(settings, status_cb, progress_cb, art_cb, tag_cb)`` -- the GUI
-  wrapper (:94-137) with the AI/art/MP3 branches out of scope: it reports
+  wrapper (:94-137): mastering, the optional MP3 export (:97-98, ``export_to_mp3``
+  :140-150, through an ``ffmpeg`` on PATH exactly as the reference calls it), and
+  the AI/art branches out of scope: it reports
   ``"Success: Processing complete! (No art generated)"``, ``art_callback(None)``;
   on any error ``"Error: ..."``, ``progress(0, 1)``, ``art(None)``,
   ``tag("Processing failed.")`` exactly like :131-137.
 * ``EQ_PRESETS`` (:32-38).
 
-All DSP runs on the GPU (libamx.so via amx.engine); nothing here computes samples.
+All per-sample work runs on the GPU (libamx.so via amx.engine): the host parses the
+WAV container and moves the file's own bytes to the device; the s16 conversion of
+ffmpeg's split (any PCM format, mono duplicated) is a kernel (amx_pcm_to_s16), and a
+float32 file goes straight into the chain, whose first kernel quantises it.
 """
 import logging
 import os
+import subprocess
 import sys
 import traceback
 
@@ -33,11 +39,34 @@ from amx.chunking import chunk_bounds, packet_frames  # noqa: E402
 from amx.settings import EQ_PRESETS  # noqa: E402,F401
 
 __all__ = ["master_audio", "process_audio", "process_audio_with_ffmpeg_pipeline", "EQ_PRESETS",
-           "master_array"]
+           "master_array", "export_to_mp3"]
 
 
 def _noop(*a, **k):
     return None
+
+
+def _device_input(path):
+    """The input file on the device, as the chunk chain reads it: (d_in, fs, frames,
+    channels_in, input_s16, block_align).  float32 stays float32 (the chain's first
+    kernel quantises it, A.1); every other format is decoded to stereo s16 by
+    amx_pcm_to_s16 (what ffmpeg's split writes + pydub's set_channels(2))."""
+    import torch
+    from amx import capi
+    raw, info, code = wavio.read_wav_raw(path)
+    if info.channels not in (1, 2):
+        raise ValueError("only mono and stereo inputs are supported (%d channels)" % info.channels)
+    frames = raw.size // info.block_align
+    d_raw = torch.from_numpy(np.ascontiguousarray(raw)).to("cuda")
+    if code == "f32":
+        return d_raw.view(torch.float32), info.sample_rate, frames, info.channels, False, info.block_align
+    if code == "s16" and info.channels == 2:
+        return d_raw.view(torch.int16), info.sample_rate, frames, 2, True, info.block_align
+    d_in = torch.empty((max(1, frames), 2), dtype=torch.int16, device="cuda")
+    capi.check(capi.load().amx_pcm_to_s16(capi.ptr(d_raw), frames, info.channels,
+                                          capi.PCM_FORMATS[code], capi.ptr(d_in),
+                                          capi.ptr_stream()), "amx_pcm_to_s16")
+    return d_in, info.sample_rate, frames, 2, True, info.block_align
 
 
 def master_audio(settings, status_callback=None, progress_callback=None):
@@ -51,20 +80,22 @@ def master_audio(settings, status_callback=None, progress_callback=None):
         raise ValueError("Input or output file not specified.")              # :173
     status("Splitting audio into manageable chunks...")                       # :176
     progress(0, 100)                                                          # :177
-    native, info = wavio.read_wav_native(input_file)
-    x16 = wavio.to_s16(native, info)                                          # ffmpeg -> s16 chunks
-    fs = info.sample_rate
-    bounds = chunk_bounds(x16.shape[0], fs, packet_frames(info.block_align))
+    d_in, fs, frames, ch_in, s16, block_align = _device_input(input_file)
+    bounds = chunk_bounds(frames, fs, packet_frames(block_align))             # :178
     status("Splitting complete.")                                             # :180
     num_chunks = len(bounds)
     total_steps = num_chunks + 4                                              # :184
-    d_in = torch.from_numpy(np.ascontiguousarray(x16)).to("cuda")
-    job = MasteringJob(fs, x16.shape[1], settings, [x16.shape[0]], input_s16=True,
+    job = MasteringJob(fs, ch_in, settings, [frames], input_s16=s16,
                        chunks=[(0, s, n) for s, n in bounds])
+    # every chunk's chain runs in the same launches (chunks are independent,
+    # :185-204); the per-chunk callbacks fire while the device works on them and
+    # "Re-assembling" fires once the chain is done
+    if num_chunks:
+        job.run_chunks(d_in)
     for i in range(num_chunks):
         status(f"Processing chunk {i+1} of {num_chunks}...")                  # :186
         progress(i + 1, total_steps)                                          # :187
-    job.run_chunks(d_in)
+    torch.cuda.current_stream().synchronize()
     status("Re-assembling processed chunks with concat filter...")           # :205
     progress(num_chunks + 1, total_steps)                                     # :206
     status("Concatenation complete.")                                         # :213
@@ -76,7 +107,7 @@ def master_audio(settings, status_callback=None, progress_callback=None):
         job.histograms()
     job.decide()
     report = job.fetch_report()          # raises DynamicModeUnsupported before any output
-    if report["modes"][0] == "skip":
+    if report["modes"] and report["modes"][0] == "skip":
         logging.warning("Measured loudness is -inf (silent audio). Skipping normalization.")
     status("Applying final limiting and exporting...")                        # :221
     progress(num_chunks + 3, total_steps)                                     # :222
@@ -91,10 +122,33 @@ def master_audio(settings, status_callback=None, progress_callback=None):
 process_audio_with_ffmpeg_pipeline = master_audio
 
 
-def process_audio(settings, status_callback, progress_callback, art_callback, tag_callback):
-    """:94-137 with the MP3/AI/art branches out of scope."""
+def export_to_mp3(input_wav_path, status_callback):
+    """:140-150 as the reference does it: the external ffmpeg encodes the mastered
+    WAV to VBR MP3 (-q:a 0); a missing ffmpeg fails the same way (status
+    "Error: Failed to create MP3 file.")."""
+    if not input_wav_path or not os.path.exists(input_wav_path):
+        logging.warning("Input WAV file not found for MP3 conversion.")
+        status_callback("Warning: Could not find master WAV to create MP3.")
+        return
+    output_mp3_path = os.path.splitext(input_wav_path)[0] + ".mp3"
+    status_callback("Creating high-quality MP3...")
+    logging.info(f"Exporting WAV to MP3: {input_wav_path} -> {output_mp3_path}")
     try:
-        master_audio(settings, status_callback, progress_callback)
+        mp3_command = ['ffmpeg', '-i', input_wav_path, '-q:a', '0', '-y', output_mp3_path]
+        subprocess.run(mp3_command, check=True, capture_output=True, text=True)
+        logging.info("MP3 export successful.")
+        status_callback("High-quality MP3 created successfully.")
+    except Exception:
+        logging.exception("Error during MP3 export.")
+        status_callback("Error: Failed to create MP3 file.")
+
+
+def process_audio(settings, status_callback, progress_callback, art_callback, tag_callback):
+    """:94-137 with the AI / art branches out of scope."""
+    try:
+        output_wav_path = master_audio(settings, status_callback, progress_callback)
+        if settings.get("create_mp3", False):                                 # :97-98
+            export_to_mp3(output_wav_path, status_callback)
         status_callback("Mastering complete. Preparing for AI analysis...")
         status_callback("Success: Processing complete! (No art generated)")
         art_callback(None)

@@ -335,6 +335,9 @@ __global__ void __launch_bounds__(64) k_env0(const ChainDev *__restrict__ cdp,
     const ChainDev &cd = *cdp;
     const int lane = threadIdx.x;
     if (blockIdx.x == 0 && blockIdx.y == 0 && lane < AMX_ENV_MAX_ROUNDS) flags[lane] = 0;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && lane < 64) {
+        for (int k = lane; k < AMX_ENV_MAX_ROUNDS * AMX_ENV_NCTR; k += 64) flags[AMX_ENV_MAX_ROUNDS + k] = 0;
+    }
     const int j = blockIdx.x * 64 + lane;
     const int b = blockIdx.y;
     const bool valid = j < n_es;
@@ -411,6 +414,9 @@ __global__ void __launch_bounds__(64) k_envfix(const ChainDev *__restrict__ cdp,
                                                int *flags, int round, int fix) {
     if (round > 0 && __builtin_amdgcn_readfirstlane(flags[round - 1]) == 0) return;
     const ChainDev &cd = *cdp;
+    // per-round counters after the round flags: segments re-run, the most re-runs in
+    // one wave (its chain of dependent fixes), waves with work, look-back steps
+    int *ctr = flags + AMX_ENV_MAX_ROUNDS + round * AMX_ENV_NCTR;
     const int lane = threadIdx.x;
     const int w0 = blockIdx.x * 64;
     const int j = w0 + lane;
@@ -430,13 +436,15 @@ __global__ void __launch_bounds__(64) k_envfix(const ChainDev *__restrict__ cdp,
         if (__ballot(lb)) {
             // the wave's first chunk: last active segment before w0 (uniform)
             const int first0 = __shfl(sg.first, 0);
-            int last = -1;
+            int last = -1, steps = 0;
             for (int base = w0 - 64; base + 63 >= first0; base -= 64) {
                 const int jj = base + lane;
+                steps++;
                 const unsigned long long mk = __ballot(jj >= first0 && act[bo + jj] != 0);
                 if (mk) { last = base + 63 - __clzll((long long)mk); break; }
             }
             if (lb) p = last;
+            if (lane == 0) atomicMax(ctr + 3, steps);
         }
         if (!valid) p = -1;
         if (valid) prev[bo + j] = p;
@@ -455,6 +463,7 @@ __global__ void __launch_bounds__(64) k_envfix(const ChainDev *__restrict__ cdp,
     unsigned long long work = __ballot(need);
     if (!work) return;
     if (lane == 0) flags[round] = 1;
+    int nfix = 0;
     const int64_t loc = chunks[sg.chunk].loc_off;
     bool fixed = false;
     while (work) {
@@ -467,6 +476,7 @@ __global__ void __launch_bounds__(64) k_envfix(const ChainDev *__restrict__ cdp,
         const double r = env_fix_segment<RCP>(cd, mm + ro, ck + ro / AMX_ENV_TF_, posw, lenw, aw,
                                               nsw, enw);
         if (lane == w) { en = r; fixed = true; }
+        nfix++;
         // lanes starting from segment w0 + w take its new end now
         if (lane > w && valid && p == w0 + w) {
             ns = r;
@@ -477,6 +487,11 @@ __global__ void __launch_bounds__(64) k_envfix(const ChainDev *__restrict__ cdp,
     if (fixed) {
         ev[bo + j] = en;
         sv[bo + j] = ns;
+    }
+    if (lane == 0) {                      // diagnostics (amx_env_counters)
+        atomicAdd(ctr + 0, nfix);
+        atomicMax(ctr + 1, nfix);
+        atomicAdd(ctr + 2, 1);
     }
 }
 
@@ -714,12 +729,16 @@ hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, double *m) {
     return hipGetLastError();
 }
 
+// part 0: the speculation (k_env0); part 1: the parallel fix-up rounds (k_envfix)
 template <bool RCP>
 static void env_launch_t(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
-                         int *act, int *prev, int *flags, int rounds) {
+                         int *act, int *prev, int *flags, int rounds, int part) {
     const dim3 gw((unsigned)((d.n_es + 63) / 64), 3);
-    hipLaunchKernelGGL(k_env0<RCP>, gw, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es, m, ck, sv,
-                       ev, act, d.nloc, d.warm, d.Le, flags);
+    if (part == 0) {
+        hipLaunchKernelGGL(k_env0<RCP>, gw, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es, m, ck,
+                           sv, ev, act, d.nloc, d.warm, d.Le, flags);
+        return;
+    }
     // rounds == 0: only prev[] (everything is left to k_envseq)
     for (int k = 0; k < (rounds > 0 ? rounds : 1); k++)
         hipLaunchKernelGGL(k_envfix<RCP>, gw, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es, m,
@@ -727,13 +746,13 @@ static void env_launch_t(const DynLaunch &d, const double *m, double *ck, double
 }
 
 hipError_t launch_env(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
-                      int *act, int *prev, int *flags, int rounds) {
+                      int *act, int *prev, int *flags, int rounds, int part) {
     if (d.n_es <= 0) return hipSuccess;
     if (d.warm % (AMX_ENV_TF * AMX_ENV_PF) || d.Le % (AMX_ENV_TF * AMX_ENV_PF))
         return hipErrorInvalidValue;
     if (rounds < 0 || rounds > AMX_ENV_MAX_ROUNDS) return hipErrorInvalidValue;
-    if (d.rcp) env_launch_t<true>(d, m, ck, sv, ev, act, prev, flags, rounds);
-    else env_launch_t<false>(d, m, ck, sv, ev, act, prev, flags, rounds);
+    if (d.rcp) env_launch_t<true>(d, m, ck, sv, ev, act, prev, flags, rounds, part);
+    else env_launch_t<false>(d, m, ck, sv, ev, act, prev, flags, rounds, part);
     return hipGetLastError();
 }
 

@@ -14,7 +14,16 @@
 #define AMX_CTL_FAST 1    // k_decide control word: limiter provably idle
 #define AMX_STATS 16      // doubles per track written by k_decide
 #define AMX_ENV_MAX_ROUNDS 16  // k_envfix rounds (one flag word each)
+#define AMX_ENV_NCTR 4         // k_envfix diagnostic counters per round (after the flags)
 #define AMX_EQC 64        // compact EQ coefficient block (see ChainDev::eqc)
+#ifndef AMX_PCM_U8        // input PCM formats (include/amx.h amx_pcm_to_s16)
+#define AMX_PCM_U8 0
+#define AMX_PCM_S16 1
+#define AMX_PCM_S24 2
+#define AMX_PCM_S32 3
+#define AMX_PCM_F32 4
+#define AMX_PCM_F64 5
+#endif
 
 // One EQ stage of _apply_eq_to_channel (audio_mastering_engine.py:277-282).
 struct EqStageDev {
@@ -138,8 +147,11 @@ struct DynLaunch {
     hipStream_t st;
 };
 hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, double *m);
+// input decode: PCM of any supported format -> stereo s16 frames (amx_io.hip)
+hipError_t launch_pcm_to_s16(const void *raw, int64_t frames, int channels, int fmt, int16_t *out,
+                             hipStream_t st);
 hipError_t launch_env(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
-                      int *act, int *prev, int *flags, int rounds);
+                      int *act, int *prev, int *flags, int rounds, int part);
 hipError_t launch_envseq(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
                          const int *act, const int *prev, const int *flags, int rounds);
 hipError_t launch_gain_overlay(const DynLaunch &d, const double *m, const double *ck,

@@ -1,0 +1,82 @@
+// amx_io.hip -- the input file's PCM -> the s16 stereo frames the chunk chain reads.
+//
+// The reference never sees the input's own sample format: ffmpeg's segment split
+// (audio_mastering_engine.py:178) writes every chunk as a 16-bit PCM WAV (the wav
+// muxer's default codec), converting with libswresample's audioconvert, and pydub
+// then duplicates a mono chunk to stereo (set_channels(2), :190).  Restated per
+// format (audioconvert.c CONV_FUNC, no dither -- swr's default):
+//   u8  : (v - 0x80) << 8
+//   s16 : v
+//   s24 : decoded to s32 as v << 8, then >> 16          (= v >> 8, arithmetic)
+//   s32 : v >> 16
+//   f32 : av_clip_int16(lrintf(v * 32768))
+//   f64 : av_clip_int16(lrint(v * 32768))
+// (float32 input normally skips this kernel: k_front1s quantises it in the chain's
+// first pass.)  One thread per frame, grid-stride; a memory-bound pass.
+#include "amx_dev.hpp"
+
+namespace amx {
+
+template <int FMT>
+__device__ __forceinline__ int16_t pcm_sample(const uint8_t *__restrict__ raw, int64_t s) {
+    if constexpr (FMT == AMX_PCM_U8) {
+        return (int16_t)(((int)raw[s] - 0x80) * 256);
+    } else if constexpr (FMT == AMX_PCM_S16) {
+        return reinterpret_cast<const int16_t *>(raw)[s];
+    } else if constexpr (FMT == AMX_PCM_S24) {
+        const uint8_t *p = raw + 3 * s;
+        const int v = (int)((uint32_t)p[0] << 8 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 24);
+        return (int16_t)(v >> 16);
+    } else if constexpr (FMT == AMX_PCM_S32) {
+        return (int16_t)(reinterpret_cast<const int32_t *>(raw)[s] >> 16);
+    } else if constexpr (FMT == AMX_PCM_F32) {
+        return q_f32_to_s16_ffmpeg(reinterpret_cast<const float *>(raw)[s]);
+    } else {
+        double v = rint(reinterpret_cast<const double *>(raw)[s] * 32768.0);
+        v = fmin(fmax(v, -32768.0), 32767.0);
+        return (int16_t)(int)v;
+    }
+}
+
+template <int FMT, int CH>
+__global__ void __launch_bounds__(AMX_BLOCK) k_pcm_to_s16(const uint8_t *__restrict__ raw,
+                                                          int64_t frames,
+                                                          uint32_t *__restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * AMX_BLOCK;
+    for (int64_t i = (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x; i < frames; i += stride) {
+        const int16_t l = pcm_sample<FMT>(raw, i * CH);
+        const int16_t r = CH == 2 ? pcm_sample<FMT>(raw, i * CH + 1) : l;   // mono -> L = R (:190)
+        out[i] = pack2(l, r);
+    }
+}
+
+template <int FMT>
+static hipError_t pcm_t(const uint8_t *raw, int64_t frames, int channels, uint32_t *out,
+                        hipStream_t st) {
+    const int64_t want = (frames + AMX_BLOCK - 1) / AMX_BLOCK;
+    const unsigned g = (unsigned)(want < 8192 ? (want > 0 ? want : 1) : 8192);
+    if (channels == 2)
+        hipLaunchKernelGGL((k_pcm_to_s16<FMT, 2>), dim3(g), dim3(AMX_BLOCK), 0, st, raw, frames, out);
+    else
+        hipLaunchKernelGGL((k_pcm_to_s16<FMT, 1>), dim3(g), dim3(AMX_BLOCK), 0, st, raw, frames, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_pcm_to_s16(const void *raw, int64_t frames, int channels, int fmt, int16_t *out,
+                             hipStream_t st) {
+    if (frames <= 0) return hipSuccess;
+    if (channels != 1 && channels != 2) return hipErrorInvalidValue;
+    const uint8_t *r = reinterpret_cast<const uint8_t *>(raw);
+    uint32_t *o = reinterpret_cast<uint32_t *>(out);
+    switch (fmt) {
+    case AMX_PCM_U8: return pcm_t<AMX_PCM_U8>(r, frames, channels, o, st);
+    case AMX_PCM_S16: return pcm_t<AMX_PCM_S16>(r, frames, channels, o, st);
+    case AMX_PCM_S24: return pcm_t<AMX_PCM_S24>(r, frames, channels, o, st);
+    case AMX_PCM_S32: return pcm_t<AMX_PCM_S32>(r, frames, channels, o, st);
+    case AMX_PCM_F32: return pcm_t<AMX_PCM_F32>(r, frames, channels, o, st);
+    case AMX_PCM_F64: return pcm_t<AMX_PCM_F64>(r, frames, channels, o, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace amx

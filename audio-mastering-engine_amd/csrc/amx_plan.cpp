@@ -174,6 +174,8 @@ struct amx_plan {
     int n_tracks = 0, n_chunks = 0, n_seg = 0, n_kseg = 0, n_blk = 0, n_kblk = 0;
     int64_t max_nkseg = 0;
     int64_t nloc = 0, out_frames = 0, max_chunk_out = 0, max_span = 0, max_chunk_n = 0;
+    int64_t in_frames = 0;  // input frames the chunks read (max in_offset + frames)
+    int mono16 = 0;         // mono int16 input: duplicated to stereo into ws o_dup first
     std::vector<ChunkDev> chunks;
     std::vector<SegDev> segs;
     std::vector<KwSegDev> ksegs;
@@ -209,7 +211,7 @@ struct amx_plan {
     size_t o_a16, o_e, o_s, o_p16, o_ex, o_sx, o_bands, o_r, o_m, o_gain, o_esv, o_ee0, o_eflags, o_eact,
         o_eprev;
     size_t o_ekw, o_skw, o_parts, o_phop;
-    size_t o_eb, o_ebx, o_ebk, o_pk;
+    size_t o_eb, o_ebx, o_ebk, o_pk, o_dup = 0;
     amx::ScanPlan scan_eq() const { return {D, n_blk, lev_eq, d_blks, d_M, d_Mp}; }
     amx::ScanPlan scan_xo() const { return {AMX_XO_DIM, mb ? n_blk : 0, lev_x, d_blks, d_Mx, d_Mpx}; }
     amx::ScanPlan scan_kw() const { return {AMX_KW_DIM, n_kblk, lev_kw, d_kblks, d_Mkw, d_Mpkw}; }
@@ -264,8 +266,6 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     if (desc->sample_rate <= 0) return fail(AMX_EINVAL, "sample_rate must be > 0");
     if (desc->channels_in != 1 && desc->channels_in != 2)
         return fail(AMX_EINVAL, "channels_in must be 1 or 2");
-    if (desc->input_s16 && desc->channels_in != 2)
-        return fail(AMX_EINVAL, "int16 input must be stereo (duplicate mono on the host)");
     if (desc->analog_on && !desc->tanh_lut)
         return fail(AMX_EINVAL, "analog character needs the float32 tanh table (tanh_lut)");
     *out = nullptr;
@@ -286,7 +286,10 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     ChainDev &cd = p->cd;
     memset(&cd, 0, sizeof cd);
     cd.fs = fs;
-    cd.chin = desc->channels_in;
+    // mono int16 is duplicated to stereo on the device first (k_pcm_to_s16), so the
+    // chain reads stereo int16 frames
+    p->mono16 = (desc->input_s16 && desc->channels_in == 1) ? 1 : 0;
+    cd.chin = p->mono16 ? 2 : desc->channels_in;
     cd.in_s16 = desc->input_s16 ? 1 : 0;
     cd.analog_on = desc->analog_on ? 1 : 0;
     cd.has_lut = desc->tanh_lut ? 1 : 0;
@@ -472,6 +475,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         }
         ch.out_n = n2;
         ch.track = chunks[c].track;
+        p->in_frames = std::max(p->in_frames, (int64_t)(chunks[c].in_offset + chunks[c].frames));
         ch.seg0 = (int32_t)p->segs.size();
         int64_t ns = (ch.n + p->L - 1) / p->L;
         ch.nseg = (int32_t)ns;
@@ -686,10 +690,11 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         p->o_m = (size_t)align_up(off, (3 * nl + 2 * mpad) * 8) + mpad * 8;
         p->o_esv = (size_t)align_up(off, 3 * ne * 8);
         p->o_ee0 = (size_t)align_up(off, 3 * ne * 8);
-        p->o_eflags = (size_t)align_up(off, AMX_ENV_MAX_ROUNDS * 4);
+        p->o_eflags = (size_t)align_up(off, AMX_ENV_MAX_ROUNDS * (1 + AMX_ENV_NCTR) * 4);
         p->o_eact = (size_t)align_up(off, 3 * ne * 4);
         p->o_eprev = (size_t)align_up(off, 3 * ne * 4);
     }
+    if (p->mono16) p->o_dup = (size_t)align_up(off, (size_t)p->in_frames * 4);
     const size_t nb = (size_t)p->n_blk, nkb = (size_t)p->n_kblk;
     p->o_eb = (size_t)align_up(off, nb * 2 * (D ? D : 1) * 8);
     if (p->mb) {
@@ -771,6 +776,11 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
                       p->warm,    p->Le,       p->cd.env_rcp, p->d_tabs, st};
     switch (stage) {
     case AMX_STAGE_FRONT1:
+        if (p->mono16) {
+            int16_t *dup = wsp<int16_t>(d_ws, p->o_dup);
+            HIPCHK(amx::launch_pcm_to_s16(d_in, p->in_frames, 1, AMX_PCM_S16, dup, st));
+            d_in = reinterpret_cast<const float *>(dup);
+        }
         HIPCHK(amx::launch_front1(l, p->D, (p->cd.chin == 2 && !p->cd.in_s16) ? 2 : 1,
                                   p->cd.analog_on != 0, d_in, p->d_lut, a16, p->d_G, e));
         break;
@@ -801,11 +811,13 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
         break;
     case AMX_STAGE_ENV:
         if (p->mb)
-            HIPCHK(amx::launch_env(dl, mframe, ck, esv, ee0, eact, eprev, eflags, p->rounds));
+            HIPCHK(amx::launch_env(dl, mframe, ck, esv, ee0, eact, eprev, eflags, p->rounds, 0));
         break;
     case AMX_STAGE_FIX:
-        if (p->mb)
+        if (p->mb) {
+            HIPCHK(amx::launch_env(dl, mframe, ck, esv, ee0, eact, eprev, eflags, p->rounds, 1));
             HIPCHK(amx::launch_envseq(dl, mframe, ck, esv, ee0, eact, eprev, eflags, p->rounds));
+        }
         break;
     case AMX_STAGE_APPLY:
         if (p->mb)
@@ -852,6 +864,27 @@ int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, double *d_kw_tail, dou
     p->kw_rest_states = 1;   // s = the start states from rest: pass 2 without a carry reuses them
     if (d_kw_tail)
         HIPCHK(amx::launch_kw_tail(p->d_spans, p->n_tracks, s, e, p->d_tailpow, d_kw_tail, st));
+    return AMX_OK;
+}
+
+int amx_pcm_to_s16(const void *d_raw, int64_t frames, int32_t channels, int32_t format,
+                   int16_t *d_out, void *stream) {
+    if (frames < 0 || (frames > 0 && (!d_raw || !d_out))) return fail(AMX_EINVAL, "null argument");
+    if (channels != 1 && channels != 2) return fail(AMX_EINVAL, "channels must be 1 or 2");
+    if (format < AMX_PCM_U8 || format > AMX_PCM_F64) return fail(AMX_EINVAL, "bad PCM format %d", format);
+    HIPCHK(amx::launch_pcm_to_s16(d_raw, frames, channels, format, d_out, (hipStream_t)stream));
+    return AMX_OK;
+}
+
+int amx_env_counters(const amx_plan *p, const void *d_ws, int32_t *out, int32_t n) {
+    if (!p || !out || n < 0) return fail(AMX_EINVAL, "null argument");
+    const int32_t have = AMX_ENV_MAX_ROUNDS * AMX_ENV_NCTR;
+    for (int32_t i = 0; i < n; i++) out[i] = 0;
+    if (!p->mb || p->n_es == 0) return AMX_OK;
+    if (!d_ws) return fail(AMX_EINVAL, "null workspace");
+    const int32_t k = n < have ? n : have;
+    HIPCHK(hipMemcpy(out, reinterpret_cast<const char *>(d_ws) + p->o_eflags + AMX_ENV_MAX_ROUNDS * 4,
+                     (size_t)k * 4, hipMemcpyDeviceToHost));
     return AMX_OK;
 }
 

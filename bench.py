@@ -1,18 +1,24 @@
 """Benchmark: mastered Msamples/s (48 kHz stereo f32) at N GPUs + HBM roofline.
 
-Workload (BASELINE.json configs[1], the metric's single-GPU config): per rank a
-5-minute stereo 48 kHz float32 program (synthetic, seeded), mastered with the
-"Vocal Clarity" EQ preset and loudness normalisation to -14 LUFS, i.e. the whole
-process_audio_with_ffmpeg_pipeline path (audio_mastering_engine.py:171-226):
-chunk chain + concat, loudnorm measurement + linear gain, alimiter.  At N GPUs the
-job is ONE track of N x 5 min, chunk-sharded over the ranks (weak scaling) with the
-RCCL all-reduce of the loudness partials.  Input is resident in HBM before timing;
-output (16-bit PCM, what the reference writes) stays in HBM.
+Workload (default configs[2], C3 -- the north_star's "fused EQ -> multiband-comp ->
+LUFS chain"): per rank a 5-minute stereo 48 kHz float32 program (synthetic, seeded),
+mastered with the "Vocal Clarity" EQ preset, width 1.3, analog character 40 %, the
+3-band multiband compressor (GUI default thresholds / ratios) and loudness
+normalisation to -14 LUFS, i.e. the whole process_audio_with_ffmpeg_pipeline path
+(audio_mastering_engine.py:171-226): chunk chain + concat, loudnorm measurement +
+linear gain, alimiter.  At N GPUs the job is ONE track of N x 5 min, chunk-sharded
+over the ranks (weak scaling) with the RCCL all-reduce of the loudness partials.
+Input is resident in HBM before timing; the output (16-bit PCM, what the reference
+writes) stays in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+
+c2 = configs[1] (EQ + loudnorm + alimiter), c4 = configs[3] (8 whole 4-minute tracks
+per GPU, track-sharded, no exchange), c5 = configs[4] (60 min at 96 kHz per GPU).
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -21,24 +27,44 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "audio-mastering-engine_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (spec)
+FP64_PEAK_TFS = 78.6           # MI355X fp64 vector, spec (half the 157.3 TF fp32 rate); measured 68
+CHAIN_BYTES = 8                # 4 B f32 read + 4 B write per channel-sample (chain)
+E2E_BYTES = 16                 # + the gain / limiter pass
 
 VOCAL = dict(bass_boost=-1.0, mid_cut=2.0, presence_boost=2.5, treble_boost=1.0)
 MB = dict(multiband=True, low_thresh=-25.0, low_ratio=6.0, mid_thresh=-20.0, mid_ratio=3.0,
           high_thresh=-15.0, high_ratio=4.0)
+C3 = dict(VOCAL, lufs=-14.0, width=1.3, analog_character=40.0, **MB)
 CONFIGS = {
     "c2": dict(VOCAL, lufs=-14.0),
-    "c3": dict(VOCAL, lufs=-14.0, width=1.3, analog_character=40.0, **MB),
-    "c5": dict(VOCAL, lufs=-14.0, width=1.3, analog_character=40.0, **MB),
+    "c3": C3,
+    "c4": C3,
+    "c5": C3,
 }
-# sample rate and default length per config (BASELINE.json configs; C5 = 60 min at 96 kHz)
-CONFIG_FS = {"c2": 48000, "c3": 48000, "c5": 96000}
-CONFIG_SECONDS = {"c2": 300.0, "c3": 300.0, "c5": 3600.0}
+# sample rate, seconds per track, tracks per GPU (BASELINE.json configs)
+CONFIG_FS = {"c2": 48000, "c3": 48000, "c4": 48000, "c5": 96000}
+CONFIG_SECONDS = {"c2": 300.0, "c3": 300.0, "c4": 240.0, "c5": 3600.0}
+CONFIG_TRACKS = {"c2": 1, "c3": 1, "c4": 8, "c5": 1}
+WORKLOAD = {
+    "c2": "configs[1]: 5 min stereo 48 kHz f32 per GPU, EQ 'Vocal Clarity' + loudnorm -14 LUFS "
+          "(linear) + alimiter; N GPUs = one N x 5 min track, chunk-sharded",
+    "c3": "configs[2]: 5 min stereo 48 kHz f32 per GPU, C2 + multiband compressor (3-band "
+          "crossover, GUI thresholds/ratios) + width 1.3 + analog character 40; N GPUs = one "
+          "N x 5 min track, chunk-sharded",
+    "c4": "configs[3]: batch of 4 min stereo 48 kHz f32 tracks, 8 per GPU (64 at N = 8), C3 "
+          "settings, whole tracks sharded over the ranks (no exchange)",
+    "c5": "configs[4]: 60 min stereo 96 kHz f32 per GPU, C3 settings, hipGraph-captured step",
+}
+# the reference's own Python chain, 1 core (measured in the survey container):
+# context for the C oracle's rate, which is ~50-90x faster than the reference
+REF_PY = {"c2": (20.9, "EQ only (the C2 chain's scipy part; ffmpeg stages not measurable)"),
+          "c3": (0.42, "EQ + analog + width + multiband (crossover + 3 pydub compressors)")}
 
 
-def stage_bytes(stage, frames, ch_in, mb):
-    """Algorithmic HBM bytes of one launch: what the stage must read
-    and write per frame, x frames.  int16 stereo frame = 4 B; f32 stereo = 8 B."""
+def stage_bytes(stage, frames, ch_in):
+    """Per-kernel byte MODEL: what each stage's kernel must read and
+    write per stereo frame, x frames.  int16 stereo frame = 4 B; f32 stereo = 8 B.
+    Reported beside the §8(d) roofline, not as it."""
     fin = 4 * ch_in
     per = {
         "front1": fin + 4,              # f32 input -> s16 chain input
@@ -52,9 +78,6 @@ def stage_bytes(stage, frames, ch_in, mb):
         "apply": 12 + 24 + 1.5 + 4,     # bands + m + checkpoints -> output
     }
     return per.get(stage, 0) * frames
-
-
-FP64_PEAK_TFS = 78.6   # MI355X fp64 vector, spec (half the 157.3 TF fp32 rate); measured 68
 
 
 def front2_flops(frames, settings, mb):
@@ -71,35 +94,37 @@ def front2_flops(frames, settings, mb):
     return per * 2 * frames
 
 
-# kernels of each stage (rocprofv3 short names) for the PMC traffic lookup
-STAGE_KERNELS = {
-    "front1": ("k_front1s", "k_front1"), "front2": ("k_front2",), "xover": ("k_xover2",),
-    "rms": ("k_rms",), "env": ("k_env0", "k_envfix"), "apply": ("k_gain_overlay",),
-    "loud1": ("k_kw1", "k_peak_reduce"), "loud2": ("k_kw2", "k_hops"), "final": ("k_final",),
-}
+# the one kernel of each single-kernel stage (rocprofv3 short names)
+STAGE_KERNEL = {"front1": "k_front1s", "front2": "k_front2", "xover": "k_xover2", "rms": "k_rms",
+                "env": "k_env0", "apply": "k_gain_overlay", "final": "k_final"}
+# launches per step of kernels that run more than once (the envelope fix rounds)
+PER_STEP = {"k_envfix": 2}
+# the pipeline's kernels (runtime copy / torch helper kernels excluded from step traffic)
+PIPELINE_PREFIX = "k_"
 
 
-def stage_traffic(stage, config):
-    """HBM bytes per launch of `stage` from the committed PMC summary
-    (profiles/traffic_<config>.json, scripts/gpu_traffic.sh), or None."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                        "traffic_%s.json" % config)
+def load_traffic(config):
+    """Per-launch HBM bytes from the committed PMC summary (profiles/traffic_<config>.json,
+    scripts/gpu_traffic.sh: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, separate passes)."""
+    path = os.path.join(ROOT, "profiles", "traffic_%s.json" % config)
     try:
-        ks = json.load(open(path))["kernels"]
+        return json.load(open(path))["kernels"]
     except (OSError, ValueError, KeyError):
         return None
-    names = STAGE_KERNELS.get(stage, ())
-    hit = [v["hbm_bytes"] for k, v in ks.items() if k in names]
-    return int(sum(hit)) if hit else None
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: enough for a >= 2 s timed region)")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--seconds", type=float, default=None, help="per GPU (default: the config's)")
+    ap.add_argument("--soak", type=float, default=2.0,
+                    help="seconds of untimed graph replays after the warm-up, so the GPU is "
+                         "visibly busy before the timed region")
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--seconds", type=float, default=None, help="per track (default: the config's)")
+    ap.add_argument("--tracks", type=int, default=None, help="tracks per GPU (c4; default 8)")
     ap.add_argument("--seg-frames", type=int, default=128)
     ap.add_argument("--env-warm", type=int, default=None,
                     help="compressor envelope warm-up frames (default: the plan's, 2048)")
@@ -116,7 +141,7 @@ def main():
     import torch
     import torch.distributed as dist
     from amx import synth
-    from amx.dist import ShardedTrack
+    from amx.dist import ShardedBatch, ShardedTrack
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -127,16 +152,24 @@ def main():
     fs = CONFIG_FS[args.config]
     if args.seconds is None:
         args.seconds = CONFIG_SECONDS[args.config]
+    n_tr = args.tracks if args.tracks is not None else CONFIG_TRACKS[args.config]
     settings = CONFIGS[args.config]
     if args.env_warm is not None:
         settings = dict(settings, _env_warm=int(args.env_warm))
-    per_rank = int(args.seconds * fs)
-    total = per_rank * world
-    track = ShardedTrack(fs, 2, settings, total, rank, world, quantum=512,
-                         seg_frames=args.seg_frames)
-    x = synth.mix_like(track.local_frames, fs, 2, seed=rank)
+    per_track = int(args.seconds * fs)
+    batch = args.config == "c4"
+    if batch:
+        frames = [per_track] * (n_tr * world)
+        runner = ShardedBatch(fs, 2, settings, frames, rank, world, quantum=512,
+                              seg_frames=args.seg_frames)
+        xs = [synth.mix_like(frames[t], fs, 2, seed=1000 + t) for t in runner.tracks]
+        x = np.concatenate(xs, axis=0)
+    else:
+        runner = ShardedTrack(fs, 2, settings, per_track * world, rank, world, quantum=512,
+                              seg_frames=args.seg_frames)
+        x = synth.mix_like(runner.local_frames, fs, 2, seed=rank)
     d_in = torch.from_numpy(x).cuda()
-    job = track.job
+    job = runner.job
 
     def barrier():
         if world > 1:
@@ -144,17 +177,32 @@ def main():
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        track.step(d_in)
+        runner.step(d_in)
     # the step's device work is replayed from captured hipGraphs (every kernel, same
     # buffers): one graph at N = 1, the three stretches between collectives at N > 1
     graph = not args.eager
     if graph:
-        track.capture(d_in)
-        track.replay()
-    run = track.replay if graph else (lambda: track.step(d_in))
+        runner.capture(d_in)
+        runner.replay()
+    run = runner.replay if graph else (lambda: runner.step(d_in))
+    # soak: untimed replays for >= args.soak seconds (also sizes the default K)
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    n_soak = 0
+    while True:
+        run()
+        n_soak += 1
+        if n_soak % 8 == 0 or n_soak == 1:
+            barrier()
+            if time.perf_counter() - t0 >= args.soak:
+                break
+    barrier()
+    soak_s = time.perf_counter() - t0
+    t_est = soak_s / n_soak
+    steps = args.steps if args.steps is not None else max(10, int(math.ceil(2.0 / t_est)))
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
         run()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -162,9 +210,10 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    ms_per_step = elapsed * 1000.0 / args.steps
-    samples_total = sum(track.span_frames) * 2          # output channel-samples, all ranks
-    value = samples_total * args.steps / elapsed / 1e6
+    ms_per_step = elapsed * 1000.0 / steps
+    samples_total = sum(runner.span_frames) * 2          # output channel-samples, all ranks
+    samples_rank = job.info.out_frames * 2
+    value = samples_total * steps / elapsed / 1e6
 
     # host-inclusive rate (reported beside `value`, never as it): pinned H2D of the f32
     # input, the step, D2H of the int16 output, serialised on the stream
@@ -173,86 +222,110 @@ def main():
         n_out = job.info.out_frames
         h_in = torch.from_numpy(x).pin_memory()
         h_out = torch.empty((n_out, 2), dtype=torch.int16).pin_memory()
+        k_h = max(3, min(steps, 20))
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(k_h):
             d_in.copy_(h_in, non_blocking=True)
             run()
             h_out.copy_(job.y[:n_out], non_blocking=True)
         torch.cuda.synchronize()
-        e2e = (time.perf_counter() - t1) / args.steps
+        e2e = (time.perf_counter() - t1) / k_h
         host_incl = {"value": round(samples_total / e2e / 1e6, 3), "unit": "Msamples/s",
                      "ms_per_step": round(e2e * 1e3, 4),
                      "what": "pinned H2D of the f32 input + the step + D2H of the int16 output"}
+        del h_in
         # the same, double-buffered (amx.stream_io.TrackStream): H2D of track i+1, the
         # step of track i and D2H of track i-1 overlap on three streams; for f32 input
         # and for an s16 WAV input (half the H2D bytes)
-        if not args.no_pipeline:
+        if not args.no_pipeline and not batch and fs * args.seconds <= 48000 * 600:
             from amx.stream_io import TrackStream
             host_incl["pipelined"] = {}
-            del h_in
             for kind, s16 in (("f32", False), ("s16", True)):
-                ts = TrackStream(fs, 2, settings, per_rank, depth=2, input_s16=s16, quantum=512,
+                ts = TrackStream(fs, 2, settings, per_track, depth=2, input_s16=s16, quantum=512,
                                  seg_frames=args.seg_frames)
                 hi = ts.pinned_input()
                 hi.copy_(torch.from_numpy(synth.to_s16(x)) if s16 else torch.from_numpy(x))
                 outs = [ts.pinned_output() for _ in range(2)]
-                n_tr = max(4, args.steps)
+                n_p = max(4, min(steps, 20))
                 ts.run([hi] * 2, outs)                        # warm-up
                 t1 = time.perf_counter()
-                ts.run([hi] * n_tr, [outs[i % 2] for i in range(n_tr)])
-                e2p = (time.perf_counter() - t1) / n_tr
+                ts.run([hi] * n_p, [outs[i % 2] for i in range(n_p)])
+                e2p = (time.perf_counter() - t1) / n_p
                 host_incl["pipelined"][kind] = {
                     "value": round(samples_total / e2p / 1e6, 3), "ms_per_track": round(e2p * 1e3, 4),
-                    "tracks": n_tr, "h2d_bytes": int(hi.numel() * hi.element_size()),
+                    "tracks": n_p, "h2d_bytes": int(hi.numel() * hi.element_size()),
                     "d2h_bytes": int(outs[0].numel() * 2)}
                 del ts, hi, outs
 
-    # per-stage device time: the same K steps again with HIP events bracketing each
-    # stage on the launch stream (kept out of the timed region above)
+    # per-stage device time: steps again with HIP events bracketing each stage on the
+    # launch stream (kept out of the timed region above)
+    n_ev = max(3, min(steps, 20))
     job.stage_events = []
-    for _ in range(args.steps):
-        track.step(d_in)
+    for _ in range(n_ev):
+        runner.step(d_in)
     barrier()
     per_stage = {}
     for name, a, b in job.stage_events:
         per_stage[name] = per_stage.get(name, 0.0) + a.elapsed_time(b)
-    per_stage = {k: v / args.steps for k, v in per_stage.items()}
+    per_stage = {k: v / n_ev for k, v in per_stage.items()}
     job.stage_events = None
+    env_ctr = job.env_counters() if settings.get("multiband") else None
     report = job.fetch_report()
-    frames = track.local_frames
+    frames = runner.local_frames
     mb = bool(settings.get("multiband"))
-    candidates = {k: v for k, v in per_stage.items() if stage_bytes(k, frames, 2, mb) > 0}
-    dom = max(candidates, key=candidates.get)
-    dom_ms = candidates[dom]
-    dom_bytes = stage_bytes(dom, frames, 2, mb)
-    achieved = dom_bytes / (dom_ms / 1e3) / 1e9
+    # dominant kernel: the slowest single-kernel stage
+    cand = {k: v for k, v in per_stage.items() if k in STAGE_KERNEL}
+    dom = max(cand, key=cand.get)
+    dom_ms = cand[dom]
+    kern = STAGE_KERNEL[dom]
+    alg_bytes = CHAIN_BYTES * samples_rank                 # SURVEY §8(d) per launch
+    achieved = alg_bytes / (dom_ms / 1e3) / 1e9
+    model_bytes = stage_bytes(dom, frames, 2)
+    traffic = load_traffic(args.config)
+    dom_traffic = int(traffic[kern]["hbm_bytes"]) if traffic and kern in traffic else None
+    step_traffic = None
+    if traffic:
+        step_traffic = int(sum(v["hbm_bytes"] * PER_STEP.get(k, 1) for k, v in traffic.items()
+                               if k.startswith(PIPELINE_PREFIX)))
     f2_flops = front2_flops(frames, settings, mb)
 
     line = {
         "metric": "mastered Msamples/sec (48 kHz stereo f32) at 1/2/4/8 GPUs; % HBM roofline",
-        "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+        "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (amx.synth.mix_like, seeded per rank)",
-        "config": {"workload": "configs[1]: 5 min stereo 48 kHz f32 per GPU, EQ 'Vocal Clarity' + "
-                               "loudnorm -14 LUFS (linear) + alimiter; N GPUs = one N x 5 min track, "
-                               "chunk-sharded" if args.config == "c2" else
-                               ("configs[2]: C2 + multiband + width 1.3 + analog 40" if args.config == "c3"
-                                else "configs[4]: 60 min stereo 96 kHz f32 per GPU, C3 settings"),
-                   "sample_rate": fs,
-                   "settings": args.config, "seconds_per_gpu": args.seconds,
-                   "seg_frames": args.seg_frames, "parallelism": "chunk-shard x%d" % world,
-                   "launch": ("hipGraph replay" if world == 1 else "hipGraph segments + eager collectives")
-                             if graph else "eager"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+        "data": "synthetic (amx.synth.mix_like, seeded per rank / track)",
+        "config": {"workload": WORKLOAD[args.config], "sample_rate": fs,
+                   "settings": args.config, "seconds_per_track": args.seconds,
+                   "tracks_per_gpu": len(runner.tracks) if batch else 1,
+                   "seg_frames": args.seg_frames,
+                   "parallelism": ("track-shard x%d" if batch else "chunk-shard x%d") % world,
+                   "launch": ("hipGraph replay" if world == 1 or batch else
+                              "hipGraph segments + eager collectives") if graph else "eager"},
+        "timed_region_s": round(elapsed, 4), "soak": {"seconds": round(soak_s, 3), "replays": n_soak},
+        "roofline": {"bound": "hbm", "kernel": kern, "stage": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "bytes_per_launch": int(dom_bytes), "avg_launch_ms": round(dom_ms, 4),
-                     "traffic": stage_traffic(dom, args.config),
-                     "traffic_source": "profiles/traffic_%s.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
-                                       % args.config},
+                     "traffic": dom_traffic,
+                     "bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(dom_ms, 4),
+                     "bytes_rule": "SURVEY §8(d): 8 B per output channel-sample (f32 read + write) "
+                                   "x the %d channel-samples one launch processes" % samples_rank,
+                     "kernel_model": {"bytes_per_launch": int(model_bytes),
+                                      "achieved": round(model_bytes / (dom_ms / 1e3) / 1e9, 2),
+                                      "frac": round(model_bytes / (dom_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                      "what": "the kernel's own minimum reads + writes (DESIGN.md §3.3)"},
+                     "traffic_source": "profiles/traffic_%s.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
+                                       "per launch)" % args.config},
+        "chain_roofline": {
+            "bytes_per_step": int(CHAIN_BYTES * samples_rank),
+            "achieved": round(CHAIN_BYTES * samples_rank / (ms_per_step / 1e3) / 1e9, 2),
+            "frac": round(CHAIN_BYTES * samples_rank / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "frac_end_to_end": round(E2E_BYTES * samples_rank / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "step_traffic": step_traffic,
+            "what": "whole step (every kernel) at SURVEY §8(d)'s 8 B/sample chain and 16 B/sample "
+                    "end-to-end; step_traffic = the PMC bytes of every pipeline kernel per step"},
         "host_inclusive": host_incl,
-        "roofline_fp64": {"bound": "fp64", "kernel": "front2",
+        "roofline_fp64": {"bound": "fp64", "kernel": "k_front2",
                           "achieved": round(f2_flops / (per_stage["front2"] / 1e3) / 1e12, 2),
                           "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                           "frac": round(f2_flops / (per_stage["front2"] / 1e3) / 1e12 / FP64_PEAK_TFS, 4),
@@ -262,51 +335,94 @@ def main():
                  "scan_window_eq": int(job.info.scan_levels_eq),
                  "scan_window_xover": int(job.info.scan_levels_xover),
                  "scan_window_kw": int(job.info.scan_levels_kw)},
+        "env_fixup": env_ctr,
         "limiter_fast": report.get("limiter_fast"),
         "loudnorm": report.get("stats"),
         "loudnorm_mode": report.get("modes"),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
-        x16 = oracle.quantize(x)
-        c = [(s - track.in0, n) for s, n in track.bounds]
-        t0 = time.perf_counter()
-        ref, _ = oracle.pipeline(x16, fs, settings, c)
-        dt = time.perf_counter() - t0
-        line["cpu_baseline"] = {"value": round(x16.shape[0] * 2 / dt / 1e6, 3), "unit": "Msamples/s",
-                                "cores": 1, "kind": "port",
-                                "sample": "full workload: 1 pass of the %.0f s track through the C "
-                                          "oracle (oracle/amx_oracle.c), single thread" % args.seconds,
-                                "seconds": round(dt, 3)}
-        # all-cores variant: the chunks are independent (:185-204), so a
-        # thread pool runs the oracle's chunk chain on them at once (ctypes releases the
-        # GIL); loudness, gain and the alimiter stay serial, as in the reference
-        threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1,
-                             len(c)))
-        from concurrent.futures import ThreadPoolExecutor
-        t0 = time.perf_counter()
-        with ThreadPoolExecutor(threads) as ex:
-            outs = list(ex.map(lambda sn: oracle.chunk(x16[sn[0]:sn[0] + sn[1]], fs, settings), c))
+        line.update(cpu_leg(args, runner, x, fs, settings, job, batch))
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_leg(args, runner, x, fs, settings, job, batch):
+    """cpu_baseline (the C oracle, 1 core, on a bounded sample of the workload) and
+    parity_vs_oracle (the oracle over the WHOLE workload, chunk chains on a thread
+    pool, compared bit for bit with the GPU output)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from concurrent.futures import ThreadPoolExecutor
+    out = {}
+    x16 = oracle.quantize(x)
+    if batch:
+        tracks = []
+        off = 0
+        for t in runner.tracks:
+            n = runner.track_frames[t]
+            tracks.append((x16[off:off + n], runner.track_bounds[t]))
+            off += n
+    else:
+        tracks = [(x16, [(s - runner.in0, n) for s, n in runner.bounds])]
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1, 16))
+
+    def pipeline_threaded(xt, bounds, ex):
+        outs = list(ex.map(lambda sn: oracle.chunk(xt[sn[0]:sn[0] + sn[1]], fs, settings), bounds))
         cat = np.concatenate(outs, axis=0)
         yy = cat
         if settings.get("lufs") is not None:
             mode, g = oracle.loudnorm_linear_gain(oracle.loudnorm_measure(cat, fs), float(settings["lufs"]))
             if mode == "linear":
                 yy = oracle.linear_gain(cat, g)
-        ref_p = oracle.alimiter(yy, fs)
-        dtp = time.perf_counter() - t0
-        line["cpu_baseline"]["all_cores"] = {
-            "value": round(x16.shape[0] * 2 / dtp / 1e6, 3), "cores": threads, "seconds": round(dtp, 3),
-            "what": "chunk chains on a thread pool, loudness + alimiter serial",
-            "same_output": bool(np.array_equal(ref_p, ref))}
-        y = job.y[:job.info.out_frames].cpu().numpy()
+        return oracle.alimiter(yy, fs)
+
+    # 1 core on a bounded sample: whole chunks of the first track, up to ~20 s of audio
+    # per... as many chunks as fit ~10-30 s of CPU (the whole 5-min track at C2/C3)
+    xt0, b0 = tracks[0]
+    nch = len(b0) if fs * args.seconds <= 48000 * 300 else max(1, min(len(b0), 10))
+    sb = b0[:nch]
+    s_end = sb[-1][0] + sb[-1][1]
+    t0 = time.perf_counter()
+    ref1, _ = oracle.pipeline(xt0[:s_end], fs, settings, sb)
+    dt = time.perf_counter() - t0
+    rp = REF_PY.get("c2" if args.config == "c2" else "c3")
+    out["cpu_baseline"] = {
+        "value": round(s_end * 2 / dt / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
+        "sample": "%d of %d chunks (%.0f s of audio) of the first track through the whole C oracle "
+                  "pipeline (oracle/amx_oracle.c), single thread" % (nch, len(b0), s_end / fs),
+        "seconds": round(dt, 3),
+        "reference_python_context": {
+            "value": rp[0], "unit": "Msamples/s", "cores": 1,
+            "what": "the reference's own Python chain (%s), BASELINE.md, survey container -- "
+                    "the C oracle above is faster than the reference itself" % rp[1]}}
+    # whole workload on all cores (chunk chains on a thread pool; loudness + alimiter
+    # serial per track, as in the reference) -- also the parity reference
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        refs = [pipeline_threaded(xt, b, ex) for xt, b in tracks]
+    dtp = time.perf_counter() - t0
+    tot = sum(xt.shape[0] for xt, _ in tracks)
+    out["cpu_baseline"]["all_cores"] = {
+        "value": round(tot * 2 / dtp / 1e6, 3), "cores": threads, "seconds": round(dtp, 3),
+        "what": "the whole workload: chunk chains on a thread pool, loudness + alimiter serial"}
+    if nch == len(b0):
+        out["cpu_baseline"]["all_cores"]["same_output_as_1_core"] = bool(np.array_equal(refs[0], ref1))
+    mx, ex_n, n_all = 0, 0, 0
+    for t, ref in enumerate(refs):
+        y = (job.track_output(t) if batch else job.y[:job.info.out_frames]).cpu().numpy()
+        if y.shape != ref.shape:
+            out["parity_vs_oracle"] = {"shape_mismatch": [list(y.shape), list(ref.shape)], "track": t}
+            return out
         d = np.abs(y.astype(np.int32) - ref.astype(np.int32))
-        line["parity_vs_oracle"] = {"max_abs_lsb": int(d.max()), "exact_frac": float((d == 0).mean())}
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+        mx = max(mx, int(d.max()))
+        ex_n += int((d == 0).sum())
+        n_all += d.size
+    out["parity_vs_oracle"] = {"max_abs_lsb": mx, "exact_frac": ex_n / max(1, n_all),
+                               "tracks": len(refs), "what": "whole workload, bit for bit"}
+    return out
 
 
 if __name__ == "__main__":

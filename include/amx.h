@@ -58,7 +58,8 @@ typedef struct amx_chain_desc {
     int32_t sample_rate;
     int32_t channels_in;          /* 1 or 2; mono is duplicated to stereo (:190) */
     int32_t input_s16;            /* 0: d_in is float32 (quantised on device like ffmpeg's
-                                     f32->s16 segment split, A.1); 1: d_in is int16 already */
+                                     f32->s16 segment split, A.1); 1: d_in is int16 already
+                                     (mono int16 is duplicated to stereo on the device) */
     int32_t pad0_;
     /* analog character (:258-266), applied if analog_on */
     int32_t analog_on;
@@ -164,12 +165,33 @@ AMX_API int amx_run_chunks(amx_plan *plan, const float *d_in, int16_t *d_out, vo
 #define AMX_STAGE_SCAN_XO 3  /* crossover scan */
 #define AMX_STAGE_XOVER 4    /* crossover -> 3 int16 bands */
 #define AMX_STAGE_RMS 5      /* exact audioop.rms detector per frame (block prefix sums) */
-#define AMX_STAGE_ENV 6      /* envelope: speculation + parallel fix rounds + gained bands */
-#define AMX_STAGE_FIX 7      /* envelope: in-order exactness walk (no-op when converged) */
+#define AMX_STAGE_ENV 6      /* envelope: speculation (every segment from a warmed-up guess) */
+#define AMX_STAGE_FIX 7      /* envelope: parallel fix rounds + in-order exactness walk */
 #define AMX_STAGE_APPLY 8    /* overlay of the gained bands -> chunk output */
 #define AMX_STAGE_COUNT 9
 AMX_API int amx_run_stage(amx_plan *plan, int32_t stage, const float *d_in, int16_t *d_out,
                           void *d_ws, void *stream);
+
+/* Input decode (the s16 conversion of ffmpeg's segment split, :178, + pydub's
+ * set_channels(2), :190): d_raw holds `frames` interleaved frames of `channels` (1 or
+ * 2) samples in `format`; d_out [frames][2] int16 receives what the split's s16 WAV
+ * chunks hold, mono duplicated to L = R.  Asynchronous on the stream.  A float32
+ * file needs no call: amx_run_chunks quantises it (input_s16 = 0). */
+#define AMX_PCM_U8 0      /* (v - 0x80) << 8 */
+#define AMX_PCM_S16 1     /* v */
+#define AMX_PCM_S24 2     /* 3-byte little-endian; v >> 8 */
+#define AMX_PCM_S32 3     /* v >> 16 */
+#define AMX_PCM_F32 4     /* clip(lrintf(v * 32768)) */
+#define AMX_PCM_F64 5     /* clip(lrint(v * 32768)) */
+AMX_API int amx_pcm_to_s16(const void *d_raw, int64_t frames, int32_t channels, int32_t format,
+                           int16_t *d_out, void *stream);
+
+/* Diagnostics of the compressor envelope's fix-up (AMX_STAGE_FIX) of the last step run
+ * on d_ws: per round r, out[4r..4r+3] = segments re-run, the most re-runs in one wave
+ * (the length of its chain of dependent fixes), waves with work, and the longest
+ * look-back (in 64-segment steps) of round 0's link search.  Synchronous (hipMemcpy):
+ * call it outside graph capture.  Replaces no reference line. */
+AMX_API int amx_env_counters(const amx_plan *plan, const void *d_ws, int32_t *out, int32_t n);
 
 /* Loudness pass 1 over d_out (libebur128 restated, ffmpeg loudnorm :229):
  * K-filter zero-state GEMV per segment + exact scan + sample peak.

@@ -218,3 +218,30 @@ def test_shard_geometry_matches_one_gpu_timeline():
             assert t0 == [sum(span[:r]) for r in range(world)]
         if not mb:
             assert out_n == [n for _, n in bounds]
+
+
+def _batch_worker(rank, world, port, frames):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        r = adist.shard_tracks(frames, world)
+        mine = torch.tensor(list(r[rank]), dtype=torch.int64)
+        allr = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        got = [tuple(int(v) for v in t) for t in allr]
+        # every rank derives the same split on its own: the runs tile the batch in
+        # order, no rank is empty, no track is in two ranks (no exchange needed)
+        assert got == r
+        assert got[0][0] == 0 and got[-1][1] == len(frames)
+        assert all(got[i][1] == got[i + 1][0] for i in range(world - 1))
+        assert all(b > a for a, b in got)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("frames", [[11520000] * 16, [5, 1, 1, 1, 1, 5, 2]])
+def test_batch_split_gloo_world2(frames):
+    """C4 batch split over two ranks (gloo): each rank's ShardedBatch share, agreed
+    without any exchange of data."""
+    mp.spawn(_batch_worker, args=(2, _free_port(), frames), nprocs=2, join=True)

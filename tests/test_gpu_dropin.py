@@ -1,0 +1,156 @@
+"""The file-level drop-in on the GPU: master_audio / process_audio
+(audio_mastering_engine.py:94-137, :171-226) from WAV files of every supported PCM
+format, mono and stereo, with recording callbacks.  The status strings and the
+progress sequence must be the reference's exactly, and the output WAV must equal
+the oracle's pipeline on the s16 chunks ffmpeg's split would write, bit for bit."""
+import os
+import shutil
+import tempfile
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+MB = dict(multiband=True, low_thresh=-25.0, low_ratio=6.0, mid_thresh=-20.0, mid_ratio=3.0,
+          high_thresh=-15.0, high_ratio=4.0)
+C3 = dict(bass_boost=-1.0, mid_cut=2.0, presence_boost=2.5, treble_boost=1.0, lufs=-14.0,
+          width=1.3, analog_character=40.0, **MB)
+
+
+def _native(x, code):
+    """float [-1, 1) signal -> the file's native samples for `code`."""
+    if code in ("f32", "f64"):
+        return x.astype(np.float32 if code == "f32" else np.float64)
+    if code == "u8":
+        return np.clip(np.round(x * 127.0) + 128, 0, 255).astype(np.uint8)
+    if code == "s16":
+        return np.clip(np.round(x * 32767.0), -32768, 32767).astype(np.int16)
+    if code == "s24":
+        return np.clip(np.round(x * 8388607.0), -8388608, 8388607).astype(np.int32)
+    return np.clip(np.round(x.astype(np.float64) * 2147483647.0), -2147483648, 2147483647).astype(np.int32)
+
+
+def _expected_calls(n_chunks, lufs):
+    n = n_chunks
+    st = ["Splitting audio into manageable chunks...", "Splitting complete."]
+    st += ["Processing chunk %d of %d..." % (i + 1, n) for i in range(n)]
+    st += ["Re-assembling processed chunks with concat filter...", "Concatenation complete."]
+    if lufs:
+        st += ["Normalizing final loudness..."]
+    st += ["Applying final limiting and exporting..."]
+    pr = [(0, 100)] + [(i + 1, n + 4) for i in range(n)] + [(n + 1, n + 4)]
+    if lufs:
+        pr += [(n + 2, n + 4)]
+    pr += [(n + 3, n + 4), (n + 4, n + 4)]
+    return st, pr
+
+
+@pytest.mark.parametrize("code,channels,seconds,settings", [
+    ("s16", 2, 64.0, C3), ("s16", 1, 31.0, dict(bass_boost=3.0, treble_boost=3.0)),
+    ("s24", 2, 33.0, C3), ("s24", 1, 12.0, dict(C3, lufs=None)),
+    ("f32", 2, 45.0, C3), ("f32", 1, 30.5, dict(bass_boost=-2.0, lufs=-16.0)),
+    ("u8", 2, 6.0, dict(mid_cut=2.0)), ("s32", 2, 8.0, C3), ("f64", 1, 7.0, dict(C3, width=1.0)),
+])
+def test_master_audio_files(gpu, oracle_mod, code, channels, seconds, settings):
+    import audio_mastering_engine as ame
+    from amx import synth, wavio
+    from amx.chunking import chunk_bounds, packet_frames
+    fs = 44100 if code in ("s16",) and channels == 1 else 48000
+    n = int(fs * seconds)
+    x = synth.mix_like(n, fs, channels, seed=int(seconds * 7) + channels)
+    if channels == 1:
+        x = x.reshape(-1)
+    nat = _native(x, code)
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "in.wav"), os.path.join(d, "out.wav")
+        wavio.write_wav_pcm(src, nat, fs, code)
+        st, pr = [], []
+        out = ame.master_audio(dict(settings, input_file=src, output_file=dst), st.append,
+                               lambda a, b: pr.append((a, b)))
+        assert out == dst
+        y, info = wavio.read_wav_native(dst)
+        # what ffmpeg's split writes (host restatement, test side only) + the oracle
+        raw, winfo, _ = wavio.read_wav_raw(src)
+        x16 = wavio.to_s16(wavio.read_wav_native(src)[0], winfo)
+        bounds = chunk_bounds(n, fs, packet_frames(winfo.block_align))
+    assert info.sample_rate == fs and info.bits == 16 and info.channels == 2
+    want_st, want_pr = _expected_calls(len(bounds), settings.get("lufs") is not None)
+    assert st == want_st
+    assert pr == want_pr
+    ref, _ = oracle_mod.pipeline(x16, fs, settings, bounds)
+    assert y.shape == ref.shape
+    d = np.abs(y.astype(np.int32) - ref.astype(np.int32))
+    assert d.max() == 0, "max |diff| %d LSB" % d.max()
+
+
+@pytest.mark.parametrize("code", ["u8", "s16", "s24", "s32", "f32", "f64"])
+@pytest.mark.parametrize("channels", [1, 2])
+def test_pcm_to_s16_decode(gpu, code, channels):
+    """amx_pcm_to_s16 equals the host restatement of ffmpeg's conversions on every
+    edge value (full scale, clipping floats, rounding ties, negative shifts)."""
+    import torch
+    from amx import capi, wavio
+    rng = np.random.default_rng(5)
+    n = 70001
+    if code in ("f32", "f64"):
+        edge = np.array([0.0, -0.0, 1.0, -1.0, 1.5, -1.5, 0.5 / 32768, 1.5 / 32768, -0.5 / 32768,
+                         32767.5 / 32768, -32768.5 / 32768, 2.5 / 32768])
+        v = np.concatenate([edge, rng.uniform(-1.2, 1.2, n * channels - edge.size)])
+        v = v.astype(np.float32 if code == "f32" else np.float64)
+    elif code == "u8":
+        v = rng.integers(0, 256, n * channels).astype(np.uint8)
+    elif code == "s16":
+        v = rng.integers(-32768, 32768, n * channels).astype(np.int16)
+    elif code == "s24":
+        v = np.concatenate([[-8388608, 8388607, -1, 0, 255, -256],
+                            rng.integers(-8388608, 8388608, n * channels - 6)]).astype(np.int32)
+    else:
+        v = np.concatenate([[-2147483648, 2147483647, -1, 0, 65535, -65536],
+                            rng.integers(-2147483648, 2147483648, n * channels - 6)]).astype(np.int32)
+    v = v.reshape(n, channels)
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "x.wav")
+        wavio.write_wav_pcm(p, v if channels == 2 else v.reshape(-1), 48000, code)
+        raw, info, c = wavio.read_wav_raw(p)
+        want = wavio.to_s16(wavio.read_wav_native(p)[0], info)
+    if channels == 1:
+        want = np.repeat(want.reshape(-1, 1), 2, axis=1)
+    d_raw = torch.from_numpy(np.ascontiguousarray(raw)).cuda()
+    out = torch.empty((n, 2), dtype=torch.int16, device="cuda")
+    capi.check(capi.load().amx_pcm_to_s16(capi.ptr(d_raw), n, channels, capi.PCM_FORMATS[c],
+                                          capi.ptr(out), capi.ptr_stream()), "amx_pcm_to_s16")
+    np.testing.assert_array_equal(out.cpu().numpy(), want)
+
+
+def test_process_audio_callbacks_and_mp3(gpu):
+    """process_audio (:94-137): success path with create_mp3 -- the external ffmpeg
+    when the box has one, else the reference's own failure message -- and the
+    error path's four callbacks."""
+    import audio_mastering_engine as ame
+    from amx import synth, wavio
+    fs = 48000
+    x = synth.mix_like(fs * 3, fs, 2, seed=9)
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "in.wav"), os.path.join(d, "out.wav")
+        wavio.write_wav_f32(src, x, fs)
+        st, pr, art, tag = [], [], [], []
+        ame.process_audio(dict(C3, input_file=src, output_file=dst, create_mp3=True), st.append,
+                          lambda a, b: pr.append((a, b)), art.append, tag.append)
+        assert os.path.exists(dst)
+        mp3 = ["Creating high-quality MP3..."]
+        if shutil.which("ffmpeg"):
+            mp3.append("High-quality MP3 created successfully.")
+            assert os.path.exists(os.path.join(d, "out.mp3"))
+        else:
+            mp3.append("Error: Failed to create MP3 file.")
+        k = st.index("Applying final limiting and exporting...")
+        assert st[k + 1:] == mp3 + ["Mastering complete. Preparing for AI analysis...",
+                                    "Success: Processing complete! (No art generated)"]
+        assert art == [None] and tag == []
+        # error path: a missing input file
+        st, pr, art, tag = [], [], [], []
+        ame.process_audio(dict(input_file=os.path.join(d, "nope.wav"), output_file=dst), st.append,
+                          lambda a, b: pr.append((a, b)), art.append, tag.append)
+        assert st[-1].startswith("Error: ") and pr[-1] == (0, 1)
+        assert art == [None] and tag == ["Processing failed."]

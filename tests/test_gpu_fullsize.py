@@ -1,0 +1,104 @@
+"""BASELINE configs at their real size against the oracle:
+
+* C5: one 60-minute stereo 96 kHz track, C3 settings, on one GPU;
+* C4: one rank's share of the 64 x 4 min batch -- 8 whole tracks in one plan
+  (amx.dist.ShardedBatch at world 1 of 8 would hold the same 8).
+
+The oracle's chunk chains run on a thread pool (the chunks are independent,
+audio_mastering_engine.py:185-204); its loudness measurement and alimiter run
+serially over each whole track, as the reference's ffmpeg passes do."""
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+MB = dict(multiband=True, low_thresh=-25.0, low_ratio=6.0, mid_thresh=-20.0, mid_ratio=3.0,
+          high_thresh=-15.0, high_ratio=4.0)
+C3 = dict(bass_boost=-1.0, mid_cut=2.0, presence_boost=2.5, treble_boost=1.0, lufs=-14.0,
+          width=1.3, analog_character=40.0, **MB)
+
+
+def _threads():
+    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1))
+
+
+def oracle_pipeline_threaded(oracle_mod, x16, fs, settings, bounds, ex):
+    outs = list(ex.map(lambda sn: oracle_mod.chunk(x16[sn[0]:sn[0] + sn[1]], fs, settings), bounds))
+    cat = np.concatenate(outs, axis=0)
+    st = None
+    y = cat
+    if settings.get("lufs") is not None:
+        st = oracle_mod.loudnorm_measure(cat, fs)
+        mode, g = oracle_mod.loudnorm_linear_gain(st, float(settings["lufs"]))
+        assert mode == "linear", (mode, st)
+        y = oracle_mod.linear_gain(cat, g)
+    return oracle_mod.alimiter(y, fs), st
+
+
+def _long_signal(n, fs, seed):
+    """A long program without a synthesis cost proportional to its length: a 5-minute
+    synthetic mix tiled, times a slow gain envelope (period ~17 min) so no two chunks
+    hold the same samples."""
+    from amx import synth
+    base = synth.mix_like(min(n, fs * 300), fs, 2, seed=seed)
+    reps = -(-n // base.shape[0])
+    x = np.tile(base, (reps, 1))[:n]
+    t = np.arange(n, dtype=np.float64) / fs
+    env = (0.75 + 0.25 * np.sin(2 * np.pi * t / 1020.0 + 0.3)).astype(np.float32)
+    x *= env[:, None]
+    return x
+
+
+def test_c5_60min_96k_vs_oracle(gpu, oracle_mod):
+    import torch
+    from amx.chunking import chunk_bounds
+    from amx.engine import master_array
+    fs = 96000
+    n = fs * 3600
+    x = _long_signal(n, fs, seed=55)
+    y, rep = master_array(torch.from_numpy(x), fs, C3, quantum=512)
+    y = y.cpu().numpy()
+    job = rep["job"]
+    ctr = job.env_counters()
+    print("C5 envelope fix-up counters per round:", ctr)
+    x16 = oracle_mod.quantize(x)
+    del x
+    with ThreadPoolExecutor(_threads()) as ex:
+        ref, st = oracle_pipeline_threaded(oracle_mod, x16, fs, C3, chunk_bounds(n, fs, 512), ex)
+    assert rep["stats"][0] == st, (rep["stats"], st)
+    assert y.shape == ref.shape
+    d = np.abs(y.astype(np.int32) - ref.astype(np.int32))
+    assert d.max() == 0, "C5: max |diff| %d LSB, exact %.8f" % (d.max(), float((d == 0).mean()))
+
+
+def test_c4_rank_share_8x4min_vs_oracle(gpu, oracle_mod):
+    """8 tracks of 4 minutes (one rank's share of configs[3]) in one plan, each track
+    against the oracle's whole pipeline on that track alone."""
+    import torch
+    from amx import synth
+    from amx.chunking import chunk_bounds
+    from amx.dist import ShardedBatch
+    fs = 48000
+    frames = [fs * 240] * 64
+    b = ShardedBatch(fs, 2, C3, frames, rank=3, world=8, quantum=512)
+    assert b.tracks == list(range(24, 32))
+    xs = [synth.mix_like(frames[t], fs, 2, seed=1000 + t) for t in b.tracks]
+    d_in = torch.from_numpy(np.ascontiguousarray(np.concatenate(xs))).cuda()
+    b.step(d_in)
+    rep = b.job.fetch_report()
+    assert rep["modes"] == ["linear"] * 8
+    with ThreadPoolExecutor(_threads()) as ex:
+        for k, t in enumerate(b.tracks):
+            x16 = oracle_mod.quantize(xs[k])
+            ref, st = oracle_pipeline_threaded(oracle_mod, x16, fs, C3, chunk_bounds(frames[t], fs, 512), ex)
+            assert rep["stats"][k] == st, (k, rep["stats"][k], st)
+            y = b.job.track_output(k).cpu().numpy()
+            assert y.shape == ref.shape
+            np.testing.assert_array_equal(y, ref, err_msg="track %d" % t)
+    # the graph replay (bench.py's timed path) gives the same batch output
+    y0 = b.job.y[:b.job.info.out_frames].clone()
+    b.capture(d_in)
+    assert torch.equal(b.replay(), y0)
