@@ -57,7 +57,7 @@ def _device_input(path):
     if info.channels not in (1, 2):
         raise ValueError("only mono and stereo inputs are supported (%d channels)" % info.channels)
     frames = raw.size // info.block_align
-    d_raw = torch.from_numpy(np.ascontiguousarray(raw)).to("cuda")
+    d_raw = torch.from_numpy(raw.copy()).to("cuda")
     if code == "f32":
         return d_raw.view(torch.float32), info.sample_rate, frames, info.channels, False, info.block_align
     if code == "s16" and info.channels == 2:

@@ -389,92 +389,292 @@ EXPORT void orc_kweight_coefs(int fs, double *b, double *a) {
     a[4] = pa[2] * ra[2];
 }
 
-/* Streaming libebur128 (MODE_I | MODE_LRA | MODE_SAMPLE_PEAK) over an s16 track
- * fed as doubles x/32768 (what loudnorm receives, at the native rate here --
- * ffmpeg's loudnorm pass 1 resamples to 192 kHz first: not reproduced).
- * Outputs the gating-block histogram, the short-term (LRA) histogram, per
- * channel sample peak and the number of gating blocks. */
+/* Streaming libebur128 state (MODE_I | MODE_LRA | MODE_SAMPLE_PEAK), FFmpeg's
+ * libavfilter/ebur128.c: ff_ebur128_add_frames_double() -> ebur128_filter (sample
+ * peak, 4th-order DF-II K filter, DBL_MIN flush at the end of every filter call),
+ * ebur128_calc_gating_block (400 ms blocks every 100 ms, 3 s short-term blocks
+ * every 1 s) into the 1000-bin histograms. */
+typedef struct {
+    int channels;
+    double b[5], a[5];
+    size_t h100, ring_frames, idx, needed, st_counter;
+    double *ring;
+    double v[8][5];
+    uint64_t *hist, *st_hist;
+    double peak[8];
+    int64_t nb;
+} Ebur;
+
+static void ebur_init(Ebur *e, int fs, int channels, uint64_t *hist, uint64_t *st_hist) {
+    orc_ebur128_tables(NULL, NULL);
+    memset(e, 0, sizeof *e);
+    e->channels = channels;
+    orc_kweight_coefs(fs, e->b, e->a);
+    e->h100 = (size_t)((fs + 5) / 10);
+    e->ring_frames = (size_t)fs * 3000 / 1000;
+    if (e->ring_frames % e->h100) e->ring_frames = (e->ring_frames + e->h100) - (e->ring_frames % e->h100);
+    e->ring = (double *)calloc(e->ring_frames * channels, sizeof(double));
+    e->hist = hist;
+    e->st_hist = st_hist;
+    memset(hist, 0, 1000 * sizeof(uint64_t));
+    memset(st_hist, 0, 1000 * sizeof(uint64_t));
+    e->needed = e->h100 * 4;
+}
+
+/* ebur128_filter_double on `take` interleaved frames */
+static void ebur_filter(Ebur *e, const double *x, size_t take) {
+    const int ch = e->channels;
+    for (int c = 0; c < ch; c++) {
+        double mx = 0.0;
+        for (size_t i = 0; i < take; i++) {
+            double s = x[i * ch + c];
+            if (s > mx) mx = s; else if (-s > mx) mx = -1.0 * s;
+        }
+        if (mx > e->peak[c]) e->peak[c] = mx;
+    }
+    const double *a = e->a, *b = e->b;
+    for (int c = 0; c < ch; c++) {
+        double *v = e->v[c];
+        for (size_t i = 0; i < take; i++) {
+            v[0] = x[i * ch + c] - a[1] * v[1] - a[2] * v[2] - a[3] * v[3] - a[4] * v[4];
+            e->ring[e->idx + i * ch + c] = b[0] * v[0] + b[1] * v[1] + b[2] * v[2] + b[3] * v[3] + b[4] * v[4];
+            v[4] = v[3]; v[3] = v[2]; v[2] = v[1]; v[1] = v[0];
+        }
+        for (int k = 1; k < 5; k++) v[k] = fabs(v[k]) < DBL_MIN ? 0.0 : v[k];
+    }
+}
+
+static double ebur_block_energy(const Ebur *e, size_t fpb) {
+    const int ch = e->channels;
+    double sum = 0.0;
+    for (int c = 0; c < ch; c++) {
+        double cs = 0.0;
+        if (e->idx < fpb * ch) {
+            for (size_t i = 0; i < e->idx / ch; ++i) cs += e->ring[i * ch + c] * e->ring[i * ch + c];
+            for (size_t i = e->ring_frames - (fpb - e->idx / ch); i < e->ring_frames; ++i)
+                cs += e->ring[i * ch + c] * e->ring[i * ch + c];
+        } else {
+            for (size_t i = e->idx / ch - fpb; i < e->idx / ch; ++i) cs += e->ring[i * ch + c] * e->ring[i * ch + c];
+        }
+        sum += cs;
+    }
+    return sum / (double)fpb;
+}
+
+/* ff_ebur128_add_frames_double: one call, split at the block boundaries */
+static void ebur_add(Ebur *e, const double *x, size_t frames) {
+    const int ch = e->channels;
+    size_t src = 0;
+    while (frames > 0) {
+        if (frames >= e->needed) {
+            ebur_filter(e, x + src * ch, e->needed);
+            src += e->needed;
+            frames -= e->needed;
+            e->idx += e->needed * ch;
+            double en = ebur_block_energy(e, e->h100 * 4);       /* gating block */
+            e->nb++;
+            if (en >= hist_bounds[0]) ++e->hist[find_hist_index(en)];
+            e->st_counter += e->needed;
+            if (e->st_counter == e->h100 * 30) {
+                double st = ebur_block_energy(e, e->h100 * 30);
+                if (st >= hist_bounds[0]) ++e->st_hist[find_hist_index(st)];
+                e->st_counter = e->h100 * 20;
+            }
+            e->needed = e->h100;
+            if (e->idx == e->ring_frames * ch) e->idx = 0;
+        } else {
+            ebur_filter(e, x + src * ch, frames);
+            e->idx += frames * ch;
+            e->st_counter += frames;
+            e->needed -= frames;
+            frames = 0;
+        }
+    }
+}
+
+/* libebur128 over an s16 track fed as doubles x/32768 at its own rate, as ONE
+ * add_frames call (kept for the EBU Tech 3341/3342 known answers; ffmpeg's
+ * loudnorm pass 1 measures at 192 kHz, orc_ebur128_192k below). */
 EXPORT void orc_ebur128(const int16_t *x, int64_t n, int fs, int channels,
                         uint64_t *hist, uint64_t *st_hist, double *peak,
                         int64_t *n_blocks) {
-    orc_ebur128_tables(NULL, NULL);
-    double b[5], a[5];
-    orc_kweight_coefs(fs, b, a);
-    const size_t h100 = (size_t)((fs + 5) / 10);
-    size_t ring_frames = (size_t)fs * 3000 / 1000;
-    if (ring_frames % h100) ring_frames = (ring_frames + h100) - (ring_frames % h100);
-    double *ring = (double *)calloc(ring_frames * channels, sizeof(double));
-    double v[8][5];
-    memset(v, 0, sizeof(v));
-    memset(hist, 0, 1000 * sizeof(uint64_t));
-    memset(st_hist, 0, 1000 * sizeof(uint64_t));
-    for (int c = 0; c < channels; c++) peak[c] = 0.0;
-    size_t idx = 0;               /* audio_data_index, in samples */
-    size_t needed = h100 * 4;
-    size_t st_counter = 0;
-    int64_t nb = 0;
-    int64_t pos = 0;
-    while (pos < n) {
-        size_t take = (size_t)(n - pos) >= needed ? needed : (size_t)(n - pos);
-        /* sample peak */
-        for (int c = 0; c < channels; c++) {
-            double mx = 0.0;
-            for (size_t i = 0; i < take; i++) {
-                double s = (double)x[(pos + i) * channels + c] * (1.0 / 32768.0);
-                if (s > mx) mx = s; else if (-s > mx) mx = -1.0 * s;
-            }
-            if (mx > peak[c]) peak[c] = mx;
+    Ebur e;
+    ebur_init(&e, fs, channels, hist, st_hist);
+    double *buf = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1) * channels);
+    for (int64_t i = 0; i < n * channels; i++) buf[i] = (double)x[i] * (1.0 / 32768.0);
+    ebur_add(&e, buf, (size_t)n);
+    for (int c = 0; c < channels; c++) peak[c] = e.peak[c];
+    *n_blocks = e.nb;
+    free(buf);
+    free(e.ring);
+}
+
+/* ------------------------------------- libswresample: s16 -> 192 kHz float
+ * ffmpeg's loudnorm pass 1 (:229) gets no measured_* values, so af_loudnorm is in
+ * dynamic mode and asks for 192 kHz input (query_formats); ffmpeg auto-inserts a
+ * resampler: libswresample with its defaults (swresample options.c): filter_size
+ * 32, phase_shift 10, linear_interp 1, exact_rational 1, cutoff 0 -> 0.97, Kaiser
+ * window beta 9.  s16 in / dbl out picks the FLTP internal format (swr_init), so
+ * the filter bank is float32 and every output sample is a float32 dot product.
+ * Restated from resample.c (build_filter, bessel, resample_init,
+ * invert_initial_buffer, resample_flush) and the float kernel's order of operations
+ * on an x86-64 host with FMA3 (resample.asm, ymm: 8 fused chains over taps
+ * k, k+8, k+16, k+24, then (a0+a4 + a2+a6) + (a1+a5 + a3+a7)).  With exact_rational
+ * the phase step is an integer (frac stays 0), so linear interpolation adds 0.
+ * PARITY UNPINNED: no ffmpeg binary or fixture exists here; a host without FMA3
+ * sums in another order (differences of float32 rounding in the measured values). */
+#define SWR_TAPS 32
+#define SWR_CENTER 15            /* (taps - 1) / 2 */
+
+static double swr_bessel(double x) {
+    double lastv = 0, t, v;
+    double inv[100];
+    for (int k = 0; k < 100; k++) inv[k] = 1.0 / ((double)(k + 1) * (double)(k + 1));
+    x = x * x / 4;
+    t = x;
+    v = 1 + x;
+    for (int i = 1; v != lastv; i += 2) {
+        t *= x * inv[i];
+        v += t;
+        lastv = v;
+        t *= x * inv[i + 1];
+        v += t;
+    }
+    return v;
+}
+
+static int64_t gcd64(int64_t a, int64_t b) { while (b) { int64_t t = a % b; a = b; b = t; } return a; }
+
+/* L = out/g phases, M = in/g phase step; 0 = supported (exact rational, L <= 1024,
+ * upsampling), else -1 */
+EXPORT int orc_swr_geometry(int in_rate, int out_rate, int *L, int *M) {
+    if (in_rate <= 0 || out_rate <= 0) return -1;
+    int64_t g = gcd64(in_rate, out_rate);
+    int64_t l = out_rate / g, m = in_rate / g;
+    if (l > 1024) return -1;
+    if ((double)out_rate * 0.97 / in_rate < 1.0 && !(l == 1 && m == 1)) return -1;   /* downsampling */
+    *L = (int)l;
+    *M = (int)m;
+    return 0;
+}
+
+/* build_filter (factor 1: upsampling, Kaiser, FLTP, scale 1): bank[ph][i], ph < L */
+EXPORT int orc_swr_bank(int in_rate, int out_rate, float *bank) {
+    int L, M;
+    if (orc_swr_geometry(in_rate, out_rate, &L, &M)) return -1;
+    const int pc = L, tap_count = SWR_TAPS, center = SWR_CENTER;
+    const int ph_nb = pc % 2 ? pc : pc / 2 + 1;
+    const double factor = 1.0, beta = 9.0;
+    double tab[SWR_TAPS];
+    double *sin_lut = (double *)malloc(sizeof(double) * ph_nb);
+    double norm = 0;
+    for (int ph = 0; ph < ph_nb; ph++) sin_lut[ph] = sin(M_PI * ph / pc) * (center & 1 ? 1 : -1);
+    for (int ph = 0; ph < ph_nb; ph++) {
+        double s = sin_lut[ph];
+        for (int i = 0; i < tap_count; i++) {
+            double x = M_PI * ((double)(i - center) - (double)ph / pc) * factor;
+            double y;
+            if (x == 0) y = 1.0;
+            else y = s / x;                                    /* factor == 1.0 */
+            double w = 2.0 * x / (factor * tap_count * M_PI);
+            y *= swr_bessel(beta * sqrt(fmax(1 - w * w, 0)));
+            tab[i] = y;
+            s = -s;
+            if (!ph) norm += y;
         }
-        /* K filter (4th-order DF-II as in libebur128) */
+        for (int i = 0; i < tap_count; i++) bank[ph * tap_count + i] = (float)(tab[i] * 1 / norm);
+        if (pc % 2) continue;
+        for (int i = 0; i < tap_count; i++)
+            if (pc - ph < pc) bank[(pc - ph) * tap_count + tap_count - 1 - i] = bank[ph * tap_count + i];
+    }
+    free(sin_lut);
+    return 0;
+}
+
+EXPORT int64_t orc_swr_out_frames(int64_t n, int in_rate, int out_rate) {
+    int L, M;
+    if (orc_swr_geometry(in_rate, out_rate, &L, &M)) return -1;
+    return (n * L + M - 1) / M;
+}
+
+/* input sample k of the stream the resampler sees: mirrored at both ends
+ * (invert_initial_buffer: x[-k] = x[k]; resample_flush: x[n+j] = x[n-1-j]) */
+static inline int64_t swr_reflect(int64_t k, int64_t n) {
+    for (;;) {
+        if (k < 0) k = -k;
+        else if (k >= n) k = 2 * n - 1 - k;
+        else return k;
+    }
+}
+
+/* the float kernel's order (see above) */
+static inline float swr_dot(const float *w, const float *h) {
+    float a[8];
+    for (int k = 0; k < 8; k++) {
+        float acc = fmaf(w[k], h[k], 0.0f);
+        acc = fmaf(w[k + 8], h[k + 8], acc);
+        acc = fmaf(w[k + 16], h[k + 16], acc);
+        acc = fmaf(w[k + 24], h[k + 24], acc);
+        a[k] = acc;
+    }
+    const float b0 = a[0] + a[4], b1 = a[1] + a[5], b2 = a[2] + a[6], b3 = a[3] + a[7];
+    return (b0 + b2) + (b1 + b3);
+}
+
+/* output frames [j0, j1) of the 192 kHz stream, interleaved doubles */
+static void swr_block(const int16_t *x, int64_t n, int channels, int L, int M, const float *bank,
+                      int64_t j0, int64_t j1, double *out) {
+    float w[SWR_TAPS];
+    for (int64_t j = j0; j < j1; j++) {
+        const int64_t idx = j * M, base = idx / L;
+        const int ph = (int)(idx % L);
         for (int c = 0; c < channels; c++) {
-            for (size_t i = 0; i < take; i++) {
-                double s = (double)x[(pos + i) * channels + c] * (1.0 / 32768.0);
-                v[c][0] = s - a[1] * v[c][1] - a[2] * v[c][2] - a[3] * v[c][3] - a[4] * v[c][4];
-                ring[idx + i * channels + c] = b[0] * v[c][0] + b[1] * v[c][1] + b[2] * v[c][2] +
-                                               b[3] * v[c][3] + b[4] * v[c][4];
-                v[c][4] = v[c][3]; v[c][3] = v[c][2]; v[c][2] = v[c][1]; v[c][1] = v[c][0];
-            }
-            for (int k = 1; k < 5; k++) v[c][k] = fabs(v[c][k]) < DBL_MIN ? 0.0 : v[c][k];
-        }
-        pos += (int64_t)take;
-        idx += take * channels;
-        st_counter += take;
-        if (take == needed) {
-            /* gating block of 4*h100 frames (ebur128_calc_gating_block) */
-            for (int pass = 0; pass < 2; pass++) {
-                size_t fpb = pass == 0 ? h100 * 4 : h100 * 30;
-                if (pass == 1 && st_counter != h100 * 30) continue;
-                double sum = 0.0;
-                for (int c = 0; c < channels; c++) {
-                    double cs = 0.0;
-                    if (idx < fpb * channels) {
-                        for (size_t i = 0; i < idx / channels; ++i)
-                            cs += ring[i * channels + c] * ring[i * channels + c];
-                        for (size_t i = ring_frames - (fpb - idx / channels); i < ring_frames; ++i)
-                            cs += ring[i * channels + c] * ring[i * channels + c];
-                    } else {
-                        for (size_t i = idx / channels - fpb; i < idx / channels; ++i)
-                            cs += ring[i * channels + c] * ring[i * channels + c];
-                    }
-                    sum += cs;
-                }
-                sum /= (double)fpb;
-                if (pass == 0) {
-                    nb++;
-                    if (sum >= hist_bounds[0]) ++hist[find_hist_index(sum)];
-                } else {
-                    if (sum >= hist_bounds[0]) ++st_hist[find_hist_index(sum)];
-                    st_counter = h100 * 20;
-                }
-            }
-            needed = h100;
-            if (idx == ring_frames * channels) idx = 0;
-        } else {
-            needed -= take;
+            for (int i = 0; i < SWR_TAPS; i++)
+                w[i] = (float)x[swr_reflect(base - SWR_CENTER + i, n) * channels + c] * (1.0f / 32768.0f);
+            out[(j - j0) * channels + c] = (double)swr_dot(w, bank + (size_t)ph * SWR_TAPS);
         }
     }
-    *n_blocks = nb;
-    free(ring);
+}
+
+/* the upsampled stream itself (tests: small inputs) */
+EXPORT int orc_upsample(const int16_t *x, int64_t n, int channels, int in_rate, int out_rate,
+                        double *out) {
+    int L, M;
+    if (orc_swr_geometry(in_rate, out_rate, &L, &M)) return -1;
+    float *bank = (float *)malloc(sizeof(float) * (size_t)L * SWR_TAPS);
+    orc_swr_bank(in_rate, out_rate, bank);
+    swr_block(x, n, channels, L, M, bank, 0, orc_swr_out_frames(n, in_rate, out_rate), out);
+    free(bank);
+    return 0;
+}
+
+/* loudnorm pass 1 as ffmpeg runs it: the s16 track resampled to 192 kHz and fed to
+ * libebur128 in af_loudnorm's dynamic-mode frames (first min(3 s, all), then
+ * 100 ms at a time: these calls set where the K filter's DBL_MIN flush happens). */
+EXPORT int orc_ebur128_192k(const int16_t *x, int64_t n, int fs, int channels,
+                            uint64_t *hist, uint64_t *st_hist, double *peak, int64_t *n_blocks) {
+    const int out_rate = 192000;
+    int L, M;
+    if (orc_swr_geometry(fs, out_rate, &L, &M)) return -1;
+    float *bank = (float *)malloc(sizeof(float) * (size_t)L * SWR_TAPS);
+    orc_swr_bank(fs, out_rate, bank);
+    const int64_t n_out = n > 0 ? orc_swr_out_frames(n, fs, out_rate) : 0;
+    const int64_t first = (int64_t)out_rate * 3, step = (int64_t)out_rate / 10;
+    double *buf = (double *)malloc(sizeof(double) * (size_t)first * channels);
+    Ebur e;
+    ebur_init(&e, out_rate, channels, hist, st_hist);
+    for (int64_t j = 0; j < n_out;) {
+        const int64_t take = (j == 0 ? first : step) < n_out - j ? (j == 0 ? first : step) : n_out - j;
+        swr_block(x, n, channels, L, M, bank, j, j + take, buf);
+        ebur_add(&e, buf, (size_t)take);
+        j += take;
+    }
+    for (int c = 0; c < channels; c++) peak[c] = e.peak[c];
+    *n_blocks = e.nb;
+    free(buf);
+    free(bank);
+    free(e.ring);
+    return 0;
 }
 
 /* ------------------------------------------------------------ alimiter */

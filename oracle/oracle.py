@@ -57,6 +57,7 @@ def lib():
         L.orc_overlay_len.restype = _i64
         L.orc_overlay3.restype = _i64
         L.orc_chunk.restype = _i64
+        L.orc_swr_out_frames.restype = _i64
         _lib = L
     return _lib
 
@@ -270,6 +271,47 @@ def ebur128(x16, fs):
     return hist, st_hist, peak, int(nb.value)
 
 
+def ebur128_192k(x16, fs):
+    """libebur128 over the track resampled to 192 kHz as ffmpeg's loudnorm pass 1
+    does (amx_oracle.c orc_ebur128_192k)."""
+    x16 = np.ascontiguousarray(x16, np.int16)
+    ch = x16.shape[1]
+    hist = np.zeros(1000, np.uint64)
+    st_hist = np.zeros(1000, np.uint64)
+    peak = np.zeros(ch, np.float64)
+    nb = _i64(0)
+    rc = lib().orc_ebur128_192k(_p(x16, _i16p), _i64(x16.shape[0]), ctypes.c_int(fs), ctypes.c_int(ch),
+                                _p(hist, _u64p), _p(st_hist, _u64p), _p(peak, _f64p), ctypes.byref(nb))
+    if rc != 0:
+        raise ValueError("no 192 kHz resampler for %d Hz input" % fs)
+    return hist, st_hist, peak, int(nb.value)
+
+
+def swr_geometry(fs, out_rate=192000):
+    L, M = ctypes.c_int(), ctypes.c_int()
+    if lib().orc_swr_geometry(ctypes.c_int(fs), ctypes.c_int(out_rate), ctypes.byref(L), ctypes.byref(M)):
+        raise ValueError("unsupported rate %d" % fs)
+    return L.value, M.value
+
+
+def swr_bank(fs, out_rate=192000):
+    L, _ = swr_geometry(fs, out_rate)
+    bank = np.zeros((L, 32), np.float32)
+    lib().orc_swr_bank(ctypes.c_int(fs), ctypes.c_int(out_rate), _p(bank, _f32p))
+    return bank
+
+
+def upsample(x16, fs, out_rate=192000):
+    """the 192 kHz float stream (as doubles) the pass-1 measurement sees"""
+    x16 = np.ascontiguousarray(x16, np.int16)
+    ch = x16.shape[1]
+    n_out = int(lib().orc_swr_out_frames(_i64(x16.shape[0]), ctypes.c_int(fs), ctypes.c_int(out_rate)))
+    out = np.zeros((max(n_out, 0), ch), np.float64)
+    lib().orc_upsample(_p(x16, _i16p), _i64(x16.shape[0]), ctypes.c_int(ch), ctypes.c_int(fs),
+                       ctypes.c_int(out_rate), _p(out, _f64p))
+    return out
+
+
 def ebur128_tables():
     e = np.zeros(1000, np.float64)
     b = np.zeros(1001, np.float64)
@@ -311,9 +353,10 @@ def loudness_stats(hist, st_hist):
     return float(out[0]), float(out[1]), float(out[2])
 
 
-def loudnorm_measure(x16, fs):
-    """pass-1 JSON 'input_*' strings (native-rate restatement, see amx_oracle.c)."""
-    hist, st, peak, _ = ebur128(x16, fs)
+def loudnorm_measure(x16, fs, native=False):
+    """pass-1 JSON 'input_*' strings: ffmpeg measures the track resampled to 192 kHz
+    (amx_oracle.c orc_ebur128_192k); native=True measures at the track's own rate."""
+    hist, st, peak, _ = ebur128(x16, fs) if native else ebur128_192k(x16, fs)
     I, lra, thr = loudness_stats(hist, st)
     tp = float(peak.max()) if peak.size else 0.0
     tp_db = 20.0 * np.log10(tp) if tp > 0 else -np.inf

@@ -130,7 +130,7 @@ def test_process_audio_callbacks_and_mp3(gpu):
     import audio_mastering_engine as ame
     from amx import synth, wavio
     fs = 48000
-    x = synth.mix_like(fs * 3, fs, 2, seed=9)
+    x = synth.mix_like(fs * 12, fs, 2, seed=9)     # long enough for a loudness range (linear mode)
     with tempfile.TemporaryDirectory() as d:
         src, dst = os.path.join(d, "in.wav"), os.path.join(d, "out.wav")
         wavio.write_wav_f32(src, x, fs)
