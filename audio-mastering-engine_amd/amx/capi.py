@@ -14,10 +14,11 @@ c_double_p = ctypes.POINTER(ctypes.c_double)
 c_float_p = ctypes.POINTER(ctypes.c_float)
 
 AMX_OK, AMX_EINVAL, AMX_EHIP, AMX_ENOMEM, AMX_ERANGE = 0, -1, -2, -3, -4
-ABI_VERSION = 2
+ABI_VERSION = 3
 CTL_FAST = 1
 MODES = ("off", "skip", "linear", "dynamic")
 STATS = 16
+UP_EDGE = 16      # frames of a neighbour rank the 192 kHz resampler window reaches (amx.h)
 STAGES = ("front1", "scan_eq", "front2", "scan_xo", "xover", "rms", "env", "fix", "apply")
 
 
@@ -68,7 +69,8 @@ class PlanInfo(ctypes.Structure):
                 ("n_segments", ctypes.c_int64), ("seg_frames", ctypes.c_int32),
                 ("scan_levels_eq", ctypes.c_int32), ("scan_levels_xover", ctypes.c_int32),
                 ("scan_levels_kw", ctypes.c_int32), ("eq_dim", ctypes.c_int32),
-                ("hop_frames", ctypes.c_int32)]
+                ("hop_frames", ctypes.c_int32), ("meas_rate", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("max_hops", ctypes.c_int64)]
 
 
 class TrackSpan(ctypes.Structure):
@@ -110,11 +112,11 @@ def load(path=None):
     L.amx_plan_track_span.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(TrackSpan)]
     L.amx_run_chunks.argtypes = [vp, vp, vp, vp, vp]
     L.amx_run_stage.argtypes = [vp, ctypes.c_int32, vp, vp, vp, vp]
-    L.amx_loudness_pass1.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.amx_loudness_pass1.argtypes = [vp, vp, vp, vp, vp, vp, vp]
     L.amx_pcm_to_s16.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, vp, vp]
     L.amx_env_counters.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]
     L.amx_kw_propagate.argtypes = [vp, ctypes.c_int64, c_double_p, c_double_p]
-    L.amx_loudness_pass2.argtypes = [vp, vp, vp, vp, ctypes.c_int64, vp, vp]
+    L.amx_loudness_pass2.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int64, vp, vp]
     L.amx_loudness_histograms.argtypes = [vp, vp, ctypes.c_int64, vp, vp, vp, vp]
     L.amx_limiter_geometry.argtypes = [vp, ctypes.POINTER(FinalDesc), ctypes.POINTER(ctypes.c_int32),
                                        ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]

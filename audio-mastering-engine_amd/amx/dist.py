@@ -6,6 +6,10 @@ audio_mastering_engine.py:178); rank r owns a contiguous run of chunks.  The chu
 chain needs no communication (all DSP state resets per chunk, :185-204).  The
 exchange steps are the track-level ones:
 
+0. Edges: the loudness measurement resamples the track to 192 kHz (ffmpeg's
+   pass 1), whose 32-tap window reaches 16 frames into each neighbour's span, and
+   the alimiter's look-ahead needs the previous rank's last B - 1 frames: one
+   all-gather of every rank's first and last frames, right after the chunk chain.
 1. K-filter carry (loudnorm measurement is continuous over the concatenated
    track): all-gather each rank's zero-start tail state (8 doubles), then
    carry(r) = sum_{q<r} A^{frames between span q and span r} tail(q) on the device
@@ -187,7 +191,17 @@ def chain_state_speculative(state, run, is_rest, rank, world, group=None, first_
 
 
 class ShardedTrack:
-    """This rank's part of one chunk-sharded track."""
+    """This rank's part of one chunk-sharded track.
+
+    A step has three exchanges (every one a single collective over all ranks):
+      1. edges: each rank's first 16 and last max(16, B - 1) output frames, all-gathered
+         as raw bytes -- the 192 kHz resampler window of the loudness measurement
+         reaches 16 frames into both neighbours, and the alimiter's look-ahead ring
+         needs the previous rank's last B - 1 frames;
+      2. K-filter tails (8 doubles) and sample peaks (4 doubles), all-gathered: every
+         rank builds its incoming K-filter state (amx_kw_carry) and the track's peaks;
+      3. hop energies, all-reduced (SUM).
+    """
 
     def __init__(self, sample_rate, channels_in, settings, track_frames, rank, world, *,
                  quantum=None, input_s16=False, seg_frames=128, group=None):
@@ -211,26 +225,78 @@ class ShardedTrack:
         self.job = MasteringJob(fs, channels_in, settings, [self.local_frames], chunks=chunks,
                                 track_frame0=[self.tframe0], track_total=[self.ttotal],
                                 input_s16=input_s16, seg_frames=seg_frames)
-        self.halo_all = None
         if world > 1:
             frames_after = [sum(self.span_frames[q + 1:rank]) for q in range(rank)]
             self.job.plan.kw_carry_setup(frames_after)
-            self.tails_all = torch.zeros((world, 2, 4), dtype=torch.float64, device=self.job.device)
+            dev = self.job.device
+            self.tails_all = torch.zeros((world, 2, 4), dtype=torch.float64, device=dev)
+            from . import capi
+            self.ne = capi.UP_EDGE                                  # frames after the span start
+            self.nl = max(capi.UP_EDGE, self.job.halo_frames)       # frames before the span end
+            fw = (4 * (self.ne + self.nl) + 7) // 8                 # doubles holding them
+            self._ebuf = torch.zeros(fw, dtype=torch.float64, device=dev)
+            self._eall = torch.zeros(world * fw, dtype=torch.float64, device=dev)
+            self._xbuf = torch.zeros(12, dtype=torch.float64, device=dev)
+            self._xall = torch.zeros(world * 12, dtype=torch.float64, device=dev)
 
     # -------------------------------------------------------------- exchanges
-    def exchange_carry(self):
-        job = self.job
-        gather_tails(job.kw_tail, self.tails_all, self.group)
+    def _all_gather(self, out, inp):
+        (a, b), st = _staged(self.group, out, inp)
+        dist.all_gather_into_tensor(a, b, group=self.group)
+        if st:
+            out.copy_(a)
+
+    def _pack_edges(self):
+        """This span's first ne and last nl output frames (zero-padded when shorter)."""
+        job, n = self.job, self.span_frames[self.rank]
+        b = self._ebuf.view(torch.uint8)
+        b.zero_()
+        m = min(self.ne, n)
+        if m > 0:
+            b[:4 * m].copy_(job.out[:m].contiguous().view(torch.uint8).reshape(-1))
+        m = min(self.nl, n)
+        if m > 0:
+            o = 4 * (self.ne + self.nl - m)
+            b[o:o + 4 * m].copy_(job.out[n - m:n].contiguous().view(torch.uint8).reshape(-1))
+
+    def _unpack_edges(self):
+        """Previous rank's last frames -> the resampler's low edge and the limiter halo;
+        next rank's first frames -> the resampler's high edge."""
+        job, r, world = self.job, self.rank, self.world
+        ea = self._eall.view(world, -1).view(torch.uint8)
+        ne, nl, E = self.ne, self.nl, job.edge.shape[2]
+        if r > 0:
+            last = ea[r - 1][4 * ne:4 * (ne + nl)].view(torch.int16).reshape(nl, 2)
+            job.edge[0, 0].copy_(last[nl - E:])
+            h = job.halo_frames
+            if h > 0:
+                job.halo[0, :h].copy_(last[nl - h:])
+        if r < world - 1:
+            job.edge[0, 1].copy_(ea[r + 1][:4 * E].view(torch.int16).reshape(E, 2))
+
+    def exchange_edges(self):
+        self._pack_edges()
+        self._all_gather(self._eall, self._ebuf)
+        self._unpack_edges()
+
+    def _pack_x(self):
+        xb, job = self._xbuf, self.job
+        xb[0:8].copy_(job.kw_tail.reshape(-1)[:8])
+        xb[8:12].copy_(job.peak.reshape(-1)[:4])
+
+    def _unpack_x(self):
         from . import capi
+        job, world = self.job, self.world
+        xa = self._xall.view(world, -1)
+        self.tails_all.copy_(xa[:, 0:8].reshape(world, 2, 4))
         capi.check(capi.load().amx_kw_carry(job.plan.h, capi.ptr(self.tails_all), capi.ptr(job.kw_carry),
                                             job._s(None)), "amx_kw_carry")
+        job.peak.reshape(-1)[:4].copy_(xa[:, 8:12].amax(0))
 
-    def exchange_halo(self):
-        job = self.job
-        h = job.halo_frames
-        prev = gather_halo(job.out, self.span_frames[self.rank], h, self.rank, self.world, self.group)
-        if prev is not None:
-            job.halo[0, :h].copy_(prev)
+    def exchange_carry_peaks(self):
+        self._pack_x()
+        self._all_gather(self._xall, self._xbuf)
+        self._unpack_x()
 
     def limiter_sequential(self):
         job = self.job
@@ -241,29 +307,21 @@ class ShardedTrack:
     def capture(self, d_in):
         """Record the step's device work as hipGraphs (torch.cuda.CUDAGraph over HIP
         stream capture).  One rank: the whole step (MasteringJob.capture).  N ranks:
-        the stretches between the step's two collectives, each one graph:
-          G1  chunk chain, loudness pass 1, and packing this rank's exchange word --
-              K-filter tail (8 doubles), sample peaks (2), limiter halo (the span's
-              last B-1 frames as raw bytes) -- into one buffer;
-          all-gather of those buffers (everything every rank needs from the others
-              once the chunk chain is done, in ONE collective instead of three);
-          G2  unpack: carry from the tails (amx_kw_carry), peak = max over ranks, the
-              previous rank's halo; loudness pass 2;
+        the stretches between the step's three collectives, each one graph:
+          G1  chunk chain, packing the span's edge frames;
+          all-gather of the edges;
+          G2  unpacking them, loudness pass 1 (GEMV + scan from rest + tail + peaks),
+              packing tail and peaks;
+          all-gather of tails and peaks;
+          G3  carry (amx_kw_carry), peak = max over ranks, loudness pass 2;
           all-reduce(SUM) of the hop energies (loudnorm on);
-          G3  histograms + decision + the limiter on the device's decision;
-        then the host reads the decision and, only if the limiter can engage, re-runs
-        it as the sequential rank-to-rank chain."""
+          G4  histograms + decision + the limiter on the device's decision;
+        then the host reads the decision and, only if the limiter can engage, hands
+        its state rank to rank."""
         if self.world == 1:
             return self.job.capture(d_in)
         job = self.job
         lufs_on = job.dd.lufs_on
-        rank, world = self.rank, self.world
-        h = job.halo_frames
-        n = self.span_frames[rank]
-        hw = (4 * h + 7) // 8                     # doubles holding the halo's bytes
-        self._xbuf = torch.zeros(10 + hw, dtype=torch.float64, device=job.device)
-        # flat [world * words]: all_gather_into_tensor's output, rank-major
-        self._xall = torch.zeros(world * (10 + hw), dtype=torch.float64, device=job.device)
 
         def seg(*fns):
             g = torch.cuda.CUDAGraph()
@@ -272,41 +330,19 @@ class ShardedTrack:
                     fn()
             return g
 
-        from . import capi
-
-        def pack():
-            xb = self._xbuf
-            xb[0:8].copy_(job.kw_tail.reshape(-1)[:8])
-            xb[8:10].copy_(job.peak.reshape(-1)[:2])
-            m = min(h, n)
-            if m > 0:                             # front zero padding stays zero
-                mine = job.out[n - m:n].contiguous().view(torch.uint8).reshape(-1)
-                xb.view(torch.uint8)[80 + 4 * (h - m):80 + 4 * h].copy_(mine)
-
-        def unpack():
-            xa = self._xall.view(world, -1)
-            self.tails_all.copy_(xa[:, 0:8].reshape(world, 2, 4))
-            capi.check(capi.load().amx_kw_carry(job.plan.h, capi.ptr(self.tails_all),
-                                                capi.ptr(job.kw_carry), job._s(None)), "amx_kw_carry")
-            job.peak.reshape(-1)[:2].copy_(xa[:, 8:10].amax(0))
-            if rank > 0 and h > 0:
-                prev = xa[rank - 1].view(torch.uint8)[80:80 + 4 * h].view(torch.int16).reshape(h, 2)
-                job.halo[0, :h].copy_(prev)
-
         torch.cuda.synchronize()
-        g1 = seg(lambda: job.run_chunks(d_in), lambda: job.loudness_pass1(tail=True), pack)
-        g2 = seg(unpack, lambda: job.loudness_pass2(carry=True)) if lufs_on else seg(unpack)
-        # the limiter is launched on the device's own decision (k_decide's word): the
-        # idle path is then complete without a host round trip; when the limiter can
-        # engage, replay() re-runs it as the rank-to-rank sequential chain
+        g1 = seg(lambda: job.run_chunks(d_in), self._pack_edges)
+        g2 = seg(self._unpack_edges, lambda: job.loudness_pass1(tail=True), self._pack_x)
+        g3 = seg(self._unpack_x, lambda: job.loudness_pass2(carry=True)) if lufs_on else seg(self._unpack_x)
+
         # the limiter state is zeroed in the graph, so when the device picks the general
         # limiter the in-graph run IS the speculative from-rest run of
         # chain_state_speculative: replay() then only hands the end states along
         def fin():
             job.lim_state.zero_()
             job.finalize(None)
-        g3 = seg(job.histograms, job.decide, fin) if lufs_on else seg(job.decide, fin)
-        self._g = [g1, g2, g3]
+        g4 = seg(job.histograms, job.decide, fin) if lufs_on else seg(job.decide, fin)
+        self._g = [g1, g2, g3, g4]
         self._ctl_host = torch.zeros(1, dtype=torch.int32).pin_memory()
         self._ctl_ev = torch.cuda.Event()
         return self._g
@@ -316,16 +352,15 @@ class ShardedTrack:
             return self.job.replay()
         from . import capi
         job = self.job
-        g1, g2, g3 = self._g
+        g1, g2, g3, g4 = self._g
         g1.replay()
-        (a, b), st = _staged(self.group, self._xall, self._xbuf)
-        dist.all_gather_into_tensor(a, b, group=self.group)
-        if st:
-            self._xall.copy_(a)
+        self._all_gather(self._eall, self._ebuf)
         g2.replay()
+        self._all_gather(self._xall, self._xbuf)
+        g3.replay()
         if job.dd.lufs_on:
             reduce_loudness(job.hops, None, self.group)
-        g3.replay()
+        g4.replay()
         # The one host read of the step: RCCL operations are enqueued by the host, so
         # only the host can decide whether the limiter's rank-to-rank hand-off runs.
         # The word is the same on every rank (computed from all-reduced data); when it
@@ -340,41 +375,28 @@ class ShardedTrack:
                                     self.group, first_run_done=True)
         return job.y[:job.info.out_frames]
 
-    def _limit(self, capi):
-        """the limiter path k_decide chose (the same word on every rank: it is
-        computed from all-reduced data)"""
+    def step(self, d_in):
+        """One pass of the whole path over this rank's chunks (input resident)."""
+        from . import capi
         job = self.job
+        if self.world == 1:
+            return job.run(d_in)
+        job.run_chunks(d_in)
+        self.exchange_edges()
+        job.timed("loud1", lambda: job.loudness_pass1(tail=True))
+        self.exchange_carry_peaks()
+        lufs_on = job.dd.lufs_on
+        if lufs_on:
+            job.timed("loud2", lambda: job.loudness_pass2(carry=True))
+            reduce_loudness(job.hops, None, self.group)
+            job.timed("hist", job.histograms)
+        job.timed("decide", job.decide)
         fast = bool(int(job.ctl[0].item()) & capi.CTL_FAST)
         if fast:
             job.timed("final", lambda: job.finalize(True))
         else:
             job.lim_state.zero_()
             self.limiter_sequential()
-
-    def _finish(self, capi):
-        self.exchange_halo()
-        self._limit(capi)
-
-    def step(self, d_in):
-        """One pass of the whole path over this rank's chunks (input resident)."""
-        from . import capi
-        job = self.job
-        job.run_chunks(d_in)
-        job.timed("loud1", lambda: job.loudness_pass1(tail=self.world > 1))
-        lufs_on = job.dd.lufs_on
-        if self.world > 1:
-            self.exchange_carry()
-        if lufs_on:
-            job.timed("loud2", lambda: job.loudness_pass2(carry=self.world > 1))
-        if self.world > 1:
-            reduce_loudness(job.hops if lufs_on else None, job.peak, self.group)
-        if lufs_on:
-            job.timed("hist", job.histograms)
-        job.timed("decide", job.decide)
-        if self.world == 1:
-            job.timed("final", lambda: job.finalize(None))
-        else:
-            self._finish(capi)
         job.report = {"chunks": len(job.chunks), "segments": job.info.n_segments}
         return job.y[:job.info.out_frames]
 

@@ -67,11 +67,17 @@ class MasteringJob:
         self.y = torch.empty_like(self.out)
         T = max(1, self.n_tracks)
         self.spans = [self.plan.span(t) for t in range(self.n_tracks)]
-        self.hop = info.hop_frames
-        self.max_hops = max([s.track_frames_total // self.hop + 1 for s in self.spans] + [1])
+        self.hop = info.hop_frames                 # 100 ms of the 192 kHz measurement stream
+        self.max_hops = max(1, int(info.max_hops))
         self.kw_tail = torch.zeros((T, 2, 4), dtype=torch.float64, device=dev)
         self.kw_carry = torch.zeros((T, 2, 4), dtype=torch.float64, device=dev)
-        self.peak = torch.zeros((T, 2), dtype=torch.float64, device=dev)
+        # per track: the measured (192 kHz) stream's sample peak L, R; d_out's own L, R
+        self.peak = torch.zeros((T, 4), dtype=torch.float64, device=dev)
+        # the 16 d_out frames before / after a span inside its track (chunk-sharded
+        # ranks: the neighbours' frames the resampler window reaches); unused otherwise
+        self.edge = torch.zeros((T, 2, capi.UP_EDGE, 2), dtype=torch.int16, device=dev)
+        self.needs_edge = any(s.track_frame0 > 0 or s.track_frame0 + s.out_frames < s.track_frames_total
+                              for s in self.spans)
         self.hops = torch.zeros((T, self.max_hops, 2), dtype=torch.float64, device=dev)
         self.hist = torch.zeros((T, 1000), dtype=torch.int64, device=dev)
         self.st_hist = torch.zeros((T, 1000), dtype=torch.int64, device=dev)
@@ -141,12 +147,14 @@ class MasteringJob:
         """tail: also the K-filter end state from rest (only a chunk-sharded track's
         next rank needs it)."""
         capi.check(capi.load().amx_loudness_pass1(self.plan.h, capi.ptr(self.out),
+                                                  capi.ptr(self.edge) if self.needs_edge else None,
                                                   capi.ptr(self.kw_tail) if tail else None,
                                                   capi.ptr(self.peak), capi.ptr(self.ws), self._s(stream)),
                    "amx_loudness_pass1")
 
     def loudness_pass2(self, stream=None, carry=True):
         capi.check(capi.load().amx_loudness_pass2(self.plan.h, capi.ptr(self.out),
+                                                  capi.ptr(self.edge) if self.needs_edge else None,
                                                   capi.ptr(self.kw_carry) if carry else None,
                                                   capi.ptr(self.hops), int(self.max_hops),
                                                   capi.ptr(self.ws), self._s(stream)),

@@ -16,6 +16,7 @@
 #define AMX_ENV_MAX_ROUNDS 16  // k_envfix rounds (one flag word each)
 #define AMX_ENV_NCTR 4         // k_envfix diagnostic counters per round (after the flags)
 #define AMX_EQC 64        // compact EQ coefficient block (see ChainDev::eqc)
+#define AMX_MEAS_RATE 192000  // loudnorm pass 1 measures at 192 kHz (af_loudnorm dynamic mode)
 #ifndef AMX_PCM_U8        // input PCM formats (include/amx.h amx_pcm_to_s16)
 #define AMX_PCM_U8 0
 #define AMX_PCM_S16 1
@@ -106,8 +107,13 @@ struct ScanBlk {
 };
 
 struct SpanDev {
-    int64_t out_off, out_n, tframe0, ttotal;
+    int64_t out_off, out_n, tframe0, ttotal;   // chain-output frames (d_out) of the span
     int32_t kseg0, nkseg;
+    // the loudness measurement's stream (192 kHz when resampled, else == the chain's):
+    // first frame of the span in the whole track, frames of the span, of the track
+    int64_t m_tframe0, m_n, m_total;
+    int32_t edge_lo, edge_hi;   // resampler window past the span start / end reads the
+                                // neighbour rank's frames (edge buffer), else mirrors
 };
 
 // ---------------------------------------------------------------- launchers
@@ -170,6 +176,31 @@ hipError_t launch_hops(const SpanDev *spans, int n_tracks, const KwSegDev *ks, i
 hipError_t launch_hist(const SpanDev *spans, int n_tracks, int hop, const double *hops,
                        int64_t max_hops, const double *bounds, unsigned long long *hist,
                        unsigned long long *st_hist, hipStream_t st);
+// loudness at 192 kHz (amx_loud192.hip): the resampled stream is recomputed from d_out
+#define AMX_UP_EDGE 16     // frames of the neighbour rank's output the resampler window needs
+#define AMX_UP_BLOCK 64
+struct UpArgs {
+    const ChainDev *cd;
+    const KwSegDev *ks;
+    int n_kseg;
+    const SpanDev *spans;
+    int Lin, Lout;            // input frames / 192 kHz outputs per K segment
+    int static_l;             // L when M == 1 (unrolled kernels), else 0 (tables)
+    int hop;
+    const int32_t *obase, *oph;   // per output n < Lout: input frame (segment-relative), phase
+    const float *bank;            // [L][32] float32 polyphase bank
+    const uint32_t *x, *edge;     // d_out (stereo s16 dwords); edge [tracks][2][AMX_UP_EDGE]
+    const double *G;              // pass 1: GEMV rows A^{Lout-1-n} B
+    double *e;
+    const double *s;              // pass 2: segment start states
+    double *parts;
+    int64_t *part_hop;
+    uint32_t *pk;                 // [seg][4]: 192 kHz |u| max L, R (float bits), native |x| L, R
+};
+hipError_t launch_up1(const UpArgs &a, int n_spans, hipStream_t st);
+int swr_geometry(int in_rate, int out_rate, int *L, int *M);   // host (amx_plan.cpp)
+int swr_bank(int in_rate, int out_rate, float *bank);
+hipError_t launch_up2(const UpArgs &a, hipStream_t st);
 // finalize
 // general alimiter scratch (plan-owned, amx_limiter_prepare): per segment of
 // seg_frames frames the guessed start state G and the end state E (warm-up of
@@ -206,7 +237,7 @@ int peak_reduce_blocks(int64_t max_nkseg);
 hipError_t launch_peak_reduce(const SpanDev *spans, int n_tracks, int64_t max_nkseg,
                               const uint32_t *pk, double *peak, unsigned int *cnt, int *part,
                               const KwSegDev *ks, int L, const int16_t *x, const double *G,
-                              double *e, int kw_fix, hipStream_t st);
+                              double *e, int kw_fix, int resamp, hipStream_t st);
 hipError_t launch_kw_tail(const SpanDev *spans, int n_tracks, const double *s, const double *e,
                           const double *P, double *tail, hipStream_t st);
 }  // namespace amx

@@ -206,8 +206,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_hops(const SpanDev *__restrict__ 
     const int t = blockIdx.y;
     const SpanDev sp = spans[t];
     const int lane = threadIdx.x & 63;
-    const int64_t hfirst = sp.tframe0 / hop;
-    const int64_t hlast = sp.nkseg ? (sp.tframe0 + sp.out_n - 1) / hop : hfirst - 1;
+    const int64_t hfirst = sp.m_tframe0 / hop;
+    const int64_t hlast = sp.nkseg ? (sp.m_tframe0 + sp.m_n - 1) / hop : hfirst - 1;
     const int64_t h = (int64_t)blockIdx.x * (AMX_BLOCK / 64) + (threadIdx.x >> 6);
     if (h >= max_hops) return;                       // wave-uniform
     if (h < hfirst || h > hlast) {                   // hops of other ranks' spans: 0
@@ -217,10 +217,10 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_hops(const SpanDev *__restrict__ 
         }
         return;
     }
-    // span-local frame range of hop h
-    int64_t a = h * hop - sp.tframe0, bnd = (h + 1) * hop - sp.tframe0;
+    // span-local frame range of hop h (measurement stream)
+    int64_t a = h * hop - sp.m_tframe0, bnd = (h + 1) * hop - sp.m_tframe0;
     if (a < 0) a = 0;
-    if (bnd > sp.out_n) bnd = sp.out_n;
+    if (bnd > sp.m_n) bnd = sp.m_n;
     const int64_t j0 = a / L, j1 = (bnd - 1) / L;
     double s0 = 0.0, s1 = 0.0;
     for (int64_t jj = j0 + lane; jj <= j1; jj += 64) {
@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(AMX_HIST_THREADS) k_hist(const SpanDev *__rest
     for (int i = threadIdx.x; i < AMX_HIST_BINS; i += AMX_HIST_THREADS) { h[i] = 0u; sh[i] = 0u; }
     for (int i = threadIdx.x; i <= AMX_HIST_BINS; i += AMX_HIST_THREADS) bd[i] = bounds[i];
     __syncthreads();
-    int64_t nh = sp.ttotal / hop;
+    int64_t nh = sp.m_total / hop;
     if (nh > max_hops) nh = max_hops;
     const double *H = hops + (int64_t)t * max_hops * 2;
     for (int64_t k = threadIdx.x; k + 4 <= nh; k += AMX_HIST_THREADS) {
@@ -356,8 +356,9 @@ __global__ void __launch_bounds__(AMX_PEAK_THREADS) k_peak_reduce(const SpanDev 
                                                                   const KwSegDev *__restrict__ ks,
                                                                   int L, const uint32_t *__restrict__ x,
                                                                   const double *__restrict__ G,
-                                                                  double *__restrict__ e, int kw_fix) {
-    __shared__ int red[2][AMX_PEAK_THREADS / 64];
+                                                                  double *__restrict__ e, int kw_fix,
+                                                                  int resamp) {
+    __shared__ int red[4][AMX_PEAK_THREADS / 64];
     const int t = blockIdx.y;
     const SpanDev sp = spans[t];
     const int64_t q0 = (int64_t)blockIdx.x * AMX_PEAK_THREADS * AMX_PEAK_PER_THREAD;
@@ -392,23 +393,27 @@ __global__ void __launch_bounds__(AMX_PEAK_THREADS) k_peak_reduce(const SpanDev 
             }
         }
     }
-    int m0 = 0, m1 = 0;
+    // per segment: resamp -> [4] = 192 kHz |u| max L, R as float bits (non-negative
+    // floats order like their bits), native |x| L, R as int16 magnitudes; else [2] = |x|
+    const int stride = resamp ? 4 : 2;
+    int m[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < AMX_PEAK_PER_THREAD; i++) {
         const int64_t q = q0 + threadIdx.x + (int64_t)i * AMX_PEAK_THREADS;
         const bool ok = q < sp.nkseg;
         const int64_t j = (int64_t)sp.kseg0 + (ok ? q : 0);
-        const uint32_t a0 = pk[j * 2], a1 = pk[j * 2 + 1];
-        m0 = max(m0, ok ? (int)a0 : 0);
-        m1 = max(m1, ok ? (int)a1 : 0);
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t v = c < stride ? pk[j * stride + c] : 0u;
+            m[c] = max(m[c], ok ? (int)v : 0);
+        }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        m0 = max(m0, __shfl_xor(m0, o));
-        m1 = max(m1, __shfl_xor(m1, o));
-    }
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+        for (int o = 32; o > 0; o >>= 1) m[c] = max(m[c], __shfl_xor(m[c], o));
     if ((threadIdx.x & 63) == 0) {
-        red[0][threadIdx.x >> 6] = m0;
-        red[1][threadIdx.x >> 6] = m1;
+#pragma unroll
+        for (int c = 0; c < 4; c++) red[c][threadIdx.x >> 6] = m[c];
     }
     __syncthreads();
     // the block's maxima go to its slot of `part`; the last block of the track to
@@ -416,28 +421,34 @@ __global__ void __launch_bounds__(AMX_PEAK_THREADS) k_peak_reduce(const SpanDev 
     // counter -- no zeroing pass before, no atomics on the result
     __shared__ bool last;
     if (threadIdx.x == 0) {
-        int a = 0, b = 0;
-        for (int w = 0; w < AMX_PEAK_THREADS / 64; w++) {
-            a = max(a, red[0][w]);
-            b = max(b, red[1][w]);
-        }
+        int mm[4] = {0, 0, 0, 0};
+        for (int w = 0; w < AMX_PEAK_THREADS / 64; w++)
+            for (int c = 0; c < 4; c++) mm[c] = max(mm[c], red[c][w]);
         const int nb = (int)((sp.nkseg + (int64_t)AMX_PEAK_THREADS * AMX_PEAK_PER_THREAD - 1) /
                              ((int64_t)AMX_PEAK_THREADS * AMX_PEAK_PER_THREAD));
-        int *pt = part + ((int64_t)t * gridDim.x + blockIdx.x) * 2;
-        pt[0] = a;
-        pt[1] = b;
+        int *pt = part + ((int64_t)t * gridDim.x + blockIdx.x) * 4;
+        for (int c = 0; c < 4; c++) pt[c] = mm[c];
         __threadfence();
         last = atomicAdd(cnt + t, 1u) == (unsigned)(nb - 1);
         if (last) {
             __threadfence();
-            int ma = 0, mb = 0;
+            int ma[4] = {0, 0, 0, 0};
             for (int k = 0; k < nb; k++) {
-                const volatile int *q = part + ((int64_t)t * gridDim.x + k) * 2;
-                ma = max(ma, q[0]);
-                mb = max(mb, q[1]);
+                const volatile int *q = part + ((int64_t)t * gridDim.x + k) * 4;
+                for (int c = 0; c < 4; c++) ma[c] = max(ma[c], q[c]);
             }
-            peak[2 * t] = (double)ma * (1.0 / 32768.0);
-            peak[2 * t + 1] = (double)mb * (1.0 / 32768.0);
+            // peak[t][4]: the measured stream's sample peak (loudnorm's input_tp) per
+            // channel, then the chain output's own sample peak (the limiter's input bound)
+            double *pp = peak + 4 * t;
+            if (resamp) {
+                pp[0] = (double)__int_as_float(ma[0]);
+                pp[1] = (double)__int_as_float(ma[1]);
+                pp[2] = (double)ma[2] * (1.0 / 32768.0);
+                pp[3] = (double)ma[3] * (1.0 / 32768.0);
+            } else {
+                pp[0] = pp[2] = (double)ma[0] * (1.0 / 32768.0);
+                pp[1] = pp[3] = (double)ma[1] * (1.0 / 32768.0);
+            }
             cnt[t] = 0u;
         }
     }
@@ -451,11 +462,11 @@ int peak_reduce_blocks(int64_t max_nkseg) {
 hipError_t launch_peak_reduce(const SpanDev *spans, int n_tracks, int64_t max_nkseg,
                               const uint32_t *pk, double *peak, unsigned int *cnt, int *part,
                               const KwSegDev *ks, int L, const int16_t *x, const double *G,
-                              double *e, int kw_fix, hipStream_t st) {
+                              double *e, int kw_fix, int resamp, hipStream_t st) {
     dim3 g((unsigned)peak_reduce_blocks(max_nkseg), (unsigned)n_tracks);
     if (empty(g)) return hipSuccess;
     hipLaunchKernelGGL(k_peak_reduce, g, dim3(AMX_PEAK_THREADS), 0, st, spans, pk, peak, cnt, part,
-                       ks, L, reinterpret_cast<const uint32_t *>(x), G, e, kw_fix);
+                       ks, L, reinterpret_cast<const uint32_t *>(x), G, e, kw_fix, resamp);
     return hipGetLastError();
 }
 
@@ -509,14 +520,43 @@ __device__ __forceinline__ double lufs_of(double e) { return 10 * log10(e) - 0.6
 
 // Wave-parallel histogram arithmetic: lane l owns bins [16 l, 16 l + 16).  Counts
 // are integers (exact in double), so count sums and prefix walks are exact in any
-// order; the energy sums use a fixed lane order + butterfly (deterministic; they
-// differ from libebur128's sequential order only in the last bits, far below the
-// "%.2f" the statistics are printed with).
+// order; the energy sums keep libebur128's sequential order (wave_seq_sum).
 #define AMX_BPL 16
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
+}
+
+// sum over the bins j >= lo, ascending, of count_j * energy_j in libebur128's
+// sequential order (ebur128_gated_loudness / ebur128_loudness_range loops): the
+// owning lanes form the products, the non-empty ones are compacted in bin order into
+// this wave's LDS buffer (adding an empty bin's 0.0 leaves the sum unchanged) and
+// lane 0 adds them one by one; the sum is broadcast.  Bit-identical to the C loop.
+__device__ double wave_seq_sum(const double (&cc)[AMX_BPL], const double (&en)[AMX_BPL], int lo,
+                               double *sbuf) {
+    const int lane = threadIdx.x & 63;
+    int mine = 0;
+#pragma unroll
+    for (int q = 0; q < AMX_BPL; q++) mine += (lane * AMX_BPL + q >= lo && cc[q] != 0.0) ? 1 : 0;
+    int incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int up = __shfl_up(incl, o);
+        if (lane >= o) incl += up;
+    }
+    int off = incl - mine;
+    const int tot = __shfl(incl, 63);
+#pragma unroll
+    for (int q = 0; q < AMX_BPL; q++)
+        if (lane * AMX_BPL + q >= lo && cc[q] != 0.0) sbuf[off++] = cc[q] * en[q];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    double acc = 0.0;
+    if (lane == 0)
+        for (int k = 0; k < tot; k++) acc += sbuf[k];
+    __builtin_amdgcn_wave_barrier();
+    return __shfl(acc, 0);
 }
 
 // bin search without a table walk: the largest b < 1000 with bounds[b] <= v (what
@@ -545,6 +585,7 @@ __device__ __forceinline__ double wave_bin_value(const double (&en)[AMX_BPL], in
 __global__ void __launch_bounds__(128) k_decide(DecideArgs a) {
     const int t = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     __shared__ double s_lra;
+    __shared__ double s_sum[2][AMX_HIST_BINS];
     double I = -INFINITY, thr = -70.0, lra = 0.0;
     if (a.lufs_on) {
         // lane l owns bins [16 l, 16 l + 16): this wave's counts, the bin energies and
@@ -566,11 +607,11 @@ __global__ void __launch_bounds__(128) k_decide(DecideArgs a) {
         const double b0 = __shfl(bd[0], 0);
         if (wv == 0) {
             // integrated loudness with the relative gate (ebur128_gated_loudness)
-            double rel = 0.0, cnt = 0.0;
+            double cnt = 0.0;
 #pragma unroll
-            for (int q = 0; q < AMX_BPL; q++) { rel += cc[q] * en[q]; cnt += cc[q]; }
-            rel = wave_sum(rel);
-            cnt = wave_sum(cnt);
+            for (int q = 0; q < AMX_BPL; q++) cnt += cc[q];
+            double rel = wave_seq_sum(cc, en, 0, s_sum[0]);
+            cnt = wave_sum(cnt);                           // integers: exact in any order
             if (cnt != 0.0) {
                 rel /= cnt;
                 rel *= 0.1;                                // pow(10, -10/10)
@@ -581,24 +622,20 @@ __global__ void __launch_bounds__(128) k_decide(DecideArgs a) {
                     start = wave_find_bin(bd, rel);
                     if (rel > wave_bin_value(en, start)) ++start;
                 }
-                double g = 0.0, above = 0.0;
+                double above = 0.0;
 #pragma unroll
-                for (int q = 0; q < AMX_BPL; q++) {
-                    const bool in = lane * AMX_BPL + q >= start;
-                    g += in ? cc[q] * en[q] : 0.0;
-                    above += in ? cc[q] : 0.0;
-                }
-                g = wave_sum(g);
+                for (int q = 0; q < AMX_BPL; q++) above += lane * AMX_BPL + q >= start ? cc[q] : 0.0;
+                const double g = wave_seq_sum(cc, en, start, s_sum[0]);
                 above = wave_sum(above);
                 if (above != 0.0) I = lufs_of(g / above);
             }
         } else {
             // loudness range (ebur128_loudness_range) on the short-term histogram
-            double size = 0.0, power = 0.0;
+            double size = 0.0;
 #pragma unroll
-            for (int q = 0; q < AMX_BPL; q++) { size += cc[q]; power += cc[q] * en[q]; }
+            for (int q = 0; q < AMX_BPL; q++) size += cc[q];
             size = wave_sum(size);
-            power = wave_sum(power);
+            double power = wave_seq_sum(cc, en, 0, s_sum[1]);
             if (size != 0.0) {
                 power /= size;
                 const double integ = 0.01 * power;         // pow(10, -20/10)
@@ -651,7 +688,10 @@ __global__ void __launch_bounds__(128) k_decide(DecideArgs a) {
     __syncthreads();
     if (a.lufs_on) lra = s_lra;
     if (threadIdx.x != 0) return;
-    const double pk = fmax(a.peak[2 * t], a.peak[2 * t + 1]);
+    // input_tp: the measured (192 kHz) stream's sample peak; the limiter bound below
+    // uses the chain output's own peak (the samples the gain and alimiter see)
+    const double pk = fmax(a.peak[4 * t], a.peak[4 * t + 1]);
+    const double pk_out = fmax(a.peak[4 * t + 2], a.peak[4 * t + 3]);
     const double tp = pk > 0.0 ? 20.0 * log10(pk) : -INFINITY;
     const double si = round2(I), stp = round2(tp), slra = round2(lra), sthr = round2(thr);
     int mode = 0;                                   // 0 off, 1 skip, 2 linear, 3 dynamic
@@ -671,14 +711,14 @@ __global__ void __launch_bounds__(128) k_decide(DecideArgs a) {
         }
     }
     // max |sample| after the gain stage (llrint(x*g) clipped), the limiter's input
-    const double m16 = rint(pk * 32768.0);
+    const double m16 = rint(pk_out * 32768.0);
     double amax = m16 / 32768.0;
     if (gain > 0.0) amax = fmin(rint(((m16 * (1.0 / 32768.0)) * gain) * 32768.0), 32768.0) / 32768.0;
     const bool fast = amax * a.level_in <= a.limit;
     double *o = a.stats + (int64_t)t * AMX_STATS;
     o[0] = I; o[1] = lra; o[2] = thr; o[3] = tp;
     o[4] = si; o[5] = stp; o[6] = slra; o[7] = sthr;
-    o[8] = (double)mode; o[9] = gain; o[10] = fast ? 1.0 : 0.0; o[11] = pk;
+    o[8] = (double)mode; o[9] = gain; o[10] = fast ? 1.0 : 0.0; o[11] = pk; o[12] = pk_out;
     a.gains[t] = gain;
     a.ctl[t] = (fast ? AMX_CTL_FAST : 0) | (mode << 4);
 }

@@ -157,10 +157,80 @@ void *align_up(size_t &off, size_t bytes) {
 
 }  // namespace
 
+namespace amx {
+// libswresample's resampler geometry and filter bank for the loudness measurement's
+// 192 kHz stream (what ffmpeg inserts ahead of af_loudnorm in dynamic mode, :229).
+// Restated from resample.c resample_init / build_filter with swresample's defaults:
+// filter_size 32, phase_shift 10, exact_rational 1, cutoff 0.97, Kaiser beta 9, FLTP
+// (float32 bank, scale 1).  Upsampling only (factor 1); L = out/gcd phases (<= 1024,
+// else exact_rational does not apply and the rate is unsupported), M = in/gcd.
+int swr_geometry(int in_rate, int out_rate, int *L, int *M) {
+    if (in_rate <= 0 || out_rate <= 0) return -1;
+    int64_t a = in_rate, b = out_rate;
+    while (b) { int64_t t = a % b; a = b; b = t; }
+    const int64_t l = out_rate / a, m = in_rate / a;
+    if (l > 1024) return -1;
+    if ((double)out_rate * 0.97 / in_rate < 1.0 && !(l == 1 && m == 1)) return -1;
+    *L = (int)l;
+    *M = (int)m;
+    return 0;
+}
+
+static double swr_bessel(double x) {
+    double lastv = 0, t, v;
+    double inv[100];
+    for (int k = 0; k < 100; k++) inv[k] = 1.0 / ((double)(k + 1) * (double)(k + 1));
+    x = x * x / 4;
+    t = x;
+    v = 1 + x;
+    for (int i = 1; v != lastv && i < 98; i += 2) {
+        t *= x * inv[i];
+        v += t;
+        lastv = v;
+        t *= x * inv[i + 1];
+        v += t;
+    }
+    return v;
+}
+
+int swr_bank(int in_rate, int out_rate, float *bank) {
+    int L, M;
+    if (swr_geometry(in_rate, out_rate, &L, &M)) return -1;
+    const int pc = L, taps = 32, center = 15;
+    const int ph_nb = pc % 2 ? pc : pc / 2 + 1;
+    std::vector<double> sin_lut(ph_nb), tab(taps);
+    double norm = 0;
+    for (int ph = 0; ph < ph_nb; ph++) sin_lut[ph] = std::sin(M_PI * ph / pc) * (center & 1 ? 1 : -1);
+    for (int ph = 0; ph < ph_nb; ph++) {
+        double sv = sin_lut[ph];
+        for (int i = 0; i < taps; i++) {
+            const double x = M_PI * ((double)(i - center) - (double)ph / pc) * 1.0;
+            double y = x == 0 ? 1.0 : sv / x;
+            const double w = 2.0 * x / (1.0 * taps * M_PI);
+            y *= swr_bessel(9.0 * std::sqrt(std::max(1 - w * w, 0.0)));
+            tab[i] = y;
+            sv = -sv;
+            if (!ph) norm += y;
+        }
+        for (int i = 0; i < taps; i++) bank[ph * taps + i] = (float)(tab[i] * 1 / norm);
+        if (pc % 2) continue;
+        if (pc - ph < pc)
+            for (int i = 0; i < taps; i++) bank[(pc - ph) * taps + taps - 1 - i] = bank[ph * taps + i];
+    }
+    return 0;
+}
+}  // namespace amx
+
 struct amx_plan {
     amx_chain_desc desc;
     ChainDev cd;
     int L = 256, Lkw = 512, hop = 0;
+    // loudness measurement stream: ffmpeg's pass 1 resamples to 192 kHz (L phases,
+    // step M; Lin chain frames = Lout 192 kHz frames per K segment); resamp = 0 when
+    // the track already is at 192 kHz (the measurement runs on d_out itself)
+    int resamp = 0, upL = 1, upM = 1, upLin = 0, upLout = 0, up_static = 0, up_ok = 1;
+    int32_t *d_obase = nullptr, *d_oph = nullptr;
+    float *d_bank = nullptr;
     int mask = 0, D = 0;
     int lev_eq = 0, lev_x = 0, lev_kw = 0;
     int mb = 0;
@@ -175,6 +245,7 @@ struct amx_plan {
     int64_t max_nkseg = 0;
     int64_t nloc = 0, out_frames = 0, max_chunk_out = 0, max_span = 0, max_chunk_n = 0;
     int64_t in_frames = 0;  // input frames the chunks read (max in_offset + frames)
+    int64_t max_hops = 1;   // 100 ms hops of the longest track's measurement stream
     int mono16 = 0;         // mono int16 input: duplicated to stereo into ws o_dup first
     std::vector<ChunkDev> chunks;
     std::vector<SegDev> segs;
@@ -281,8 +352,32 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     }
     p->L = seg_frames > 0 ? seg_frames : 256;
     p->L = (p->L + AMX_TF_FRAMES - 1) / AMX_TF_FRAMES * AMX_TF_FRAMES;   // whole LDS tiles
-    p->hop = (fs + 5) / 10;                    // libebur128 samples_in_100ms
-    p->Lkw = 128 < p->hop ? 128 : p->hop / AMX_TF_FRAMES * AMX_TF_FRAMES;
+    // the loudness measurement's rate: 192 kHz (af_loudnorm dynamic mode, :229)
+    const int kfs = AMX_MEAS_RATE;
+    std::vector<float> bank;
+    std::vector<int32_t> obase, oph;
+    if (fs != kfs) {
+        p->resamp = 1;
+        if (amx::swr_geometry(fs, kfs, &p->upL, &p->upM) != 0) {
+            p->up_ok = 0;     // no exact-rational resampler: amx_loudness_pass1 fails
+        } else {
+            const int kk = std::max(1, (512 + p->upL / 2) / p->upL);
+            p->upLin = p->upM * kk;
+            p->upLout = p->upL * kk;
+            bank.assign((size_t)p->upL * 32, 0.0f);
+            amx::swr_bank(fs, kfs, bank.data());
+            // M == 1: the unrolled kernels (phase pattern static, phase 0 the identity)
+            bool ident0 = bank[15] == 1.0f;
+            for (int i = 0; i < 32; i++) ident0 = ident0 && (i == 15 || bank[i] == 0.0f);
+            p->up_static = (p->upM == 1 && (p->upL == 2 || p->upL == 4) && ident0 &&
+                            p->upLin % 16 == 0) ? p->upL : 0;
+        }
+    }
+    p->hop = (kfs + 5) / 10;                   // libebur128 samples_in_100ms at 192 kHz
+    {
+        const int chain_hop = (fs + 5) / 10;
+        p->Lkw = 128 < chain_hop ? 128 : chain_hop / AMX_TF_FRAMES * AMX_TF_FRAMES;
+    }
     ChainDev &cd = p->cd;
     memset(&cd, 0, sizeof cd);
     cd.fs = fs;
@@ -357,7 +452,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     // K-weighting coefficients (libebur128 ebur128_init_filter)
     {
         double f0 = 1681.974450955533, G = 3.999843853973347, Q = 0.7071752369554196;
-        double K = std::tan(M_PI * f0 / (double)fs);
+        double K = std::tan(M_PI * f0 / (double)kfs);
         double Vh = std::pow(10.0, G / 20.0);
         double Vb = std::pow(Vh, 0.4996667741545416);
         double pb[3] = {0.0, 0.0, 0.0}, pa[3] = {1.0, 0.0, 0.0};
@@ -370,7 +465,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         pa[2] = (1.0 - K / Q + K * K) / a0;
         f0 = 38.13547087602444;
         Q = 0.5003270373238773;
-        K = std::tan(M_PI * f0 / (double)fs);
+        K = std::tan(M_PI * f0 / (double)kfs);
         ra[1] = 2.0 * (K * K - 1.0) / (1.0 + K / Q + K * K);
         ra[2] = (1.0 - K / Q + K * K) / (1.0 + K / Q + K * K);
         // libebur128 multiplies the two sections into one 4th-order direct form II;
@@ -520,37 +615,79 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     p->n_es = (int)p->esegs.size();
     p->out_frames = outo;
     p->n_seg = (int)p->segs.size();
-    // K-weighting segments per track span
+    // K-weighting segments per track span, on the measurement stream: output j of
+    // the 192 kHz stream is made from the chain frames around floor(j M / L); a span
+    // of chain frames [f0, f0 + n) of its track owns outputs [J(f0), J(f0 + n)),
+    // J(f) = ceil(f L / M); segment q = chain frames f0 + q Lin + [0, Lin) = outputs
+    // J(f0) + q Lout + [0, Lout)
+    const int64_t uL = p->upL, uM = p->upM;
+    auto J = [&](int64_t f) { return (f * uL + uM - 1) / uM; };
+    int64_t pattern = -1;     // (J(f0) M - f0 L): the phase pattern, equal for all spans
     for (int t = 0; t < n_tracks; t++) {
         SpanDev &sp = p->spans[t];
         sp.tframe0 = track_frame0 ? track_frame0[t] : 0;
         sp.ttotal = track_total_frames ? track_total_frames[t] : sp.out_n;
         sp.kseg0 = (int32_t)p->ksegs.size();
-        int64_t nk = (sp.out_n + p->Lkw - 1) / p->Lkw;
+        const int Lseg = p->resamp ? p->upLout : p->Lkw;
+        const int Lsin = p->resamp ? p->upLin : p->Lkw;
+        if (p->resamp && p->up_ok) {
+            sp.m_tframe0 = J(sp.tframe0);
+            sp.m_n = J(sp.tframe0 + sp.out_n) - sp.m_tframe0;
+            sp.m_total = J(sp.ttotal);
+            const int64_t pat = sp.m_tframe0 * uM - sp.tframe0 * uL;
+            if (sp.out_n > 0) {
+                if (pattern >= 0 && pat != pattern) {
+                    delete p;
+                    return fail(AMX_EINVAL, "spans with different 192 kHz phase patterns in one plan");
+                }
+                pattern = pat;
+            }
+        } else {
+            sp.m_tframe0 = sp.tframe0;
+            sp.m_n = sp.out_n;
+            sp.m_total = sp.ttotal;
+        }
+        sp.edge_lo = sp.tframe0 > 0 ? 1 : 0;
+        sp.edge_hi = sp.tframe0 + sp.out_n < sp.ttotal ? 1 : 0;
+        int64_t nk = (p->resamp && !p->up_ok) ? 0 : (sp.m_n + Lseg - 1) / Lseg;
         sp.nkseg = (int32_t)nk;
         add_blocks(p->kblks, sp.kseg0, (int32_t)nk, t);
         for (int64_t k = 0; k < nk; k++) {
             KwSegDev s{};
-            s.out_pos = sp.out_off + k * p->Lkw;
-            s.tframe = sp.tframe0 + k * p->Lkw;
+            s.out_pos = sp.out_off + k * Lsin;
+            s.tframe = sp.m_tframe0 + k * Lseg;
             s.track = t;
-            s.len = (int32_t)((sp.out_n - k * p->Lkw) < p->Lkw ? (sp.out_n - k * p->Lkw) : p->Lkw);
+            s.len = (int32_t)((sp.m_n - k * Lseg) < Lseg ? (sp.m_n - k * Lseg) : Lseg);
             s.first = sp.kseg0;
             s.last = (k == nk - 1) ? 1 : 0;
             p->ksegs.push_back(s);
         }
         p->max_span = sp.out_n > p->max_span ? sp.out_n : p->max_span;
         p->max_nkseg = sp.nkseg > p->max_nkseg ? sp.nkseg : p->max_nkseg;
+        p->max_hops = std::max(p->max_hops, sp.m_total / p->hop + 1);
+    }
+    if (p->resamp && p->up_ok) {
+        // per output n of a segment: the chain frame its window is centred on (relative
+        // to the segment's first frame) and its phase
+        if (pattern < 0) pattern = 0;
+        obase.resize(p->upLout);
+        oph.resize(p->upLout);
+        for (int64_t n = 0; n < p->upLout; n++) {
+            const int64_t idx = pattern + n * uM;     // (J0 + n) M - f0 L
+            obase[n] = (int32_t)(idx / uL);
+            oph[n] = (int32_t)(idx % uL);
+        }
+        if (p->up_static && pattern != 0) p->up_static = 0;
     }
     p->n_kseg = (int)p->ksegs.size();
     // hop splits on 16-frame tile boundaries (k_kw2 picks the hop piece per tile)
-    p->kw_aligned = (p->hop % AMX_TF_FRAMES == 0 && p->Lkw % AMX_TF_FRAMES == 0) ? 1 : 0;
+    p->kw_aligned = (!p->resamp && p->hop % AMX_TF_FRAMES == 0 && p->Lkw % AMX_TF_FRAMES == 0) ? 1 : 0;
     for (int t = 0; t < n_tracks; t++)
         if (p->spans[t].tframe0 % AMX_TF_FRAMES) p->kw_aligned = 0;
     // the K-filter segment grid equals the chain's when there is no multiband
     // (output frames == input frames) and every chunk but a span's last is whole
     // segments long: k_front2 then does loudness pass 1 on the output it writes
-    p->fuse_kw = (!p->mb && p->Lkw == p->L && p->n_kseg == p->n_seg) ? 1 : 0;
+    p->fuse_kw = (!p->resamp && !p->mb && p->Lkw == p->L && p->n_kseg == p->n_seg) ? 1 : 0;
     for (int c = 0; c < n_chunks && p->fuse_kw; c++) {
         const bool span_last = (c == n_chunks - 1) || (chunks[c + 1].track != chunks[c].track);
         if (!span_last && (p->chunks[c].n % p->L) != 0) p->fuse_kw = 0;
@@ -608,12 +745,13 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             double y = sos_step_h(cd.kw1, z, x);
             sos_step_h(cd.kw2, z + 2, y);
         });
-        Gkw = kw.gemv_table(p->Lkw);
-        Mkw = matpow(kw.A, p->Lkw, AMX_KW_DIM);
-        p->lev_kw = kw.window_powers((int64_t)p->Lkw * AMX_SCAN_S, tol, 16, Mpkw);
+        const int Lseg = p->resamp ? std::max(1, p->upLout) : p->Lkw;
+        Gkw = kw.gemv_table(Lseg);
+        Mkw = matpow(kw.A, Lseg, AMX_KW_DIM);
+        p->lev_kw = kw.window_powers((int64_t)Lseg * AMX_SCAN_S, tol, 16, Mpkw);
         if (p->lev_kw < 0) {
             delete p;
-            return fail(AMX_ERANGE, "K-weighting decays too slowly for %d-frame segments", p->Lkw);
+            return fail(AMX_ERANGE, "K-weighting decays too slowly for %d-frame segments", Lseg);
         }
         p->tail_pow.assign((size_t)n_tracks * 16, 0.0);
         for (int t = 0; t < n_tracks; t++) {
@@ -661,11 +799,14 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     UP(p->d_bounds, bounds, 1001);
     UP(p->d_energies, energies, 1000);
     UP(p->d_tailpow, p->tail_pow.data(), p->tail_pow.size());
+    UP(p->d_obase, obase.data(), obase.size());
+    UP(p->d_oph, oph.data(), oph.size());
+    UP(p->d_bank, bank.data(), bank.size());
     {
         std::vector<unsigned int> zero((size_t)(p->n_tracks > 0 ? p->n_tracks : 1), 0u);
         UP(p->d_pcnt, zero.data(), zero.size());
         const size_t nb = (size_t)amx::peak_reduce_blocks(p->max_nkseg);
-        UP(p->d_ppart, (const int *)nullptr, (size_t)(p->n_tracks > 0 ? p->n_tracks : 1) * (nb ? nb : 1) * 2);
+        UP(p->d_ppart, (const int *)nullptr, (size_t)(p->n_tracks > 0 ? p->n_tracks : 1) * (nb ? nb : 1) * 4);
         for (const SpanDev &sp : p->spans) p->any_empty_span |= sp.nkseg == 0 ? 1 : 0;
     }
     if (desc->tanh_lut) UP(p->d_lut, desc->tanh_lut, 65536);
@@ -702,7 +843,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     }
     p->o_ebk = (size_t)align_up(off, nkb * 2 * AMX_KW_DIM * 8);
     p->o_ekw = (size_t)align_up(off, nk * 2 * AMX_KW_DIM * 8);
-    p->o_pk = (size_t)align_up(off, nk * 2 * 4);
+    p->o_pk = (size_t)align_up(off, nk * 4 * 4);
     p->o_skw = (size_t)align_up(off, nk * 2 * AMX_KW_DIM * 8);
     p->o_parts = (size_t)align_up(off, nk * 4 * 8);
     p->o_phop = (size_t)align_up(off, nk * 8);
@@ -718,7 +859,7 @@ void amx_plan_free(amx_plan *p) {
                     p->d_Mx,  p->d_Mpx,    p->d_Gkw,  p->d_Mkw,   p->d_Mpkw,   p->d_tabs,
                     p->d_bounds, p->d_tailpow, p->d_lut, p->d_energies, p->d_carryP,
                     p->d_esegs, p->d_eseg0, p->d_neseg, p->d_pcnt, p->d_ppart,
-                    p->lim.seg_state, p->lim.cnt};
+                    p->lim.seg_state, p->lim.cnt, p->d_obase, p->d_oph, p->d_bank};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     delete p;
@@ -738,6 +879,8 @@ int amx_plan_get_info(const amx_plan *p, amx_plan_info *info) {
     info->scan_levels_kw = p->lev_kw;
     info->eq_dim = p->D;
     info->hop_frames = p->hop;
+    info->meas_rate = AMX_MEAS_RATE;
+    info->max_hops = p->max_hops;
     return AMX_OK;
 }
 
@@ -837,17 +980,54 @@ int amx_run_chunks(amx_plan *p, const float *d_in, int16_t *d_out, void *d_ws, v
 
 }  // extern "C"
 
+namespace {
+amx::UpArgs up_args(const amx_plan *p, const int16_t *d_out, const int16_t *d_edge, void *d_ws) {
+    amx::UpArgs a{};
+    a.cd = p->d_cd;
+    a.ks = p->d_ksegs;
+    a.n_kseg = p->n_kseg;
+    a.spans = p->d_spans;
+    a.Lin = p->upLin;
+    a.Lout = p->upLout;
+    a.static_l = p->up_static;
+    a.hop = p->hop;
+    a.obase = p->d_obase;
+    a.oph = p->d_oph;
+    a.bank = p->d_bank;
+    a.x = reinterpret_cast<const uint32_t *>(d_out);
+    a.edge = reinterpret_cast<const uint32_t *>(d_edge);
+    a.G = p->d_Gkw;
+    a.e = wsp<double>(d_ws, p->o_ekw);
+    a.s = wsp<double>(d_ws, p->o_skw);
+    a.parts = wsp<double>(d_ws, p->o_parts);
+    a.part_hop = wsp<int64_t>(d_ws, p->o_phop);
+    a.pk = wsp<uint32_t>(d_ws, p->o_pk);
+    return a;
+}
+int check_edges(const amx_plan *p, const int16_t *d_edge) {
+    if (!p->resamp || d_edge) return AMX_OK;
+    for (const SpanDev &sp : p->spans)
+        if (sp.out_n > 0 && (sp.edge_lo || sp.edge_hi))
+            return fail(AMX_EINVAL, "a span inside its track needs the neighbour frames (d_edge)");
+    return AMX_OK;
+}
+}  // namespace
+
 extern "C" {
 
-int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, double *d_kw_tail, double *d_peak,
-                       void *d_ws, void *stream) {
+int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, const int16_t *d_edge, double *d_kw_tail,
+                       double *d_peak, void *d_ws, void *stream) {
     if (!p || !d_peak || (p->n_kseg > 0 && (!d_out || !d_ws)))
         return fail(AMX_EINVAL, "null argument");
+    if (p->resamp && !p->up_ok)
+        return fail(AMX_ERANGE, "%d Hz has no exact-rational 192 kHz resampler (loudnorm pass 1)",
+                    p->cd.fs);
+    if (int rc = check_edges(p, d_edge)) return rc;
     hipStream_t st = (hipStream_t)stream;
     // k_peak_reduce writes every track's peak; only tracks without a K segment (empty
     // spans) need the zero written here
     if (p->any_empty_span || p->n_kseg == 0)
-        HIPCHK(hipMemsetAsync(d_peak, 0, sizeof(double) * 2 * (size_t)p->n_tracks, st));
+        HIPCHK(hipMemsetAsync(d_peak, 0, sizeof(double) * 4 * (size_t)p->n_tracks, st));
     p->kw_rest_states = 0;
     if (p->n_kseg == 0) {
         if (d_kw_tail) HIPCHK(hipMemsetAsync(d_kw_tail, 0, sizeof(double) * 8 * (size_t)p->n_tracks, st));
@@ -855,11 +1035,13 @@ int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, double *d_kw_tail, dou
     }
     double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
     uint32_t *pk = wsp<uint32_t>(d_ws, p->o_pk);
-    if (!p->fuse_kw)  // else the GEMV + per-segment peaks were made by k_front2 (amx_run_chunks)
+    if (p->resamp)    // GEMV over the 192 kHz stream + its sample peak (amx_loud192.hip)
+        HIPCHK(amx::launch_up1(up_args(p, d_out, d_edge, d_ws), p->n_tracks, st));
+    else if (!p->fuse_kw)  // else the GEMV + per-segment peaks were made by k_front2 (amx_run_chunks)
         HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e, pk, st));
     HIPCHK(amx::launch_peak_reduce(p->d_spans, p->n_tracks, p->max_nkseg, pk, d_peak, p->d_pcnt,
                                    p->d_ppart, p->d_ksegs, p->Lkw, d_out, p->d_Gkw, e, p->fuse_kw,
-                                   st));
+                                   p->resamp, st));
     HIPCHK(amx::launch_scan(p->scan_kw(), e, s, nullptr, wsp<double>(d_ws, p->o_ebk), st));
     p->kw_rest_states = 1;   // s = the start states from rest: pass 2 without a carry reuses them
     if (d_kw_tail)
@@ -900,10 +1082,17 @@ int amx_kw_propagate(const amx_plan *p, int64_t frames, const double *in8, doubl
     return AMX_OK;
 }
 
-int amx_loudness_pass2(amx_plan *p, const int16_t *d_out, const double *d_kw_carry,
-                       double *d_hops, int64_t max_hops, void *d_ws, void *stream) {
+int amx_loudness_pass2(amx_plan *p, const int16_t *d_out, const int16_t *d_edge,
+                       const double *d_kw_carry, double *d_hops, int64_t max_hops, void *d_ws,
+                       void *stream) {
     if (!p || !d_hops || max_hops <= 0 || (p->n_kseg > 0 && (!d_out || !d_ws)))
         return fail(AMX_EINVAL, "null argument");
+    if (p->resamp && !p->up_ok)
+        return fail(AMX_ERANGE, "%d Hz has no exact-rational 192 kHz resampler (loudnorm pass 1)",
+                    p->cd.fs);
+    if (max_hops < p->max_hops) return fail(AMX_EINVAL, "max_hops %lld < %lld", (long long)max_hops,
+                                            (long long)p->max_hops);
+    if (int rc = check_edges(p, d_edge)) return rc;
     hipStream_t st = (hipStream_t)stream;
     if (p->n_kseg == 0) {
         HIPCHK(hipMemsetAsync(d_hops, 0, sizeof(double) * 2 * (size_t)max_hops * p->n_tracks, st));
@@ -914,10 +1103,13 @@ int amx_loudness_pass2(amx_plan *p, const int16_t *d_out, const double *d_kw_car
     int64_t *phop = wsp<int64_t>(d_ws, p->o_phop);
     if (d_kw_carry || !p->kw_rest_states)
         HIPCHK(amx::launch_scan(p->scan_kw(), e, s, d_kw_carry, wsp<double>(d_ws, p->o_ebk), st));
-    HIPCHK(amx::launch_kw2(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, p->hop, d_out, s, parts, phop,
-                           p->kw_aligned, st));
-    HIPCHK(amx::launch_hops(p->d_spans, p->n_tracks, p->d_ksegs, p->Lkw, p->hop, parts, phop, d_hops,
-                            max_hops, st));
+    if (p->resamp)
+        HIPCHK(amx::launch_up2(up_args(p, d_out, d_edge, d_ws), st));
+    else
+        HIPCHK(amx::launch_kw2(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, p->hop, d_out, s, parts, phop,
+                               p->kw_aligned, st));
+    HIPCHK(amx::launch_hops(p->d_spans, p->n_tracks, p->d_ksegs, p->resamp ? p->upLout : p->Lkw,
+                            p->hop, parts, phop, d_hops, max_hops, st));
     return AMX_OK;
 }
 
@@ -1023,7 +1215,14 @@ int amx_kw_carry_setup(amx_plan *p, int32_t n_prev, const int64_t *frames_after)
     std::vector<double> P((size_t)(n_prev > 0 ? n_prev : 1) * 16, 0.0);
     for (int q = 0; q < n_prev; q++) {
         if (frames_after[q] < 0) return fail(AMX_EINVAL, "frames_after[%d] < 0", q);
-        Mat m = matpow(p->kw_model.A, frames_after[q], AMX_KW_DIM);
+        // the gap on the measurement stream: J(f0) - J(f0 - frames_after), J(f) = ceil(f L / M)
+        int64_t gap = frames_after[q];
+        if (p->resamp && p->n_tracks > 0) {
+            const int64_t f0 = p->spans[0].tframe0, L = p->upL, M = p->upM;
+            auto J = [&](int64_t f) { return (f * L + M - 1) / M; };
+            gap = J(f0) - J(f0 - frames_after[q]);
+        }
+        Mat m = matpow(p->kw_model.A, gap, AMX_KW_DIM);
         for (int k = 0; k < 16; k++) P[(size_t)q * 16 + k] = m[k];
     }
     if (p->d_carryP) (void)hipFree(p->d_carryP);

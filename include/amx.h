@@ -43,7 +43,7 @@ extern "C" {
 #define AMX_ENOMEM -3     /* host allocation failed */
 #define AMX_ERANGE -4     /* a size or filter is outside what the plan supports */
 
-#define AMX_ABI_VERSION 2
+#define AMX_ABI_VERSION 3
 
 #if defined(__GNUC__)
 #define AMX_API __attribute__((visibility("default")))
@@ -127,7 +127,11 @@ typedef struct amx_plan_info {
     int32_t scan_levels_xover;
     int32_t scan_levels_kw;
     int32_t eq_dim;
-    int32_t hop_frames;           /* libebur128 samples_in_100ms */
+    int32_t hop_frames;           /* libebur128 samples_in_100ms of the measurement stream */
+    int32_t meas_rate;            /* the loudness measurement's rate: 192000 (see pass 1) */
+    int32_t pad_;
+    int64_t max_hops;             /* 100 ms hops of the longest track's measurement stream + 1:
+                                     the d_hops row length amx_loudness_pass2 needs */
 } amx_plan_info;
 
 /* Per-track output span of this plan inside the full track timeline (for chunk
@@ -193,24 +197,34 @@ AMX_API int amx_pcm_to_s16(const void *d_raw, int64_t frames, int32_t channels, 
  * call it outside graph capture.  Replaces no reference line. */
 AMX_API int amx_env_counters(const amx_plan *plan, const void *d_ws, int32_t *out, int32_t n);
 
-/* Loudness pass 1 over d_out (libebur128 restated, ffmpeg loudnorm :229):
- * K-filter zero-state GEMV per segment + exact scan + sample peak.
+/* Loudness pass 1 over d_out as ffmpeg's loudnorm pass 1 measures it (:229): with no
+ * measured_* values af_loudnorm runs in dynamic mode, which takes 192 kHz input, so
+ * the track is measured on libswresample's 192 kHz upsampling of it (recomputed on
+ * the fly, never stored; exact-rational rates only, else AMX_ERANGE) -- libebur128's
+ * K filter, 400 ms / 3 s blocks and sample peak at 192 kHz.
+ * K-filter zero-state GEMV per segment + exact scan + sample peaks.
+ * d_edge [n_tracks][2][16][2] int16: the 16 output frames before and after a span
+ * that does not start / end its track (the neighbour ranks' frames, which the
+ * resampler's 32-tap window reaches); NULL when every span is a whole track.
  * d_kw_tail [n_tracks][2][4]: K-filter state at each span end assuming the span
  * started from rest (what the NEXT rank of a chunk-sharded track needs, see
- * amx_kw_propagate; NULL = not wanted, e.g. one GPU); d_peak [n_tracks][2]: max |x|
- * per channel (zeroed here). */
-AMX_API int amx_loudness_pass1(amx_plan *plan, const int16_t *d_out, double *d_kw_tail, double *d_peak,
-                       void *d_ws, void *stream);
+ * amx_kw_propagate; NULL = not wanted, e.g. one GPU); d_peak [n_tracks][4]: per
+ * channel the measured (192 kHz) stream's max |x| (loudnorm's input_tp), then
+ * d_out's own max |x| (the limiter's input bound). */
+AMX_API int amx_loudness_pass1(amx_plan *plan, const int16_t *d_out, const int16_t *d_edge,
+                               double *d_kw_tail, double *d_peak, void *d_ws, void *stream);
 /* Host helper for chunk-sharded tracks: out8 = A^frames * in8 (per channel 4x4 K-filter
- * transition), so carry(r+1) = A^{len_r} carry(r) + tail(r). */
+ * transition at the measurement rate; frames of the measurement stream), so
+ * carry(r+1) = A^{len_r} carry(r) + tail(r). */
 AMX_API int amx_kw_propagate(const amx_plan *plan, int64_t frames, const double *in8, double *out8);
 /* Loudness pass 2: K-filter from the exact state (d_kw_carry [n_tracks][2][4] = state
  * entering each span, NULL = rest: then the start states amx_loudness_pass1 left are
  * reused, so pass 1 must run first on the same d_ws), squared and summed per 100 ms hop on the
  * WHOLE-track hop grid: d_hops [n_tracks][max_hops][2] (zeroed here; hops a span only
  * partly covers hold partial sums -- sum them over ranks, e.g. RCCL all-reduce). */
-AMX_API int amx_loudness_pass2(amx_plan *plan, const int16_t *d_out, const double *d_kw_carry,
-                       double *d_hops, int64_t max_hops, void *d_ws, void *stream);
+AMX_API int amx_loudness_pass2(amx_plan *plan, const int16_t *d_out, const int16_t *d_edge,
+                               const double *d_kw_carry, double *d_hops, int64_t max_hops,
+                               void *d_ws, void *stream);
 /* Gating-block (400 ms / 100 ms hop) and short-term (3 s / 1 s) histograms from
  * whole-track hop energies.  d_hist, d_st_hist [n_tracks][1000] uint64 (zeroed here). */
 AMX_API int amx_loudness_histograms(amx_plan *plan, const double *d_hops, int64_t max_hops,
@@ -235,7 +249,9 @@ AMX_API int amx_limiter_prepare(amx_plan *plan, const amx_final_desc *fd, int32_
  * :229-242): per track, from the histograms and sample peak:
  *   d_stats [n_tracks][16] doubles: I, LRA, thresh, TP(dB), the same four after
  *     ffmpeg's "%.2f" print + parse, mode (0 off, 1 skip = silent, 2 linear,
- *     3 dynamic = unsupported), gain, limiter-idle flag, sample peak;
+ *     3 dynamic = unsupported), gain, limiter-idle flag, measured (192 kHz) sample
+ *     peak, d_out's sample peak;
+ *   d_peak [n_tracks][4] from amx_loudness_pass1;
  *   d_gains [n_tracks]: the linear gain, or -1 (no normalisation);
  *   d_ctl [n_tracks] int32: bit 0 = limiter provably idle (AMX_CTL_FAST), bits 4..7
  *     mode -- consumed by amx_finalize without a host round trip.
@@ -253,7 +269,8 @@ AMX_API int amx_loudness_decide(amx_plan *plan, const amx_decide_desc *dd, const
 
 /* Chunk-sharded tracks: K-filter state entering this plan's (single) span from the
  * zero-start tails of the n_prev spans before it.  Setup (host, once): frames_after[q]
- * = frames between the end of span q and the start of this span.  Then, on the
+ * = d_out frames between the end of span q and the start of this span (converted to
+ * the measurement stream inside).  Then, on the
  * stream: d_carry [2][4] = sum_q A^{frames_after[q]} d_tails[q] (d_tails [n_prev][2][4]). */
 AMX_API int amx_kw_carry_setup(amx_plan *plan, int32_t n_prev, const int64_t *frames_after);
 AMX_API int amx_kw_carry(amx_plan *plan, const double *d_tails, double *d_carry, void *stream);

@@ -128,13 +128,16 @@ def test_loudness_histograms_vs_oracle(gpu, oracle_mod):
     hist = job.hist.cpu().numpy().view(np.uint64)[0]
     st = job.st_hist.cpu().numpy().view(np.uint64)[0]
     out = job.out[:n].cpu().numpy()
-    oh, ost, opk, nb = oracle_mod.ebur128(out, fs)
+    # ffmpeg's pass 1 measures the track upsampled to 192 kHz
+    oh, ost, opk, nb = oracle_mod.ebur128_192k(out, fs)
     assert hist.sum() == oh.sum() and st.sum() == ost.sum()
     # summation order differs (hop partials vs libebur128's ring sums): allow a
     # block to land in a neighbouring bin only when it sits on a boundary
     assert np.abs(hist.astype(np.int64) - oh.astype(np.int64)).sum() <= 2
     assert np.abs(st.astype(np.int64) - ost.astype(np.int64)).sum() <= 2
-    np.testing.assert_array_equal(job.peak.cpu().numpy()[0], opk)
+    pk = job.peak.cpu().numpy()[0]
+    np.testing.assert_array_equal(pk[:2], opk)                      # 192 kHz sample peak, bit-exact
+    np.testing.assert_array_equal(pk[2:], np.abs(out.astype(np.int32)).max(axis=0) / 32768.0)
     job.decide()
     assert job.fetch_report(raise_dynamic=False)["stats"][0] == oracle_mod.loudnorm_measure(out, fs)
 
@@ -156,12 +159,13 @@ def test_pipeline_vs_oracle(gpu, oracle_mod, fs, settings, seconds, seed):
     job = rep["job"]
     ref, info = oracle_mod.pipeline(oracle_mod.quantize(x), fs, settings, chunk_bounds(n, fs, 512))
     _cmp(job.out[:job.info.out_frames].cpu().numpy(), info["concat"], "concat fs=%d" % fs)
-    oh, ost, opk, _ = oracle_mod.ebur128(info["concat"], fs)
+    oh, ost, opk, _ = oracle_mod.ebur128_192k(info["concat"], fs)
     gh = job.hist.cpu().numpy().view(np.uint64)[0]
     gst = job.st_hist.cpu().numpy().view(np.uint64)[0]
     assert np.abs(gh.astype(np.int64) - oh.astype(np.int64)).sum() <= 2, np.nonzero(gh != oh)
     assert np.abs(gst.astype(np.int64) - ost.astype(np.int64)).sum() <= 2
     assert rep["stats"][0] == info["stats"], (rep["stats"], info["stats"])
+    np.testing.assert_array_equal(job.peak.cpu().numpy()[0][:2], opk)
     assert rep["modes"] == ["linear"]
     _cmp(y.cpu().numpy(), ref, "pipeline fs=%d" % fs)
 
@@ -379,3 +383,30 @@ def test_track_stream_matches_single_jobs(gpu, s16):
         torch.cuda.synchronize()
         assert torch.equal(y.cpu(), outs[i]), "track %d output" % i
         assert torch.equal(job.stats.cpu(), stats[i]), "track %d stats" % i
+
+
+@pytest.mark.parametrize("fs", [48000, 44100, 96000])
+def test_tp_decision_at_192k(gpu, oracle_mod, fs):
+    """The linear / dynamic decision (af_loudnorm, :240) on the 192 kHz input_tp: a
+    square-ish signal has inter-sample peaks well above its samples, so targets a
+    hair either side of TP + offset = -1.5 must flip the device's decision exactly
+    where the oracle's does -- and where a native-rate measurement would not."""
+    import torch
+    from amx import synth
+    from amx.engine import MasteringJob
+    n = int(fs * 12.0)
+    x = synth.music_like(n, fs, 2, seed=17, peak_dbfs=-1.0)
+    x = np.clip(x * 3.0, -0.5, 0.5).astype(np.float32)          # clipped: inter-sample overs
+    x16 = oracle_mod.quantize(x)
+    st = oracle_mod.loudnorm_measure(x16, fs)
+    st_native = oracle_mod.loudnorm_measure(x16, fs, native=True)
+    assert float(st["input_tp"]) > float(st_native["input_tp"])
+    edge = -1.5 - float(st["input_tp"]) + float(st["input_i"])    # target where TP + offset = -1.5
+    for target, want in ((edge - 0.01, "linear"), (edge, None), (edge + 0.01, "dynamic")):
+        target = round(target, 2)
+        job = MasteringJob(fs, 2, dict(lufs=target), [n], input_s16=True, chunks=[(0, 0, n)])
+        job.run(torch.from_numpy(x16).cuda())
+        rep = job.fetch_report(raise_dynamic=False)
+        assert rep["stats"][0] == st, (rep["stats"][0], st)
+        mode, _ = oracle_mod.loudnorm_linear_gain(st, target)
+        assert (want is None or mode == want) and rep["modes"] == [mode], (target, mode, rep["modes"])
