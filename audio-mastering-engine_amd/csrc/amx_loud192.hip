@@ -19,11 +19,11 @@
 // outputs); all segments of a plan share the phase pattern (the plan checks it), so
 // the bank row and the GEMV row of an output are wave-uniform (scalar loads).
 //   k_up1: pass 1 -- zero-state end state of the K filter per segment: a GEMV over
-//          the segment's outputs (G[n] = A^{Lout-1-n} B), for the scan.
+//          the segment's outputs (G[n] = A^{Lout-1-n} B), for the scan; and the
+//          sample peaks (192 kHz, loudnorm's input_tp; d_out's own, the limiter's).
 //   k_up1_part: the same for a span's last, partial segment (row alignment differs).
 //   k_up2: pass 2 -- the K filter (two DF-II-T biquads) from the exact segment start
-//          state, y^2 summed per 100 ms hop piece, and the sample peak of the 192 kHz
-//          samples (loudnorm's input_tp).
+//          state, y^2 summed per 100 ms hop piece.
 // M == 1 rates (48, 96, 32 kHz ...) take the unrolled path STATIC = L: every input
 // frame has outputs at phases 0 .. L-1 and phase 0 is the identity (the bank's
 // phase-0 row is a unit impulse: u = x exactly).
@@ -35,7 +35,7 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 #define UP_TAPS 32
 #define UP_C 15            // center tap
-#define UP_TB 16           // input frames per window block (STATIC path)
+#define UP_TB 8            // input frames per window block (STATIC path)
 
 __device__ __forceinline__ f2 up_frame(uint32_t w) {
     return f2{(float)lo16(w) * (1.0f / 32768.0f), (float)hi16(w) * (1.0f / 32768.0f)};
@@ -77,19 +77,30 @@ __device__ __forceinline__ f2 up_dot(const f2 *w, const float *__restrict__ h) {
 }
 
 // ------------------------------------------------------------ pass 1 (GEMV)
+// pass 1 also takes the sample peaks (loudnorm's input_tp from the 192 kHz samples,
+// and d_out's own peak for the limiter decision), so they are known -- and, at N > 1,
+// exchanged -- before pass 2.  xc = the input frame the output's window is centred on.
 struct Up1Acc {
     double e0[AMX_KW_DIM], e1[AMX_KW_DIM];
-    __device__ void init() {
+    f2 pk, px;
+    int len;
+    __device__ void init(int n_out) {
 #pragma unroll
         for (int d = 0; d < AMX_KW_DIM; d++) { e0[d] = 0.0; e1[d] = 0.0; }
+        pk = f2{0.0f, 0.0f};
+        px = f2{0.0f, 0.0f};
+        len = n_out;
     }
-    __device__ __forceinline__ void add(const double *__restrict__ g, f2 u) {
+    __device__ __forceinline__ void add(int n, const double *__restrict__ g, f2 u, f2 xc) {
         const double u0 = (double)u.x, u1 = (double)u.y;
 #pragma unroll
         for (int d = 0; d < AMX_KW_DIM; d++) {
             e0[d] = fma(g[d], u0, e0[d]);
             e1[d] = fma(g[d], u1, e1[d]);
         }
+        const bool in = n < len;
+        pk = in ? f2{fmaxf(pk.x, fabsf(u.x)), fmaxf(pk.y, fabsf(u.y))} : pk;
+        px = in ? f2{fmaxf(px.x, fabsf(xc.x)), fmaxf(px.y, fabsf(xc.y))} : px;
     }
 };
 
@@ -98,32 +109,39 @@ struct Up2Acc {
     double c1[5], c2[5];
     double v0[4], v1[4];       // [biquad1 z0 z1, biquad2 z0 z1] per channel
     double p00, p01, p10, p11; // y^2 per (piece, channel)
-    f2 pk;
     int split;                 // first output of hop piece 1
     int len;                   // outputs of this segment
-    __device__ __forceinline__ void add(int n, f2 u) {
+    __device__ __forceinline__ void add(int n, const double *, f2 u, f2) {
         const bool in = n < len;
         const double u0 = (double)u.x, u1 = (double)u.y;
         const double a0 = bq_step(c1, v0[0], v0[1], u0);
-        const double y0 = bq_step(c2, v0[2], v0[3], a0);
+        double y0 = bq_step(c2, v0[2], v0[3], a0);
         const double a1 = bq_step(c1, v1[0], v1[1], u1);
-        const double y1 = bq_step(c2, v1[2], v1[3], a1);
-        const double q0 = in ? y0 * y0 : 0.0, q1 = in ? y1 * y1 : 0.0;
-        if (n < split) { p00 += q0; p01 += q1; }
-        else { p10 += q0; p11 += q1; }
-        const f2 au = f2{fabsf(u.x), fabsf(u.y)};
-        pk = in ? f2{fmaxf(pk.x, au.x), fmaxf(pk.y, au.y)} : pk;
+        double y1 = bq_step(c2, v1[2], v1[3], a1);
+        y0 = in ? y0 : 0.0;
+        y1 = in ? y1 : 0.0;
+        if (n < split) { p00 = fma(y0, y0, p00); p01 = fma(y1, y1, p01); }
+        else { p10 = fma(y0, y0, p10); p11 = fma(y1, y1, p11); }
     }
 };
 
-// STATIC = L (M == 1): unrolled window blocks; 0: general phase pattern from tables
+// a bank row as an opaque per-iteration pointer: without it the compiler hoists every
+// phase's 32 coefficients out of the block loop into SGPRs at once and spills them
+__device__ __forceinline__ const float *up_row(const float *bank, int ph) {
+    const float *h = bank + ph * UP_TAPS;
+    asm volatile("" : "+s"(h));
+    return h;
+}
+
+// STATIC = L (M == 1): unrolled window blocks of UP_TB input frames, outputs at phases
+// 0 .. L-1 of every frame; 0: general phase pattern from the tables
 template <int STATIC, class Acc, bool P1>
 __device__ __forceinline__ void up_run(const UpArgs &a, const SpanDev &sp, int t, int64_t g0,
                                        bool edge, Acc &acc) {
     const uint32_t *__restrict__ x = a.x;
     if constexpr (STATIC > 0) {
         constexpr int W = UP_TB + UP_TAPS - 1;                 // inputs [k0 - 15, k0 + TB + 16)
-        f2 w[W + 1];
+        f2 w[W];
         const uint32_t *xp = x + sp.out_off + g0 - UP_C;       // frame g0 - 15
 #pragma unroll
         for (int i = 0; i < W; i++)
@@ -135,18 +153,39 @@ __device__ __forceinline__ void up_run(const UpArgs &a, const SpanDev &sp, int t
             const bool more = b + 1 < nblk;
 #pragma unroll
             for (int i = 0; i < UP_TB; i++) {
-                const int64_t g = g0 - UP_C + (int64_t)(b + 1) * UP_TB + (W - UP_TB) + i;
-                nx[i] = more ? (edge ? up_word(x, a.edge, sp, t, g) : xp[(b + 1) * UP_TB + (W - UP_TB) + i]) : 0u;
+                // (past the last block: frame g0 - 15 again, in range, unused)
+                const int o = more ? (b + 1) * UP_TB + (W - UP_TB) + i : 0;
+                nx[i] = edge ? up_word(x, a.edge, sp, t, g0 - UP_C + o) : xp[o];
             }
-#pragma unroll
-            for (int kb = 0; kb < UP_TB; kb++) {
-                const int n0 = (b * UP_TB + kb) * STATIC;
+            const int nb0 = b * UP_TB * STATIC;
+            if constexpr (P1) {
+                // GEMV and peaks are order-free: phase-outer, one bank row live at a time
 #pragma unroll
                 for (int ph = 0; ph < STATIC; ph++) {
-                    const f2 u = ph == 0 ? w[kb + UP_C] : up_dot(w + kb, a.bank + ph * UP_TAPS);
-                    if constexpr (P1) acc.add(a.G + (int64_t)(n0 + ph) * AMX_KW_DIM, u);
-                    else acc.add(n0 + ph, u);
+                    const float *h = up_row(a.bank, ph);
+#pragma unroll
+                    for (int kb = 0; kb < UP_TB; kb++) {
+                        const int n = nb0 + kb * STATIC + ph;
+                        const f2 u = ph == 0 ? w[kb + UP_C] : up_dot(w + kb, h);
+                        acc.add(n, a.G + (int64_t)n * AMX_KW_DIM, u, w[kb + UP_C]);
+                    }
                 }
+            } else {
+                // the recursion needs output order: the block's samples first (phase
+                // outer), then the filter over them in order
+                f2 u[UP_TB][STATIC > 1 ? STATIC - 1 : 1];
+#pragma unroll
+                for (int ph = 1; ph < STATIC; ph++) {
+                    const float *h = up_row(a.bank, ph);
+#pragma unroll
+                    for (int kb = 0; kb < UP_TB; kb++) u[kb][ph - 1] = up_dot(w + kb, h);
+                }
+#pragma unroll
+                for (int kb = 0; kb < UP_TB; kb++)
+#pragma unroll
+                    for (int ph = 0; ph < STATIC; ph++)
+                        acc.add(nb0 + kb * STATIC + ph, nullptr, ph == 0 ? w[kb + UP_C] : u[kb][ph - 1],
+                                w[kb + UP_C]);
             }
 #pragma unroll
             for (int i = 0; i < W - UP_TB; i++) w[i] = w[i + UP_TB];
@@ -167,8 +206,7 @@ __device__ __forceinline__ void up_run(const UpArgs &a, const SpanDev &sp, int t
                 cur++;
             }
             const f2 u = up_dot(w, a.bank + a.oph[n] * UP_TAPS);
-            if constexpr (P1) acc.add(a.G + (int64_t)n * AMX_KW_DIM, u);
-            else acc.add(n, u);
+            acc.add(n, a.G + (int64_t)n * AMX_KW_DIM, u, w[UP_C]);
         }
     }
 }
@@ -182,13 +220,20 @@ __global__ void __launch_bounds__(AMX_UP_BLOCK) k_up1(UpArgs a) {
     const int64_t g0 = sg.out_pos - sp.out_off;
     const bool edge = g0 - UP_C < 0 || g0 + a.Lin + UP_TAPS - UP_C > sp.out_n;
     Up1Acc acc;
-    acc.init();
+    acc.init(valid ? sg.len : 0);
     up_run<STATIC, Up1Acc, true>(a, sp, sg.track, g0, edge, acc);
     // a span's partial last segment is k_up1_part's (its GEMV rows are right-aligned)
     if (valid && sg.len == a.Lout) {
         double *o = a.e + (int64_t)j * 2 * AMX_KW_DIM;
 #pragma unroll
         for (int d = 0; d < AMX_KW_DIM; d++) { o[d] = acc.e0[d]; o[AMX_KW_DIM + d] = acc.e1[d]; }
+    }
+    if (valid) {
+        uint32_t *q = a.pk + (int64_t)j * 4;
+        q[0] = __float_as_uint(acc.pk.x);
+        q[1] = __float_as_uint(acc.pk.y);
+        q[2] = (uint32_t)(acc.px.x * 32768.0f);      // |s16| / 32768: exact
+        q[3] = (uint32_t)(acc.px.y * 32768.0f);
     }
 }
 
@@ -204,7 +249,7 @@ __global__ void __launch_bounds__(64) k_up1_part(UpArgs a) {
     const int64_t g0 = sg.out_pos - sp.out_off;
     const int sh = a.Lout - sg.len;
     Up1Acc acc;
-    acc.init();
+    acc.init(sg.len);
     for (int n = lane; n < sg.len; n += 64) {
         const int base = a.obase[n], ph = a.oph[n];
         f2 w[UP_TAPS];
@@ -212,7 +257,7 @@ __global__ void __launch_bounds__(64) k_up1_part(UpArgs a) {
         for (int i = 0; i < UP_TAPS; i++)
             w[i] = up_frame(up_word(a.x, a.edge, sp, (int)blockIdx.x, g0 + base - UP_C + i));
         const f2 u = (a.static_l > 0 && ph == 0) ? w[UP_C] : up_dot(w, a.bank + ph * UP_TAPS);
-        acc.add(a.G + (int64_t)(n + sh) * AMX_KW_DIM, u);
+        acc.add(n, a.G + (int64_t)(n + sh) * AMX_KW_DIM, u, w[UP_C]);
     }
 #pragma unroll
     for (int d = 0; d < AMX_KW_DIM; d++)
@@ -248,7 +293,6 @@ __global__ void __launch_bounds__(AMX_UP_BLOCK) k_up2(UpArgs a) {
         acc.v1[d] = valid ? s[AMX_KW_DIM + d] : 0.0;
     }
     acc.p00 = acc.p01 = acc.p10 = acc.p11 = 0.0;
-    acc.pk = f2{0.0f, 0.0f};
     acc.len = valid ? sg.len : 0;
     const int64_t h0 = sg.tframe / a.hop;
     acc.split = (int)((h0 + 1) * a.hop - sg.tframe);
@@ -257,8 +301,6 @@ __global__ void __launch_bounds__(AMX_UP_BLOCK) k_up2(UpArgs a) {
         double *o = a.parts + (int64_t)j * 4;
         o[0] = acc.p00; o[1] = acc.p01; o[2] = acc.p10; o[3] = acc.p11;
         a.part_hop[j] = h0;
-        a.pk[(int64_t)j * 2] = __float_as_uint(acc.pk.x);
-        a.pk[(int64_t)j * 2 + 1] = __float_as_uint(acc.pk.y);
     }
 }
 
