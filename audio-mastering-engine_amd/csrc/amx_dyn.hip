@@ -207,17 +207,22 @@ __device__ __forceinline__ double lane_val(double v, int i) {
 
 // Wave-cooperative re-run of one segment's frames [f0, f1) (chunk-local; f0 a
 // multiple of 16) from the new start ns: every lane of the wave calls it with the
-// same arguments.  Per 64-frame window each lane loads and divides one frame
-// (coalesced; the next window's loads are in flight meanwhile) and the recurrence
-// runs on the lanes' values read out as scalar operands (v_readlane, no LDS round
-// trip); lanes 0, 16, 32, 48 keep the new state before their frame and rewrite that
-// checkpoint.  The stored checkpoints are the trajectory from the old start, so
-// at every 16-frame boundary the new state is compared with the stored one: once
-// they are equal the two trajectories are identical from there on, the remaining
-// checkpoints stand and the old end is the end.  Returns the segment's end state.
+// same arguments.  Per 64-frame window each lane loads one frame's m and forms its
+// inc = m / A and dec = m / R (coalesced; the next window's loads are in flight
+// meanwhile) and stores the three into LDS; the recurrence -- a chain of dependent
+// steps, the same on every lane -- then reads them 16 frames at a time as broadcast
+// LDS loads issued ahead of the chain, so a step is just its dependent min / max /
+// select (C5 made this chain the fix-up's critical path: runs of ~60 consecutive
+// mis-speculated segments in one wave, each re-run after the previous one).  Lanes
+// 0, 16, 32, 48 keep the new state before their frame and rewrite that checkpoint.
+// The stored checkpoints are the trajectory from the old start, so at every 16-frame
+// boundary the new state is compared with the stored one: once they are equal the two
+// trajectories are identical from there on, the remaining checkpoints stand and the
+// old end is the end.  Returns the segment's end state.
 template <bool RCP>
 __device__ double env_rerun_wave(const ChainDev &cd, const double *m, double *ckr, int64_t f0,
                                  int64_t f1, double ns, double old_end) {
+    __shared__ __attribute__((aligned(16))) double s_m[64], s_i[64], s_d[64];
     const int lane = threadIdx.x & 63;
     const bool ckl = (lane & (AMX_ENV_TF_ - 1)) == 0;
     double c = ns;
@@ -227,21 +232,32 @@ __device__ double env_rerun_wave(const ChainDev &cd, const double *m, double *ck
         const int64_t fn = base + 64 + lane;
         const double mn = fn < f1 ? m[fn] : 0.0;
         const double on = ckl && fn < f1 ? ckr[fn / AMX_ENV_TF_] : 0.0;
-        const double il = env_div<RCP>(ml, cd.env_A, cd.env_rA);
-        const double dl = env_div<RCP>(ml, cd.env_R, cd.env_rR);
+        s_m[lane] = ml;
+        s_i[lane] = env_div<RCP>(ml, cd.env_A, cd.env_rA);
+        s_d[lane] = env_div<RCP>(ml, cd.env_R, cd.env_rR);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
         double mine = c;
         int stop = 4;
 #pragma unroll
         for (int t = 0; t < 4; t++) {
+            double mv[16], iv[16], dv[16];
+#pragma unroll
+            for (int q = 0; q < 16; q += 2) {
+                const d2v a = *reinterpret_cast<const d2v *>(s_m + 16 * t + q);
+                const d2v b = *reinterpret_cast<const d2v *>(s_i + 16 * t + q);
+                const d2v d = *reinterpret_cast<const d2v *>(s_d + 16 * t + q);
+                mv[q] = a.x; mv[q + 1] = a.y;
+                iv[q] = b.x; iv[q + 1] = b.y;
+                dv[q] = d.x; dv[q + 1] = d.y;
+            }
             const bool same = base + 16 * t < f1 && c == lane_val(ol, 16 * t);
             if (__builtin_amdgcn_readfirstlane((int)same)) { stop = t; break; }
             mine = lane == 16 * t ? c : mine;            // state before frame base + 16 t
 #pragma unroll
-            for (int q = 0; q < 16; q++) {
-                const int i = 16 * t + q;
-                c = env_step3(c, lane_val(ml, i), lane_val(il, i), lane_val(dl, i));
-            }
+            for (int q = 0; q < 16; q++) c = env_step3(c, mv[q], iv[q], dv[q]);
         }
+        __builtin_amdgcn_wave_barrier();                  // LDS reads done before the next writes
         if (ckl && (lane >> 4) < stop && base + lane < f1) ckr[(base + lane) / AMX_ENV_TF_] = mine;
         if (stop < 4) return old_end;
         ml = mn;
