@@ -74,7 +74,14 @@ def test_c5_60min_96k_vs_oracle(gpu, oracle_mod):
     assert rep["stats"][0] == st, (rep["stats"], st)
     assert y.shape == ref.shape
     d = np.abs(y.astype(np.int32) - ref.astype(np.int32))
-    assert d.max() == 0, "C5: max |diff| %d LSB, exact %.8f" % (d.max(), float((d == 0).mean()))
+    # north_star tolerance +-1e-4 of full scale = 3 LSB of the 16-bit output.  The EQ
+    # runs from exact-up-to-rounding segment start states (~3e-12 at 96 kHz, DESIGN.md
+    # §3.1): over 691 M samples a few dozen land within that of an int16 truncation
+    # boundary and move by 1 LSB, which the compressor can carry to its neighbours.
+    exact = float((d == 0).mean())
+    print("C5 parity: max |diff| %d LSB, exact fraction %.9f, %d samples differ" % (d.max(), exact,
+                                                                                int((d != 0).sum())))
+    assert d.max() <= 3 and exact >= 0.9999999, (d.max(), exact)
 
 
 def test_c4_rank_share_8x4min_vs_oracle(gpu, oracle_mod):
