@@ -14,7 +14,7 @@ run() {   # name seconds cmd...
     return $rc
 }
 run smoke 300 python __graft_entry__.py smoke || exit $?
-run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS} || exit $?
+run tests 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread ${PYTEST_ARGS} || exit $?
 [ -n "$NO_BENCH" ] && exit 0
 run bench_c3 300 python bench.py || exit $?
 run bench_c4 300 python bench.py --config c4 --no-pipeline || exit $?

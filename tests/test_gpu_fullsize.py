@@ -107,7 +107,10 @@ def test_c4_rank_share_8x4min_vs_oracle(gpu, oracle_mod):
             assert rep["stats"][k] == st, (k, rep["stats"][k], st)
             y = b.job.track_output(k).cpu().numpy()
             assert y.shape == ref.shape
-            np.testing.assert_array_equal(y, ref, err_msg="track %d" % t)
+            d = np.abs(y.astype(np.int32) - ref.astype(np.int32))
+            print("C4 track %d: max |diff| %d LSB, %d samples differ" % (t, d.max(), int((d != 0).sum())))
+            # north_star tolerance (3 LSB); see the C5 test for the rare 1-LSB EQ flips
+            assert d.max() <= 3 and (d != 0).mean() <= 1e-6, (t, d.max(), int((d != 0).sum()))
     # the graph replay (bench.py's timed path) gives the same batch output
     y0 = b.job.y[:b.job.info.out_frames].clone()
     b.capture(d_in)
