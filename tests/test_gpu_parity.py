@@ -183,12 +183,15 @@ def test_batch_of_tracks_vs_oracle(gpu, oracle_mod):
     xs = [synth.mix_like(int(fs * 31.0), fs, 2, seed=1),
           synth.music_like(int(fs * 12.3), fs, 2, seed=2, peak_dbfs=-3.0),
           np.zeros((int(fs * 5.0), 2), np.float32)]
-    job = MasteringJob(fs, 2, C3, [x.shape[0] for x in xs], quantum=512)
+    # -16 LUFS: the music track's crest factor (192 kHz TP - I = 12.54 dB) would put a
+    # -14 LUFS target just past TP + offset = -1.5, i.e. into loudnorm's dynamic mode
+    settings = dict(C3, lufs=-16.0)
+    job = MasteringJob(fs, 2, settings, [x.shape[0] for x in xs], quantum=512)
     job.run(torch.from_numpy(np.ascontiguousarray(np.concatenate(xs))).cuda())
     rep = job.fetch_report()
     assert rep["modes"] == ["linear", "linear", "skip"], rep["modes"]
     for t, x in enumerate(xs):
-        ref, info = oracle_mod.pipeline(oracle_mod.quantize(x), fs, C3, chunk_bounds(x.shape[0], fs, 512))
+        ref, info = oracle_mod.pipeline(oracle_mod.quantize(x), fs, settings, chunk_bounds(x.shape[0], fs, 512))
         if t < 2:
             assert rep["stats"][t] == info["stats"], (t, rep["stats"][t], info["stats"])
         _cmp(job.track_output(t).cpu().numpy(), ref, "batch track %d" % t)
