@@ -16,14 +16,13 @@
 //
 // Both channels of a frame travel packed in one float2, so one v_pk_fma_f32 does a
 // tap of both channels.  One lane per K-filter segment (Lin input frames = Lout
-// outputs); all segments of a plan share the phase pattern (the plan checks it), so
-// the bank row and the GEMV row of an output are wave-uniform (scalar loads).
-//   k_up1: pass 1 -- zero-state end state of the K filter per segment: a GEMV over
-//          the segment's outputs (G[n] = A^{Lout-1-n} B), for the scan; and the
+// outputs, Lout dividing the 100 ms hop where the rate allows); all segments of a
+// plan share the phase pattern (the plan checks it), so a bank row is wave-uniform.
+//   k_up<P1>: pass 1 -- the K filter (two DF-II-T biquads) over the segment from
+//          rest: its end state is the zero-state end state the scan needs; and the
 //          sample peaks (192 kHz, loudnorm's input_tp; d_out's own, the limiter's).
-//   k_up1_part: the same for a span's last, partial segment (row alignment differs).
-//   k_up2: pass 2 -- the K filter (two DF-II-T biquads) from the exact segment start
-//          state, y^2 summed per 100 ms hop piece.
+//   k_up<P2>: pass 2 -- the K filter from the exact segment start state, y^2
+//          summed per 100 ms hop piece.
 // M == 1 rates (48, 96, 32 kHz ...) take the unrolled path STATIC = L: every input
 // frame has outputs at phases 0 .. L-1 and phase 0 is the identity (the bank's
 // phase-0 row is a unit impulse: u = x exactly).
@@ -76,68 +75,69 @@ __device__ __forceinline__ f2 up_dot(const f2 *w, const float *__restrict__ h) {
     return (b0 + b2) + (b1 + b3);
 }
 
-// ------------------------------------------------------------ pass 1 (GEMV)
-// pass 1 also takes the sample peaks (loudnorm's input_tp from the 192 kHz samples,
-// and d_out's own peak for the limiter decision), so they are known -- and, at N > 1,
-// exchanged -- before pass 2.  xc = the input frame the output's window is centred on.
-struct Up1Acc {
-    double e0[AMX_KW_DIM], e1[AMX_KW_DIM];
-    f2 pk, px;
-    int len;
-    __device__ void init(int n_out) {
-#pragma unroll
-        for (int d = 0; d < AMX_KW_DIM; d++) { e0[d] = 0.0; e1[d] = 0.0; }
-        pk = f2{0.0f, 0.0f};
-        px = f2{0.0f, 0.0f};
-        len = n_out;
-    }
-    __device__ __forceinline__ void add(int n, const double *__restrict__ g, f2 u, f2 xc) {
-        const double u0 = (double)u.x, u1 = (double)u.y;
-#pragma unroll
-        for (int d = 0; d < AMX_KW_DIM; d++) {
-            e0[d] = fma(g[d], u0, e0[d]);
-            e1[d] = fma(g[d], u1, e1[d]);
-        }
-        const bool in = n < len;
-        pk = in ? f2{fmaxf(pk.x, fabsf(u.x)), fmaxf(pk.y, fabsf(u.y))} : pk;
-        px = in ? f2{fmaxf(px.x, fabsf(xc.x)), fmaxf(px.y, fabsf(xc.y))} : px;
-    }
-};
-
-// ------------------------------------------------------------ pass 2 (filter)
-struct Up2Acc {
+// ------------------------------------------------------------ accumulators
+// Both passes run the K filter (two DF-II-T biquads per channel, the state order of
+// the scan's model [bq1 z0 z1, bq2 z0 z1]) over the segment's 192 kHz samples in
+// order: pass 1 from rest -- its end state IS the zero-state end state the scan
+// needs -- and pass 2 from the exact start state, summing y^2 per hop piece.
+// FAST: every lane of the wave has a whole segment inside one hop and away from the
+// span ends -- no masks, no hop split, no edge reads (all but ~one wave per span).
+template <bool P1, bool FAST>
+struct UpAcc {
     double c1[5], c2[5];
-    double v0[4], v1[4];       // [biquad1 z0 z1, biquad2 z0 z1] per channel
-    double p00, p01, p10, p11; // y^2 per (piece, channel)
-    int split;                 // first output of hop piece 1
-    int len;                   // outputs of this segment
-    __device__ __forceinline__ void add(int n, const double *, f2 u, f2) {
-        const bool in = n < len;
+    double v0[4], v1[4];
+    double p00, p01, p10, p11;   // pass 2: y^2 per (piece, channel)
+    f2 pk, px;                   // pass 1: 192 kHz |u| max, d_out |x| max
+    int split, len;
+    __device__ __forceinline__ void add(int n, f2 u, f2 xc) {
         const double u0 = (double)u.x, u1 = (double)u.y;
-        const double a0 = bq_step(c1, v0[0], v0[1], u0);
-        double y0 = bq_step(c2, v0[2], v0[3], a0);
-        const double a1 = bq_step(c1, v1[0], v1[1], u1);
-        double y1 = bq_step(c2, v1[2], v1[3], a1);
-        y0 = in ? y0 : 0.0;
-        y1 = in ? y1 : 0.0;
-        if (n < split) { p00 = fma(y0, y0, p00); p01 = fma(y1, y1, p01); }
-        else { p10 = fma(y0, y0, p10); p11 = fma(y1, y1, p11); }
+        if constexpr (P1 && !FAST) {
+            double w0[4], w1[4];
+#pragma unroll
+            for (int d = 0; d < 4; d++) { w0[d] = v0[d]; w1[d] = v1[d]; }
+            const double a0 = bq_step(c1, v0[0], v0[1], u0);
+            (void)bq_step(c2, v0[2], v0[3], a0);
+            const double a1 = bq_step(c1, v1[0], v1[1], u1);
+            (void)bq_step(c2, v1[2], v1[3], a1);
+            const bool in = n < len;              // past a partial segment's end: state held
+#pragma unroll
+            for (int d = 0; d < 4; d++) { v0[d] = in ? v0[d] : w0[d]; v1[d] = in ? v1[d] : w1[d]; }
+            pk = in ? f2{fmaxf(pk.x, fabsf(u.x)), fmaxf(pk.y, fabsf(u.y))} : pk;
+            px = in ? f2{fmaxf(px.x, fabsf(xc.x)), fmaxf(px.y, fabsf(xc.y))} : px;
+        } else if constexpr (P1) {
+            const double a0 = bq_step(c1, v0[0], v0[1], u0);
+            (void)bq_step(c2, v0[2], v0[3], a0);
+            const double a1 = bq_step(c1, v1[0], v1[1], u1);
+            (void)bq_step(c2, v1[2], v1[3], a1);
+            pk = f2{fmaxf(pk.x, fabsf(u.x)), fmaxf(pk.y, fabsf(u.y))};
+            px = f2{fmaxf(px.x, fabsf(xc.x)), fmaxf(px.y, fabsf(xc.y))};
+        } else {
+            const double a0 = bq_step(c1, v0[0], v0[1], u0);
+            double y0 = bq_step(c2, v0[2], v0[3], a0);
+            const double a1 = bq_step(c1, v1[0], v1[1], u1);
+            double y1 = bq_step(c2, v1[2], v1[3], a1);
+            if constexpr (FAST) {
+                p00 = fma(y0, y0, p00);
+                p01 = fma(y1, y1, p01);
+            } else {
+                const bool in = n < len;
+                y0 = in ? y0 : 0.0;
+                y1 = in ? y1 : 0.0;
+                if (n < split) { p00 = fma(y0, y0, p00); p01 = fma(y1, y1, p01); }
+                else { p10 = fma(y0, y0, p10); p11 = fma(y1, y1, p11); }
+            }
+        }
     }
 };
-
-// a bank row as an opaque per-iteration pointer: without it the compiler hoists every
-// phase's 32 coefficients out of the block loop into SGPRs at once and spills them
-__device__ __forceinline__ const float *up_row(const float *bank, int ph) {
-    const float *h = bank + ph * UP_TAPS;
-    asm volatile("" : "+s"(h));
-    return h;
-}
 
 // STATIC = L (M == 1): unrolled window blocks of UP_TB input frames, outputs at phases
-// 0 .. L-1 of every frame; 0: general phase pattern from the tables
-template <int STATIC, class Acc, bool P1>
+// 0 .. L-1 of every frame; 0: general phase pattern from the tables.
+// sb: the bank in LDS (STATIC); zp: an LDS word holding 0, read every block so the
+// compiler cannot hoist the bank rows out of the block loop (all rows live at once
+// would not fit the registers)
+template <int STATIC, bool FAST, class Acc>
 __device__ __forceinline__ void up_run(const UpArgs &a, const SpanDev &sp, int t, int64_t g0,
-                                       bool edge, Acc &acc) {
+                                       bool vec, const float *sb, const int *zp, Acc &acc) {
     const uint32_t *__restrict__ x = a.x;
     if constexpr (STATIC > 0) {
         constexpr int W = UP_TB + UP_TAPS - 1;                 // inputs [k0 - 15, k0 + TB + 16)
@@ -145,48 +145,43 @@ __device__ __forceinline__ void up_run(const UpArgs &a, const SpanDev &sp, int t
         const uint32_t *xp = x + sp.out_off + g0 - UP_C;       // frame g0 - 15
 #pragma unroll
         for (int i = 0; i < W; i++)
-            w[i] = up_frame(edge ? up_word(x, a.edge, sp, t, g0 - UP_C + i) : xp[i]);
+            w[i] = up_frame(FAST ? xp[i] : up_word(x, a.edge, sp, t, g0 - UP_C + i));
         const int nblk = a.Lin / UP_TB;
         for (int b = 0; b < nblk; b++) {
-            // next block's new inputs in flight while this block computes
+            // next block's new frames in flight while this block computes (past the
+            // last block: frames of this one again, in range, unused)
             uint32_t nx[UP_TB];
-            const bool more = b + 1 < nblk;
+            const int o0 = (b + 1 < nblk ? (b + 1) * UP_TB : b * UP_TB) + (W - UP_TB);
+            if (FAST && vec) {                                  // 16-B aligned rows
 #pragma unroll
-            for (int i = 0; i < UP_TB; i++) {
-                // (past the last block: frame g0 - 15 again, in range, unused)
-                const int o = more ? (b + 1) * UP_TB + (W - UP_TB) + i : 0;
-                nx[i] = edge ? up_word(x, a.edge, sp, t, g0 - UP_C + o) : xp[o];
-            }
-            const int nb0 = b * UP_TB * STATIC;
-            if constexpr (P1) {
-                // GEMV and peaks are order-free: phase-outer, one bank row live at a time
-#pragma unroll
-                for (int ph = 0; ph < STATIC; ph++) {
-                    const float *h = up_row(a.bank, ph);
-#pragma unroll
-                    for (int kb = 0; kb < UP_TB; kb++) {
-                        const int n = nb0 + kb * STATIC + ph;
-                        const f2 u = ph == 0 ? w[kb + UP_C] : up_dot(w + kb, h);
-                        acc.add(n, a.G + (int64_t)n * AMX_KW_DIM, u, w[kb + UP_C]);
-                    }
+                for (int i = 0; i < UP_TB; i += 4) {
+                    const uint4 q = *reinterpret_cast<const uint4 *>(xp + o0 + i);
+                    nx[i] = q.x; nx[i + 1] = q.y; nx[i + 2] = q.z; nx[i + 3] = q.w;
                 }
             } else {
-                // the recursion needs output order: the block's samples first (phase
-                // outer), then the filter over them in order
-                f2 u[UP_TB][STATIC > 1 ? STATIC - 1 : 1];
 #pragma unroll
-                for (int ph = 1; ph < STATIC; ph++) {
-                    const float *h = up_row(a.bank, ph);
+                for (int i = 0; i < UP_TB; i++)
+                    nx[i] = FAST ? xp[o0 + i] : up_word(x, a.edge, sp, t, g0 - UP_C + o0 + i);
+            }
+            const int nb0 = b * UP_TB * STATIC;
+            const float *bk = sb + zp[b & 1];
+            f2 u[UP_TB][STATIC > 1 ? STATIC - 1 : 1];
 #pragma unroll
-                    for (int kb = 0; kb < UP_TB; kb++) u[kb][ph - 1] = up_dot(w + kb, h);
+            for (int ph = 1; ph < STATIC; ph++) {
+                float h[UP_TAPS];
+#pragma unroll
+                for (int i = 0; i < UP_TAPS; i += 4) {
+                    const float4 q = *reinterpret_cast<const float4 *>(bk + ph * UP_TAPS + i);
+                    h[i] = q.x; h[i + 1] = q.y; h[i + 2] = q.z; h[i + 3] = q.w;
                 }
 #pragma unroll
-                for (int kb = 0; kb < UP_TB; kb++)
-#pragma unroll
-                    for (int ph = 0; ph < STATIC; ph++)
-                        acc.add(nb0 + kb * STATIC + ph, nullptr, ph == 0 ? w[kb + UP_C] : u[kb][ph - 1],
-                                w[kb + UP_C]);
+                for (int kb = 0; kb < UP_TB; kb++) u[kb][ph - 1] = up_dot(w + kb, h);
             }
+#pragma unroll
+            for (int kb = 0; kb < UP_TB; kb++)
+#pragma unroll
+                for (int ph = 0; ph < STATIC; ph++)
+                    acc.add(nb0 + kb * STATIC + ph, ph == 0 ? w[kb + UP_C] : u[kb][ph - 1], w[kb + UP_C]);
 #pragma unroll
             for (int i = 0; i < W - UP_TB; i++) w[i] = w[i + UP_TB];
 #pragma unroll
@@ -205,128 +200,106 @@ __device__ __forceinline__ void up_run(const UpArgs &a, const SpanDev &sp, int t
                 w[UP_TAPS - 1] = up_frame(up_word(x, a.edge, sp, t, g0 + cur + UP_TAPS - UP_C));
                 cur++;
             }
-            const f2 u = up_dot(w, a.bank + a.oph[n] * UP_TAPS);
-            acc.add(n, a.G + (int64_t)n * AMX_KW_DIM, u, w[UP_C]);
+            acc.add(n, up_dot(w, a.bank + a.oph[n] * UP_TAPS), w[UP_C]);
         }
     }
 }
 
-template <int STATIC>
-__global__ void __launch_bounds__(AMX_UP_BLOCK) k_up1(UpArgs a) {
-    const int j = blockIdx.x * AMX_UP_BLOCK + threadIdx.x;
-    const bool valid = j < a.n_kseg;
-    const KwSegDev sg = a.ks[valid ? j : a.n_kseg - 1];
-    const SpanDev sp = a.spans[sg.track];
-    const int64_t g0 = sg.out_pos - sp.out_off;
-    const bool edge = g0 - UP_C < 0 || g0 + a.Lin + UP_TAPS - UP_C > sp.out_n;
-    Up1Acc acc;
-    acc.init(valid ? sg.len : 0);
-    up_run<STATIC, Up1Acc, true>(a, sp, sg.track, g0, edge, acc);
-    // a span's partial last segment is k_up1_part's (its GEMV rows are right-aligned)
-    if (valid && sg.len == a.Lout) {
-        double *o = a.e + (int64_t)j * 2 * AMX_KW_DIM;
-#pragma unroll
-        for (int d = 0; d < AMX_KW_DIM; d++) { o[d] = acc.e0[d]; o[AMX_KW_DIM + d] = acc.e1[d]; }
-    }
-    if (valid) {
-        uint32_t *q = a.pk + (int64_t)j * 4;
-        q[0] = __float_as_uint(acc.pk.x);
-        q[1] = __float_as_uint(acc.pk.y);
-        q[2] = (uint32_t)(acc.px.x * 32768.0f);      // |s16| / 32768: exact
-        q[3] = (uint32_t)(acc.px.y * 32768.0f);
-    }
-}
-
-// one wave per span: its last segment when partial (len < Lout): lane l takes the
-// outputs n = l, l + 64, ... with its own window, rows G[n + Lout - len]
-__global__ void __launch_bounds__(64) k_up1_part(UpArgs a) {
-    const SpanDev sp = a.spans[blockIdx.x];
-    if (sp.nkseg == 0) return;
-    const int j = sp.kseg0 + sp.nkseg - 1;
-    const KwSegDev sg = a.ks[j];
-    if (sg.len == a.Lout) return;
+// both passes: P1 = pass 1 (from rest: end state + peaks), else pass 2 (hop pieces)
+template <int STATIC, bool P1>
+__global__ void __launch_bounds__(AMX_UP_BLOCK) k_up(UpArgs a) {
+    __shared__ __attribute__((aligned(16))) float sb[STATIC > 0 ? STATIC * UP_TAPS : 4];
+    __shared__ int zp[2];
     const int lane = threadIdx.x;
-    const int64_t g0 = sg.out_pos - sp.out_off;
-    const int sh = a.Lout - sg.len;
-    Up1Acc acc;
-    acc.init(sg.len);
-    for (int n = lane; n < sg.len; n += 64) {
-        const int base = a.obase[n], ph = a.oph[n];
-        f2 w[UP_TAPS];
-#pragma unroll
-        for (int i = 0; i < UP_TAPS; i++)
-            w[i] = up_frame(up_word(a.x, a.edge, sp, (int)blockIdx.x, g0 + base - UP_C + i));
-        const f2 u = (a.static_l > 0 && ph == 0) ? w[UP_C] : up_dot(w, a.bank + ph * UP_TAPS);
-        acc.add(n, a.G + (int64_t)(n + sh) * AMX_KW_DIM, u, w[UP_C]);
+    if constexpr (STATIC > 0) {
+        for (int i = lane; i < STATIC * UP_TAPS; i += AMX_UP_BLOCK) sb[i] = a.bank[i];
     }
-#pragma unroll
-    for (int d = 0; d < AMX_KW_DIM; d++)
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            acc.e0[d] += __shfl_xor(acc.e0[d], o);
-            acc.e1[d] += __shfl_xor(acc.e1[d], o);
-        }
-    if (lane == 0) {
-        double *o = a.e + (int64_t)j * 2 * AMX_KW_DIM;
-#pragma unroll
-        for (int d = 0; d < AMX_KW_DIM; d++) { o[d] = acc.e0[d]; o[AMX_KW_DIM + d] = acc.e1[d]; }
-    }
-}
-
-template <int STATIC>
-__global__ void __launch_bounds__(AMX_UP_BLOCK) k_up2(UpArgs a) {
-    const int j = blockIdx.x * AMX_UP_BLOCK + threadIdx.x;
+    if (lane < 2) zp[lane] = 0;
+    __syncthreads();
+    const int j = blockIdx.x * AMX_UP_BLOCK + lane;
     const bool valid = j < a.n_kseg;
     const KwSegDev sg = a.ks[valid ? j : a.n_kseg - 1];
     const SpanDev sp = a.spans[sg.track];
     const int64_t g0 = sg.out_pos - sp.out_off;
     const bool edge = g0 - UP_C < 0 || g0 + a.Lin + UP_TAPS - UP_C > sp.out_n;
-    Up2Acc acc;
-#pragma unroll
-    for (int i = 0; i < 3; i++) { acc.c1[i] = a.cd->kw1[i]; acc.c2[i] = a.cd->kw2[i]; }
-    acc.c1[3] = a.cd->kw1[4]; acc.c1[4] = a.cd->kw1[5];
-    acc.c2[3] = a.cd->kw2[4]; acc.c2[4] = a.cd->kw2[5];
-    const double *s = a.s + (int64_t)(valid ? j : 0) * 2 * AMX_KW_DIM;
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-        acc.v0[d] = valid ? s[d] : 0.0;
-        acc.v1[d] = valid ? s[AMX_KW_DIM + d] : 0.0;
-    }
-    acc.p00 = acc.p01 = acc.p10 = acc.p11 = 0.0;
-    acc.len = valid ? sg.len : 0;
     const int64_t h0 = sg.tframe / a.hop;
-    acc.split = (int)((h0 + 1) * a.hop - sg.tframe);
-    up_run<STATIC, Up2Acc, false>(a, sp, sg.track, g0, edge, acc);
-    if (valid) {
+    const int split = (int)((h0 + 1) * a.hop - sg.tframe);
+    const int len = valid ? sg.len : 0;
+    const bool fast = valid && !edge && len == a.Lout && (P1 || split >= a.Lout);
+    // 16-B loads when every lane's window rows are 16-B aligned
+    const bool vec = __ballot(((sp.out_off + g0 - UP_C + (UP_TAPS - 1)) & 3) != 0) == 0;
+    UpAcc<P1, true> af;
+    UpAcc<P1, false> ag;
+    auto setup = [&](auto &acc) {
+#pragma unroll
+        for (int i = 0; i < 3; i++) { acc.c1[i] = a.cd->kw1[i]; acc.c2[i] = a.cd->kw2[i]; }
+        acc.c1[3] = a.cd->kw1[4]; acc.c1[4] = a.cd->kw1[5];
+        acc.c2[3] = a.cd->kw2[4]; acc.c2[4] = a.cd->kw2[5];
+        const double *s0 = a.s + (int64_t)(valid ? j : 0) * 2 * AMX_KW_DIM;
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            acc.v0[d] = (!P1 && valid) ? s0[d] : 0.0;
+            acc.v1[d] = (!P1 && valid) ? s0[AMX_KW_DIM + d] : 0.0;
+        }
+        acc.p00 = acc.p01 = acc.p10 = acc.p11 = 0.0;
+        acc.pk = f2{0.0f, 0.0f};
+        acc.px = f2{0.0f, 0.0f};
+        acc.split = split;
+        acc.len = len;
+    };
+    double v0[4], v1[4], p[4];
+    f2 pk, px;
+    auto take = [&](auto &acc) {
+#pragma unroll
+        for (int d = 0; d < 4; d++) { v0[d] = acc.v0[d]; v1[d] = acc.v1[d]; }
+        p[0] = acc.p00; p[1] = acc.p01; p[2] = acc.p10; p[3] = acc.p11;
+        pk = acc.pk;
+        px = acc.px;
+    };
+    if (__ballot(!fast) == 0) {
+        setup(af);
+        up_run<STATIC, true>(a, sp, sg.track, g0, vec, sb, zp, af);
+        take(af);
+    } else {
+        setup(ag);
+        up_run<STATIC, false>(a, sp, sg.track, g0, vec, sb, zp, ag);
+        take(ag);
+    }
+    if (!valid) return;
+    if constexpr (P1) {
+        double *o = a.e + (int64_t)j * 2 * AMX_KW_DIM;
+#pragma unroll
+        for (int d = 0; d < AMX_KW_DIM; d++) { o[d] = v0[d]; o[AMX_KW_DIM + d] = v1[d]; }
+        uint32_t *q = a.pk + (int64_t)j * 4;
+        q[0] = __float_as_uint(pk.x);
+        q[1] = __float_as_uint(pk.y);
+        q[2] = (uint32_t)(px.x * 32768.0f);      // |s16| / 32768: exact
+        q[3] = (uint32_t)(px.y * 32768.0f);
+    } else {
         double *o = a.parts + (int64_t)j * 4;
-        o[0] = acc.p00; o[1] = acc.p01; o[2] = acc.p10; o[3] = acc.p11;
+        o[0] = p[0]; o[1] = p[1]; o[2] = p[2]; o[3] = p[3];
         a.part_hop[j] = h0;
     }
 }
 
-hipError_t launch_up1(const UpArgs &a, int n_spans, hipStream_t st) {
+template <bool P1>
+static hipError_t up_launch(const UpArgs &a, hipStream_t st) {
     if (a.n_kseg <= 0) return hipSuccess;
     const dim3 g((unsigned)((a.n_kseg + AMX_UP_BLOCK - 1) / AMX_UP_BLOCK));
     switch (a.static_l) {
-    case 0: hipLaunchKernelGGL(k_up1<0>, g, dim3(AMX_UP_BLOCK), 0, st, a); break;
-    case 2: hipLaunchKernelGGL(k_up1<2>, g, dim3(AMX_UP_BLOCK), 0, st, a); break;
-    case 4: hipLaunchKernelGGL(k_up1<4>, g, dim3(AMX_UP_BLOCK), 0, st, a); break;
+    case 0: hipLaunchKernelGGL((k_up<0, P1>), g, dim3(AMX_UP_BLOCK), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((k_up<2, P1>), g, dim3(AMX_UP_BLOCK), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((k_up<4, P1>), g, dim3(AMX_UP_BLOCK), 0, st, a); break;
     default: return hipErrorInvalidValue;
     }
-    hipLaunchKernelGGL(k_up1_part, dim3((unsigned)n_spans), dim3(64), 0, st, a);
     return hipGetLastError();
 }
 
-hipError_t launch_up2(const UpArgs &a, hipStream_t st) {
-    if (a.n_kseg <= 0) return hipSuccess;
-    const dim3 g((unsigned)((a.n_kseg + AMX_UP_BLOCK - 1) / AMX_UP_BLOCK));
-    switch (a.static_l) {
-    case 0: hipLaunchKernelGGL(k_up2<0>, g, dim3(AMX_UP_BLOCK), 0, st, a); break;
-    case 2: hipLaunchKernelGGL(k_up2<2>, g, dim3(AMX_UP_BLOCK), 0, st, a); break;
-    case 4: hipLaunchKernelGGL(k_up2<4>, g, dim3(AMX_UP_BLOCK), 0, st, a); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
+hipError_t launch_up1(const UpArgs &a, int n_spans, hipStream_t st) {
+    (void)n_spans;
+    return up_launch<true>(a, st);
 }
+
+hipError_t launch_up2(const UpArgs &a, hipStream_t st) { return up_launch<false>(a, st); }
 
 }  // namespace amx

@@ -361,7 +361,14 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         if (amx::swr_geometry(fs, kfs, &p->upL, &p->upM) != 0) {
             p->up_ok = 0;     // no exact-rational resampler: amx_loudness_pass1 fails
         } else {
-            const int kk = std::max(1, (512 + p->upL / 2) / p->upL);
+            // ~384 192 kHz outputs per K segment, a divisor of the 100 ms hop (19200)
+            // where one exists, so a segment lies inside one hop (no hop split)
+            const int hop192 = (kfs + 5) / 10;
+            int kk = std::max(1, (384 + p->upL / 2) / p->upL);
+            for (int d = 0; d <= kk; d++) {
+                if (kk - d >= 1 && hop192 % (p->upL * (kk - d)) == 0 && (p->upM * (kk - d)) % 8 == 0) { kk -= d; break; }
+                if (hop192 % (p->upL * (kk + d)) == 0 && (p->upM * (kk + d)) % 8 == 0) { kk += d; break; }
+            }
             p->upLin = p->upM * kk;
             p->upLout = p->upL * kk;
             bank.assign((size_t)p->upL * 32, 0.0f);
@@ -370,7 +377,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             bool ident0 = bank[15] == 1.0f;
             for (int i = 0; i < 32; i++) ident0 = ident0 && (i == 15 || bank[i] == 0.0f);
             p->up_static = (p->upM == 1 && (p->upL == 2 || p->upL == 4) && ident0 &&
-                            p->upLin % 16 == 0) ? p->upL : 0;
+                            p->upLin % 8 == 0) ? p->upL : 0;
         }
     }
     p->hop = (kfs + 5) / 10;                   // libebur128 samples_in_100ms at 192 kHz
