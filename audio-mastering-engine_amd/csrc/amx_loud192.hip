@@ -34,7 +34,15 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 #define UP_TAPS 32
 #define UP_C 15            // center tap
-#define UP_TB 8            // input frames per window block (STATIC path)
+// input frames per window block of the STATIC path: the window (TB + 31 frames) and the
+// block's samples (TB (L - 1)) live in registers
+#ifndef AMX_UP_TB4
+#define AMX_UP_TB4 4
+#endif
+template <int L> struct UpTB { static constexpr int v = L >= 4 ? AMX_UP_TB4 : 8; };
+#ifndef AMX_UP_WAVES
+#define AMX_UP_WAVES 3     // waves per SIMD the register budget must allow
+#endif
 
 __device__ __forceinline__ f2 up_frame(uint32_t w) {
     return f2{(float)lo16(w) * (1.0f / 32768.0f), (float)hi16(w) * (1.0f / 32768.0f)};
@@ -140,6 +148,7 @@ __device__ __forceinline__ void up_run(const UpArgs &a, const SpanDev &sp, int t
                                        bool vec, const float *sb, const int *zp, Acc &acc) {
     const uint32_t *__restrict__ x = a.x;
     if constexpr (STATIC > 0) {
+        constexpr int UP_TB = UpTB<STATIC>::v;
         constexpr int W = UP_TB + UP_TAPS - 1;                 // inputs [k0 - 15, k0 + TB + 16)
         f2 w[W];
         const uint32_t *xp = x + sp.out_off + g0 - UP_C;       // frame g0 - 15
@@ -164,16 +173,14 @@ __device__ __forceinline__ void up_run(const UpArgs &a, const SpanDev &sp, int t
                     nx[i] = FAST ? xp[o0 + i] : up_word(x, a.edge, sp, t, g0 - UP_C + o0 + i);
             }
             const int nb0 = b * UP_TB * STATIC;
-            const float *bk = sb + zp[b & 1];
+            // the bank row through scalar loads (SGPR operands of the FMAs); the
+            // offset read from LDS (always 0) keeps the compiler from hoisting every
+            // row out of the loop at once
+            const float *bk = a.bank + __builtin_amdgcn_readfirstlane(zp[b & 1]);
             f2 u[UP_TB][STATIC > 1 ? STATIC - 1 : 1];
 #pragma unroll
             for (int ph = 1; ph < STATIC; ph++) {
-                float h[UP_TAPS];
-#pragma unroll
-                for (int i = 0; i < UP_TAPS; i += 4) {
-                    const float4 q = *reinterpret_cast<const float4 *>(bk + ph * UP_TAPS + i);
-                    h[i] = q.x; h[i + 1] = q.y; h[i + 2] = q.z; h[i + 3] = q.w;
-                }
+                const float *h = bk + ph * UP_TAPS;
 #pragma unroll
                 for (int kb = 0; kb < UP_TB; kb++) u[kb][ph - 1] = up_dot(w + kb, h);
             }
@@ -207,7 +214,8 @@ __device__ __forceinline__ void up_run(const UpArgs &a, const SpanDev &sp, int t
 
 // both passes: P1 = pass 1 (from rest: end state + peaks), else pass 2 (hop pieces)
 template <int STATIC, bool P1>
-__global__ void __launch_bounds__(AMX_UP_BLOCK) k_up(UpArgs a) {
+__global__ void __launch_bounds__(AMX_UP_BLOCK) __attribute__((amdgpu_waves_per_eu(AMX_UP_WAVES)))
+k_up(UpArgs a) {
     __shared__ __attribute__((aligned(16))) float sb[STATIC > 0 ? STATIC * UP_TAPS : 4];
     __shared__ int zp[2];
     const int lane = threadIdx.x;
