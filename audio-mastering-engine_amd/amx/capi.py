@@ -95,7 +95,7 @@ def load(path=None):
     global _lib
     if _lib is not None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("AMX_LIB") or LIB_PATH     # AMX_LIB: a variant build (experiments)
     if not os.path.exists(p):
         raise AmxError("libamx.so not found at %s -- build it with "
                        "`python -c 'import __graft_entry__ as g; g.build()'`" % p)

@@ -188,11 +188,15 @@ struct UpArgs {
     int static_l;             // L when M == 1 (unrolled kernels), else 0 (tables)
     int hop;
     const int32_t *obase, *oph;   // per output n < Lout: input frame (segment-relative), phase
+    const int32_t *slow;          // segments k_up_slow takes (NULL: all, when static_l == 0)
+    int64_t n_slow;
     const float *bank;            // [L][32] float32 polyphase bank
     const uint32_t *x, *edge;     // d_out (stereo s16 dwords); edge [tracks][2][AMX_UP_EDGE]
-    const double *G;              // pass 1: GEMV rows A^{Lout-1-n} B
+    const double *G;              // rows C A^n, n < Lout (the K filter's free response)
+    const double *qh, *qt;        // Gram matrices of those rows: head sums [Lout+1][16], tail sums
+    double *eterms;               // [seg][ch][10]: per hop piece sum yz^2, sum yz (C A^n)^T
     double *e;
-    const double *s;              // pass 2: segment start states
+    const double *s;              // segment start states (after the scan)
     double *parts;
     int64_t *part_hop;
     uint32_t *pk;                 // [seg][4]: 192 kHz |u| max L, R (float bits), native |x| L, R

@@ -14,15 +14,24 @@
 // ends (x[-k] = x[k], x[n+k] = x[n-1-k]); a span that does not start / end its track
 // reads the neighbouring rank's frames from the edge buffer instead.
 //
-// Both channels of a frame travel packed in one float2, so one v_pk_fma_f32 does a
-// tap of both channels.  One lane per K-filter segment (Lin input frames = Lout
-// outputs, Lout dividing the 100 ms hop where the rate allows); all segments of a
-// plan share the phase pattern (the plan checks it), so a bank row is wave-uniform.
-//   k_up<P1>: pass 1 -- the K filter (two DF-II-T biquads) over the segment from
-//          rest: its end state is the zero-state end state the scan needs; and the
-//          sample peaks (192 kHz, loudnorm's input_tp; d_out's own, the limiter's).
-//   k_up<P2>: pass 2 -- the K filter from the exact segment start state, y^2
-//          summed per 100 ms hop piece.
+// One lane per (K-filter segment, channel): lanes 2i / 2i+1 are the L / R channel of
+// segment i (Lin input frames = Lout outputs, Lout dividing the 100 ms hop where the
+// rate allows).  A lane's window of 32 + TB - 1 float samples, its filter state and
+// accumulators fit ~90 VGPRs, so 4+ waves per SIMD hide the dependent latencies (one
+// lane per segment with both channels packed in float2 needed ~150: two waves per
+// SIMD, measured 1.2-1.4x slower).  All segments of a plan share the phase pattern
+// (the plan checks it), so a bank row is wave-uniform: scalar operands of the FMAs.
+//   k_up: the one pass over the samples -- the K filter (two DF-II-T biquads) over
+//          the segment from rest: its end state is the zero-state end state the scan
+//          needs; the sample peaks (192 kHz, loudnorm's input_tp; d_out's own, the
+//          limiter's); and, per 100 ms hop piece, what the piece's energy needs once
+//          the exact start state s is known: the filter is linear, y_n = yz_n +
+//          C A^n s (yz = the response from rest computed here), so
+//            sum y^2 = sum yz^2 + 2 s . sum yz_n (C A^n)^T + s^T Q s,
+//          Q = sum (C A^n)^T (C A^n) a plan constant.  The pass over the samples is
+//          therefore not repeated after the scan:
+//   k_up_energy: per (segment, channel), the hop pieces' energies from s (after
+//          the scan, with the carry from the previous rank at N > 1).
 // M == 1 rates (48, 96, 32 kHz ...) take the unrolled path STATIC = L: every input
 // frame has outputs at phases 0 .. L-1 and phase 0 is the identity (the bank's
 // phase-0 row is a unit impulse: u = x exactly).
@@ -30,22 +39,20 @@
 
 namespace amx {
 
-typedef float f2 __attribute__((ext_vector_type(2)));
-
 #define UP_TAPS 32
 #define UP_C 15            // center tap
-// input frames per window block of the STATIC path: the window (TB + 31 frames) and the
-// block's samples (TB (L - 1)) live in registers
-#ifndef AMX_UP_TB4
-#define AMX_UP_TB4 4
+#ifndef AMX_UP_TB
+#define AMX_UP_TB 8        // input frames per window block (STATIC path)
 #endif
-template <int L> struct UpTB { static constexpr int v = L >= 4 ? AMX_UP_TB4 : 8; };
+#ifndef AMX_UP_SB
+#define AMX_UP_SB 6        // sched_barrier mask: VALU + SALU may cross, scalar loads may not
+#endif
 #ifndef AMX_UP_WAVES
-#define AMX_UP_WAVES 3     // waves per SIMD the register budget must allow
+#define AMX_UP_WAVES 4     // waves per SIMD the register budget must allow
 #endif
 
-__device__ __forceinline__ f2 up_frame(uint32_t w) {
-    return f2{(float)lo16(w) * (1.0f / 32768.0f), (float)hi16(w) * (1.0f / 32768.0f)};
+__device__ __forceinline__ float up_sample(uint32_t w, int ch) {
+    return (float)(ch ? hi16(w) : lo16(w)) * (1.0f / 32768.0f);
 }
 
 __device__ __forceinline__ int64_t up_reflect(int64_t k, int64_t n) {
@@ -68,246 +75,404 @@ __device__ __forceinline__ uint32_t up_word(const uint32_t *__restrict__ x,
     return n > 0 ? x[sp.out_off + up_reflect(g, n)] : 0u;
 }
 
-// the FMA3 kernel's order, both channels at once
-__device__ __forceinline__ f2 up_dot(const f2 *w, const float *__restrict__ h) {
-    f2 a[8];
+// the FMA3 kernel's order
+__device__ __forceinline__ float up_dot(const float *w, const float *__restrict__ h) {
+    float a[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        f2 acc = w[k] * h[k];
-        acc = __builtin_elementwise_fma(w[k + 8], f2{h[k + 8], h[k + 8]}, acc);
-        acc = __builtin_elementwise_fma(w[k + 16], f2{h[k + 16], h[k + 16]}, acc);
-        acc = __builtin_elementwise_fma(w[k + 24], f2{h[k + 24], h[k + 24]}, acc);
+        float acc = w[k] * h[k];
+        acc = fmaf(w[k + 8], h[k + 8], acc);
+        acc = fmaf(w[k + 16], h[k + 16], acc);
+        acc = fmaf(w[k + 24], h[k + 24], acc);
         a[k] = acc;
     }
-    const f2 b0 = a[0] + a[4], b1 = a[1] + a[5], b2 = a[2] + a[6], b3 = a[3] + a[7];
+    const float b0 = a[0] + a[4], b1 = a[1] + a[5], b2 = a[2] + a[6], b3 = a[3] + a[7];
     return (b0 + b2) + (b1 + b3);
 }
 
-// ------------------------------------------------------------ accumulators
-// Both passes run the K filter (two DF-II-T biquads per channel, the state order of
-// the scan's model [bq1 z0 z1, bq2 z0 z1]) over the segment's 192 kHz samples in
-// order: pass 1 from rest -- its end state IS the zero-state end state the scan
-// needs -- and pass 2 from the exact start state, summing y^2 per hop piece.
+// ------------------------------------------------------------ accumulator
 // FAST: every lane of the wave has a whole segment inside one hop and away from the
 // span ends -- no masks, no hop split, no edge reads (all but ~one wave per span).
-template <bool P1, bool FAST>
+template <bool FAST>
 struct UpAcc {
     double c1[5], c2[5];
-    double v0[4], v1[4];
-    double p00, p01, p10, p11;   // pass 2: y^2 per (piece, channel)
-    f2 pk, px;                   // pass 1: 192 kHz |u| max, d_out |x| max
+    double v[4];                 // K-filter state (the scan model's order)
+    double z0, z1;               // sum yz^2 per hop piece
+    double q0[4], q1[4];         // sum yz_n (C A^n)^T per hop piece
+    float pk, px;                // 192 kHz |u| max, d_out |x| max
     int split, len;
-    __device__ __forceinline__ void add(int n, f2 u, f2 xc) {
-        const double u0 = (double)u.x, u1 = (double)u.y;
-        if constexpr (P1 && !FAST) {
-            double w0[4], w1[4];
+    const double *wc;            // rows C A^n (plan table)
+    __device__ __forceinline__ void add(int n, float u, float xc) {
+        const double ud = (double)u;
+        const double *r = wc + (int64_t)n * AMX_KW_DIM;              // wave-uniform row
+        if constexpr (FAST) {
+            const double a = bq_step(c1, v[0], v[1], ud);
+            const double y = bq_step(c2, v[2], v[3], a);
+            z0 = fma(y, y, z0);
 #pragma unroll
-            for (int d = 0; d < 4; d++) { w0[d] = v0[d]; w1[d] = v1[d]; }
-            const double a0 = bq_step(c1, v0[0], v0[1], u0);
-            (void)bq_step(c2, v0[2], v0[3], a0);
-            const double a1 = bq_step(c1, v1[0], v1[1], u1);
-            (void)bq_step(c2, v1[2], v1[3], a1);
-            const bool in = n < len;              // past a partial segment's end: state held
-#pragma unroll
-            for (int d = 0; d < 4; d++) { v0[d] = in ? v0[d] : w0[d]; v1[d] = in ? v1[d] : w1[d]; }
-            pk = in ? f2{fmaxf(pk.x, fabsf(u.x)), fmaxf(pk.y, fabsf(u.y))} : pk;
-            px = in ? f2{fmaxf(px.x, fabsf(xc.x)), fmaxf(px.y, fabsf(xc.y))} : px;
-        } else if constexpr (P1) {
-            const double a0 = bq_step(c1, v0[0], v0[1], u0);
-            (void)bq_step(c2, v0[2], v0[3], a0);
-            const double a1 = bq_step(c1, v1[0], v1[1], u1);
-            (void)bq_step(c2, v1[2], v1[3], a1);
-            pk = f2{fmaxf(pk.x, fabsf(u.x)), fmaxf(pk.y, fabsf(u.y))};
-            px = f2{fmaxf(px.x, fabsf(xc.x)), fmaxf(px.y, fabsf(xc.y))};
+            for (int d = 0; d < 4; d++) q0[d] = fma(y, r[d], q0[d]);
+            pk = fmaxf(pk, fabsf(u));
+            px = fmaxf(px, fabsf(xc));
         } else {
-            const double a0 = bq_step(c1, v0[0], v0[1], u0);
-            double y0 = bq_step(c2, v0[2], v0[3], a0);
-            const double a1 = bq_step(c1, v1[0], v1[1], u1);
-            double y1 = bq_step(c2, v1[2], v1[3], a1);
-            if constexpr (FAST) {
-                p00 = fma(y0, y0, p00);
-                p01 = fma(y1, y1, p01);
+            const double w0 = v[0], w1 = v[1], w2 = v[2], w3 = v[3];
+            const double a = bq_step(c1, v[0], v[1], ud);
+            double y = bq_step(c2, v[2], v[3], a);
+            const bool in = n < len;              // past a partial segment's end: state held
+            v[0] = in ? v[0] : w0; v[1] = in ? v[1] : w1;
+            v[2] = in ? v[2] : w2; v[3] = in ? v[3] : w3;
+            y = in ? y : 0.0;
+            if (n < split) {
+                z0 = fma(y, y, z0);
+#pragma unroll
+                for (int d = 0; d < 4; d++) q0[d] = fma(y, r[d], q0[d]);
             } else {
-                const bool in = n < len;
-                y0 = in ? y0 : 0.0;
-                y1 = in ? y1 : 0.0;
-                if (n < split) { p00 = fma(y0, y0, p00); p01 = fma(y1, y1, p01); }
-                else { p10 = fma(y0, y0, p10); p11 = fma(y1, y1, p11); }
+                z1 = fma(y, y, z1);
+#pragma unroll
+                for (int d = 0; d < 4; d++) q1[d] = fma(y, r[d], q1[d]);
             }
+            pk = in ? fmaxf(pk, fabsf(u)) : pk;
+            px = in ? fmaxf(px, fabsf(xc)) : px;
         }
     }
 };
 
-// STATIC = L (M == 1): unrolled window blocks of UP_TB input frames, outputs at phases
-// 0 .. L-1 of every frame; 0: general phase pattern from the tables.
-// sb: the bank in LDS (STATIC); zp: an LDS word holding 0, read every block so the
-// compiler cannot hoist the bank rows out of the block loop (all rows live at once
-// would not fit the registers)
-template <int STATIC, bool FAST, class Acc>
-__device__ __forceinline__ void up_run(const UpArgs &a, const SpanDev &sp, int t, int64_t g0,
-                                       bool vec, const float *sb, const int *zp, Acc &acc) {
-    const uint32_t *__restrict__ x = a.x;
-    if constexpr (STATIC > 0) {
-        constexpr int UP_TB = UpTB<STATIC>::v;
-        constexpr int W = UP_TB + UP_TAPS - 1;                 // inputs [k0 - 15, k0 + TB + 16)
-        f2 w[W];
-        const uint32_t *xp = x + sp.out_off + g0 - UP_C;       // frame g0 - 15
+// The fast kernel: STATIC = L (M == 1), a segment that is whole, inside one hop and
+// away from the span ends (the plan lists the others for k_up_slow): unrolled window
+// blocks of TB input frames, outputs at phases 0 .. L-1 of every frame, phase 0 the
+// frame itself.  zp: an LDS word holding 0, read every block so LLVM cannot hoist the
+// bank rows out of the block loop (all rows at once would not fit the SGPRs).
+template <int STATIC>
+__device__ __forceinline__ void up_run_fast(const UpArgs &a, const SpanDev &sp, int ch, int64_t g0,
+                                            bool vec, const int *zp, UpAcc<true> &acc) {
+    constexpr int TB = AMX_UP_TB;
+    constexpr int W = TB + UP_TAPS - 1;                        // inputs [k0 - 15, k0 + TB + 16)
+    float w[W];
+    const uint32_t *xp = a.x + sp.out_off + g0 - UP_C;         // frame g0 - 15
 #pragma unroll
-        for (int i = 0; i < W; i++)
-            w[i] = up_frame(FAST ? xp[i] : up_word(x, a.edge, sp, t, g0 - UP_C + i));
-        const int nblk = a.Lin / UP_TB;
-        for (int b = 0; b < nblk; b++) {
-            // next block's new frames in flight while this block computes (past the
-            // last block: frames of this one again, in range, unused)
-            uint32_t nx[UP_TB];
-            const int o0 = (b + 1 < nblk ? (b + 1) * UP_TB : b * UP_TB) + (W - UP_TB);
-            if (FAST && vec) {                                  // 16-B aligned rows
+    for (int i = 0; i < W; i++) w[i] = up_sample(xp[i], ch);
+    const int nblk = a.Lin / TB;
+    for (int b = 0; b < nblk; b++) {
+        // next block's new frames in flight while this block computes (past the last
+        // block: frames of this one again, in range, unused)
+        uint32_t nx[TB];
+        const int o0 = (b + 1 < nblk ? (b + 1) * TB : b * TB) + (W - TB);
+        if (vec) {                                              // 16-B aligned rows
 #pragma unroll
-                for (int i = 0; i < UP_TB; i += 4) {
-                    const uint4 q = *reinterpret_cast<const uint4 *>(xp + o0 + i);
-                    nx[i] = q.x; nx[i + 1] = q.y; nx[i + 2] = q.z; nx[i + 3] = q.w;
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < UP_TB; i++)
-                    nx[i] = FAST ? xp[o0 + i] : up_word(x, a.edge, sp, t, g0 - UP_C + o0 + i);
+            for (int i = 0; i < TB; i += 4) {
+                const uint4 q = *reinterpret_cast<const uint4 *>(xp + o0 + i);
+                nx[i] = q.x; nx[i + 1] = q.y; nx[i + 2] = q.z; nx[i + 3] = q.w;
             }
-            const int nb0 = b * UP_TB * STATIC;
-            // the bank row through scalar loads (SGPR operands of the FMAs); the
-            // offset read from LDS (always 0) keeps the compiler from hoisting every
-            // row out of the loop at once
-            const float *bk = a.bank + __builtin_amdgcn_readfirstlane(zp[b & 1]);
-            f2 u[UP_TB][STATIC > 1 ? STATIC - 1 : 1];
+        } else {
+#pragma unroll
+            for (int i = 0; i < TB; i++) nx[i] = xp[o0 + i];
+        }
+        const int nb0 = b * TB * STATIC;
+        const float *bk = a.bank + __builtin_amdgcn_readfirstlane(zp[b & 1]);
+#pragma unroll
+        for (int kb = 0; kb < TB; kb++) {
+            // outputs of frame kb in order; the scheduling barriers keep one output's
+            // scalar rows (bank row, C A^n row) in its own region: pulled ahead, the
+            // block's rows would not fit the SGPRs
+            __builtin_amdgcn_sched_barrier(AMX_UP_SB);
+            const int n0 = nb0 + kb * STATIC;
+            acc.add(n0, w[kb + UP_C], w[kb + UP_C]);
 #pragma unroll
             for (int ph = 1; ph < STATIC; ph++) {
-                const float *h = bk + ph * UP_TAPS;
-#pragma unroll
-                for (int kb = 0; kb < UP_TB; kb++) u[kb][ph - 1] = up_dot(w + kb, h);
+                __builtin_amdgcn_sched_barrier(AMX_UP_SB);
+                acc.add(n0 + ph, up_dot(w + kb, bk + ph * UP_TAPS), w[kb + UP_C]);
             }
-#pragma unroll
-            for (int kb = 0; kb < UP_TB; kb++)
-#pragma unroll
-                for (int ph = 0; ph < STATIC; ph++)
-                    acc.add(nb0 + kb * STATIC + ph, ph == 0 ? w[kb + UP_C] : u[kb][ph - 1], w[kb + UP_C]);
-#pragma unroll
-            for (int i = 0; i < W - UP_TB; i++) w[i] = w[i + UP_TB];
-#pragma unroll
-            for (int i = 0; i < UP_TB; i++) w[W - UP_TB + i] = up_frame(nx[i]);
         }
-    } else {
-        f2 w[UP_TAPS];
+        __builtin_amdgcn_sched_barrier(AMX_UP_SB);
 #pragma unroll
-        for (int i = 0; i < UP_TAPS; i++) w[i] = up_frame(up_word(x, a.edge, sp, t, g0 - UP_C + i));
-        int cur = 0;
-        for (int n = 0; n < a.Lout; n++) {
-            const int kb = a.obase[n];
-            if (kb > cur) {                                    // wave-uniform: one frame on
+        for (int i = 0; i < W - TB; i++) w[i] = w[i + TB];
 #pragma unroll
-                for (int i = 0; i < UP_TAPS - 1; i++) w[i] = w[i + 1];
-                w[UP_TAPS - 1] = up_frame(up_word(x, a.edge, sp, t, g0 + cur + UP_TAPS - UP_C));
-                cur++;
-            }
-            acc.add(n, up_dot(w, a.bank + a.oph[n] * UP_TAPS), w[UP_C]);
-        }
+        for (int i = 0; i < TB; i++) w[W - TB + i] = up_sample(nx[i], ch);
     }
 }
 
-// both passes: P1 = pass 1 (from rest: end state + peaks), else pass 2 (hop pieces)
-template <int STATIC, bool P1>
+template <class Acc>
+__device__ __forceinline__ void acc_init(const UpArgs &a, Acc &acc, int split, int len) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) { acc.c1[i] = a.cd->kw1[i]; acc.c2[i] = a.cd->kw2[i]; }
+    acc.c1[3] = a.cd->kw1[4]; acc.c1[4] = a.cd->kw1[5];
+    acc.c2[3] = a.cd->kw2[4]; acc.c2[4] = a.cd->kw2[5];
+#pragma unroll
+    for (int d = 0; d < 4; d++) { acc.v[d] = 0.0; acc.q0[d] = 0.0; acc.q1[d] = 0.0; }
+    acc.z0 = acc.z1 = 0.0;
+    acc.pk = acc.px = 0.0f;
+    acc.split = split;
+    acc.len = len;
+    acc.wc = a.G;
+}
+
+template <class Acc>
+__device__ __forceinline__ void acc_store(const UpArgs &a, const Acc &acc, int64_t j, int ch) {
+    double *o = a.e + (j * 2 + ch) * AMX_KW_DIM;
+#pragma unroll
+    for (int d = 0; d < AMX_KW_DIM; d++) o[d] = acc.v[d];
+    uint32_t *q = a.pk + j * 4;
+    q[ch] = __float_as_uint(acc.pk);
+    q[2 + ch] = (uint32_t)(acc.px * 32768.0f);      // |s16| / 32768: exact
+    // energy terms: [piece][sum yz^2, sum yz (C A^n)^T (4)]
+    double *t = a.eterms + (j * 2 + ch) * 10;
+    t[0] = acc.z0;
+    t[5] = acc.z1;
+#pragma unroll
+    for (int d = 0; d < 4; d++) { t[1 + d] = acc.q0[d]; t[6 + d] = acc.q1[d]; }
+}
+
+__device__ __forceinline__ bool up_fast_seg(const UpArgs &a, const KwSegDev &sg, const SpanDev &sp) {
+    const int64_t g0 = sg.out_pos - sp.out_off;
+    const int64_t h0 = sg.tframe / a.hop;
+    const int64_t split = (h0 + 1) * a.hop - sg.tframe;
+    return g0 - UP_C >= 0 && g0 + a.Lin + UP_TAPS - UP_C <= sp.out_n && sg.len == a.Lout &&
+           split >= a.Lout;
+}
+
+// one lane per (segment, channel); lanes of segments k_up_slow owns return at once
+template <int STATIC>
 __global__ void __launch_bounds__(AMX_UP_BLOCK) __attribute__((amdgpu_waves_per_eu(AMX_UP_WAVES)))
 k_up(UpArgs a) {
-    __shared__ __attribute__((aligned(16))) float sb[STATIC > 0 ? STATIC * UP_TAPS : 4];
     __shared__ int zp[2];
     const int lane = threadIdx.x;
-    if constexpr (STATIC > 0) {
-        for (int i = lane; i < STATIC * UP_TAPS; i += AMX_UP_BLOCK) sb[i] = a.bank[i];
-    }
     if (lane < 2) zp[lane] = 0;
     __syncthreads();
-    const int j = blockIdx.x * AMX_UP_BLOCK + lane;
-    const bool valid = j < a.n_kseg;
-    const KwSegDev sg = a.ks[valid ? j : a.n_kseg - 1];
+    const int ch = lane & 1;
+    const int64_t j = (int64_t)blockIdx.x * (AMX_UP_BLOCK / 2) + (lane >> 1);
+    if (j >= a.n_kseg) return;
+    const KwSegDev sg = a.ks[j];
     const SpanDev sp = a.spans[sg.track];
+    if (!up_fast_seg(a, sg, sp)) return;
     const int64_t g0 = sg.out_pos - sp.out_off;
-    const bool edge = g0 - UP_C < 0 || g0 + a.Lin + UP_TAPS - UP_C > sp.out_n;
-    const int64_t h0 = sg.tframe / a.hop;
-    const int split = (int)((h0 + 1) * a.hop - sg.tframe);
-    const int len = valid ? sg.len : 0;
-    const bool fast = valid && !edge && len == a.Lout && (P1 || split >= a.Lout);
     // 16-B loads when every lane's window rows are 16-B aligned
     const bool vec = __ballot(((sp.out_off + g0 - UP_C + (UP_TAPS - 1)) & 3) != 0) == 0;
-    UpAcc<P1, true> af;
-    UpAcc<P1, false> ag;
-    auto setup = [&](auto &acc) {
+    UpAcc<true> acc;
+    acc_init(a, acc, a.Lout, a.Lout);
+    up_run_fast<STATIC>(a, sp, ch, g0, vec, zp, acc);
+    acc_store(a, acc, j, ch);
+}
+
+// The general kernel, over the plan's list of the segments k_up does not take (span
+// ends, partial segments, hop splits) -- or over every segment when the rate has no
+// unrolled form (M > 1, e.g. 44.1 kHz: phase pattern from the tables, the window
+// moves one frame at a time): neighbour / mirrored frames, masks, two hop pieces.
+__global__ void __launch_bounds__(AMX_UP_BLOCK) k_up_slow(UpArgs a) {
+    const int lane = threadIdx.x;
+    const int ch = lane & 1;
+    const int64_t q = (int64_t)blockIdx.x * (AMX_UP_BLOCK / 2) + (lane >> 1);
+    if (q >= a.n_slow) return;
+    const int64_t j = a.slow ? a.slow[q] : q;
+    const KwSegDev sg = a.ks[j];
+    const SpanDev sp = a.spans[sg.track];
+    const int t = sg.track;
+    const int64_t g0 = sg.out_pos - sp.out_off;
+    const int64_t h0 = sg.tframe / a.hop;
+    UpAcc<false> acc;
+    acc_init(a, acc, (int)((h0 + 1) * a.hop - sg.tframe), sg.len);
+    float w[UP_TAPS];
+    for (int i = 0; i < UP_TAPS; i++) {
+        const float v = up_sample(up_word(a.x, a.edge, sp, t, g0 - UP_C + i), ch);
 #pragma unroll
-        for (int i = 0; i < 3; i++) { acc.c1[i] = a.cd->kw1[i]; acc.c2[i] = a.cd->kw2[i]; }
-        acc.c1[3] = a.cd->kw1[4]; acc.c1[4] = a.cd->kw1[5];
-        acc.c2[3] = a.cd->kw2[4]; acc.c2[4] = a.cd->kw2[5];
-        const double *s0 = a.s + (int64_t)(valid ? j : 0) * 2 * AMX_KW_DIM;
-#pragma unroll
-        for (int d = 0; d < 4; d++) {
-            acc.v0[d] = (!P1 && valid) ? s0[d] : 0.0;
-            acc.v1[d] = (!P1 && valid) ? s0[AMX_KW_DIM + d] : 0.0;
-        }
-        acc.p00 = acc.p01 = acc.p10 = acc.p11 = 0.0;
-        acc.pk = f2{0.0f, 0.0f};
-        acc.px = f2{0.0f, 0.0f};
-        acc.split = split;
-        acc.len = len;
-    };
-    double v0[4], v1[4], p[4];
-    f2 pk, px;
-    auto take = [&](auto &acc) {
-#pragma unroll
-        for (int d = 0; d < 4; d++) { v0[d] = acc.v0[d]; v1[d] = acc.v1[d]; }
-        p[0] = acc.p00; p[1] = acc.p01; p[2] = acc.p10; p[3] = acc.p11;
-        pk = acc.pk;
-        px = acc.px;
-    };
-    if (__ballot(!fast) == 0) {
-        setup(af);
-        up_run<STATIC, true>(a, sp, sg.track, g0, vec, sb, zp, af);
-        take(af);
-    } else {
-        setup(ag);
-        up_run<STATIC, false>(a, sp, sg.track, g0, vec, sb, zp, ag);
-        take(ag);
+        for (int k = 0; k < UP_TAPS; k++) w[k] = k == i ? v : w[k];
     }
-    if (!valid) return;
-    if constexpr (P1) {
-        double *o = a.e + (int64_t)j * 2 * AMX_KW_DIM;
+    int cur = 0;
+    for (int n = 0; n < a.Lout; n++) {
+        const int kb = a.obase[n];
+        if (kb > cur) {                                         // one frame on
 #pragma unroll
-        for (int d = 0; d < AMX_KW_DIM; d++) { o[d] = v0[d]; o[AMX_KW_DIM + d] = v1[d]; }
-        uint32_t *q = a.pk + (int64_t)j * 4;
-        q[0] = __float_as_uint(pk.x);
-        q[1] = __float_as_uint(pk.y);
-        q[2] = (uint32_t)(px.x * 32768.0f);      // |s16| / 32768: exact
-        q[3] = (uint32_t)(px.y * 32768.0f);
-    } else {
-        double *o = a.parts + (int64_t)j * 4;
-        o[0] = p[0]; o[1] = p[1]; o[2] = p[2]; o[3] = p[3];
-        a.part_hop[j] = h0;
+            for (int i = 0; i < UP_TAPS - 1; i++) w[i] = w[i + 1];
+            w[UP_TAPS - 1] = up_sample(up_word(a.x, a.edge, sp, t, g0 + cur + UP_TAPS - UP_C), ch);
+            cur++;
+        }
+        const int ph = a.oph[n];
+        const float u = (a.static_l > 0 && ph == 0) ? w[UP_C] : up_dot(w, a.bank + ph * UP_TAPS);
+        acc.add(n, u, w[UP_C]);
+    }
+    acc_store(a, acc, j, ch);
+}
+
+// The static path's left-over segments (span ends, partial segments, hop splits: a
+// few per span), one wave per segment: the lane-per-segment form above would run each
+// of them as one serial lane over Lout outputs, all taps and edge tests included --
+// longer than the whole fast kernel.  Here the wave stages the segment's frames in LDS,
+// computes the 2 x Lout resampled samples and the peaks in parallel, and only the K
+// filter recursion (one lane per channel) stays serial.
+__global__ void __launch_bounds__(64) k_up_edge(UpArgs a) {
+    extern __shared__ uint32_t sh[];
+    const int lane = threadIdx.x;
+    const int64_t j = a.slow[blockIdx.x];
+    const KwSegDev sg = a.ks[j];
+    const SpanDev sp = a.spans[sg.track];
+    const int t = sg.track;
+    const int64_t g0 = sg.out_pos - sp.out_off;
+    const int nf = a.Lin + UP_TAPS;                               // frames g0 - 15 + [0, nf)
+    uint32_t *fr = sh;
+    float *us = reinterpret_cast<float *>(sh + nf);               // [n][ch]
+    for (int i = lane; i < nf; i += 64) fr[i] = up_word(a.x, a.edge, sp, t, g0 - UP_C + i);
+    __syncthreads();
+    const int len = sg.len;
+    const int ch = lane & 1;
+    float pk = 0.0f, px = 0.0f;
+    for (int i = lane; i < 2 * a.Lout; i += 64) {                 // i & 1 == ch
+        const int n = i >> 1;
+        const int kb = a.obase[n], ph = a.oph[n];
+        float w[UP_TAPS];
+#pragma unroll
+        for (int k = 0; k < UP_TAPS; k++) w[k] = up_sample(fr[kb + k], ch);
+        const float u = (a.static_l > 0 && ph == 0) ? w[UP_C] : up_dot(w, a.bank + ph * UP_TAPS);
+        us[i] = u;
+        if (n < len) {
+            pk = fmaxf(pk, fabsf(u));
+            px = fmaxf(px, fabsf(w[UP_C]));
+        }
+    }
+#pragma unroll
+    for (int o = 2; o < 64; o <<= 1) {                            // max over the channel's lanes
+        pk = fmaxf(pk, __shfl_xor(pk, o));
+        px = fmaxf(px, __shfl_xor(px, o));
+    }
+    __syncthreads();
+    // the K filter recursion, one lane per channel: y_n into LDS (0 past len)
+    double *ys = reinterpret_cast<double *>(sh + ((nf + 2 * a.Lout + 1) & ~1));   // [n][ch]
+    if (lane < 2) {
+        double c1[5], c2[5];
+#pragma unroll
+        for (int k = 0; k < 3; k++) { c1[k] = a.cd->kw1[k]; c2[k] = a.cd->kw2[k]; }
+        c1[3] = a.cd->kw1[4]; c1[4] = a.cd->kw1[5];
+        c2[3] = a.cd->kw2[4]; c2[4] = a.cd->kw2[5];
+        double v[4] = {0.0, 0.0, 0.0, 0.0};
+        int n = 0;
+        for (; n + 8 <= len; n += 8) {
+            float ub[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) ub[k] = us[2 * (n + k) + ch];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                ys[2 * (n + k) + ch] = bq_step(c2, v[2], v[3], bq_step(c1, v[0], v[1], (double)ub[k]));
+        }
+        for (; n < len; n++)
+            ys[2 * n + ch] = bq_step(c2, v[2], v[3], bq_step(c1, v[0], v[1], (double)us[2 * n + ch]));
+        for (; n < a.Lout; n++) ys[2 * n + ch] = 0.0;
+        double *o = a.e + (j * 2 + ch) * AMX_KW_DIM;
+#pragma unroll
+        for (int d = 0; d < AMX_KW_DIM; d++) o[d] = v[d];
+        uint32_t *pq = a.pk + j * 4;
+        pq[ch] = __float_as_uint(pk);
+        pq[2 + ch] = (uint32_t)(px * 32768.0f);
+    }
+    __syncthreads();
+    // energy terms per hop piece, all lanes: sum y^2, sum y (C A^n)^T
+    const int64_t h0 = sg.tframe / a.hop;
+    const int split = (int)((h0 + 1) * a.hop - sg.tframe);
+    double acc[2][2][5] = {};                                     // [ch][piece][term]
+    for (int n = lane; n < len; n += 64) {
+        const double *r = a.G + (int64_t)n * AMX_KW_DIM;
+        const int pc = n < split ? 0 : 1;
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const double y = ys[2 * n + c];
+#pragma unroll
+            for (int p = 0; p < 2; p++) {
+                const double yy = p == pc ? y : 0.0;
+                acc[c][p][0] = fma(yy, yy, acc[c][p][0]);
+#pragma unroll
+                for (int d = 0; d < 4; d++) acc[c][p][1 + d] = fma(yy, r[d], acc[c][p][1 + d]);
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; c++)
+#pragma unroll
+        for (int p = 0; p < 2; p++)
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                double x = acc[c][p][k];
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) x += __shfl_xor(x, o);
+                acc[c][p][k] = x;
+            }
+    if (lane < 2) {
+        double *te = a.eterms + (j * 2 + ch) * 10;
+#pragma unroll
+        for (int p = 0; p < 2; p++)
+#pragma unroll
+            for (int k = 0; k < 5; k++) te[p * 5 + k] = ch ? acc[1][p][k] : acc[0][p][k];
     }
 }
 
-template <bool P1>
-static hipError_t up_launch(const UpArgs &a, hipStream_t st) {
-    if (a.n_kseg <= 0) return hipSuccess;
-    const dim3 g((unsigned)((a.n_kseg + AMX_UP_BLOCK - 1) / AMX_UP_BLOCK));
-    switch (a.static_l) {
-    case 0: hipLaunchKernelGGL((k_up<0, P1>), g, dim3(AMX_UP_BLOCK), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((k_up<2, P1>), g, dim3(AMX_UP_BLOCK), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((k_up<4, P1>), g, dim3(AMX_UP_BLOCK), 0, st, a); break;
-    default: return hipErrorInvalidValue;
+// hop pieces' energies from the exact start states: E = sum yz^2 + 2 s.q + s^T Q s,
+// Q the piece's Gram matrix of the rows C A^n (plan tables: head Qh[k] = sum_{n<k},
+// tail Qt[k] = sum_{k<=n<Lout}); one thread per (segment, channel)
+__global__ void __launch_bounds__(AMX_BLOCK) k_up_energy(UpArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x;
+    if (i >= 2 * (int64_t)a.n_kseg) return;
+    const int64_t j = i >> 1;
+    const int ch = (int)(i & 1);
+    const KwSegDev sg = a.ks[j];
+    const int64_t h0 = sg.tframe / a.hop;
+    const int split = (int)((h0 + 1) * a.hop - sg.tframe);
+    const int len = sg.len;
+    const double *s = a.s + (j * 2 + ch) * AMX_KW_DIM;
+    const double *t = a.eterms + (j * 2 + ch) * 10;
+    double sv[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++) sv[d] = s[d];
+    auto quad = [&](const double *Q) {           // s^T Q s
+        double r = 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            double row = 0.0;
+#pragma unroll
+            for (int w = 0; w < 4; w++) row = fma(Q[u * 4 + w], sv[w], row);
+            r = fma(sv[u], row, r);
+        }
+        return r;
+    };
+    const int e0 = split < len ? split : len;    // piece 0 = outputs [0, e0)
+    const double *Qh = a.qh + (int64_t)e0 * 16;
+    double E0 = t[0], E1 = 0.0;
+    double c0 = 0.0, c1 = 0.0;
+#pragma unroll
+    for (int d = 0; d < 4; d++) { c0 = fma(sv[d], t[1 + d], c0); c1 = fma(sv[d], t[6 + d], c1); }
+    E0 = E0 + 2.0 * c0 + quad(Qh);
+    if (split < len) {                           // piece 1 = outputs [split, len)
+        double Q[16];
+        const double *Qa = a.qt + (int64_t)split * 16, *Qb = a.qt + (int64_t)len * 16;
+#pragma unroll
+        for (int k = 0; k < 16; k++) Q[k] = Qa[k] - Qb[k];
+        E1 = t[5] + 2.0 * c1 + quad(Q);
     }
-    return hipGetLastError();
+    double *o = a.parts + j * 4;
+    o[ch] = E0;
+    o[2 + ch] = E1;
+    if (ch == 0) a.part_hop[j] = h0;
 }
 
 hipError_t launch_up1(const UpArgs &a, int n_spans, hipStream_t st) {
     (void)n_spans;
-    return up_launch<true>(a, st);
+    if (a.n_kseg <= 0) return hipSuccess;
+    if (a.static_l > 0) {
+        const dim3 g((unsigned)((a.n_kseg + AMX_UP_BLOCK / 2 - 1) / (AMX_UP_BLOCK / 2)));
+        switch (a.static_l) {
+        case 2: hipLaunchKernelGGL(k_up<2>, g, dim3(AMX_UP_BLOCK), 0, st, a); break;
+        case 4: hipLaunchKernelGGL(k_up<4>, g, dim3(AMX_UP_BLOCK), 0, st, a); break;
+        default: return hipErrorInvalidValue;
+        }
+    }
+    if (a.n_slow > 0 && a.slow)
+        hipLaunchKernelGGL(k_up_edge, dim3((unsigned)a.n_slow), dim3(64),
+                           (size_t)((a.Lin + UP_TAPS + 2 * a.Lout + 1) & ~1) * 4 + (size_t)a.Lout * 16, st, a);
+    else if (a.n_slow > 0)
+        hipLaunchKernelGGL(k_up_slow, dim3((unsigned)((a.n_slow + AMX_UP_BLOCK / 2 - 1) / (AMX_UP_BLOCK / 2))),
+                           dim3(AMX_UP_BLOCK), 0, st, a);
+    return hipGetLastError();
 }
 
-hipError_t launch_up2(const UpArgs &a, hipStream_t st) { return up_launch<false>(a, st); }
+hipError_t launch_up2(const UpArgs &a, hipStream_t st) {
+    if (a.n_kseg <= 0) return hipSuccess;
+    const int64_t n = 2 * (int64_t)a.n_kseg;
+    hipLaunchKernelGGL(k_up_energy, dim3((unsigned)((n + AMX_BLOCK - 1) / AMX_BLOCK)), dim3(AMX_BLOCK), 0, st, a);
+    return hipGetLastError();
+}
 
 }  // namespace amx

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -230,6 +231,9 @@ struct amx_plan {
     // the track already is at 192 kHz (the measurement runs on d_out itself)
     int resamp = 0, upL = 1, upM = 1, upLin = 0, upLout = 0, up_static = 0, up_ok = 1;
     int32_t *d_obase = nullptr, *d_oph = nullptr;
+    int32_t *d_slow = nullptr;   // K segments k_up_slow takes (static path); n_slow of them
+    int64_t n_slow = 0;
+    double *d_qh = nullptr, *d_qt = nullptr;
     float *d_bank = nullptr;
     int mask = 0, D = 0;
     int lev_eq = 0, lev_x = 0, lev_kw = 0;
@@ -281,7 +285,7 @@ struct amx_plan {
     size_t ws_bytes = 0;
     size_t o_a16, o_e, o_s, o_p16, o_ex, o_sx, o_bands, o_r, o_m, o_gain, o_esv, o_ee0, o_eflags, o_eact,
         o_eprev;
-    size_t o_ekw, o_skw, o_parts, o_phop;
+    size_t o_ekw, o_skw, o_parts, o_phop, o_eterms = 0;
     size_t o_eb, o_ebx, o_ebk, o_pk, o_dup = 0;
     amx::ScanPlan scan_eq() const { return {D, n_blk, lev_eq, d_blks, d_M, d_Mp}; }
     amx::ScanPlan scan_xo() const { return {AMX_XO_DIM, mb ? n_blk : 0, lev_x, d_blks, d_Mx, d_Mpx}; }
@@ -364,7 +368,9 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             // ~384 192 kHz outputs per K segment, a divisor of the 100 ms hop (19200)
             // where one exists, so a segment lies inside one hop (no hop split)
             const int hop192 = (kfs + 5) / 10;
-            int kk = std::max(1, (384 + p->upL / 2) / p->upL);
+            int target = 480;                 // (AMX_UP_LOUT overrides, for measurements)
+            if (const char *ev = std::getenv("AMX_UP_LOUT")) target = std::max(16, std::atoi(ev));
+            int kk = std::max(1, (target + p->upL / 2) / p->upL);
             for (int d = 0; d <= kk; d++) {
                 if (kk - d >= 1 && hop192 % (p->upL * (kk - d)) == 0 && (p->upM * (kk - d)) % 8 == 0) { kk -= d; break; }
                 if (hop192 % (p->upL * (kk + d)) == 0 && (p->upM * (kk + d)) % 8 == 0) { kk += d; break; }
@@ -687,6 +693,26 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         if (p->up_static && pattern != 0) p->up_static = 0;
     }
     p->n_kseg = (int)p->ksegs.size();
+    // the segments the unrolled 192 kHz kernel leaves to the general one: windows that
+    // reach past the span's frames, partial segments, segments holding a hop boundary
+    // (the same test as up_fast_seg in amx_loud192.hip)
+    std::vector<int32_t> slow;
+    if (p->resamp && p->up_ok) {
+        if (p->up_static) {
+            for (int32_t j = 0; j < p->n_kseg; j++) {
+                const KwSegDev &sg = p->ksegs[j];
+                const SpanDev &sp = p->spans[sg.track];
+                const int64_t g0 = sg.out_pos - sp.out_off;
+                const int64_t split = (sg.tframe / p->hop + 1) * p->hop - sg.tframe;
+                const bool fast = g0 - 15 >= 0 && g0 + p->upLin + 17 <= sp.out_n &&
+                                  sg.len == p->upLout && split >= p->upLout;
+                if (!fast) slow.push_back(j);
+            }
+            p->n_slow = (int64_t)slow.size();
+        } else {
+            p->n_slow = p->n_kseg;       // every segment, d_slow NULL
+        }
+    }
     // hop splits on 16-frame tile boundaries (k_kw2 picks the hop piece per tile)
     p->kw_aligned = (!p->resamp && p->hop % AMX_TF_FRAMES == 0 && p->Lkw % AMX_TF_FRAMES == 0) ? 1 : 0;
     for (int t = 0; t < n_tracks; t++)
@@ -704,7 +730,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
 
     // ------------------------------------------------------- LTI models
     const double tol = 1e-22;
-    std::vector<double> G, M, Mp, Gx, Mx, Mpx, Gkw, Mkw, Mpkw;
+    std::vector<double> G, M, Mp, Gx, Mx, Mpx, Gkw, Mkw, Mpkw, qh, qt;
     if (D > 0) {
         Lti eq;
         eq.derive(D, [&](double *z, double x) {
@@ -753,7 +779,42 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             sos_step_h(cd.kw2, z + 2, y);
         });
         const int Lseg = p->resamp ? std::max(1, p->upLout) : p->Lkw;
-        Gkw = kw.gemv_table(Lseg);
+        if (p->resamp) {
+            // the measurement kernels keep no GEMV table: their pass over the samples
+            // runs the filter from rest and needs the free-response rows C A^n and
+            // their Gram sums (amx_loud192.hip k_up / k_up_energy)
+            double Cr[AMX_KW_DIM];
+            for (int k = 0; k < AMX_KW_DIM; k++) {
+                double z[AMX_KW_DIM] = {0.0, 0.0, 0.0, 0.0};
+                z[k] = 1.0;
+                const double y1 = sos_step_h(cd.kw1, z, 0.0);
+                Cr[k] = sos_step_h(cd.kw2, z + 2, y1);
+            }
+            Gkw.assign((size_t)Lseg * AMX_KW_DIM, 0.0);
+            qh.assign((size_t)(Lseg + 1) * 16, 0.0);
+            qt.assign((size_t)(Lseg + 1) * 16, 0.0);
+            std::vector<double> r(Cr, Cr + AMX_KW_DIM), t(AMX_KW_DIM);
+            for (int n = 0; n < Lseg; n++) {
+                for (int d = 0; d < AMX_KW_DIM; d++) Gkw[(size_t)n * AMX_KW_DIM + d] = r[d];
+                for (int u = 0; u < 4; u++)
+                    for (int w = 0; w < 4; w++)
+                        qh[(size_t)(n + 1) * 16 + u * 4 + w] = qh[(size_t)n * 16 + u * 4 + w] + r[u] * r[w];
+                for (int d = 0; d < AMX_KW_DIM; d++) {     // r <- r A
+                    double acc = 0.0;
+                    for (int k = 0; k < AMX_KW_DIM; k++) acc += r[k] * kw.A[(size_t)k * AMX_KW_DIM + d];
+                    t[d] = acc;
+                }
+                r = t;
+            }
+            for (int n = Lseg - 1; n >= 0; n--) {
+                const double *g = &Gkw[(size_t)n * AMX_KW_DIM];
+                for (int u = 0; u < 4; u++)
+                    for (int w = 0; w < 4; w++)
+                        qt[(size_t)n * 16 + u * 4 + w] = qt[(size_t)(n + 1) * 16 + u * 4 + w] + g[u] * g[w];
+            }
+        } else {
+            Gkw = kw.gemv_table(Lseg);
+        }
         Mkw = matpow(kw.A, Lseg, AMX_KW_DIM);
         p->lev_kw = kw.window_powers((int64_t)Lseg * AMX_SCAN_S, tol, 16, Mpkw);
         if (p->lev_kw < 0) {
@@ -807,7 +868,10 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     UP(p->d_energies, energies, 1000);
     UP(p->d_tailpow, p->tail_pow.data(), p->tail_pow.size());
     UP(p->d_obase, obase.data(), obase.size());
+    UP(p->d_qh, qh.data(), qh.size());
+    UP(p->d_qt, qt.data(), qt.size());
     UP(p->d_oph, oph.data(), oph.size());
+    if (!slow.empty()) UP(p->d_slow, slow.data(), slow.size());
     UP(p->d_bank, bank.data(), bank.size());
     {
         std::vector<unsigned int> zero((size_t)(p->n_tracks > 0 ? p->n_tracks : 1), 0u);
@@ -853,6 +917,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     p->o_pk = (size_t)align_up(off, nk * 4 * 4);
     p->o_skw = (size_t)align_up(off, nk * 2 * AMX_KW_DIM * 8);
     p->o_parts = (size_t)align_up(off, nk * 4 * 8);
+    if (p->resamp) p->o_eterms = (size_t)align_up(off, nk * 2 * 10 * 8);
     p->o_phop = (size_t)align_up(off, nk * 8);
     p->ws_bytes = (off + 255) & ~(size_t)255;
     *out = p;
@@ -866,7 +931,8 @@ void amx_plan_free(amx_plan *p) {
                     p->d_Mx,  p->d_Mpx,    p->d_Gkw,  p->d_Mkw,   p->d_Mpkw,   p->d_tabs,
                     p->d_bounds, p->d_tailpow, p->d_lut, p->d_energies, p->d_carryP,
                     p->d_esegs, p->d_eseg0, p->d_neseg, p->d_pcnt, p->d_ppart,
-                    p->lim.seg_state, p->lim.cnt, p->d_obase, p->d_oph, p->d_bank};
+                    p->lim.seg_state, p->lim.cnt, p->d_obase, p->d_oph, p->d_bank,
+                    p->d_qh, p->d_qt, p->d_slow};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     delete p;
@@ -1000,10 +1066,15 @@ amx::UpArgs up_args(const amx_plan *p, const int16_t *d_out, const int16_t *d_ed
     a.hop = p->hop;
     a.obase = p->d_obase;
     a.oph = p->d_oph;
+    a.slow = p->d_slow;
+    a.n_slow = p->n_slow;
     a.bank = p->d_bank;
     a.x = reinterpret_cast<const uint32_t *>(d_out);
     a.edge = reinterpret_cast<const uint32_t *>(d_edge);
     a.G = p->d_Gkw;
+    a.qh = p->d_qh;
+    a.qt = p->d_qt;
+    a.eterms = wsp<double>(d_ws, p->o_eterms);
     a.e = wsp<double>(d_ws, p->o_ekw);
     a.s = wsp<double>(d_ws, p->o_skw);
     a.parts = wsp<double>(d_ws, p->o_parts);
