@@ -201,7 +201,7 @@ struct UpArgs {
     int64_t *part_hop;
     uint32_t *pk;                 // [seg][4]: 192 kHz |u| max L, R (float bits), native |x| L, R
 };
-hipError_t launch_up1(const UpArgs &a, int n_spans, hipStream_t st);
+hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent_t fork, hipEvent_t join);
 int swr_geometry(int in_rate, int out_rate, int *L, int *M);   // host (amx_plan.cpp)
 int swr_bank(int in_rate, int out_rate, float *bank);
 hipError_t launch_up2(const UpArgs &a, hipStream_t st);

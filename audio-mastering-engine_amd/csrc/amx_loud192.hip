@@ -448,23 +448,41 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_up_energy(UpArgs a) {
     if (ch == 0) a.part_hop[j] = h0;
 }
 
-hipError_t launch_up1(const UpArgs &a, int n_spans, hipStream_t st) {
-    (void)n_spans;
+hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
     if (a.n_kseg <= 0) return hipSuccess;
+    const unsigned nblk = (unsigned)((a.n_kseg + AMX_UP_BLOCK / 2 - 1) / (AMX_UP_BLOCK / 2));
     if (a.static_l > 0) {
-        const dim3 g((unsigned)((a.n_kseg + AMX_UP_BLOCK / 2 - 1) / (AMX_UP_BLOCK / 2)));
+        // the left-over segments' kernel is latency-bound (a serial K-filter lane per
+        // channel): it runs on the plan's second stream beside the fast kernel
+        const bool side = a.n_slow > 0 && aux && fork && join;
+        if (a.n_slow > 0) {
+            hipStream_t es = side ? aux : st;
+            if (side) {
+                hipError_t e = hipEventRecord(fork, st);
+                if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
+                if (e != hipSuccess) return e;
+            }
+            hipLaunchKernelGGL(k_up_edge, dim3((unsigned)a.n_slow), dim3(64),
+                               (size_t)((a.Lin + UP_TAPS + 2 * a.Lout + 1) & ~1) * 4 + (size_t)a.Lout * 16,
+                               es, a);
+            if (side) {
+                hipError_t e = hipEventRecord(join, aux);
+                if (e != hipSuccess) return e;
+            }
+        }
         switch (a.static_l) {
-        case 2: hipLaunchKernelGGL(k_up<2>, g, dim3(AMX_UP_BLOCK), 0, st, a); break;
-        case 4: hipLaunchKernelGGL(k_up<4>, g, dim3(AMX_UP_BLOCK), 0, st, a); break;
+        case 2: hipLaunchKernelGGL(k_up<2>, dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a); break;
+        case 4: hipLaunchKernelGGL(k_up<4>, dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a); break;
         default: return hipErrorInvalidValue;
         }
-    }
-    if (a.n_slow > 0 && a.slow)
-        hipLaunchKernelGGL(k_up_edge, dim3((unsigned)a.n_slow), dim3(64),
-                           (size_t)((a.Lin + UP_TAPS + 2 * a.Lout + 1) & ~1) * 4 + (size_t)a.Lout * 16, st, a);
-    else if (a.n_slow > 0)
+        if (side) {
+            hipError_t e = hipStreamWaitEvent(st, join, 0);
+            if (e != hipSuccess) return e;
+        }
+    } else {
         hipLaunchKernelGGL(k_up_slow, dim3((unsigned)((a.n_slow + AMX_UP_BLOCK / 2 - 1) / (AMX_UP_BLOCK / 2))),
                            dim3(AMX_UP_BLOCK), 0, st, a);
+    }
     return hipGetLastError();
 }
 

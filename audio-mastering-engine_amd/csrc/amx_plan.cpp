@@ -231,8 +231,10 @@ struct amx_plan {
     // the track already is at 192 kHz (the measurement runs on d_out itself)
     int resamp = 0, upL = 1, upM = 1, upLin = 0, upLout = 0, up_static = 0, up_ok = 1;
     int32_t *d_obase = nullptr, *d_oph = nullptr;
-    int32_t *d_slow = nullptr;   // K segments k_up_slow takes (static path); n_slow of them
+    int32_t *d_slow = nullptr;   // K segments k_up_edge takes (static path); n_slow of them
     int64_t n_slow = 0;
+    hipStream_t up_aux = nullptr;            // k_up_edge's stream, forked from / joined to the caller's
+    hipEvent_t up_fork = nullptr, up_join = nullptr;
     double *d_qh = nullptr, *d_qt = nullptr;
     float *d_bank = nullptr;
     int mask = 0, D = 0;
@@ -920,6 +922,14 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     if (p->resamp) p->o_eterms = (size_t)align_up(off, nk * 2 * 10 * 8);
     p->o_phop = (size_t)align_up(off, nk * 8);
     p->ws_bytes = (off + 255) & ~(size_t)255;
+    if (p->resamp && p->up_static && p->n_slow > 0) {
+        if (hipStreamCreateWithFlags(&p->up_aux, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&p->up_fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&p->up_join, hipEventDisableTiming) != hipSuccess) {
+            amx_plan_free(p);
+            return fail(AMX_EHIP, "stream / event creation failed");
+        }
+    }
     *out = p;
     return AMX_OK;
 }
@@ -935,6 +945,9 @@ void amx_plan_free(amx_plan *p) {
                     p->d_qh, p->d_qt, p->d_slow};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
+    if (p->up_fork) (void)hipEventDestroy(p->up_fork);
+    if (p->up_join) (void)hipEventDestroy(p->up_join);
+    if (p->up_aux) (void)hipStreamDestroy(p->up_aux);
     delete p;
 }
 
@@ -1114,7 +1127,7 @@ int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, const int16_t *d_edge,
     double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
     uint32_t *pk = wsp<uint32_t>(d_ws, p->o_pk);
     if (p->resamp)    // GEMV over the 192 kHz stream + its sample peak (amx_loud192.hip)
-        HIPCHK(amx::launch_up1(up_args(p, d_out, d_edge, d_ws), p->n_tracks, st));
+        HIPCHK(amx::launch_up1(up_args(p, d_out, d_edge, d_ws), st, p->up_aux, p->up_fork, p->up_join));
     else if (!p->fuse_kw)  // else the GEMV + per-segment peaks were made by k_front2 (amx_run_chunks)
         HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e, pk, st));
     HIPCHK(amx::launch_peak_reduce(p->d_spans, p->n_tracks, p->max_nkseg, pk, d_peak, p->d_pcnt,
@@ -1334,8 +1347,12 @@ int amx_finalize(amx_plan *p, const amx_final_desc *fd, const int16_t *d_x,
     const double level = fd->auto_level ? 1 / fd->limit : 1;
     if ((d_ctl || !fast) && !d_lim_state) return fail(AMX_EINVAL, "general limiter needs d_lim_state");
     if ((d_ctl || !fast) && (!p->lim.seg_state || p->lim.buffer_size != bs)) {
-        // not captured into a graph: amx_limiter_prepare allocates (callers that
-        // capture call it first)
+        // amx_limiter_prepare allocates: not while the stream is being captured into a
+        // graph (callers that capture call it first)
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIPCHK(hipStreamIsCapturing(st, &cs));
+        if (cs != hipStreamCaptureStatusNone)
+            return fail(AMX_EINVAL, "amx_finalize: call amx_limiter_prepare before capturing the stream");
         rc = amx_limiter_prepare(p, fd, 0, -1);
         if (rc) return rc;
     }
