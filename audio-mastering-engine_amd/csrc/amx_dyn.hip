@@ -7,7 +7,10 @@
 //   att  <- (r_i > thr and att <= m_i) ? min(att + m_i/A, m_i) : max(att - m_i/R, 0)
 //   out_i = audioop.mul(frame_i, 10^(-att/20))   if att != 0
 //
-// r is embarrassingly parallel (k_rms: block prefix sums).  The envelope is a
+// r is embarrassingly parallel (k_rms: block prefix sums).  It is stored as the u16
+// table index r (m = mt[r] is a host table of C-libm values: 2 B per frame instead of
+// the 8 B of m, read ~5 times per step); the readers gather m from the table, with
+// lanes laid over consecutive frames so a gather touches few table lines.  The envelope is a
 // sequential nonlinear recurrence; it is parallelised by exact speculation:
 //   k_env0: every envelope segment of Le frames runs from att = 0 started W frames
 //     earlier (the trajectories of this recurrence coincide after clamp events, so
@@ -39,17 +42,15 @@ typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 // [base - AMX_RMS_LOOKPAD, base + AMX_RMS_F) are prefix-summed in LDS (exact
 // int64), so S_i = P(i) - P(i - look) with no sequential sliding window.  Frames
 // before the chunk count as 0 (audioop.rms over the shorter window divides by the
-// frames present).  Loads are 16-B vectors (the LDS origin is 16-frame aligned),
-// and each thread's 16 table gathers m_i = max_attenuation(r_i) are all in flight
-// at once -- consecutive frames have similar r, so they hit the same lines.
+// frames present).  Loads are 16-B vectors (the LDS origin is 16-frame aligned);
+// the output is r_i itself (u16, clamped to 32768 = |sample| max), m is not formed here.
 #define AMX_RMS_F 4096
 #define AMX_RMS_MAXLOOK 1024
 #define AMX_RMS_LOOKPAD 1024
 __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ cdp,
                                                    const ChunkDev *__restrict__ chunks,
                                                    const uint32_t *__restrict__ bands,
-                                                   const double *__restrict__ tabs,
-                                                   double *__restrict__ mm, int64_t nloc) {
+                                                   uint16_t *__restrict__ mi, int64_t nloc) {
     constexpr int N = AMX_RMS_F + AMX_RMS_LOOKPAD;
     constexpr int PER = N / AMX_BLOCK;                 // 20 slots per thread
     constexpr int VEC = PER / 4;                       // as 5 16-B loads
@@ -61,8 +62,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
     const int64_t base = (int64_t)blockIdx.x * AMX_RMS_F;
     if (base >= ch.n) return;                          // block-uniform
     const uint32_t *x = bands + b * nloc + ch.loc_off;
-    double *mo = mm + b * nloc + ch.loc_off;
-    const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
+    uint16_t *mo = mi + b * nloc + ch.loc_off;
     const int64_t rowlen = (ch.n + 15) / 16 * 16;     // the chunk row (16-frame aligned)
     // LDS slot k holds frame base - LOOKPAD + k
     const int64_t f0 = base - AMX_RMS_LOOKPAD;
@@ -100,7 +100,6 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
     __syncthreads();
     // frame i = base + nn uses slots [nn + LOOKPAD - look, nn + LOOKPAD)
     constexpr int OUT = AMX_RMS_F / AMX_BLOCK;
-    uint32_t rc[OUT];
 #pragma unroll
     for (int k = 0; k < OUT; k++) {
         const int nn = t + k * AMX_BLOCK;
@@ -109,16 +108,15 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
         const int64_t cnt = 2 * (i - wlo);
         const long long S = P[nn + AMX_RMS_LOOKPAD - 1] - P[nn + AMX_RMS_LOOKPAD - 1 - look];
         const uint32_t rms = cnt ? (uint32_t)sqrt((double)S / (double)cnt) : 0u;
-        rc[k] = rms > 32768u ? 32768u : rms;                  // |sample| <= 32768
+        if (i < ch.n) mo[i] = (uint16_t)(rms > 32768u ? 32768u : rms);    // |sample| <= 32768
     }
-    double mv[OUT];
-#pragma unroll
-    for (int k = 0; k < OUT; k++) mv[k] = mt[rc[k]];
-#pragma unroll
-    for (int k = 0; k < OUT; k++) {
-        const int64_t i = base + t + k * AMX_BLOCK;
-        if (i < ch.n) mo[i] = mv[k];
-    }
+}
+
+// m of table index r.  Rows hold r only where a chunk has frames: the padding and a
+// row's tail past the chunk hold anything, and are clamped into the table (their m is
+// never used)
+__device__ __forceinline__ double m_of(const double *__restrict__ mt, uint32_t r) {
+    return mt[r < 32768u ? r : 32768u];
 }
 
 // --------------------------------------------------------- envelope helpers
@@ -220,17 +218,17 @@ __device__ __forceinline__ double lane_val(double v, int i) {
 // trajectories are identical from there on, the remaining checkpoints stand and the
 // old end is the end.  Returns the segment's end state.
 template <bool RCP>
-__device__ double env_rerun_wave(const ChainDev &cd, const double *m, double *ckr, int64_t f0,
-                                 int64_t f1, double ns, double old_end) {
+__device__ double env_rerun_wave(const ChainDev &cd, const uint16_t *m, const double *mt, double *ckr,
+                                 int64_t f0, int64_t f1, double ns, double old_end) {
     __shared__ __attribute__((aligned(16))) double s_m[64], s_i[64], s_d[64];
     const int lane = threadIdx.x & 63;
     const bool ckl = (lane & (AMX_ENV_TF_ - 1)) == 0;
     double c = ns;
-    double ml = f0 + lane < f1 ? m[f0 + lane] : 0.0;
+    double ml = f0 + lane < f1 ? m_of(mt, m[f0 + lane]) : 0.0;
     double ol = ckl && f0 + lane < f1 ? ckr[(f0 + lane) / AMX_ENV_TF_] : 0.0;
     for (int64_t base = f0; base < f1; base += 64) {
         const int64_t fn = base + 64 + lane;
-        const double mn = fn < f1 ? m[fn] : 0.0;
+        const double mn = fn < f1 ? m_of(mt, m[fn]) : 0.0;
         const double on = ckl && fn < f1 ? ckr[fn / AMX_ENV_TF_] : 0.0;
         s_m[lane] = ml;
         s_i[lane] = env_div<RCP>(ml, cd.env_A, cd.env_rA);
@@ -276,38 +274,60 @@ __device__ double env_rerun_wave(const ChainDev &cd, const double *m, double *ck
 // the chunk -- from which k_gain_overlay re-derives every frame's attenuation in
 // parallel.  No gains are computed here: this is the latency-bound sequential
 // part, kept to ~16 fp64 operations per frame.
-// Frames move in 16-frame tiles.  A lane's tile is one 128-B row of m (64 rows per
-// wave); the wave loads the 64 rows cooperatively -- lane l moves 16-B piece l % 8
-// of rows 8 i + l / 8, so each load instruction covers 8 whole lines instead of 64
-// lines' 16-B fragments -- and stages them in LDS (padded rows, conflict-free b128
-// reads).  The loads run AMX_ENV_PF tiles ahead of the tile being computed (a ring
-// of register tiles): one tile is ~16 dependent steps, shorter than a miss to HBM,
-// so a one-tile lookahead left the wave waiting on every tile.  Frames before the
-// chunk or after the segment are fed as m = 0 (state held); the m buffer is padded
-// so those rows read in bounds.  W and Le are multiples of 16 AMX_ENV_PF and chunk
-// rows start 16-frame aligned, so the warm-up / main boundary is tile-uniform,
-// every vector is 16-B aligned and checkpoints fall on tile starts.
+// Frames move in 16-frame tiles.  A lane's tile is one 32-B row of r (64 rows per
+// wave); the wave loads the 64 rows cooperatively -- lane l moves 8-B piece l % 4 of
+// rows 16 i + l / 4 -- gathers m = mt[r] for the four frames of each piece (the four
+// lanes of a row gather neighbouring entries: slowly varying r, few table lines per
+// gather) and stages m in LDS (padded rows, conflict-free b128 reads).  The r loads
+// run AMX_ENV_PF tiles ahead and the gathers 2 tiles ahead of the tile being computed
+// (one tile is ~16 dependent steps, shorter than a miss to HBM).  Per tile the 16
+// quotient pairs are formed first (independent chains), then the recurrence runs
+// alone: at one wave per SIMD nothing else hides a stall.  Frames before the chunk or
+// after the segment are fed as m = 0 (state held); the buffer is padded so those rows
+// read in bounds.  W and Le are multiples of 16 AMX_ENV_PF and chunk rows start
+// 16-frame aligned, so the warm-up / main boundary is tile-uniform, every vector is
+// aligned and checkpoints fall on tile starts.
 #define AMX_ENV_TF 16
 #define AMX_ENV_MP 18      // m tile pitch in doubles (144 B)
-#define AMX_ENV_PF 4       // tiles in flight
+#define AMX_ENV_PF 8       // r tiles in flight
+
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+
+// m of one staged piece (4 frames: r in the 4 u16 of v)
+__device__ __forceinline__ void env_gather(const double *__restrict__ mt, const u2v (&I)[4],
+                                           double (&G)[16]) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const uint32_t r = (I[i][e >> 1] >> (16 * (e & 1))) & 0xffffu;
+            G[4 * i + e] = m_of(mt, r);
+        }
+    }
+}
 
 template <bool RCP>
-__device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, d2v (&M)[8],
-                                          const double *const (&mrow)[8], int q, int ntile,
-                                          int nwarm, int64_t start, int64_t end, double *ckr,
-                                          double &att, double &s_spec, bool &any) {
+__device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, double (&G)[16],
+                                          u2v (&Islot)[4], const u2v (&Inext)[4],
+                                          const uint16_t *const (&irow)[4], const double *mt, int q,
+                                          int ntile, int nwarm, int64_t start, int64_t end,
+                                          double *ckr, double &att, double &s_spec, bool &any) {
     const int lane = threadIdx.x;
+    // stage tile q's m (gathered two tiles ago)
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const int r = 8 * i + (lane >> 3);
-        *reinterpret_cast<d2v *>(sm + r * AMX_ENV_MP + 2 * (lane & 7)) = M[i];
+    for (int i = 0; i < 4; i++) {
+        double *d = sm + ((lane >> 2) + 16 * i) * AMX_ENV_MP + 4 * (lane & 3);
+        *reinterpret_cast<d2v *>(d) = d2v{G[4 * i], G[4 * i + 1]};
+        *reinterpret_cast<d2v *>(d + 2) = d2v{G[4 * i + 2], G[4 * i + 3]};
     }
     __builtin_amdgcn_wave_barrier();
     {
-        // refill this ring slot with tile q + PF (past the end: re-read, unused)
+        // this ring slot (tile q's r, gathered already) takes tile q + PF (past the
+        // end: re-read, unused); then the gathers of tile q + 2
         const int qn = (q + AMX_ENV_PF < ntile ? q + AMX_ENV_PF : q) * AMX_ENV_TF;
 #pragma unroll
-        for (int i = 0; i < 8; i++) M[i] = *reinterpret_cast<const d2v *>(mrow[i] + qn);
+        for (int i = 0; i < 4; i++) Islot[i] = *reinterpret_cast<const u2v *>(irow[i] + qn);
+        env_gather(mt, Inext, G);
     }
     const int64_t f0 = start + (int64_t)q * AMX_ENV_TF;
     const bool in = f0 >= 0 && f0 < end;           // whole tile in (else held)
@@ -333,8 +353,16 @@ __device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, d2v (&
 #pragma unroll
             for (int f = 0; f < AMX_ENV_TF; f++) any |= mv[f] != 0.0;
         }
+        double iv[AMX_ENV_TF], dv[AMX_ENV_TF];
 #pragma unroll
-        for (int f = 0; f < AMX_ENV_TF; f++) att = env_step<RCP>(cd, att, mv[f]);
+        for (int f = 0; f < AMX_ENV_TF; f++) {
+            iv[f] = env_div<RCP>(mv[f], cd.env_A, cd.env_rA);
+            dv[f] = env_div<RCP>(mv[f], cd.env_R, cd.env_rR);
+            mv[f] = __builtin_canonicalize(mv[f]);      // fmin's operand, once per frame here
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int f = 0; f < AMX_ENV_TF; f++) att = env_step3(att, mv[f], iv[f], dv[f]);
     }
 }
 
@@ -342,7 +370,8 @@ template <bool RCP>
 __global__ void __launch_bounds__(64) k_env0(const ChainDev *__restrict__ cdp,
                                              const ChunkDev *__restrict__ chunks,
                                              const SegDev *__restrict__ es, int n_es,
-                                             const double *__restrict__ mm,
+                                             const uint16_t *__restrict__ mi,
+                                             const double *__restrict__ tabs,
                                              double *__restrict__ ck,
                                              double *__restrict__ sv, double *__restrict__ ev,
                                              int *__restrict__ act, int64_t nloc, int warm,
@@ -363,25 +392,29 @@ __global__ void __launch_bounds__(64) k_env0(const ChainDev *__restrict__ cdp,
     const int64_t start = sg.pos - warm;                // frame of step 0 (may be < 0)
     const int64_t end = valid ? sg.pos + sg.len : sg.pos;
     double *ckr = ck + rowoff / AMX_ENV_TF;             // checkpoint k: before frame 16 k
+    const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
     const int ntile = (warm + Le) / AMX_ENV_TF, nwarm = warm / AMX_ENV_TF;
-    const double *mrow[8];
+    const uint16_t *irow[4];
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const int r = 8 * i + (lane >> 3);
-        mrow[i] = mm + __shfl(rowoff + start, r) + 2 * (lane & 7);
+    for (int i = 0; i < 4; i++) {
+        const int r = 16 * i + (lane >> 2);
+        irow[i] = mi + __shfl(rowoff + start, r) + 4 * (lane & 3);
     }
-    d2v M[AMX_ENV_PF][8];
+    u2v I[AMX_ENV_PF][4];
 #pragma unroll
     for (int u = 0; u < AMX_ENV_PF; u++)
 #pragma unroll
-        for (int i = 0; i < 8; i++) M[u][i] = *reinterpret_cast<const d2v *>(mrow[i] + u * AMX_ENV_TF);
+        for (int i = 0; i < 4; i++) I[u][i] = *reinterpret_cast<const u2v *>(irow[i] + u * AMX_ENV_TF);
+    double G[2][16];
+    env_gather(mt, I[0], G[0]);
+    env_gather(mt, I[1], G[1]);
     double att = 0.0, s_spec = 0.0;
     bool any = false;
     for (int q0 = 0; q0 < ntile; q0 += AMX_ENV_PF) {
 #pragma unroll
         for (int u = 0; u < AMX_ENV_PF; u++)
-            env0_tile<RCP>(cd, sm, M[u], mrow, q0 + u, ntile, nwarm, start, end, ckr, att, s_spec,
-                           any);
+            env0_tile<RCP>(cd, sm, G[u & 1], I[u], I[(u + 2) % AMX_ENV_PF], irow, mt, q0 + u, ntile,
+                           nwarm, start, end, ckr, att, s_spec, any);
     }
     if (valid) {
         sv[(int64_t)b * n_es + j] = s_spec;
@@ -393,16 +426,16 @@ __global__ void __launch_bounds__(64) k_env0(const ChainDev *__restrict__ cdp,
 // the wave fixes segment [pos, pos + len) of a chunk row from the new start ns (all
 // lanes, uniform arguments); returns the segment's end state
 template <bool RCP>
-__device__ __forceinline__ double env_fix_segment(const ChainDev &cd, const double *mrow,
-                                                  double *ckr, int64_t pos, int len, bool active,
-                                                  double ns, double old_end) {
+__device__ __forceinline__ double env_fix_segment(const ChainDev &cd, const uint16_t *mrow,
+                                                  const double *mt, double *ckr, int64_t pos, int len,
+                                                  bool active, double ns, double old_end) {
     if (!active) {
         // identity transfer: the held state is every checkpoint of the segment
         const int64_t k0 = pos / AMX_ENV_TF_, k1 = (pos + len + AMX_ENV_TF_ - 1) / AMX_ENV_TF_;
         for (int64_t k = k0 + (threadIdx.x & 63); k < k1; k += 64) ckr[k] = ns;
         return ns;
     }
-    return env_rerun_wave<RCP>(cd, mrow, ckr, pos, pos + len, ns, old_end);
+    return env_rerun_wave<RCP>(cd, mrow, mt, ckr, pos, pos + len, ns, old_end);
 }
 
 // ------------------------------------------------ rounds: parallel fix-up
@@ -423,7 +456,8 @@ template <bool RCP>
 __global__ void __launch_bounds__(64) k_envfix(const ChainDev *__restrict__ cdp,
                                                const ChunkDev *__restrict__ chunks,
                                                const SegDev *__restrict__ es, int n_es,
-                                               const double *__restrict__ mm,
+                                               const uint16_t *__restrict__ mm,
+                                               const double *__restrict__ tabs,
                                                double *__restrict__ ck, double *sv, double *ev,
                                                const int *__restrict__ act,
                                                int *__restrict__ prev, int64_t nloc,
@@ -489,8 +523,8 @@ __global__ void __launch_bounds__(64) k_envfix(const ChainDev *__restrict__ cdp,
         const bool aw = __shfl((int)a, w) != 0;
         const double nsw = __shfl(ns, w), enw = __shfl(en, w);
         const int64_t ro = b * nloc + locw;
-        const double r = env_fix_segment<RCP>(cd, mm + ro, ck + ro / AMX_ENV_TF_, posw, lenw, aw,
-                                              nsw, enw);
+        const double r = env_fix_segment<RCP>(cd, mm + ro, tabs + (int64_t)b * 3 * AMX_TAB,
+                                              ck + ro / AMX_ENV_TF_, posw, lenw, aw, nsw, enw);
         if (lane == w) { en = r; fixed = true; }
         nfix++;
         // lanes starting from segment w0 + w take its new end now
@@ -522,7 +556,8 @@ __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
                                                const SegDev *__restrict__ es, int n_es,
                                                const int *__restrict__ eseg0,
                                                const int *__restrict__ neseg,
-                                               const double *__restrict__ mm,
+                                               const uint16_t *__restrict__ mm,
+                                               const double *__restrict__ tabs,
                                                double *__restrict__ ck,
                                                double *__restrict__ sv, double *__restrict__ ev,
                                                const int *__restrict__ act,
@@ -554,8 +589,9 @@ __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
         const SegDev sg = es[found];
         const int p = Pv[found];
         const double ns = p >= 0 ? E[p] : 0.0;
-        const double r = env_fix_segment<RCP>(cd, mm + ro, ck + ro / AMX_ENV_TF_, sg.pos, sg.len,
-                                              A[found] != 0, ns, E[found]);
+        const double r = env_fix_segment<RCP>(cd, mm + ro, tabs + (int64_t)b * 3 * AMX_TAB,
+                                              ck + ro / AMX_ENV_TF_, sg.pos, sg.len, A[found] != 0,
+                                              ns, E[found]);
         __syncthreads();                    // every lane has read E/S of `found`
         if (lane == 0) {
             E[found] = r;
@@ -575,18 +611,20 @@ __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
 // recurrence from the checkpoint before its first frame (exact: the same operation
 // sequence from the same state) and applies the gain; the three gained samples are
 // summed with int16 saturation, band by band.
-// Memory: a wave owns 1024 consecutive frames.  Per band its m (8 KB) and samples
-// (4 KB) are read by 16-B pieces over consecutive lanes (every load instruction
-// one contiguous KiB) into LDS rows of 16 frames, the next band's pieces already in
-// flight; the output goes back the same way.  (Thread-owned 16-frame runs read
-// directly touch 64 lines per instruction and left the loads TA-bound.)
-#define AMX_GO_MP 18       // m row pitch in doubles (144 B: 16-B aligned, b128 conflict-free)
+// Memory: a wave owns 1024 consecutive frames.  Per band its samples (4 KB) are read
+// by 16-B pieces over consecutive lanes (every load instruction one contiguous KiB)
+// into LDS rows of 16 frames, the next band's pieces already in flight (thread-owned
+// 16-frame runs read directly touch 64 lines per instruction and left the loads
+// TA-bound); the output goes back the same way.  A thread reads its own 16 r (32 B:
+// the wave's loads still cover one contiguous 2 KB) and gathers m = mt[r] --
+// neighbouring threads hold neighbouring frames, so a gather touches few table lines.
 #define AMX_GO_XP 20       // sample / output row pitch in dwords (80 B)
 #define AMX_GO_WAVES (AMX_BLOCK / 64)
 template <bool RCP>
 __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__restrict__ cdp,
                                                             const ChunkDev *__restrict__ chunks,
-                                                            const double *__restrict__ mm,
+                                                            const uint16_t *__restrict__ mm,
+                                                            const double *__restrict__ tabs,
                                                             const double *__restrict__ ck,
                                                             const uint32_t *__restrict__ bands,
                                                             uint32_t *__restrict__ out,
@@ -596,7 +634,6 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
                                                             const int *__restrict__ eseg0,
                                                             const int *__restrict__ neseg,
                                                             int n_es, int seg_tiles) {
-    __shared__ __attribute__((aligned(16))) double sm_all[AMX_GO_WAVES][64 * AMX_GO_MP];
     __shared__ __attribute__((aligned(16))) uint32_t sx_all[AMX_GO_WAVES][64 * AMX_GO_XP];
     const ChainDev &cd = *cdp;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -606,26 +643,20 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
     const int64_t n = ch.n, n2 = ch.out_n;
     if (wbase >= n2) return;                            // wave-uniform; no block barriers below
     const int64_t n1 = n1tab[c];
-    double *smw = sm_all[wv];
     uint32_t *sxw = sx_all[wv];
     const int64_t i0 = wbase + lane * AMX_ENV_TF_;      // this thread's first frame
     // the chunk row holds (n + 15) / 16 * 16 frames; pieces past it re-read its start
     const int64_t rowlen = (n + AMX_ENV_TF_ - 1) / AMX_ENV_TF_ * AMX_ENV_TF_;
-    // loader pieces: m piece p = 64 i + lane (i < 8) = frames 2p, 2p+1 of the wave;
-    // sample piece p = 64 i + lane (i < 4) = frames 4p .. 4p+3
-    int64_t mo[8], xo[4];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const int64_t f = wbase + 2 * (64 * i + lane);
-        mo[i] = ch.loc_off + (f < rowlen ? f : 0);
-    }
+    // r: this thread's 16 frames; sample piece p = 64 i + lane (i < 4) = frames 4p .. 4p+3
+    const int64_t mo = ch.loc_off + (i0 < rowlen ? i0 : 0);
+    int64_t xo[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int64_t f = wbase + 4 * (64 * i + lane);
         xo[i] = ch.loc_off + (f < rowlen ? f : 0);
     }
     // seg_tiles (Le == this wave's 1024 frames): a band whose envelope segment has no
-    // over-threshold frame (act == 0) has m = 0 on the whole tile -- its m is not read
+    // over-threshold frame (act == 0) has m = 0 on the whole tile -- its r is not read
     bool mzero[3] = {false, false, false};
     const int jt = (int)(wbase / (64 * AMX_ENV_TF_));
     if (seg_tiles && jt < neseg[c]) {
@@ -633,11 +664,11 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
 #pragma unroll
         for (int b = 0; b < 3; b++) mzero[b] = act[(int64_t)b * n_es + js] == 0;
     }
-    d2v Mp[8];
+    u4v Mp[2];
     u4v Xp[4];
 #pragma unroll
-    for (int i = 0; i < 8; i++)
-        Mp[i] = mzero[0] ? d2v{0.0, 0.0} : *reinterpret_cast<const d2v *>(mm + mo[i]);
+    for (int i = 0; i < 2; i++)
+        Mp[i] = mzero[0] ? u4v{0u, 0u, 0u, 0u} : *reinterpret_cast<const u4v *>(mm + mo + 8 * i);
 #pragma unroll
     for (int i = 0; i < 4; i++) Xp[i] = *reinterpret_cast<const u4v *>(bands + xo[i]);
     uint32_t acc[AMX_ENV_TF_];
@@ -645,13 +676,15 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
     for (int f = 0; f < AMX_ENV_TF_; f++) acc[f] = 0u;
 #pragma unroll
     for (int b = 0; b < 3; b++) {
-        // stage this band's pieces: m piece p -> row p / 8, doubles 2 (p % 8);
-        // sample piece p -> row p / 4, dwords 4 (p % 4)
+        // this band's m for the thread's frames (frames past the chunk: r = 0, m = 0)
+        const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
+        double mv[AMX_ENV_TF_];
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int p = 64 * i + lane;
-            *reinterpret_cast<d2v *>(smw + (p >> 3) * AMX_GO_MP + 2 * (p & 7)) = Mp[i];
+        for (int f = 0; f < AMX_ENV_TF_; f++) {
+            const uint32_t r = (Mp[f >> 3][(f & 7) >> 1] >> (16 * (f & 1))) & 0xffffu;
+            mv[f] = m_of(mt, i0 + f < n ? r : 0u);
         }
+        // sample piece p -> row p / 4, dwords 4 (p % 4)
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const int p = 64 * i + lane;
@@ -661,19 +694,12 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
         if (b < 2) {                                    // next band in flight
             const int64_t bo = (int64_t)(b + 1) * nloc;
 #pragma unroll
-            for (int i = 0; i < 8; i++)
-                Mp[i] = mzero[b + 1] ? d2v{0.0, 0.0} : *reinterpret_cast<const d2v *>(mm + bo + mo[i]);
+            for (int i = 0; i < 2; i++)
+                Mp[i] = mzero[b + 1] ? u4v{0u, 0u, 0u, 0u} : *reinterpret_cast<const u4v *>(mm + bo + mo + 8 * i);
 #pragma unroll
             for (int i = 0; i < 4; i++) Xp[i] = *reinterpret_cast<const u4v *>(bands + bo + xo[i]);
         }
-        double mv[AMX_ENV_TF_];
         uint32_t xv[AMX_ENV_TF_];
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const d2v v = *reinterpret_cast<const d2v *>(smw + lane * AMX_GO_MP + 2 * k);
-            mv[2 * k] = v.x;
-            mv[2 * k + 1] = v.y;
-        }
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const u4v v = *reinterpret_cast<const u4v *>(sxw + lane * AMX_GO_XP + 4 * k);
@@ -694,7 +720,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
         } else {
 #pragma unroll
             for (int f = 0; f < AMX_ENV_TF_; f++) {
-                att = env_step<RCP>(cd, att, i0 + f < n ? mv[f] : 0.0);
+                att = env_step<RCP>(cd, att, mv[f]);
                 gv[f] = gain_frame(cd, xv[f], att);
             }
         }
@@ -736,32 +762,32 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
 }
 
 // ---------------------------------------------------------------- launchers
-hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, double *m) {
+hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m) {
     if (d.look > AMX_RMS_MAXLOOK) return hipErrorInvalidValue;
     dim3 g((unsigned)((d.max_chunk_n + AMX_RMS_F - 1) / AMX_RMS_F), (unsigned)d.n_chunks, 3);
     if (empty(g)) return hipSuccess;
     hipLaunchKernelGGL(k_rms, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks,
-                       reinterpret_cast<const uint32_t *>(bands), d.tabs, m, d.nloc);
+                       reinterpret_cast<const uint32_t *>(bands), m, d.nloc);
     return hipGetLastError();
 }
 
 // part 0: the speculation (k_env0); part 1: the parallel fix-up rounds (k_envfix)
 template <bool RCP>
-static void env_launch_t(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
+static void env_launch_t(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,
                          int *act, int *prev, int *flags, int rounds, int part) {
     const dim3 gw((unsigned)((d.n_es + 63) / 64), 3);
     if (part == 0) {
-        hipLaunchKernelGGL(k_env0<RCP>, gw, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es, m, ck,
-                           sv, ev, act, d.nloc, d.warm, d.Le, flags);
+        hipLaunchKernelGGL(k_env0<RCP>, gw, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es, m, d.tabs,
+                           ck, sv, ev, act, d.nloc, d.warm, d.Le, flags);
         return;
     }
     // rounds == 0: only prev[] (everything is left to k_envseq)
     for (int k = 0; k < (rounds > 0 ? rounds : 1); k++)
         hipLaunchKernelGGL(k_envfix<RCP>, gw, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es, m,
-                           ck, sv, ev, act, prev, d.nloc, flags, k, rounds > 0 ? 1 : 0);
+                           d.tabs, ck, sv, ev, act, prev, d.nloc, flags, k, rounds > 0 ? 1 : 0);
 }
 
-hipError_t launch_env(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
+hipError_t launch_env(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,
                       int *act, int *prev, int *flags, int rounds, int part) {
     if (d.n_es <= 0) return hipSuccess;
     if (d.warm % (AMX_ENV_TF * AMX_ENV_PF) || d.Le % (AMX_ENV_TF * AMX_ENV_PF))
@@ -772,20 +798,20 @@ hipError_t launch_env(const DynLaunch &d, const double *m, double *ck, double *s
     return hipGetLastError();
 }
 
-hipError_t launch_envseq(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
+hipError_t launch_envseq(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,
                          const int *act, const int *prev, const int *flags, int rounds) {
     if (d.n_es <= 0) return hipSuccess;
     const dim3 gr((unsigned)d.n_chunks, 3);
     if (d.rcp)
         hipLaunchKernelGGL(k_envseq<true>, gr, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es,
-                           d.eseg0, d.neseg, m, ck, sv, ev, act, prev, d.nloc, flags, rounds - 1);
+                           d.eseg0, d.neseg, m, d.tabs, ck, sv, ev, act, prev, d.nloc, flags, rounds - 1);
     else
         hipLaunchKernelGGL(k_envseq<false>, gr, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es,
-                           d.eseg0, d.neseg, m, ck, sv, ev, act, prev, d.nloc, flags, rounds - 1);
+                           d.eseg0, d.neseg, m, d.tabs, ck, sv, ev, act, prev, d.nloc, flags, rounds - 1);
     return hipGetLastError();
 }
 
-hipError_t launch_gain_overlay(const DynLaunch &d, const double *m, const double *ck,
+hipError_t launch_gain_overlay(const DynLaunch &d, const uint16_t *m, const double *ck,
                                const int16_t *bands, int16_t *out, int64_t max_chunk_out,
                                const int64_t *n1tab, const int *act) {
     dim3 g((unsigned)((max_chunk_out + AMX_ENV_TF_ * AMX_BLOCK - 1) / (AMX_ENV_TF_ * AMX_BLOCK)),
@@ -795,10 +821,10 @@ hipError_t launch_gain_overlay(const DynLaunch &d, const double *m, const double
     uint32_t *o = reinterpret_cast<uint32_t *>(out);
     const int seg_tiles = (act && d.Le == 64 * AMX_ENV_TF_) ? 1 : 0;
     if (d.rcp)
-        hipLaunchKernelGGL(k_gain_overlay<true>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, m, ck,
+        hipLaunchKernelGGL(k_gain_overlay<true>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, m, d.tabs, ck,
                            x, o, d.nloc, n1tab, act, d.eseg0, d.neseg, d.n_es, seg_tiles);
     else
-        hipLaunchKernelGGL(k_gain_overlay<false>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, m, ck,
+        hipLaunchKernelGGL(k_gain_overlay<false>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, m, d.tabs, ck,
                            x, o, d.nloc, n1tab, act, d.eseg0, d.neseg, d.n_es, seg_tiles);
     return hipGetLastError();
 }

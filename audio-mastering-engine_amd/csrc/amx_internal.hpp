@@ -152,15 +152,15 @@ struct DynLaunch {
     const double *tabs;
     hipStream_t st;
 };
-hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, double *m);
+hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m);
 // input decode: PCM of any supported format -> stereo s16 frames (amx_io.hip)
 hipError_t launch_pcm_to_s16(const void *raw, int64_t frames, int channels, int fmt, int16_t *out,
                              hipStream_t st);
-hipError_t launch_env(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
+hipError_t launch_env(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,
                       int *act, int *prev, int *flags, int rounds, int part);
-hipError_t launch_envseq(const DynLaunch &d, const double *m, double *ck, double *sv, double *ev,
+hipError_t launch_envseq(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,
                          const int *act, const int *prev, const int *flags, int rounds);
-hipError_t launch_gain_overlay(const DynLaunch &d, const double *m, const double *ck,
+hipError_t launch_gain_overlay(const DynLaunch &d, const uint16_t *m, const double *ck,
                                const int16_t *bands, int16_t *out, int64_t max_chunk_out,
                                const int64_t *n1tab, const int *act);
 // loudness

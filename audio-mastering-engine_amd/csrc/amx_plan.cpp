@@ -350,7 +350,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     if (!p) return fail(AMX_ENOMEM, "out of memory");
     p->desc = *desc;
     const int fs = desc->sample_rate;
-    if (desc->env_warm_frames >= 0) p->warm = (desc->env_warm_frames + 63) / 64 * 64;   // whole ring of k_env0 tiles
+    if (desc->env_warm_frames >= 0) p->warm = (desc->env_warm_frames + 127) / 128 * 128;   // whole ring of k_env0 tiles
     if (desc->env_rounds >= 0) p->rounds = desc->env_rounds;
     if (p->rounds > AMX_ENV_MAX_ROUNDS) {
         delete p;
@@ -901,7 +901,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         // 16-frame tile past its end: pad the buffer on both sides
         // (and k_gain_overlay reads whole 1024-frame wave tiles)
         const size_t mpad = (size_t)(p->warm > 1024 ? p->warm : 1024) + 64;
-        p->o_m = (size_t)align_up(off, (3 * nl + 2 * mpad) * 8) + mpad * 8;
+        p->o_m = (size_t)align_up(off, (3 * nl + 2 * mpad) * 2) + mpad * 2;   // u16 r
         p->o_esv = (size_t)align_up(off, 3 * ne * 8);
         p->o_ee0 = (size_t)align_up(off, 3 * ne * 8);
         p->o_eflags = (size_t)align_up(off, AMX_ENV_MAX_ROUNDS * (1 + AMX_ENV_NCTR) * 4);
@@ -994,7 +994,7 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     double *sx = p->mb ? wsp<double>(d_ws, p->o_sx) : nullptr;
     int16_t *bands = p->mb ? wsp<int16_t>(d_ws, p->o_bands) : nullptr;
     double *ck = p->mb ? wsp<double>(d_ws, p->o_gain) : nullptr;
-    double *mframe = p->mb ? wsp<double>(d_ws, p->o_m) : nullptr;
+    uint16_t *mframe = p->mb ? wsp<uint16_t>(d_ws, p->o_m) : nullptr;
     double *esv = p->mb ? wsp<double>(d_ws, p->o_esv) : nullptr;
     double *ee0 = p->mb ? wsp<double>(d_ws, p->o_ee0) : nullptr;
     int *eflags = p->mb ? wsp<int>(d_ws, p->o_eflags) : nullptr;
