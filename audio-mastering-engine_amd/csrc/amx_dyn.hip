@@ -108,7 +108,9 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
         const int64_t cnt = 2 * (i - wlo);
         const long long S = P[nn + AMX_RMS_LOOKPAD - 1] - P[nn + AMX_RMS_LOOKPAD - 1 - look];
         const uint32_t rms = cnt ? (uint32_t)sqrt((double)S / (double)cnt) : 0u;
-        if (i < ch.n) mo[i] = (uint16_t)(rms > 32768u ? 32768u : rms);    // |sample| <= 32768
+        // |sample| <= 32768; the row's tail past the chunk (to the 16-frame boundary)
+        // gets r = 0, m = 0: k_env0 feeds a chunk's partial last tile without masking
+        if (i < rowlen) mo[i] = i < ch.n ? (uint16_t)(rms > 32768u ? 32768u : rms) : (uint16_t)0;
     }
 }
 
@@ -343,13 +345,10 @@ __device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, double
     // a tile outside the chunk / segment holds the state: it is skipped rather than
     // fed zeros (the same state; no per-frame selects on the common path)
     if (in) {
+        // (the partial last tile of a chunk-final segment reads r = 0 past the chunk:
+        // the state is held there without masking, k_rms)
         if (q >= nwarm) {
             ckr[f0 / AMX_ENV_TF] = att;
-            // the partial last tile of a chunk-final segment holds the state past the end
-            if (f0 + AMX_ENV_TF > end) {
-#pragma unroll
-                for (int f = 0; f < AMX_ENV_TF; f++) mv[f] = f0 + f < end ? mv[f] : 0.0;
-            }
 #pragma unroll
             for (int f = 0; f < AMX_ENV_TF; f++) any |= mv[f] != 0.0;
         }
