@@ -81,7 +81,7 @@ class TrackSpan(ctypes.Structure):
 # every symbol include/amx.h declares (checked by the CPU test suite)
 EXPORTS = ("amx_abi_version", "amx_last_error", "amx_plan_create", "amx_plan_free",
            "amx_plan_get_info", "amx_plan_track_span", "amx_run_chunks", "amx_run_stage",
-           "amx_loudness_pass1",
+           "amx_loudness_pass1", "amx_loudness_pass1_part",
            "amx_kw_propagate", "amx_loudness_pass2", "amx_loudness_histograms",
            "amx_limiter_geometry", "amx_limiter_prepare", "amx_loudness_decide", "amx_kw_carry_setup", "amx_kw_carry",
            "amx_finalize", "amx_env_counters", "amx_pcm_to_s16")
@@ -113,6 +113,7 @@ def load(path=None):
     L.amx_run_chunks.argtypes = [vp, vp, vp, vp, vp]
     L.amx_run_stage.argtypes = [vp, ctypes.c_int32, vp, vp, vp, vp]
     L.amx_loudness_pass1.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+    L.amx_loudness_pass1_part.argtypes = [vp, ctypes.c_int32, vp, vp, vp, vp, vp, vp]
     L.amx_pcm_to_s16.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, vp, vp]
     L.amx_env_counters.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]
     L.amx_kw_propagate.argtypes = [vp, ctypes.c_int64, c_double_p, c_double_p]

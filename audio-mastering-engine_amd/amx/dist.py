@@ -383,7 +383,8 @@ class ShardedTrack:
             return job.run(d_in)
         job.run_chunks(d_in)
         self.exchange_edges()
-        job.timed("loud1", lambda: job.loudness_pass1(tail=True))
+        job.timed("up", lambda: job.loudness_pass1(tail=True, part=0))
+        job.timed("loud1", lambda: job.loudness_pass1(tail=True, part=1))
         self.exchange_carry_peaks()
         lufs_on = job.dd.lufs_on
         if lufs_on:

@@ -143,14 +143,15 @@ class MasteringJob:
         ev.append((name, a, b))
         return r
 
-    def loudness_pass1(self, stream=None, tail=True):
+    def loudness_pass1(self, stream=None, tail=True, part=None):
         """tail: also the K-filter end state from rest (only a chunk-sharded track's
-        next rank needs it)."""
-        capi.check(capi.load().amx_loudness_pass1(self.plan.h, capi.ptr(self.out),
-                                                  capi.ptr(self.edge) if self.needs_edge else None,
-                                                  capi.ptr(self.kw_tail) if tail else None,
-                                                  capi.ptr(self.peak), capi.ptr(self.ws), self._s(stream)),
-                   "amx_loudness_pass1")
+        next rank needs it).  part 0 / 1: one of the two launches of the pass (the
+        sample pass / peaks + scan), None: both."""
+        for p in ((0, 1) if part is None else (part,)):
+            capi.check(capi.load().amx_loudness_pass1_part(
+                self.plan.h, p, capi.ptr(self.out), capi.ptr(self.edge) if self.needs_edge else None,
+                capi.ptr(self.kw_tail) if tail else None, capi.ptr(self.peak), capi.ptr(self.ws),
+                self._s(stream)), "amx_loudness_pass1_part")
 
     def loudness_pass2(self, stream=None, carry=True):
         capi.check(capi.load().amx_loudness_pass2(self.plan.h, capi.ptr(self.out),
@@ -223,7 +224,8 @@ class MasteringJob:
         round trip); returns y (int16 [frames, 2]).  fetch_report() reads the
         loudness decision afterwards."""
         self.run_chunks(d_in, stream)
-        self.timed("loud1", lambda: self.loudness_pass1(stream, tail=False), stream)
+        self.timed("up", lambda: self.loudness_pass1(stream, tail=False, part=0), stream)
+        self.timed("loud1", lambda: self.loudness_pass1(stream, tail=False, part=1), stream)
         if self.dd.lufs_on:
             self.timed("loud2", lambda: self.loudness_pass2(stream, carry=False), stream)
             self.timed("hist", lambda: self.histograms(stream), stream)

@@ -1106,30 +1106,37 @@ int check_edges(const amx_plan *p, const int16_t *d_edge) {
 
 extern "C" {
 
-int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, const int16_t *d_edge, double *d_kw_tail,
-                       double *d_peak, void *d_ws, void *stream) {
+int amx_loudness_pass1_part(amx_plan *p, int32_t part, const int16_t *d_out, const int16_t *d_edge,
+                            double *d_kw_tail, double *d_peak, void *d_ws, void *stream) {
     if (!p || !d_peak || (p->n_kseg > 0 && (!d_out || !d_ws)))
         return fail(AMX_EINVAL, "null argument");
+    if (part != 0 && part != 1) return fail(AMX_EINVAL, "bad part %d", part);
     if (p->resamp && !p->up_ok)
         return fail(AMX_ERANGE, "%d Hz has no exact-rational 192 kHz resampler (loudnorm pass 1)",
                     p->cd.fs);
     if (int rc = check_edges(p, d_edge)) return rc;
     hipStream_t st = (hipStream_t)stream;
+    double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
+    uint32_t *pk = wsp<uint32_t>(d_ws, p->o_pk);
+    if (part == 0) {
+        // the pass over the samples: per K segment the zero-state end state (and, at
+        // 192 kHz, the peaks and energy terms; amx_loud192.hip)
+        p->kw_rest_states = 0;
+        if (p->n_kseg == 0) return AMX_OK;
+        if (p->resamp)
+            HIPCHK(amx::launch_up1(up_args(p, d_out, d_edge, d_ws), st, p->up_aux, p->up_fork, p->up_join));
+        else if (!p->fuse_kw)  // else the GEMV + per-segment peaks were made by k_front2 (amx_run_chunks)
+            HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e, pk, st));
+        return AMX_OK;
+    }
     // k_peak_reduce writes every track's peak; only tracks without a K segment (empty
     // spans) need the zero written here
     if (p->any_empty_span || p->n_kseg == 0)
         HIPCHK(hipMemsetAsync(d_peak, 0, sizeof(double) * 4 * (size_t)p->n_tracks, st));
-    p->kw_rest_states = 0;
     if (p->n_kseg == 0) {
         if (d_kw_tail) HIPCHK(hipMemsetAsync(d_kw_tail, 0, sizeof(double) * 8 * (size_t)p->n_tracks, st));
         return AMX_OK;
     }
-    double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
-    uint32_t *pk = wsp<uint32_t>(d_ws, p->o_pk);
-    if (p->resamp)    // GEMV over the 192 kHz stream + its sample peak (amx_loud192.hip)
-        HIPCHK(amx::launch_up1(up_args(p, d_out, d_edge, d_ws), st, p->up_aux, p->up_fork, p->up_join));
-    else if (!p->fuse_kw)  // else the GEMV + per-segment peaks were made by k_front2 (amx_run_chunks)
-        HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e, pk, st));
     HIPCHK(amx::launch_peak_reduce(p->d_spans, p->n_tracks, p->max_nkseg, pk, d_peak, p->d_pcnt,
                                    p->d_ppart, p->d_ksegs, p->Lkw, d_out, p->d_Gkw, e, p->fuse_kw,
                                    p->resamp, st));
@@ -1138,6 +1145,13 @@ int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, const int16_t *d_edge,
     if (d_kw_tail)
         HIPCHK(amx::launch_kw_tail(p->d_spans, p->n_tracks, s, e, p->d_tailpow, d_kw_tail, st));
     return AMX_OK;
+}
+
+int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, const int16_t *d_edge, double *d_kw_tail,
+                       double *d_peak, void *d_ws, void *stream) {
+    int rc = amx_loudness_pass1_part(p, 0, d_out, d_edge, d_kw_tail, d_peak, d_ws, stream);
+    if (rc) return rc;
+    return amx_loudness_pass1_part(p, 1, d_out, d_edge, d_kw_tail, d_peak, d_ws, stream);
 }
 
 int amx_pcm_to_s16(const void *d_raw, int64_t frames, int32_t channels, int32_t format,

@@ -69,7 +69,8 @@ def stage_bytes(stage, frames, ch_in):
     per = {
         "front1": fin + 4,              # f32 input -> s16 chain input
         "front2": 4 + 4,                # s16 chain input -> s16 chunk output / P
-        "loud1": 4,                     # K-filter GEMV + peak: reads the track once
+        "up": 4,                        # 192 kHz sample pass (k_up): reads the track once
+        "loud1": 0,                     # peaks + scan: per-segment states only
         "loud2": 4,                     # K-filter recursion: reads the track once
         "final": 4 + 4,                 # gain + limiter: track in -> output
         "xover": 4 + 12,                # P -> 3 bands
@@ -96,7 +97,7 @@ def front2_flops(frames, settings, mb):
 
 # the one kernel of each single-kernel stage (rocprofv3 short names)
 STAGE_KERNEL = {"front1": "k_front1s", "front2": "k_front2", "xover": "k_xover2", "rms": "k_rms",
-                "env": "k_env0", "apply": "k_gain_overlay", "final": "k_final"}
+                "env": "k_env0", "apply": "k_gain_overlay", "final": "k_final", "up": "k_up"}
 # launches per step of kernels that run more than once (the envelope fix rounds)
 PER_STEP = {"k_envfix": 2}
 # the pipeline's kernels (runtime copy / torch helper kernels excluded from step traffic)

@@ -213,6 +213,13 @@ AMX_API int amx_env_counters(const amx_plan *plan, const void *d_ws, int32_t *ou
  * d_out's own max |x| (the limiter's input bound). */
 AMX_API int amx_loudness_pass1(amx_plan *plan, const int16_t *d_out, const int16_t *d_edge,
                                double *d_kw_tail, double *d_peak, void *d_ws, void *stream);
+/* amx_loudness_pass1 in its two launches (same arguments): part 0 = the one pass over
+ * the samples (at 192 kHz: k_up, and k_up_edge beside it on the plan's second stream),
+ * part 1 = peaks, scan, tails.  pass1 == part 0 then part 1; split so a caller can
+ * time the sample pass alone. */
+AMX_API int amx_loudness_pass1_part(amx_plan *plan, int32_t part, const int16_t *d_out,
+                                    const int16_t *d_edge, double *d_kw_tail, double *d_peak,
+                                    void *d_ws, void *stream);
 /* Host helper for chunk-sharded tracks: out8 = A^frames * in8 (per channel 4x4 K-filter
  * transition at the measurement rate; frames of the measurement stream), so
  * carry(r+1) = A^{len_r} carry(r) + tail(r). */

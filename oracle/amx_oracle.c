@@ -854,3 +854,511 @@ EXPORT void orc_loudness_stats(const uint64_t *hist, const uint64_t *st_hist, do
     out[1] = lra;
     out[2] = thr;
 }
+
+/* ------------------------------------------------ loudnorm: the whole filter
+ * FFmpeg af_loudnorm.c restated (config_input, init_gaussian_filter,
+ * gaussian_filter, detect_peak, true_peak_limiter, filter_frame, flush_frame and
+ * activate's framing: a first frame of 3 s, then 100 ms frames, a flush frame at
+ * EOF) on the s16 track resampled to 192 kHz (swr_block above; the 192 kHz input
+ * format is what makes ffmpeg insert the resampler, whichever mode is taken).
+ * Options as the reference passes them: pass 1 (:229) I/TP/LRA only (measured_*
+ * defaults: I 0, LRA 0, TP 99, thresh -70, offset 0), pass 2 (:240) all measured
+ * values and offset = pass 1's target_offset.  linear=1 (default): with valid
+ * measured values that meet TP and LRA, init picks LINEAR_MODE and the filter keeps
+ * the input rate (no resampler) -- orc_linear_gain covers that case; here the
+ * 192 kHz modes: dynamic (FIRST / INNER / FINAL frames) and the LINEAR_MODE a
+ * first frame shorter than 3 s falls back to.
+ * PARITY UNPINNED: restated from the published source, no ffmpeg here.  Open
+ * point: the flush frame goes through filter_frame, whose first statement feeds
+ * r128_in; if ffmpeg does that, pass 1's input_* also count the last 2.9 s twice.
+ * This restatement (and the GPU measurement) feed r128_in once. */
+enum { LN_FIRST, LN_INNER, LN_FINAL, LN_LINEAR };
+enum { LIM_OUT, LIM_ATTACK, LIM_SUSTAIN, LIM_RELEASE };
+
+typedef struct {
+    double target_i, target_lra, target_tp;          /* dB (TP in dBTP) */
+    double measured_i, measured_lra, measured_tp, measured_thresh, offset;
+} orc_loudnorm_opts;
+
+typedef struct {
+    int ch, fs;
+    double target_i, target_lra, target_tp, measured_i, measured_lra, measured_tp,
+        measured_thresh, offset;
+    double *buf;
+    int buf_size, buf_index, prev_buf_index;
+    double delta[30], weights[21], prev_delta;
+    int index;
+    double gain_reduction[2];
+    double *limiter_buf;
+    double prev_smp[8];
+    int limiter_buf_index, limiter_buf_size, limiter_state, peak_index, env_index, env_cnt,
+        attack_length, release_length;
+    int frame_type, above_threshold, prev_nb_samples;
+    Ebur rin, rout;
+    uint64_t hin[1000], sin_[1000], hout[1000], sout[1000];
+} Ln;
+
+static int ln_frame_size(int sample_rate, int frame_len_msec) {
+    const int fsz = (int)round((double)sample_rate * (frame_len_msec / 1000.0));
+    return fsz + (fsz % 2);
+}
+
+static double ln_energy_to_loudness(double e) { return 10 * log10(e) - 0.691; }
+
+static double ln_shortterm(const Ebur *e) { return ln_energy_to_loudness(ebur_block_energy(e, e->h100 * 30)); }
+
+static double ln_global(const Ebur *e) {
+    double s[3];
+    orc_loudness_stats(e->hist, e->st_hist, s);
+    return s[0];
+}
+
+static double ln_relative_threshold(const Ebur *e) {
+    double s[3];
+    orc_loudness_stats(e->hist, e->st_hist, s);
+    return s[2];
+}
+
+static void ln_init(Ln *s, int fs, int ch, const orc_loudnorm_opts *o) {
+    memset(s, 0, sizeof *s);
+    s->ch = ch;
+    s->fs = fs;
+    s->target_i = o->target_i;
+    s->target_lra = o->target_lra;
+    s->target_tp = o->target_tp;
+    s->measured_i = o->measured_i;
+    s->measured_lra = o->measured_lra;
+    s->measured_tp = o->measured_tp;
+    s->measured_thresh = o->measured_thresh;
+    s->offset = o->offset;
+    s->buf_size = ln_frame_size(fs, 3000) * ch;
+    s->buf = (double *)calloc((size_t)s->buf_size, sizeof(double));
+    s->limiter_buf_size = ln_frame_size(fs, 210) * ch;
+    s->limiter_buf = (double *)calloc((size_t)s->buf_size, sizeof(double));
+    /* init_gaussian_filter */
+    {
+        double total = 0.0;
+        const double sigma = 3.5;
+        const int off = 21 / 2;
+        const double c1 = 1.0 / (sigma * sqrt(2.0 * M_PI));
+        const double c2 = 2.0 * pow(sigma, 2.0);
+        for (int i = 0; i < 21; i++) {
+            const int x = i - off;
+            s->weights[i] = c1 * exp(-(pow(x, 2.0) / c2));
+            total += s->weights[i];
+        }
+        const double adjust = 1.0 / total;
+        for (int i = 0; i < 21; i++) s->weights[i] *= adjust;
+    }
+    s->frame_type = LN_FIRST;
+    s->index = 1;
+    s->limiter_state = LIM_OUT;
+    s->offset = pow(10., s->offset / 20.);
+    s->target_tp = pow(10., s->target_tp / 20.);
+    s->attack_length = ln_frame_size(fs, 10);
+    s->release_length = ln_frame_size(fs, 100);
+    ebur_init(&s->rin, fs, ch, s->hin, s->sin_);
+    ebur_init(&s->rout, fs, ch, s->hout, s->sout);
+}
+
+static void ln_free(Ln *s) {
+    free(s->buf);
+    free(s->limiter_buf);
+    free(s->rin.ring);
+    free(s->rout.ring);
+}
+
+static double ln_gaussian(const Ln *s, int index) {
+    double result = 0.;
+    index = index - 10 > 0 ? index - 10 : index + 20;
+    for (int i = 0; i < 21; i++)
+        result += s->delta[((index + i) < 30) ? (index + i) : (index + i - 30)] * s->weights[i];
+    return result;
+}
+
+#define LN_W(i) ((i) < s->limiter_buf_size ? (i) : (i) - s->limiter_buf_size)
+
+static void ln_detect_peak(Ln *s, int offset, int nb_samples, int channels, int *peak_delta,
+                           double *peak_value) {
+    const double *buf = s->limiter_buf;
+    const double ceiling = s->target_tp;
+    *peak_delta = -1;
+    int index = s->limiter_buf_index + (offset * channels) + (1920 * channels);
+    if (index >= s->limiter_buf_size) index -= s->limiter_buf_size;
+    if (s->frame_type == LN_FIRST)
+        for (int c = 0; c < channels; c++) s->prev_smp[c] = fabs(buf[index + c - channels]);
+    for (int n = 0; n < nb_samples; n++) {
+        for (int c = 0; c < channels; c++) {
+            double th = fabs(buf[LN_W(index + c)]);
+            double next = fabs(buf[LN_W(index + c + channels)]);
+            if ((s->prev_smp[c] <= th) && (next <= th) && (th > ceiling) && (n > 0)) {
+                int detected = 1;
+                for (int i = 2; i < 12; i++) {
+                    next = fabs(buf[LN_W(index + c + (i * channels))]);
+                    if (next > th) {
+                        detected = 0;
+                        break;
+                    }
+                }
+                if (!detected) continue;
+                double max_peak = 0.0;
+                for (c = 0; c < channels; c++) {
+                    if (c == 0 || fabs(buf[index + c]) > max_peak) max_peak = fabs(buf[index + c]);
+                    s->prev_smp[c] = fabs(buf[LN_W(index + c)]);
+                }
+                *peak_delta = n;
+                s->peak_index = index;
+                *peak_value = max_peak;
+                return;
+            }
+            s->prev_smp[c] = th;
+        }
+        index += channels;
+        if (index >= s->limiter_buf_size) index -= s->limiter_buf_size;
+    }
+}
+
+static void ln_true_peak_limiter(Ln *s, double *out, int nb_samples, int channels) {
+    double *buf = s->limiter_buf;
+    const double ceiling = s->target_tp;
+    int index = s->limiter_buf_index, smp_cnt = 0, peak_delta = -1;
+    double peak_value = 0.0;
+    if (s->frame_type == LN_FIRST) {
+        double max = 0.;
+        for (int n = 0; n < 1920; n++) {
+            for (int c = 0; c < channels; c++) max = fabs(buf[c]) > max ? fabs(buf[c]) : max;
+            buf += channels;
+        }
+        if (max > ceiling) {
+            s->gain_reduction[1] = ceiling / max;
+            s->limiter_state = LIM_SUSTAIN;
+            buf = s->limiter_buf;
+            for (int n = 0; n < 1920; n++) {
+                for (int c = 0; c < channels; c++) buf[c] *= s->gain_reduction[1];
+                buf += channels;
+            }
+        }
+        buf = s->limiter_buf;
+    }
+    do {
+        switch (s->limiter_state) {
+        case LIM_OUT:
+            ln_detect_peak(s, smp_cnt, nb_samples - smp_cnt, channels, &peak_delta, &peak_value);
+            if (peak_delta != -1) {
+                s->env_cnt = 0;
+                smp_cnt += (peak_delta - s->attack_length);
+                s->gain_reduction[0] = 1.;
+                s->gain_reduction[1] = ceiling / peak_value;
+                s->limiter_state = LIM_ATTACK;
+                s->env_index = s->peak_index - (s->attack_length * channels);
+                if (s->env_index < 0) s->env_index += s->limiter_buf_size;
+                s->env_index += (s->env_cnt * channels);
+                if (s->env_index > s->limiter_buf_size) s->env_index -= s->limiter_buf_size;
+            } else {
+                smp_cnt = nb_samples;
+            }
+            break;
+        case LIM_ATTACK:
+            for (; s->env_cnt < s->attack_length; s->env_cnt++) {
+                for (int c = 0; c < channels; c++) {
+                    double env = s->gain_reduction[0] - ((double)s->env_cnt / (s->attack_length - 1) *
+                                                         (s->gain_reduction[0] - s->gain_reduction[1]));
+                    buf[s->env_index + c] *= env;
+                }
+                s->env_index += channels;
+                if (s->env_index >= s->limiter_buf_size) s->env_index -= s->limiter_buf_size;
+                smp_cnt++;
+                if (smp_cnt >= nb_samples) {
+                    s->env_cnt++;
+                    break;
+                }
+            }
+            if (smp_cnt < nb_samples) {
+                s->env_cnt = 0;
+                s->attack_length = 1920;
+                s->limiter_state = LIM_SUSTAIN;
+            }
+            break;
+        case LIM_SUSTAIN:
+            ln_detect_peak(s, smp_cnt, nb_samples, channels, &peak_delta, &peak_value);
+            if (peak_delta == -1) {
+                s->limiter_state = LIM_RELEASE;
+                s->gain_reduction[0] = s->gain_reduction[1];
+                s->gain_reduction[1] = 1.;
+                s->env_cnt = 0;
+                break;
+            } else {
+                double gain_reduction = ceiling / peak_value;
+                if (gain_reduction < s->gain_reduction[1]) {
+                    s->limiter_state = LIM_ATTACK;
+                    s->attack_length = peak_delta;
+                    if (s->attack_length <= 1) s->attack_length = 2;
+                    s->gain_reduction[0] = s->gain_reduction[1];
+                    s->gain_reduction[1] = gain_reduction;
+                    s->env_cnt = 0;
+                    break;
+                }
+                for (s->env_cnt = 0; s->env_cnt < peak_delta; s->env_cnt++) {
+                    for (int c = 0; c < channels; c++) buf[s->env_index + c] *= s->gain_reduction[1];
+                    s->env_index += channels;
+                    if (s->env_index >= s->limiter_buf_size) s->env_index -= s->limiter_buf_size;
+                    smp_cnt++;
+                    if (smp_cnt >= nb_samples) {
+                        s->env_cnt++;
+                        break;
+                    }
+                }
+            }
+            break;
+        case LIM_RELEASE:
+            for (; s->env_cnt < s->release_length; s->env_cnt++) {
+                for (int c = 0; c < channels; c++) {
+                    double env = s->gain_reduction[0] + (((double)s->env_cnt / (s->release_length - 1)) *
+                                                         (s->gain_reduction[1] - s->gain_reduction[0]));
+                    buf[s->env_index + c] *= env;
+                }
+                s->env_index += channels;
+                if (s->env_index >= s->limiter_buf_size) s->env_index -= s->limiter_buf_size;
+                smp_cnt++;
+                if (smp_cnt >= nb_samples) {
+                    s->env_cnt++;
+                    break;
+                }
+            }
+            if (smp_cnt < nb_samples) {
+                s->env_cnt = 0;
+                s->limiter_state = LIM_OUT;
+            }
+            break;
+        }
+    } while (smp_cnt < nb_samples);
+    for (int n = 0; n < nb_samples; n++) {
+        for (int c = 0; c < channels; c++) {
+            out[c] = buf[index + c];
+            if (fabs(out[c]) > ceiling) out[c] = ceiling * (out[c] < 0 ? -1 : 1);
+        }
+        out += channels;
+        index += channels;
+        if (index >= s->limiter_buf_size) index -= s->limiter_buf_size;
+    }
+}
+
+/* filter_frame on one input frame of nb frames (src interleaved); writes the output
+ * frame to dst and returns its frame count */
+static int ln_filter_frame(Ln *s, const double *src, int nb, double *dst, int feed_in) {
+    const int ch = s->ch;
+    double *buf = s->buf, *limiter_buf = s->limiter_buf;
+    int out_nb = nb;
+    if (feed_in) ebur_add(&s->rin, src, (size_t)nb);
+    if (s->frame_type == LN_FIRST && nb < ln_frame_size(s->fs, 3000)) {
+        double global = ln_global(&s->rin), true_peak = 0.0;
+        for (int c = 0; c < ch; c++)
+            if (c == 0 || s->rin.peak[c] > true_peak) true_peak = s->rin.peak[c];
+        const double offset = pow(10., (s->target_i - global) / 20.);
+        const double offset_tp = true_peak * offset;
+        s->offset = offset_tp < s->target_tp ? offset : s->target_tp / true_peak;
+        s->frame_type = LN_LINEAR;
+    }
+    switch (s->frame_type) {
+    case LN_FIRST: {
+        for (int n = 0; n < nb; n++) {
+            for (int c = 0; c < ch; c++) buf[s->buf_index + c] = src[c];
+            src += ch;
+            s->buf_index += ch;
+        }
+        const double shortterm = ln_shortterm(&s->rin);
+        double env_shortterm;
+        if (shortterm < s->measured_thresh) {
+            s->above_threshold = 0;
+            env_shortterm = shortterm <= -70. ? 0. : s->target_i - s->measured_i;
+        } else {
+            s->above_threshold = 1;
+            env_shortterm = shortterm <= -70. ? 0. : s->target_i - shortterm;
+        }
+        for (int n = 0; n < 30; n++) s->delta[n] = pow(10., env_shortterm / 20.);
+        s->prev_delta = s->delta[s->index];
+        s->buf_index = s->limiter_buf_index = 0;
+        for (int n = 0; n < (s->limiter_buf_size / ch); n++) {
+            for (int c = 0; c < ch; c++)
+                s->limiter_buf[s->limiter_buf_index + c] = buf[s->buf_index + c] * s->delta[s->index] * s->offset;
+            s->limiter_buf_index += ch;
+            if (s->limiter_buf_index >= s->limiter_buf_size) s->limiter_buf_index -= s->limiter_buf_size;
+            s->buf_index += ch;
+        }
+        const int sub = ln_frame_size(s->fs, 100);
+        ln_true_peak_limiter(s, dst, sub, ch);
+        ebur_add(&s->rout, dst, (size_t)sub);
+        out_nb = sub;
+        s->frame_type = LN_INNER;
+        break;
+    }
+    case LN_INNER: {
+        const double gain = ln_gaussian(s, s->index + 10 < 30 ? s->index + 10 : s->index + 10 - 30);
+        const double gain_next = ln_gaussian(s, s->index + 11 < 30 ? s->index + 11 : s->index + 11 - 30);
+        for (int n = 0; n < nb; n++) {
+            for (int c = 0; c < ch; c++) {
+                buf[s->prev_buf_index + c] = src[c];
+                limiter_buf[s->limiter_buf_index + c] =
+                    buf[s->buf_index + c] * (gain + (((double)n / nb) * (gain_next - gain))) * s->offset;
+            }
+            src += ch;
+            s->limiter_buf_index += ch;
+            if (s->limiter_buf_index >= s->limiter_buf_size) s->limiter_buf_index -= s->limiter_buf_size;
+            s->prev_buf_index += ch;
+            if (s->prev_buf_index >= s->buf_size) s->prev_buf_index -= s->buf_size;
+            s->buf_index += ch;
+            if (s->buf_index >= s->buf_size) s->buf_index -= s->buf_size;
+        }
+        const int sub = (ln_frame_size(s->fs, 100) - nb) * ch;
+        s->limiter_buf_index = s->limiter_buf_index + sub < s->limiter_buf_size
+                                   ? s->limiter_buf_index + sub
+                                   : s->limiter_buf_index + sub - s->limiter_buf_size;
+        ln_true_peak_limiter(s, dst, nb, ch);
+        ebur_add(&s->rout, dst, (size_t)nb);
+        const double global = ln_global(&s->rin);
+        const double shortterm = ln_shortterm(&s->rin);
+        const double relative_threshold = ln_relative_threshold(&s->rin);
+        if (s->above_threshold == 0) {
+            if (shortterm > s->measured_thresh) s->prev_delta *= 1.0058;
+            const double shortterm_out = ln_shortterm(&s->rout);
+            if (shortterm_out >= s->target_i) s->above_threshold = 1;
+        }
+        if (shortterm < relative_threshold || shortterm <= -70. || s->above_threshold == 0) {
+            s->delta[s->index] = s->prev_delta;
+        } else {
+            const double env_global = fabs(shortterm - global) < (s->target_lra / 2.)
+                                          ? shortterm - global
+                                          : (s->target_lra / 2.) * ((shortterm - global) < 0 ? -1 : 1);
+            const double env_shortterm = s->target_i - shortterm;
+            s->delta[s->index] = pow(10., (env_global + env_shortterm) / 20.);
+        }
+        s->prev_delta = s->delta[s->index];
+        s->index++;
+        if (s->index >= 30) s->index -= 30;
+        s->prev_nb_samples = nb;
+        break;
+    }
+    case LN_FINAL: {
+        const double gain = ln_gaussian(s, s->index + 10 < 30 ? s->index + 10 : s->index + 10 - 30);
+        int src_index = 0;
+        s->limiter_buf_index = 0;
+        for (int n = 0; n < s->limiter_buf_size / ch; n++) {
+            for (int c = 0; c < ch; c++) s->limiter_buf[s->limiter_buf_index + c] = src[src_index + c] * gain * s->offset;
+            src_index += ch;
+            s->limiter_buf_index += ch;
+            if (s->limiter_buf_index >= s->limiter_buf_size) s->limiter_buf_index -= s->limiter_buf_size;
+        }
+        const int sub = ln_frame_size(s->fs, 100);
+        double *d = dst;
+        for (int i = 0; i < nb / sub; i++) {
+            ln_true_peak_limiter(s, d, sub, ch);
+            for (int n = 0; n < sub; n++) {
+                for (int c = 0; c < ch; c++) {
+                    if (src_index < (nb * ch))
+                        limiter_buf[s->limiter_buf_index + c] = src[src_index + c] * gain * s->offset;
+                    else
+                        limiter_buf[s->limiter_buf_index + c] = 0.;
+                }
+                if (src_index < (nb * ch)) src_index += ch;
+                s->limiter_buf_index += ch;
+                if (s->limiter_buf_index >= s->limiter_buf_size) s->limiter_buf_index -= s->limiter_buf_size;
+            }
+            d += (sub * ch);
+        }
+        ebur_add(&s->rout, dst, (size_t)nb);
+        break;
+    }
+    case LN_LINEAR:
+        for (int n = 0; n < nb; n++) {
+            for (int c = 0; c < ch; c++) dst[c] = src[c] * s->offset;
+            src += ch;
+            dst += ch;
+        }
+        ebur_add(&s->rout, dst - (size_t)nb * ch, (size_t)nb);
+        break;
+    }
+    return out_nb;
+}
+
+/* flush_frame: the last 3 s minus one frame, re-read from the ring, as FINAL_FRAME */
+static int ln_flush(Ln *s, double *tmp, double *dst) {
+    if (s->frame_type != LN_INNER) return 0;
+    const int ch = s->ch;
+    int nb = (s->buf_size / ch) - s->prev_nb_samples;
+    nb -= (ln_frame_size(s->fs, 100) - s->prev_nb_samples);
+    int offset = ((s->limiter_buf_size / ch) - s->prev_nb_samples) * ch;
+    offset -= (ln_frame_size(s->fs, 100) - s->prev_nb_samples) * ch;
+    s->buf_index = s->buf_index - offset < 0 ? s->buf_index - offset + s->buf_size : s->buf_index - offset;
+    double *src = tmp;
+    for (int n = 0; n < nb; n++) {
+        for (int c = 0; c < ch; c++) src[c] = s->buf[s->buf_index + c];
+        src += ch;
+        s->buf_index += ch;
+        if (s->buf_index >= s->buf_size) s->buf_index -= s->buf_size;
+    }
+    s->frame_type = LN_FINAL;
+    /* filter_frame's r128_in feed is skipped for the flush frame (see the open point) */
+    return ln_filter_frame(s, tmp, nb, dst, 0);
+}
+
+/* The filter over the whole 192 kHz stream of an s16 track: returns the output
+ * frames (192 kHz; the input's count when it is >= 3 s), writes them as s16 the way
+ * the WAV muxer's conversion does (dbl -> s16: av_clip_int16(llrint(x * 32768))) when
+ * out16 is given, and the summary: stats = [input_i, input_tp (dB), input_lra,
+ * input_thresh, output_i, output_tp (dB), output_lra, output_thresh, mode (1 linear,
+ * 0 dynamic), target_offset].  -1: no 192 kHz resampler for fs. */
+EXPORT int64_t orc_loudnorm(const int16_t *x, int64_t n, int fs, int channels,
+                            const orc_loudnorm_opts *o, int16_t *out16, double *stats) {
+    const int out_rate = 192000;
+    int L, M;
+    if (orc_swr_geometry(fs, out_rate, &L, &M)) return -1;
+    float *bank = (float *)malloc(sizeof(float) * (size_t)L * SWR_TAPS);
+    orc_swr_bank(fs, out_rate, bank);
+    const int64_t n_out = n > 0 ? orc_swr_out_frames(n, fs, out_rate) : 0;
+    Ln s;
+    ln_init(&s, out_rate, channels, o);
+    const int first = ln_frame_size(out_rate, 3000), step = ln_frame_size(out_rate, 100);
+    double *in = (double *)malloc(sizeof(double) * (size_t)first * channels);
+    double *out = (double *)malloc(sizeof(double) * (size_t)first * channels);
+    int64_t w = 0;                                   /* output frames written */
+    for (int64_t j = 0; j < n_out;) {
+        const int64_t want = s.frame_type == LN_FIRST ? first : step;
+        const int take = (int)(want < n_out - j ? want : n_out - j);
+        swr_block(x, n, channels, L, M, bank, j, j + take, in);
+        const int m = ln_filter_frame(&s, in, take, out, 1);
+        if (out16)
+            for (int64_t i = 0; i < (int64_t)m * channels; i++) {
+                double v = llrint(out[i] * 32768.0);
+                out16[w * channels + i] = (int16_t)(v > 32767 ? 32767 : (v < -32768 ? -32768 : v));
+            }
+        w += m;
+        j += take;
+    }
+    {
+        const int m = ln_flush(&s, in, out);
+        if (out16)
+            for (int64_t i = 0; i < (int64_t)m * channels; i++) {
+                double v = llrint(out[i] * 32768.0);
+                out16[w * channels + i] = (int16_t)(v > 32767 ? 32767 : (v < -32768 ? -32768 : v));
+            }
+        w += m;
+    }
+    if (stats) {
+        double a[3], b[3], tin = 0.0, tout = 0.0;
+        orc_loudness_stats(s.hin, s.sin_, a);
+        orc_loudness_stats(s.hout, s.sout, b);
+        for (int c = 0; c < channels; c++) {
+            if (c == 0 || s.rin.peak[c] > tin) tin = s.rin.peak[c];
+            if (c == 0 || s.rout.peak[c] > tout) tout = s.rout.peak[c];
+        }
+        stats[0] = a[0]; stats[1] = 20. * log10(tin); stats[2] = a[1]; stats[3] = a[2];
+        stats[4] = b[0]; stats[5] = 20. * log10(tout); stats[6] = b[1]; stats[7] = b[2];
+        stats[8] = s.frame_type == LN_LINEAR ? 1.0 : 0.0;
+        stats[9] = s.target_i - b[0];
+    }
+    free(in);
+    free(out);
+    free(bank);
+    ln_free(&s);
+    return w;
+}

@@ -376,6 +376,48 @@ def loudnorm_linear_gain(stats, target_i, target_tp=-1.5, target_lra=11.0):
     return "dynamic", None
 
 
+class _LoudnormOpts(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_double) for k in ("target_i", "target_lra", "target_tp", "measured_i",
+                                                 "measured_lra", "measured_tp", "measured_thresh",
+                                                 "offset")]
+
+
+def loudnorm(x16, fs, target_i, target_tp=-1.5, target_lra=11.0, measured=None, offset=0.0):
+    """af_loudnorm at 192 kHz over an s16 track (amx_oracle.c orc_loudnorm): the
+    dynamic mode (or the < 3 s linear fallback).  measured: dict of the pass-1 strings
+    (input_i, input_lra, input_tp, input_thresh) or None (pass 1's defaults).  Returns
+    (s16 output at 192 kHz, summary dict of ffmpeg's print_format=json strings)."""
+    x16 = np.ascontiguousarray(x16, np.int16)
+    ch = x16.shape[1]
+    o = _LoudnormOpts(target_i, target_lra, target_tp, 0.0, 0.0, 99.0, -70.0, offset)
+    if measured is not None:
+        o.measured_i = float(measured["input_i"])
+        o.measured_lra = float(measured["input_lra"])
+        o.measured_tp = float(measured["input_tp"])
+        o.measured_thresh = float(measured["input_thresh"])
+    n_out = int(lib().orc_swr_out_frames(_i64(x16.shape[0]), ctypes.c_int(fs), ctypes.c_int(192000)))
+    if n_out < 0:
+        raise ValueError("no 192 kHz resampler for %d Hz input" % fs)
+    out = np.zeros((max(n_out, 1), ch), np.int16)
+    st = np.zeros(10, np.float64)
+    f = lib().orc_loudnorm
+    f.restype = ctypes.c_int64
+    m = f(_p(x16, _i16p), _i64(x16.shape[0]), ctypes.c_int(fs), ctypes.c_int(ch), ctypes.byref(o),
+          _p(out, _i16p), _p(st, _f64p))
+    fmt = lambda v: "%.2f" % v
+    summary = {"input_i": fmt(st[0]), "input_tp": fmt(st[1]), "input_lra": fmt(st[2]),
+               "input_thresh": fmt(st[3]), "output_i": fmt(st[4]), "output_tp": "%+.2f" % st[5],
+               "output_lra": fmt(st[6]), "output_thresh": "%+.2f" % st[7],
+               "normalization_type": "linear" if st[8] else "dynamic", "target_offset": fmt(st[9])}
+    return out[:m], summary
+
+
+def loudnorm_pass1(x16, fs, target_i, target_tp=-1.5, target_lra=11.0):
+    """pass 1 (:229) as ffmpeg prints it: the whole filter runs (dynamic mode) and
+    target_offset is target_i minus its output's integrated loudness"""
+    return loudnorm(x16, fs, target_i, target_tp, target_lra)[1]
+
+
 def pipeline(x, fs, settings, chunks):
     """Whole process_audio_with_ffmpeg_pipeline (:171-226) on CPU.
 
@@ -391,6 +433,7 @@ def pipeline(x, fs, settings, chunks):
     info = {"concat": cat}
     y = cat
     lufs = settings.get("lufs")
+    out_fs = fs
     if lufs is not None:
         st = loudnorm_measure(cat, fs)
         mode, g = loudnorm_linear_gain(st, float(lufs))
@@ -398,6 +441,11 @@ def pipeline(x, fs, settings, chunks):
         if mode == "linear":
             y = linear_gain(cat, g)
         elif mode == "dynamic":
-            raise NotImplementedError("dynamic loudnorm")
+            # pass 1's target_offset needs the whole filter run; pass 2 at 192 kHz
+            p1 = loudnorm_pass1(cat, fs, float(lufs))
+            y, _ = loudnorm(cat, fs, float(lufs), measured=st, offset=float(p1["target_offset"]))
+            info.update(pass1=p1)
+            out_fs = 192000
     info["normalized"] = y
-    return alimiter(y, fs), info
+    info["sample_rate"] = out_fs
+    return alimiter(y, out_fs), info
