@@ -10,6 +10,7 @@ PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(PKG, "lib", "libamx.so")
 SOURCES = ["amx_chain.hip", "amx_scan.hip", "amx_dyn.hip", "amx_loud.hip", "amx_loud192.hip", "amx_final.hip", "amx_io.hip",
+           "amx_loudnorm.hip",
            "amx_plan.cpp"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-fvisibility=hidden", "-ffp-contract=off", "-Wall", "-Wno-unused-function"]

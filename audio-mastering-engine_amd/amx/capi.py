@@ -29,7 +29,7 @@ class AmxError(RuntimeError):
 class ChainDesc(ctypes.Structure):
     _fields_ = [
         ("sample_rate", ctypes.c_int32), ("channels_in", ctypes.c_int32),
-        ("input_s16", ctypes.c_int32), ("pad0_", ctypes.c_int32),
+        ("input_s16", ctypes.c_int32), ("measure_only", ctypes.c_int32),
         ("analog_on", ctypes.c_int32), ("analog_drive", ctypes.c_float),
         ("tanh_lut", c_float_p),
         ("analog_lo_ba", ctypes.c_double * 6), ("analog_lo_gain", ctypes.c_double),
@@ -73,6 +73,11 @@ class PlanInfo(ctypes.Structure):
                 ("max_hops", ctypes.c_int64)]
 
 
+class LoudnormDesc(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_double) for k in ("target_i", "target_lra", "target_tp", "measured_i",
+                                                 "measured_lra", "measured_tp", "measured_thresh", "offset")]
+
+
 class TrackSpan(ctypes.Structure):
     _fields_ = [("out_offset", ctypes.c_int64), ("out_frames", ctypes.c_int64),
                 ("track_frame0", ctypes.c_int64), ("track_frames_total", ctypes.c_int64)]
@@ -84,7 +89,8 @@ EXPORTS = ("amx_abi_version", "amx_last_error", "amx_plan_create", "amx_plan_fre
            "amx_loudness_pass1", "amx_loudness_pass1_part",
            "amx_kw_propagate", "amx_loudness_pass2", "amx_loudness_histograms",
            "amx_limiter_geometry", "amx_limiter_prepare", "amx_loudness_decide", "amx_kw_carry_setup", "amx_kw_carry",
-           "amx_finalize", "amx_env_counters", "amx_pcm_to_s16")
+           "amx_finalize", "amx_env_counters", "amx_pcm_to_s16", "amx_loudnorm_192k_size",
+           "amx_loudnorm_192k")
 PCM_FORMATS = {"u8": 0, "s16": 1, "s24": 2, "s32": 3, "f32": 4, "f64": 5}
 
 _lib = None
@@ -128,6 +134,10 @@ def load(path=None):
     L.amx_kw_carry.argtypes = [vp, vp, vp, vp]
     L.amx_finalize.argtypes = [vp, ctypes.POINTER(FinalDesc), vp, vp, vp, ctypes.c_int32, vp, vp,
                                vp, vp, vp]
+    L.amx_loudnorm_192k_size.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64),
+                                         ctypes.POINTER(ctypes.c_int64)]
+    L.amx_loudnorm_192k.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(LoudnormDesc), vp, vp,
+                                    ctypes.c_int64, vp, vp, vp, vp, vp]
     if L.amx_abi_version() != ABI_VERSION:
         raise AmxError("libamx ABI version mismatch")
     _lib = L

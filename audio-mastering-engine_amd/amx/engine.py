@@ -43,7 +43,7 @@ class MasteringJob:
     def __init__(self, sample_rate, channels_in, settings, track_frames, *, quantum=None,
                  input_s16=False, seg_frames=128, device=None, chunks=None, track_frame0=None,
                  track_total=None, limiter=ALIMITER, limiter_seg_frames=0,
-                 limiter_warm_frames=-1):
+                 limiter_warm_frames=-1, measure_only=False):
         if not torch.cuda.is_available():
             raise RuntimeError("amx needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.device = torch.device(device or "cuda")
@@ -53,6 +53,7 @@ class MasteringJob:
         self.input_s16 = bool(input_s16)
         self.desc, self._keep = design.chain_desc(self.fs, self.channels_in, self.settings)
         self.desc.input_s16 = 1 if input_s16 else 0
+        self.desc.measure_only = 1 if measure_only else 0
         if quantum is None:
             quantum = packet_frames(self.channels_in * (2 if input_s16 else 4))
         self.track_frames = [int(n) for n in track_frames]
@@ -194,6 +195,64 @@ class MasteringJob:
         rows = [list(buf[4 * r:4 * r + 4]) for r in range(16)]
         keys = ("reruns", "max_chain", "waves", "lookback")
         return [dict(zip(keys, r)) for r in rows if any(r)]
+
+    # --------------------------------------------- loudnorm dynamic mode (192 kHz)
+    def _job192(self, t):
+        """the 192 kHz side of track t: a measure-only plan at 192 kHz holding the
+        filter's output (its loudness measurement gives pass 1's target_offset; its
+        alimiter is the reference's :223 on the 192 kHz file) + amx_loudnorm_192k's
+        scratch"""
+        import ctypes
+        n192, wsb = ctypes.c_int64(), ctypes.c_int64()
+        capi.check(capi.load().amx_loudnorm_192k_size(self.plan.h, t, ctypes.byref(n192), ctypes.byref(wsb)),
+                   "amx_loudnorm_192k_size")
+        key = (t, n192.value)
+        if getattr(self, "_j192", None) is None or self._j192[0] != key:
+            job2 = MasteringJob(192000, 2, {"lufs": self.settings.get("lufs")}, [n192.value],
+                                input_s16=True, chunks=[(0, 0, n192.value)], device=self.device,
+                                measure_only=True)
+            ws2 = torch.empty(max(1, wsb.value), dtype=torch.uint8, device=self.device)
+            summ = torch.zeros(2, dtype=torch.float64, device=self.device)
+            self._j192 = (key, job2, ws2, summ)
+        return n192.value, self._j192[1], self._j192[2], self._j192[3]
+
+    def loudnorm_192k(self, t, desc, job2, ws2, summ, stream=None):
+        import ctypes
+        capi.check(capi.load().amx_loudnorm_192k(
+            self.plan.h, t, ctypes.byref(desc), capi.ptr(self.out), capi.ptr(self.hops),
+            int(self.max_hops), capi.ptr(self.peak), capi.ptr(job2.out), capi.ptr(summ), capi.ptr(ws2),
+            self._s(stream)), "amx_loudnorm_192k")
+
+    def dynamic_track(self, t, stats, stream=None):
+        """loudnorm's dynamic mode for track t (:240 when the linear conditions fail), as
+        the reference's two ffmpeg passes run it: pass 1's filter with the measured_*
+        defaults, whose output loudness gives target_offset; pass 2's filter with the
+        pass-1 strings; then the alimiter (:223) at 192 kHz.  Returns (int16 [n192, 2] at
+        192 kHz, info).  Every per-sample step is on the device; the host reads pass 1's
+        output loudness (one double) to form the "%.2f" string pass 2 parses."""
+        n192, job2, ws2, summ = self._job192(t)
+        target = float(self.settings["lufs"])
+        d = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
+        self.loudnorm_192k(t, d, job2, ws2, summ, stream)
+        job2.loudness_pass1(stream, tail=False)
+        job2.loudness_pass2(stream, carry=False)
+        job2.histograms(stream)
+        job2.dd.lufs_on = 1
+        job2.decide(stream)
+        i_out = float(job2.stats[0, 0].item())
+        target_offset = loudness._fmt(target - i_out)
+        d.measured_i = float(stats["input_i"])
+        d.measured_lra = float(stats["input_lra"])
+        d.measured_tp = float(stats["input_tp"])
+        d.measured_thresh = float(stats["input_thresh"])
+        d.offset = float(target_offset)
+        self.loudnorm_192k(t, d, job2, ws2, summ, stream)
+        job2.loudness_pass1(stream, tail=False)            # the limiter's input bound
+        job2.dd.lufs_on = 0
+        job2.decide(stream)
+        job2.finalize(None, stream)
+        return job2.y[:n192], {"target_offset": target_offset, "pass1_output_i": i_out,
+                               "sample_rate": 192000}
 
     # ------------------------------------------------------------ report
     def fetch_report(self, raise_dynamic=True):

@@ -106,14 +106,23 @@ def master_audio(settings, status_callback=None, progress_callback=None):
         job.loudness_pass2(carry=False)
         job.histograms()
     job.decide()
-    report = job.fetch_report()          # raises DynamicModeUnsupported before any output
-    if report["modes"] and report["modes"][0] == "skip":
+    report = job.fetch_report(raise_dynamic=False)
+    mode = report["modes"][0] if report["modes"] else "off"
+    if mode == "skip":
         logging.warning("Measured loudness is -inf (silent audio). Skipping normalization.")
+    dyn = None
+    if mode == "dynamic":
+        # loudnorm pass 2 in dynamic mode (:240): 192 kHz AGC + true-peak limiter
+        dyn = job.dynamic_track(0, report["stats"][0])
     status("Applying final limiting and exporting...")                        # :221
     progress(num_chunks + 3, total_steps)                                     # :222
-    job.finalize(None)
-    y = job.y[:job.info.out_frames].cpu().numpy()
-    wavio.write_wav_s16(output_file, y, fs)
+    if dyn is None:
+        job.finalize(None)
+        y, out_fs = job.y[:job.info.out_frames].cpu().numpy(), fs
+    else:
+        # the alimiter ran on the 192 kHz file inside dynamic_track (:223 keeps its rate)
+        y, out_fs = dyn[0].cpu().numpy(), dyn[1]["sample_rate"]
+    wavio.write_wav_s16(output_file, y, out_fs)
     progress(total_steps, total_steps)                                        # :224
     logging.info(f"Finished GPU pipeline, exported to {output_file}")
     return output_file

@@ -201,6 +201,23 @@ struct UpArgs {
     int64_t *part_hop;
     uint32_t *pk;                 // [seg][4]: 192 kHz |u| max L, R (float bits), native |x| L, R
 };
+// af_loudnorm's 192 kHz modes on one whole track (amx_loudnorm.hip)
+struct LnArgs {
+    int64_t n192;                 // 192 kHz frames
+    float *u;                     // [n192][2] the resampled stream (scratch)
+    double *ring;                 // limiter ring [40320][2] + 64 (scratch)
+    int16_t *y;                   // [n192][2] output
+    double *summary;              // [2]: 1 = the < 3 s linear fallback ran (then [1] = its offset)
+    const double *hops;           // [>= n192 / 19200][2] pass-1 hop energies of this stream
+    const double *peak;           // [2] pass-1 192 kHz sample peak per channel
+    const double *energies, *bounds;
+    double target_i, target_lra, target_tp;   // target_tp linear (the ceiling)
+    double measured_i, measured_thresh, offset;   // offset linear
+    double weights[21];           // init_gaussian_filter
+    double kb[5], ka[5];          // libebur128 K filter at 192 kHz (direct form)
+};
+hipError_t launch_loudnorm(const LnArgs &a, const uint32_t *x, int64_t n_in, int L, int M,
+                           const float *bank, hipStream_t st);
 hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent_t fork, hipEvent_t join);
 int swr_geometry(int in_rate, int out_rate, int *L, int *M);   // host (amx_plan.cpp)
 int swr_bank(int in_rate, int out_rate, float *bank);

@@ -233,6 +233,7 @@ struct amx_plan {
     int32_t *d_obase = nullptr, *d_oph = nullptr;
     int32_t *d_slow = nullptr;   // K segments k_up_edge takes (static path); n_slow of them
     int64_t n_slow = 0;
+    double kdf_b[5] = {0, 0, 0, 0, 0}, kdf_a[5] = {0, 0, 0, 0, 0};   // K filter, fused direct form (192 kHz)
     hipStream_t up_aux = nullptr;            // k_up_edge's stream, forked from / joined to the caller's
     hipEvent_t up_fork = nullptr, up_join = nullptr;
     double *d_qh = nullptr, *d_qt = nullptr;
@@ -492,6 +493,18 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             cd.kw2[k] = rb[k];
             cd.kw2[3 + k] = ra[k];
         }
+        // the fused direct form itself, for the one place that runs libebur128's filter
+        // sample by sample (loudnorm's r128_out, amx_loudnorm.hip)
+        p->kdf_b[0] = pb[0] * rb[0];
+        p->kdf_b[1] = pb[0] * rb[1] + pb[1] * rb[0];
+        p->kdf_b[2] = pb[0] * rb[2] + pb[1] * rb[1] + pb[2] * rb[0];
+        p->kdf_b[3] = pb[1] * rb[2] + pb[2] * rb[1];
+        p->kdf_b[4] = pb[2] * rb[2];
+        p->kdf_a[0] = pa[0] * ra[0];
+        p->kdf_a[1] = pa[0] * ra[1] + pa[1] * ra[0];
+        p->kdf_a[2] = pa[0] * ra[2] + pa[1] * ra[1] + pa[2] * ra[0];
+        p->kdf_a[3] = pa[1] * ra[2] + pa[2] * ra[1];
+        p->kdf_a[4] = pa[2] * ra[2];
     }
     // compressor tables (pydub compress_dynamic_range, exact C math == CPython math)
     std::vector<double> tabs;
@@ -722,7 +735,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     // the K-filter segment grid equals the chain's when there is no multiband
     // (output frames == input frames) and every chunk but a span's last is whole
     // segments long: k_front2 then does loudness pass 1 on the output it writes
-    p->fuse_kw = (!p->resamp && !p->mb && p->Lkw == p->L && p->n_kseg == p->n_seg) ? 1 : 0;
+    p->fuse_kw = (!p->resamp && !p->mb && p->Lkw == p->L && p->n_kseg == p->n_seg && !desc->measure_only) ? 1 : 0;
     for (int c = 0; c < n_chunks && p->fuse_kw; c++) {
         const bool span_last = (c == n_chunks - 1) || (chunks[c + 1].track != chunks[c].track);
         if (!span_last && (p->chunks[c].n % p->L) != 0) p->fuse_kw = 0;
@@ -1152,6 +1165,65 @@ int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, const int16_t *d_edge,
     int rc = amx_loudness_pass1_part(p, 0, d_out, d_edge, d_kw_tail, d_peak, d_ws, stream);
     if (rc) return rc;
     return amx_loudness_pass1_part(p, 1, d_out, d_edge, d_kw_tail, d_peak, d_ws, stream);
+}
+
+int amx_loudnorm_192k_size(const amx_plan *p, int32_t track, int64_t *frames, int64_t *ws_bytes) {
+    if (!p || !frames || !ws_bytes || track < 0 || track >= p->n_tracks) return fail(AMX_EINVAL, "bad argument");
+    if (!p->resamp || !p->up_ok)
+        return fail(AMX_ERANGE, "loudnorm's 192 kHz modes need an exact-rational 192 kHz resampler");
+    const SpanDev &sp = p->spans[track];
+    const int64_t n192 = (sp.out_n * p->upL + p->upM - 1) / p->upM;
+    *frames = n192;
+    *ws_bytes = ((n192 * 2 * (int64_t)sizeof(float) + 255) / 256) * 256 + (2 * 40320 + 64) * (int64_t)sizeof(double);
+    return AMX_OK;
+}
+
+int amx_loudnorm_192k(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const int16_t *d_out,
+                      const double *d_hops, int64_t max_hops, const double *d_peak, int16_t *d_y192,
+                      double *d_summary, void *d_ws2, void *stream) {
+    int64_t n192 = 0, wsb = 0;
+    if (int rc = amx_loudnorm_192k_size(p, track, &n192, &wsb)) return rc;
+    if (!d || !d_out || !d_hops || !d_peak || !d_y192 || !d_summary || !d_ws2)
+        return fail(AMX_EINVAL, "null argument");
+    const SpanDev &sp = p->spans[track];
+    if (sp.tframe0 != 0 || sp.ttotal != sp.out_n)
+        return fail(AMX_EINVAL, "loudnorm's 192 kHz modes run on whole tracks (one plan holds the track)");
+    if (max_hops < n192 / 19200 + 1) return fail(AMX_EINVAL, "d_hops holds %lld hops", (long long)max_hops);
+    amx::LnArgs a{};
+    a.n192 = n192;
+    a.u = reinterpret_cast<float *>(d_ws2);
+    a.ring = reinterpret_cast<double *>(reinterpret_cast<char *>(d_ws2) + ((n192 * 2 * (int64_t)sizeof(float) + 255) / 256) * 256);
+    a.y = d_y192;
+    a.summary = d_summary;
+    a.hops = d_hops + (int64_t)track * max_hops * 2;
+    a.peak = d_peak + (int64_t)track * 4;
+    a.energies = p->d_energies;
+    a.bounds = p->d_bounds;
+    // af_loudnorm init / config_input: dB options to the linear factors it keeps
+    a.target_i = d->target_i;
+    a.target_lra = d->target_lra;
+    a.target_tp = std::pow(10., d->target_tp / 20.);
+    a.measured_i = d->measured_i;
+    a.measured_thresh = d->measured_thresh;
+    a.offset = std::pow(10., d->offset / 20.);
+    {   // init_gaussian_filter
+        double total = 0.0;
+        const double sigma = 3.5;
+        const int off = 21 / 2;
+        const double c1 = 1.0 / (sigma * std::sqrt(2.0 * M_PI));
+        const double c2 = 2.0 * std::pow(sigma, 2.0);
+        for (int i = 0; i < 21; i++) {
+            const int x = i - off;
+            a.weights[i] = c1 * std::exp(-(std::pow(x, 2.0) / c2));
+            total += a.weights[i];
+        }
+        const double adjust = 1.0 / total;
+        for (int i = 0; i < 21; i++) a.weights[i] *= adjust;
+    }
+    for (int k = 0; k < 5; k++) { a.kb[k] = p->kdf_b[k]; a.ka[k] = p->kdf_a[k]; }
+    HIPCHK(amx::launch_loudnorm(a, reinterpret_cast<const uint32_t *>(d_out) + sp.out_off, sp.out_n, p->upL,
+                                p->upM, p->d_bank, (hipStream_t)stream));
+    return AMX_OK;
 }
 
 int amx_pcm_to_s16(const void *d_raw, int64_t frames, int32_t channels, int32_t format,

@@ -60,7 +60,10 @@ typedef struct amx_chain_desc {
     int32_t input_s16;            /* 0: d_in is float32 (quantised on device like ffmpeg's
                                      f32->s16 segment split, A.1); 1: d_in is int16 already
                                      (mono int16 is duplicated to stereo on the device) */
-    int32_t pad0_;
+    int32_t measure_only;         /* 1: the plan only measures / limits a track it is given in
+                                     d_out (amx_run_chunks is not called): loudness pass 1
+                                     then runs its own sample pass instead of the one
+                                     k_front2 fuses into the chain */
     /* analog character (:258-266), applied if analog_on */
     int32_t analog_on;
     float analog_drive;           /* float32(1 + 0.5*cf) */
@@ -220,6 +223,28 @@ AMX_API int amx_loudness_pass1(amx_plan *plan, const int16_t *d_out, const int16
 AMX_API int amx_loudness_pass1_part(amx_plan *plan, int32_t part, const int16_t *d_out,
                                     const int16_t *d_edge, double *d_kw_tail, double *d_peak,
                                     void *d_ws, void *stream);
+/* af_loudnorm's 192 kHz modes (FFmpeg af_loudnorm.c; restated in oracle/amx_oracle.c
+ * orc_loudnorm) on one whole track of the plan: the reference's pass 1 (:229) runs them
+ * with the measured_* defaults (its JSON target_offset = target_i - the integrated
+ * loudness of this output), and pass 2 (:240) runs them whenever the linear conditions
+ * fail ("dynamic mode": 3 s look-ahead AGC smoothed over 100 ms frames, true-peak
+ * limiter at target_tp, 192 kHz output).  A track shorter than 3 s takes af_loudnorm's
+ * linear fallback (still at 192 kHz).  Options in dB as the reference passes them. */
+typedef struct amx_loudnorm_desc {
+    double target_i, target_lra, target_tp;                     /* I, LRA, TP */
+    double measured_i, measured_lra, measured_tp, measured_thresh, offset;   /* pass 1: 0, 0, 99, -70, 0 */
+} amx_loudnorm_desc;
+/* output frames (ceil(frames * 192000 / fs)) and the d_ws2 bytes amx_loudnorm_192k needs */
+AMX_API int amx_loudnorm_192k_size(const amx_plan *plan, int32_t track, int64_t *frames, int64_t *ws_bytes);
+/* d_out: the plan's chain output (the track to normalise); d_hops / max_hops and d_peak:
+ * amx_loudness_pass2's hop energies and amx_loudness_pass1's peaks of the same plan (the
+ * 192 kHz stream's r128_in statistics); d_y192 [frames][2] s16: the output as the WAV
+ * muxer writes it (av_clip_int16(llrint(x * 32768))); d_summary [2] (1, offset when the
+ * < 3 s linear fallback ran, else 0, the final above_threshold). */
+AMX_API int amx_loudnorm_192k(amx_plan *plan, int32_t track, const amx_loudnorm_desc *desc,
+                              const int16_t *d_out, const double *d_hops, int64_t max_hops,
+                              const double *d_peak, int16_t *d_y192, double *d_summary, void *d_ws2,
+                              void *stream);
 /* Host helper for chunk-sharded tracks: out8 = A^frames * in8 (per channel 4x4 K-filter
  * transition at the measurement rate; frames of the measurement stream), so
  * carry(r+1) = A^{len_r} carry(r) + tail(r). */
