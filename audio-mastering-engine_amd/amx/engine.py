@@ -210,7 +210,7 @@ class MasteringJob:
         if getattr(self, "_j192", None) is None or self._j192[0] != key:
             job2 = MasteringJob(192000, 2, {"lufs": self.settings.get("lufs")}, [n192.value],
                                 input_s16=True, chunks=[(0, 0, n192.value)], device=self.device,
-                                measure_only=True)
+                                measure_only=True, seg_frames=1024)   # the K scan's window at 192 kHz
             ws2 = torch.empty(max(1, wsb.value), dtype=torch.uint8, device=self.device)
             summ = torch.zeros(2, dtype=torch.float64, device=self.device)
             self._j192 = (key, job2, ws2, summ)

@@ -831,7 +831,9 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             Gkw = kw.gemv_table(Lseg);
         }
         Mkw = matpow(kw.A, Lseg, AMX_KW_DIM);
-        p->lev_kw = kw.window_powers((int64_t)Lseg * AMX_SCAN_S, tol, 16, Mpkw);
+        // up to 32 block powers: a track measured at its own 192 kHz rate (loudnorm's
+        // output) needs ~20 with 128-frame segments (the 38 Hz pole)
+        p->lev_kw = kw.window_powers((int64_t)Lseg * AMX_SCAN_S, tol, 32, Mpkw);
         if (p->lev_kw < 0) {
             delete p;
             return fail(AMX_ERANGE, "K-weighting decays too slowly for %d-frame segments", Lseg);
