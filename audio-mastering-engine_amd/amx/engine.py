@@ -212,7 +212,7 @@ class MasteringJob:
                                 input_s16=True, chunks=[(0, 0, n192.value)], device=self.device,
                                 measure_only=True, seg_frames=1024)   # the K scan's window at 192 kHz
             ws2 = torch.empty(max(1, wsb.value), dtype=torch.uint8, device=self.device)
-            summ = torch.zeros(2, dtype=torch.float64, device=self.device)
+            summ = torch.zeros(16, dtype=torch.float64, device=self.device)
             self._j192 = (key, job2, ws2, summ)
         return n192.value, self._j192[1], self._j192[2], self._j192[3]
 
@@ -251,8 +251,12 @@ class MasteringJob:
         job2.dd.lufs_on = 0
         job2.decide(stream)
         job2.finalize(None, stream)
+        prof = summ.cpu().numpy()
         return job2.y[:n192], {"target_offset": target_offset, "pass1_output_i": i_out,
-                               "sample_rate": 192000}
+                               "sample_rate": 192000,
+                               "pass2_cycles": {k: float(prof[i]) for i, k in enumerate(
+                                   ("fill", "detect", "envelope", "output", "stats", "r128_out",
+                                    "detect_calls", "serial_chunks"), start=2)}}
 
     # ------------------------------------------------------------ report
     def fetch_report(self, raise_dynamic=True):

@@ -239,8 +239,10 @@ AMX_API int amx_loudnorm_192k_size(const amx_plan *plan, int32_t track, int64_t 
 /* d_out: the plan's chain output (the track to normalise); d_hops / max_hops and d_peak:
  * amx_loudness_pass2's hop energies and amx_loudness_pass1's peaks of the same plan (the
  * 192 kHz stream's r128_in statistics); d_y192 [frames][2] s16: the output as the WAV
- * muxer writes it (av_clip_int16(llrint(x * 32768))); d_summary [2] (1, offset when the
- * < 3 s linear fallback ran, else 0, the final above_threshold). */
+ * muxer writes it (av_clip_int16(llrint(x * 32768))); d_summary [16]: [0..1] = (1, offset)
+ * when the < 3 s linear fallback ran, else (0, the final above_threshold); [2..9] =
+ * device cycles in the ring fills, peak scans, envelopes, output, statistics and
+ * r128_out, then the peak-scan calls and their serial chunks (diagnostics). */
 AMX_API int amx_loudnorm_192k(amx_plan *plan, int32_t track, const amx_loudnorm_desc *desc,
                               const int16_t *d_out, const double *d_hops, int64_t max_hops,
                               const double *d_peak, int16_t *d_y192, double *d_summary, void *d_ws2,
