@@ -25,7 +25,9 @@ from .settings import ALIMITER, LOUDNORM_LRA, LOUDNORM_TP
 
 
 class DynamicModeUnsupported(NotImplementedError):
-    """loudnorm would run in dynamic mode (192 kHz AGC); SURVEY.md §8f row 1."""
+    """loudnorm takes dynamic mode (192 kHz AGC) on a path that only finalises linear
+    tracks (the captured-graph step, the pipelined TrackStream, chunk-sharded N > 1):
+    master_audio / master_array run it through MasteringJob.dynamic_track."""
 
 
 def final_desc(params=ALIMITER):
@@ -276,8 +278,8 @@ class MasteringJob:
                               "input_lra": loudness._fmt(row[6]), "input_thresh": loudness._fmt(row[7])})
             if mode == "dynamic" and raise_dynamic:
                 raise DynamicModeUnsupported(
-                    "loudnorm would use dynamic mode for these measurements %s; only linear "
-                    "mode is implemented (DESIGN.md: next rows)" % (stats[-1],))
+                    "loudnorm takes dynamic mode for these measurements %s: finish the track "
+                    "with dynamic_track() (master_audio / master_array do)" % (stats[-1],))
         self.report.update({"stats": stats if self.dd.lufs_on else None, "modes": modes,
                             "gains": gains, "limiter_fast": all(fast)})
         return self.report
@@ -341,6 +343,13 @@ def master_array(x, sample_rate, settings, *, quantum=None, seg_frames=128, limi
                        input_s16=s16, seg_frames=seg_frames, limiter_seg_frames=limiter_seg_frames,
                        limiter_warm_frames=limiter_warm_frames)
     y = job.run(x)
-    job.fetch_report()
+    rep = job.fetch_report(raise_dynamic=False)
+    if rep["modes"] and rep["modes"][0] == "dynamic":
+        # loudnorm pass 2 in dynamic mode (:240): the 192 kHz path replaces the linear
+        # step's output (run() finalised the track without a gain; it is recomputed here)
+        y, info = job.dynamic_track(0, rep["stats"][0])
+        job.report.update(dynamic=info, sample_rate=info["sample_rate"])
+    else:
+        job.report["sample_rate"] = job.fs
     job.report["job"] = job
     return y, job.report

@@ -31,8 +31,9 @@ def test_struct_sizes_match_header():
     src = r'''
 #include <stdio.h>
 #include "amx.h"
-int main(){printf("%zu %zu %zu %zu %zu\n", sizeof(amx_chain_desc), sizeof(amx_chunk),
-  sizeof(amx_final_desc), sizeof(amx_plan_info), sizeof(amx_track_span));return 0;}'''
+int main(){printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(amx_chain_desc), sizeof(amx_chunk),
+  sizeof(amx_final_desc), sizeof(amx_plan_info), sizeof(amx_track_span),
+  sizeof(amx_decide_desc), sizeof(amx_loudnorm_desc));return 0;}'''
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "p.c")
         open(c, "w").write(src)
@@ -41,7 +42,8 @@ int main(){printf("%zu %zu %zu %zu %zu\n", sizeof(amx_chain_desc), sizeof(amx_ch
         sizes = [int(v) for v in subprocess.run([exe], capture_output=True, text=True).stdout.split()]
     assert sizes == [ctypes.sizeof(capi.ChainDesc), ctypes.sizeof(capi.Chunk),
                      ctypes.sizeof(capi.FinalDesc), ctypes.sizeof(capi.PlanInfo),
-                     ctypes.sizeof(capi.TrackSpan)]
+                     ctypes.sizeof(capi.TrackSpan), ctypes.sizeof(capi.DecideDesc),
+                     ctypes.sizeof(capi.LoudnormDesc)]
 
 
 def test_design_uses_reference_coefficients():
