@@ -47,6 +47,9 @@ namespace amx {
 #ifndef AMX_UP_SB
 #define AMX_UP_SB 6        // sched_barrier mask: VALU + SALU may cross, scalar loads may not
 #endif
+#ifndef UP_DOT
+#define UP_DOT up_dot2      // packed-pair form of the fast kernel's dot products
+#endif
 #ifndef AMX_UP_WAVES
 #define AMX_UP_WAVES 4     // waves per SIMD the register budget must allow
 #endif
@@ -75,6 +78,25 @@ __device__ __forceinline__ uint32_t up_word(const uint32_t *__restrict__ x,
     return n > 0 ? x[sp.out_off + up_reflect(g, n)] : 0u;
 }
 
+typedef float up_f2 __attribute__((ext_vector_type(2)));
+
+// the FMA3 kernel's order with the 8 chains as 4 packed pairs (v_pk_fma_f32 / v_pk_add_f32):
+// the same operations, lane by lane, as up_dot
+__device__ __forceinline__ float up_dot2(const float *w, const float *__restrict__ h) {
+    up_f2 a[4];
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {
+        up_f2 acc = up_f2{w[k], w[k + 1]} * up_f2{h[k], h[k + 1]};
+        acc = __builtin_elementwise_fma(up_f2{w[k + 8], w[k + 9]}, up_f2{h[k + 8], h[k + 9]}, acc);
+        acc = __builtin_elementwise_fma(up_f2{w[k + 16], w[k + 17]}, up_f2{h[k + 16], h[k + 17]}, acc);
+        acc = __builtin_elementwise_fma(up_f2{w[k + 24], w[k + 25]}, up_f2{h[k + 24], h[k + 25]}, acc);
+        a[k >> 1] = acc;
+    }
+    const up_f2 b01 = a[0] + a[2], b23 = a[1] + a[3];     // (a0+a4, a1+a5), (a2+a6, a3+a7)
+    const up_f2 c = b01 + b23;                            // (b0+b2, b1+b3)
+    return c.x + c.y;
+}
+
 // the FMA3 kernel's order
 __device__ __forceinline__ float up_dot(const float *w, const float *__restrict__ h) {
     float a[8];
@@ -88,6 +110,15 @@ __device__ __forceinline__ float up_dot(const float *w, const float *__restrict_
     }
     const float b0 = a[0] + a[4], b1 = a[1] + a[5], b2 = a[2] + a[6], b3 = a[3] + a[7];
     return (b0 + b2) + (b1 + b3);
+}
+
+// libebur128's second K section, the RLB high-pass: b = (1, -2, 1) always, so the
+// DF-II-T step is bq_step's arithmetic without its two unit multiplies (same values)
+__device__ __forceinline__ double hp_step(const double *q, double &z0, double &z1, double x) {
+    const double y = x + z0;
+    z0 = fma(-q[3], y, fma(-2.0, x, z1));
+    z1 = fma(-q[4], y, x);
+    return y;
 }
 
 // ------------------------------------------------------------ accumulator
@@ -107,7 +138,7 @@ struct UpAcc {
         const double *r = wc + (int64_t)n * AMX_KW_DIM;              // wave-uniform row
         if constexpr (FAST) {
             const double a = bq_step(c1, v[0], v[1], ud);
-            const double y = bq_step(c2, v[2], v[3], a);
+            const double y = hp_step(c2, v[2], v[3], a);
             z0 = fma(y, y, z0);
 #pragma unroll
             for (int d = 0; d < 4; d++) q0[d] = fma(y, r[d], q0[d]);
@@ -116,7 +147,7 @@ struct UpAcc {
         } else {
             const double w0 = v[0], w1 = v[1], w2 = v[2], w3 = v[3];
             const double a = bq_step(c1, v[0], v[1], ud);
-            double y = bq_step(c2, v[2], v[3], a);
+            double y = hp_step(c2, v[2], v[3], a);
             const bool in = n < len;              // past a partial segment's end: state held
             v[0] = in ? v[0] : w0; v[1] = in ? v[1] : w1;
             v[2] = in ? v[2] : w2; v[3] = in ? v[3] : w3;
@@ -179,7 +210,7 @@ __device__ __forceinline__ void up_run_fast(const UpArgs &a, const SpanDev &sp, 
 #pragma unroll
             for (int ph = 1; ph < STATIC; ph++) {
                 __builtin_amdgcn_sched_barrier(AMX_UP_SB);
-                acc.add(n0 + ph, up_dot(w + kb, bk + ph * UP_TAPS), w[kb + UP_C]);
+                acc.add(n0 + ph, UP_DOT(w + kb, bk + ph * UP_TAPS), w[kb + UP_C]);
             }
         }
         __builtin_amdgcn_sched_barrier(AMX_UP_SB);
@@ -348,10 +379,10 @@ __global__ void __launch_bounds__(64) k_up_edge(UpArgs a) {
             for (int k = 0; k < 8; k++) ub[k] = us[2 * (n + k) + ch];
 #pragma unroll
             for (int k = 0; k < 8; k++)
-                ys[2 * (n + k) + ch] = bq_step(c2, v[2], v[3], bq_step(c1, v[0], v[1], (double)ub[k]));
+                ys[2 * (n + k) + ch] = hp_step(c2, v[2], v[3], bq_step(c1, v[0], v[1], (double)ub[k]));
         }
         for (; n < len; n++)
-            ys[2 * n + ch] = bq_step(c2, v[2], v[3], bq_step(c1, v[0], v[1], (double)us[2 * n + ch]));
+            ys[2 * n + ch] = hp_step(c2, v[2], v[3], bq_step(c1, v[0], v[1], (double)us[2 * n + ch]));
         for (; n < a.Lout; n++) ys[2 * n + ch] = 0.0;
         double *o = a.e + (j * 2 + ch) * AMX_KW_DIM;
 #pragma unroll
