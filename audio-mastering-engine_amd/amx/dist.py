@@ -442,3 +442,13 @@ class ShardedBatch:
 
     def replay(self):
         return self.job.replay()
+
+    def finish_dynamic(self):
+        """After a step: finish this rank's tracks that loudnorm sends to dynamic mode
+        (MasteringJob.finish_dynamic); returns {global track index: info}."""
+        info = self.job.finish_dynamic()
+        return {self.tracks[t]: v for t, v in info.items()}
+
+    def track_output(self, k):
+        """global track k's output (192 kHz after finish_dynamic if it took dynamic mode)"""
+        return self.job.track_output(self.tracks.index(k))

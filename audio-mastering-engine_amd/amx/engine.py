@@ -26,8 +26,9 @@ from .settings import ALIMITER, LOUDNORM_LRA, LOUDNORM_TP
 
 class DynamicModeUnsupported(NotImplementedError):
     """loudnorm takes dynamic mode (192 kHz AGC) on a path that only finalises linear
-    tracks (the captured-graph step, the pipelined TrackStream, chunk-sharded N > 1):
-    master_audio / master_array run it through MasteringJob.dynamic_track."""
+    tracks (chunk-sharded N > 1, or TrackStream.run without ``dynamic=``): master_audio /
+    master_array, MasteringJob.finish_dynamic, ShardedBatch.finish_dynamic and
+    TrackStream.run(dynamic={}) run it through MasteringJob.dynamic_track."""
 
 
 def final_desc(params=ALIMITER):
@@ -320,7 +321,23 @@ class MasteringJob:
         self._graph.replay()
         return self.y[:self.info.out_frames]
 
+    def finish_dynamic(self, report=None):
+        """After a step of whole tracks: every track loudnorm sends to dynamic mode is
+        finished by dynamic_track (its 192 kHz output replaces the slot the step wrote);
+        returns {track: info}."""
+        rep = report if report is not None else self.fetch_report(raise_dynamic=False)
+        self.dyn_out = {}
+        for t, mode in enumerate(rep["modes"]):
+            if mode == "dynamic":
+                y, info = self.dynamic_track(t, rep["stats"][t])
+                self.dyn_out[t] = (y.clone(), info)
+        return {t: v[1] for t, v in self.dyn_out.items()}
+
     def track_output(self, t):
+        """track t's output: its slot of y, or its 192 kHz output after finish_dynamic"""
+        dyn = getattr(self, "dyn_out", None)
+        if dyn and t in dyn:
+            return dyn[t][0]
         s = self.spans[t]
         return self.y[s.out_offset:s.out_offset + s.out_frames]
 

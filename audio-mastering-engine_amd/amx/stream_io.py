@@ -59,9 +59,15 @@ class TrackStream:
     def pinned_stats(self):
         return torch.empty(self.jobs[0].stats.shape, dtype=torch.float64).pin_memory()
 
-    def run(self, h_ins, h_outs, h_stats=None):
+    def run(self, h_ins, h_outs, h_stats=None, dynamic=None):
         """Master every pinned input in ``h_ins`` into the pinned output at the same index
-        (and its loudnorm statistics row into ``h_stats``); returns when all are done."""
+        (and its loudnorm statistics row into ``h_stats``); returns when all are done.
+
+        A track loudnorm sends to dynamic mode has a 192 kHz output that does not fit its
+        48 kHz slot: with ``dynamic=None`` that raises DynamicModeUnsupported; with a dict,
+        each such track is stepped again after the pipeline drains and finished by
+        MasteringJob.dynamic_track, and ``dynamic[i] = (int16 [n192, 2] host tensor, info)``
+        (its ``h_outs[i]`` is left as the linear path wrote it)."""
         if len(h_outs) != len(h_ins) or (h_stats is not None and len(h_stats) != len(h_ins)):
             raise ValueError("h_ins, h_outs (and h_stats) must have the same length")
         for h in h_ins:
@@ -109,8 +115,15 @@ class TrackStream:
         torch.cuda.synchronize()
         # the device decided each track's loudnorm mode; a track that needs dynamic mode
         # must not pass as mastered (its gain would silently be "none")
-        for i, r in enumerate(h_stats):
-            if int(r.reshape(-1, r.shape[-1])[:, 8].max()) == 3:
-                from .engine import DynamicModeUnsupported
-                raise DynamicModeUnsupported("track %d: loudnorm would use dynamic mode" % i)
+        dyn = [i for i, r in enumerate(h_stats) if int(r.reshape(-1, r.shape[-1])[:, 8].max()) == 3]
+        if dyn and dynamic is None:
+            from .engine import DynamicModeUnsupported
+            raise DynamicModeUnsupported("track %d: loudnorm would use dynamic mode" % dyn[0])
+        for i in dyn:
+            job = self.jobs[0]
+            self.d_in[0].copy_(h_ins[i])
+            job.replay()
+            rep = job.fetch_report(raise_dynamic=False)
+            y, info = job.dynamic_track(0, rep["stats"][0])
+            dynamic[i] = (y.cpu(), info)
         return h_outs

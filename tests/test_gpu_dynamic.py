@@ -95,3 +95,77 @@ def test_master_audio_dynamic(gpu, oracle_mod, seconds, intro):
     assert rinfo["mode"] == "dynamic", rinfo.get("stats")
     assert info.sample_rate == 192000 == rinfo["sample_rate"]
     _cmp(y, ref, "master_audio dynamic %.1f s intro %.1f" % (seconds, intro))
+
+
+def test_batch_linear_and_dynamic(gpu, oracle_mod):
+    """one plan, two whole tracks (a C4-style batch): one stays linear, one takes dynamic
+    mode; finish_dynamic replaces the dynamic track's slot with its 192 kHz output"""
+    import torch
+    from amx import synth
+    from amx.chunking import chunk_bounds
+    from amx.engine import MasteringJob
+    fs = 48000
+    settings = dict(mid_cut=2.0, lufs=-16.0)
+    xa = synth.mix_like(fs * 10, fs, 2, seed=21)
+    xb = _dynamic_signal(9.0, fs, 22)
+    job = MasteringJob(fs, 2, settings, [xa.shape[0], xb.shape[0]], quantum=512)
+    d_in = torch.from_numpy(np.ascontiguousarray(np.concatenate([xa, xb]))).cuda()
+    job.run(d_in)
+    rep = job.fetch_report(raise_dynamic=False)
+    assert rep["modes"] == ["linear", "dynamic"], rep["modes"]
+    info = job.finish_dynamic(rep)
+    assert list(info) == [1] and info[1]["sample_rate"] == 192000
+    for t, x in enumerate((xa, xb)):
+        x16 = oracle_mod.quantize(x)
+        ref, rinfo = oracle_mod.pipeline(x16, fs, settings, chunk_bounds(x16.shape[0], fs, 512))
+        _cmp(job.track_output(t).cpu().numpy(), ref, "batch track %d (%s)" % (t, rinfo["mode"]))
+
+
+def test_trackstream_dynamic(gpu, oracle_mod):
+    """pipelined TrackStream: a dynamic track raises by default; with dynamic={} it is
+    stepped again and finished at 192 kHz, the linear tracks keep their slots"""
+    import torch
+    from amx import synth
+    from amx.chunking import chunk_bounds
+    from amx.engine import DynamicModeUnsupported
+    from amx.stream_io import TrackStream
+    fs, n = 48000, 48000 * 6
+    settings = dict(bass_boost=1.0, lufs=-14.0)
+    xs = [synth.mix_like(n, fs, 2, seed=31), _dynamic_signal(6.0, fs, 32), synth.mix_like(n, fs, 2, seed=33)]
+    ts = TrackStream(fs, 2, settings, n, depth=2, quantum=512)
+    h_ins = [ts.pinned_input().copy_(torch.from_numpy(x)) for x in xs]
+    h_outs = [ts.pinned_output() for _ in xs]
+    with pytest.raises(DynamicModeUnsupported):
+        ts.run(h_ins, h_outs)
+    dyn = {}
+    ts.run(h_ins, h_outs, dynamic=dyn)
+    assert list(dyn) == [1] and dyn[1][1]["sample_rate"] == 192000
+    for i, x in enumerate(xs):
+        x16 = oracle_mod.quantize(x)
+        ref, rinfo = oracle_mod.pipeline(x16, fs, settings, chunk_bounds(n, fs, 512))
+        y = dyn[i][0] if i in dyn else h_outs[i]
+        _cmp(y.numpy(), ref, "TrackStream track %d (%s)" % (i, rinfo["mode"]))
+
+
+def test_sharded_batch_dynamic(gpu, oracle_mod):
+    """ShardedBatch (C4 share, rank 0 of 2): finish_dynamic after the step, outputs by
+    global track index"""
+    import torch
+    from amx import synth
+    from amx.chunking import chunk_bounds
+    from amx.dist import ShardedBatch
+    fs = 48000
+    settings = dict(bass_boost=1.0, lufs=-14.0)
+    xs = [_dynamic_signal(5.0, fs, 41), synth.mix_like(fs * 4, fs, 2, seed=42),
+          synth.mix_like(fs * 9, fs, 2, seed=43)]
+    frames = [x.shape[0] for x in xs]
+    b = ShardedBatch(fs, 2, settings, frames, rank=0, world=2, quantum=512)
+    mine = [xs[k] for k in b.tracks]
+    d_in = torch.from_numpy(np.ascontiguousarray(np.concatenate(mine))).cuda()
+    b.step(d_in)
+    info = b.finish_dynamic()
+    assert 0 in b.tracks and list(info) == [0]
+    for k in b.tracks:
+        x16 = oracle_mod.quantize(xs[k])
+        ref, rinfo = oracle_mod.pipeline(x16, fs, settings, chunk_bounds(frames[k], fs, 512))
+        _cmp(b.track_output(k).cpu().numpy(), ref, "ShardedBatch track %d (%s)" % (k, rinfo["mode"]))
