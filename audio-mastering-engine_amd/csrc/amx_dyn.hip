@@ -47,6 +47,31 @@ typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 #define AMX_RMS_F 4096
 #define AMX_RMS_MAXLOOK 1024
 #define AMX_RMS_LOOKPAD 1024
+
+// LDS index of prefix slot k: one spare slot per 80 keeps the scan's stores (lane
+// stride 20 slots, 16-lane ds_write_b64 groups) on 16 distinct bank pairs
+__device__ __forceinline__ int rms_slot(int k) { return k + k / 80; }
+
+// audioop.rms's (unsigned) sqrt((double) S / cnt), S = the window's exact sum of
+// squares (< 2^53, so the reference's double sum is exact), cnt the samples present.
+// That value is max{k : k^2 cnt <= S}: with S, cnt integers, S/cnt just below k^2 is
+// at least 1/cnt >= 2^-11 below it, far more than the double ulp at k^2 <= 2^30
+// (2^-22), so the division cannot round up onto k^2, and then sqrt stays below k
+// (by >= 1/(2 k cnt) >> ulp(k)); S/cnt >= k^2 gives sqrt >= k by monotone rounding.
+// So a float estimate (within 0.01 of sqrt(S/cnt)) corrected by one exact integer test
+// gives the same r without the double division and square root.  rc ~ 1/cnt.
+__device__ __forceinline__ uint32_t rms_floor(uint64_t S, uint32_t cnt, double rc) {
+    // S < 2^44 and k^2 cnt < 2^53: the double forms below are exact integers
+    const double sd = fma((double)(uint32_t)(S >> 32), 4294967296.0, (double)(uint32_t)S);
+    const double cd = (double)cnt;
+    const uint32_t k = (uint32_t)__builtin_amdgcn_sqrtf((float)(sd * rc));
+    const uint32_t k1 = k + 1;
+    const bool up = (double)__umul24(k1, k1) * cd <= sd;
+    const bool down = (double)__umul24(k, k) * cd > sd;
+    const uint32_t r = k + (uint32_t)up - (uint32_t)(down & !up);
+    return cnt ? (r > 32768u ? 32768u : r) : 0u;
+}
+
 __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ cdp,
                                                    const ChunkDev *__restrict__ chunks,
                                                    const uint32_t *__restrict__ bands,
@@ -54,8 +79,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
     constexpr int N = AMX_RMS_F + AMX_RMS_LOOKPAD;
     constexpr int PER = N / AMX_BLOCK;                 // 20 slots per thread
     constexpr int VEC = PER / 4;                       // as 5 16-B loads
-    __shared__ long long P[N];
-    __shared__ long long wsum[AMX_BLOCK / 64];
+    __shared__ unsigned long long P[N + N / 80];
+    __shared__ unsigned long long wsum[AMX_BLOCK / 64];
     const int look = cdp->look;
     const int c = blockIdx.y, b = blockIdx.z;
     const ChunkDev ch = chunks[c];
@@ -67,50 +92,78 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
     // LDS slot k holds frame base - LOOKPAD + k
     const int64_t f0 = base - AMX_RMS_LOOKPAD;
     const int t = threadIdx.x;
-    long long v[PER];
+    // a0^2 + a1^2 <= 2^31: one frame's squares fit a u32
+    uint32_t v[PER];
+    if (f0 >= 0 && f0 + N <= ch.n) {                   // block-uniform: no frame masks
 #pragma unroll
-    for (int q = 0; q < VEC; q++) {
-        const int64_t f = f0 + t * PER + 4 * q;
-        const bool ok = f >= 0 && f < rowlen;
-        const u4v u = *reinterpret_cast<const u4v *>(x + (ok ? f : 0));
+        for (int q = 0; q < VEC; q++) {
+            const u4v u = *reinterpret_cast<const u4v *>(x + f0 + t * PER + 4 * q);
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const long long a0 = lo16(u[e]), a1 = hi16(u[e]);
-            v[4 * q + e] = (ok && f + e < ch.n) ? a0 * a0 + a1 * a1 : 0;
+            for (int e = 0; e < 4; e++) {
+                const int32_t a0 = lo16(u[e]), a1 = hi16(u[e]);
+                v[4 * q + e] = (uint32_t)(a0 * a0) + (uint32_t)(a1 * a1);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < VEC; q++) {
+            const int64_t f = f0 + t * PER + 4 * q;
+            const bool ok = f >= 0 && f < rowlen;
+            const u4v u = *reinterpret_cast<const u4v *>(x + (ok ? f : 0));
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int32_t a0 = lo16(u[e]), a1 = hi16(u[e]);
+                v[4 * q + e] = (ok && f + e < ch.n) ? (uint32_t)(a0 * a0) + (uint32_t)(a1 * a1) : 0u;
+            }
         }
     }
-    // block inclusive scan: per-thread serial, wave scan of totals, cross-wave
-    long long run = 0;
+    // block inclusive scan: per-thread total, wave scan of totals, cross-wave
+    unsigned long long run = 0;
 #pragma unroll
-    for (int q = 0; q < PER; q++) { run += v[q]; v[q] = run; }
-    long long incl = run;
+    for (int q = 0; q < PER; q++) run += v[q];
+    unsigned long long incl = run;
     const int lane = t & 63, w = t >> 6;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const long long up = __shfl_up(incl, o);
+        const unsigned long long up = __shfl_up(incl, o);
         if (lane >= o) incl += up;
     }
     if (lane == 63) wsum[w] = incl;
     __syncthreads();
-    long long wpre = 0;
-    for (int q = 0; q < w; q++) wpre += wsum[q];
-    const long long excl = wpre + incl - run;
+    unsigned long long p = incl - run;
+    for (int q = 0; q < w; q++) p += wsum[q];
+    const int s0 = rms_slot(t * PER);                  // the thread's 20 slots share one pad
 #pragma unroll
-    for (int q = 0; q < PER; q++) P[t * PER + q] = excl + v[q];
+    for (int q = 0; q < PER; q++) { p += v[q]; P[s0 + q] = p; }
     __syncthreads();
     // frame i = base + nn uses slots [nn + LOOKPAD - look, nn + LOOKPAD)
     constexpr int OUT = AMX_RMS_F / AMX_BLOCK;
-#pragma unroll
-    for (int k = 0; k < OUT; k++) {
-        const int nn = t + k * AMX_BLOCK;
+    const uint32_t cfull = 2u * (uint32_t)look;
+    const double rfull = 1.0 / (double)cfull;
+    const bool whole = base >= look && base + AMX_RMS_F <= ch.n;   // block-uniform
+    auto rms_at = [&](int k) -> uint32_t {
+        const uint32_t nn = (uint32_t)t + (uint32_t)k * AMX_BLOCK;
+        const uint32_t e1 = nn + (AMX_RMS_LOOKPAD - 1), e0 = e1 - (uint32_t)look;
+        // e / 80 for e < 2^13 as (e * 52429) >> 22
+        const uint64_t S = P[e1 + (__umul24(e1, 52429u) >> 22)] - P[e0 + (__umul24(e0, 52429u) >> 22)];
+        if (whole) return rms_floor(S, cfull, rfull);
         const int64_t i = base + nn;
-        const int64_t wlo = i - look < 0 ? 0 : i - look;
-        const int64_t cnt = 2 * (i - wlo);
-        const long long S = P[nn + AMX_RMS_LOOKPAD - 1] - P[nn + AMX_RMS_LOOKPAD - 1 - look];
-        const uint32_t rms = cnt ? (uint32_t)sqrt((double)S / (double)cnt) : 0u;
-        // |sample| <= 32768; the row's tail past the chunk (to the 16-frame boundary)
-        // gets r = 0, m = 0: k_env0 feeds a chunk's partial last tile without masking
-        if (i < rowlen) mo[i] = i < ch.n ? (uint16_t)(rms > 32768u ? 32768u : rms) : (uint16_t)0;
+        const bool head = i < look;                    // a chunk's first look frames
+        const uint32_t cnt = head ? 2u * (uint32_t)i : cfull;
+        return rms_floor(S, cnt, head ? 1.0 / (double)cnt : rfull);
+    };
+    if (whole) {
+#pragma unroll
+        for (int k = 0; k < OUT; k++) mo[base + t + k * AMX_BLOCK] = (uint16_t)rms_at(k);
+    } else {
+#pragma unroll
+        for (int k = 0; k < OUT; k++) {
+            const int64_t i = base + t + k * AMX_BLOCK;
+            const uint32_t rms = rms_at(k);
+            // the row's tail past the chunk (to the 16-frame boundary) gets r = 0, m = 0:
+            // k_env0 feeds a chunk's partial last tile without masking
+            if (i < rowlen) mo[i] = i < ch.n ? (uint16_t)rms : (uint16_t)0;
+        }
     }
 }
 

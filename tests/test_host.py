@@ -160,3 +160,27 @@ int64_t check(const double *x, int64_t n, double b) {
         for b in (5.0 * (fs / 1000.0), 50.0 * (fs / 1000.0)):
             assert lib.check(x.ctypes.data, x.size, b) == 0, (fs, b)
     assert lib.check(x.ctypes.data, x.size, 20.0) == 0
+
+
+def test_rms_integer_form_matches_audioop():
+    """k_rms forms audioop.rms's (unsigned) sqrt((double) S / cnt) as max{k : k^2 cnt <= S}
+    from a float estimate plus one exact test (amx_dyn.hip rms_floor).  Check the identity
+    and the estimate's +-1 correction on the worst cases: S at and one below k^2 cnt, for
+    every window size the compressor uses (cnt = 2 * frames, 5 ms at 8 .. 192 kHz) and
+    the head of a chunk (cnt = 2 .. 2 look)."""
+    import math
+    rng = np.random.default_rng(0)
+    cnts = sorted({2 * i for i in range(1, 1025, 7)} | {80, 441 * 2, 480, 960, 2048})
+    for cnt in cnts:
+        ks = np.unique(np.concatenate([np.arange(0, 64), rng.integers(0, 32769, 200), [32767, 32768]]))
+        for k in ks.tolist():
+            for S in {k * k * cnt - 1, k * k * cnt, k * k * cnt + 1, (k + 1) * (k + 1) * cnt - 1}:
+                if S < 0 or S > cnt * 2 ** 30:
+                    continue
+                ref = int(math.sqrt(S / cnt))
+                assert max(0, math.isqrt(S // cnt)) == ref, (S, cnt)
+                est = int(np.sqrt(np.float32(float(S) * (1.0 / cnt))))
+                r = est + (1 if (est + 1) ** 2 * cnt <= S else 0)
+                if not (est + 1) ** 2 * cnt <= S and est * est * cnt > S:
+                    r = est - 1
+                assert min(r, 32768) == ref, (S, cnt, est)
