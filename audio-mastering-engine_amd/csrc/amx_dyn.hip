@@ -242,10 +242,17 @@ __device__ __forceinline__ double exp10_gain(const double *__restrict__ E, doubl
 // -att / 20 is the IEEE quotient, formed by reciprocal multiply + one FMA residual
 // step (Markstein: exact for a correctly rounded 1/20; tests/test_host.py checks it
 // against division on random attenuations).
-__device__ __forceinline__ uint32_t gain_frame(const ChainDev &cd, uint32_t v, double att) {
+__device__ __forceinline__ double gain_factor(const ChainDev &cd, double att) {
     const double q = -att * cd.exc[15];
-    const double f = exp10_gain(cd.exc, fma(fma(-q, 20.0, -att), cd.exc[15], q));
+    return exp10_gain(cd.exc, fma(fma(-q, 20.0, -att), cd.exc[15], q));
+}
+
+__device__ __forceinline__ uint32_t gain_apply(uint32_t v, double f) {
     return pack2((int16_t)mul16(lo16(v), f), (int16_t)mul16(hi16(v), f));
+}
+
+__device__ __forceinline__ uint32_t gain_frame(const ChainDev &cd, uint32_t v, double att) {
+    return gain_apply(v, gain_factor(cd, att));
 }
 
 #define AMX_ENV_TF_ 16   // checkpoint spacing (frames)
@@ -759,16 +766,22 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
         }
         __builtin_amdgcn_wave_barrier();
         double att = i0 < n ? ck[(b * nloc + ch.loc_off + i0) / AMX_ENV_TF_] : 0.0;
-        // a wave whose 1024 frames of this band start at att = 0 and have m = 0
-        // throughout holds att = 0: every frame passes unchanged (the reference's
-        // "att != 0" test), so the envelope steps and gains are skipped
-        bool busy = att != 0.0;
+        // m = 0 on every frame of the wave (below the threshold) holds each lane's att,
+        // so its gain is one value: formed once instead of per frame.  With att = 0 as
+        // well every frame passes unchanged (the reference's "att != 0" test)
+        bool loud = false;
 #pragma unroll
-        for (int f = 0; f < AMX_ENV_TF_; f++) busy = busy || mv[f] != 0.0;
+        for (int f = 0; f < AMX_ENV_TF_; f++) loud = loud || mv[f] != 0.0;
         uint32_t gv[AMX_ENV_TF_];
-        if (__ballot(busy) == 0) {
+        if (__ballot(loud) == 0) {
+            if (__ballot(att != 0.0) == 0) {
 #pragma unroll
-            for (int f = 0; f < AMX_ENV_TF_; f++) gv[f] = xv[f];
+                for (int f = 0; f < AMX_ENV_TF_; f++) gv[f] = xv[f];
+            } else {
+                const double g = gain_factor(cd, att);
+#pragma unroll
+                for (int f = 0; f < AMX_ENV_TF_; f++) gv[f] = gain_apply(xv[f], g);
+            }
         } else {
 #pragma unroll
             for (int f = 0; f < AMX_ENV_TF_; f++) {

@@ -353,6 +353,8 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     const int fs = desc->sample_rate;
     if (desc->env_warm_frames >= 0) p->warm = (desc->env_warm_frames + 127) / 128 * 128;   // whole ring of k_env0 tiles
     if (desc->env_rounds >= 0) p->rounds = desc->env_rounds;
+    if (const char *ev = std::getenv("AMX_ENV_LE"))      // (measurements only)
+        p->Le = std::max(128, std::atoi(ev) / 128 * 128);
     if (p->rounds > AMX_ENV_MAX_ROUNDS) {
         delete p;
         return fail(AMX_EINVAL, "env_rounds %d > %d", desc->env_rounds, AMX_ENV_MAX_ROUNDS);

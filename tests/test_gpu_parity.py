@@ -78,17 +78,22 @@ def test_multichunk_chain_vs_oracle(gpu, oracle_mod, fs, settings, seconds, seg_
 
 
 @pytest.mark.parametrize("warm,rounds", [(0, 0), (0, 1), (64, 2), (-1, -1)])
-@pytest.mark.parametrize("signal", ["music", "mix"])
+@pytest.mark.parametrize("signal", ["music", "mix", "held"])
 def test_compressor_fixup_paths(gpu, oracle_mod, warm, rounds, signal):
     """The envelope is exact however the work is split between speculation, the
     parallel fix-up rounds and the in-order walk (amx_dyn.hip): warm-up 0 and no
     rounds leaves everything to the walk; the music signal has long held-state
-    (below-threshold) stretches between loud passages."""
+    (below-threshold) stretches between loud passages; "held" drops to -60 dB after
+    2 s, so every band holds a non-zero attenuation over whole waves (the overlay's
+    one-gain-per-lane path)."""
     from amx import synth
     fs = 48000
     n = int(fs * 9.7)
     if signal == "music":
         x = synth.music_like(n, fs, 2, seed=7, peak_dbfs=-3.0)
+    elif signal == "held":
+        x = synth.music_like(n, fs, 2, seed=9, peak_dbfs=-1.0)
+        x[2 * fs:] *= 1e-3
     else:
         x = synth.mix_like(n, fs, 2, seed=7)
     x16 = oracle_mod.quantize(x)
