@@ -374,7 +374,7 @@ __device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, double
                                           const uint16_t *const (&irow)[4], const double *mt, int q,
                                           int ntile, int nwarm, int64_t start, int64_t end,
                                           double *ckr, double &att, double &s_spec, bool &any) {
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     // stage tile q's m (gathered two tiles ago)
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -425,8 +425,15 @@ __device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, double
     }
 }
 
+// Launch: W = 1, 2 or 4 waves per workgroup (a workgroup's waves go to
+// distinct SIMDs) with enough dynamic LDS that a CU holds one workgroup, and no more
+// workgroups than CUs.  The staging (gathers, LDS) is the CU's shared path, so a step
+// costs about W times the single-wave cost; the plan picks Le so that all segments fit
+// one resident wave set, which also shrinks the warm-up share (W + Le) / Le.
+#define AMX_ENV_WG 4
+#define AMX_ENV_LDS_PIN (48 * 1024)      // + 36 KB static: > 80 KB, one workgroup per CU
 template <bool RCP>
-__global__ void __launch_bounds__(64) k_env0(const ChainDev *__restrict__ cdp,
+__global__ void __launch_bounds__(64 * AMX_ENV_WG) k_env0(const ChainDev *__restrict__ cdp,
                                              const ChunkDev *__restrict__ chunks,
                                              const SegDev *__restrict__ es, int n_es,
                                              const uint16_t *__restrict__ mi,
@@ -435,14 +442,15 @@ __global__ void __launch_bounds__(64) k_env0(const ChainDev *__restrict__ cdp,
                                              double *__restrict__ sv, double *__restrict__ ev,
                                              int *__restrict__ act, int64_t nloc, int warm,
                                              int Le, int *__restrict__ flags) {
-    __shared__ __attribute__((aligned(16))) double sm[64 * AMX_ENV_MP];
+    __shared__ __attribute__((aligned(16))) double sm_all[AMX_ENV_WG][64 * AMX_ENV_MP];
     const ChainDev &cd = *cdp;
-    const int lane = threadIdx.x;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && lane < AMX_ENV_MAX_ROUNDS) flags[lane] = 0;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && lane < 64) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    double *sm = sm_all[wv];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < AMX_ENV_MAX_ROUNDS) flags[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) {
         for (int k = lane; k < AMX_ENV_MAX_ROUNDS * AMX_ENV_NCTR; k += 64) flags[AMX_ENV_MAX_ROUNDS + k] = 0;
     }
-    const int j = blockIdx.x * 64 + lane;
+    const int j = (blockIdx.x * (blockDim.x >> 6) + wv) * 64 + lane;
     const int b = blockIdx.y;
     const bool valid = j < n_es;
     const SegDev sg = es[valid ? j : n_es - 1];
@@ -714,10 +722,10 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
         const int64_t f = wbase + 4 * (64 * i + lane);
         xo[i] = ch.loc_off + (f < rowlen ? f : 0);
     }
-    // seg_tiles (Le == this wave's 1024 frames): a band whose envelope segment has no
+    // seg_tiles (= Le, a multiple of this wave's 1024 frames): a band whose envelope segment has no
     // over-threshold frame (act == 0) has m = 0 on the whole tile -- its r is not read
     bool mzero[3] = {false, false, false};
-    const int jt = (int)(wbase / (64 * AMX_ENV_TF_));
+    const int jt = seg_tiles ? (int)(wbase / seg_tiles) : 0;   // the envelope segment holding the wave
     if (seg_tiles && jt < neseg[c]) {
         const int js = eseg0[c] + jt;
 #pragma unroll
@@ -842,8 +850,10 @@ static void env_launch_t(const DynLaunch &d, const uint16_t *m, double *ck, doub
                          int *act, int *prev, int *flags, int rounds, int part) {
     const dim3 gw((unsigned)((d.n_es + 63) / 64), 3);
     if (part == 0) {
-        hipLaunchKernelGGL(k_env0<RCP>, gw, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es, m, d.tabs,
-                           ck, sv, ev, act, d.nloc, d.warm, d.Le, flags);
+        const int wg = d.env_wg >= 1 && d.env_wg <= AMX_ENV_WG ? d.env_wg : 1;
+        const dim3 g0((unsigned)((d.n_es + 64 * wg - 1) / (64 * wg)), 3);
+        hipLaunchKernelGGL(k_env0<RCP>, g0, dim3(64 * wg), d.env_pin ? AMX_ENV_LDS_PIN : 0, d.st, d.cd,
+                           d.chunks, d.es, d.n_es, m, d.tabs, ck, sv, ev, act, d.nloc, d.warm, d.Le, flags);
         return;
     }
     // rounds == 0: only prev[] (everything is left to k_envseq)
@@ -884,7 +894,8 @@ hipError_t launch_gain_overlay(const DynLaunch &d, const uint16_t *m, const doub
     if (empty(g)) return hipSuccess;
     const uint32_t *x = reinterpret_cast<const uint32_t *>(bands);
     uint32_t *o = reinterpret_cast<uint32_t *>(out);
-    const int seg_tiles = (act && d.Le == 64 * AMX_ENV_TF_) ? 1 : 0;
+    // a wave's 1024 frames lie in one envelope segment when Le is a multiple of 1024
+    const int seg_tiles = (act && d.Le % (64 * AMX_ENV_TF_) == 0) ? d.Le : 0;
     if (d.rcp)
         hipLaunchKernelGGL(k_gain_overlay<true>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, m, d.tabs, ck,
                            x, o, d.nloc, n1tab, act, d.eseg0, d.neseg, d.n_es, seg_tiles);

@@ -242,6 +242,7 @@ struct amx_plan {
     int lev_eq = 0, lev_x = 0, lev_kw = 0;
     int mb = 0;
     int Le = 1024, warm = 2048, rounds = 2;   // compressor envelope segments (amx_dyn.hip)
+    int env_wg = 1, env_pin = 0;              // k_env0 placement (amx_dyn.hip launch_env)
     int n_es = 0;
     std::vector<SegDev> esegs;
     std::vector<int> eseg0, neseg;
@@ -353,8 +354,8 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     const int fs = desc->sample_rate;
     if (desc->env_warm_frames >= 0) p->warm = (desc->env_warm_frames + 127) / 128 * 128;   // whole ring of k_env0 tiles
     if (desc->env_rounds >= 0) p->rounds = desc->env_rounds;
-    if (const char *ev = std::getenv("AMX_ENV_LE"))      // (measurements only)
-        p->Le = std::max(128, std::atoi(ev) / 128 * 128);
+    const char *env_le = std::getenv("AMX_ENV_LE");      // (measurements only)
+    if (env_le) p->Le = std::max(128, std::atoi(env_le) / 128 * 128);
     if (p->rounds > AMX_ENV_MAX_ROUNDS) {
         delete p;
         return fail(AMX_EINVAL, "env_rounds %d > %d", desc->env_rounds, AMX_ENV_MAX_ROUNDS);
@@ -584,6 +585,34 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     }
     p->n_tracks = n_tracks;
     p->n_chunks = n_chunks;
+    if (p->mb) {
+        // k_env0 runs one resident wave set: env_wg waves per CU (one workgroup per CU),
+        // Le the shortest multiple of 128 (>= 1024) whose segments fit it, so no CU runs
+        // waves in turn and the warm-up share W / Le shrinks as the job grows
+        // (AMX_ENV_WG = 0 is the single-wave-workgroup launch)
+        int wg = 2;
+        if (const char *ev = std::getenv("AMX_ENV_WG")) wg = std::atoi(ev);
+        if (wg > 0) {
+            p->env_wg = std::min(wg, 4);
+            p->env_pin = 1;
+            if (!env_le) {
+                int dev = 0, ncu = 0;
+                if (hipGetDevice(&dev) != hipSuccess ||
+                    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 3)
+                    ncu = 256;
+                const int64_t fit = (int64_t)(ncu / 3) * 64 * p->env_wg;   // segments per band
+                int64_t total = 0;
+                for (int c = 0; c < n_chunks; c++) total += chunks[c].frames;
+                int64_t Le = std::max<int64_t>(1024, (total / fit + 127) / 128 * 128);
+                for (;; Le += 128) {
+                    int64_t ne = 0;
+                    for (int c = 0; c < n_chunks; c++) ne += (chunks[c].frames + Le - 1) / Le;
+                    if (ne <= fit || Le >= (int64_t)1 << 24) break;
+                }
+                p->Le = (int)Le;
+            }
+        }
+    }
     int64_t loc = 0, outo = 0;
     p->spans.assign(n_tracks, SpanDev{});
     std::vector<int> track_seen(n_tracks, 0);
@@ -917,7 +946,8 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         // m rows are read whole-tile by k_env0, from W frames before a chunk to the
         // 16-frame tile past its end: pad the buffer on both sides
         // (and k_gain_overlay reads whole 1024-frame wave tiles)
-        const size_t mpad = (size_t)(p->warm > 1024 ? p->warm : 1024) + 64;
+        // (k_env0's last tiles of a chunk-final segment read up to Le frames past it)
+        const size_t mpad = (size_t)std::max(std::max(p->warm, p->Le), 1024) + 64;
         p->o_m = (size_t)align_up(off, (3 * nl + 2 * mpad) * 2) + mpad * 2;   // u16 r
         p->o_esv = (size_t)align_up(off, 3 * ne * 8);
         p->o_ee0 = (size_t)align_up(off, 3 * ne * 8);
@@ -1019,7 +1049,8 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     int *eprev = p->mb ? wsp<int>(d_ws, p->o_eprev) : nullptr;
     amx::DynLaunch dl{p->d_cd,    p->d_chunks, p->n_chunks, p->d_esegs, p->n_es,
                       p->d_eseg0, p->d_neseg,  p->nloc,     p->max_chunk_n, p->cd.look,
-                      p->warm,    p->Le,       p->cd.env_rcp, p->d_tabs, st};
+                      p->warm,    p->Le,       p->cd.env_rcp, p->d_tabs, st,
+                      p->env_wg,  p->env_pin};
     switch (stage) {
     case AMX_STAGE_FRONT1:
         if (p->mono16) {
