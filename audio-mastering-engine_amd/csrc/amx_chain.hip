@@ -280,6 +280,70 @@ __global__ void __launch_bounds__(AMX_BLOCK, 4) k_front1s(const ChainDev *__rest
 // over Gkw, right-aligned for a span's final partial segment like k_kw1) and the
 // per-(segment, channel) sample peak -- so the track is not read again for it.
 #define AMX_EQ_F 4   // frames per stage-major sub-tile (must divide AMX_TF)
+// Wave-local 16-B tile mover (rows of AMX_TF frames x 4 B, chunk rows 16-frame
+// aligned; a store row that is not falls back to dwords): the wave's 32 rows, mover lane l moves 16-B piece l % 4 (frames
+// 4 (l % 4) .. + 3) of rows l / 4 and l / 4 + 16 -- two vector loads / stores per
+// lane per tile from row offsets formed once, instead of a dword per element with
+// its row offset and bound re-read from LDS (tile_fetch / tile_store).  Frames at or
+// past a row's length load as 0 and are not stored.
+#define AMX_VT_PITCH 20   // dwords per LDS row (16-B aligned rows)
+typedef uint32_t vt4 __attribute__((ext_vector_type(4)));
+struct VRows {
+    int32_t base[2];      // dword offset of the row's frame 0 (an invalid row: 0; plans
+                          // hold < 2^31 frames, amx_plan_create)
+    int len[2];           // frames in the row (an invalid row: 0)
+};
+
+__device__ __forceinline__ void vt_fetch(vt4 (&R)[2], const uint32_t *__restrict__ src, const VRows &vr,
+                                         int k) {
+    const int c4 = 4 * (threadIdx.x & 3);
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const int n = k + c4;
+        const bool ok = n < vr.len[i];
+        vt4 v = *reinterpret_cast<const vt4 *>(src + vr.base[i] + (ok ? n : 0));
+#pragma unroll
+        for (int e = 0; e < 4; e++) v[e] = n + e < vr.len[i] ? v[e] : 0u;
+        R[i] = v;
+    }
+}
+
+__device__ __forceinline__ void vt_put(uint32_t *lds, const vt4 (&R)[2]) {
+    const int r0 = (threadIdx.x & 63) >> 2, c4 = 4 * (threadIdx.x & 3);
+    *reinterpret_cast<vt4 *>(lds + r0 * AMX_VT_PITCH + c4) = R[0];
+    *reinterpret_cast<vt4 *>(lds + (r0 + 16) * AMX_VT_PITCH + c4) = R[1];
+}
+
+__device__ __forceinline__ void vt_store(const uint32_t *lds, uint32_t *__restrict__ dst, const VRows &vr,
+                                         int k) {
+    const int r0 = (threadIdx.x & 63) >> 2, c4 = 4 * (threadIdx.x & 3);
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const vt4 v = *reinterpret_cast<const vt4 *>(lds + (r0 + 16 * i) * AMX_VT_PITCH + c4);
+        const int n = k + c4;
+        uint32_t *d = dst + vr.base[i] + n;
+        if (n + 4 <= vr.len[i] && (vr.base[i] & 3) == 0) {   // (d_out rows need not be 16-B aligned)
+            *reinterpret_cast<vt4 *>(d) = v;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+                if (n + e < vr.len[i]) d[e] = v[e];
+        }
+    }
+}
+
+// the mover rows of this lane, from the compute lanes (lane 2 r holds row r's offset)
+__device__ __forceinline__ VRows vt_rows(int32_t base, int len) {
+    VRows vr;
+    const int r0 = (threadIdx.x & 63) >> 2;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        vr.base[i] = __shfl(base, 2 * (r0 + 16 * i));
+        vr.len[i] = __shfl(len, 2 * (r0 + 16 * i));
+    }
+    return vr;
+}
+
 template <int MASK, bool MB, bool KW>
 __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const ChainDev *__restrict__ cdp,
                                                       const ChunkDev *__restrict__ chunks,
@@ -294,31 +358,25 @@ __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const 
                                                       uint32_t *__restrict__ pk) {
     constexpr int D = EqDim<MASK>::v;
     constexpr int ROWS = AMX_BLOCK / 2;
-    using T = Tile<1, ROWS>;
-    __shared__ uint32_t s_in[T::WORDS];
-    __shared__ uint32_t s_out[T::WORDS];
-    __shared__ int64_t rb_in[ROWS], rb_out[ROWS];
-    __shared__ int rl[ROWS];
+    constexpr int WV = AMX_BLOCK / 64;
+    __shared__ __attribute__((aligned(16))) uint32_t s_in_all[WV][32 * AMX_VT_PITCH];
+    __shared__ __attribute__((aligned(16))) uint32_t s_out_all[WV][32 * AMX_VT_PITCH];
+    __shared__ int2 s_orow[WV][32];   // per row: output dword offset, frames (read at the store)
     const ChainDev &cd = *cdp;
-    const int t = threadIdx.x, row = t >> 1, chn = t & 1;
-    const int j = blockIdx.x * ROWS + row;
+    const int t = threadIdx.x, wv = t >> 6, row = (t & 63) >> 1, chn = t & 1;
+    const int j = blockIdx.x * ROWS + wv * 32 + row;
     bool need_x = false;
-    if (chn == 0) {
-        rb_in[row] = 0;
-        rb_out[row] = 0;
-        rl[row] = 0;
-    }
+    int32_t b_in = 0, b_out = 0;
+    int len = 0;
     double z[D > 0 ? D : 1];
 #pragma unroll
     for (int d = 0; d < D; d++) z[d] = 0.0;
     if (j < n_seg) {
         const SegDev sg = segs[j];
         const ChunkDev ch = chunks[sg.chunk];
-        if (chn == 0) {
-            rb_in[row] = ch.loc_off + sg.pos;
-            rb_out[row] = (to_out ? ch.out_off : ch.loc_off) + sg.pos;
-            rl[row] = sg.len;
-        }
+        b_in = (int32_t)(ch.loc_off + sg.pos);
+        b_out = (int32_t)((to_out ? ch.out_off : ch.loc_off) + sg.pos);
+        len = sg.len;
         need_x = MB && !sg.last;
         if constexpr (D > 0) {
             const double *s = s_eq + ((int64_t)j * 2 + chn) * D;
@@ -339,17 +397,19 @@ __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const 
     const int negm = (cd.st[0].neg ? 1 : 0) | (cd.st[3].neg ? 8 : 0);
     const float w = cd.width;
     const int won = cd.width_on;
-    // tiles are wave-local (tile_row LOCAL): a wave stages, computes and stores only
-    // its own 32 rows, so it never waits for the other waves of the workgroup
-    amx_wave_sync();
-    TileRegs<1, ROWS> R;
-    tile_fetch<1, ROWS, true>(R, a16, rb_in, nullptr, rl, 0);
+    // tiles are wave-local: a wave stages, computes and stores only its own 32 rows
+    // (the vector mover), so it never waits for the other waves of the workgroup
+    const VRows vin = vt_rows(b_in, len);
+    if (chn == 0) s_orow[wv][row] = make_int2(b_out, len);
+    uint32_t *s_in = s_in_all[wv], *s_out = s_out_all[wv];
+    vt4 R[2];
+    vt_fetch(R, a16, vin, 0);
     for (int k = 0; k < L; k += AMX_TF) {
-        tile_put<1, ROWS, true>(s_in, R, nullptr, rl, k);
+        vt_put(s_in, R);
         amx_wave_sync();
-        if (k + AMX_TF < L) tile_fetch<1, ROWS, true>(R, a16, rb_in, nullptr, rl, k + AMX_TF);
-        const uint32_t *rp = s_in + row * T::PITCH;
-        uint32_t *op = s_out + row * T::PITCH;
+        if (k + AMX_TF < L) vt_fetch(R, a16, vin, k + AMX_TF);
+        const uint32_t *rp = s_in + row * AMX_VT_PITCH;
+        uint32_t *op = s_out + row * AMX_VT_PITCH;
 #pragma unroll 1
         for (int f0 = 0; f0 < AMX_TF; f0 += AMX_EQ_F) {
             float xf[AMX_EQ_F];
@@ -396,7 +456,15 @@ __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const 
             }
         }
         amx_wave_sync();
-        tile_store<1, ROWS, true>(s_out, dst, rb_out, rl, k);
+        {
+            // the output rows from LDS: kept in registers they spill the 5-wave variants
+            const int r0 = (t & 63) >> 2;
+            const int2 o0 = s_orow[wv][r0], o1 = s_orow[wv][r0 + 16];
+            VRows vout;
+            vout.base[0] = o0.x; vout.len[0] = o0.y;
+            vout.base[1] = o1.x; vout.len[1] = o1.y;
+            vt_store(s_out, dst, vout, k);
+        }
         amx_wave_sync();                    // s_in / s_out are rewritten by the next tile
     }
     if constexpr (MB) {
@@ -418,42 +486,38 @@ __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const 
 
 // ------------------------------------------------ crossover pass 2 -> 3 bands
 // One thread per (segment, channel); mid = (x - low) - high in float64 (:304).
+// Wave-local tiles through the vector mover; the L lane writes the low and mid
+// pairs, the R lane the high pair.
 __global__ void __launch_bounds__(AMX_BLOCK) k_xover2(const ChainDev *__restrict__ cdp,
                                                       const ChunkDev *__restrict__ chunks,
                                                       const SegDev *__restrict__ segs, int n_seg,
                                                       int L, const uint32_t *__restrict__ p16,
                                                       const double *__restrict__ s_x,
                                                       uint32_t *__restrict__ bands, int64_t nloc) {
-    constexpr int ROWS = AMX_BLOCK / 2;
-    using T = Tile<1, ROWS>;
-    __shared__ uint32_t s_in[T::WORDS];
-    __shared__ uint32_t s_lo[T::WORDS], s_mi[T::WORDS], s_hi[T::WORDS];
-    __shared__ int64_t rb[ROWS];
-    __shared__ int rl[ROWS];
+    constexpr int WV = AMX_BLOCK / 64;
+    __shared__ __attribute__((aligned(16))) uint32_t s_in[WV][32 * AMX_VT_PITCH];
+    __shared__ __attribute__((aligned(16))) uint32_t s_b[WV][2][32 * AMX_VT_PITCH];
     __shared__ double s_c[24];
     const ChainDev &cd = *cdp;
-    const int t = threadIdx.x, row = t >> 1, chn = t & 1;
-    const int j = blockIdx.x * ROWS + row;
+    const int t = threadIdx.x, wv = t >> 6, lane = t & 63, row = lane >> 1, chn = lane & 1;
+    const int j = blockIdx.x * (AMX_BLOCK / 2) + wv * 32 + row;
     if (t < 12) s_c[t] = cd.xlo[t];
     else if (t < 24) s_c[t] = cd.xhi[t - 12];
     double z[AMX_XO_DIM];
 #pragma unroll
     for (int d = 0; d < AMX_XO_DIM; d++) z[d] = 0.0;
-    if (chn == 0) {
-        rb[row] = 0;
-        rl[row] = 0;
-    }
+    int32_t base = 0;
+    int len = 0;
     if (j < n_seg) {
         const SegDev sg = segs[j];
         const ChunkDev ch = chunks[sg.chunk];
-        if (chn == 0) {
-            rb[row] = ch.loc_off + sg.pos;
-            rl[row] = sg.len;
-        }
+        base = (int32_t)(ch.loc_off + sg.pos);
+        len = sg.len;
         const double *s = s_x + ((int64_t)j * 2 + chn) * AMX_XO_DIM;
 #pragma unroll
         for (int d = 0; d < AMX_XO_DIM; d++) z[d] = s[d];
     }
+    const VRows vr = vt_rows(base, len);
     __syncthreads();
     double c[20];   // 4 sections x (b0 b1 b2 a1 a2): low 1, low 2, high 1, high 2
 #pragma unroll
@@ -464,19 +528,24 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_xover2(const ChainDev *__restrict
         c[5 * sc + 3] = s_c[6 * sc + 4];
         c[5 * sc + 4] = s_c[6 * sc + 5];
     }
-    // wave-local tiles (tile_row LOCAL), the next tile's loads in flight while this
-    // one is filtered
-    TileRegs<1, ROWS> R;
-    tile_fetch<1, ROWS, true>(R, p16, rb, nullptr, rl, 0);
+    // the high band goes back through the input tile (read into registers first)
+    uint32_t *si = s_in[wv], *slo = s_b[wv][0], *smi = s_b[wv][1], *shi = si;
+    vt4 R[2];
+    vt_fetch(R, p16, vr, 0);
     for (int k = 0; k < L; k += AMX_TF) {
-        tile_put<1, ROWS, true>(s_in, R, nullptr, rl, k);
+        vt_put(si, R);
         amx_wave_sync();
-        if (k + AMX_TF < L) tile_fetch<1, ROWS, true>(R, p16, rb, nullptr, rl, k + AMX_TF);
-        const uint32_t *rp = s_in + row * T::PITCH;
-        const int o = row * T::PITCH;
+        if (k + AMX_TF < L) vt_fetch(R, p16, vr, k + AMX_TF);
+        uint32_t xin[AMX_TF];
+#pragma unroll
+        for (int q = 0; q < AMX_TF / 4; q++) {
+            const vt4 v = *reinterpret_cast<const vt4 *>(si + row * AMX_VT_PITCH + 4 * q);
+            xin[4 * q] = v.x; xin[4 * q + 1] = v.y; xin[4 * q + 2] = v.z; xin[4 * q + 3] = v.w;
+        }
+        const int o = row * AMX_VT_PITCH;
 #pragma unroll 4
         for (int f = 0; f < AMX_TF; f++) {
-            const uint32_t p = rp[f];
+            const uint32_t p = xin[f];
             const int16_t v = chn ? hi16(p) : lo16(p);
             const double x = (double)((float)v / 32768.0f);   // :300 float32 then float64
             double l = bq_step(c, z[0], z[1], x);
@@ -489,15 +558,16 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_xover2(const ChainDev *__restrict
             const int om = __builtin_amdgcn_update_dpp(0, qm, 0xB1, 0xF, 0xF, false);
             const int oh = __builtin_amdgcn_update_dpp(0, qh, 0xB1, 0xF, 0xF, false);
             if (chn == 0) {
-                s_lo[o + f] = pack2((int16_t)ql, (int16_t)ol);
-                s_mi[o + f] = pack2((int16_t)qm, (int16_t)om);
-                s_hi[o + f] = pack2((int16_t)qh, (int16_t)oh);
+                slo[o + f] = pack2((int16_t)ql, (int16_t)ol);
+                smi[o + f] = pack2((int16_t)qm, (int16_t)om);
+            } else {
+                shi[o + f] = pack2((int16_t)oh, (int16_t)qh);
             }
         }
         amx_wave_sync();
-        tile_store<1, ROWS, true>(s_lo, bands, rb, rl, k);
-        tile_store<1, ROWS, true>(s_mi, bands + nloc, rb, rl, k);
-        tile_store<1, ROWS, true>(s_hi, bands + 2 * nloc, rb, rl, k);
+        vt_store(slo, bands, vr, k);
+        vt_store(smi, bands + nloc, vr, k);
+        vt_store(shi, bands + 2 * nloc, vr, k);
         amx_wave_sync();
     }
 }

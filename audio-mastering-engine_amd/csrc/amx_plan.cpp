@@ -670,6 +670,11 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         loc += (ch.n + 15) / 16 * 16;   // chunk rows of per-frame scratch start 16-frame aligned
         outo += n2;
     }
+    if (loc >= ((int64_t)1 << 31) || outo >= ((int64_t)1 << 31)) {
+        delete p;   // the chain kernels' row offsets are 32-bit (amx_chain.hip VRows)
+        return fail(AMX_ERANGE, "a plan holds fewer than 2^31 frames (%lld): split the batch",
+                    (long long)std::max(loc, outo));
+    }
     p->nloc = loc;
     p->n_es = (int)p->esegs.size();
     p->out_frames = outo;
@@ -1380,16 +1385,26 @@ int amx_limiter_prepare(amx_plan *p, const amx_final_desc *fd, int32_t seg_frame
         p->lim.max_segs == max_segs)
         return AMX_OK;
     const int T = p->n_tracks > 0 ? p->n_tracks : 1;
+    // the new scratch is allocated before the old is released, so a failed
+    // allocation leaves the plan's previous (consistent) limiter scratch in place
+    double *seg_state = nullptr;
+    unsigned *cnt = nullptr;
+    if (hipMalloc(&seg_state, (size_t)T * max_segs * 2 * sd * sizeof(double)) != hipSuccess ||
+        hipMalloc(&cnt, (size_t)T * sizeof(unsigned)) != hipSuccess ||
+        hipMemset(cnt, 0, (size_t)T * sizeof(unsigned)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
+        if (seg_state) (void)hipFree(seg_state);
+        if (cnt) (void)hipFree(cnt);
+        return fail(AMX_EHIP, "limiter scratch allocation failed");
+    }
     if (p->lim.seg_state) (void)hipFree(p->lim.seg_state);
     if (p->lim.cnt) (void)hipFree(p->lim.cnt);
     const int64_t cap = p->lim.warm_cap;
     p->lim = amx::LimScratch{};
     p->lim.warm_frames = warm_frames;
     p->lim.warm_cap = cap;
-    HIPCHK(hipMalloc(&p->lim.seg_state, (size_t)T * max_segs * 2 * sd * sizeof(double)));
-    HIPCHK(hipMalloc(&p->lim.cnt, (size_t)T * sizeof(unsigned)));
-    HIPCHK(hipMemset(p->lim.cnt, 0, (size_t)T * sizeof(unsigned)));
-    HIPCHK(hipDeviceSynchronize());
+    p->lim.seg_state = seg_state;
+    p->lim.cnt = cnt;
     p->lim.seg_frames = seg_frames;
     p->lim.max_segs = max_segs;
     p->lim.buffer_size = bs;
