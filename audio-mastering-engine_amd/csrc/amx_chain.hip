@@ -159,18 +159,26 @@ __device__ __forceinline__ void front1s_run(const ChainDev &cd, const float *__r
         __syncthreads();
         if (k + AMX_TF < L) fetch(k + AMX_TF);
         if constexpr (AN) {
-            // tanh table lookups for the whole tile first, all in flight together
-            // (one per frame per lane: lane `half` takes its own channel), written
-            // back over that channel's input word; the frame loop then reads both
-            // channels' tanh from the row (a per-frame lookup left an L2 round trip
-            // on every step of the loop)
-            uint32_t *rw = s_in + row * AMX_F1_PITCH + half;
-            float th[AMX_TF];
+            // The analog stage couples the channels, so a lane takes whole frames: the
+            // two lanes of a pair take every other frame (f = 2 i + half), both
+            // channels, through the tanh table and the shelves -- each frame's analog
+            // arithmetic is done once, not by both lanes -- and write its s16 pair
+            // to the output row, from which the GEMV loop reads every frame.  The
+            // table lookups of the tile are all issued first (a lookup per step left an
+            // L2 round trip on every step).
+            float t0[AMX_TF / 2], t1[AMX_TF / 2];
 #pragma unroll
-            for (int f = 0; f < AMX_TF; f++)
-                th[f] = lut[(int)q_f32_to_s16_ffmpeg(__uint_as_float(rw[2 * f])) + 32768];
+            for (int i = 0; i < AMX_TF / 2; i++) {
+                const int f = 2 * i + half;
+                t0[i] = lut[(int)q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f])) + 32768];
+                t1[i] = lut[(int)q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f + 1])) + 32768];
+            }
 #pragma unroll
-            for (int f = 0; f < AMX_TF; f++) rw[2 * f] = __float_as_uint(th[f]);
+            for (int i = 0; i < AMX_TF / 2; i++) {
+                int16_t l, r;
+                analog_shelves(cd, t0[i], t1[i], l, r);
+                s_out[row * (AMX_TF + 1) + 2 * i + half] = pack2(l, r);
+            }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
         }
@@ -178,12 +186,14 @@ __device__ __forceinline__ void front1s_run(const ChainDev &cd, const float *__r
         for (int f = 0; f < AMX_TF; f++) {
             int16_t l, r;
             if constexpr (AN) {
-                analog_shelves(cd, __uint_as_float(rp[2 * f]), __uint_as_float(rp[2 * f + 1]), l, r);
+                const uint32_t w = s_out[row * (AMX_TF + 1) + f];
+                l = lo16(w);
+                r = hi16(w);
             } else {
                 l = q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f]));
                 r = q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f + 1]));
+                if (half == 0) s_out[row * (AMX_TF + 1) + f] = pack2(l, r);
             }
-            if (half == 0) s_out[row * (AMX_TF + 1) + f] = pack2(l, r);
             double x0 = (double)((float)l / 32768.0f), x1 = (double)((float)r / 32768.0f);
             if constexpr (PART) {
                 x0 = k + f < len ? x0 : 0.0;

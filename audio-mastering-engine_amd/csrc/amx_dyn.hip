@@ -210,10 +210,11 @@ __device__ __forceinline__ double env_step(const ChainDev &cd, double att, doubl
 }
 
 // audioop.mul clamp + floor (CPython Modules/audioop.c fbound), branch-free:
-// > 32767 -> 32767, < -32767 -> -32768, then floor
+// > 32767 -> 32767, < -32767 -> -32768, then floor.  floor(max(val, -32768)) is the
+// same: a val in [-32768, -32767) floors to -32768 by itself (one max instead of a
+// compare and two selects)
 __device__ __forceinline__ int mul16(int v, double f) {
-    const double val = fmin((double)v * f, 32767.0);
-    return (int)floor(val < -32768.0 + 1.0 ? -32768.0 : val);
+    return (int)floor(fmax(fmin((double)v * f, 32767.0), -32768.0));
 }
 
 // 10^x for the gain: ROCm device-libs' exp10 (ocml) operation for operation --

@@ -18,6 +18,8 @@
 
 namespace amx {
 
+typedef double d2s __attribute__((ext_vector_type(2)));
+
 // ------------------------------------------------ up / down sweeps in a block
 template <int D, int GP, bool DOWN>
 __global__ void __launch_bounds__(AMX_BLOCK) k_scan_blk(const ScanBlk *__restrict__ blks,
@@ -29,7 +31,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_scan_blk(const ScanBlk *__restric
                                                         double *__restrict__ eb) {
     static_assert(GP >= D && GP <= 64 && (64 % GP) == 0, "group must tile a wave");
     constexpr int GPB = AMX_BLOCK / GP;
-    __shared__ double lds[AMX_BLOCK];
+    __shared__ __attribute__((aligned(16))) double lds[AMX_BLOCK];
     const int t = threadIdx.x;
     const int gi = t / GP, i = t % GP;
     const int64_t g = (int64_t)blockIdx.x * GPB + gi;     // (block, channel) = 2 b + ch
@@ -90,13 +92,25 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_scan_blk(const ScanBlk *__restric
         __builtin_amdgcn_wave_barrier();
         // four partial sums: the dependent fp64 FMA latency (~30 cycles) would
         // otherwise serialise D FMAs per step
+        // the vector is read as 16-B pairs (D even): half the LDS instructions
         double a0 = row ? ev[q] : 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        double mv[D];
+#pragma unroll
+        for (int k = 0; k < D; k += 2) {
+            if (k + 1 < D) {
+                const d2s pr = *reinterpret_cast<const d2s *>(my + k);
+                mv[k] = pr.x;
+                mv[k + 1] = pr.y;
+            } else {
+                mv[k] = my[k];
+            }
+        }
 #pragma unroll
         for (int k = 0; k < D; k += 4) {
-            a0 = fma(mrow[k], my[k], a0);
-            if (k + 1 < D) a1 = fma(mrow[k + 1], my[k + 1], a1);
-            if (k + 2 < D) a2 = fma(mrow[k + 2], my[k + 2], a2);
-            if (k + 3 < D) a3 = fma(mrow[k + 3], my[k + 3], a3);
+            a0 = fma(mrow[k], mv[k], a0);
+            if (k + 1 < D) a1 = fma(mrow[k + 1], mv[k + 1], a1);
+            if (k + 2 < D) a2 = fma(mrow[k + 2], mv[k + 2], a2);
+            if (k + 3 < D) a3 = fma(mrow[k + 3], mv[k + 3], a3);
         }
         __builtin_amdgcn_wave_barrier();
         v = (a0 + a1) + (a2 + a3);
