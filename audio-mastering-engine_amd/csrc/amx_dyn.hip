@@ -344,8 +344,9 @@ __device__ double env_rerun_wave(const ChainDev &cd, const uint16_t *m, const do
 // gather) and stages m in LDS (padded rows, conflict-free b128 reads).  The r loads
 // run AMX_ENV_PF tiles ahead and the gathers 2 tiles ahead of the tile being computed
 // (one tile is ~16 dependent steps, shorter than a miss to HBM).  Per tile the 16
-// quotient pairs are formed first (independent chains), then the recurrence runs
-// alone: at one wave per SIMD nothing else hides a stall.  Frames before the chunk or
+// quotient pairs and the recurrence are one scheduling region.  (The recurrence's
+// dependences do not set the time: with them removed the kernel took the same time;
+// DESIGN.md §3.4.)  Frames before the chunk or
 // after the segment are fed as m = 0 (state held); the buffer is padded so those rows
 // read in bounds.  W and Le are multiples of 16 AMX_ENV_PF and chunk rows start
 // 16-frame aligned, so the warm-up / main boundary is tile-uniform, every vector is
@@ -420,7 +421,8 @@ __device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, double
             dv[f] = env_div<RCP>(mv[f], cd.env_R, cd.env_rR);
             mv[f] = __builtin_canonicalize(mv[f]);      // fmin's operand, once per frame here
         }
-        __builtin_amdgcn_sched_barrier(0);
+        // (no scheduling barrier: the scheduler may start the recurrence while later
+        // quotients are still being formed; measured 206 -> 201 us at C3)
 #pragma unroll
         for (int f = 0; f < AMX_ENV_TF; f++) att = env_step3(att, mv[f], iv[f], dv[f]);
     }
