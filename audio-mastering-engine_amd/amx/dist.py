@@ -190,6 +190,16 @@ def chain_state_speculative(state, run, is_rest, rank, world, group=None, first_
         dist.send(s, dst=rank + 1, group=group)
 
 
+def _check_linear(ctl):
+    """A chunk-sharded track finalises linear loudnorm only: the device's mode word
+    (k_decide, bits 4..7; 3 = dynamic) is read with the limiter flag each step, so a track
+    that needs dynamic mode raises instead of coming out unnormalised."""
+    if (ctl >> 4) & 15 == 3:
+        from .engine import DynamicModeUnsupported
+        raise DynamicModeUnsupported("chunk-sharded track: loudnorm takes dynamic mode; run it "
+                                     "whole (master_audio / MasteringJob.finish_dynamic)")
+
+
 class ShardedTrack:
     """This rank's part of one chunk-sharded track.
 
@@ -369,6 +379,7 @@ class ShardedTrack:
         self._ctl_host.copy_(job.ctl[:1], non_blocking=True)
         self._ctl_ev.record()
         self._ctl_ev.synchronize()
+        _check_linear(int(self._ctl_host[0]))
         if not (int(self._ctl_host[0]) & capi.CTL_FAST):
             chain_state_speculative(job.lim_state, lambda: job.finalize(False),
                                     lambda v: is_rest_state(v, job.bs), self.rank, self.world,
@@ -392,7 +403,9 @@ class ShardedTrack:
             reduce_loudness(job.hops, None, self.group)
             job.timed("hist", job.histograms)
         job.timed("decide", job.decide)
-        fast = bool(int(job.ctl[0].item()) & capi.CTL_FAST)
+        ctl = int(job.ctl[0].item())
+        _check_linear(ctl)
+        fast = bool(ctl & capi.CTL_FAST)
         if fast:
             job.timed("final", lambda: job.finalize(True))
         else:

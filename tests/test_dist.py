@@ -245,3 +245,15 @@ def test_batch_split_gloo_world2(frames):
     """C4 batch split over two ranks (gloo): each rank's ShardedBatch share, agreed
     without any exchange of data."""
     mp.spawn(_batch_worker, args=(2, _free_port(), frames), nprocs=2, join=True)
+
+
+def test_sharded_track_mode_word():
+    """A chunk-sharded step reads k_decide's control word (bit 0 limiter idle, bits 4..7
+    loudnorm mode): dynamic mode (3) raises rather than leaving the track unnormalised."""
+    from amx.engine import DynamicModeUnsupported
+    for mode in (0, 1, 2):
+        for fast in (0, 1):
+            adist._check_linear((mode << 4) | fast)
+    for fast in (0, 1):
+        with pytest.raises(DynamicModeUnsupported):
+            adist._check_linear((3 << 4) | fast)
