@@ -200,22 +200,25 @@ class MasteringJob:
         return [dict(zip(keys, r)) for r in rows if any(r)]
 
     # --------------------------------------------- loudnorm dynamic mode (192 kHz)
-    def _job192(self, t):
+    def _job192(self, t, cached=True):
         """the 192 kHz side of track t: a measure-only plan at 192 kHz holding the
         filter's output (its loudness measurement gives pass 1's target_offset; its
         alimiter is the reference's :223 on the 192 kHz file) + amx_loudnorm_192k's
-        scratch"""
+        scratch.  cached: kept for the next call on the same track (one at a time);
+        else a fresh set, so several tracks can run at once (finish_dynamic)."""
         import ctypes
         n192, wsb = ctypes.c_int64(), ctypes.c_int64()
         capi.check(capi.load().amx_loudnorm_192k_size(self.plan.h, t, ctypes.byref(n192), ctypes.byref(wsb)),
                    "amx_loudnorm_192k_size")
         key = (t, n192.value)
-        if getattr(self, "_j192", None) is None or self._j192[0] != key:
+        if not cached or getattr(self, "_j192", None) is None or self._j192[0] != key:
             job2 = MasteringJob(192000, 2, {"lufs": self.settings.get("lufs")}, [n192.value],
                                 input_s16=True, chunks=[(0, 0, n192.value)], device=self.device,
                                 measure_only=True, seg_frames=1024)   # the K scan's window at 192 kHz
             ws2 = torch.empty(max(1, wsb.value), dtype=torch.uint8, device=self.device)
             summ = torch.zeros(16, dtype=torch.float64, device=self.device)
+            if not cached:
+                return n192.value, job2, ws2, summ
             self._j192 = (key, job2, ws2, summ)
         return n192.value, self._j192[1], self._j192[2], self._j192[3]
 
@@ -233,7 +236,15 @@ class MasteringJob:
         pass-1 strings; then the alimiter (:223) at 192 kHz.  Returns (int16 [n192, 2] at
         192 kHz, info).  Every per-sample step is on the device; the host reads pass 1's
         output loudness (one double) to form the "%.2f" string pass 2 parses."""
-        n192, job2, ws2, summ = self._job192(t)
+        run = self._dyn_pass1(t, stream, cached=True)
+        self._dyn_pass2(run, stats, stream)
+        return self._dyn_result(run, stream)
+
+    def _dyn_pass1(self, t, stream, cached, side=None):
+        """pass 1 of the dynamic path, enqueued: the filter with the measured_* defaults
+        and the 192 kHz measurement of its output.  side: the 192 kHz set of _job192,
+        made beforehand (a plan's creation synchronises the device)."""
+        n192, job2, ws2, summ = side if side is not None else self._job192(t, cached)
         target = float(self.settings["lufs"])
         d = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
         self.loudnorm_192k(t, d, job2, ws2, summ, stream)
@@ -242,24 +253,39 @@ class MasteringJob:
         job2.histograms(stream)
         job2.dd.lufs_on = 1
         job2.decide(stream)
-        i_out = float(job2.stats[0, 0].item())
-        target_offset = loudness._fmt(target - i_out)
+        return {"t": t, "n192": n192, "job2": job2, "ws2": ws2, "summ": summ, "desc": d}
+
+    def _dyn_pass2(self, run, stats, stream):
+        """reads pass 1's output loudness (waits for that stream only) and enqueues pass 2's
+        filter, the 192 kHz measurement of its output and the alimiter"""
+        job2, d = run["job2"], run["desc"]
+        # read on the track's own stream: a read on the legacy default stream would also
+        # wait for every other track's work enqueued so far
+        with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
+            i_out = float(job2.stats[0, 0].item())
+        target = float(self.settings["lufs"])
+        run["target_offset"] = loudness._fmt(target - i_out)
+        run["i_out"] = i_out
         d.measured_i = float(stats["input_i"])
         d.measured_lra = float(stats["input_lra"])
         d.measured_tp = float(stats["input_tp"])
         d.measured_thresh = float(stats["input_thresh"])
-        d.offset = float(target_offset)
-        self.loudnorm_192k(t, d, job2, ws2, summ, stream)
+        d.offset = float(run["target_offset"])
+        self.loudnorm_192k(run["t"], d, job2, run["ws2"], run["summ"], stream)
         job2.loudness_pass1(stream, tail=False)            # the limiter's input bound
         job2.dd.lufs_on = 0
         job2.decide(stream)
         job2.finalize(None, stream)
-        prof = summ.cpu().numpy()
-        return job2.y[:n192], {"target_offset": target_offset, "pass1_output_i": i_out,
-                               "sample_rate": 192000,
-                               "pass2_cycles": {k: float(prof[i]) for i, k in enumerate(
-                                   ("fill", "detect", "envelope", "output", "stats", "r128_out",
-                                    "detect_calls", "serial_chunks"), start=2)}}
+
+    def _dyn_result(self, run, stream):
+        with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
+            prof = run["summ"].cpu().numpy()
+        return run["job2"].y[:run["n192"]], {
+            "target_offset": run["target_offset"], "pass1_output_i": run["i_out"],
+            "sample_rate": 192000,
+            "pass2_cycles": {k: float(prof[i]) for i, k in enumerate(
+                ("fill", "detect", "envelope", "output", "stats", "r128_out",
+                 "detect_calls", "serial_chunks"), start=2)}}
 
     # ------------------------------------------------------------ report
     def fetch_report(self, raise_dynamic=True):
@@ -327,10 +353,29 @@ class MasteringJob:
         returns {track: info}."""
         rep = report if report is not None else self.fetch_report(raise_dynamic=False)
         self.dyn_out = {}
-        for t, mode in enumerate(rep["modes"]):
-            if mode == "dynamic":
-                y, info = self.dynamic_track(t, rep["stats"][t])
-                self.dyn_out[t] = (y.clone(), info)
+        dyn = [t for t, mode in enumerate(rep["modes"]) if mode == "dynamic"]
+        if len(dyn) == 1:
+            y, info = self.dynamic_track(dyn[0], rep["stats"][dyn[0]])
+            self.dyn_out[dyn[0]] = (y.clone(), info)
+        elif dyn:
+            # Several tracks: each on a stream of its own with its own 192 kHz scratch.  A
+            # filter run is one workgroup working in order, so the tracks' runs go side by
+            # side on different CUs instead of one after another.  Pass 2 of a track is
+            # enqueued as soon as its own pass 1 has been read back.
+            # The 192 kHz plans are made first: creating one synchronises the device.
+            sides = [self._job192(t, cached=False) for t in dyn]
+            cur = torch.cuda.current_stream(self.device)
+            runs = []
+            for t, side in zip(dyn, sides):
+                st = torch.cuda.Stream(device=self.device)   # (HIP spreads streams over its hardware queues)
+                st.wait_stream(cur)
+                runs.append((st, self._dyn_pass1(t, st, cached=False, side=side)))
+            for st, run in runs:
+                self._dyn_pass2(run, rep["stats"][run["t"]], st)
+            for st, run in runs:
+                y, info = self._dyn_result(run, st)
+                cur.wait_stream(st)
+                self.dyn_out[run["t"]] = (y.clone(), info)
         return {t: v[1] for t, v in self.dyn_out.items()}
 
     def track_output(self, t):

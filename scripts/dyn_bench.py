@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--seconds", type=float, default=300.0)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--batch", type=int, default=0,
+                    help="also time a batch of this many dynamic tracks: one after another "
+                         "(dynamic_track) and side by side (finish_dynamic)")
     args = ap.parse_args()
     import torch
     from amx.engine import MasteringJob
@@ -70,6 +73,25 @@ def main():
     out["cpu_oracle"] = {"seconds_of_audio": args.cpu_seconds, "s": round(cpu_s, 3),
                          "realtime_x": round(args.cpu_seconds / cpu_s, 1), "cores": 1}
     out["gpu_realtime_x"] = round(args.seconds / gpu_s, 1)
+    if args.batch > 1:
+        xs = [signal(args.seconds, fs, 11 + k) for k in range(args.batch)]
+        bj = MasteringJob(fs, 2, settings, [v.shape[0] for v in xs])
+        bj.run(torch.from_numpy(np.ascontiguousarray(np.concatenate(xs))).cuda())
+        brep = bj.fetch_report(raise_dynamic=False)
+        assert all(m == "dynamic" for m in brep["modes"]), brep["modes"]
+        bj.finish_dynamic(brep)                                   # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for t in range(args.batch):
+            bj.dynamic_track(t, brep["stats"][t])
+        torch.cuda.synchronize()
+        seq_s = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        bj.finish_dynamic(brep)
+        torch.cuda.synchronize()
+        par_s = time.perf_counter() - t0
+        out["batch"] = {"tracks": args.batch, "one_after_another_s": round(seq_s, 4),
+                        "side_by_side_s": round(par_s, 4), "speedup": round(seq_s / par_s, 2)}
     print(json.dumps(out))
 
 

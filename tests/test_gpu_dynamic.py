@@ -169,3 +169,26 @@ def test_sharded_batch_dynamic(gpu, oracle_mod):
         x16 = oracle_mod.quantize(xs[k])
         ref, rinfo = oracle_mod.pipeline(x16, fs, settings, chunk_bounds(frames[k], fs, 512))
         _cmp(b.track_output(k).cpu().numpy(), ref, "ShardedBatch track %d (%s)" % (k, rinfo["mode"]))
+
+
+def test_batch_several_dynamic(gpu, oracle_mod):
+    """finish_dynamic with several dynamic tracks runs them side by side (a stream and
+    192 kHz scratch each); every track still matches its own oracle pipeline"""
+    import torch
+    from amx import synth
+    from amx.chunking import chunk_bounds
+    from amx.engine import MasteringJob
+    fs = 48000
+    settings = dict(bass_boost=1.0, lufs=-14.0)
+    xs = [_dynamic_signal(6.0, fs, 51), synth.mix_like(fs * 5, fs, 2, seed=52),
+          _dynamic_signal(7.5, fs, 53), _dynamic_signal(4.0, fs, 54, intro=1.5)]
+    job = MasteringJob(fs, 2, settings, [x.shape[0] for x in xs], quantum=512)
+    job.run(torch.from_numpy(np.ascontiguousarray(np.concatenate(xs))).cuda())
+    rep = job.fetch_report(raise_dynamic=False)
+    assert rep["modes"] == ["dynamic", "linear", "dynamic", "dynamic"], rep["modes"]
+    info = job.finish_dynamic(rep)
+    assert sorted(info) == [0, 2, 3] and all(v["sample_rate"] == 192000 for v in info.values())
+    for t, x in enumerate(xs):
+        x16 = oracle_mod.quantize(x)
+        ref, rinfo = oracle_mod.pipeline(x16, fs, settings, chunk_bounds(x16.shape[0], fs, 512))
+        _cmp(job.track_output(t).cpu().numpy(), ref, "several-dynamic batch track %d (%s)" % (t, rinfo["mode"]))
