@@ -91,7 +91,8 @@ EXPORTS = ("amx_abi_version", "amx_last_error", "amx_plan_create", "amx_plan_fre
            "amx_limiter_geometry", "amx_limiter_prepare", "amx_loudness_decide", "amx_kw_carry_setup", "amx_kw_carry",
            "amx_finalize", "amx_env_counters", "amx_pcm_to_s16", "amx_loudnorm_192k_size",
            "amx_loudnorm_192k")
-PCM_FORMATS = {"u8": 0, "s16": 1, "s24": 2, "s32": 3, "f32": 4, "f64": 5}
+PCM_FORMATS = {"u8": 0, "s16": 1, "s24": 2, "s32": 3, "f32": 4, "f64": 5,
+               "s8": 6, "s16be": 7, "s24be": 8, "s32be": 9, "f32be": 10, "f64be": 11}
 
 _lib = None
 

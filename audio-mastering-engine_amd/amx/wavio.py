@@ -1,7 +1,8 @@
 """Minimal RIFF/WAVE reader/writer (PCM 8/16/24/32 and IEEE float 32/64).
 
 Host I/O for master_audio(): the reference reads any format ffmpeg decodes and
-writes 16-bit PCM (:178, :223); this build reads WAV and writes s16 WAV.
+writes 16-bit PCM (:178, :223); this build reads WAV and AIFF / AIFF-C (aiffio.py,
+read_audio_raw) and writes s16 WAV.
 """
 import struct
 
@@ -54,6 +55,23 @@ def read_wav_raw(path):
     n = len(payload) // fmt.block_align
     raw = np.frombuffer(payload, np.uint8, count=n * fmt.block_align)
     return raw, fmt, code
+
+
+def read_audio_raw(path):
+    """read_wav_raw for a WAV file, aiffio.read_aiff_raw for AIFF / AIFF-C (the GUI's
+    *.wav / *.aiff inputs, mastering_gui.py:170)"""
+    from . import aiffio
+    if aiffio.is_aiff(path):
+        return aiffio.read_aiff_raw(path)
+    return read_wav_raw(path)
+
+
+def read_audio_native(path):
+    """read_wav_native / aiffio.read_aiff_native by the file's own header"""
+    from . import aiffio
+    if aiffio.is_aiff(path):
+        return aiffio.read_aiff_native(path)
+    return read_wav_native(path)
 
 
 def read_wav_native(path):

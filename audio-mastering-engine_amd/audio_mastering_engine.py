@@ -53,7 +53,7 @@ def _device_input(path):
     amx_pcm_to_s16 (what ffmpeg's split writes + pydub's set_channels(2))."""
     import torch
     from amx import capi
-    raw, info, code = wavio.read_wav_raw(path)
+    raw, info, code = wavio.read_audio_raw(path)          # WAV or AIFF / AIFF-C
     if info.channels not in (1, 2):
         raise ValueError("only mono and stereo inputs are supported (%d channels)" % info.channels)
     frames = raw.size // info.block_align

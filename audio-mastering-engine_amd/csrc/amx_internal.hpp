@@ -24,6 +24,12 @@
 #define AMX_PCM_S32 3
 #define AMX_PCM_F32 4
 #define AMX_PCM_F64 5
+#define AMX_PCM_S8 6
+#define AMX_PCM_S16BE 7
+#define AMX_PCM_S24BE 8
+#define AMX_PCM_S32BE 9
+#define AMX_PCM_F32BE 10
+#define AMX_PCM_F64BE 11
 #endif
 
 // One EQ stage of _apply_eq_to_channel (audio_mastering_engine.py:277-282).

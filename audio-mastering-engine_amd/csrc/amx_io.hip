@@ -11,6 +11,10 @@
 //   s32 : v >> 16
 //   f32 : av_clip_int16(lrintf(v * 32768))
 //   f64 : av_clip_int16(lrint(v * 32768))
+// AIFF / AIFF-C input (the GUI's *.aiff, mastering_gui.py:170): big-endian PCM and float
+// take the same conversions after the byte swap (pcm_s16be ... pcm_f64be decode to the
+// same sample formats); AIFF's 8-bit is signed (pcm_s8 decodes to u8 as v + 0x80, so
+// the s16 value is v << 8).
 // (float32 input normally skips this kernel: k_front1s quantises it in the chain's
 // first pass.)  One thread per frame, grid-stride; a memory-bound pass.
 #include "amx_dev.hpp"
@@ -31,8 +35,34 @@ __device__ __forceinline__ int16_t pcm_sample(const uint8_t *__restrict__ raw, i
         return (int16_t)(reinterpret_cast<const int32_t *>(raw)[s] >> 16);
     } else if constexpr (FMT == AMX_PCM_F32) {
         return q_f32_to_s16_ffmpeg(reinterpret_cast<const float *>(raw)[s]);
-    } else {
+    } else if constexpr (FMT == AMX_PCM_F64) {
         double v = rint(reinterpret_cast<const double *>(raw)[s] * 32768.0);
+        v = fmin(fmax(v, -32768.0), 32767.0);
+        return (int16_t)(int)v;
+    } else if constexpr (FMT == AMX_PCM_S8) {
+        return (int16_t)((int)(int8_t)raw[s] * 256);
+    } else if constexpr (FMT == AMX_PCM_S16BE) {
+        const uint8_t *p = raw + 2 * s;
+        return (int16_t)(uint16_t)((uint32_t)p[0] << 8 | (uint32_t)p[1]);
+    } else if constexpr (FMT == AMX_PCM_S24BE) {
+        const uint8_t *p = raw + 3 * s;
+        const int v = (int)((uint32_t)p[2] << 8 | (uint32_t)p[1] << 16 | (uint32_t)p[0] << 24);
+        return (int16_t)(v >> 16);
+    } else if constexpr (FMT == AMX_PCM_S32BE) {
+        const uint8_t *p = raw + 4 * s;
+        const int v = (int)((uint32_t)p[3] | (uint32_t)p[2] << 8 | (uint32_t)p[1] << 16 | (uint32_t)p[0] << 24);
+        return (int16_t)(v >> 16);
+    } else if constexpr (FMT == AMX_PCM_F32BE) {
+        const uint8_t *p = raw + 4 * s;
+        const uint32_t b = (uint32_t)p[3] | (uint32_t)p[2] << 8 | (uint32_t)p[1] << 16 | (uint32_t)p[0] << 24;
+        return q_f32_to_s16_ffmpeg(__uint_as_float(b));
+    } else {
+        static_assert(FMT == AMX_PCM_F64BE, "PCM format");
+        const uint8_t *p = raw + 8 * s;
+        uint64_t b = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) b = b << 8 | (uint64_t)p[k];
+        double v = rint(__longlong_as_double((long long)b) * 32768.0);
         v = fmin(fmax(v, -32768.0), 32767.0);
         return (int16_t)(int)v;
     }
@@ -75,6 +105,12 @@ hipError_t launch_pcm_to_s16(const void *raw, int64_t frames, int channels, int 
     case AMX_PCM_S32: return pcm_t<AMX_PCM_S32>(r, frames, channels, o, st);
     case AMX_PCM_F32: return pcm_t<AMX_PCM_F32>(r, frames, channels, o, st);
     case AMX_PCM_F64: return pcm_t<AMX_PCM_F64>(r, frames, channels, o, st);
+    case AMX_PCM_S8: return pcm_t<AMX_PCM_S8>(r, frames, channels, o, st);
+    case AMX_PCM_S16BE: return pcm_t<AMX_PCM_S16BE>(r, frames, channels, o, st);
+    case AMX_PCM_S24BE: return pcm_t<AMX_PCM_S24BE>(r, frames, channels, o, st);
+    case AMX_PCM_S32BE: return pcm_t<AMX_PCM_S32BE>(r, frames, channels, o, st);
+    case AMX_PCM_F32BE: return pcm_t<AMX_PCM_F32BE>(r, frames, channels, o, st);
+    case AMX_PCM_F64BE: return pcm_t<AMX_PCM_F64BE>(r, frames, channels, o, st);
     default: return hipErrorInvalidValue;
     }
 }

@@ -1270,7 +1270,7 @@ int amx_pcm_to_s16(const void *d_raw, int64_t frames, int32_t channels, int32_t 
                    int16_t *d_out, void *stream) {
     if (frames < 0 || (frames > 0 && (!d_raw || !d_out))) return fail(AMX_EINVAL, "null argument");
     if (channels != 1 && channels != 2) return fail(AMX_EINVAL, "channels must be 1 or 2");
-    if (format < AMX_PCM_U8 || format > AMX_PCM_F64) return fail(AMX_EINVAL, "bad PCM format %d", format);
+    if (format < AMX_PCM_U8 || format > AMX_PCM_F64BE) return fail(AMX_EINVAL, "bad PCM format %d", format);
     HIPCHK(amx::launch_pcm_to_s16(d_raw, frames, channels, format, d_out, (hipStream_t)stream));
     return AMX_OK;
 }

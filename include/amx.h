@@ -190,6 +190,14 @@ AMX_API int amx_run_stage(amx_plan *plan, int32_t stage, const float *d_in, int1
 #define AMX_PCM_S32 3     /* v >> 16 */
 #define AMX_PCM_F32 4     /* clip(lrintf(v * 32768)) */
 #define AMX_PCM_F64 5     /* clip(lrint(v * 32768)) */
+/* big-endian PCM (AIFF / AIFF-C, the GUI's *.aiff, mastering_gui.py:170) and AIFF's
+ * signed 8-bit: the same conversions after the byte swap; s8: v << 8 */
+#define AMX_PCM_S8 6
+#define AMX_PCM_S16BE 7
+#define AMX_PCM_S24BE 8
+#define AMX_PCM_S32BE 9
+#define AMX_PCM_F32BE 10
+#define AMX_PCM_F64BE 11
 AMX_API int amx_pcm_to_s16(const void *d_raw, int64_t frames, int32_t channels, int32_t format,
                            int16_t *d_out, void *stream);
 

@@ -154,3 +154,80 @@ def test_process_audio_callbacks_and_mp3(gpu):
                           lambda a, b: pr.append((a, b)), art.append, tag.append)
         assert st[-1].startswith("Error: ") and pr[-1] == (0, 1)
         assert art == [None] and tag == ["Processing failed."]
+
+
+def _native_aiff(x, code):
+    if code.startswith("f"):
+        return x.astype(np.float32 if code == "f32be" else np.float64)
+    bits = {"s8": 8, "s16be": 16, "s16": 16, "s24be": 24, "s32be": 32}[code]
+    m = float((1 << (bits - 1)) - 1)
+    return np.clip(np.round(x.astype(np.float64) * m), -m - 1, m).astype(np.int64)
+
+
+@pytest.mark.parametrize("code", ["s8", "s16be", "s24be", "s32be", "f32be", "f64be"])
+@pytest.mark.parametrize("channels", [1, 2])
+def test_pcm_to_s16_decode_aiff(gpu, code, channels):
+    """the big-endian / signed-8-bit codes of amx_pcm_to_s16 on AIFF payloads equal the
+    host restatement of ffmpeg's conversions, edge values included"""
+    import torch
+    from amx import aiffio, capi, wavio
+    rng = np.random.default_rng(6)
+    n = 50003
+    if code.startswith("f"):
+        edge = np.array([0.0, -0.0, 1.0, -1.0, 1.5, -1.5, 0.5 / 32768, 1.5 / 32768, -0.5 / 32768,
+                         32767.5 / 32768, -32768.5 / 32768, 2.5 / 32768])
+        v = np.concatenate([edge, rng.uniform(-1.2, 1.2, n * channels - edge.size)])
+    else:
+        bits = {"s8": 8, "s16be": 16, "s24be": 24, "s32be": 32}[code]
+        lo, hi = -(1 << (bits - 1)), (1 << (bits - 1)) - 1
+        v = np.concatenate([[lo, hi, -1, 0, 1], rng.integers(lo, hi + 1, n * channels - 5)])
+    v = v.reshape(n, channels)
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "x.aiff")
+        aiffio.write_aiff(p, v if channels == 2 else v.reshape(-1), 48000, code)
+        raw, info, c = wavio.read_audio_raw(p)
+        want = wavio.to_s16(wavio.read_audio_native(p)[0], info)
+    assert c == code
+    if channels == 1:
+        want = np.repeat(want.reshape(-1, 1), 2, axis=1)
+    d_raw = torch.from_numpy(np.ascontiguousarray(raw)).cuda()
+    out = torch.empty((n, 2), dtype=torch.int16, device="cuda")
+    capi.check(capi.load().amx_pcm_to_s16(capi.ptr(d_raw), n, channels, capi.PCM_FORMATS[c],
+                                          capi.ptr(out), capi.ptr_stream()), "amx_pcm_to_s16")
+    np.testing.assert_array_equal(out.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("code,channels,seconds,settings", [
+    ("s16be", 2, 33.0, C3), ("s24be", 1, 12.0, dict(bass_boost=2.0, lufs=-16.0)),
+    ("f32be", 2, 20.0, C3), ("s8", 2, 6.0, dict(mid_cut=2.0)), ("s16", 2, 9.0, dict(C3, lufs=None)),
+])
+def test_master_audio_aiff(gpu, oracle_mod, code, channels, seconds, settings):
+    """master_audio from AIFF / AIFF-C files (the GUI's *.aiff): the reference's callbacks
+    and the oracle's output on the s16 chunks ffmpeg's split would write, bit for bit"""
+    import audio_mastering_engine as ame
+    from amx import aiffio, synth, wavio
+    from amx.chunking import chunk_bounds, packet_frames
+    fs = 44100
+    n = int(fs * seconds)
+    x = synth.mix_like(n, fs, channels, seed=int(seconds * 3) + channels)
+    nat = _native_aiff(x if channels == 2 else x.reshape(-1), code)
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "in.aiff"), os.path.join(d, "out.wav")
+        aiffio.write_aiff(src, nat, fs, code)
+        st, pr = [], []
+        out = ame.master_audio(dict(settings, input_file=src, output_file=dst), st.append,
+                               lambda a, b: pr.append((a, b)))
+        assert out == dst
+        y, info = wavio.read_wav_native(dst)
+        raw, ainfo, _ = wavio.read_audio_raw(src)
+        x16 = wavio.to_s16(wavio.read_audio_native(src)[0], ainfo)
+        if channels == 1:
+            x16 = x16.reshape(-1)
+        bounds = chunk_bounds(n, fs, packet_frames(ainfo.block_align))
+    assert info.sample_rate == fs and info.bits == 16 and info.channels == 2
+    want_st, want_pr = _expected_calls(len(bounds), settings.get("lufs") is not None)
+    assert st == want_st and pr == want_pr
+    ref, _ = oracle_mod.pipeline(x16, fs, settings, bounds)
+    assert y.shape == ref.shape
+    d = np.abs(y.astype(np.int32) - ref.astype(np.int32))
+    assert d.max() == 0, "max |diff| %d LSB" % d.max()

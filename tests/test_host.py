@@ -184,3 +184,48 @@ def test_rms_integer_form_matches_audioop():
                 if not (est + 1) ** 2 * cnt <= S and est * est * cnt > S:
                     r = est - 1
                 assert min(r, 32768) == ref, (S, cnt, est)
+
+
+@pytest.mark.parametrize("code", ["s8", "s16be", "s24be", "s32be", "f32be", "f64be", "s16"])
+@pytest.mark.parametrize("channels", [1, 2])
+def test_aiff_reader(tmp_path, code, channels):
+    """AIFF / AIFF-C (the GUI's *.aiff, mastering_gui.py:170): the parser's raw bytes,
+    PCM code and sample rate, and its native decode, round-trip through the test writer;
+    plain AIFF PCM is also read by the stdlib's independent aifc parser."""
+    import warnings
+    from amx import aiffio, capi, wavio
+    rng = np.random.default_rng(3)
+    n = 1001
+    if code.startswith("f"):
+        v = rng.uniform(-1.2, 1.2, (n, channels))
+    else:
+        bits = {"s8": 8, "s16be": 16, "s16": 16, "s24be": 24, "s32be": 32}[code]
+        v = rng.integers(-(1 << (bits - 1)), 1 << (bits - 1), (n, channels))
+    x = v if channels == 2 else v.reshape(-1)
+    p = str(tmp_path / "x.aiff")
+    aiffio.write_aiff(p, x, 44100, code)
+    raw, info, c = wavio.read_audio_raw(p)
+    assert c == code and c in capi.PCM_FORMATS and info.sample_rate == 44100 and info.channels == channels
+    assert raw.size == n * info.block_align
+    nat, info2 = wavio.read_audio_native(p)
+    want = v.astype(np.float32 if code == "f32be" else np.float64) if code.startswith("f") else v
+    if code == "s8":
+        want = v + 128                                   # pcm_s8 decodes to u8 (v + 0x80)
+    np.testing.assert_array_equal(nat, want.reshape(n, channels))
+    # ffmpeg's s16 values: 8-bit v << 8, 24/32-bit >> 8 / >> 16, floats lrint(v 32768)
+    s16 = wavio.to_s16(nat, info2)
+    if code == "s8":
+        np.testing.assert_array_equal(s16, (v << 8).reshape(n, channels))
+    if code in ("s8", "s16be", "s24be", "s32be"):
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", DeprecationWarning)
+            import aifc
+        with aifc.open(p, "rb") as f:
+            assert (f.getnchannels(), f.getframerate(), f.getnframes()) == (channels, 44100, n)
+            assert f.readframes(n) == raw.tobytes()
+
+
+def test_aiff_ext80_rates():
+    from amx import aiffio
+    for fs in (8000, 22050, 44100, 48000, 88200, 96000, 192000):
+        assert aiffio._ext80(aiffio._to_ext80(fs)) == fs
