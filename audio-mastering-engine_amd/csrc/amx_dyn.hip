@@ -38,19 +38,20 @@ typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 #define AMX_TAB 32769
 
 // ----------------------------------------- compressor RMS detector (exact)
-// One workgroup = AMX_RMS_F frames of one (chunk, band); squares of the window
-// [base - AMX_RMS_LOOKPAD, base + AMX_RMS_F) are prefix-summed in LDS (exact
-// int64), so S_i = P(i) - P(i - look) with no sequential sliding window.  Frames
-// before the chunk count as 0 (audioop.rms over the shorter window divides by the
-// frames present).  Loads are 16-B vectors (the LDS origin is 16-frame aligned);
+// One workgroup = AMX_RMS_N - LP frames of one (chunk, band); squares of the window
+// [base - LP, base + AMX_RMS_N - LP) are prefix-summed in LDS (exact int64), so
+// S_i = P(i) - P(i - look) with no sequential sliding window; LP is the smallest of
+// 256 / 512 / 1024 frames >= look (5 ms: 220 / 240 / 480 at 44.1 / 48 / 96 kHz), so the
+// halo re-read is 6-14 % and the 33 KB of prefix sums leave room for 4 workgroups per CU.
+// Frames before the chunk count as 0 (audioop.rms over the shorter window divides by
+// the frames present).  Loads are 16-B vectors (the LDS origin is 16-frame aligned);
 // the output is r_i itself (u16, clamped to 32768 = |sample| max), m is not formed here.
-#define AMX_RMS_F 4096
+#define AMX_RMS_N 4096
 #define AMX_RMS_MAXLOOK 1024
-#define AMX_RMS_LOOKPAD 1024
 
-// LDS index of prefix slot k: one spare slot per 80 keeps the scan's stores (lane
-// stride 20 slots, 16-lane ds_write_b64 groups) on 16 distinct bank pairs
-__device__ __forceinline__ int rms_slot(int k) { return k + k / 80; }
+// LDS index of prefix slot k: one spare slot per 16 keeps the scan's stores (lane
+// stride 17 slots, odd) on distinct bank pairs
+__device__ __forceinline__ int rms_slot(int k) { return k + (k >> 4); }
 
 // audioop.rms's (unsigned) sqrt((double) S / cnt), S = the window's exact sum of
 // squares (< 2^53, so the reference's double sum is exact), cnt the samples present.
@@ -72,25 +73,28 @@ __device__ __forceinline__ uint32_t rms_floor(uint64_t S, uint32_t cnt, double r
     return cnt ? (r > 32768u ? 32768u : r) : 0u;
 }
 
+template <int LP>
 __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ cdp,
                                                    const ChunkDev *__restrict__ chunks,
                                                    const uint32_t *__restrict__ bands,
                                                    uint16_t *__restrict__ mi, int64_t nloc) {
-    constexpr int N = AMX_RMS_F + AMX_RMS_LOOKPAD;
-    constexpr int PER = N / AMX_BLOCK;                 // 20 slots per thread
-    constexpr int VEC = PER / 4;                       // as 5 16-B loads
-    __shared__ unsigned long long P[N + N / 80];
+    constexpr int N = AMX_RMS_N;
+    constexpr int F = N - LP;                          // frames out per workgroup
+    constexpr int PER = N / AMX_BLOCK;                 // 16 slots per thread
+    constexpr int VEC = PER / 4;                       // as 4 16-B loads
+    static_assert(F % AMX_BLOCK == 0 && PER % 4 == 0, "tile shape");
+    __shared__ unsigned long long P[N + N / 16];
     __shared__ unsigned long long wsum[AMX_BLOCK / 64];
     const int look = cdp->look;
     const int c = blockIdx.y, b = blockIdx.z;
     const ChunkDev ch = chunks[c];
-    const int64_t base = (int64_t)blockIdx.x * AMX_RMS_F;
+    const int64_t base = (int64_t)blockIdx.x * F;
     if (base >= ch.n) return;                          // block-uniform
     const uint32_t *x = bands + b * nloc + ch.loc_off;
     uint16_t *mo = mi + b * nloc + ch.loc_off;
     const int64_t rowlen = (ch.n + 15) / 16 * 16;     // the chunk row (16-frame aligned)
-    // LDS slot k holds frame base - LOOKPAD + k
-    const int64_t f0 = base - AMX_RMS_LOOKPAD;
+    // LDS slot k holds frame base - LP + k
+    const int64_t f0 = base - LP;
     const int t = threadIdx.x;
     // a0^2 + a1^2 <= 2^31: one frame's squares fit a u32
     uint32_t v[PER];
@@ -132,20 +136,19 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
     __syncthreads();
     unsigned long long p = incl - run;
     for (int q = 0; q < w; q++) p += wsum[q];
-    const int s0 = rms_slot(t * PER);                  // the thread's 20 slots share one pad
+    const int s0 = rms_slot(t * PER);                  // the thread's 16 slots share one pad
 #pragma unroll
     for (int q = 0; q < PER; q++) { p += v[q]; P[s0 + q] = p; }
     __syncthreads();
-    // frame i = base + nn uses slots [nn + LOOKPAD - look, nn + LOOKPAD)
-    constexpr int OUT = AMX_RMS_F / AMX_BLOCK;
+    // frame i = base + nn uses slots [nn + LP - look, nn + LP)
+    constexpr int OUT = F / AMX_BLOCK;
     const uint32_t cfull = 2u * (uint32_t)look;
     const double rfull = 1.0 / (double)cfull;
-    const bool whole = base >= look && base + AMX_RMS_F <= ch.n;   // block-uniform
+    const bool whole = base >= look && base + F <= ch.n;   // block-uniform
     auto rms_at = [&](int k) -> uint32_t {
         const uint32_t nn = (uint32_t)t + (uint32_t)k * AMX_BLOCK;
-        const uint32_t e1 = nn + (AMX_RMS_LOOKPAD - 1), e0 = e1 - (uint32_t)look;
-        // e / 80 for e < 2^13 as (e * 52429) >> 22
-        const uint64_t S = P[e1 + (__umul24(e1, 52429u) >> 22)] - P[e0 + (__umul24(e0, 52429u) >> 22)];
+        const uint32_t e1 = nn + (LP - 1), e0 = e1 - (uint32_t)look;
+        const uint64_t S = P[e1 + (e1 >> 4)] - P[e0 + (e0 >> 4)];
         if (whole) return rms_floor(S, cfull, rfull);
         const int64_t i = base + nn;
         const bool head = i < look;                    // a chunk's first look frames
@@ -838,12 +841,20 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
 }
 
 // ---------------------------------------------------------------- launchers
+template <int LP>
+static void rms_t(const DynLaunch &d, const int16_t *bands, uint16_t *m) {
+    constexpr int F = AMX_RMS_N - LP;
+    dim3 g((unsigned)((d.max_chunk_n + F - 1) / F), (unsigned)d.n_chunks, 3);
+    if (empty(g)) return;
+    hipLaunchKernelGGL(k_rms<LP>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks,
+                       reinterpret_cast<const uint32_t *>(bands), m, d.nloc);
+}
+
 hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m) {
     if (d.look > AMX_RMS_MAXLOOK) return hipErrorInvalidValue;
-    dim3 g((unsigned)((d.max_chunk_n + AMX_RMS_F - 1) / AMX_RMS_F), (unsigned)d.n_chunks, 3);
-    if (empty(g)) return hipSuccess;
-    hipLaunchKernelGGL(k_rms, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks,
-                       reinterpret_cast<const uint32_t *>(bands), m, d.nloc);
+    if (d.look <= 256) rms_t<256>(d, bands, m);
+    else if (d.look <= 512) rms_t<512>(d, bands, m);
+    else rms_t<1024>(d, bands, m);
     return hipGetLastError();
 }
 
