@@ -29,17 +29,22 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_scan_blk(const ScanBlk *__restric
                                                         const double *__restrict__ Mbk, int K,
                                                         const double *__restrict__ carry,
                                                         double *__restrict__ eb) {
-    static_assert(GP >= D && GP <= 64 && (64 % GP) == 0, "group must tile a wave");
-    constexpr int GPB = AMX_BLOCK / GP;
+    // GW groups of GP lanes in each wave (a group never straddles waves, so wave
+    // barriers order its LDS exchange); lanes past GW GP are idle.  GP = D packs the
+    // groups: D = 20 -> 3 groups per wave (60 lanes) instead of 2 of 32.
+    static_assert(GP >= D && GP <= 64, "group fits a wave");
+    constexpr int GW = 64 / GP;
+    constexpr int GPB = GW * (AMX_BLOCK / 64);
     __shared__ __attribute__((aligned(16))) double lds[AMX_BLOCK];
-    const int t = threadIdx.x;
-    const int gi = t / GP, i = t % GP;
-    const int64_t g = (int64_t)blockIdx.x * GPB + gi;     // (block, channel) = 2 b + ch
-    const bool gvalid = g < 2LL * n_blk;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int gl = l / GP, i = l % GP;
+    const bool lane_ok = gl < GW;
+    const int64_t g = (int64_t)blockIdx.x * GPB + w * GW + (lane_ok ? gl : 0);   // (block, channel) = 2 b + ch
+    const bool gvalid = lane_ok && g < 2LL * n_blk;
     const int b = gvalid ? (int)(g >> 1) : 0;
     const int ch = (int)(g & 1);
     const ScanBlk bk = blks[b];
-    const bool row = i < D;
+    const bool row = lane_ok && i < D;
     const int ri = row ? i : 0;
     double mrow[D];
 #pragma unroll
@@ -54,7 +59,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_scan_blk(const ScanBlk *__restric
         const int64_t jj = (int64_t)bk.seg0 + qq;
         ev[q] = e[(jj * 2 + ch) * D + ri];
     }
-    double *my = lds + gi * GP;
+    // an idle lane reads group 0's vector (discarded) and writes nothing
+    double *my = lds + w * 64 + (lane_ok ? gl * GP : 0);
     double v = 0.0;
     if constexpr (DOWN) {
         // block start state: windowed sum over the previous K blocks of the stream
@@ -67,7 +73,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_scan_blk(const ScanBlk *__restric
         for (int k = 1; k < K; k++) {
             const int bb = b - k;
             const bool ok = gvalid && bb >= bk.first;
-            my[i] = (ok && row) ? xin(bb) : 0.0;
+            if (lane_ok) my[i] = (ok && row) ? xin(bb) : 0.0;
             __builtin_amdgcn_wave_barrier();
             const double *P = Mbk + ((int64_t)(k - 1) * D + ri) * D;
             double a0 = 0.0, a1 = 0.0;
@@ -88,7 +94,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_scan_blk(const ScanBlk *__restric
             if (row) s[(jj * 2 + ch) * D + i] = v;
             if (q == n - 1) break;                         // the next block has its own B
         }
-        my[i] = v;
+        if (lane_ok) my[i] = v;
         __builtin_amdgcn_wave_barrier();
         // four partial sums: the dependent fp64 FMA latency (~30 cycles) would
         // otherwise serialise D FMAs per step
@@ -122,7 +128,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_scan_blk(const ScanBlk *__restric
 template <int D, int GP>
 static hipError_t scan_t(const ScanPlan &p, const double *e, double *s, const double *carry,
                          double *eb, hipStream_t st) {
-    constexpr int GPB = AMX_BLOCK / GP;
+    constexpr int GPB = (64 / GP) * (AMX_BLOCK / 64);
     const dim3 gb((unsigned)((2 * (int64_t)p.n_blk + GPB - 1) / GPB));
     hipLaunchKernelGGL((k_scan_blk<D, GP, false>), gb, dim3(AMX_BLOCK), 0, st, p.blks, p.n_blk, e,
                        s, p.M, p.Mbk, p.K, carry, eb);
@@ -138,11 +144,11 @@ hipError_t launch_scan(const ScanPlan &p, const double *e, double *s, const doub
     case 2: return scan_t<2, 2>(p, e, s, carry, eb, st);
     case 4: return scan_t<4, 4>(p, e, s, carry, eb, st);
     case 8: return scan_t<8, 8>(p, e, s, carry, eb, st);
-    case 10: return scan_t<10, 16>(p, e, s, carry, eb, st);
-    case 12: return scan_t<12, 16>(p, e, s, carry, eb, st);
+    case 10: return scan_t<10, 10>(p, e, s, carry, eb, st);
+    case 12: return scan_t<12, 12>(p, e, s, carry, eb, st);
     case 16: return scan_t<16, 16>(p, e, s, carry, eb, st);
-    case 18: return scan_t<18, 32>(p, e, s, carry, eb, st);
-    case 20: return scan_t<20, 32>(p, e, s, carry, eb, st);
+    case 18: return scan_t<18, 18>(p, e, s, carry, eb, st);
+    case 20: return scan_t<20, 20>(p, e, s, carry, eb, st);
     }
     return hipErrorInvalidValue;
 }
