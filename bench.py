@@ -74,9 +74,9 @@ def stage_bytes(stage, frames, ch_in):
         "loud2": 4,                     # K-filter recursion: reads the track once
         "final": 4 + 4,                 # gain + limiter: track in -> output
         "xover": 4 + 12,                # P -> 3 bands
-        "rms": 12 + 24,                 # 3 bands -> 3 x f64 max attenuation m
-        "env": 24 + 1.5,                # m once -> 3 x f64 checkpoint per 16 frames
-        "apply": 12 + 24 + 1.5 + 4,     # bands + m + checkpoints -> output
+        "rms": 12 + 6,                  # 3 bands -> 3 x u16 rms index r (m = table[r])
+        "env": 6 + 1.5,                 # r once -> 3 x f64 checkpoint per 16 frames
+        "apply": 12 + 6 + 1.5 + 4,      # bands + r + checkpoints -> output
     }
     return per.get(stage, 0) * frames
 
