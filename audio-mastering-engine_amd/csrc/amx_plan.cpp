@@ -241,7 +241,7 @@ struct amx_plan {
     int mask = 0, D = 0;
     int lev_eq = 0, lev_x = 0, lev_kw = 0;
     int mb = 0;
-    int Le = 1024, warm = 2048, rounds = 2;   // compressor envelope segments (amx_dyn.hip)
+    int Le = 1024, warm = 2304, rounds = 2;   // compressor envelope segments (amx_dyn.hip)
     int env_wg = 1, env_pin = 0;              // k_env0 placement (amx_dyn.hip launch_env)
     int n_es = 0;
     std::vector<SegDev> esegs;

@@ -95,7 +95,7 @@ typedef struct amx_chain_desc {
                                      log/pow, which is what CPython's math uses (pydub) */
     /* compressor envelope parallelisation (amx_dyn.hip); results are exact for any
      * values, these only move work between the speculative and the fix-up passes */
-    int32_t env_warm_frames;      /* speculative warm-up per envelope segment (rounded up to 64); <0 -> 2048 */
+    int32_t env_warm_frames;      /* speculative warm-up per envelope segment (rounded up to 128); <0 -> 2304 */
     int32_t env_rounds;           /* parallel fix-up rounds before the in-order walk (0..16); <0 -> 2 */
 } amx_chain_desc;
 
