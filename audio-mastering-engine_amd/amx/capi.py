@@ -84,13 +84,13 @@ class TrackSpan(ctypes.Structure):
 
 
 # every symbol include/amx.h declares (checked by the CPU test suite)
-EXPORTS = ("amx_abi_version", "amx_last_error", "amx_plan_create", "amx_plan_free",
+EXPORTS = ("amx_abi_version", "amx_last_error", "amx_build_id", "amx_plan_create", "amx_plan_free",
            "amx_plan_get_info", "amx_plan_track_span", "amx_run_chunks", "amx_run_stage",
            "amx_loudness_pass1", "amx_loudness_pass1_part",
            "amx_kw_propagate", "amx_loudness_pass2", "amx_loudness_histograms",
            "amx_limiter_geometry", "amx_limiter_prepare", "amx_loudness_decide", "amx_kw_carry_setup", "amx_kw_carry",
            "amx_finalize", "amx_env_counters", "amx_pcm_to_s16", "amx_loudnorm_192k_size",
-           "amx_loudnorm_192k")
+           "amx_loudnorm_192k", "amx_loudnorm_192k_ex")
 PCM_FORMATS = {"u8": 0, "s16": 1, "s24": 2, "s32": 3, "f32": 4, "f64": 5,
                "s8": 6, "s16be": 7, "s24be": 8, "s32be": 9, "f32be": 10, "f64be": 11}
 
@@ -139,10 +139,26 @@ def load(path=None):
                                          ctypes.POINTER(ctypes.c_int64)]
     L.amx_loudnorm_192k.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(LoudnormDesc), vp, vp,
                                     ctypes.c_int64, vp, vp, vp, vp, vp]
+    L.amx_loudnorm_192k_ex.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(LoudnormDesc), vp, vp, vp, vp,
+                                       ctypes.c_int64, vp, vp, vp, vp, vp]
     if L.amx_abi_version() != ABI_VERSION:
         raise AmxError("libamx ABI version mismatch")
+    L.amx_build_id.restype = ctypes.c_char_p
+    stamp = L.amx_build_id().decode()
+    if p == LIB_PATH:
+        # provenance: the in-tree library must be compiled from the sources of this tree
+        from . import build
+        want = build.source_hash()
+        if stamp != want:
+            raise AmxError("libamx.so at %s was built from sources %s, this tree's are %s: "
+                           "rebuild it (amx.build.build())" % (p, stamp[:16], want[:16]))
     _lib = L
     return L
+
+
+def build_id():
+    """the source hash stamped into the loaded library (amx_build_id)"""
+    return load().amx_build_id().decode()
 
 
 def check(rc, what):

@@ -280,12 +280,17 @@ class MasteringJob:
     def _dyn_result(self, run, stream):
         with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
             prof = run["summ"].cpu().numpy()
-        return run["job2"].y[:run["n192"]], {
-            "target_offset": run["target_offset"], "pass1_output_i": run["i_out"],
-            "sample_rate": 192000,
-            "pass2_cycles": {k: float(prof[i]) for i, k in enumerate(
+        info = {"target_offset": run["target_offset"], "pass1_output_i": run["i_out"],
+                "sample_rate": 192000}
+        if prof[12] > 0 and prof[13] == 0:
+            # the parallel form (amx_loudnorm.hip k_lp_*): its walker's diagnostics
+            info["pass2_parallel"] = {"segments": int(prof[12]), "reruns": int(prof[10]),
+                                      "final_rerun": bool(prof[11])}
+        else:
+            info["pass2_cycles"] = {k: float(prof[i]) for i, k in enumerate(
                 ("fill", "detect", "envelope", "output", "stats", "r128_out",
-                 "detect_calls", "serial_chunks"), start=2)}}
+                 "detect_calls", "serial_chunks"), start=2)}
+        return run["job2"].y[:run["n192"]], info
 
     # ------------------------------------------------------------ report
     def fetch_report(self, raise_dynamic=True):

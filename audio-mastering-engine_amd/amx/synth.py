@@ -67,6 +67,23 @@ def to_s16(x):
     return np.clip(y, -32768, 32767).astype(np.int16)
 
 
+def mix_tiled(n_frames, sample_rate, channels=2, seed=0, block_seconds=60.0):
+    """mix_like of one block_seconds block, repeated (each repeat circularly shifted by a
+    seeded amount) to n_frames: the same kind of program at a fraction of the host time
+    (mix_like costs ~1 s per 20 s of 48 kHz stereo), for long benchmark inputs."""
+    n = int(n_frames)
+    nb = min(n, int(block_seconds * sample_rate))
+    if n == 0 or nb == n:
+        return mix_like(n, sample_rate, channels, seed)
+    blk = mix_like(nb, sample_rate, channels, seed)
+    rng = np.random.default_rng(SEED_BASE + 2000 + int(seed))
+    out = np.empty((n, channels), np.float32)
+    for o in range(0, n, nb):
+        k = min(nb, n - o)
+        out[o:o + k] = np.roll(blk, int(rng.integers(0, nb)), axis=0)[:k]
+    return out
+
+
 def mix_like(n_frames, sample_rate, channels=2, seed=0, peak_dbfs=-3.0):
     """A "mixed" program signal with a modest peak-to-loudness ratio (~9-11 dB):
     a bass line of partials in 110-240 Hz, mid/high partials and 1/f noise, slow

@@ -23,6 +23,16 @@ __device__ __forceinline__ int16_t f64_to_s16(double x) {
     v = v * 32767.0;
     return (int16_t)(int)v;
 }
+// "%.2f" then float(): the exact decimal rounding (half-even on exact ties) of v (the
+// loudnorm statistics strings the reference parses, :237-241)
+__device__ __forceinline__ double round2(double v) {
+    if (!isfinite(v)) return v;
+    const double p = v * 100.0;
+    const double err = fma(v, 100.0, -p);        // v*100 == p + err exactly
+    double k = rint(p);
+    if (fabs(p - k) == 0.5 && err != 0.0) k = err > 0.0 ? floor(p) + 1.0 : floor(p);
+    return k / 100.0;
+}
 __device__ __forceinline__ int16_t sat16(int v) {
     return (int16_t)(v > 32767 ? 32767 : (v < -32768 ? -32768 : v));
 }

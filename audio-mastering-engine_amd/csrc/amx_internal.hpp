@@ -222,9 +222,47 @@ struct LnArgs {
     double measured_i, measured_thresh, offset;   // offset linear
     double weights[21];           // init_gaussian_filter
     double kb[5], ka[5];          // libebur128 K filter at 192 kHz (direct form)
+    // set when the parallel form (LpArgs) runs first: this kernel then only runs the
+    // tracks it hands over (lp_ctl[0] != 0) with the options it resolved (lp_dctl)
+    const int *lp_ctl;
+    const double *lp_dctl;
 };
-hipError_t launch_loudnorm(const LnArgs &a, const uint32_t *x, int64_t n_in, int L, int M,
-                           const float *bank, hipStream_t st);
+// af_loudnorm dynamic mode in parallel form (amx_loudnorm.hip):
+// per-frame statistics and gains from pass 1's hop energies, then the true-peak
+// limiter as warmed-up segments of 100 ms frames with an in-order check and repair.
+#define AMX_LN_RING 40320          // frame_size(192000, 210): the limiter ring, frames
+#define AMX_LN_WIN 2048            // ring frames compared at a segment boundary
+#define AMX_LN_REC (16 + 2 * AMX_LN_WIN)   // doubles of one boundary state record
+struct LpArgs {
+    int64_t n;                    // 192 kHz frames
+    int64_t S0;                   // first output frame of the FINAL (flush) frame
+    int T, nb_last;               // INNER frames, frames of the last one
+    int Fs, Wf;                   // frames per segment, warm-up frames
+    int J, M, K, P;               // INNER segments after segment 0, FINAL segments, all, waves
+    const float *u;               // [n][2] the resampled stream
+    const double *hops;           // [>= n / 19200 + 1][2] pass-1 hop energies (r128_in)
+    const double *energies, *bounds;
+    double target_i, target_lra, ceiling, measured_i, measured_thresh, offset;  // host values
+    const double *measured_src;   // non-NULL: measured I / thresh from this k_decide row ([4], [7])
+    const double *offset_src;     // non-NULL: offset = "%.2f"(target_i - offset_src[0]) dB
+    double weights[21];
+    double *v;                    // [T] AGC value of each INNER frame (when not held)
+    int *hold;                    // [T] 1: the frame keeps the previous delta
+    double *D;                    // [T] delta written by each INNER frame
+    double *G;                    // [T + 1] Gaussian-smoothed gain of each INNER frame, FINAL's
+    double *ramp;                 // [19200] i / 19200.0
+    double *recG, *recE;          // [K][AMX_LN_REC] guessed start / end states per segment
+    double *wrec;                 // [2][AMX_LN_REC] walker-made end states
+    int *cnt, *match;             // [K + 1] boundary arrivals, start guess == previous end
+    double *rings;                // [P][AMX_LN_RING][2] per-wave limiter rings
+    double *wring;                // [AMX_LN_RING][2] the walker's ring
+    int *ctl;                     // [16] 0 serial, 1 re-runs, 2 FINAL re-run, 3 above_threshold
+    double *dctl;                 // [8] 0 d0, 1 offset (linear), 2 measured_i, 3 measured_thresh
+    int16_t *y;                   // [n][2] output
+    double *summary;              // [16]
+};
+hipError_t launch_loudnorm(const LnArgs &a, const LpArgs &p, const uint32_t *x, int64_t n_in, int L,
+                           int M, const float *bank, hipStream_t st);
 hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent_t fork, hipEvent_t join);
 int swr_geometry(int in_rate, int out_rate, int *L, int *M);   // host (amx_plan.cpp)
 int swr_bank(int in_rate, int out_rate, float *bank);

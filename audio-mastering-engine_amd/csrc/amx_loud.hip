@@ -506,15 +506,7 @@ hipError_t launch_kw_tail(const SpanDev *spans, int n_tracks, const double *s, c
 // non-empty histogram bins are compacted in ascending order (adding an empty bin's
 // 0.0 is exact) and lane 0 runs the sequential double sums over them.
 
-// "%.2f" then float(): the exact decimal rounding (half-even on exact ties) of v
-__device__ double round2(double v) {
-    if (!isfinite(v)) return v;
-    const double p = v * 100.0;
-    const double err = fma(v, 100.0, -p);        // v*100 == p + err exactly
-    double k = rint(p);
-    if (fabs(p - k) == 0.5 && err != 0.0) k = err > 0.0 ? floor(p) + 1.0 : floor(p);
-    return k / 100.0;
-}
+// round2 ("%.2f" then float()): amx_dev.hpp
 
 __device__ __forceinline__ double lufs_of(double e) { return 10 * log10(e) - 0.691; }
 

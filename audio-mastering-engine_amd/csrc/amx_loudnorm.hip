@@ -178,10 +178,13 @@ __device__ void ln_global(LnShared &L, double &global, double &rel_thr) {
 }
 
 // gating block ending at hop k (k >= 4): the mean square of hops k-4 .. k-1
-__device__ __forceinline__ void ln_add_block(LnShared &L, const double *hops, int64_t k) {
+__device__ __forceinline__ double ln_block_energy(const double *hops, int64_t k) {
     const double c0 = ((hops[2 * (k - 4)] + hops[2 * (k - 3)]) + hops[2 * (k - 2)]) + hops[2 * (k - 1)];
     const double c1 = ((hops[2 * (k - 4) + 1] + hops[2 * (k - 3) + 1]) + hops[2 * (k - 2) + 1]) + hops[2 * (k - 1) + 1];
-    const double en = (c0 + c1) / (double)(4 * LN_FR);
+    return (c0 + c1) / (double)(4 * LN_FR);
+}
+__device__ __forceinline__ void ln_add_block(LnShared &L, const double *hops, int64_t k) {
+    const double en = ln_block_energy(hops, k);
     __syncthreads();
     if (threadIdx.x == 0 && en >= L.B[0]) L.hist[ln_find_bin(L.B, en)] += 1u;
     __syncthreads();
@@ -510,7 +513,16 @@ __device__ double ln_out_energy(const double *ring, int lbi, int nb, double ceil
     return r;
 }
 
-__global__ void __launch_bounds__(LN_NT) k_ln_dyn(LnArgs a) {
+__global__ void __launch_bounds__(LN_NT) k_ln_dyn(LnArgs a0) {
+    // after the parallel form's statistics (k_lp_stats): only the tracks it hands over
+    // (the < 3 s linear fallback, a quiet start), with the options it resolved
+    if (a0.lp_ctl && a0.lp_ctl[0] == 0) return;
+    LnArgs a = a0;
+    if (a0.lp_dctl) {
+        a.offset = a0.lp_dctl[1];
+        a.measured_i = a0.lp_dctl[2];
+        a.measured_thresh = a0.lp_dctl[3];
+    }
     __shared__ LnShared L;
     const int tid = threadIdx.x;
     for (int i = tid; i < 1000; i += LN_NT) { L.hist[i] = 0u; L.E[i] = a.energies[i]; }
@@ -536,7 +548,12 @@ __global__ void __launch_bounds__(LN_NT) k_ln_dyn(LnArgs a) {
             a.y[2 * j] = ln_s16((double)u[2 * j] * off);
             a.y[2 * j + 1] = ln_s16((double)u[2 * j + 1] * off);
         }
-        if (tid == 0) { a.summary[0] = 1.0; a.summary[1] = off; }
+        if (tid == 0) {
+            a.summary[0] = 1.0;
+            a.summary[1] = off;
+            for (int q = 10; q < 13; q++) a.summary[q] = 0.0;
+            a.summary[13] = (a0.lp_ctl && a0.lp_ctl[0] == 2) ? 1.0 : 0.0;
+        }
         return;
     }
     // ---- FIRST frame (3 s)
@@ -695,15 +712,788 @@ __global__ void __launch_bounds__(LN_NT) k_ln_dyn(LnArgs a) {
         a.summary[7] = (double)P.feed;
         a.summary[8] = (double)P.n_detect;
         a.summary[9] = (double)P.n_serial;
+        for (int q = 10; q < 13; q++) a.summary[q] = 0.0;
+        a.summary[13] = (a0.lp_ctl && a0.lp_ctl[0] == 2) ? 1.0 : 0.0;   // handed over by k_lp_walk
     }
 }
 
-hipError_t launch_loudnorm(const LnArgs &a, const uint32_t *x, int64_t n_in, int L, int M,
-                           const float *bank, hipStream_t st) {
-    if (a.n192 <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ln_upsample, dim3((unsigned)((a.n192 + AMX_BLOCK - 1) / AMX_BLOCK)), dim3(AMX_BLOCK),
-                       0, st, x, n_in, L, M, bank, a.n192, a.u);
-    hipLaunchKernelGGL(k_ln_dyn, dim3(1), dim3(LN_NT), 0, st, a);
+// ======================================================================
+// Dynamic mode in parallel form.  k_ln_dyn above runs af_loudnorm
+// frame by frame on one workgroup; it stays the path for the < 3 s linear fallback
+// and for a track whose first 3 s are below measured_thresh (above_threshold 0: the
+// output's own short-term loudness then steers the gains).  Every other track -- the
+// reference's pass 1 always, pass 2 unless the track starts quietly -- runs here:
+//  1. With above_threshold 1 the AGC value an INNER frame t writes depends only on
+//     r128_in after that frame (3 s short-term, gated integrated loudness, relative
+//     gate), i.e. on pass 1's hop energies of this 192 kHz stream: k_lp_stats forms
+//     every frame's value at once, k_lp_dscan the deltas (a held frame keeps the
+//     previous delta: a last-valid scan), k_lp_gains the Gaussian gain of every frame
+//     (frame t's fill uses the deltas of frames t-30 .. t-10).
+//  2. The limiter ring then holds a known stream: every fill is u * gain ramp * offset.
+//     A wave keeps only the slots the limiter has multiplied (one flag bit per slot in
+//     LDS, the values in a per-wave ring in HBM); an unflagged slot's value is formed
+//     from u when read.  The ring is literal -- slot indices, wrap reads and FINAL's
+//     re-basing are af_loudnorm's own -- so a frame with the limiter idle costs a
+//     64-wide peak scan and the output pass.
+//  3. The limiter forgets: two runs that differ at some frame agree again after a
+//     release completes or a new deepest reduction is attacked.  k_lp_seg runs every
+//     segment of Fs frames at once, each from rest Wf frames early, and records its
+//     guessed start state and its end state (the scalars and the 2048 ring slots from
+//     the frame start: every slot multiplied and not yet output lies there; a record
+//     with a flag outside is marked and never matches); the second of two neighbours
+//     to finish compares them.  k_lp_walk walks the boundaries in order and re-runs,
+//     with output, any segment whose start guess was wrong, from the true state.
+// Every output sample is the reference's operation sequence applied from the true
+// state, so the result equals k_ln_dyn's given the same gains.
+#define LP_FR LN_FR
+#define LP_FIRST LN_FIRST
+#define LP_RS AMX_LN_RING
+#define LP_ATT LN_ATT
+#define LP_FW (LP_RS / 32)       // flag words per ring
+#define LP_NFIN 29               // FINAL's 100 ms sub-frames: (576000 - 19200) / 19200
+#define LP_REC AMX_LN_REC
+#define LP_WIN AMX_LN_WIN
+#define LP_STAT_NT 256
+#define LP_STAT_F 16             // INNER frames per k_lp_stats workgroup
+#define LP_DIRTY 7               // record slot: 1 = a flagged slot lies outside the window
+
+enum { LO_OUT = 0, LO_ATTACK, LO_SUSTAIN, LO_RELEASE };
+
+__device__ __forceinline__ double lp_bsum(double v, double *red) {
+    v = ln_wsum(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double r = 0.0;
+#pragma unroll
+    for (int w = 0; w < LP_STAT_NT / 64; w++) r += red[w];
+    return r;
+}
+
+// 3 s short-term loudness ending at hop k (hops k-30 .. k-1), every thread
+__device__ __forceinline__ double lp_shortterm(const double *hops, int64_t k, double *red) {
+    double c0 = 0.0, c1 = 0.0;
+    if (threadIdx.x < 30 && k - 30 + (int)threadIdx.x >= 0) {
+        c0 = hops[2 * (k - 30 + threadIdx.x)];
+        c1 = hops[2 * (k - 30 + threadIdx.x) + 1];
+    }
+    return 10 * log10((lp_bsum(c0, red) + lp_bsum(c1, red)) / (double)LP_FIRST) - 0.691;
+}
+
+// frame statistics: block 0 the FIRST frame and the resolved options; block b > 0
+// the INNER frames [16 (b - 1), 16 b): the histogram of the blocks before them, then
+// frame by frame its block, the gated loudness, the short-term loudness, the value
+__global__ void __launch_bounds__(LP_STAT_NT) k_lp_stats(LpArgs a) {
+    __shared__ unsigned hist[1000];
+    __shared__ double E[1000], B[1001], red[LP_STAT_NT / 64];
+    const int tid = threadIdx.x;
+    const double mi = a.measured_src ? a.measured_src[4] : a.measured_i;
+    const double mt = a.measured_src ? a.measured_src[7] : a.measured_thresh;
+    if (blockIdx.x == 0) {
+        const bool full = a.n >= LP_FIRST;
+        const double st = full ? lp_shortterm(a.hops, LP_FIRST / LP_FR, red) : 0.0;
+        if (tid == 0) {
+            const bool above = !(st < mt);
+            const double env = st <= -70. ? 0. : a.target_i - (above ? st : mi);
+            a.ctl[0] = (full && above) ? 0 : 1;
+            a.ctl[1] = 0;
+            a.ctl[2] = 0;
+            a.ctl[3] = above ? 1 : 0;
+            a.dctl[0] = pow(10., env / 20.);
+            a.dctl[1] = a.offset_src ? pow(10., round2(a.target_i - a.offset_src[0]) / 20.) : a.offset;
+            a.dctl[2] = mi;
+            a.dctl[3] = mt;
+        }
+        return;
+    }
+    const int t0 = (blockIdx.x - 1) * LP_STAT_F;
+    if (a.n < LP_FIRST || t0 >= a.T) return;
+    for (int i = tid; i < 1000; i += LP_STAT_NT) { hist[i] = 0u; E[i] = a.energies[i]; }
+    for (int i = tid; i < 1001; i += LP_STAT_NT) B[i] = a.bounds[i];
+    __syncthreads();
+    // gating blocks ending at hops 4 .. 30 + t0 (the FIRST frame's and every full INNER
+    // frame's before t0)
+    for (int64_t k = 4 + tid; k <= 30 + t0; k += LP_STAT_NT) {
+        const double en = ln_block_energy(a.hops, k);
+        if (en >= B[0]) atomicAdd(&hist[ln_find_bin(B, en)], 1u);
+    }
+    __syncthreads();
+    for (int j = 0; j < LP_STAT_F && t0 + j < a.T; j++) {
+        const int t = t0 + j;
+        const bool full = t < a.T - 1 || a.nb_last == LP_FR;
+        const int64_t kt = full ? 31 + t : 30 + t;        // r128_in's hops after this frame
+        if (full && tid == 0) {
+            const double en = ln_block_energy(a.hops, kt);
+            if (en >= B[0]) hist[ln_find_bin(B, en)] += 1u;
+        }
+        __syncthreads();
+        // ebur128 gated loudness and relative threshold (ln_global's arithmetic)
+        double s = 0.0, c = 0.0;
+        for (int q = tid; q < 1000; q += LP_STAT_NT) { s += (double)hist[q] * E[q]; c += (double)hist[q]; }
+        s = lp_bsum(s, red);
+        c = lp_bsum(c, red);
+        double global = -HUGE_VAL, rel_thr = -70.0;
+        if (c != 0.0) {
+            double rel = s / c;
+            rel *= 0.1;
+            rel_thr = 10 * log10(rel) - 0.691;
+            int start;
+            if (rel < B[0]) start = 0;
+            else {
+                start = ln_find_bin(B, rel);
+                if (rel > E[start]) ++start;
+            }
+            double g = 0.0, ab = 0.0;
+            for (int q = start + tid; q < 1000; q += LP_STAT_NT) { g += (double)hist[q] * E[q]; ab += (double)hist[q]; }
+            g = lp_bsum(g, red);
+            ab = lp_bsum(ab, red);
+            global = ab == 0.0 ? -HUGE_VAL : 10 * log10(g / ab) - 0.691;
+        }
+        const double st = lp_shortterm(a.hops, kt, red);
+        if (tid == 0) {
+            const bool hold = st < rel_thr || st <= -70.;
+            a.hold[t] = hold ? 1 : 0;
+            double v = 0.0;
+            if (!hold) {
+                const double env_global = fabs(st - global) < (a.target_lra / 2.)
+                                              ? st - global
+                                              : (a.target_lra / 2.) * ((st - global) < 0 ? -1 : 1);
+                const double env_shortterm = a.target_i - st;
+                v = pow(10., (env_global + env_shortterm) / 20.);
+            }
+            a.v[t] = v;
+        }
+    }
+}
+
+// the delta each INNER frame writes: its value, or (held) the previous frame's; the
+// FIRST frame's d0 before any value.  One workgroup: last-valid index scan.
+__global__ void __launch_bounds__(1024) k_lp_dscan(LpArgs a) {
+    if (a.ctl[0]) return;
+    __shared__ int s[1024];
+    const int tid = threadIdx.x, T = a.T;
+    const int per = (T + 1023) / 1024, lo = tid * per, hi = min(T, lo + per);
+    int last = -1;
+    for (int t = lo; t < hi; t++)
+        if (!a.hold[t]) last = t;
+    s[tid] = last;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = tid >= o ? s[tid - o] : -1;
+        __syncthreads();
+        s[tid] = max(s[tid], v);
+        __syncthreads();
+    }
+    int cur = tid > 0 ? s[tid - 1] : -1;
+    const double d0 = a.dctl[0];
+    for (int t = lo; t < hi; t++) {
+        if (!a.hold[t]) cur = t;
+        a.D[t] = cur >= 0 ? a.v[cur] : d0;
+    }
+}
+
+// G[t] = gaussian_filter at INNER frame t (t = T: the FINAL frame's gain): the 21
+// weights over the deltas of frames t-30 .. t-10 (the FIRST frame's d0 before 0),
+// summed in af_loudnorm's order; and the fill ramp i / 19200
+__global__ void __launch_bounds__(256) k_lp_gains(LpArgs a) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (int64_t i = g; i < LP_FR; i += (int64_t)gridDim.x * 256) a.ramp[i] = (double)i / (double)LP_FR;
+    if (a.ctl[0] || g > a.T) return;
+    const int t = (int)g;
+    const double d0 = a.dctl[0];
+    double r = 0.;
+#pragma unroll
+    for (int i = 0; i < 21; i++) {
+        const int f = t + i - 30;
+        r += (f >= 0 ? a.D[f] : d0) * a.weights[i];
+    }
+    a.G[t] = r;
+}
+
+// ------------------------------------------------------------ one wave's limiter
+// Frame phi: 0 = FIRST, 1 .. T = INNER frame phi - 1, T + 1 .. T + 29 = FINAL's
+// 100 ms calls.  Positions are 192 kHz frame indices of the output stream.
+struct LpFrame {
+    int phi, nb, lbi, sF, fin;
+    int64_t base, F;       // first output position; the fill frontier (positions < F)
+};
+
+__device__ __forceinline__ int lp_mod(int64_t v) { return (int)(v % LP_RS); }
+
+__device__ __forceinline__ LpFrame lp_frame(const LpArgs &a, int phi) {
+    LpFrame f;
+    f.phi = phi;
+    if (phi == 0) {
+        f.base = 0;
+        f.nb = LP_FR;
+        f.F = LP_RS;
+        f.fin = 0;
+    } else if (phi <= a.T) {
+        const int t = phi - 1;
+        f.base = (int64_t)LP_FR * phi;
+        f.nb = t < a.T - 1 ? LP_FR : a.nb_last;
+        f.F = LP_RS + (int64_t)LP_FR * t + f.nb;
+        f.fin = 0;
+    } else {
+        const int i = phi - a.T - 1;
+        f.base = a.S0 + (int64_t)LP_FR * i;
+        f.nb = LP_FR;
+        f.F = a.S0 + LP_RS + (int64_t)LP_FR * i;
+        f.fin = 1;
+    }
+    const int64_t o = f.fin ? a.S0 : 0;     // FINAL re-bases the ring at S0
+    f.lbi = lp_mod(f.base - o);
+    f.sF = lp_mod(f.F - o);
+    return f;
+}
+
+// the segment starts: 0, 1 + k Fs (INNER, never the partial last frame), S0's frame
+// T + 1 and every Fs FINAL frames after it
+__device__ __forceinline__ int lp_seg_start(const LpArgs &a, int k) {
+    if (k == 0) return 0;
+    if (k <= a.J) return 1 + k * a.Fs;
+    return a.T + 1 + (k - a.J - 1) * a.Fs;
+}
+
+struct LpWave {
+    double2 *ring;         // [LP_RS] the multiplied slots' values (HBM)
+    unsigned *flags;       // [LP_FW] LDS: slot multiplied since its last fill
+    double *st;            // [2][80] LDS: |x| of a peak-scan group
+    LpFrame f;
+    int mode, env_cnt, env_index, attack_length;
+    double gr0, gr1;
+    double d0, off;
+};
+
+// the position a slot holds: the latest filled one with that slot
+__device__ __forceinline__ int64_t lp_pos(const LpFrame &f, int s) {
+    int d = s - f.sF;
+    if (d < 0) d += LP_RS;
+    return f.F - LP_RS + d;
+}
+
+// the fill value of a position (af_loudnorm filter_frame: FIRST, INNER, FINAL)
+__device__ __forceinline__ double2 lp_fill(const LpArgs &a, const LpWave &W, int64_t pos) {
+    if (W.f.fin) {
+        if (pos >= a.n) return make_double2(0.0, 0.0);
+        const float2 x = reinterpret_cast<const float2 *>(a.u)[pos];
+        const double g = a.G[a.T];
+        return make_double2(((double)x.x * g) * W.off, ((double)x.y * g) * W.off);
+    }
+    const float2 x = reinterpret_cast<const float2 *>(a.u)[pos];
+    if (pos < LP_RS) return make_double2(((double)x.x * W.d0) * W.off, ((double)x.y * W.d0) * W.off);
+    const int64_t q = pos - LP_RS;
+    const int t = (int)(q / LP_FR), i = (int)(q - (int64_t)t * LP_FR);
+    const double r = (t < a.T - 1 || a.nb_last == LP_FR) ? a.ramp[i] : (double)i / (double)a.nb_last;
+    const double g0 = a.G[t], g1 = a.G[t + 1];
+    const double g = g0 + (r * (g1 - g0));
+    return make_double2(((double)x.x * g) * W.off, ((double)x.y * g) * W.off);
+}
+
+__device__ __forceinline__ bool lp_flag(const LpWave &W, int s) { return (W.flags[s >> 5] >> (s & 31)) & 1u; }
+
+__device__ __forceinline__ double2 lp_val(const LpArgs &a, const LpWave &W, int s) {
+    if (lp_flag(W, s)) return W.ring[s];
+    return lp_fill(a, W, lp_pos(W.f, s));
+}
+
+__device__ __forceinline__ void lp_clear_range(LpWave &W, int lo, int hi) {   // slots [lo, hi)
+    if (hi <= lo) return;
+    for (int w = (lo >> 5) + (int)threadIdx.x; w <= ((hi - 1) >> 5); w += 64) {
+        const int b0 = w * 32;
+        const int x0 = max(lo, b0) - b0, x1 = min(hi, b0 + 32) - b0;
+        const unsigned m = (x1 - x0 == 32) ? 0xffffffffu : (((1u << (x1 - x0)) - 1u) << x0);
+        W.flags[w] &= ~m;
+    }
+}
+
+// the fill at the start of frame phi: the slots it refills lose their flags
+__device__ void lp_refill(const LpArgs &a, LpWave &W, int phi) {
+    int s0 = 0, cnt = LP_RS;
+    if (phi != 0 && phi != a.T + 1) {
+        if (phi <= a.T) {
+            const int t = phi - 1;
+            s0 = lp_mod((int64_t)LP_FR * t);
+            cnt = t < a.T - 1 ? LP_FR : a.nb_last;
+        } else {
+            s0 = lp_mod((int64_t)LP_FR * (phi - a.T - 2));
+            cnt = LP_FR;
+        }
+    }
+    if (cnt >= LP_RS) {
+        for (int w = threadIdx.x; w < LP_FW; w += 64) W.flags[w] = 0u;
+    } else {
+        lp_clear_range(W, s0, min(s0 + cnt, LP_RS));
+        if (s0 + cnt > LP_RS) lp_clear_range(W, 0, s0 + cnt - LP_RS);
+    }
+    __syncthreads();
+}
+
+// multiply k slots from e0 by env(i) (af_loudnorm's envelope loops)
+template <class F>
+__device__ __forceinline__ void lp_env(const LpArgs &a, LpWave &W, int e0, int k, F env) {
+    for (int i0 = 0; i0 < k; i0 += 64) {
+        const int i = i0 + (int)threadIdx.x;
+        if (i < k) {
+            int s = e0 + i;
+            if (s >= LP_RS) s -= LP_RS;
+            double2 v = lp_val(a, W, s);
+            const double g = env(i);
+            v.x = v.x * g;
+            v.y = v.y * g;
+            W.ring[s] = v;
+            atomicOr(&W.flags[s >> 5], 1u << (s & 31));
+        }
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ int lp_env_end(int e0, int k) {
+    int e = e0 + (k > 0 ? k : 0);
+    return e >= LP_RS ? e - LP_RS : e;
+}
+
+// detect_peak from offset smp over count positions: peak_delta or -1; the peak's |x|
+// and slot.  64 positions per step: the first one that is a candidate with its
+// previous sample as predecessor is found by a ballot; only from there on is the scan
+// serial (a candidate that fails the 10-sample look-ahead keeps the older predecessor)
+__device__ int lp_detect(const LpArgs &a, LpWave &W, int smp, int count, double &peak_value,
+                         int &peak_slot) {
+    const int lane = threadIdx.x;
+    int slot0 = W.f.lbi + smp + LP_ATT;
+    if (slot0 >= LP_RS) slot0 -= LP_RS;
+    const double ceiling = a.ceiling;
+    double pv0 = 0.0, pv1 = 0.0;               // n = 0 never qualifies (n > 0)
+    double *st0 = W.st, *st1 = W.st + 80;
+    for (int nb0 = 0; nb0 < count; nb0 += 64) {
+        {
+            int s = slot0 + nb0 + lane;
+            if (s >= LP_RS) s -= LP_RS;
+            const double2 v = lp_val(a, W, s);
+            double2 v2 = make_double2(0.0, 0.0);
+            if (lane < 12) {
+                int s2 = slot0 + nb0 + 64 + lane;
+                if (s2 >= LP_RS) s2 -= LP_RS;
+                v2 = lp_val(a, W, s2);
+            }
+            __syncthreads();                   // the previous group's serial reads are done
+            st0[lane] = fabs(v.x);
+            st1[lane] = fabs(v.y);
+            if (lane < 12) {
+                st0[64 + lane] = fabs(v2.x);
+                st1[64 + lane] = fabs(v2.y);
+            }
+            __syncthreads();
+        }
+        const int n = nb0 + lane;
+        const int last = (count - nb0 < 64 ? count - nb0 : 64) - 1;
+        bool cand = false;
+        if (n < count && n > 0) {
+            const double t0 = st0[lane], t1 = st1[lane];
+            const double p0 = lane == 0 ? pv0 : st0[lane - 1], p1 = lane == 0 ? pv1 : st1[lane - 1];
+            cand = (p0 <= t0 && st0[lane + 1] <= t0 && t0 > ceiling) ||
+                   (p1 <= t1 && st1[lane + 1] <= t1 && t1 > ceiling);
+        }
+        const unsigned long long m = __ballot(cand);
+        if (!m) {
+            pv0 = st0[last];
+            pv1 = st1[last];
+            continue;
+        }
+        const int L0 = __ffsll((long long)m) - 1;
+        if (L0 > 0) {
+            pv0 = st0[L0 - 1];
+            pv1 = st1[L0 - 1];
+        }
+        for (int k = L0; k <= last; k++) {
+            const int nn = nb0 + k;
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                const double *sc = c ? st1 : st0;
+                double &pv = c ? pv1 : pv0;
+                const double t = sc[k];
+                if (pv <= t && sc[k + 1] <= t && t > ceiling && nn > 0) {
+                    bool detected = true;
+                    for (int i = 2; i < 12; i++)
+                        if (sc[k + i] > t) { detected = false; break; }
+                    if (!detected) continue;
+                    const double q0 = st0[k], q1 = st1[k];
+                    peak_value = q1 > q0 ? q1 : q0;
+                    int ps = slot0 + nn;
+                    if (ps >= LP_RS) ps -= LP_RS;
+                    peak_slot = ps;
+                    return nn;
+                }
+                pv = t;
+            }
+        }
+    }
+    return -1;
+}
+
+// the output of the frame: the ring from its first slot, clamped to the ceiling, s16
+__device__ void lp_emit(const LpArgs &a, const LpWave &W) {
+    const double ceiling = a.ceiling;
+    uint32_t *y = reinterpret_cast<uint32_t *>(a.y);
+    for (int i0 = 0; i0 < W.f.nb; i0 += 64) {
+        const int i = i0 + (int)threadIdx.x;
+        if (i < W.f.nb) {
+            int s = W.f.lbi + i;
+            if (s >= LP_RS) s -= LP_RS;
+            const double2 v = lp_val(a, W, s);
+            double o0 = v.x, o1 = v.y;
+            if (fabs(o0) > ceiling) o0 = ceiling * (o0 < 0 ? -1 : 1);
+            if (fabs(o1) > ceiling) o1 = ceiling * (o1 < 0 ? -1 : 1);
+            y[W.f.base + i] = pack2(ln_s16(o0), ln_s16(o1));
+        }
+    }
+}
+
+// true_peak_limiter on frame W.f (af_loudnorm), then its output when emit
+__device__ void lp_call(const LpArgs &a, LpWave &W, bool emit) {
+    const int nb = W.f.nb;
+    const double ceiling = a.ceiling;
+    if (W.f.phi == 0) {
+        double mx = 0.0;
+        for (int i = threadIdx.x; i < LP_ATT; i += 64) {
+            const double2 v = lp_val(a, W, i);
+            mx = fmax(mx, fmax(fabs(v.x), fabs(v.y)));
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) mx = fmax(mx, __shfl_xor(mx, o));
+        if (mx > ceiling) {
+            W.gr1 = ceiling / mx;
+            W.mode = LO_SUSTAIN;
+            const double g = W.gr1;
+            lp_env(a, W, 0, LP_ATT, [&](int) { return g; });
+        }
+    }
+    int smp = 0;
+    double pv = 0.0;
+    int pslot = 0;
+    do {
+        if (W.mode == LO_OUT) {
+            const int pd = lp_detect(a, W, smp, nb - smp, pv, pslot);
+            if (pd != -1) {
+                W.env_cnt = 0;
+                smp += (pd - W.attack_length);
+                W.gr0 = 1.;
+                W.gr1 = ceiling / pv;
+                W.mode = LO_ATTACK;
+                int e = pslot - W.attack_length;
+                if (e < 0) e += LP_RS;
+                e += W.env_cnt;
+                if (e > LP_RS) e -= LP_RS;
+                W.env_index = e;
+            } else {
+                smp = nb;
+            }
+        } else if (W.mode == LO_ATTACK) {
+            int k = W.attack_length - W.env_cnt;
+            if (k > nb - smp) k = nb - smp;
+            if (k < 0) k = 0;
+            const int c0 = W.env_cnt, al = W.attack_length;
+            const double g0 = W.gr0, g1 = W.gr1;
+            lp_env(a, W, W.env_index, k, [&](int i) { return g0 - ((double)(c0 + i) / (al - 1) * (g0 - g1)); });
+            W.env_index = lp_env_end(W.env_index, k);
+            W.env_cnt += k;
+            smp += k;
+            if (smp < nb) {
+                W.env_cnt = 0;
+                W.attack_length = LP_ATT;
+                W.mode = LO_SUSTAIN;
+            }
+        } else if (W.mode == LO_SUSTAIN) {
+            const int pd = lp_detect(a, W, smp, nb, pv, pslot);
+            if (pd == -1) {
+                W.mode = LO_RELEASE;
+                W.gr0 = W.gr1;
+                W.gr1 = 1.;
+                W.env_cnt = 0;
+            } else {
+                const double gain_reduction = ceiling / pv;
+                if (gain_reduction < W.gr1) {
+                    W.mode = LO_ATTACK;
+                    W.attack_length = pd <= 1 ? 2 : pd;
+                    W.gr0 = W.gr1;
+                    W.gr1 = gain_reduction;
+                    W.env_cnt = 0;
+                } else {
+                    int k = pd;
+                    if (k > nb - smp) k = nb - smp;
+                    if (k < 0) k = 0;
+                    const double g1 = W.gr1;
+                    lp_env(a, W, W.env_index, k, [&](int) { return g1; });
+                    W.env_index = lp_env_end(W.env_index, k);
+                    W.env_cnt = k;
+                    smp += k;
+                }
+            }
+        } else {   // RELEASE
+            const int rl = LP_FR;
+            int k = rl - W.env_cnt;
+            if (k > nb - smp) k = nb - smp;
+            if (k < 0) k = 0;
+            const int c0 = W.env_cnt;
+            const double g0 = W.gr0, g1 = W.gr1;
+            lp_env(a, W, W.env_index, k, [&](int i) { return g0 + (((double)(c0 + i) / (rl - 1)) * (g1 - g0)); });
+            W.env_index = lp_env_end(W.env_index, k);
+            W.env_cnt += k;
+            smp += k;
+            if (smp < nb) {
+                W.env_cnt = 0;
+                W.mode = LO_OUT;
+            }
+        }
+    } while (smp < nb);
+    if (emit) lp_emit(a, W);
+}
+
+__device__ void lp_rest(LpWave &W) {        // af_loudnorm's initial limiter state
+    W.mode = LO_OUT;
+    W.env_cnt = 0;
+    W.env_index = 0;
+    W.attack_length = LP_ATT;
+    W.gr0 = 0.0;
+    W.gr1 = 0.0;
+    for (int w = threadIdx.x; w < LP_FW; w += 64) W.flags[w] = 0u;
+    __syncthreads();
+}
+
+// the state at the start of frame W.f (after its fill): scalars and the values of
+// the 2048 slots from the frame's first; [LP_DIRTY] = a flag outside those slots
+__device__ void lp_snapshot(const LpArgs &a, const LpWave &W, double *rec) {
+    const int lane = threadIdx.x;
+    const int w0 = W.f.lbi;
+    bool out = false;
+    for (int w = lane; w < LP_FW; w += 64) {
+        unsigned m = W.flags[w];
+        // clear the window's bits: slots [w0, w0 + LP_WIN) mod LP_RS
+#pragma unroll
+        for (int part = 0; part < 2; part++) {
+            const int lo = part == 0 ? w0 : 0;
+            const int hi = part == 0 ? min(w0 + LP_WIN, LP_RS) : max(w0 + LP_WIN - LP_RS, 0);
+            const int b0 = w * 32;
+            const int x0 = max(lo, b0) - b0, x1 = min(hi, b0 + 32) - b0;
+            if (x1 > x0) m &= ~((x1 - x0 == 32) ? 0xffffffffu : (((1u << (x1 - x0)) - 1u) << x0));
+        }
+        out |= m != 0u;
+    }
+    const bool dirty = __ballot(out) != 0ull;
+    if (lane == 0) {
+        rec[0] = W.mode;
+        rec[1] = W.env_cnt;
+        rec[2] = W.env_index;
+        rec[3] = W.attack_length;
+        rec[4] = W.gr0;
+        rec[5] = W.gr1;
+        rec[6] = W.f.phi;
+        rec[LP_DIRTY] = dirty ? 1.0 : 0.0;
+    }
+    for (int j = lane; j < LP_WIN; j += 64) {
+        int s = w0 + j;
+        if (s >= LP_RS) s -= LP_RS;
+        const double2 v = lp_val(a, W, s);
+        rec[16 + 2 * j] = v.x;
+        rec[17 + 2 * j] = v.y;
+    }
+}
+
+// the same state back into a wave (every window slot flagged with its recorded value)
+__device__ void lp_restore(const LpArgs &a, LpWave &W, const double *rec, int phi) {
+    W.f = lp_frame(a, phi);
+    W.mode = (int)rec[0];
+    W.env_cnt = (int)rec[1];
+    W.env_index = (int)rec[2];
+    W.attack_length = (int)rec[3];
+    W.gr0 = rec[4];
+    W.gr1 = rec[5];
+    for (int w = threadIdx.x; w < LP_FW; w += 64) W.flags[w] = 0u;
+    __syncthreads();
+    for (int j = threadIdx.x; j < LP_WIN; j += 64) {
+        int s = W.f.lbi + j;
+        if (s >= LP_RS) s -= LP_RS;
+        W.ring[s] = make_double2(rec[16 + 2 * j], rec[17 + 2 * j]);
+        atomicOr(&W.flags[s >> 5], 1u << (s & 31));
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ bool lp_bits_eq(double x, double y) {
+    return __double_as_longlong(x) == __double_as_longlong(y);
+}
+
+// two states at the same frame lead to the same future: equal scalars (only the mode
+// when both are at rest: OUT re-initialises the rest) and equal window values, and
+// neither has a multiplied slot outside the window
+__device__ bool lp_same(const double *A, const double *B) {
+    bool diff = A[LP_DIRTY] != 0.0 || B[LP_DIRTY] != 0.0 || (int)A[0] != (int)B[0];
+    if ((int)A[0] != LO_OUT || (int)B[0] != LO_OUT)
+        for (int q = 0; q < 6; q++) diff |= !lp_bits_eq(A[q], B[q]);
+    for (int j = threadIdx.x; j < 2 * LP_WIN; j += 64) diff |= !lp_bits_eq(A[16 + j], B[16 + j]);
+    return __ballot(diff) == 0ull;
+}
+
+// boundary j: the later of segment j-1 (its end state) and segment j (its guess) to
+// arrive compares them
+__device__ void lp_arrive(const LpArgs &a, int j) {
+    __threadfence();
+    int old = 0;
+    if (threadIdx.x == 0) old = atomicAdd(&a.cnt[j], 1);
+    old = __shfl(old, 0);
+    if (old == 1) {
+        __threadfence();
+        const bool same = lp_same(a.recE + (int64_t)(j - 1) * LP_REC, a.recG + (int64_t)j * LP_REC);
+        if (threadIdx.x == 0) a.match[j] = same ? 1 : 0;
+    }
+}
+
+__device__ __forceinline__ void lp_wave_init(const LpArgs &a, LpWave &W, double2 *ring, unsigned *flags,
+                                             double *st) {
+    W.ring = ring;
+    W.flags = flags;
+    W.st = st;
+    W.d0 = a.dctl[0];
+    W.off = a.dctl[1];
+}
+
+// every segment at once (persistent waves): from rest Wf frames before its start
+__global__ void __launch_bounds__(64) k_lp_seg(LpArgs a) {
+    if (a.ctl[0]) return;
+    __shared__ unsigned flags[LP_FW];
+    __shared__ double st[160];
+    LpWave W;
+    lp_wave_init(a, W, reinterpret_cast<double2 *>(a.rings) + (int64_t)blockIdx.x * LP_RS, flags, st);
+    const int NF = a.T + 1 + LP_NFIN;
+    for (int k = blockIdx.x; k < a.K; k += gridDim.x) {
+        const int ak = lp_seg_start(a, k), bk = k + 1 < a.K ? lp_seg_start(a, k + 1) : NF;
+        const int w = ak - a.Wf > 0 ? ak - a.Wf : 0;
+        lp_rest(W);
+        for (int phi = w; phi < bk; phi++) {
+            W.f = lp_frame(a, phi);
+            lp_refill(a, W, phi);
+            if (phi == ak) {
+                lp_snapshot(a, W, a.recG + (int64_t)k * LP_REC);
+                if (k > 0) lp_arrive(a, k);
+            }
+            lp_call(a, W, phi >= ak);
+        }
+        if (k + 1 < a.K) {
+            W.f = lp_frame(a, bk);
+            lp_refill(a, W, bk);
+            lp_snapshot(a, W, a.recE + (int64_t)k * LP_REC);
+            lp_arrive(a, k + 1);
+        }
+    }
+}
+
+// in order over the boundaries: skip the matched ones, re-run a segment whose start
+// guess was wrong from the true state (rewriting its output).  If the limiter is
+// active where FINAL re-bases the ring, FINAL runs here from that state.  A true state
+// with a multiplied slot outside its window (never expected) hands the whole track
+// to k_ln_dyn (ctl[0] = 2).
+__global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
+    if (a.ctl[0]) return;
+    __shared__ unsigned flags[LP_FW];
+    __shared__ double st[160];
+    LpWave W;
+    lp_wave_init(a, W, reinterpret_cast<double2 *>(a.wring), flags, st);
+    const int lane = threadIdx.x;
+    const int NF = a.T + 1 + LP_NFIN, kS0 = a.J + 1;
+    const double *cur = a.recE;
+    bool k4 = true;
+    int toggle = 0, reruns = 0, fin = 0, fallback = 0;
+    int k = 1;
+    while (k < a.K) {
+        if (k4) {
+            while (k < a.K) {
+                const int j = k + lane;
+                const bool stop = j >= a.K || j == kS0 || a.match[j] == 0;
+                const unsigned long long m = __ballot(stop);
+                if (m) {
+                    k += __ffsll((long long)m) - 1;
+                    break;
+                }
+                k += 64;
+            }
+            if (k >= a.K) break;
+            cur = a.recE + (int64_t)(k - 1) * LP_REC;
+        }
+        if (cur[LP_DIRTY] != 0.0) {
+            fallback = 1;
+            break;
+        }
+        if (k == kS0 && (int)cur[0] != LO_OUT) {
+            lp_restore(a, W, cur, a.T + 1);
+            for (int phi = a.T + 1; phi < NF; phi++) {
+                if (phi > a.T + 1) {
+                    W.f = lp_frame(a, phi);
+                    lp_refill(a, W, phi);
+                }
+                lp_call(a, W, true);
+            }
+            fin = 1;
+            break;
+        }
+        const bool ok = k4 ? (a.match[k] != 0) : lp_same(cur, a.recG + (int64_t)k * LP_REC);
+        if (ok) {
+            cur = a.recE + (int64_t)k * LP_REC;
+            k4 = true;
+            k++;
+            continue;
+        }
+        const int ak = lp_seg_start(a, k), bk = k + 1 < a.K ? lp_seg_start(a, k + 1) : NF;
+        lp_restore(a, W, cur, ak);
+        for (int phi = ak; phi < bk; phi++) {
+            if (phi > ak) {
+                W.f = lp_frame(a, phi);
+                lp_refill(a, W, phi);
+            }
+            lp_call(a, W, true);
+        }
+        reruns++;
+        if (k + 1 < a.K) {
+            W.f = lp_frame(a, bk);
+            lp_refill(a, W, bk);
+            double *r = a.wrec + (int64_t)toggle * LP_REC;
+            toggle ^= 1;
+            lp_snapshot(a, W, r);
+            __syncthreads();
+            cur = r;
+            k4 = false;
+        }
+        k++;
+    }
+    if (lane == 0) {
+        if (fallback) a.ctl[0] = 2;
+        a.ctl[1] = reruns;
+        a.ctl[2] = fin;
+        a.summary[0] = 0.0;
+        a.summary[1] = 1.0;
+        for (int q = 2; q < 10; q++) a.summary[q] = 0.0;
+        a.summary[10] = (double)reruns;
+        a.summary[11] = (double)fin;
+        a.summary[12] = (double)a.K;
+        a.summary[13] = (double)fallback;
+    }
+}
+
+hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x, int64_t n_in, int L,
+                           int M, const float *bank, hipStream_t st) {
+    if (ln.n192 <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ln_upsample, dim3((unsigned)((ln.n192 + AMX_BLOCK - 1) / AMX_BLOCK)), dim3(AMX_BLOCK),
+                       0, st, x, n_in, L, M, bank, ln.n192, ln.u);
+    hipLaunchKernelGGL(k_lp_stats, dim3(1 + (lp.T + LP_STAT_F - 1) / LP_STAT_F), dim3(LP_STAT_NT), 0, st, lp);
+    hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
+    const int gb = max((lp.T + 1 + 255) / 256, (LP_FR + 255) / 256);
+    hipLaunchKernelGGL(k_lp_gains, dim3(gb), dim3(256), 0, st, lp);
+    hipError_t e = hipMemsetAsync(lp.cnt, 0, sizeof(int) * (size_t)(lp.K + 1), st);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(lp.match, 0, sizeof(int) * (size_t)(lp.K + 1), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lp_seg, dim3(lp.P), dim3(64), 0, st, lp);
+    hipLaunchKernelGGL(k_lp_walk, dim3(1), dim3(64), 0, st, lp);
+    hipLaunchKernelGGL(k_ln_dyn, dim3(1), dim3(LN_NT), 0, st, ln);
     return hipGetLastError();
 }
 

@@ -230,6 +230,7 @@ struct amx_plan {
     // step M; Lin chain frames = Lout 192 kHz frames per K segment); resamp = 0 when
     // the track already is at 192 kHz (the measurement runs on d_out itself)
     int resamp = 0, upL = 1, upM = 1, upLin = 0, upLout = 0, up_static = 0, up_ok = 1;
+    int meas_native = 0;    // no 192 kHz resampler for this rate: peaks only, no loudnorm
     int32_t *d_obase = nullptr, *d_oph = nullptr;
     int32_t *d_slow = nullptr;   // K segments k_up_edge takes (static path); n_slow of them
     int64_t n_slow = 0;
@@ -336,6 +337,13 @@ extern "C" {
 
 int amx_abi_version(void) { return AMX_ABI_VERSION; }
 const char *amx_last_error(void) { return g_err.c_str(); }
+#ifndef AMX_SRC_HASH
+#define AMX_SRC_HASH "unstamped"
+#endif
+// "AMX_SRC_HASH=<hex>" in the binary: amx/build.py reads it from the file without
+// loading the library (no HIP runtime before torch's)
+static const char amx_stamp[] = "AMX_SRC_HASH=" AMX_SRC_HASH;
+const char *amx_build_id(void) { return amx_stamp + 13; }
 
 int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t n_chunks,
                     const int64_t *track_frame0, const int64_t *track_total_frames,
@@ -363,13 +371,21 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     p->L = seg_frames > 0 ? seg_frames : 256;
     p->L = (p->L + AMX_TF_FRAMES - 1) / AMX_TF_FRAMES * AMX_TF_FRAMES;   // whole LDS tiles
     // the loudness measurement's rate: 192 kHz (af_loudnorm dynamic mode, :229)
-    const int kfs = AMX_MEAS_RATE;
+    int kfs = AMX_MEAS_RATE;
     std::vector<float> bank;
     std::vector<int32_t> obase, oph;
     if (fs != kfs) {
         p->resamp = 1;
         if (amx::swr_geometry(fs, kfs, &p->upL, &p->upM) != 0) {
-            p->up_ok = 0;     // no exact-rational resampler: amx_loudness_pass1 fails
+            // no exact-rational resampler (192000 / gcd > 1024 phases: 22.05 / 11.025 kHz):
+            // libswresample's inexact 1024-phase path is not restated.  The plan measures
+            // at the track's own rate, which gives the limiter its peaks (the only
+            // measurement lufs=None needs); amx_loudness_decide refuses loudnorm on it.
+            p->up_ok = 0;
+            p->resamp = 0;
+            p->meas_native = 1;
+            p->upL = p->upM = 1;
+            kfs = fs;
         } else {
             // ~384 192 kHz outputs per K segment, a divisor of the 100 ms hop (19200)
             // where one exists, so a segment lies inside one hop (no hop split)
@@ -391,6 +407,12 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             p->up_static = (p->upM == 1 && (p->upL == 2 || p->upL == 4) && ident0 &&
                             p->upLin % 8 == 0) ? p->upL : 0;
         }
+    } else {
+        // already 192 kHz: ffmpeg inserts no resampler ahead of af_loudnorm, only the s16
+        // -> dbl conversion x / 32768; a one-phase bank that is the unit impulse makes
+        // k_ln_upsample produce exactly that (every other tap adds 0)
+        bank.assign(32, 0.0f);
+        bank[15] = 1.0f;
     }
     p->hop = (kfs + 5) / 10;                   // libebur128 samples_in_100ms at 192 kHz
     {
@@ -1017,7 +1039,7 @@ int amx_plan_get_info(const amx_plan *p, amx_plan_info *info) {
     info->scan_levels_kw = p->lev_kw;
     info->eq_dim = p->D;
     info->hop_frames = p->hop;
-    info->meas_rate = AMX_MEAS_RATE;
+    info->meas_rate = p->meas_native ? p->cd.fs : AMX_MEAS_RATE;
     info->max_hops = p->max_hops;
     return AMX_OK;
 }
@@ -1148,6 +1170,60 @@ amx::UpArgs up_args(const amx_plan *p, const int16_t *d_out, const int16_t *d_ed
     a.pk = wsp<uint32_t>(d_ws, p->o_pk);
     return a;
 }
+// ---- loudnorm's 192 kHz modes: scratch layout (amx_loudnorm.hip)
+#define LN_FIRST_FRAMES 576000     // frame_size(192000, 3000)
+struct LnLayout {
+    int T = 0, nb_last = 0, Fs = 4, Wf = 3, J = 0, M = 0, K = 0, P = 0;
+    int64_t o_u = 0, o_ring = 0, o_ctl = 0, o_dctl = 0, o_v = 0, o_hold = 0, o_D = 0, o_G = 0, o_ramp = 0;
+    int64_t o_recG = 0, o_recE = 0, o_wrec = 0, o_cnt = 0, o_match = 0, o_rings = 0, o_wring = 0, total = 0;
+};
+// INNER frames, segments of Fs frames (AMX_LN_SEG, default 4) each warmed up Wf frames
+// (AMX_LN_WARM, default 3) before its start, waves of k_lp_seg
+LnLayout ln_layout(int64_t n192) {
+    LnLayout l;
+    if (const char *ev = std::getenv("AMX_LN_SEG")) l.Fs = std::max(1, std::atoi(ev));
+    if (const char *ev = std::getenv("AMX_LN_WARM")) l.Wf = std::max(0, std::atoi(ev));
+    if (n192 >= LN_FIRST_FRAMES) {
+        l.T = (int)((n192 - LN_FIRST_FRAMES + 19199) / 19200);
+        l.nb_last = l.T > 0 ? (int)(n192 - LN_FIRST_FRAMES - 19200LL * (l.T - 1)) : 0;
+    }
+    // boundaries only at full INNER frames (a partial last frame's wrap reads reach the
+    // frame before it), at FINAL's start and inside FINAL
+    const int t_ok = (l.T > 0 && l.nb_last == 19200) ? l.T : l.T - 1;
+    l.J = t_ok >= 1 + l.Fs ? (t_ok - 1) / l.Fs : 0;
+    l.M = (29 + l.Fs - 1) / l.Fs;
+    l.K = 1 + l.J + l.M;
+    l.P = std::min(l.K, 1024);
+    int64_t o = 0;
+    auto take = [&](int64_t bytes) { const int64_t at = o; o += ((bytes + 255) / 256) * 256; return at; };
+    l.o_u = take(n192 * 2 * (int64_t)sizeof(float));
+    l.o_ring = take((2 * 40320 + 64) * (int64_t)sizeof(double));
+    l.o_ctl = take(16 * sizeof(int));
+    l.o_dctl = take(8 * sizeof(double));
+    l.o_v = take((int64_t)l.T * sizeof(double));
+    l.o_hold = take((int64_t)l.T * sizeof(int));
+    l.o_D = take((int64_t)l.T * sizeof(double));
+    l.o_G = take((int64_t)(l.T + 1) * sizeof(double));
+    l.o_ramp = take(19200 * sizeof(double));
+    l.o_recG = take((int64_t)l.K * AMX_LN_REC * sizeof(double));
+    l.o_recE = take((int64_t)l.K * AMX_LN_REC * sizeof(double));
+    l.o_wrec = take(2 * AMX_LN_REC * sizeof(double));
+    l.o_cnt = take((int64_t)(l.K + 1) * sizeof(int));
+    l.o_match = take((int64_t)(l.K + 1) * sizeof(int));
+    l.o_rings = take((int64_t)l.P * AMX_LN_RING * 2 * sizeof(double));
+    l.o_wring = take((int64_t)AMX_LN_RING * 2 * sizeof(double));
+    l.total = o;
+    return l;
+}
+// the 192 kHz stream's frames of a whole track (the resampler's output, or the track
+// itself when it already is 192 kHz)
+int ln_frames(const amx_plan *p, int32_t track, int64_t *n192) {
+    if (p->meas_native || (p->resamp && !p->up_ok))
+        return fail(AMX_ERANGE, "loudnorm's 192 kHz modes need an exact-rational 192 kHz resampler");
+    const SpanDev &sp = p->spans[track];
+    *n192 = p->resamp ? (sp.out_n * p->upL + p->upM - 1) / p->upM : sp.out_n;
+    return AMX_OK;
+}
 int check_edges(const amx_plan *p, const int16_t *d_edge) {
     if (!p->resamp || d_edge) return AMX_OK;
     for (const SpanDev &sp : p->spans)
@@ -1209,30 +1285,32 @@ int amx_loudness_pass1(amx_plan *p, const int16_t *d_out, const int16_t *d_edge,
 
 int amx_loudnorm_192k_size(const amx_plan *p, int32_t track, int64_t *frames, int64_t *ws_bytes) {
     if (!p || !frames || !ws_bytes || track < 0 || track >= p->n_tracks) return fail(AMX_EINVAL, "bad argument");
-    if (!p->resamp || !p->up_ok)
-        return fail(AMX_ERANGE, "loudnorm's 192 kHz modes need an exact-rational 192 kHz resampler");
-    const SpanDev &sp = p->spans[track];
-    const int64_t n192 = (sp.out_n * p->upL + p->upM - 1) / p->upM;
+    int64_t n192 = 0;
+    if (int rc = ln_frames(p, track, &n192)) return rc;
     *frames = n192;
-    *ws_bytes = ((n192 * 2 * (int64_t)sizeof(float) + 255) / 256) * 256 + (2 * 40320 + 64) * (int64_t)sizeof(double);
+    *ws_bytes = ln_layout(n192).total;
     return AMX_OK;
 }
 
-int amx_loudnorm_192k(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const int16_t *d_out,
-                      const double *d_hops, int64_t max_hops, const double *d_peak, int16_t *d_y192,
-                      double *d_summary, void *d_ws2, void *stream) {
-    int64_t n192 = 0, wsb = 0;
-    if (int rc = amx_loudnorm_192k_size(p, track, &n192, &wsb)) return rc;
+int amx_loudnorm_192k_ex(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const double *d_measured,
+                         const double *d_offset_i, const int16_t *d_out, const double *d_hops,
+                         int64_t max_hops, const double *d_peak, int16_t *d_y192, double *d_summary,
+                         void *d_ws2, void *stream) {
+    if (!p || track < 0 || track >= p->n_tracks) return fail(AMX_EINVAL, "bad argument");
+    int64_t n192 = 0;
+    if (int rc = ln_frames(p, track, &n192)) return rc;
     if (!d || !d_out || !d_hops || !d_peak || !d_y192 || !d_summary || !d_ws2)
         return fail(AMX_EINVAL, "null argument");
     const SpanDev &sp = p->spans[track];
     if (sp.tframe0 != 0 || sp.ttotal != sp.out_n)
         return fail(AMX_EINVAL, "loudnorm's 192 kHz modes run on whole tracks (one plan holds the track)");
     if (max_hops < n192 / 19200 + 1) return fail(AMX_EINVAL, "d_hops holds %lld hops", (long long)max_hops);
+    const LnLayout lo = ln_layout(n192);
+    char *w = reinterpret_cast<char *>(d_ws2);
     amx::LnArgs a{};
     a.n192 = n192;
-    a.u = reinterpret_cast<float *>(d_ws2);
-    a.ring = reinterpret_cast<double *>(reinterpret_cast<char *>(d_ws2) + ((n192 * 2 * (int64_t)sizeof(float) + 255) / 256) * 256);
+    a.u = reinterpret_cast<float *>(w + lo.o_u);
+    a.ring = reinterpret_cast<double *>(w + lo.o_ring);
     a.y = d_y192;
     a.summary = d_summary;
     a.hops = d_hops + (int64_t)track * max_hops * 2;
@@ -1261,9 +1339,58 @@ int amx_loudnorm_192k(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, co
         for (int i = 0; i < 21; i++) a.weights[i] *= adjust;
     }
     for (int k = 0; k < 5; k++) { a.kb[k] = p->kdf_b[k]; a.ka[k] = p->kdf_a[k]; }
-    HIPCHK(amx::launch_loudnorm(a, reinterpret_cast<const uint32_t *>(d_out) + sp.out_off, sp.out_n, p->upL,
+    amx::LpArgs q{};
+    q.n = n192;
+    q.S0 = n192 - (LN_FIRST_FRAMES - 19200);
+    q.T = lo.T;
+    q.nb_last = lo.nb_last;
+    q.Fs = lo.Fs;
+    q.Wf = lo.Wf;
+    q.J = lo.J;
+    q.M = lo.M;
+    q.K = lo.K;
+    q.P = lo.P;
+    q.u = a.u;
+    q.hops = a.hops;
+    q.energies = a.energies;
+    q.bounds = a.bounds;
+    q.target_i = a.target_i;
+    q.target_lra = a.target_lra;
+    q.ceiling = a.target_tp;
+    q.measured_i = a.measured_i;
+    q.measured_thresh = a.measured_thresh;
+    q.offset = a.offset;
+    q.measured_src = d_measured;
+    q.offset_src = d_offset_i;
+    for (int i = 0; i < 21; i++) q.weights[i] = a.weights[i];
+    q.v = reinterpret_cast<double *>(w + lo.o_v);
+    q.hold = reinterpret_cast<int *>(w + lo.o_hold);
+    q.D = reinterpret_cast<double *>(w + lo.o_D);
+    q.G = reinterpret_cast<double *>(w + lo.o_G);
+    q.ramp = reinterpret_cast<double *>(w + lo.o_ramp);
+    q.recG = reinterpret_cast<double *>(w + lo.o_recG);
+    q.recE = reinterpret_cast<double *>(w + lo.o_recE);
+    q.wrec = reinterpret_cast<double *>(w + lo.o_wrec);
+    q.cnt = reinterpret_cast<int *>(w + lo.o_cnt);
+    q.match = reinterpret_cast<int *>(w + lo.o_match);
+    q.rings = reinterpret_cast<double *>(w + lo.o_rings);
+    q.wring = reinterpret_cast<double *>(w + lo.o_wring);
+    q.ctl = reinterpret_cast<int *>(w + lo.o_ctl);
+    q.dctl = reinterpret_cast<double *>(w + lo.o_dctl);
+    q.y = d_y192;
+    q.summary = d_summary;
+    a.lp_ctl = q.ctl;
+    a.lp_dctl = q.dctl;
+    HIPCHK(amx::launch_loudnorm(a, q, reinterpret_cast<const uint32_t *>(d_out) + sp.out_off, sp.out_n, p->upL,
                                 p->upM, p->d_bank, (hipStream_t)stream));
     return AMX_OK;
+}
+
+int amx_loudnorm_192k(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const int16_t *d_out,
+                      const double *d_hops, int64_t max_hops, const double *d_peak, int16_t *d_y192,
+                      double *d_summary, void *d_ws2, void *stream) {
+    return amx_loudnorm_192k_ex(p, track, d, nullptr, nullptr, d_out, d_hops, max_hops, d_peak, d_y192,
+                                d_summary, d_ws2, stream);
 }
 
 int amx_pcm_to_s16(const void *d_raw, int64_t frames, int32_t channels, int32_t format,
@@ -1417,6 +1544,10 @@ int amx_loudness_decide(amx_plan *p, const amx_decide_desc *dd, const amx_final_
     if (!p || !dd || !fd || !d_peak || !d_stats || !d_gains || !d_ctl ||
         (dd->lufs_on && (!d_hist || !d_st_hist)))
         return fail(AMX_EINVAL, "null argument");
+    if (dd->lufs_on && p->meas_native)
+        return fail(AMX_ERANGE, "%d Hz: loudnorm measures the track resampled to 192 kHz and this rate "
+                    "has no exact-rational resampler (libswresample's 1024-phase path is not "
+                    "restated); lufs=None works", p->cd.fs);
     amx::DecideArgs a{};
     a.n_tracks = p->n_tracks;
     a.lufs_on = dd->lufs_on ? 1 : 0;

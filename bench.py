@@ -11,10 +11,14 @@ over the ranks (weak scaling) with the RCCL all-reduce of the loudness partials.
 Input is resident in HBM before timing; the output (16-bit PCM, what the reference
 writes) stays in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--strong]
 
 c2 = configs[1] (EQ + loudnorm + alimiter), c4 = configs[3] (8 whole 4-minute tracks
 per GPU, track-sharded, no exchange), c5 = configs[4] (60 min at 96 kHz per GPU).
+--strong: ONE track of the config's length split over the N ranks (configs[4] as
+BASELINE.json states it: one 60-min 96 kHz track chunk-sharded over 8 GPUs).
+At N = 1 the default run also times C2, C4 and C5 on the GPU (``other_configs``:
+hipGraph replays, no CPU leg), so every config has a number from the driver's run.
 """
 import argparse
 import json
@@ -23,11 +27,14 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "audio-mastering-engine_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFS = 78.6           # MI355X fp64 vector, spec (half the 157.3 TF fp32 rate); measured 68
+FP32_PEAK_TFS = 157.3          # MI355X fp32 vector, spec
 CHAIN_BYTES = 8                # 4 B f32 read + 4 B write per channel-sample (chain)
 E2E_BYTES = 16                 # + the gain / limiter pass
 
@@ -104,6 +111,83 @@ PER_STEP = {"k_envfix": 2}
 PIPELINE_PREFIX = "k_"
 
 
+def synth_input(frames, fs, seed):
+    """the seeded synthetic program; inputs longer than 10 minutes repeat a 60 s block
+    (amx.synth.mix_tiled: mix_like costs ~1 s of host time per 20 s of audio)"""
+    from amx import synth
+    if frames > 600 * fs:
+        return synth.mix_tiled(frames, fs, 2, seed=seed)
+    return synth.mix_like(frames, fs, 2, seed=seed)
+
+
+def load_flops(config):
+    """Per-launch FLOPs from the committed PMC summary (profiles/flops_<config>.json,
+    scripts/gpu_flops.sh: rocprofv3 SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_{F64,F32}, one pass)."""
+    path = os.path.join(ROOT, "profiles", "flops_%s.json" % config)
+    try:
+        return json.load(open(path))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def time_graph(runner, d_in, warmup, soak_s, min_s):
+    """warm-up steps, capture, soak, then >= min_s seconds of replays; ms per step"""
+    import torch
+    for _ in range(warmup):
+        runner.step(d_in)
+    runner.capture(d_in)
+    runner.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < soak_s or n < 2:
+        runner.replay()
+        n += 1
+        if n % 4 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    t_est = (time.perf_counter() - t0) / n
+    steps = max(5, int(math.ceil(min_s / t_est)))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        runner.replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3 / steps, steps
+
+
+def other_configs(args):
+    """C2, C4, C5 on this GPU (N = 1): the same step as their own bench lines (hipGraph
+    replay of the whole pipeline on HBM-resident synthetic input), timed over >= 1 s;
+    no CPU leg, no per-stage events"""
+    import gc
+    import torch
+    from amx.dist import ShardedBatch, ShardedTrack
+    out = {}
+    for cfg in ("c2", "c4", "c5"):
+        fs = CONFIG_FS[cfg]
+        per_track = int(CONFIG_SECONDS[cfg] * fs)
+        if cfg == "c4":
+            frames = [per_track] * CONFIG_TRACKS[cfg]
+            runner = ShardedBatch(fs, 2, CONFIGS[cfg], frames, 0, 1, quantum=512, seg_frames=args.seg_frames)
+            x = np.concatenate([synth_input(frames[t], fs, 1000 + t) for t in runner.tracks], axis=0)
+        else:
+            runner = ShardedTrack(fs, 2, CONFIGS[cfg], per_track, 0, 1, quantum=512, seg_frames=args.seg_frames)
+            x = synth_input(runner.local_frames, fs, 0)
+        d_in = torch.from_numpy(x).cuda()
+        del x
+        ms, steps = time_graph(runner, d_in, 2, 0.5, 1.0)
+        samples = sum(runner.span_frames) * 2
+        rep = runner.job.fetch_report()
+        out[cfg] = {"workload": WORKLOAD[cfg], "ms_per_step": round(ms, 4), "steps": steps,
+                    "value": round(samples / (ms / 1e3) / 1e6, 3), "unit": "Msamples/s",
+                    "chain_frac": round(CHAIN_BYTES * samples / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "loudnorm_mode": rep.get("modes"), "limiter_fast": rep.get("limiter_fast")}
+        del runner, d_in
+        gc.collect()
+        torch.cuda.empty_cache()
+    return out
+
+
 def load_traffic(config):
     """Per-launch HBM bytes from the committed PMC summary (profiles/traffic_<config>.json,
     scripts/gpu_traffic.sh: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, separate passes)."""
@@ -132,6 +216,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true", help="skip the double-buffered host rate")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from the host")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: one track of the config's length split over the ranks")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="skip the GPU-only timings of the other configs (N = 1 default run)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--one-device", action="store_true",
@@ -163,12 +251,13 @@ def main():
         frames = [per_track] * (n_tr * world)
         runner = ShardedBatch(fs, 2, settings, frames, rank, world, quantum=512,
                               seg_frames=args.seg_frames)
-        xs = [synth.mix_like(frames[t], fs, 2, seed=1000 + t) for t in runner.tracks]
+        xs = [synth_input(frames[t], fs, 1000 + t) for t in runner.tracks]
         x = np.concatenate(xs, axis=0)
     else:
-        runner = ShardedTrack(fs, 2, settings, per_track * world, rank, world, quantum=512,
+        total = per_track if args.strong else per_track * world
+        runner = ShardedTrack(fs, 2, settings, total, rank, world, quantum=512,
                               seg_frames=args.seg_frames)
-        x = synth.mix_like(runner.local_frames, fs, 2, seed=rank)
+        x = synth_input(runner.local_frames, fs, rank)
     d_in = torch.from_numpy(x).cuda()
     job = runner.job
 
@@ -290,12 +379,26 @@ def main():
         step_traffic = int(sum(v["hbm_bytes"] * PER_STEP.get(k, 1) for k, v in traffic.items()
                                if k.startswith(PIPELINE_PREFIX)))
     f2_flops = front2_flops(frames, settings, mb)
+    flops = load_flops(args.config)
+    chain_flops = None
+    if flops:
+        f64 = sum(v["fp64_flops"] * PER_STEP.get(k, 1) for k, v in flops.items() if k.startswith(PIPELINE_PREFIX))
+        f32 = sum(v["fp32_flops"] * PER_STEP.get(k, 1) for k, v in flops.items() if k.startswith(PIPELINE_PREFIX))
+        chain_flops = {
+            "fp64_flops_per_step": int(f64), "fp32_flops_per_step": int(f32),
+            "fp64_per_sample": round(f64 / samples_rank, 1), "fp32_per_sample": round(f32 / samples_rank, 1),
+            "achieved_fp64": round(f64 / (ms_per_step / 1e3) / 1e12, 3),
+            "peak_fp64": FP64_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": round(f64 / (ms_per_step / 1e3) / 1e12 / FP64_PEAK_TFS, 4),
+            "frac_fp64_plus_fp32": round((f64 / FP64_PEAK_TFS + f32 / FP32_PEAK_TFS) / (ms_per_step / 1e3) / 1e12, 4),
+            "source": "profiles/flops_%s.json (rocprofv3 SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_{F64,F32} x 64 "
+                      "lanes, FMA x 2; issued lanes, per launch) over the measured step time" % args.config}
 
     line = {
         "metric": "mastered Msamples/sec (48 kHz stereo f32) at 1/2/4/8 GPUs; % HBM roofline",
         "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (amx.synth.mix_like, seeded per rank / track)",
         "config": {"workload": WORKLOAD[args.config], "sample_rate": fs,
                    "settings": args.config, "seconds_per_track": args.seconds,
@@ -325,6 +428,7 @@ def main():
             "step_traffic": step_traffic,
             "what": "whole step (every kernel) at SURVEY §8(d)'s 8 B/sample chain and 16 B/sample "
                     "end-to-end; step_traffic = the PMC bytes of every pipeline kernel per step"},
+        "chain_flop_frac": chain_flops,
         "host_inclusive": host_incl,
         "roofline_fp64": {"bound": "fp64", "kernel": "k_front2",
                           "achieved": round(f2_flops / (per_stage["front2"] / 1e3) / 1e12, 2),
@@ -343,6 +447,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line.update(cpu_leg(args, runner, x, fs, settings, job, batch))
+    if rank == 0 and world == 1 and args.config == "c3" and not args.no_other_configs:
+        line["other_configs"] = other_configs(args)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -148,6 +148,10 @@ typedef struct amx_track_span {
 
 AMX_API int amx_abi_version(void);
 AMX_API const char *amx_last_error(void);
+/* Build provenance: the SHA-256 (hex) of the sources this library was compiled from
+ * (csrc/*, include/amx.h; amx/build.py source_hash), stamped at compile time.  The
+ * Python binding refuses a library whose stamp differs from the tree it runs in. */
+AMX_API const char *amx_build_id(void);
 
 /* Build a plan (host only: designs nothing, derives scan matrices and segment
  * tables from the given coefficients, uploads small constant tables).
@@ -248,13 +252,27 @@ AMX_API int amx_loudnorm_192k_size(const amx_plan *plan, int32_t track, int64_t 
  * amx_loudness_pass2's hop energies and amx_loudness_pass1's peaks of the same plan (the
  * 192 kHz stream's r128_in statistics); d_y192 [frames][2] s16: the output as the WAV
  * muxer writes it (av_clip_int16(llrint(x * 32768))); d_summary [16]: [0..1] = (1, offset)
- * when the < 3 s linear fallback ran, else (0, the final above_threshold); [2..9] =
- * device cycles in the ring fills, peak scans, envelopes, output, statistics and
- * r128_out, then the peak-scan calls and their serial chunks (diagnostics). */
+ * when the < 3 s linear fallback ran, else (0, the final above_threshold).  Diagnostics:
+ * on the frame-by-frame path (a quiet start) [2..9] = device cycles in the ring fills,
+ * peak scans, envelopes, output, statistics and r128_out, then the peak-scan calls and
+ * their serial chunks; on the parallel path [10..13] = segments re-run in order, FINAL
+ * re-run (limiter active at its start), segments, hand-over to the frame-by-frame path. */
 AMX_API int amx_loudnorm_192k(amx_plan *plan, int32_t track, const amx_loudnorm_desc *desc,
                               const int16_t *d_out, const double *d_hops, int64_t max_hops,
                               const double *d_peak, int16_t *d_y192, double *d_summary, void *d_ws2,
                               void *stream);
+/* The same with the measured_* options and pass 1's target_offset read on the device,
+ * so the whole dynamic path can be captured into one graph: d_measured (nullable) = a
+ * k_decide statistics row of the track (amx_loudness_decide d_stats: [4] input_i, [7]
+ * input_thresh, already the "%.2f" values pass 2 parses); d_offset_i (nullable) = the
+ * statistics row of pass 1's output measurement ([0] its integrated loudness): offset =
+ * "%.2f"(target_i - that) dB, as pass 1's JSON target_offset (:229-241).  A NULL
+ * pointer takes desc's value. */
+AMX_API int amx_loudnorm_192k_ex(amx_plan *plan, int32_t track, const amx_loudnorm_desc *desc,
+                                 const double *d_measured, const double *d_offset_i,
+                                 const int16_t *d_out, const double *d_hops, int64_t max_hops,
+                                 const double *d_peak, int16_t *d_y192, double *d_summary, void *d_ws2,
+                                 void *stream);
 /* Host helper for chunk-sharded tracks: out8 = A^frames * in8 (per channel 4x4 K-filter
  * transition at the measurement rate; frames of the measurement stream), so
  * carry(r+1) = A^{len_r} carry(r) + tail(r). */

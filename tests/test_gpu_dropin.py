@@ -84,6 +84,67 @@ def test_master_audio_files(gpu, oracle_mod, code, channels, seconds, settings):
     assert d.max() == 0, "max |diff| %d LSB" % d.max()
 
 
+@pytest.mark.parametrize("fs", [22050, 11025])
+def test_master_audio_rates_without_192k_resampler(gpu, oracle_mod, fs):
+    """22.05 / 11.025 kHz have no exact-rational 192 kHz resampler (192000 / gcd > 1024
+    phases).  With lufs=None the reference runs no loudnorm: the plan measures at the
+    track's own rate (the limiter's peaks are all it needs) and the output is the
+    oracle's bit for bit.  With loudnorm on, the decision refuses with ERANGE (the
+    inexact 1024-phase resampler is not restated) instead of measuring something else."""
+    import audio_mastering_engine as ame
+    from amx import capi, synth, wavio
+    from amx.chunking import chunk_bounds, packet_frames
+    n = int(fs * 40.0)
+    x = synth.mix_like(n, fs, 2, seed=fs)
+    settings = dict(C3, lufs=None)
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "in.wav"), os.path.join(d, "out.wav")
+        wavio.write_wav_pcm(src, _native(x, "s16"), fs, "s16")
+        out = ame.master_audio(dict(settings, input_file=src, output_file=dst))
+        assert out == dst
+        y, info = wavio.read_wav_native(dst)
+        raw, winfo, _ = wavio.read_wav_raw(src)
+        x16 = wavio.to_s16(wavio.read_wav_native(src)[0], winfo)
+        bounds = chunk_bounds(n, fs, packet_frames(winfo.block_align))
+        with pytest.raises(capi.AmxError, match="no exact-rational resampler"):
+            ame.master_audio(dict(C3, input_file=src, output_file=dst))
+    assert info.sample_rate == fs
+    ref, _ = oracle_mod.pipeline(x16, fs, settings, bounds)
+    assert y.shape == ref.shape
+    assert int(np.abs(y.astype(np.int32) - ref.astype(np.int32)).max()) == 0
+
+
+def test_master_audio_192k_dynamic(gpu, oracle_mod):
+    """a 192 kHz input that loudnorm sends to dynamic mode: ffmpeg inserts no resampler
+    (only s16 -> dbl), the filter and the alimiter run at the input rate"""
+    import audio_mastering_engine as ame
+    from amx import synth, wavio
+    from amx.chunking import chunk_bounds, packet_frames
+    fs = 192000
+    n = int(fs * 8.0)
+    x = synth.mix_like(n, fs, 2, seed=19) * 0.12
+    rng = np.random.default_rng(19)
+    for k in rng.integers(0, n - 800, 16):
+        x[k:k + 200] += rng.uniform(-0.9, 0.9, (200, 2))
+    x = np.clip(x, -1.0, 1.0).astype(np.float32)
+    settings = dict(bass_boost=1.0, lufs=-14.0)
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "in.wav"), os.path.join(d, "out.wav")
+        wavio.write_wav_f32(src, x, fs)
+        ame.master_audio(dict(settings, input_file=src, output_file=dst))
+        y, info = wavio.read_wav_native(dst)
+        raw, winfo, _ = wavio.read_wav_raw(src)
+        x16 = wavio.to_s16(wavio.read_wav_native(src)[0], winfo)
+        bounds = chunk_bounds(n, fs, packet_frames(winfo.block_align))
+    ref, rinfo = oracle_mod.pipeline(x16, fs, settings, bounds)
+    assert rinfo["mode"] == "dynamic", rinfo.get("stats")
+    assert info.sample_rate == 192000 == rinfo["sample_rate"]
+    assert y.shape == ref.shape
+    d = np.abs(y.astype(np.int32) - ref.astype(np.int32))
+    print("192 kHz dynamic: max |diff| %d LSB, exact %.7f" % (d.max(), (d == 0).mean()))
+    assert d.max() <= 3 and (d == 0).mean() >= 0.999
+
+
 @pytest.mark.parametrize("code", ["u8", "s16", "s24", "s32", "f32", "f64"])
 @pytest.mark.parametrize("channels", [1, 2])
 def test_pcm_to_s16_decode(gpu, code, channels):

@@ -74,6 +74,84 @@ def test_filter_vs_oracle(gpu, oracle_mod, seconds, seed, intro):
         _cmp(y, ref, "loudnorm filter %.1f s intro %.1f %s" % (seconds, intro, "pass 2" if measured else "pass 1"))
 
 
+@pytest.mark.parametrize("seg,warm", [(1, 0), (2, 1), (7, 0), (4, 3)])
+def test_parallel_splits_vs_oracle(gpu, oracle_mod, monkeypatch, seg, warm):
+    """the parallel form under work splits that make most start guesses wrong (no
+    warm-up, one-frame segments) on material that keeps the true-peak limiter busy
+    (an offset of +9 dB): the walker's re-runs and the FINAL re-run carry the result,
+    which must still be the oracle's"""
+    import torch
+    from amx import capi
+    from amx.engine import MasteringJob
+    monkeypatch.setenv("AMX_LN_SEG", str(seg))
+    monkeypatch.setenv("AMX_LN_WARM", str(warm))
+    fs = 48000
+    x = _dynamic_signal(20.0, fs, 17)
+    x16 = oracle_mod.quantize(x)
+    st = oracle_mod.loudnorm_measure(x16, fs)
+    job = MasteringJob(fs, 2, {"lufs": -14.0}, [x16.shape[0]], input_s16=True,
+                       chunks=[(0, 0, x16.shape[0])], measure_only=True)
+    job.out[:x16.shape[0]].copy_(torch.from_numpy(x16))
+    job.loudness_pass1(tail=False)
+    job.loudness_pass2(carry=False)
+    job.histograms()
+    job.decide()
+    n192, job2, ws2, summ = job._job192(0, cached=False)[0:4]
+    for offset in (0.0, 9.0):
+        d = capi.LoudnormDesc(-14.0, 11.0, -1.5, float(st["input_i"]), float(st["input_lra"]),
+                              float(st["input_tp"]), float(st["input_thresh"]), offset)
+        job.loudnorm_192k(0, d, job2, ws2, summ)
+        s = summ.cpu().numpy()
+        assert s[12] > 0 and s[13] == 0, s
+        ref, _ = oracle_mod.loudnorm(x16, fs, -14.0, measured=st, offset=offset)
+        print("split Fs=%d Wf=%d offset %.1f: %d segments, %d re-run, FINAL re-run %d" %
+              (seg, warm, offset, s[12], s[10], s[11]))
+        _cmp(job2.out[:n192].cpu().numpy(), ref, "parallel split Fs=%d Wf=%d offset %.1f" % (seg, warm, offset))
+
+
+@pytest.mark.timeout(900)
+def test_filter_300s_vs_oracle(gpu, oracle_mod):
+    """a 5-minute track (the C2/C3 length) through the parallel form of dynamic mode
+    (k_lp_stats / k_lp_seg / k_lp_walk) against orc_loudnorm, with pass 1's options and
+    with pass 2's (the measured strings, an offset): every segment boundary checked, the
+    FINAL flush frame, the whole 192 kHz output compared"""
+    import time
+    import torch
+    from amx import capi
+    from amx.engine import MasteringJob
+    fs = 48000
+    x = _dynamic_signal(300.0, fs, 3)
+    x16 = oracle_mod.quantize(x)
+    st = oracle_mod.loudnorm_measure(x16, fs)
+    job = MasteringJob(fs, 2, {"lufs": -14.0}, [x16.shape[0]], input_s16=True,
+                       chunks=[(0, 0, x16.shape[0])], measure_only=True)
+    job.out[:x16.shape[0]].copy_(torch.from_numpy(x16))
+    job.loudness_pass1(tail=False)
+    job.loudness_pass2(carry=False)
+    job.histograms()
+    job.decide()
+    assert job.fetch_report(raise_dynamic=False)["stats"][0] == st
+    n192, job2, ws2, summ = job._job192(0)
+    for measured, offset in ((None, 0.0), (st, 2.37)):
+        d = capi.LoudnormDesc(-14.0, 11.0, -1.5, 0.0, 0.0, 99.0, -70.0, offset)
+        if measured:
+            d.measured_i, d.measured_lra = float(st["input_i"]), float(st["input_lra"])
+            d.measured_tp, d.measured_thresh = float(st["input_tp"]), float(st["input_thresh"])
+        job.loudnorm_192k(0, d, job2, ws2, summ)           # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        job.loudnorm_192k(0, d, job2, ws2, summ)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        s = summ.cpu().numpy()
+        assert s[12] > 0 and s[13] == 0, s            # the parallel form ran (no hand-over)
+        y = job2.out[:n192].cpu().numpy()
+        ref, _ = oracle_mod.loudnorm(x16, fs, -14.0, measured=measured, offset=offset)
+        print("300 s filter %s: %.2f ms, %d segments, %d re-run, FINAL re-run %d" %
+              ("pass 2" if measured else "pass 1", dt * 1e3, s[12], s[10], s[11]))
+        _cmp(y, ref, "loudnorm filter 300 s %s" % ("pass 2" if measured else "pass 1"))
+
+
 @pytest.mark.parametrize("seconds,intro", [(12.0, 0.0), (2.0, 0.0), (8.0, 3.5)])
 def test_master_audio_dynamic(gpu, oracle_mod, seconds, intro):
     import audio_mastering_engine as ame

