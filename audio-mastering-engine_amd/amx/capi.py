@@ -139,7 +139,7 @@ def load(path=None):
                                          ctypes.POINTER(ctypes.c_int64)]
     L.amx_loudnorm_192k.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(LoudnormDesc), vp, vp,
                                     ctypes.c_int64, vp, vp, vp, vp, vp]
-    L.amx_loudnorm_192k_ex.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(LoudnormDesc), vp, vp, vp, vp,
+    L.amx_loudnorm_192k_ex.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(LoudnormDesc), vp, vp, vp, vp, vp,
                                        ctypes.c_int64, vp, vp, vp, vp, vp]
     if L.amx_abi_version() != ABI_VERSION:
         raise AmxError("libamx ABI version mismatch")

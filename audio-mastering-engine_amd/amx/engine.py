@@ -101,6 +101,8 @@ class MasteringJob:
         self.lim_state = torch.zeros((T, self.state_doubles), dtype=torch.float64, device=dev)
         # general-path limiter segments: allocated now, never inside a graph capture
         self.plan.limiter_prepare(self.fd, limiter_seg_frames, limiter_warm_frames)
+        self._i_out = torch.zeros((T,), dtype=torch.float64, device=dev)   # pass 1's output I (dynamic)
+        self._dyn_sides = None     # per track, the 192 kHz sets run() enqueues (prepare_dynamic)
         self.report = {}
 
     # ------------------------------------------------------------ device steps
@@ -222,65 +224,62 @@ class MasteringJob:
             self._j192 = (key, job2, ws2, summ)
         return n192.value, self._j192[1], self._j192[2], self._j192[3]
 
-    def loudnorm_192k(self, t, desc, job2, ws2, summ, stream=None):
+    def loudnorm_192k(self, t, desc, job2, ws2, summ, stream=None, measured=None, offset_i=None, gate=None):
+        """amx_loudnorm_192k_ex: measured / offset_i / gate are device rows (None: desc's
+        host values, no gate) -- see include/amx.h"""
         import ctypes
-        capi.check(capi.load().amx_loudnorm_192k(
-            self.plan.h, t, ctypes.byref(desc), capi.ptr(self.out), capi.ptr(self.hops),
-            int(self.max_hops), capi.ptr(self.peak), capi.ptr(job2.out), capi.ptr(summ), capi.ptr(ws2),
-            self._s(stream)), "amx_loudnorm_192k")
+        capi.check(capi.load().amx_loudnorm_192k_ex(
+            self.plan.h, t, ctypes.byref(desc), capi.ptr(measured), capi.ptr(offset_i), capi.ptr(gate),
+            capi.ptr(self.out), capi.ptr(self.hops), int(self.max_hops), capi.ptr(self.peak), capi.ptr(job2.out),
+            capi.ptr(summ), capi.ptr(ws2), self._s(stream)), "amx_loudnorm_192k")
 
-    def dynamic_track(self, t, stats, stream=None):
+    def dynamic_track(self, t, stats=None, stream=None):
         """loudnorm's dynamic mode for track t (:240 when the linear conditions fail), as
         the reference's two ffmpeg passes run it: pass 1's filter with the measured_*
         defaults, whose output loudness gives target_offset; pass 2's filter with the
         pass-1 strings; then the alimiter (:223) at 192 kHz.  Returns (int16 [n192, 2] at
-        192 kHz, info).  Every per-sample step is on the device; the host reads pass 1's
-        output loudness (one double) to form the "%.2f" string pass 2 parses."""
-        run = self._dyn_pass1(t, stream, cached=True)
-        self._dyn_pass2(run, stats, stream)
+        192 kHz, info).  Every step is on the device, without a host round trip (the
+        "%.2f" strings pass 2 parses are formed there); the host reads the result."""
+        run = self._dyn_enqueue(t, self._job192(t, cached=True), stream)
         return self._dyn_result(run, stream)
 
-    def _dyn_pass1(self, t, stream, cached, side=None):
-        """pass 1 of the dynamic path, enqueued: the filter with the measured_* defaults
-        and the 192 kHz measurement of its output.  side: the 192 kHz set of _job192,
-        made beforehand (a plan's creation synchronises the device)."""
-        n192, job2, ws2, summ = side if side is not None else self._job192(t, cached)
+    def _dyn_enqueue(self, t, side, stream, gate=False):
+        """Both passes of the dynamic path for track t, enqueued on `stream`: pass 1's
+        filter with the measured_* defaults and the 192 kHz measurement of its output
+        (its integrated loudness is pass 1's target_offset); pass 2's filter with the
+        track's own pass-1 statistics (k_decide's "%.2f" values) and that offset; the
+        192 kHz measurement of its output (the alimiter's input bound) and the alimiter.
+        side: the 192 kHz set of _job192 (made beforehand: a plan's creation synchronises
+        the device).  gate: every loudnorm kernel first checks the track's control word
+        and returns unless it says dynamic (a captured step holds the path for whichever
+        tracks need it)."""
+        n192, job2, ws2, summ = side
         target = float(self.settings["lufs"])
-        d = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
-        self.loudnorm_192k(t, d, job2, ws2, summ, stream)
+        g = self.ctl[t:t + 1] if gate else None
+        d1 = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
+        self.loudnorm_192k(t, d1, job2, ws2, summ, stream, gate=g)
         job2.loudness_pass1(stream, tail=False)
         job2.loudness_pass2(stream, carry=False)
         job2.histograms(stream)
         job2.dd.lufs_on = 1
         job2.decide(stream)
-        return {"t": t, "n192": n192, "job2": job2, "ws2": ws2, "summ": summ, "desc": d}
-
-    def _dyn_pass2(self, run, stats, stream):
-        """reads pass 1's output loudness (waits for that stream only) and enqueues pass 2's
-        filter, the 192 kHz measurement of its output and the alimiter"""
-        job2, d = run["job2"], run["desc"]
-        # read on the track's own stream: a read on the legacy default stream would also
-        # wait for every other track's work enqueued so far
         with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
-            i_out = float(job2.stats[0, 0].item())
-        target = float(self.settings["lufs"])
-        run["target_offset"] = loudness._fmt(target - i_out)
-        run["i_out"] = i_out
-        d.measured_i = float(stats["input_i"])
-        d.measured_lra = float(stats["input_lra"])
-        d.measured_tp = float(stats["input_tp"])
-        d.measured_thresh = float(stats["input_thresh"])
-        d.offset = float(run["target_offset"])
-        self.loudnorm_192k(run["t"], d, job2, run["ws2"], run["summ"], stream)
+            self._i_out[t:t + 1].copy_(job2.stats[0, 0:1])       # pass 1's output loudness
+        d2 = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
+        self.loudnorm_192k(t, d2, job2, ws2, summ, stream, measured=self.stats[t], offset_i=self._i_out[t:t + 1],
+                           gate=g)
         job2.loudness_pass1(stream, tail=False)            # the limiter's input bound
         job2.dd.lufs_on = 0
         job2.decide(stream)
         job2.finalize(None, stream)
+        return {"t": t, "n192": n192, "job2": job2, "ws2": ws2, "summ": summ}
 
     def _dyn_result(self, run, stream):
         with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
             prof = run["summ"].cpu().numpy()
-        info = {"target_offset": run["target_offset"], "pass1_output_i": run["i_out"],
+            i_out = float(self._i_out[run["t"]].item())
+        target = float(self.settings["lufs"])
+        info = {"target_offset": loudness._fmt(target - i_out), "pass1_output_i": i_out,
                 "sample_rate": 192000}
         if prof[12] > 0 and prof[13] == 0:
             # the parallel form (amx_loudnorm.hip k_lp_*): its walker's diagnostics
@@ -328,15 +327,43 @@ class MasteringJob:
             self.timed("hist", lambda: self.histograms(stream), stream)
         self.timed("decide", lambda: self.decide(stream), stream)
         self.timed("final", lambda: self.finalize(None, stream), stream)
+        if self._dyn_sides:
+            # the dynamic path of every track, gated on the device by the track's decision
+            # (a linear track's kernels return at once): the step needs no host round trip
+            # whichever mode loudnorm takes
+            for t, side in enumerate(self._dyn_sides):
+                self._dyn_enqueue(t, side, stream, gate=True)
         self.report = {"chunks": len(self.chunks), "segments": self.info.n_segments}
         return self.y[:self.info.out_frames]
 
-    def capture(self, d_in):
+    def prepare_dynamic(self):
+        """Make run() (and a graph captured from it) hold loudnorm's dynamic path for every
+        track, gated on the device: the 192 kHz plans and scratch are made here, outside
+        any capture.  Afterwards dynamic_output(t) is track t's 192 kHz result when the
+        step's decision was dynamic."""
+        if self.dd.lufs_on and self._dyn_sides is None:
+            self._dyn_sides = [self._job192(t, cached=False) for t in range(self.n_tracks)]
+
+    def dynamic_output(self, t, stream=None):
+        """after a step with prepare_dynamic(): (int16 [n192, 2], info) of track t if its
+        loudnorm took dynamic mode, else None (synchronises the stream)"""
+        if not self._dyn_sides:
+            return None
+        mode = capi.MODES[int(self.stats[t, 8].item())]
+        if mode != "dynamic":
+            return None
+        n192, job2, ws2, summ = self._dyn_sides[t]
+        return self._dyn_result({"t": t, "n192": n192, "job2": job2, "ws2": ws2, "summ": summ}, stream)
+
+    def capture(self, d_in, dynamic=False):
         """Record run(d_in) as one hipGraph (torch.cuda.CUDAGraph over the HIP stream
         capture): replay() then re-issues the whole pipeline -- every kernel, same
         buffers -- with one launch, so the host's per-kernel launch cost is off the
         critical path.  run() has no host round trip, so the captured graph is the
-        complete step."""
+        complete step.  dynamic: the graph also holds loudnorm's dynamic path
+        (prepare_dynamic), so a track that takes it is finished inside the step too."""
+        if dynamic:
+            self.prepare_dynamic()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -374,9 +401,7 @@ class MasteringJob:
             for t, side in zip(dyn, sides):
                 st = torch.cuda.Stream(device=self.device)   # (HIP spreads streams over its hardware queues)
                 st.wait_stream(cur)
-                runs.append((st, self._dyn_pass1(t, st, cached=False, side=side)))
-            for st, run in runs:
-                self._dyn_pass2(run, rep["stats"][run["t"]], st)
+                runs.append((st, self._dyn_enqueue(t, side, st)))
             for st, run in runs:
                 y, info = self._dyn_result(run, st)
                 cur.wait_stream(st)

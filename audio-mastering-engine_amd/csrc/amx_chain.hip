@@ -117,7 +117,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_front1(const ChainDev *__restrict
 // t: 16-B column t % 8 of rows t / 8 + 32 m), issued one tile ahead; only a
 // workgroup with a partial (chunk-final) segment clamps addresses (PART).
 #define AMX_F1_PITCH (2 * AMX_TF + 2)   // dwords per LDS row: 8-B aligned, conflict-free
-template <int D, bool AN, bool PART>
+// HT: lut is the odd-symmetric half table in LDS (k_front1h): tanh(s) = sign(s) lut[|s|]
+template <int D, bool AN, bool PART, bool HT = false>
 __device__ __forceinline__ void front1s_run(const ChainDev &cd, const float *__restrict__ lut,
                                             const uint32_t *__restrict__ const *ip,
                                             const int *ilen, uint32_t *const *op,
@@ -170,8 +171,16 @@ __device__ __forceinline__ void front1s_run(const ChainDev &cd, const float *__r
 #pragma unroll
             for (int i = 0; i < AMX_TF / 2; i++) {
                 const int f = 2 * i + half;
-                t0[i] = lut[(int)q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f])) + 32768];
-                t1[i] = lut[(int)q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f + 1])) + 32768];
+                const int q0 = (int)q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f]));
+                const int q1 = (int)q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f + 1]));
+                if constexpr (HT) {
+                    const float v0 = lut[q0 < 0 ? -q0 : q0], v1 = lut[q1 < 0 ? -q1 : q1];
+                    t0[i] = q0 < 0 ? -v0 : v0;
+                    t1[i] = q1 < 0 ? -v1 : v1;
+                } else {
+                    t0[i] = lut[q0 + 32768];
+                    t1[i] = lut[q1 + 32768];
+                }
             }
 #pragma unroll
             for (int i = 0; i < AMX_TF / 2; i++) {
@@ -275,6 +284,69 @@ __global__ void __launch_bounds__(AMX_BLOCK, 4) k_front1s(const ChainDev *__rest
     else
         front1s_run<D, AN, false>(cd, lut, ip, ilen, op, c4, rg, s_in, s_out, row, half, L, len,
                                   G, sG, eo);
+}
+
+// k_front1s<D, true> with the tanh table in LDS.  numpy's float32 tanh table is odd
+// (the plan checks every pair bit for bit, amx_plan.cpp), so its 32 769-entry half
+// (128 KB) fits the 160 KB LDS beside the tile buffers: one workgroup per CU, persistent
+// over the segment blocks, loads the half table once; a lookup is an LDS read instead of
+// a gather from the 256 KB global table through the texture path.
+#define AMX_HALF_LUT 32769
+template <int D>
+__global__ void __launch_bounds__(AMX_BLOCK, 1) k_front1h(const ChainDev *__restrict__ cdp,
+                                                          const ChunkDev *__restrict__ chunks,
+                                                          const SegDev *__restrict__ segs,
+                                                          int n_seg, int L,
+                                                          const uint32_t *__restrict__ in,
+                                                          const float *__restrict__ lut_half,
+                                                          uint32_t *__restrict__ a16,
+                                                          const double *__restrict__ G,
+                                                          double *__restrict__ e) {
+    constexpr int ROWS = AMX_BLOCK / 2;
+    constexpr int H = D / 2;
+    __shared__ float s_tab[AMX_HALF_LUT];
+    __shared__ uint32_t s_in[ROWS * AMX_F1_PITCH];
+    __shared__ uint32_t s_out[ROWS * (AMX_TF + 1)];
+    __shared__ __attribute__((aligned(16))) double sG[AMX_TF * (D > 0 ? D : 2)];
+    __shared__ int64_t rb_in[ROWS], rb_out[ROWS];
+    __shared__ int rl[ROWS];
+    static_assert(AMX_TF * D / 2 <= AMX_BLOCK, "one 16-B piece of the G tile per thread");
+    static_assert(D % 2 == 0, "state split in halves");
+    for (int i = threadIdx.x; i < AMX_HALF_LUT; i += AMX_BLOCK) s_tab[i] = lut_half[i];
+    const ChainDev &cd = *cdp;
+    const int t = threadIdx.x, row = t >> 1, half = t & 1;
+    const int nblk = (n_seg + ROWS - 1) / ROWS;
+    for (int b = blockIdx.x; b < nblk; b += gridDim.x) {
+        __syncthreads();                       // the previous block's rb / rl reads are done
+        const int j = b * ROWS + row;
+        const bool valid = j < n_seg;
+        const SegDev sg = segs[valid ? j : n_seg - 1];
+        const ChunkDev ch = chunks[sg.chunk];
+        const int len = valid ? sg.len : 0;
+        if (half == 0) {
+            rb_in[row] = valid ? (ch.in_off + sg.pos) * 2 : 0;
+            rb_out[row] = valid ? ch.loc_off + sg.pos : 0;
+            rl[row] = len;
+        }
+        const int part = __syncthreads_or(len < L);
+        const int c4 = t & 7, rg = t >> 3;
+        const uint32_t *ip[4];
+        int ilen[4];
+        uint32_t *op[4];
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            ip[m] = in + rb_in[rg + 32 * m] + 4 * c4;
+            ilen[m] = rl[rg + 32 * m];
+            op[m] = a16 + rb_out[rg + 32 * m] + 2 * c4;
+        }
+        double *eo = (D > 0 && valid && !sg.last) ? e + (int64_t)j * 2 * D + half * H : nullptr;
+        if (part)
+            front1s_run<D, true, true, true>(cd, s_tab, ip, ilen, op, c4, rg, s_in, s_out, row, half, L,
+                                             len, G, sG, eo);
+        else
+            front1s_run<D, true, false, true>(cd, s_tab, ip, ilen, op, c4, rg, s_in, s_out, row, half, L,
+                                              len, G, sG, eo);
+    }
 }
 
 // ------------------------------------------- pass 2: EQ from true state -> int16
@@ -591,10 +663,30 @@ static hipError_t front1_t(const Launch &l, const uint32_t *in, const float *lut
     return hipGetLastError();
 }
 
+static int cu_count() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
 template <int D, bool AN>
 static hipError_t front1s_t(const Launch &l, const uint32_t *in, const float *lut, uint32_t *a16,
                             const double *G, double *e) {
     const int rows = AMX_BLOCK / 2;
+    if constexpr (AN) {
+        if (l.lut_half) {
+            const int nblk = (l.n_seg + rows - 1) / rows;
+            dim3 grid((unsigned)(nblk < cu_count() ? nblk : cu_count()));
+            hipLaunchKernelGGL((k_front1h<D>), grid, dim3(AMX_BLOCK), 0, l.stream, l.cd, l.chunks, l.segs,
+                               l.n_seg, l.L, in, l.lut_half, a16, G, e);
+            return hipGetLastError();
+        }
+    }
     dim3 grid((unsigned)((l.n_seg + rows - 1) / rows));
     hipLaunchKernelGGL((k_front1s<D, AN>), grid, dim3(AMX_BLOCK), 0, l.stream, l.cd, l.chunks,
                        l.segs, l.n_seg, l.L, in, lut, a16, G, e);

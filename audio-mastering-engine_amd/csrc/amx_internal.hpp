@@ -130,6 +130,7 @@ struct Launch {
     const SegDev *segs;
     int32_t n_chunks, n_seg, L;
     hipStream_t stream;
+    const float *lut_half = nullptr;   // odd tanh table's half (k_front1h), NULL: the full table
 };
 struct ScanPlan {
     int D, n_blk, K;
@@ -245,6 +246,7 @@ struct LpArgs {
     double target_i, target_lra, ceiling, measured_i, measured_thresh, offset;  // host values
     const double *measured_src;   // non-NULL: measured I / thresh from this k_decide row ([4], [7])
     const double *offset_src;     // non-NULL: offset = "%.2f"(target_i - offset_src[0]) dB
+    const int32_t *gate;          // non-NULL: run only if this k_decide control word says dynamic
     double weights[21];
     double *v;                    // [T] AGC value of each INNER frame (when not held)
     int *hold;                    // [T] 1: the frame keeps the previous delta
@@ -256,13 +258,16 @@ struct LpArgs {
     int *cnt, *match;             // [K + 1] boundary arrivals, start guess == previous end
     double *rings;                // [P][AMX_LN_RING][2] per-wave limiter rings
     double *wring;                // [AMX_LN_RING][2] the walker's ring
-    int *ctl;                     // [16] 0 serial, 1 re-runs, 2 FINAL re-run, 3 above_threshold
-    double *dctl;                 // [8] 0 d0, 1 offset (linear), 2 measured_i, 3 measured_thresh
+    int *ctl;                     // [16] 0: 0 parallel, 1 frame by frame (k_ln_dyn), 2 handed over,
+                                  // 3 gated off; 1 re-runs, 2 FINAL re-run, 3 above_threshold
+    double *dctl;                 // [8] 0 d0, 1 offset (linear), 2 measured_i, 3 measured_thresh,
+                                  // 4 offset (dB)
     int16_t *y;                   // [n][2] output
     double *summary;              // [16]
 };
 hipError_t launch_loudnorm(const LnArgs &a, const LpArgs &p, const uint32_t *x, int64_t n_in, int L,
                            int M, const float *bank, hipStream_t st);
+#define AMX_LN_GATED(g) ((g) && (((g)[0] >> 4) & 15) != 3)   // k_decide mode 3 = dynamic
 hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent_t fork, hipEvent_t join);
 int swr_geometry(int in_rate, int out_rate, int *L, int *M);   // host (amx_plan.cpp)
 int swr_bank(int in_rate, int out_rate, float *bank);

@@ -67,9 +67,10 @@ __device__ __forceinline__ float ln_dot(const float *w, const float *__restrict_
 // one thread per 192 kHz frame: both channels
 __global__ void __launch_bounds__(AMX_BLOCK) k_ln_upsample(const uint32_t *__restrict__ x, int64_t n_in,
                                                            int L, int M, const float *__restrict__ bank,
-                                                           int64_t n192, float *__restrict__ u) {
+                                                           int64_t n192, float *__restrict__ u,
+                                                           const int32_t *__restrict__ gate) {
     const int64_t j = (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x;
-    if (j >= n192) return;
+    if (j >= n192 || AMX_LN_GATED(gate)) return;
     const int64_t idx = j * M, base = idx / L;
     const int ph = (int)(idx % L);
     float w0[LN_TAPS], w1[LN_TAPS];
@@ -516,7 +517,7 @@ __device__ double ln_out_energy(const double *ring, int lbi, int nb, double ceil
 __global__ void __launch_bounds__(LN_NT) k_ln_dyn(LnArgs a0) {
     // after the parallel form's statistics (k_lp_stats): only the tracks it hands over
     // (the < 3 s linear fallback, a quiet start), with the options it resolved
-    if (a0.lp_ctl && a0.lp_ctl[0] == 0) return;
+    if (a0.lp_ctl && (a0.lp_ctl[0] == 0 || a0.lp_ctl[0] == 3)) return;
     LnArgs a = a0;
     if (a0.lp_dctl) {
         a.offset = a0.lp_dctl[1];
@@ -789,6 +790,10 @@ __global__ void __launch_bounds__(LP_STAT_NT) k_lp_stats(LpArgs a) {
     const int tid = threadIdx.x;
     const double mi = a.measured_src ? a.measured_src[4] : a.measured_i;
     const double mt = a.measured_src ? a.measured_src[7] : a.measured_thresh;
+    if (AMX_LN_GATED(a.gate)) {        // the track is not in dynamic mode: nothing runs
+        if (blockIdx.x == 0 && tid == 0) a.ctl[0] = 3;
+        return;
+    }
     if (blockIdx.x == 0) {
         const bool full = a.n >= LP_FIRST;
         const double st = full ? lp_shortterm(a.hops, LP_FIRST / LP_FR, red) : 0.0;
@@ -800,7 +805,9 @@ __global__ void __launch_bounds__(LP_STAT_NT) k_lp_stats(LpArgs a) {
             a.ctl[2] = 0;
             a.ctl[3] = above ? 1 : 0;
             a.dctl[0] = pow(10., env / 20.);
-            a.dctl[1] = a.offset_src ? pow(10., round2(a.target_i - a.offset_src[0]) / 20.) : a.offset;
+            const double off_db = a.offset_src ? round2(a.target_i - a.offset_src[0]) : 20. * log10(a.offset);
+            a.dctl[1] = a.offset_src ? pow(10., off_db / 20.) : a.offset;
+            a.dctl[4] = off_db;
             a.dctl[2] = mi;
             a.dctl[3] = mt;
         }
@@ -1482,7 +1489,7 @@ hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x
                            int M, const float *bank, hipStream_t st) {
     if (ln.n192 <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_ln_upsample, dim3((unsigned)((ln.n192 + AMX_BLOCK - 1) / AMX_BLOCK)), dim3(AMX_BLOCK),
-                       0, st, x, n_in, L, M, bank, ln.n192, ln.u);
+                       0, st, x, n_in, L, M, bank, ln.n192, ln.u, lp.gate);
     hipLaunchKernelGGL(k_lp_stats, dim3(1 + (lp.T + LP_STAT_F - 1) / LP_STAT_F), dim3(LP_STAT_NT), 0, st, lp);
     hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
     const int gb = max((lp.T + 1 + 255) / 256, (LP_FR + 255) / 256);

@@ -33,21 +33,28 @@ int fail(int code, const char *fmt, ...) {
     } while (0)
 
 // ------------------------------------------------------------ dense helpers
+// The scan tables (GEMV rows A^n B, A^L, block powers) are computed in long double (x86
+// 80-bit, 64-bit mantissa) and rounded to double once: built in double by repeated
+// products they carried ~1e-12 of error into the segment start states at 96 kHz
+// (DESIGN.md §3.1), 20x the sequential recursion's own rounding; rounded once they
+// carry less than it.
+using LD = long double;
 using Mat = std::vector<double>;  // row-major D x D
+using MatL = std::vector<LD>;
 
-Mat matmul(const Mat &a, const Mat &b, int D) {
-    Mat c((size_t)D * D, 0.0);
+MatL matmul(const MatL &a, const MatL &b, int D) {
+    MatL c((size_t)D * D, 0.0L);
     for (int i = 0; i < D; i++)
         for (int k = 0; k < D; k++) {
-            double v = a[(size_t)i * D + k];
-            if (v == 0.0) continue;
+            const LD v = a[(size_t)i * D + k];
+            if (v == 0.0L) continue;
             for (int j = 0; j < D; j++) c[(size_t)i * D + j] += v * b[(size_t)k * D + j];
         }
     return c;
 }
-Mat matpow(const Mat &a, int64_t p, int D) {
-    Mat r((size_t)D * D, 0.0), b = a;
-    for (int i = 0; i < D; i++) r[(size_t)i * D + i] = 1.0;
+MatL matpow(const MatL &a, int64_t p, int D) {
+    MatL r((size_t)D * D, 0.0L), b = a;
+    for (int i = 0; i < D; i++) r[(size_t)i * D + i] = 1.0L;
     while (p > 0) {
         if (p & 1) r = matmul(r, b, D);
         b = matmul(b, b, D);
@@ -55,46 +62,48 @@ Mat matpow(const Mat &a, int64_t p, int D) {
     }
     return r;
 }
-double norm_inf(const Mat &a, int D) {
-    double m = 0.0;
+LD norm_inf(const MatL &a, int D) {
+    LD m = 0.0L;
     for (int i = 0; i < D; i++) {
-        double s = 0.0;
+        LD s = 0.0L;
         for (int j = 0; j < D; j++) s += std::fabs(a[(size_t)i * D + j]);
         m = s > m ? s : m;
     }
     return m;
 }
+Mat to_double(const MatL &a) { return Mat(a.begin(), a.end()); }
 
-// A linear time-invariant model s' = A s + B x of a chain, derived by stepping a
-// host copy of the chain from unit states / a unit input.
+// A linear time-invariant model s' = A s + B x of a chain, derived (in long double) by
+// stepping a host copy of the chain from unit states / a unit input.
 struct Lti {
     int D = 0;
-    Mat A;
-    std::vector<double> B;
+    MatL A;
+    std::vector<LD> B;
     template <class Step>
     void derive(int dim, Step step) {
         D = dim;
-        A.assign((size_t)D * D, 0.0);
-        B.assign(D, 0.0);
-        std::vector<double> s(D);
+        A.assign((size_t)D * D, 0.0L);
+        B.assign(D, 0.0L);
+        std::vector<LD> s(D);
         for (int k = 0; k < D; k++) {
-            std::fill(s.begin(), s.end(), 0.0);
-            s[k] = 1.0;
-            step(s.data(), 0.0);
+            std::fill(s.begin(), s.end(), 0.0L);
+            s[k] = 1.0L;
+            step(s.data(), 0.0L);
             for (int i = 0; i < D; i++) A[(size_t)i * D + k] = s[i];
         }
-        std::fill(s.begin(), s.end(), 0.0);
-        step(s.data(), 1.0);
+        std::fill(s.begin(), s.end(), 0.0L);
+        step(s.data(), 1.0L);
         for (int i = 0; i < D; i++) B[i] = s[i];
     }
+    Mat pow(int64_t p) const { return to_double(matpow(A, p, D)); }
     // G[n][d] = (A^{L-1-n} B)[d]
     std::vector<double> gemv_table(int L) const {
         std::vector<double> G((size_t)L * D);
-        std::vector<double> v = B, t(D);
+        std::vector<LD> v = B, t(D);
         for (int n = L - 1; n >= 0; n--) {
-            for (int d = 0; d < D; d++) G[(size_t)n * D + d] = v[d];
+            for (int d = 0; d < D; d++) G[(size_t)n * D + d] = (double)v[d];
             for (int i = 0; i < D; i++) {
-                double acc = 0.0;
+                LD acc = 0.0L;
                 for (int k = 0; k < D; k++) acc += A[(size_t)i * D + k] * v[k];
                 t[i] = acc;
             }
@@ -105,48 +114,33 @@ struct Lti {
     // window powers Mb^k, k = 1 .. K-1, of Mb = A^LS; K = the first k with
     // ||Mb^k|| <= tol (the block scan sums the previous K-1 blocks' contributions).
     int window_powers(int64_t LS, double tol, int max_k, std::vector<double> &out) const {
-        Mat Mb = matpow(A, LS, D);
-        Mat cur = Mb;
+        MatL Mb = matpow(A, LS, D);
+        MatL cur = Mb;
         out.clear();
         int K = 1;
         while (norm_inf(cur, D) > tol) {
-            out.insert(out.end(), cur.begin(), cur.end());
+            for (LD v : cur) out.push_back((double)v);
             cur = matmul(cur, Mb, D);
             K++;
             if (K > max_k) return -1;
         }
         return K;
     }
-    // powers M^(2^l), l < levels, of M = A^L; levels chosen so that the neglected
-    // tail ||M^(2^levels)|| <= tol (the scan looks back 2^levels - 1 segments).
-    int scan_powers(int L, double tol, int max_levels, std::vector<double> &out) const {
-        Mat M = matpow(A, L, D);
-        std::vector<Mat> pw;
-        Mat cur = M;
-        int levels = 0;
-        while (norm_inf(cur, D) > tol) {
-            pw.push_back(cur);
-            cur = matmul(cur, cur, D);
-            levels++;
-            if (levels > max_levels) return -1;
-        }
-        out.clear();
-        for (auto &m : pw) out.insert(out.end(), m.begin(), m.end());
-        return levels;
-    }
 };
 
 // host step functions (same math as the device chains, no rounding claims)
-void shelf_step_h(const double *c, double *z, double &x, int neg, double gm1) {
-    double y = z[0] + c[0] * x;
-    z[0] = (z[1] + x * c[1]) - y * c[4];
-    z[1] = x * c[2] - y * c[5];
-    x = neg ? y : x + (y - x) * gm1;
+template <class T>
+void shelf_step_h(const double *c, T *z, T &x, int neg, double gm1) {
+    T y = z[0] + (T)c[0] * x;
+    z[0] = (z[1] + x * (T)c[1]) - y * (T)c[4];
+    z[1] = x * (T)c[2] - y * (T)c[5];
+    x = neg ? y : x + (y - x) * (T)gm1;
 }
-double sos_step_h(const double *c, double *z, double x) {
-    double y = c[0] * x + z[0];
-    z[0] = (c[1] * x - c[4] * y) + z[1];
-    z[1] = c[2] * x - c[5] * y;
+template <class T>
+T sos_step_h(const double *c, T *z, T x) {
+    T y = (T)c[0] * x + z[0];
+    z[0] = ((T)c[1] * x - (T)c[4] * y) + z[1];
+    z[1] = (T)c[2] * x - (T)c[5] * y;
     return y;
 }
 
@@ -282,6 +276,7 @@ struct amx_plan {
     int n_prev = 0;
     double *d_tailpow = nullptr;
     float *d_lut = nullptr;
+    float *d_lut_half = nullptr;   // the odd tanh table's half [0, 32768] (k_front1h), or NULL
     unsigned int *d_pcnt = nullptr;   // k_peak_reduce's per-track block counter (self re-arming)
     int *d_ppart = nullptr;           // its per-block partial maxima
     int any_empty_span = 0;           // a span with no K segment: its peak is zeroed directly
@@ -806,7 +801,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     std::vector<double> G, M, Mp, Gx, Mx, Mpx, Gkw, Mkw, Mpkw, qh, qt;
     if (D > 0) {
         Lti eq;
-        eq.derive(D, [&](double *z, double x) {
+        eq.derive(D, [&](LD *z, LD x) {
             int o = 0;
             for (int s = 0; s < 4; s++) {
                 const EqStageDev &st = cd.st[s];
@@ -814,15 +809,15 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
                     shelf_step_h(st.c, z + o, x, st.neg, st.gm1);
                     o += 2;
                 } else if (st.kind == 2) {
-                    double b = x;
+                    LD b = x;
                     for (int k = 0; k < 4; k++) b = sos_step_h(st.c + 6 * k, z + o + 2 * k, b);
-                    x = x + b * st.gm1;
+                    x = x + b * (LD)st.gm1;
                     o += 8;
                 }
             }
         });
         G = eq.gemv_table(p->L);
-        M = matpow(eq.A, p->L, D);
+        M = eq.pow(p->L);
         p->lev_eq = eq.window_powers((int64_t)p->L * AMX_SCAN_S, tol, 16, Mp);
         if (p->lev_eq < 0) {
             delete p;
@@ -831,14 +826,14 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     }
     if (p->mb) {
         Lti xo;
-        xo.derive(AMX_XO_DIM, [&](double *z, double x) {
-            double l = sos_step_h(cd.xlo, z, x);
+        xo.derive(AMX_XO_DIM, [&](LD *z, LD x) {
+            LD l = sos_step_h(cd.xlo, z, x);
             sos_step_h(cd.xlo + 6, z + 2, l);
-            double h = sos_step_h(cd.xhi, z + 4, x);
+            LD h = sos_step_h(cd.xhi, z + 4, x);
             sos_step_h(cd.xhi + 6, z + 6, h);
         });
         Gx = xo.gemv_table(p->L);
-        Mx = matpow(xo.A, p->L, AMX_XO_DIM);
+        Mx = xo.pow(p->L);
         p->lev_x = xo.window_powers((int64_t)p->L * AMX_SCAN_S, tol, 16, Mpx);
         if (p->lev_x < 0) {
             delete p;
@@ -847,8 +842,8 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     }
     {
         Lti &kw = p->kw_model;
-        kw.derive(AMX_KW_DIM, [&](double *z, double x) {
-            double y = sos_step_h(cd.kw1, z, x);
+        kw.derive(AMX_KW_DIM, [&](LD *z, LD x) {
+            LD y = sos_step_h(cd.kw1, z, x);
             sos_step_h(cd.kw2, z + 2, y);
         });
         const int Lseg = p->resamp ? std::max(1, p->upLout) : p->Lkw;
@@ -856,39 +851,48 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             // the measurement kernels keep no GEMV table: their pass over the samples
             // runs the filter from rest and needs the free-response rows C A^n and
             // their Gram sums (amx_loud192.hip k_up / k_up_energy)
-            double Cr[AMX_KW_DIM];
+            LD Cr[AMX_KW_DIM];
             for (int k = 0; k < AMX_KW_DIM; k++) {
-                double z[AMX_KW_DIM] = {0.0, 0.0, 0.0, 0.0};
-                z[k] = 1.0;
-                const double y1 = sos_step_h(cd.kw1, z, 0.0);
+                LD z[AMX_KW_DIM] = {0.0L, 0.0L, 0.0L, 0.0L};
+                z[k] = 1.0L;
+                const LD y1 = sos_step_h(cd.kw1, z, 0.0L);
                 Cr[k] = sos_step_h(cd.kw2, z + 2, y1);
             }
             Gkw.assign((size_t)Lseg * AMX_KW_DIM, 0.0);
             qh.assign((size_t)(Lseg + 1) * 16, 0.0);
             qt.assign((size_t)(Lseg + 1) * 16, 0.0);
-            std::vector<double> r(Cr, Cr + AMX_KW_DIM), t(AMX_KW_DIM);
+            std::vector<LD> r(Cr, Cr + AMX_KW_DIM), t(AMX_KW_DIM), gl((size_t)Lseg * AMX_KW_DIM);
+            std::vector<LD> qa(16, 0.0L);
             for (int n = 0; n < Lseg; n++) {
-                for (int d = 0; d < AMX_KW_DIM; d++) Gkw[(size_t)n * AMX_KW_DIM + d] = r[d];
+                for (int d = 0; d < AMX_KW_DIM; d++) {
+                    gl[(size_t)n * AMX_KW_DIM + d] = r[d];
+                    Gkw[(size_t)n * AMX_KW_DIM + d] = (double)r[d];
+                }
                 for (int u = 0; u < 4; u++)
-                    for (int w = 0; w < 4; w++)
-                        qh[(size_t)(n + 1) * 16 + u * 4 + w] = qh[(size_t)n * 16 + u * 4 + w] + r[u] * r[w];
+                    for (int w = 0; w < 4; w++) {
+                        qa[u * 4 + w] += r[u] * r[w];
+                        qh[(size_t)(n + 1) * 16 + u * 4 + w] = (double)qa[u * 4 + w];
+                    }
                 for (int d = 0; d < AMX_KW_DIM; d++) {     // r <- r A
-                    double acc = 0.0;
+                    LD acc = 0.0L;
                     for (int k = 0; k < AMX_KW_DIM; k++) acc += r[k] * kw.A[(size_t)k * AMX_KW_DIM + d];
                     t[d] = acc;
                 }
                 r = t;
             }
+            std::fill(qa.begin(), qa.end(), 0.0L);
             for (int n = Lseg - 1; n >= 0; n--) {
-                const double *g = &Gkw[(size_t)n * AMX_KW_DIM];
+                const LD *g = &gl[(size_t)n * AMX_KW_DIM];
                 for (int u = 0; u < 4; u++)
-                    for (int w = 0; w < 4; w++)
-                        qt[(size_t)n * 16 + u * 4 + w] = qt[(size_t)(n + 1) * 16 + u * 4 + w] + g[u] * g[w];
+                    for (int w = 0; w < 4; w++) {
+                        qa[u * 4 + w] += g[u] * g[w];
+                        qt[(size_t)n * 16 + u * 4 + w] = (double)qa[u * 4 + w];
+                    }
             }
         } else {
             Gkw = kw.gemv_table(Lseg);
         }
-        Mkw = matpow(kw.A, Lseg, AMX_KW_DIM);
+        Mkw = kw.pow(Lseg);
         // up to 32 block powers: a track measured at its own 192 kHz rate (loudnorm's
         // output) needs ~20 with 128-frame segments (the 38 Hz pole)
         p->lev_kw = kw.window_powers((int64_t)Lseg * AMX_SCAN_S, tol, 32, Mpkw);
@@ -901,7 +905,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             const SpanDev &sp = p->spans[t];
             if (sp.nkseg == 0) continue;
             int len_last = p->ksegs[sp.kseg0 + sp.nkseg - 1].len;
-            Mat P = matpow(kw.A, len_last, AMX_KW_DIM);
+            Mat P = kw.pow(len_last);
             for (int k = 0; k < 16; k++) p->tail_pow[(size_t)t * 16 + k] = P[k];
         }
     }
@@ -956,6 +960,22 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         for (const SpanDev &sp : p->spans) p->any_empty_span |= sp.nkseg == 0 ? 1 : 0;
     }
     if (desc->tanh_lut) UP(p->d_lut, desc->tanh_lut, 65536);
+    if (desc->tanh_lut && desc->analog_on) {
+        // numpy's float32 tanh is odd: lut[32768 - k] == -lut[32768 + k] bit for bit (sign
+        // of zero included) for every k; then tanh(s) = sign(s) * half[|s|] with half[k] =
+        // lut[32768 + k] and half[32768] = -lut[0].  Checked per table: any pair that
+        // differs keeps the full table in global memory (k_front1s).
+        const uint32_t *b = reinterpret_cast<const uint32_t *>(desc->tanh_lut);
+        bool odd = true;
+        for (int k = 1; k < 32768 && odd; k++) odd = b[32768 - k] == (b[32768 + k] ^ 0x80000000u);
+        const char *ev = std::getenv("AMX_F1_HALF");            // (measurements: 0 = full table)
+        if (odd && !(ev && std::atoi(ev) == 0)) {
+            std::vector<float> half(32769);
+            for (int k = 0; k < 32768; k++) half[k] = desc->tanh_lut[32768 + k];
+            half[32768] = -desc->tanh_lut[0];
+            UP(p->d_lut_half, half.data(), half.size());
+        }
+    }
 #undef UP
     // ------------------------------------------------------- workspace layout
     size_t off = 0;
@@ -1016,7 +1036,7 @@ void amx_plan_free(amx_plan *p) {
                     p->d_bounds, p->d_tailpow, p->d_lut, p->d_energies, p->d_carryP,
                     p->d_esegs, p->d_eseg0, p->d_neseg, p->d_pcnt, p->d_ppart,
                     p->lim.seg_state, p->lim.cnt, p->d_obase, p->d_oph, p->d_bank,
-                    p->d_qh, p->d_qt, p->d_slow};
+                    p->d_qh, p->d_qt, p->d_slow, p->d_lut_half};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     if (p->up_fork) (void)hipEventDestroy(p->up_fork);
@@ -1060,7 +1080,7 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     if (stage < 0 || stage >= AMX_STAGE_COUNT) return fail(AMX_EINVAL, "bad stage %d", stage);
     if (p->n_seg == 0) return AMX_OK;
     hipStream_t st = (hipStream_t)stream;
-    amx::Launch l{p->d_cd, p->d_chunks, p->d_segs, p->n_chunks, p->n_seg, p->L, st};
+    amx::Launch l{p->d_cd, p->d_chunks, p->d_segs, p->n_chunks, p->n_seg, p->L, st, p->d_lut_half};
     int16_t *a16 = wsp<int16_t>(d_ws, p->o_a16);
     double *e = wsp<double>(d_ws, p->o_e), *s = wsp<double>(d_ws, p->o_s);
     int16_t *p16 = p->mb ? wsp<int16_t>(d_ws, p->o_p16) : nullptr;
@@ -1293,7 +1313,7 @@ int amx_loudnorm_192k_size(const amx_plan *p, int32_t track, int64_t *frames, in
 }
 
 int amx_loudnorm_192k_ex(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const double *d_measured,
-                         const double *d_offset_i, const int16_t *d_out, const double *d_hops,
+                         const double *d_offset_i, const int32_t *d_gate, const int16_t *d_out, const double *d_hops,
                          int64_t max_hops, const double *d_peak, int16_t *d_y192, double *d_summary,
                          void *d_ws2, void *stream) {
     if (!p || track < 0 || track >= p->n_tracks) return fail(AMX_EINVAL, "bad argument");
@@ -1362,6 +1382,7 @@ int amx_loudnorm_192k_ex(amx_plan *p, int32_t track, const amx_loudnorm_desc *d,
     q.offset = a.offset;
     q.measured_src = d_measured;
     q.offset_src = d_offset_i;
+    q.gate = d_gate;
     for (int i = 0; i < 21; i++) q.weights[i] = a.weights[i];
     q.v = reinterpret_cast<double *>(w + lo.o_v);
     q.hold = reinterpret_cast<int *>(w + lo.o_hold);
@@ -1389,7 +1410,7 @@ int amx_loudnorm_192k_ex(amx_plan *p, int32_t track, const amx_loudnorm_desc *d,
 int amx_loudnorm_192k(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const int16_t *d_out,
                       const double *d_hops, int64_t max_hops, const double *d_peak, int16_t *d_y192,
                       double *d_summary, void *d_ws2, void *stream) {
-    return amx_loudnorm_192k_ex(p, track, d, nullptr, nullptr, d_out, d_hops, max_hops, d_peak, d_y192,
+    return amx_loudnorm_192k_ex(p, track, d, nullptr, nullptr, nullptr, d_out, d_hops, max_hops, d_peak, d_y192,
                                 d_summary, d_ws2, stream);
 }
 
@@ -1416,7 +1437,7 @@ int amx_env_counters(const amx_plan *p, const void *d_ws, int32_t *out, int32_t 
 
 int amx_kw_propagate(const amx_plan *p, int64_t frames, const double *in8, double *out8) {
     if (!p || !in8 || !out8 || frames < 0) return fail(AMX_EINVAL, "bad argument");
-    Mat P = matpow(p->kw_model.A, frames, AMX_KW_DIM);
+    Mat P = p->kw_model.pow(frames);
     for (int c = 0; c < 2; c++)
         for (int i = 0; i < AMX_KW_DIM; i++) {
             double acc = 0.0;
@@ -1580,7 +1601,7 @@ int amx_kw_carry_setup(amx_plan *p, int32_t n_prev, const int64_t *frames_after)
             auto J = [&](int64_t f) { return (f * L + M - 1) / M; };
             gap = J(f0) - J(f0 - frames_after[q]);
         }
-        Mat m = matpow(p->kw_model.A, gap, AMX_KW_DIM);
+        Mat m = p->kw_model.pow(gap);
         for (int k = 0; k < 16; k++) P[(size_t)q * 16 + k] = m[k];
     }
     if (p->d_carryP) (void)hipFree(p->d_carryP);

@@ -149,7 +149,7 @@ typedef struct amx_track_span {
 AMX_API int amx_abi_version(void);
 AMX_API const char *amx_last_error(void);
 /* Build provenance: the SHA-256 (hex) of the sources this library was compiled from
- * (csrc/*, include/amx.h; amx/build.py source_hash), stamped at compile time.  The
+ * (csrc sources and headers, include/amx.h; amx/build.py source_hash), stamped at compile time.  The
  * Python binding refuses a library whose stamp differs from the tree it runs in. */
 AMX_API const char *amx_build_id(void);
 
@@ -267,10 +267,13 @@ AMX_API int amx_loudnorm_192k(amx_plan *plan, int32_t track, const amx_loudnorm_
  * input_thresh, already the "%.2f" values pass 2 parses); d_offset_i (nullable) = the
  * statistics row of pass 1's output measurement ([0] its integrated loudness): offset =
  * "%.2f"(target_i - that) dB, as pass 1's JSON target_offset (:229-241).  A NULL
- * pointer takes desc's value. */
+ * pointer takes desc's value.  d_gate (nullable) = the track's amx_loudness_decide
+ * control word (d_ctl + track): unless it says dynamic mode, every kernel of the call
+ * returns at once (a captured step then holds the dynamic path for the tracks that
+ * need it). */
 AMX_API int amx_loudnorm_192k_ex(amx_plan *plan, int32_t track, const amx_loudnorm_desc *desc,
                                  const double *d_measured, const double *d_offset_i,
-                                 const int16_t *d_out, const double *d_hops, int64_t max_hops,
+                                 const int32_t *d_gate, const int16_t *d_out, const double *d_hops, int64_t max_hops,
                                  const double *d_peak, int16_t *d_y192, double *d_summary, void *d_ws2,
                                  void *stream);
 /* Host helper for chunk-sharded tracks: out8 = A^frames * in8 (per channel 4x4 K-filter

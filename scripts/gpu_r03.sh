@@ -19,6 +19,7 @@ for s in ${STEPS}; do
   case $s in
     dyn)      run dyn 900 $PYT tests/test_gpu_dynamic.py || exit $? ;;
     dynfast)  run dynfast 600 $PYT tests/test_gpu_dynamic.py -k "splits or filter_vs" || exit $? ;;
+    dropnew)  run dropnew 600 $PYT tests/test_gpu_dropin.py -k "rates or 192k" || exit $? ;;
     dyn300)   run dyn300 900 $PYT tests/test_gpu_dynamic.py -k "300s" || exit $? ;;
     dynbench) run dynbench 300 python scripts/dyn_bench.py --seconds 300 --reps 3 --cpu-seconds 10 || exit $? ;;
     tests)    run tests 1100 $PYT tests -m gpu || exit $? ;;

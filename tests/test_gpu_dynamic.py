@@ -109,6 +109,79 @@ def test_parallel_splits_vs_oracle(gpu, oracle_mod, monkeypatch, seg, warm):
         _cmp(job2.out[:n192].cpu().numpy(), ref, "parallel split Fs=%d Wf=%d offset %.1f" % (seg, warm, offset))
 
 
+@pytest.mark.parametrize("warm", [3, 0])
+def test_parallel_final_rerun_vs_oracle(gpu, oracle_mod, monkeypatch, warm):
+    """a loud tail keeps the true-peak limiter busy across the FINAL flush frame's start,
+    where af_loudnorm re-bases its ring with the limiter's envelope index still set: the
+    walker runs FINAL itself from the true state"""
+    import torch
+    from amx import capi
+    from amx.engine import MasteringJob
+    monkeypatch.setenv("AMX_LN_WARM", str(warm))
+    fs = 48000
+    x = _dynamic_signal(14.0, fs, 23)
+    n = x.shape[0]
+    t = np.arange(n - 4 * fs, n) / fs
+    # loud enough to keep the limiter busy under a +14 dB offset, not so loud that the
+    # quiet start falls below the relative gate (that track would run frame by frame)
+    x[n - 4 * fs:] = (0.25 * np.sin(2 * np.pi * 997.0 * t) * (1.0 + 0.3 * np.sin(2 * np.pi * 3.0 * t)))[:, None]
+    x = np.clip(x, -1.0, 1.0).astype(np.float32)
+    x16 = oracle_mod.quantize(x)
+    st = oracle_mod.loudnorm_measure(x16, fs)
+    job = MasteringJob(fs, 2, {"lufs": -14.0}, [x16.shape[0]], input_s16=True,
+                       chunks=[(0, 0, x16.shape[0])], measure_only=True)
+    job.out[:x16.shape[0]].copy_(torch.from_numpy(x16))
+    job.loudness_pass1(tail=False)
+    job.loudness_pass2(carry=False)
+    job.histograms()
+    job.decide()
+    n192, job2, ws2, summ = job._job192(0, cached=False)
+    d = capi.LoudnormDesc(-14.0, 11.0, -1.5, float(st["input_i"]), float(st["input_lra"]),
+                          float(st["input_tp"]), float(st["input_thresh"]), 14.0)
+    job.loudnorm_192k(0, d, job2, ws2, summ)
+    s = summ.cpu().numpy()
+    ref, _ = oracle_mod.loudnorm(x16, fs, -14.0, measured=st, offset=14.0)
+    print("loud tail Wf=%d: %d segments, %d re-run, FINAL re-run %d" % (warm, s[12], s[10], s[11]))
+    assert s[12] > 0 and s[13] == 0 and s[11] == 1, s
+    _cmp(job2.out[:n192].cpu().numpy(), ref, "loud tail, FINAL re-run, Wf=%d" % warm)
+
+
+def test_graph_step_with_dynamic(gpu, oracle_mod):
+    """capture(dynamic=True): one hipGraph holds the whole step of a two-track batch, one
+    track linear and one that loudnorm sends to dynamic mode; replays give the eager
+    outputs bit for bit, and the dynamic track matches the oracle's pipeline"""
+    import torch
+    from amx import synth
+    from amx.chunking import chunk_bounds
+    from amx.engine import MasteringJob
+    fs = 48000
+    settings = dict(mid_cut=2.0, lufs=-14.0)
+    xa = synth.mix_like(fs * 10, fs, 2, seed=61)
+    xb = _dynamic_signal(11.0, fs, 62)
+    d_in = torch.from_numpy(np.ascontiguousarray(np.concatenate([xa, xb]))).cuda()
+    eager = MasteringJob(fs, 2, settings, [xa.shape[0], xb.shape[0]], quantum=512)
+    eager.run(d_in)
+    rep = eager.fetch_report(raise_dynamic=False)
+    assert rep["modes"] == ["linear", "dynamic"], rep["modes"]
+    eager.finish_dynamic(rep)
+    want = [eager.track_output(t).cpu().numpy() for t in range(2)]
+    job = MasteringJob(fs, 2, settings, [xa.shape[0], xb.shape[0]], quantum=512)
+    job.capture(d_in, dynamic=True)
+    for _ in range(2):
+        job.replay()
+        torch.cuda.synchronize()
+        rep2 = job.fetch_report(raise_dynamic=False)
+        assert rep2["modes"] == ["linear", "dynamic"]
+        assert job.dynamic_output(0) is None
+        y1, info = job.dynamic_output(1)
+        assert info["target_offset"] == eager.dyn_out[1][1]["target_offset"]
+        assert np.array_equal(job.track_output(0).cpu().numpy(), want[0])
+        assert np.array_equal(y1.cpu().numpy(), want[1])
+    ref, rinfo = oracle_mod.pipeline(oracle_mod.quantize(xb), fs, settings, chunk_bounds(xb.shape[0], fs, 512))
+    assert rinfo["mode"] == "dynamic"
+    _cmp(want[1], ref, "graph step, dynamic track")
+
+
 @pytest.mark.timeout(900)
 def test_filter_300s_vs_oracle(gpu, oracle_mod):
     """a 5-minute track (the C2/C3 length) through the parallel form of dynamic mode
