@@ -225,8 +225,14 @@ struct LnArgs {
     double kb[5], ka[5];          // libebur128 K filter at 192 kHz (direct form)
     // set when the parallel form (LpArgs) runs first: this kernel then only runs the
     // tracks it hands over (lp_ctl[0] != 0) with the options it resolved (lp_dctl)
-    const int *lp_ctl;
+    int *lp_ctl;
     const double *lp_dctl;
+    // a quiet start (above_threshold 0) runs here only until the output's short-term
+    // loudness lifts it: at the next segment start the state is handed to the parallel
+    // form (lp_recG[k] holds it, lp_D the deltas written so far); INNER segment k >= 1
+    // starts at frame 1 + k lp_Fs, k <= lp_J
+    double *lp_D, *lp_recG;
+    int lp_Fs, lp_J;
 };
 // af_loudnorm dynamic mode in parallel form (amx_loudnorm.hip):
 // per-frame statistics and gains from pass 1's hop energies, then the true-peak
@@ -259,7 +265,9 @@ struct LpArgs {
     double *rings;                // [P][AMX_LN_RING][2] per-wave limiter rings
     double *wring;                // [AMX_LN_RING][2] the walker's ring
     int *ctl;                     // [16] 0: 0 parallel, 1 frame by frame (k_ln_dyn), 2 handed over,
-                                  // 3 gated off; 1 re-runs, 2 FINAL re-run, 3 above_threshold
+                                  // 3 gated off, 4 quiet start run by k_ln_dyn up to segment
+                                  // ctl[4], parallel from there; 1 re-runs, 2 FINAL re-run,
+                                  // 3 above_threshold at FIRST, 5 frame of the hand-over
     double *dctl;                 // [8] 0 d0, 1 offset (linear), 2 measured_i, 3 measured_thresh,
                                   // 4 offset (dB)
     int16_t *y;                   // [n][2] output

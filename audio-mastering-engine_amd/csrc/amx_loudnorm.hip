@@ -514,10 +514,12 @@ __device__ double ln_out_energy(const double *ring, int lbi, int nb, double ceil
     return r;
 }
 
-__global__ void __launch_bounds__(LN_NT) k_ln_dyn(LnArgs a0) {
-    // after the parallel form's statistics (k_lp_stats): only the tracks it hands over
-    // (the < 3 s linear fallback, a quiet start), with the options it resolved
-    if (a0.lp_ctl && (a0.lp_ctl[0] == 0 || a0.lp_ctl[0] == 3)) return;
+// phase 0 (after k_lp_stats): the tracks the parallel form does not start -- the < 3 s
+// linear fallback, a quiet start (handed over at the first segment start after
+// above_threshold turns 1, lp_ctl[0] = 4); phase 1 (after k_lp_walk): a whole track the
+// walker handed back (lp_ctl[0] = 2), frame by frame to the end
+__global__ void __launch_bounds__(LN_NT) k_ln_dyn(LnArgs a0, int phase) {
+    if (a0.lp_ctl && a0.lp_ctl[0] != (phase == 0 ? 1 : 2)) return;
     LnArgs a = a0;
     if (a0.lp_dctl) {
         a.offset = a0.lp_dctl[1];
@@ -606,8 +608,10 @@ __global__ void __launch_bounds__(LN_NT) k_ln_dyn(LnArgs a0) {
         for (int i = 0; i < 21; i++) r += delta[((idx + i) < 30) ? (idx + i) : (idx + i - 30)] * a.weights[i];
         return r;
     };
+    int ho_f = -1, ho_k = -1;                            // hand-over frame / segment (quiet start)
     // ---- INNER frames (100 ms)
     while (Pin < n) {
+        const int t_in = (int)((Pin - LN_FIRST) / LN_FR);     // this INNER frame
         const int nb = (int)(n - Pin < LN_FR ? n - Pin : LN_FR);
         const uint64_t t_fill = clock64();
         const double gain = gauss(index + 10 < 30 ? index + 10 : index + 10 - 30);
@@ -675,6 +679,46 @@ __global__ void __launch_bounds__(LN_NT) k_ln_dyn(LnArgs a0) {
         prev_delta = dnew;
         index = index + 1 < 30 ? index + 1 : 0;
         P.stats += clock64() - t_stats;
+        if (a0.lp_D && tid == 0) a0.lp_D[t_in] = dnew;
+        if (phase == 0 && a0.lp_recG && above && ho_f < 0) {
+            // from here the deltas follow r128_in alone: hand over at the next segment
+            // start (frame 1 + k Fs, k <= J) -- after frame ho_f - 1, before ho_f's fill
+            const int phi = t_in + 1;
+            int k = (phi + a0.lp_Fs - 1) / a0.lp_Fs;
+            if (k < 1) k = 1;
+            if (k <= a0.lp_J) {
+                ho_k = k;
+                ho_f = 1 + k * a0.lp_Fs;
+            } else {
+                ho_f = 0;                                      // none left: run to the end
+            }
+        }
+        if (ho_f > 0 && t_in + 1 == ho_f - 1) {
+            // the state at frame ho_f's start, as k_lp_snapshot records it: the limiter
+            // scalars (envelope slot in frames) and the 2048 ring slots from the frame's
+            // first output position (19200 ho_f; INNER slot = position mod the ring)
+            double *rec = a0.lp_recG + (int64_t)ho_k * AMX_LN_REC;
+            if (tid == 0) {
+                rec[0] = S.state;
+                rec[1] = S.env_cnt;
+                rec[2] = S.env_index / 2;
+                rec[3] = S.attack_length;
+                rec[4] = S.gr0;
+                rec[5] = S.gr1;
+                rec[6] = ho_f;
+                rec[7] = 0.0;
+                a0.lp_ctl[0] = 4;
+                a0.lp_ctl[4] = ho_k;
+                a0.lp_ctl[5] = ho_f;
+            }
+            const int s0 = (int)(((int64_t)LN_FR * ho_f) % LN_LIMF);
+            for (int j = tid; j < AMX_LN_WIN; j += LN_NT) {
+                const int sl = s0 + j < LN_LIMF ? s0 + j : s0 + j - LN_LIMF;
+                rec[16 + 2 * j] = ring[2 * sl];
+                rec[17 + 2 * j] = ring[2 * sl + 1];
+            }
+            return;
+        }
     }
     // ---- FINAL frame (flush_frame: the last 3 s less one frame, re-read)
     {
@@ -876,13 +920,16 @@ __global__ void __launch_bounds__(LP_STAT_NT) k_lp_stats(LpArgs a) {
 // the delta each INNER frame writes: its value, or (held) the previous frame's; the
 // FIRST frame's d0 before any value.  One workgroup: last-valid index scan.
 __global__ void __launch_bounds__(1024) k_lp_dscan(LpArgs a) {
-    if (a.ctl[0]) return;
+    if (a.ctl[0] != 0 && a.ctl[0] != 4) return;
     __shared__ int s[1024];
     const int tid = threadIdx.x, T = a.T;
+    // a quiet start: k_ln_dyn wrote the deltas of the INNER frames before the hand-over
+    // frame; they stand (a fixed value each)
+    const int t0 = a.ctl[0] == 4 ? a.ctl[5] - 1 : 0;
     const int per = (T + 1023) / 1024, lo = tid * per, hi = min(T, lo + per);
     int last = -1;
     for (int t = lo; t < hi; t++)
-        if (!a.hold[t]) last = t;
+        if (t < t0 || !a.hold[t]) last = t;
     s[tid] = last;
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {
@@ -894,8 +941,12 @@ __global__ void __launch_bounds__(1024) k_lp_dscan(LpArgs a) {
     int cur = tid > 0 ? s[tid - 1] : -1;
     const double d0 = a.dctl[0];
     for (int t = lo; t < hi; t++) {
+        if (t < t0) {
+            cur = t;
+            continue;
+        }
         if (!a.hold[t]) cur = t;
-        a.D[t] = cur >= 0 ? a.v[cur] : d0;
+        a.D[t] = cur < 0 ? d0 : (cur < t0 ? a.D[cur] : a.v[cur]);
     }
 }
 
@@ -905,7 +956,7 @@ __global__ void __launch_bounds__(1024) k_lp_dscan(LpArgs a) {
 __global__ void __launch_bounds__(256) k_lp_gains(LpArgs a) {
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
     for (int64_t i = g; i < LP_FR; i += (int64_t)gridDim.x * 256) a.ramp[i] = (double)i / (double)LP_FR;
-    if (a.ctl[0] || g > a.T) return;
+    if ((a.ctl[0] != 0 && a.ctl[0] != 4) || g > a.T) return;
     const int t = (int)g;
     const double d0 = a.dctl[0];
     double r = 0.;
@@ -1366,24 +1417,38 @@ __device__ __forceinline__ void lp_wave_init(const LpArgs &a, LpWave &W, double2
 
 // every segment at once (persistent waves): from rest Wf frames before its start
 __global__ void __launch_bounds__(64) k_lp_seg(LpArgs a) {
-    if (a.ctl[0]) return;
+    if (a.ctl[0] != 0 && a.ctl[0] != 4) return;
+    const int kh = a.ctl[0] == 4 ? a.ctl[4] : 0;     // a quiet start: k_ln_dyn ran segments < kh
     __shared__ unsigned flags[LP_FW];
     __shared__ double st[160];
     LpWave W;
     lp_wave_init(a, W, reinterpret_cast<double2 *>(a.rings) + (int64_t)blockIdx.x * LP_RS, flags, st);
     const int NF = a.T + 1 + LP_NFIN;
     for (int k = blockIdx.x; k < a.K; k += gridDim.x) {
+        if (k < kh) continue;
         const int ak = lp_seg_start(a, k), bk = k + 1 < a.K ? lp_seg_start(a, k + 1) : NF;
-        const int w = ak - a.Wf > 0 ? ak - a.Wf : 0;
-        lp_rest(W);
-        for (int phi = w; phi < bk; phi++) {
-            W.f = lp_frame(a, phi);
-            lp_refill(a, W, phi);
-            if (phi == ak) {
-                lp_snapshot(a, W, a.recG + (int64_t)k * LP_REC);
-                if (k > 0) lp_arrive(a, k);
+        if (k == kh && kh > 0) {
+            // the hand-over segment starts from k_ln_dyn's true state (recG[kh])
+            lp_restore(a, W, a.recG + (int64_t)k * LP_REC, ak);
+            for (int phi = ak; phi < bk; phi++) {
+                if (phi > ak) {
+                    W.f = lp_frame(a, phi);
+                    lp_refill(a, W, phi);
+                }
+                lp_call(a, W, true);
             }
-            lp_call(a, W, phi >= ak);
+        } else {
+            const int w = ak - a.Wf > 0 ? ak - a.Wf : 0;
+            lp_rest(W);
+            for (int phi = w; phi < bk; phi++) {
+                W.f = lp_frame(a, phi);
+                lp_refill(a, W, phi);
+                if (phi == ak) {
+                    lp_snapshot(a, W, a.recG + (int64_t)k * LP_REC);
+                    if (k > kh) lp_arrive(a, k);
+                }
+                lp_call(a, W, phi >= ak);
+            }
         }
         if (k + 1 < a.K) {
             W.f = lp_frame(a, bk);
@@ -1400,17 +1465,18 @@ __global__ void __launch_bounds__(64) k_lp_seg(LpArgs a) {
 // with a multiplied slot outside its window (never expected) hands the whole track
 // to k_ln_dyn (ctl[0] = 2).
 __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
-    if (a.ctl[0]) return;
+    if (a.ctl[0] != 0 && a.ctl[0] != 4) return;
+    const int kh = a.ctl[0] == 4 ? a.ctl[4] : 0;
     __shared__ unsigned flags[LP_FW];
     __shared__ double st[160];
     LpWave W;
     lp_wave_init(a, W, reinterpret_cast<double2 *>(a.wring), flags, st);
     const int lane = threadIdx.x;
     const int NF = a.T + 1 + LP_NFIN, kS0 = a.J + 1;
-    const double *cur = a.recE;
+    const double *cur = a.recE + (int64_t)kh * LP_REC;
     bool k4 = true;
     int toggle = 0, reruns = 0, fin = 0, fallback = 0;
-    int k = 1;
+    int k = kh + 1;
     while (k < a.K) {
         if (k4) {
             while (k < a.K) {
@@ -1482,6 +1548,7 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
         a.summary[11] = (double)fin;
         a.summary[12] = (double)a.K;
         a.summary[13] = (double)fallback;
+        a.summary[14] = a.ctl[0] == 4 ? (double)a.ctl[5] : 0.0;    // quiet start: hand-over frame
     }
 }
 
@@ -1491,6 +1558,7 @@ hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x
     hipLaunchKernelGGL(k_ln_upsample, dim3((unsigned)((ln.n192 + AMX_BLOCK - 1) / AMX_BLOCK)), dim3(AMX_BLOCK),
                        0, st, x, n_in, L, M, bank, ln.n192, ln.u, lp.gate);
     hipLaunchKernelGGL(k_lp_stats, dim3(1 + (lp.T + LP_STAT_F - 1) / LP_STAT_F), dim3(LP_STAT_NT), 0, st, lp);
+    hipLaunchKernelGGL(k_ln_dyn, dim3(1), dim3(LN_NT), 0, st, ln, 0);
     hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
     const int gb = max((lp.T + 1 + 255) / 256, (LP_FR + 255) / 256);
     hipLaunchKernelGGL(k_lp_gains, dim3(gb), dim3(256), 0, st, lp);
@@ -1500,7 +1568,7 @@ hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lp_seg, dim3(lp.P), dim3(64), 0, st, lp);
     hipLaunchKernelGGL(k_lp_walk, dim3(1), dim3(64), 0, st, lp);
-    hipLaunchKernelGGL(k_ln_dyn, dim3(1), dim3(LN_NT), 0, st, ln);
+    hipLaunchKernelGGL(k_ln_dyn, dim3(1), dim3(LN_NT), 0, st, ln, 1);
     return hipGetLastError();
 }
 

@@ -1402,6 +1402,10 @@ int amx_loudnorm_192k_ex(amx_plan *p, int32_t track, const amx_loudnorm_desc *d,
     q.summary = d_summary;
     a.lp_ctl = q.ctl;
     a.lp_dctl = q.dctl;
+    a.lp_D = q.D;
+    a.lp_recG = q.recG;
+    a.lp_Fs = q.Fs;
+    a.lp_J = q.J;
     HIPCHK(amx::launch_loudnorm(a, q, reinterpret_cast<const uint32_t *>(d_out) + sp.out_off, sp.out_n, p->upL,
                                 p->upM, p->d_bank, (hipStream_t)stream));
     return AMX_OK;

@@ -109,6 +109,42 @@ def test_parallel_splits_vs_oracle(gpu, oracle_mod, monkeypatch, seg, warm):
         _cmp(job2.out[:n192].cpu().numpy(), ref, "parallel split Fs=%d Wf=%d offset %.1f" % (seg, warm, offset))
 
 
+@pytest.mark.parametrize("seg,warm,intro", [(4, 3, 6.0), (1, 0, 6.0), (4, 3, 12.5)])
+def test_quiet_start_handover_vs_oracle(gpu, oracle_mod, monkeypatch, seg, warm, intro):
+    """a quiet intro (the first 3 s below measured_thresh: above_threshold 0, so the
+    output's own short-term loudness steers the gains) runs frame by frame in k_ln_dyn
+    until the output reaches the target, then the state is handed to the parallel form at
+    the next segment start (summary[14] = that frame); the whole output stays the
+    oracle's"""
+    import torch
+    from amx import capi
+    from amx.engine import MasteringJob
+    monkeypatch.setenv("AMX_LN_SEG", str(seg))
+    monkeypatch.setenv("AMX_LN_WARM", str(warm))
+    fs = 48000
+    x = _dynamic_signal(40.0, fs, 29, intro=intro)
+    x16 = oracle_mod.quantize(x)
+    st = oracle_mod.loudnorm_measure(x16, fs)
+    job = MasteringJob(fs, 2, {"lufs": -14.0}, [x16.shape[0]], input_s16=True,
+                       chunks=[(0, 0, x16.shape[0])], measure_only=True)
+    job.out[:x16.shape[0]].copy_(torch.from_numpy(x16))
+    job.loudness_pass1(tail=False)
+    job.loudness_pass2(carry=False)
+    job.histograms()
+    job.decide()
+    n192, job2, ws2, summ = job._job192(0, cached=False)
+    for offset in (8.0, 14.0):
+        d = capi.LoudnormDesc(-14.0, 11.0, -1.5, float(st["input_i"]), float(st["input_lra"]),
+                              float(st["input_tp"]), float(st["input_thresh"]), offset)
+        job.loudnorm_192k(0, d, job2, ws2, summ)
+        s = summ.cpu().numpy()
+        ref, _ = oracle_mod.loudnorm(x16, fs, -14.0, measured=st, offset=offset)
+        print("quiet start %.1f s, Fs=%d Wf=%d offset %.1f: hand-over at frame %d, %d segments, %d re-run" %
+              (intro, seg, warm, offset, s[14], s[12], s[10]))
+        assert s[12] > 0 and s[13] == 0 and s[14] > 0, s
+        _cmp(job2.out[:n192].cpu().numpy(), ref, "quiet start %.1f s Fs=%d Wf=%d offset %.1f" % (intro, seg, warm, offset))
+
+
 @pytest.mark.parametrize("warm", [3, 0])
 def test_parallel_final_rerun_vs_oracle(gpu, oracle_mod, monkeypatch, warm):
     """a loud tail keeps the true-peak limiter busy across the FINAL flush frame's start,
