@@ -360,7 +360,10 @@ __device__ double env_rerun_wave(const ChainDev &cd, const uint16_t *m, const do
 
 typedef uint32_t u2v __attribute__((ext_vector_type(2)));
 
-// m of one staged piece (4 frames: r in the 4 u16 of v)
+// m of one staged piece (4 frames: r in the 4 u16 of v).  No clamp: an index is a u16
+// (<= 65535) and a band's three tables (m, m/A, m/R: 3 x 32769 entries) lie behind mt,
+// so every index reads in bounds; indices above 32768 occur only in rows k_rms did not
+// write (padding before a chunk, past a segment), whose tiles k_env0 skips
 __device__ __forceinline__ void env_gather(const double *__restrict__ mt, const u2v (&I)[4],
                                            double (&G)[16]) {
 #pragma unroll
@@ -368,45 +371,91 @@ __device__ __forceinline__ void env_gather(const double *__restrict__ mt, const 
 #pragma unroll
         for (int e = 0; e < 4; e++) {
             const uint32_t r = (I[i][e >> 1] >> (16 * (e & 1))) & 0xffffu;
-            G[4 * i + e] = m_of(mt, r);
+            G[4 * i + e] = mt[r];
         }
     }
 }
 
-template <bool RCP>
-__device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, double (&G)[16],
+// v_min_f64 without the operand canonicalisation the compiler adds for fmin (IEEE
+// mode quiets signalling NaNs; m is a table value, never a NaN): the instruction fmin
+// compiles to, one fp64 operation per frame fewer
+__device__ __forceinline__ double min_f64_raw(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// env_step3 with that min (k_env0's speculation)
+__device__ __forceinline__ double env_step3_raw(double att, double m, double inc, double dec) {
+    const double up = min_f64_raw(att + inc, m);
+    const double dn = fmax(att - dec, 0.0);
+    return att <= m ? up : dn;
+}
+
+// the wave's 64 rows of a tile are quiet -- every r below rq, the first table index with
+// m != 0 -- so every m is 0 and every lane's state is held through the tile
+typedef unsigned short us2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bool env_tile_quiet(const u2v (&I)[4], uint32_t rq) {
+    us2v a = __builtin_bit_cast(us2v, I[0][0]);
+    a = __builtin_elementwise_max(a, __builtin_bit_cast(us2v, I[0][1]));
+#pragma unroll
+    for (int i = 1; i < 4; i++) {
+        a = __builtin_elementwise_max(a, __builtin_bit_cast(us2v, I[i][0]));
+        a = __builtin_elementwise_max(a, __builtin_bit_cast(us2v, I[i][1]));
+    }
+    const uint32_t mx = a.x > a.y ? a.x : a.y;
+    return __ballot(mx >= rq) == 0ull;
+}
+
+// QS: quiet tiles (env_tile_quiet, wave-uniform) skip their gathers, staging and steps;
+// qf carries the flag of the tile whose m sits in G (tile q on entry, q + 2 on exit)
+template <bool RCP, bool QS>
+__device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, double (&G)[16], bool &qf,
                                           u2v (&Islot)[4], const u2v (&Inext)[4],
-                                          const uint16_t *const (&irow)[4], const double *mt, int q,
+                                          const uint16_t *const (&irow)[4], const double *mt,
+                                          uint32_t rq, int q,
                                           int ntile, int nwarm, int64_t start, int64_t end,
                                           double *ckr, double &att, double &s_spec, bool &any) {
     const int lane = threadIdx.x & 63;
+    const bool quiet = QS && qf;
     // stage tile q's m (gathered two tiles ago)
+    if (!quiet) {
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        double *d = sm + ((lane >> 2) + 16 * i) * AMX_ENV_MP + 4 * (lane & 3);
-        *reinterpret_cast<d2v *>(d) = d2v{G[4 * i], G[4 * i + 1]};
-        *reinterpret_cast<d2v *>(d + 2) = d2v{G[4 * i + 2], G[4 * i + 3]};
+        for (int i = 0; i < 4; i++) {
+            double *d = sm + ((lane >> 2) + 16 * i) * AMX_ENV_MP + 4 * (lane & 3);
+            *reinterpret_cast<d2v *>(d) = d2v{G[4 * i], G[4 * i + 1]};
+            *reinterpret_cast<d2v *>(d + 2) = d2v{G[4 * i + 2], G[4 * i + 3]};
+        }
     }
     __builtin_amdgcn_wave_barrier();
     {
         // this ring slot (tile q's r, gathered already) takes tile q + PF (past the
         // end: re-read, unused); then the gathers of tile q + 2
         const int qn = (q + AMX_ENV_PF < ntile ? q + AMX_ENV_PF : q) * AMX_ENV_TF;
+        bool qn2 = false;
+        if constexpr (QS) qn2 = env_tile_quiet(Inext, rq);
+        qf = qn2;
 #pragma unroll
         for (int i = 0; i < 4; i++) Islot[i] = *reinterpret_cast<const u2v *>(irow[i] + qn);
-        env_gather(mt, Inext, G);
+        if (!qn2) env_gather(mt, Inext, G);
     }
     const int64_t f0 = start + (int64_t)q * AMX_ENV_TF;
     const bool in = f0 >= 0 && f0 < end;           // whole tile in (else held)
     double mv[AMX_ENV_TF];
+    if (!quiet) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const d2v v = *reinterpret_cast<const d2v *>(sm + lane * AMX_ENV_MP + 2 * i);
-        mv[2 * i] = v.x;
-        mv[2 * i + 1] = v.y;
+        for (int i = 0; i < 8; i++) {
+            const d2v v = *reinterpret_cast<const d2v *>(sm + lane * AMX_ENV_MP + 2 * i);
+            mv[2 * i] = v.x;
+            mv[2 * i + 1] = v.y;
+        }
     }
     __builtin_amdgcn_wave_barrier();
     if (q == nwarm) s_spec = att;
+    if (quiet) {
+        if (in && q >= nwarm) ckr[f0 / AMX_ENV_TF] = att;
+        return;
+    }
     // a tile outside the chunk / segment holds the state: it is skipped rather than
     // fed zeros (the same state; no per-frame selects on the common path)
     if (in) {
@@ -414,20 +463,27 @@ __device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, double
         // the state is held there without masking, k_rms)
         if (q >= nwarm) {
             ckr[f0 / AMX_ENV_TF] = att;
+            // any m != 0 in the tile: the OR of the 16 values' bits, sign masked (-0.0 is
+            // a zero m); integer ORs instead of a fp64 compare per frame
+            uint32_t h = 0, l = 0;
 #pragma unroll
-            for (int f = 0; f < AMX_ENV_TF; f++) any |= mv[f] != 0.0;
+            for (int f = 0; f < AMX_ENV_TF; f++) {
+                const unsigned long long x = (unsigned long long)__double_as_longlong(mv[f]);
+                h |= (uint32_t)(x >> 32);
+                l |= (uint32_t)x;
+            }
+            any |= ((h & 0x7fffffffu) | l) != 0u;
         }
         double iv[AMX_ENV_TF], dv[AMX_ENV_TF];
 #pragma unroll
         for (int f = 0; f < AMX_ENV_TF; f++) {
             iv[f] = env_div<RCP>(mv[f], cd.env_A, cd.env_rA);
             dv[f] = env_div<RCP>(mv[f], cd.env_R, cd.env_rR);
-            mv[f] = __builtin_canonicalize(mv[f]);      // fmin's operand, once per frame here
         }
         // (no scheduling barrier: the scheduler may start the recurrence while later
         // quotients are still being formed; measured 206 -> 201 us at C3)
 #pragma unroll
-        for (int f = 0; f < AMX_ENV_TF; f++) att = env_step3(att, mv[f], iv[f], dv[f]);
+        for (int f = 0; f < AMX_ENV_TF; f++) att = env_step3_raw(att, mv[f], iv[f], dv[f]);
     }
 }
 
@@ -436,9 +492,12 @@ __device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, double
 // workgroups than CUs.  The staging (gathers, LDS) is the CU's shared path, so a step
 // costs about W times the single-wave cost; the plan picks Le so that all segments fit
 // one resident wave set, which also shrinks the warm-up share (W + Le) / Le.
+// IL (band-interleaved, W = 3): wave w of a workgroup runs band w of the same 64
+// segments, so a CU holds one wave per band; quiet tiles (QS) are skipped, and a band
+// below its threshold leaves its SIMD -- and the CU's gather path -- to the other two.
 #define AMX_ENV_WG 4
 #define AMX_ENV_LDS_PIN (48 * 1024)      // + 36 KB static: > 80 KB, one workgroup per CU
-template <bool RCP>
+template <bool RCP, bool IL>
 __global__ void __launch_bounds__(64 * AMX_ENV_WG) k_env0(const ChainDev *__restrict__ cdp,
                                              const ChunkDev *__restrict__ chunks,
                                              const SegDev *__restrict__ es, int n_es,
@@ -450,14 +509,15 @@ __global__ void __launch_bounds__(64 * AMX_ENV_WG) k_env0(const ChainDev *__rest
                                              int Le, int *__restrict__ flags) {
     __shared__ __attribute__((aligned(16))) double sm_all[AMX_ENV_WG][64 * AMX_ENV_MP];
     const ChainDev &cd = *cdp;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // (the wave index as a scalar: the band's table base stays an SGPR pair under IL)
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double *sm = sm_all[wv];
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < AMX_ENV_MAX_ROUNDS) flags[threadIdx.x] = 0;
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) {
         for (int k = lane; k < AMX_ENV_MAX_ROUNDS * AMX_ENV_NCTR; k += 64) flags[AMX_ENV_MAX_ROUNDS + k] = 0;
     }
-    const int j = (blockIdx.x * (blockDim.x >> 6) + wv) * 64 + lane;
-    const int b = blockIdx.y;
+    const int j = IL ? blockIdx.x * 64 + lane : (blockIdx.x * (blockDim.x >> 6) + wv) * 64 + lane;
+    const int b = IL ? wv : blockIdx.y;
     const bool valid = j < n_es;
     const SegDev sg = es[valid ? j : n_es - 1];
     const ChunkDev ch = chunks[sg.chunk];
@@ -479,15 +539,26 @@ __global__ void __launch_bounds__(64 * AMX_ENV_WG) k_env0(const ChainDev *__rest
 #pragma unroll
         for (int i = 0; i < 4; i++) I[u][i] = *reinterpret_cast<const u2v *>(irow[i] + u * AMX_ENV_TF);
     double G[2][16];
-    env_gather(mt, I[0], G[0]);
-    env_gather(mt, I[1], G[1]);
+    const uint32_t rq = (uint32_t)cd.rq[b];
+    bool qf[2] = {false, false};
+    if constexpr (IL) {
+        qf[0] = env_tile_quiet(I[0], rq);
+        qf[1] = env_tile_quiet(I[1], rq);
+    }
+    if (!qf[0]) env_gather(mt, I[0], G[0]);
+    if (!qf[1]) env_gather(mt, I[1], G[1]);
+    // the warm-up's start guess: a chunk's first frames start from 0 (exact: the
+    // reference starts every chunk there); elsewhere m of the warm-up's first frame --
+    // inside a compressed stretch the state sits at or near m, and trajectories meet
+    // sooner from there than from 0 (scripts/env_warm_sim.py)
     double att = 0.0, s_spec = 0.0;
+    if (cd.env_guess && start >= 0) att = mt[mi[rowoff + start]];
     bool any = false;
     for (int q0 = 0; q0 < ntile; q0 += AMX_ENV_PF) {
 #pragma unroll
         for (int u = 0; u < AMX_ENV_PF; u++)
-            env0_tile<RCP>(cd, sm, G[u & 1], I[u], I[(u + 2) % AMX_ENV_PF], irow, mt, q0 + u, ntile,
-                           nwarm, start, end, ckr, att, s_spec, any);
+            env0_tile<RCP, IL>(cd, sm, G[u & 1], qf[u & 1], I[u], I[(u + 2) % AMX_ENV_PF], irow, mt, rq,
+                               q0 + u, ntile, nwarm, start, end, ckr, att, s_spec, any);
     }
     if (valid) {
         sv[(int64_t)b * n_es + j] = s_spec;
@@ -865,8 +936,14 @@ static void env_launch_t(const DynLaunch &d, const uint16_t *m, double *ck, doub
     const dim3 gw((unsigned)((d.n_es + 63) / 64), 3);
     if (part == 0) {
         const int wg = d.env_wg >= 1 && d.env_wg <= AMX_ENV_WG ? d.env_wg : 1;
+        if (d.env_il) {     // band-interleaved: one wave per band of 64 segments
+            const dim3 g0((unsigned)((d.n_es + 63) / 64), 1);
+            hipLaunchKernelGGL((k_env0<RCP, true>), g0, dim3(192), d.env_pin ? AMX_ENV_LDS_PIN : 0, d.st, d.cd,
+                               d.chunks, d.es, d.n_es, m, d.tabs, ck, sv, ev, act, d.nloc, d.warm, d.Le, flags);
+            return;
+        }
         const dim3 g0((unsigned)((d.n_es + 64 * wg - 1) / (64 * wg)), 3);
-        hipLaunchKernelGGL(k_env0<RCP>, g0, dim3(64 * wg), d.env_pin ? AMX_ENV_LDS_PIN : 0, d.st, d.cd,
+        hipLaunchKernelGGL((k_env0<RCP, false>), g0, dim3(64 * wg), d.env_pin ? AMX_ENV_LDS_PIN : 0, d.st, d.cd,
                            d.chunks, d.es, d.n_es, m, d.tabs, ck, sv, ev, act, d.nloc, d.warm, d.Le, flags);
         return;
     }

@@ -59,6 +59,8 @@ struct ChainDev {
     // compressor (pydub compress_dynamic_range, :306-308)
     int32_t look;          // int(5 ms * fs)
     int32_t rthr[3];       // smallest integer rms with rms > thresh_rms
+    int32_t rq[3];         // first table index r with m(r) != 0 (32769: none); r < rq is quiet
+    int32_t pad_rq_;
     double kw1[6], kw2[6]; // K-weighting as two DF-II-T biquads (libebur128 pb/pa, rb/ra)
     // Active EQ stages packed in order for register-resident use (amx_dev.hpp eq_chain):
     //   shelf: b0 b1 b2 a1 a2 gx     (gx = g-1, or the negative-gain factor g / f32(g))
@@ -68,7 +70,10 @@ struct ChainDev {
     // when the reciprocal-multiply with one FMA correction was checked on the host to
     // equal the IEEE quotient for every table value m (amx_dyn.hip env_div)
     double env_A, env_R, env_rA, env_rR;
-    int32_t env_rcp, pad1_;
+    int32_t env_rcp;
+    // k_env0's warm-up start guess: 1 = m of the warm-up's first frame, 0 = att = 0
+    // 
+    int32_t env_guess;
     // exp10 constants of the gain (amx_dyn.hip exp10_gain): read through the plan so
     // they are scalar operands of the FMAs (a 64-bit literal is not encodable)
     double exc[16];
@@ -159,6 +164,7 @@ struct DynLaunch {
     const double *tabs;
     hipStream_t st;
     int env_wg, env_pin;         // k_env0: waves per workgroup, one workgroup per CU
+    int env_il;                  // k_env0: band-interleaved workgroups (3 waves, one per band)
 };
 hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m);
 // input decode: PCM of any supported format -> stereo s16 frames (amx_io.hip)

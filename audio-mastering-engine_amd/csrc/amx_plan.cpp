@@ -237,7 +237,7 @@ struct amx_plan {
     int lev_eq = 0, lev_x = 0, lev_kw = 0;
     int mb = 0;
     int Le = 1024, warm = 2304, rounds = 2;   // compressor envelope segments (amx_dyn.hip)
-    int env_wg = 1, env_pin = 0;              // k_env0 placement (amx_dyn.hip launch_env)
+    int env_wg = 1, env_pin = 0, env_il = 0;  // k_env0 placement (amx_dyn.hip launch_env)
     int n_es = 0;
     std::vector<SegDev> esegs;
     std::vector<int> eseg0, neseg;
@@ -560,6 +560,9 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
                 mt[32769 + r] = m / A;
                 mt[2 * 32769 + r] = m / R;
             }
+            int rq = 0;
+            while (rq <= 32768 && mt[rq] == 0.0) rq++;
+            cd.rq[b] = rq;
         }
         // the device forms m / A as q = m (1/A), q + (m - q A) (1/A) (two FMAs, exact
         // to the IEEE quotient by Markstein's theorem for a correctly rounded 1/A);
@@ -577,6 +580,8 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         cd.env_R = R;
         cd.env_rA = 1.0 / A;
         cd.env_rR = 1.0 / R;
+        cd.env_guess = 1;                                   // (measurements: AMX_ENV_GUESS=0)
+        if (const char *ev = std::getenv("AMX_ENV_GUESS")) cd.env_guess = std::atoi(ev) != 0;
         cd.env_rcp = 1;
         for (size_t i = 0; i < (size_t)3 * 3 * 32769 && cd.env_rcp; i += 1) {
             if (i % (3 * 32769) >= 32769) continue;
@@ -609,18 +614,23 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         // (AMX_ENV_WG = 0 is the single-wave-workgroup launch)
         int wg = 2;
         if (const char *ev = std::getenv("AMX_ENV_WG")) wg = std::atoi(ev);
+        int64_t le_min = 1024;                                   // (measurements: AMX_ENV_LEMIN)
+        if (const char *ev = std::getenv("AMX_ENV_LEMIN")) le_min = std::max(128, std::atoi(ev)) / 128 * 128;
+        if (const char *ev = std::getenv("AMX_ENV_IL")) p->env_il = std::atoi(ev) != 0;
         if (wg > 0) {
-            p->env_wg = std::min(wg, 4);
+            p->env_wg = p->env_il ? 3 : std::min(wg, 4);
             p->env_pin = 1;
             if (!env_le) {
                 int dev = 0, ncu = 0;
                 if (hipGetDevice(&dev) != hipSuccess ||
                     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 3)
                     ncu = 256;
-                const int64_t fit = (int64_t)(ncu / 3) * 64 * p->env_wg;   // segments per band
+                // segments per band: W waves of one band per CU, or (W = 3, band-interleaved)
+                // one wave per band of the same 64 segments per CU
+                const int64_t fit = p->env_il ? (int64_t)ncu * 64 : (int64_t)(ncu / 3) * 64 * p->env_wg;
                 int64_t total = 0;
                 for (int c = 0; c < n_chunks; c++) total += chunks[c].frames;
-                int64_t Le = std::max<int64_t>(1024, (total / fit + 127) / 128 * 128);
+                int64_t Le = std::max<int64_t>(le_min, (total / fit + 127) / 128 * 128);
                 for (;; Le += 128) {
                     int64_t ne = 0;
                     for (int c = 0; c < n_chunks; c++) ne += (chunks[c].frames + Le - 1) / Le;
@@ -1097,7 +1107,7 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     amx::DynLaunch dl{p->d_cd,    p->d_chunks, p->n_chunks, p->d_esegs, p->n_es,
                       p->d_eseg0, p->d_neseg,  p->nloc,     p->max_chunk_n, p->cd.look,
                       p->warm,    p->Le,       p->cd.env_rcp, p->d_tabs, st,
-                      p->env_wg,  p->env_pin};
+                      p->env_wg,  p->env_pin,  p->env_il};
     switch (stage) {
     case AMX_STAGE_FRONT1:
         if (p->mono16) {
