@@ -62,6 +62,15 @@ WORKLOAD = {
           "settings, whole tracks sharded over the ranks (no exchange)",
     "c5": "configs[4]: 60 min stereo 96 kHz f32 per GPU, C3 settings, hipGraph-captured step",
 }
+# --strong: the total work is fixed, one track split over the N ranks (configs[4] as stated)
+WORKLOAD_STRONG = {
+    "c5": "configs[4]: ONE 60 min stereo 96 kHz f32 track, C3 settings, chunk-sharded over the N "
+          "GPUs (strong scaling: the same track at every N)",
+    "c3": "configs[2] settings: ONE 5 min stereo 48 kHz f32 track chunk-sharded over the N GPUs "
+          "(strong scaling)",
+    "c2": "configs[1] settings: ONE 5 min stereo 48 kHz f32 track chunk-sharded over the N GPUs "
+          "(strong scaling)",
+}
 # the reference's own Python chain, 1 core (measured in the survey container):
 # context for the C oracle's rate, which is ~50-90x faster than the reference
 REF_PY = {"c2": (20.9, "EQ only (the C2 chain's scipy part; ffmpeg stages not measurable)"),
@@ -400,7 +409,8 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (amx.synth.mix_like, seeded per rank / track)",
-        "config": {"workload": WORKLOAD[args.config], "sample_rate": fs,
+        "config": {"workload": (WORKLOAD_STRONG.get(args.config, WORKLOAD[args.config]) if args.strong
+                                else WORKLOAD[args.config]), "sample_rate": fs,
                    "settings": args.config, "seconds_per_track": args.seconds,
                    "tracks_per_gpu": len(runner.tracks) if batch else 1,
                    "seg_frames": args.seg_frames,
