@@ -15,6 +15,8 @@
 
 namespace amx {
 
+#define AMX_HALF_LUT 32769   // entries of the odd tanh table's half (tanh(s) = sign(s) half[|s|])
+
 __device__ __forceinline__ void decode_in(const ChainDev &cd, const uint32_t *row, int f,
                                           int win, int16_t &l, int16_t &r) {
     if (win == 2) {
@@ -291,7 +293,6 @@ __global__ void __launch_bounds__(AMX_BLOCK, 4) k_front1s(const ChainDev *__rest
 // (128 KB) fits the 160 KB LDS beside the tile buffers: one workgroup per CU, persistent
 // over the segment blocks, loads the half table once; a lookup is an LDS read instead of
 // a gather from the 256 KB global table through the texture path.
-#define AMX_HALF_LUT 32769
 template <int D>
 __global__ void __launch_bounds__(AMX_BLOCK, 1) k_front1h(const ChainDev *__restrict__ cdp,
                                                           const ChunkDev *__restrict__ chunks,
@@ -346,6 +347,216 @@ __global__ void __launch_bounds__(AMX_BLOCK, 1) k_front1h(const ChainDev *__rest
         else
             front1s_run<D, true, false, true>(cd, s_tab, ip, ilen, op, c4, rg, s_in, s_out, row, half, L,
                                               len, G, sG, eo);
+    }
+}
+
+// ----------------------------------- analog character as its own elementwise pass
+// Float32 stereo input with the analog stage (:258-266): quantise (A.1), the tanh
+// table, the two channel-axis shelves -> the chain's s16 input a16.  Every frame is
+// independent (the shelves filter along the channel axis), so a thread takes 4 frames of
+// one chunk (two 16-B loads, one 16-B store) and the launch has a wave per 256 frames:
+// thousands of waves in flight hide the table gathers that stalled the segment kernel,
+// which did this work on 2 waves per 64 segments beside its GEMV.  The EQ GEMV then runs
+// over a16 (k_gemv16).
+__global__ void __launch_bounds__(AMX_BLOCK) k_analog(const ChainDev *__restrict__ cdp,
+                                                      const ChunkDev *__restrict__ chunks,
+                                                      const float *__restrict__ in,
+                                                      const float *__restrict__ lut,
+                                                      uint32_t *__restrict__ a16) {
+    const ChainDev &cd = *cdp;
+    const ChunkDev ch = chunks[blockIdx.y];
+    const int64_t f = ((int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x) * 4;
+    if (f >= ch.n) return;
+    const float *src = in + (ch.in_off + f) * 2;
+    uint32_t *dst = a16 + ch.loc_off + f;
+    const bool full = f + 4 <= ch.n;
+    float x[8];
+    if (full && (ch.in_off & 1) == 0) {
+        const float4 u0 = *reinterpret_cast<const float4 *>(src);
+        const float4 u1 = *reinterpret_cast<const float4 *>(src + 4);
+        x[0] = u0.x; x[1] = u0.y; x[2] = u0.z; x[3] = u0.w;
+        x[4] = u1.x; x[5] = u1.y; x[6] = u1.z; x[7] = u1.w;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; e++) x[e] = f + e / 2 < ch.n ? src[e] : 0.0f;
+    }
+    float t[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) t[e] = lut[(int)q_f32_to_s16_ffmpeg(x[e]) + 32768];
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int16_t l, r;
+        analog_shelves(cd, t[2 * i], t[2 * i + 1], l, r);
+        o[i] = pack2(l, r);
+    }
+    if (full && (ch.loc_off & 3) == 0) {
+        *reinterpret_cast<uint4 *>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if (f + i < ch.n) dst[i] = o[i];
+    }
+}
+
+// k_analog with the tanh table in LDS (measured: the global-table form is bound by the
+// L2 -> L1 traffic of its scattered table reads, 105 us at C3).  numpy's float32 tanh
+// table is odd (the plan checks every pair bit for bit), so the 32 769-entry half table
+// (128 KB) sits in the LDS of one 1024-thread workgroup per CU (4 waves per SIMD), loaded
+// once; the workgroups then stride over every chunk's 4-frame groups.
+__device__ __forceinline__ void analog_load8(const float *src, int64_t f, int64_t n, bool vin, float (&x)[8]) {
+    if (f + 4 <= n && vin) {
+        const float4 u0 = *reinterpret_cast<const float4 *>(src);
+        const float4 u1 = *reinterpret_cast<const float4 *>(src + 4);
+        x[0] = u0.x; x[1] = u0.y; x[2] = u0.z; x[3] = u0.w;
+        x[4] = u1.x; x[5] = u1.y; x[6] = u1.z; x[7] = u1.w;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; e++) x[e] = f + e / 2 < n ? src[e] : 0.0f;
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_analog_h(const ChainDev *__restrict__ cdp,
+                                                   const ChunkDev *__restrict__ chunks, int n_chunks,
+                                                   const float *__restrict__ in,
+                                                   const float *__restrict__ lut_half,
+                                                   uint32_t *__restrict__ a16) {
+    __shared__ float s_tab[AMX_HALF_LUT];
+    for (int i = threadIdx.x; i < AMX_HALF_LUT; i += 1024) s_tab[i] = lut_half[i];
+    __syncthreads();
+    const ChainDev &cd = *cdp;
+    const int64_t stride = (int64_t)gridDim.x * 1024 * 4;
+    for (int c = 0; c < n_chunks; c++) {
+        const ChunkDev ch = chunks[c];
+        const bool vin = (ch.in_off & 1) == 0, vout = (ch.loc_off & 3) == 0;
+        int64_t f = ((int64_t)blockIdx.x * 1024 + threadIdx.x) * 4;
+        if (f >= ch.n) continue;
+        auto work = [&](const float (&x)[8], int64_t ff) {
+            float t[8];
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const int q = (int)q_f32_to_s16_ffmpeg(x[e]);
+                const float v = s_tab[q < 0 ? -q : q];
+                t[e] = q < 0 ? -v : v;                 // tanh(s) = sign(s) half[|s|]
+            }
+            uint32_t o[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                int16_t l, r;
+                analog_shelves(cd, t[2 * i], t[2 * i + 1], l, r);
+                o[i] = pack2(l, r);
+            }
+            uint32_t *dst = a16 + ch.loc_off + ff;
+            if (ff + 4 <= ch.n && vout) {
+                *reinterpret_cast<uint4 *>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if (ff + i < ch.n) dst[i] = o[i];
+            }
+        };
+        // two register sets: the next group's input is in flight while one is computed
+        float xa[8], xb[8];
+        analog_load8(in + (ch.in_off + f) * 2, f, ch.n, vin, xa);
+        for (;;) {
+            int64_t fn = f + stride;
+            if (fn < ch.n) analog_load8(in + (ch.in_off + fn) * 2, fn, ch.n, vin, xb);
+            work(xa, f);
+            if (fn >= ch.n) break;
+            f = fn;
+            fn = f + stride;
+            if (fn < ch.n) analog_load8(in + (ch.in_off + fn) * 2, fn, ch.n, vin, xa);
+            work(xb, f);
+            if (fn >= ch.n) break;
+            f = fn;
+        }
+    }
+}
+
+// EQ pass 1 over the s16 stereo chain input a16 (after k_analog): the GEMV of
+// k_front1s without the input conversion -- two threads per segment, each holding both
+// channels' accumulators for half of the D state components, G tiles through LDS.  A
+// row's 16-frame tile is 64 B: lane t loads 16-B piece t % 4 of rows t / 4 + 64 m
+// (chunk rows are 16-frame aligned); frames at or past a row's length load as 0.  The
+// accumulation order is k_front1s's, so e is the same to the bit.
+#define AMX_G16_PITCH (AMX_TF + 4)   // dwords per LDS row (16-B aligned rows)
+template <int D>
+__global__ void __launch_bounds__(AMX_BLOCK, 4) k_gemv16(const ChainDev *__restrict__ cdp,
+                                                         const ChunkDev *__restrict__ chunks,
+                                                         const SegDev *__restrict__ segs,
+                                                         int n_seg, int L,
+                                                         const uint32_t *__restrict__ a16,
+                                                         const double *__restrict__ G,
+                                                         double *__restrict__ e) {
+    constexpr int ROWS = AMX_BLOCK / 2;
+    constexpr int H = D / 2;
+    constexpr int GQ = AMX_TF * D / 2;                  // 16-B pieces of a G tile
+    static_assert(GQ <= AMX_BLOCK && D % 2 == 0 && D > 0, "tile shape");
+    __shared__ __attribute__((aligned(16))) uint32_t s_in[ROWS * AMX_G16_PITCH];
+    __shared__ __attribute__((aligned(16))) double sG[AMX_TF * D];
+    __shared__ int64_t rb[ROWS];
+    __shared__ int rl[ROWS];
+    const int t = threadIdx.x, row = t >> 1, half = t & 1;
+    const int j = blockIdx.x * ROWS + row;
+    const bool valid = j < n_seg;
+    const SegDev sg = segs[valid ? j : n_seg - 1];
+    if (half == 0) {
+        rb[row] = valid ? chunks[sg.chunk].loc_off + sg.pos : 0;
+        rl[row] = valid ? sg.len : 0;
+    }
+    __syncthreads();
+    const int c4 = 4 * (t & 3);
+    const uint32_t *ip[2];
+    int ilen[2];
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+        ip[m] = a16 + rb[(t >> 2) + 64 * m] + c4;
+        ilen[m] = rl[(t >> 2) + 64 * m];
+    }
+    uint4 R[2], RG;
+    auto fetch = [&](int k) {
+        RG = t < GQ ? *reinterpret_cast<const uint4 *>(G + (int64_t)k * D + 2 * t) : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            const int n = k + c4;
+            uint4 v = *reinterpret_cast<const uint4 *>(ip[m] + (n < ilen[m] ? k : 0));
+            v.x = n < ilen[m] ? v.x : 0u;
+            v.y = n + 1 < ilen[m] ? v.y : 0u;
+            v.z = n + 2 < ilen[m] ? v.z : 0u;
+            v.w = n + 3 < ilen[m] ? v.w : 0u;
+            R[m] = v;
+        }
+    };
+    double a0[H], a1[H];
+#pragma unroll
+    for (int d = 0; d < H; d++) { a0[d] = 0.0; a1[d] = 0.0; }
+    fetch(0);
+    const uint32_t *rp = s_in + row * AMX_G16_PITCH;
+    for (int k = 0; k < L; k += AMX_TF) {
+#pragma unroll
+        for (int m = 0; m < 2; m++)
+            *reinterpret_cast<uint4 *>(s_in + ((t >> 2) + 64 * m) * AMX_G16_PITCH + c4) = R[m];
+        if (t < GQ) reinterpret_cast<uint4 *>(sG)[t] = RG;
+        __syncthreads();
+        if (k + AMX_TF < L) fetch(k + AMX_TF);
+#pragma unroll 1
+        for (int f = 0; f < AMX_TF; f++) {
+            const uint32_t w = rp[f];
+            const double x0 = (double)((float)lo16(w) / 32768.0f);
+            const double x1 = (double)((float)hi16(w) / 32768.0f);
+            const double *g = sG + f * D + half * H;
+#pragma unroll
+            for (int d = 0; d < H; d++) {
+                a0[d] = fma(g[d], x0, a0[d]);
+                a1[d] = fma(g[d], x1, a1[d]);
+            }
+        }
+        __syncthreads();
+    }
+    if (valid && !sg.last) {
+        double *eo = e + (int64_t)j * 2 * D + half * H;
+#pragma unroll
+        for (int d = 0; d < H; d++) { eo[d] = a0[d]; eo[D + d] = a1[d]; }
     }
 }
 
@@ -679,7 +890,27 @@ static hipError_t front1s_t(const Launch &l, const uint32_t *in, const float *lu
                             const double *G, double *e) {
     const int rows = AMX_BLOCK / 2;
     if constexpr (AN) {
-        if (l.lut_half) {
+        if (l.f1_mode == AMX_F1_SPLIT) {
+            // analog as an elementwise pass, then the GEMV over its s16 output
+            if (l.lut_half) {
+                const int64_t quads = (l.max_chunk_n + 3) / 4;
+                const int64_t wgs = (quads * (int64_t)l.n_chunks + 1023) / 1024;
+                const dim3 gh((unsigned)(wgs < cu_count() ? (wgs > 0 ? wgs : 1) : cu_count()));
+                hipLaunchKernelGGL(k_analog_h, gh, dim3(1024), 0, l.stream, l.cd, l.chunks, l.n_chunks,
+                                   reinterpret_cast<const float *>(in), l.lut_half, a16);
+            } else {
+                const dim3 ga((unsigned)((l.max_chunk_n + 4 * AMX_BLOCK - 1) / (4 * AMX_BLOCK)),
+                              (unsigned)l.n_chunks);
+                hipLaunchKernelGGL(k_analog, ga, dim3(AMX_BLOCK), 0, l.stream, l.cd, l.chunks,
+                                   reinterpret_cast<const float *>(in), lut, a16);
+            }
+            if constexpr (D > 0) {
+                hipLaunchKernelGGL((k_gemv16<D>), dim3((unsigned)((l.n_seg + rows - 1) / rows)), dim3(AMX_BLOCK), 0,
+                                   l.stream, l.cd, l.chunks, l.segs, l.n_seg, l.L, a16, G, e);
+            }
+            return hipGetLastError();
+        }
+        if (l.f1_mode == AMX_F1_HALF && l.lut_half) {
             const int nblk = (l.n_seg + rows - 1) / rows;
             dim3 grid((unsigned)(nblk < cu_count() ? nblk : cu_count()));
             hipLaunchKernelGGL((k_front1h<D>), grid, dim3(AMX_BLOCK), 0, l.stream, l.cd, l.chunks, l.segs,

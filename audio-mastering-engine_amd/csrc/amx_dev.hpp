@@ -61,25 +61,38 @@ __device__ __forceinline__ double sos_step(const double *c, double &z0, double &
 // lfilter along the channel axis (:264-265) = a length-2 sequence per frame.
 // tanh comes from the plan's 65536-entry table of numpy's float32 tanh over every
 // int16 input (design.py), so the result is the reference's own rounding.
-// the part after the tanh table: t0, t1 = tanh of the left / right sample
+// the part after the tanh table: t0, t1 = tanh of the left / right sample.
+// lfilter's zero initial state makes the reference add 0.0 to the first products
+// (y0 = 0 + b0 x0, (0 + x0 b1), v0, (0 + u0 b2_1)); those adds are left out.  0 + p == p
+// except for p = -0.0, and a zero of either sign meeting + - x with finite operands
+// gives the same nonzero values and zeros of possibly other sign, which the int16
+// conversion maps to the same 0: the outputs are those of the reference's sequence.
+// The clip to [-1, 1] is a raw v_min_f64 / v_max_f64 pair (the values are never NaN:
+// table values through finite coefficients).
+__device__ __forceinline__ double f64_clip1_raw(double x) {
+    double a, b;
+    asm("v_min_f64 %0, %1, 1.0" : "=v"(a) : "v"(x));
+    asm("v_max_f64 %0, %1, -1.0" : "=v"(b) : "v"(a));
+    return b;
+}
 __device__ __forceinline__ void analog_shelves(const ChainDev &cd, float t0, float t1, int16_t &ol,
                                                int16_t &orr) {
     const double x0 = (double)t0;
     const double x1 = (double)t1;
     const double *b1 = cd.an_lo, *b2 = cd.an_hi;
-    // first shelf (120 Hz low, +cf dB): y0 = 0 + b0*x0 ; Z0 = (0 + x0*b1) - y0*a1 ; y1 = Z0 + b0*x1
-    double y0 = 0.0 + b1[0] * x0;
-    double z0 = (0.0 + x0 * b1[1]) - y0 * b1[4];
-    double y1 = z0 + b1[0] * x1;
-    double u0 = x0 + (y0 - x0) * cd.an_glo1;
-    double u1 = x1 + (y1 - x1) * cd.an_glo1;
-    double v0 = 0.0 + b2[0] * u0;
-    double w = (0.0 + u0 * b2[1]) - v0 * b2[4];
-    double v1 = w + b2[0] * u1;
-    double o0 = u0 + (v0 - u0) * cd.an_ghi1;
-    double o1 = u1 + (v1 - u1) * cd.an_ghi1;
-    ol = f64_to_s16(o0);
-    orr = f64_to_s16(o1);
+    // first shelf (120 Hz low, +cf dB): y0 = b0*x0 ; Z0 = x0*b1 - y0*a1 ; y1 = Z0 + b0*x1
+    const double y0 = b1[0] * x0;
+    const double z0 = x0 * b1[1] - y0 * b1[4];
+    const double y1 = z0 + b1[0] * x1;
+    const double u0 = x0 + (y0 - x0) * cd.an_glo1;
+    const double u1 = x1 + (y1 - x1) * cd.an_glo1;
+    const double v0 = b2[0] * u0;
+    const double w = u0 * b2[1] - v0 * b2[4];
+    const double v1 = w + b2[0] * u1;
+    const double o0 = u0 + (v0 - u0) * cd.an_ghi1;
+    const double o1 = u1 + (v1 - u1) * cd.an_ghi1;
+    ol = (int16_t)(int)(f64_clip1_raw(o0) * 32767.0);
+    orr = (int16_t)(int)(f64_clip1_raw(o1) * 32767.0);
 }
 
 __device__ __forceinline__ void analog_frame(const ChainDev &cd, const float *__restrict__ lut,

@@ -129,13 +129,20 @@ struct SpanDev {
 
 // ---------------------------------------------------------------- launchers
 namespace amx {
+// pass 1 for float32 stereo input with the analog stage: k_analog(_h) + k_gemv16 (default),
+// k_front1h (tanh half table in LDS), k_front1s (global table) -- AMX_F1 = 0 / 1 / 2
+#define AMX_F1_SPLIT 0
+#define AMX_F1_HALF 1
+#define AMX_F1_FULL 2
 struct Launch {
     const ChainDev *cd;
     const ChunkDev *chunks;
     const SegDev *segs;
     int32_t n_chunks, n_seg, L;
     hipStream_t stream;
-    const float *lut_half = nullptr;   // odd tanh table's half (k_front1h), NULL: the full table
+    const float *lut_half = nullptr;   // odd tanh table's half (k_front1h, k_analog_h), NULL: the full table
+    int f1_mode = AMX_F1_SPLIT;        // float32 stereo + analog: which pass-1 form (amx_chain.hip)
+    int64_t max_chunk_n = 0;           // frames of the longest chunk (elementwise grids)
 };
 struct ScanPlan {
     int D, n_blk, K;

@@ -238,6 +238,7 @@ struct amx_plan {
     int mb = 0;
     int Le = 1024, warm = 2304, rounds = 2;   // compressor envelope segments (amx_dyn.hip)
     int env_wg = 1, env_pin = 0, env_il = 0;  // k_env0 placement (amx_dyn.hip launch_env)
+    int f1_mode = AMX_F1_SPLIT;               // pass-1 form for float32 stereo + analog
     int n_es = 0;
     std::vector<SegDev> esegs;
     std::vector<int> eseg0, neseg;
@@ -978,8 +979,14 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         const uint32_t *b = reinterpret_cast<const uint32_t *>(desc->tanh_lut);
         bool odd = true;
         for (int k = 1; k < 32768 && odd; k++) odd = b[32768 - k] == (b[32768 + k] ^ 0x80000000u);
-        const char *ev = std::getenv("AMX_F1_HALF");            // (measurements: 0 = full table)
-        if (odd && !(ev && std::atoi(ev) == 0)) {
+        // (measurements: AMX_F1 = 1 runs k_front1h, 2 k_front1s; default the split form,
+        // whose k_analog_h reads the half table from LDS -- AMX_F1_LDS = 0: k_analog, the
+        // global table)
+        if (const char *ev = std::getenv("AMX_F1")) p->f1_mode = std::atoi(ev);
+        if (p->f1_mode == AMX_F1_HALF && !odd) p->f1_mode = AMX_F1_FULL;
+        bool half_for_split = p->f1_mode == AMX_F1_SPLIT && odd;
+        if (const char *ev = std::getenv("AMX_F1_LDS")) half_for_split = half_for_split && std::atoi(ev) != 0;
+        if (p->f1_mode == AMX_F1_HALF || half_for_split) {
             std::vector<float> half(32769);
             for (int k = 0; k < 32768; k++) half[k] = desc->tanh_lut[32768 + k];
             half[32768] = -desc->tanh_lut[0];
@@ -1090,7 +1097,8 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     if (stage < 0 || stage >= AMX_STAGE_COUNT) return fail(AMX_EINVAL, "bad stage %d", stage);
     if (p->n_seg == 0) return AMX_OK;
     hipStream_t st = (hipStream_t)stream;
-    amx::Launch l{p->d_cd, p->d_chunks, p->d_segs, p->n_chunks, p->n_seg, p->L, st, p->d_lut_half};
+    amx::Launch l{p->d_cd, p->d_chunks, p->d_segs, p->n_chunks, p->n_seg, p->L, st, p->d_lut_half,
+                  p->f1_mode, p->max_chunk_n};
     int16_t *a16 = wsp<int16_t>(d_ws, p->o_a16);
     double *e = wsp<double>(d_ws, p->o_e), *s = wsp<double>(d_ws, p->o_s);
     int16_t *p16 = p->mb ? wsp<int16_t>(d_ws, p->o_p16) : nullptr;
