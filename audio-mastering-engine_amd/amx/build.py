@@ -18,7 +18,7 @@ OUT = os.path.join(PKG, "lib", "libamx.so")
 HEADER = os.path.join(PKG, "..", "include", "amx.h")
 SOURCES = ["amx_chain.hip", "amx_scan.hip", "amx_dyn.hip", "amx_loud.hip", "amx_loud192.hip", "amx_final.hip", "amx_io.hip",
            "amx_loudnorm.hip",
-           "amx_plan.cpp"]
+           "amx_plan.cpp", "amx_flac.cpp"]
 HEADERS = ["amx_internal.hpp", "amx_dev.hpp"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-fvisibility=hidden", "-ffp-contract=off", "-Wall", "-Wno-unused-function"]

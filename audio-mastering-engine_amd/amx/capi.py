@@ -78,6 +78,12 @@ class LoudnormDesc(ctypes.Structure):
                                                  "measured_lra", "measured_tp", "measured_thresh", "offset")]
 
 
+class FlacInfo(ctypes.Structure):
+    _fields_ = [("sample_rate", ctypes.c_int32), ("channels", ctypes.c_int32),
+                ("bits_per_sample", ctypes.c_int32), ("max_block", ctypes.c_int32),
+                ("total_frames", ctypes.c_int64)]
+
+
 class TrackSpan(ctypes.Structure):
     _fields_ = [("out_offset", ctypes.c_int64), ("out_frames", ctypes.c_int64),
                 ("track_frame0", ctypes.c_int64), ("track_frames_total", ctypes.c_int64)]
@@ -90,7 +96,7 @@ EXPORTS = ("amx_abi_version", "amx_last_error", "amx_build_id", "amx_plan_create
            "amx_kw_propagate", "amx_loudness_pass2", "amx_loudness_histograms",
            "amx_limiter_geometry", "amx_limiter_prepare", "amx_loudness_decide", "amx_kw_carry_setup", "amx_kw_carry",
            "amx_finalize", "amx_env_counters", "amx_pcm_to_s16", "amx_loudnorm_192k_size",
-           "amx_loudnorm_192k", "amx_loudnorm_192k_ex")
+           "amx_loudnorm_192k", "amx_loudnorm_192k_ex", "amx_flac_info", "amx_flac_decode")
 PCM_FORMATS = {"u8": 0, "s16": 1, "s24": 2, "s32": 3, "f32": 4, "f64": 5,
                "s8": 6, "s16be": 7, "s24be": 8, "s32be": 9, "f32be": 10, "f64be": 11}
 
@@ -141,6 +147,9 @@ def load(path=None):
                                     ctypes.c_int64, vp, vp, vp, vp, vp]
     L.amx_loudnorm_192k_ex.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(LoudnormDesc), vp, vp, vp, vp, vp,
                                        ctypes.c_int64, vp, vp, vp, vp, vp]
+    L.amx_flac_info.argtypes = [vp, ctypes.c_int64, ctypes.POINTER(FlacInfo)]
+    L.amx_flac_decode.argtypes = [vp, ctypes.c_int64, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
+                                  ctypes.c_int32, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
     if L.amx_abi_version() != ABI_VERSION:
         raise AmxError("libamx ABI version mismatch")
     L.amx_build_id.restype = ctypes.c_char_p

@@ -37,6 +37,36 @@ def chunk_bounds(n_frames, fs, quantum=512, segment_time=SEGMENT_TIME_S):
     return [(s, e - s) for s, e in zip(starts, ends)]
 
 
+def chunk_bounds_packets(n_frames, fs, packet_starts, segment_time=SEGMENT_TIME_S):
+    """chunk_bounds for packets of varying length (a FLAC stream's frames): a chunk starts
+    at the first packet whose start is at or after k * segment_time"""
+    n = int(n_frames)
+    if n <= 0:
+        return []
+    ps = np.asarray(packet_starts, np.int64)
+    starts = [0]
+    k = 1
+    while True:
+        t = k * segment_time * int(fs)
+        i = int(np.searchsorted(ps, t, side="left"))
+        if i >= len(ps) or ps[i] >= n:
+            break
+        if ps[i] > starts[-1]:
+            starts.append(int(ps[i]))
+        k += 1
+    ends = starts[1:] + [n]
+    return [(s, e - s) for s, e in zip(starts, ends)]
+
+
+def bounds_for(n_frames, fs, info):
+    """the split of :178 for an input file's WavInfo: packets of varying length when the
+    reader found them (FLAC), else the PCM demuxer's 4096-byte packets"""
+    ps = getattr(info, "packet_starts", None)
+    if ps is not None:
+        return chunk_bounds_packets(n_frames, fs, ps)
+    return chunk_bounds(n_frames, fs, packet_frames(info.block_align))
+
+
 def plan_tracks(track_frames, fs, quantum=512, segment_time=SEGMENT_TIME_S, explicit=None):
     """Chunks for tracks laid out back to back in one input buffer.
 

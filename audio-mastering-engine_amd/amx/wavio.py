@@ -1,8 +1,8 @@
 """Minimal RIFF/WAVE reader/writer (PCM 8/16/24/32 and IEEE float 32/64).
 
 Host I/O for master_audio(): the reference reads any format ffmpeg decodes and
-writes 16-bit PCM (:178, :223); this build reads WAV and AIFF / AIFF-C (aiffio.py,
-read_audio_raw) and writes s16 WAV.
+writes 16-bit PCM (:178, :223); this build reads WAV, AIFF / AIFF-C (aiffio.py) and
+FLAC (flacio.py) -- read_audio_raw -- and writes s16 WAV.
 """
 import struct
 
@@ -58,19 +58,25 @@ def read_wav_raw(path):
 
 
 def read_audio_raw(path):
-    """read_wav_raw for a WAV file, aiffio.read_aiff_raw for AIFF / AIFF-C (the GUI's
-    *.wav / *.aiff inputs, mastering_gui.py:170)"""
-    from . import aiffio
+    """read_wav_raw for a WAV file, aiffio.read_aiff_raw for AIFF / AIFF-C,
+    flacio.read_flac_raw for FLAC (the GUI's *.wav / *.aiff / *.flac inputs,
+    mastering_gui.py:170)"""
+    from . import aiffio, flacio
     if aiffio.is_aiff(path):
         return aiffio.read_aiff_raw(path)
+    if flacio.is_flac(path):
+        return flacio.read_flac_raw(path)
     return read_wav_raw(path)
 
 
 def read_audio_native(path):
-    """read_wav_native / aiffio.read_aiff_native by the file's own header"""
-    from . import aiffio
+    """read_wav_native / aiffio.read_aiff_native / flacio.read_flac_native by the file's
+    own header"""
+    from . import aiffio, flacio
     if aiffio.is_aiff(path):
         return aiffio.read_aiff_native(path)
+    if flacio.is_flac(path):
+        return flacio.read_flac_native(path)
     return read_wav_native(path)
 
 

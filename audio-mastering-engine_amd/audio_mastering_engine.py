@@ -35,7 +35,7 @@ if _HERE not in sys.path:
 import numpy as np  # noqa: E402
 
 from amx import wavio  # noqa: E402
-from amx.chunking import chunk_bounds, packet_frames  # noqa: E402
+from amx.chunking import bounds_for  # noqa: E402
 from amx.settings import EQ_PRESETS  # noqa: E402,F401
 
 __all__ = ["master_audio", "process_audio", "process_audio_with_ffmpeg_pipeline", "EQ_PRESETS",
@@ -48,25 +48,25 @@ def _noop(*a, **k):
 
 def _device_input(path):
     """The input file on the device, as the chunk chain reads it: (d_in, fs, frames,
-    channels_in, input_s16, block_align).  float32 stays float32 (the chain's first
+    channels_in, input_s16, WavInfo).  float32 stays float32 (the chain's first
     kernel quantises it, A.1); every other format is decoded to stereo s16 by
     amx_pcm_to_s16 (what ffmpeg's split writes + pydub's set_channels(2))."""
     import torch
     from amx import capi
-    raw, info, code = wavio.read_audio_raw(path)          # WAV or AIFF / AIFF-C
+    raw, info, code = wavio.read_audio_raw(path)          # WAV, AIFF / AIFF-C or FLAC
     if info.channels not in (1, 2):
         raise ValueError("only mono and stereo inputs are supported (%d channels)" % info.channels)
     frames = raw.size // info.block_align
     d_raw = torch.from_numpy(raw.copy()).to("cuda")
     if code == "f32":
-        return d_raw.view(torch.float32), info.sample_rate, frames, info.channels, False, info.block_align
+        return d_raw.view(torch.float32), info.sample_rate, frames, info.channels, False, info
     if code == "s16" and info.channels == 2:
-        return d_raw.view(torch.int16), info.sample_rate, frames, 2, True, info.block_align
+        return d_raw.view(torch.int16), info.sample_rate, frames, 2, True, info
     d_in = torch.empty((max(1, frames), 2), dtype=torch.int16, device="cuda")
     capi.check(capi.load().amx_pcm_to_s16(capi.ptr(d_raw), frames, info.channels,
                                           capi.PCM_FORMATS[code], capi.ptr(d_in),
                                           capi.ptr_stream()), "amx_pcm_to_s16")
-    return d_in, info.sample_rate, frames, 2, True, info.block_align
+    return d_in, info.sample_rate, frames, 2, True, info
 
 
 def master_audio(settings, status_callback=None, progress_callback=None):
@@ -80,8 +80,8 @@ def master_audio(settings, status_callback=None, progress_callback=None):
         raise ValueError("Input or output file not specified.")              # :173
     status("Splitting audio into manageable chunks...")                       # :176
     progress(0, 100)                                                          # :177
-    d_in, fs, frames, ch_in, s16, block_align = _device_input(input_file)
-    bounds = chunk_bounds(frames, fs, packet_frames(block_align))             # :178
+    d_in, fs, frames, ch_in, s16, info = _device_input(input_file)
+    bounds = bounds_for(frames, fs, info)                                     # :178
     status("Splitting complete.")                                             # :180
     num_chunks = len(bounds)
     total_steps = num_chunks + 4                                              # :184

@@ -205,6 +205,25 @@ AMX_API int amx_run_stage(amx_plan *plan, int32_t stage, const float *d_in, int1
 AMX_API int amx_pcm_to_s16(const void *d_raw, int64_t frames, int32_t channels, int32_t format,
                            int16_t *d_out, void *stream);
 
+/* FLAC input (the GUI's *.flac, mastering_gui.py:170; ffmpeg decodes it at :178).  Host
+ * decoder of the FLAC bitstream (RFC 9639), frames decoded on a thread pool (threads <= 0:
+ * one per core).  amx_flac_decode writes out_frames x channels interleaved int32 samples,
+ * left-justified to 32 bits (sample << (32 - bits_per_sample)) -- ffmpeg's decoded value,
+ * which amx_pcm_to_s16 with AMX_PCM_S32 turns into the s16 chunk samples ffmpeg writes
+ * (>> 16) -- and the frames decoded to *frames_out (out NULL: only *frames_out).  With
+ * n_blocks, the FLAC frames' block sizes in stream order go to blocks[0 .. *n_blocks)
+ * (blocks NULL: only the count): they are the packets whose start times the segment
+ * split cuts at (:178).  Errors: AMX_EINVAL (not FLAC, a corrupt frame), AMX_ERANGE
+ * (out_frames or max_blocks too small). */
+typedef struct amx_flac_info_t {
+    int32_t sample_rate, channels, bits_per_sample, max_block;
+    int64_t total_frames;   /* STREAMINFO's total samples per channel (0: unknown) */
+} amx_flac_info_t;
+AMX_API int amx_flac_info(const uint8_t *data, int64_t size, amx_flac_info_t *info);
+AMX_API int amx_flac_decode(const uint8_t *data, int64_t size, int32_t *out, int64_t out_frames,
+                            int64_t *frames_out, int32_t threads, int32_t *blocks, int64_t max_blocks,
+                            int64_t *n_blocks);
+
 /* Diagnostics of the compressor envelope's fix-up (AMX_STAGE_FIX) of the last step run
  * on d_ws: per round r, out[4r..4r+3] = segments re-run, the most re-runs in one wave
  * (the length of its chain of dependent fixes), waves with work, and the longest

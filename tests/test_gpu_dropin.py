@@ -294,3 +294,47 @@ def test_master_audio_aiff(gpu, oracle_mod, code, channels, seconds, settings):
     assert y.shape == ref.shape
     d = np.abs(y.astype(np.int32) - ref.astype(np.int32))
     assert d.max() == 0, "max |diff| %d LSB" % d.max()
+
+
+@pytest.mark.parametrize("bps,channels,seconds,variable,settings", [
+    (16, 2, 31.0, False, C3), (24, 2, 12.0, True, dict(C3, lufs=None)), (16, 1, 8.0, True, dict(bass_boost=2.0)),
+])
+def test_master_audio_flac(gpu, oracle_mod, bps, channels, seconds, variable, settings):
+    """master_audio from FLAC files (the GUI's *.flac): libamx's decoder, the device decode
+    of its s32 samples, chunk cuts at the FLAC frames (the demuxer's packets); the
+    reference's callbacks and the oracle's output on the s16 chunks ffmpeg would write,
+    bit for bit"""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    import flac_enc
+    import audio_mastering_engine as ame
+    from amx import synth, wavio
+    from amx.chunking import bounds_for
+    fs = 44100
+    n = int(fs * seconds)
+    x = synth.mix_like(n, fs, channels, seed=int(seconds) + bps)
+    hi = (1 << (bps - 1)) - 1
+    nat = np.clip(np.round(np.asarray(x, np.float64).reshape(n, channels) * hi), -hi - 1, hi).astype(np.int64)
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "in.flac"), os.path.join(d, "out.wav")
+        with open(src, "wb") as f:
+            f.write(flac_enc.encode(nat, fs, bps, seed=bps, variable=variable, kinds=["fixed2", "lpc", "verbatim"]))
+        st, pr = [], []
+        out = ame.master_audio(dict(settings, input_file=src, output_file=dst), st.append,
+                               lambda a, b: pr.append((a, b)))
+        assert out == dst
+        y, info = wavio.read_wav_native(dst)
+        xn, finfo = wavio.read_audio_native(src)
+        x16 = wavio.to_s16(xn, finfo)
+        if channels == 1:
+            x16 = x16.reshape(-1)
+        bounds = bounds_for(n, fs, finfo)
+    assert np.array_equal(wavio.to_s16(xn, finfo).astype(np.int64).reshape(n, channels),
+                          (nat << (16 - bps)) if bps <= 16 else (nat >> (bps - 16)))
+    assert info.sample_rate == fs and info.bits == 16 and info.channels == 2
+    want_st, want_pr = _expected_calls(len(bounds), settings.get("lufs") is not None)
+    assert st == want_st and pr == want_pr
+    ref, _ = oracle_mod.pipeline(x16, fs, settings, bounds)
+    assert y.shape == ref.shape
+    dd = np.abs(y.astype(np.int32) - ref.astype(np.int32))
+    assert dd.max() == 0, "max |diff| %d LSB" % dd.max()
