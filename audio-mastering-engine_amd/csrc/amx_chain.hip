@@ -721,9 +721,7 @@ __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const 
                 float v = MASK ? (float)x[f] : xf[f];
                 if (won) {
                     const float o = pair_swap(v);
-                    float l = chn ? o : v, r = chn ? v : o;
-                    width_frame(w, l, r);
-                    v = chn ? r : l;
+                    v = width_one(w, chn ? o : v, chn ? v : o, chn);
                 }
                 const int16_t qv = f32_to_s16(v);
                 const int other = __builtin_amdgcn_update_dpp(0, (int)qv, 0xB1, 0xF, 0xF, false);

@@ -12,16 +12,18 @@ __device__ __forceinline__ int16_t q_f32_to_s16_ffmpeg(float x) {
     v = fminf(fmaxf(v, -32768.0f), 32767.0f);
     return (int16_t)(int)v;
 }
+// float_array_to_audio_segment (:255-256): np.clip to [-1, 1], * 32767, astype(int16).
+// The clip is one v_med3_f32 / a raw v_min_f64 + v_max_f64 pair instead of two compares
+// and selects (each select waits on its compare's VCC): the same value for every
+// non-NaN input, and the chain's values are never NaN (int16 samples through finite
+// coefficients)
 __device__ __forceinline__ int16_t f32_to_s16(float x) {
-    // float_array_to_audio_segment (:255-256) on float32 arrays
-    float v = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
-    v = v * 32767.0f;
+    const float v = __builtin_amdgcn_fmed3f(x, -1.0f, 1.0f) * 32767.0f;
     return (int16_t)(int)v;
 }
+__device__ __forceinline__ double f64_clip1_raw(double x);
 __device__ __forceinline__ int16_t f64_to_s16(double x) {
-    double v = x < -1.0 ? -1.0 : (x > 1.0 ? 1.0 : x);
-    v = v * 32767.0;
-    return (int16_t)(int)v;
+    return (int16_t)(int)(f64_clip1_raw(x) * 32767.0);
 }
 // "%.2f" then float(): the exact decimal rounding (half-even on exact ties) of v (the
 // loudnorm statistics strings the reference parses, :237-241)
@@ -272,8 +274,13 @@ __device__ __forceinline__ void width_frame(float w, float &l, float &r) {
     float mid = (l + r) / 2.0f, side = (l - r) / 2.0f;
     side = side * w;
     float nl = mid + side, nr = mid - side;
-    l = nl < -1.0f ? -1.0f : (nl > 1.0f ? 1.0f : nl);
-    r = nr < -1.0f ? -1.0f : (nr > 1.0f ? 1.0f : nr);
+    l = __builtin_amdgcn_fmed3f(nl, -1.0f, 1.0f);
+    r = __builtin_amdgcn_fmed3f(nr, -1.0f, 1.0f);
+}
+// the one channel a lane keeps (chn 0: left = clip(mid + side), 1: right = clip(mid - side))
+__device__ __forceinline__ float width_one(float w, float l, float r, int chn) {
+    const float mid = (l + r) / 2.0f, side = ((l - r) / 2.0f) * w;
+    return __builtin_amdgcn_fmed3f(chn ? mid - side : mid + side, -1.0f, 1.0f);
 }
 
 // ------------------------------------------------------- LDS tile stager
