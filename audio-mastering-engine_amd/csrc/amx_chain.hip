@@ -436,8 +436,10 @@ __global__ void __launch_bounds__(1024) k_analog_h(const ChainDev *__restrict__ 
 #pragma unroll
             for (int e = 0; e < 8; e++) {
                 const int q = (int)q_f32_to_s16_ffmpeg(x[e]);
-                const float v = s_tab[q < 0 ? -q : q];
-                t[e] = q < 0 ? -v : v;                 // tanh(s) = sign(s) half[|s|]
+                // tanh(s) = sign(s) half[|s|]: half[] >= +0, so the sign is q's sign bit
+                // OR-ed into the value's (the plan checked lut[-s] == -lut[s] bit for bit)
+                const float v = s_tab[abs(q)];
+                t[e] = __int_as_float(__float_as_int(v) | (q & (int)0x80000000));
             }
             uint32_t o[4];
 #pragma unroll

@@ -212,12 +212,12 @@ __device__ __forceinline__ double env_step(const ChainDev &cd, double att, doubl
     return env_step3(att, m, env_div<RCP>(m, cd.env_A, cd.env_rA), env_div<RCP>(m, cd.env_R, cd.env_rR));
 }
 
-// audioop.mul clamp + floor (CPython Modules/audioop.c fbound), branch-free:
-// > 32767 -> 32767, < -32767 -> -32768, then floor.  floor(max(val, -32768)) is the
-// same: a val in [-32768, -32767) floors to -32768 by itself (one max instead of a
-// compare and two selects)
+// audioop.mul: floor(fbound(v * f)) (CPython Modules/audioop.c), the clamp to
+// [-32768, 32767] included.  The compressor's factor is 0 <= f <= 1 (10^(-att/20), att
+// >= 0; exp10_gain gives exactly 1 at 0 and never rounds above it), so for an int16 v the
+// product already lies in [-32768, 32767] and the clamp never acts: floor alone.
 __device__ __forceinline__ int mul16(int v, double f) {
-    return (int)floor(fmax(fmin((double)v * f, 32767.0), -32768.0));
+    return (int)floor((double)v * f);
 }
 
 // 10^x for the gain: ROCm device-libs' exp10 (ocml) operation for operation --
