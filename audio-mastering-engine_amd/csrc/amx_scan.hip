@@ -36,7 +36,16 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_scan_blk(const ScanBlk *__restric
     constexpr int GW = 64 / GP;
     constexpr int GPB = GW * (AMX_BLOCK / 64);
     __shared__ __attribute__((aligned(16))) double lds[AMX_BLOCK];
+    // the window's block powers Mb^k (k = 1 .. K - 1, (K - 1) D^2 doubles), staged in LDS
+    // once per workgroup: read from memory inside the window loop they put a load's
+    // latency on each of its K - 1 dependent steps (C5: K = 6)
+    __shared__ __attribute__((aligned(16))) double s_pow[DOWN ? AMX_SCAN_PW * D * D : 1];
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    if constexpr (DOWN) {
+        const int np = (K - 1 < AMX_SCAN_PW ? K - 1 : AMX_SCAN_PW) * D * D;
+        for (int k = t; k < np; k += AMX_BLOCK) s_pow[k] = Mbk[k];
+        __syncthreads();
+    }
     const int gl = l / GP, i = l % GP;
     const bool lane_ok = gl < GW;
     const int64_t g = (int64_t)blockIdx.x * GPB + w * GW + (lane_ok ? gl : 0);   // (block, channel) = 2 b + ch
@@ -70,12 +79,22 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_scan_blk(const ScanBlk *__restric
             return eb[((int64_t)(bb - 1) * 2 + ch) * D + ri];
         };
         v = (gvalid && row) ? xin(b) : 0.0;
+        // the window's inputs, loaded before its chain
+        double xs[AMX_SCAN_PW + 1];
+#pragma unroll
+        for (int k = 1; k <= AMX_SCAN_PW; k++) {
+            const int bb = b - k;
+            xs[k] = (k < K && gvalid && bb >= bk.first && row) ? xin(bb) : 0.0;
+        }
         for (int k = 1; k < K; k++) {
             const int bb = b - k;
             const bool ok = gvalid && bb >= bk.first;
-            if (lane_ok) my[i] = (ok && row) ? xin(bb) : 0.0;
+            double xk = 0.0;
+#pragma unroll
+            for (int q = 1; q <= AMX_SCAN_PW; q++) xk = q == k ? xs[q] : xk;
+            if (lane_ok) my[i] = k <= AMX_SCAN_PW ? xk : ((ok && row) ? xin(bb) : 0.0);
             __builtin_amdgcn_wave_barrier();
-            const double *P = Mbk + ((int64_t)(k - 1) * D + ri) * D;
+            const double *P = (k <= AMX_SCAN_PW ? s_pow : Mbk) + ((int64_t)(k - 1) * D + ri) * D;
             double a0 = 0.0, a1 = 0.0;
 #pragma unroll
             for (int m = 0; m < D; m += 2) {
