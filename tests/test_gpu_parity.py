@@ -418,3 +418,22 @@ def test_tp_decision_at_192k(gpu, oracle_mod, fs):
         assert rep["stats"][0] == st, (rep["stats"][0], st)
         mode, _ = oracle_mod.loudnorm_linear_gain(st, target)
         assert (want is None or mode == want) and rep["modes"] == [mode], (target, mode, rep["modes"])
+
+
+@pytest.mark.parametrize("env", [{"AMX_F1_LDS": "0"}, {"AMX_F1": "1"}, {"AMX_F1": "2"}],
+                         ids=["split-global-table", "front1h", "front1s"])
+def test_front1_variants_vs_oracle(gpu, oracle_mod, monkeypatch, env):
+    """every form of the analog + EQ front (amx_chain.hip front1s_t) gives the default's
+    result: k_analog (the tanh table in global memory, the form an even table would
+    take), the fused k_front1h (half table in LDS) and k_front1s (full table)"""
+    from amx import synth
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    fs = 48000
+    n = int(fs * 3.1)
+    x16 = oracle_mod.quantize(synth.music_like(n, fs, 2, seed=31, peak_dbfs=-1.0))
+    settings = dict(C3, analog_character=100.0)
+    cuts = [(0, n // 2 + 3), (n // 2 + 3, n - n // 2 - 3)]
+    out, _ = _chunk_chain(x16, fs, settings, cuts, seg_frames=128)
+    ref = np.concatenate([oracle_mod.chunk(x16[s:s + m], fs, settings) for s, m in cuts])
+    _cmp(out, ref, "front1 %s" % env)
