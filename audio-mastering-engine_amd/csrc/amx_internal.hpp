@@ -201,6 +201,9 @@ hipError_t launch_hist(const SpanDev *spans, int n_tracks, int hop, const double
 // loudness at 192 kHz (amx_loud192.hip): the resampled stream is recomputed from d_out
 #define AMX_UP_EDGE 16     // frames of the neighbour rank's output the resampler window needs
 #define AMX_UP_BLOCK 64
+// k_up_poly's template form as one code (launch switch, plan)
+#define AMX_UP_POLY(cmin, cmax, tb) ((cmin) * 256 + (cmax) * 16 + (tb))
+int up_poly_form(int cmin, int cmax, int tb);   // the code if that form is built, else 0
 struct UpArgs {
     const ChainDev *cd;
     const KwSegDev *ks;
@@ -208,6 +211,9 @@ struct UpArgs {
     const SpanDev *spans;
     int Lin, Lout;            // input frames / 192 kHz outputs per K segment
     int static_l;             // L when M == 1 (unrolled kernels), else 0 (tables)
+    int poly;                 // k_up_poly's form (AMX_UP_POLY), else 0
+    const int32_t *fcnt;      // k_up_poly: per segment frame, the outputs it is the base of
+    const float *bankn;       // k_up_poly: [Lout][32] the bank rows in output order
     int hop;
     const int32_t *obase, *oph;   // per output n < Lout: input frame (segment-relative), phase
     const int32_t *slow;          // segments k_up_slow takes (NULL: all, when static_l == 0)

@@ -283,6 +283,73 @@ k_up(UpArgs a) {
     acc_store(a, acc, j, ch);
 }
 
+// M > 1 rates (44.1 / 88.2 / 176.4 kHz) and the M == 1 rates without an unrolled phase
+// loop (32 / 64 kHz): k_up's register window of TB + 31 frames, taken frame by frame.
+// Frame kb of a block is the base of cnt consecutive outputs (CMIN <= cnt <= CMAX, the
+// plan's per-frame table fcnt: the phase pattern is the same for every segment, so the
+// count is wave-uniform).  Output n's bank row is row n of the plan's table in output
+// order (bankn[n] = bank[oph[n]]): a scalar load at an address the output counter gives,
+// where k_up_slow first loads obase[n] and oph[n] and only then the row, and moves its
+// window one frame at a time through masked, bounds-tested loads.  The segments this
+// kernel leaves (span ends, partial segments, hop splits) go to k_up_edge, as for k_up.
+template <int CMIN, int CMAX, int TB>
+__global__ void __launch_bounds__(AMX_UP_BLOCK) __attribute__((amdgpu_waves_per_eu(AMX_UP_WAVES)))
+k_up_poly(UpArgs a) {
+    static_assert(CMIN >= 1 && CMIN <= CMAX, "every frame is the base of >= 1 output");
+    const int lane = threadIdx.x;
+    const int ch = lane & 1;
+    const int64_t j = (int64_t)blockIdx.x * (AMX_UP_BLOCK / 2) + (lane >> 1);
+    if (j >= a.n_kseg) return;
+    const KwSegDev sg = a.ks[j];
+    const SpanDev sp = a.spans[sg.track];
+    if (!up_fast_seg(a, sg, sp)) return;
+    const int64_t g0 = sg.out_pos - sp.out_off;
+    UpAcc<true> acc;
+    acc_init(a, acc, a.Lout, a.Lout);
+    constexpr int W = TB + UP_TAPS - 1;                        // inputs [k0 - 15, k0 + TB + 16)
+    float w[W];
+    const uint32_t *xp = a.x + sp.out_off + g0 - UP_C;         // frame g0 - 15
+#pragma unroll
+    for (int i = 0; i < W; i++) w[i] = up_sample(xp[i], ch);
+    const int nblk = a.Lin / TB;
+    int n = 0;                                                 // next output (wave-uniform)
+    for (int b = 0; b < nblk; b++) {
+        uint32_t nx[TB];
+        const int o0 = (b + 1 < nblk ? (b + 1) * TB : b * TB) + (W - TB);
+#pragma unroll
+        for (int i = 0; i < TB; i++) nx[i] = xp[o0 + i];
+        const int32_t *cn = a.fcnt + b * TB;
+#pragma unroll
+        for (int kb = 0; kb < TB; kb++) {
+            const int c = cn[kb];
+#pragma unroll
+            for (int o = 0; o < CMAX; o++) {
+                if (o < CMIN || o < c) {
+                    __builtin_amdgcn_sched_barrier(AMX_UP_SB);
+                    acc.add(n, UP_DOT(w + kb, a.bankn + (int64_t)n * UP_TAPS), w[kb + UP_C]);
+                    n++;
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(AMX_UP_SB);
+#pragma unroll
+        for (int i = 0; i < W - TB; i++) w[i] = w[i + TB];
+#pragma unroll
+        for (int i = 0; i < TB; i++) w[W - TB + i] = up_sample(nx[i], ch);
+    }
+    acc_store(a, acc, j, ch);
+}
+
+// the (CMIN, CMAX, TB) forms k_up_poly is built for
+#define AMX_UP_POLY_FORMS(X) X(4, 5, 7) X(2, 3, 7) X(1, 2, 7) X(6, 6, 8) X(3, 3, 8)
+
+int up_poly_form(int cmin, int cmax, int tb) {
+#define AMX_UP_POLY_HAS(c0, c1, t) if (cmin == c0 && cmax == c1 && tb == t) return AMX_UP_POLY(c0, c1, t);
+    AMX_UP_POLY_FORMS(AMX_UP_POLY_HAS)
+#undef AMX_UP_POLY_HAS
+    return 0;
+}
+
 // The general kernel, over the plan's list of the segments k_up does not take (span
 // ends, partial segments, hop splits) -- or over every segment when the rate has no
 // unrolled form (M > 1, e.g. 44.1 kHz: phase pattern from the tables, the window
@@ -482,7 +549,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_up_energy(UpArgs a) {
 hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
     if (a.n_kseg <= 0) return hipSuccess;
     const unsigned nblk = (unsigned)((a.n_kseg + AMX_UP_BLOCK / 2 - 1) / (AMX_UP_BLOCK / 2));
-    if (a.static_l > 0) {
+    if (a.static_l > 0 || a.poly > 0) {
         // the left-over segments' kernel is latency-bound (a serial K-filter lane per
         // channel): it runs on the plan's second stream beside the fast kernel
         const bool side = a.n_slow > 0 && aux && fork && join;
@@ -501,9 +568,14 @@ hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent
                 if (e != hipSuccess) return e;
             }
         }
-        switch (a.static_l) {
+        switch (a.static_l > 0 ? a.static_l : a.poly) {
         case 2: hipLaunchKernelGGL(k_up<2>, dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a); break;
         case 4: hipLaunchKernelGGL(k_up<4>, dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a); break;
+#define AMX_UP_POLY_CASE(c0, c1, t)                                                                  \
+        case AMX_UP_POLY(c0, c1, t):                                                                 \
+            hipLaunchKernelGGL((k_up_poly<c0, c1, t>), dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a); break;
+        AMX_UP_POLY_FORMS(AMX_UP_POLY_CASE)
+#undef AMX_UP_POLY_CASE
         default: return hipErrorInvalidValue;
         }
         if (side) {

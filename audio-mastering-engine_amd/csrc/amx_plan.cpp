@@ -226,7 +226,10 @@ struct amx_plan {
     int resamp = 0, upL = 1, upM = 1, upLin = 0, upLout = 0, up_static = 0, up_ok = 1;
     int meas_native = 0;    // no 192 kHz resampler for this rate: peaks only, no loudnorm
     int32_t *d_obase = nullptr, *d_oph = nullptr;
-    int32_t *d_slow = nullptr;   // K segments k_up_edge takes (static path); n_slow of them
+    int32_t *d_slow = nullptr;   // K segments k_up_edge takes (static / poly path); n_slow of them
+    int up_poly = 0;             // k_up_poly's form (AMX_UP_POLY) when the rate has one
+    int32_t *d_fcnt = nullptr;   // k_up_poly: outputs per segment frame
+    float *d_bankn = nullptr;    // k_up_poly: bank rows in output order
     int64_t n_slow = 0;
     double kdf_b[5] = {0, 0, 0, 0, 0}, kdf_a[5] = {0, 0, 0, 0, 0};   // K filter, fused direct form (192 kHz)
     hipStream_t up_aux = nullptr;            // k_up_edge's stream, forked from / joined to the caller's
@@ -369,7 +372,8 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     // the loudness measurement's rate: 192 kHz (af_loudnorm dynamic mode, :229)
     int kfs = AMX_MEAS_RATE;
     std::vector<float> bank;
-    std::vector<int32_t> obase, oph;
+    std::vector<int32_t> obase, oph, fcnt;
+    std::vector<float> bankn;
     if (fs != kfs) {
         p->resamp = 1;
         if (amx::swr_geometry(fs, kfs, &p->upL, &p->upM) != 0) {
@@ -770,6 +774,27 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             oph[n] = (int32_t)(idx % uL);
         }
         if (p->up_static && pattern != 0) p->up_static = 0;
+        if (!p->up_static) {
+            // k_up_poly: frame f of a segment is the base of the outputs n with obase[n]
+            // == f (consecutive n; every frame has one when L >= M); the form is (min,
+            // max count, a block of TB frames dividing Lin)
+            fcnt.assign((size_t)p->upLin, 0);
+            bool ok = p->upL >= p->upM;
+            for (int64_t n = 0; n < p->upLout && ok; n++) {
+                ok = obase[n] >= 0 && obase[n] < p->upLin && (n == 0 || obase[n] >= obase[n - 1]);
+                if (ok) fcnt[obase[n]]++;
+            }
+            int cmin = 1 << 30, cmax = 0;
+            for (int32_t c : fcnt) { cmin = std::min(cmin, c); cmax = std::max(cmax, c); }
+            const int tb = p->upLin % 8 == 0 ? 8 : (p->upLin % 7 == 0 ? 7 : 0);
+            if (ok && cmin >= 1 && tb) p->up_poly = amx::up_poly_form(cmin, cmax, tb);
+            if (const char *ev = std::getenv("AMX_UP_POLY")) p->up_poly = std::atoi(ev) ? p->up_poly : 0;
+            if (p->up_poly) {
+                bankn.resize((size_t)p->upLout * 32);
+                for (int64_t n = 0; n < p->upLout; n++)
+                    for (int k = 0; k < 32; k++) bankn[(size_t)n * 32 + k] = bank[(size_t)oph[n] * 32 + k];
+            }
+        }
     }
     p->n_kseg = (int)p->ksegs.size();
     // the segments the unrolled 192 kHz kernel leaves to the general one: windows that
@@ -777,7 +802,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     // (the same test as up_fast_seg in amx_loud192.hip)
     std::vector<int32_t> slow;
     if (p->resamp && p->up_ok) {
-        if (p->up_static) {
+        if (p->up_static || p->up_poly) {
             for (int32_t j = 0; j < p->n_kseg; j++) {
                 const KwSegDev &sg = p->ksegs[j];
                 const SpanDev &sp = p->spans[sg.track];
@@ -963,6 +988,10 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     UP(p->d_oph, oph.data(), oph.size());
     if (!slow.empty()) UP(p->d_slow, slow.data(), slow.size());
     UP(p->d_bank, bank.data(), bank.size());
+    if (p->up_poly) {
+        UP(p->d_fcnt, fcnt.data(), fcnt.size());
+        UP(p->d_bankn, bankn.data(), bankn.size());
+    }
     {
         std::vector<unsigned int> zero((size_t)(p->n_tracks > 0 ? p->n_tracks : 1), 0u);
         UP(p->d_pcnt, zero.data(), zero.size());
@@ -1033,7 +1062,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     if (p->resamp) p->o_eterms = (size_t)align_up(off, nk * 2 * 10 * 8);
     p->o_phop = (size_t)align_up(off, nk * 8);
     p->ws_bytes = (off + 255) & ~(size_t)255;
-    if (p->resamp && p->up_static && p->n_slow > 0) {
+    if (p->resamp && (p->up_static || p->up_poly) && p->n_slow > 0) {
         if (hipStreamCreateWithFlags(&p->up_aux, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&p->up_fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&p->up_join, hipEventDisableTiming) != hipSuccess) {
@@ -1053,7 +1082,7 @@ void amx_plan_free(amx_plan *p) {
                     p->d_bounds, p->d_tailpow, p->d_lut, p->d_energies, p->d_carryP,
                     p->d_esegs, p->d_eseg0, p->d_neseg, p->d_pcnt, p->d_ppart,
                     p->lim.seg_state, p->lim.cnt, p->d_obase, p->d_oph, p->d_bank,
-                    p->d_qh, p->d_qt, p->d_slow, p->d_lut_half};
+                    p->d_qh, p->d_qt, p->d_slow, p->d_lut_half, p->d_fcnt, p->d_bankn};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     if (p->up_fork) (void)hipEventDestroy(p->up_fork);
@@ -1189,6 +1218,9 @@ amx::UpArgs up_args(const amx_plan *p, const int16_t *d_out, const int16_t *d_ed
     a.Lin = p->upLin;
     a.Lout = p->upLout;
     a.static_l = p->up_static;
+    a.poly = p->up_poly;
+    a.fcnt = p->d_fcnt;
+    a.bankn = p->d_bankn;
     a.hop = p->hop;
     a.obase = p->d_obase;
     a.oph = p->d_oph;

@@ -25,20 +25,26 @@ CASES = {
     # a full-scale square: the limiter never comes to rest, so rank 1's first run (from
     # rest) is wrong and it must re-run from the state rank 0 hands it
     "square_limiter": dict(),
+    # 44.1 kHz: rank 1's span starts off the 192 kHz phase grid (147 chain frames per 640
+    # outputs), so its resampler segments run with a non-zero phase pattern (k_up_poly)
+    "c3_lufs_44k1": dict(bass_boost=-1.0, mid_cut=2.0, presence_boost=2.5, treble_boost=1.0,
+                         lufs=-14.0, width=1.3, analog_character=40.0, **MB),
 }
+RATE = {"c3_lufs_44k1": 44100}
 
 
 # input gain per case: the loud case drives 0.1 % of the frames over the limit, so the final
 # alimiter (limit 0.98) must engage and the ranks hand its state along
-GAIN = {"c3_lufs": 1.0, "loud_limiter": 1.3, "square_limiter": 1.0}
+GAIN = {"c3_lufs": 1.0, "loud_limiter": 1.3, "square_limiter": 1.0, "c3_lufs_44k1": 1.0}
 
 
 def _track(seconds, case):
     from amx import synth
-    n = int(FS * seconds)
+    fs = RATE.get(case, FS)
+    n = int(fs * seconds)
     if case == "square_limiter":
-        return synth.square(n, FS, 2, freq=110.0, amp=1.0)
-    return (synth.mix_like(n, FS, 2, seed=3) * np.float32(GAIN[case])).astype(np.float32)
+        return synth.square(n, fs, 2, freq=110.0, amp=1.0)
+    return (synth.mix_like(n, fs, 2, seed=3) * np.float32(GAIN[case])).astype(np.float32)
 
 
 def _worker(rank, world, port, case, seconds, outdir):
@@ -52,7 +58,7 @@ def _worker(rank, world, port, case, seconds, outdir):
     try:
         torch.cuda.set_device(0)
         x = _track(seconds, case)
-        tr = ShardedTrack(FS, 2, CASES[case], x.shape[0], rank, world, quantum=512)
+        tr = ShardedTrack(RATE.get(case, FS), 2, CASES[case], x.shape[0], rank, world, quantum=512)
         d_in = torch.from_numpy(np.ascontiguousarray(x[tr.in0:tr.in0 + tr.local_frames])).cuda()
         y = tr.step(d_in)
         torch.cuda.synchronize()
@@ -83,9 +89,9 @@ def test_two_ranks_match_one(gpu, case):
     from amx.dist import ShardedTrack
     # 3 chunks -> ranks own 2 + 1; the sequential-limiter case 2 chunks (that path walks
     # every frame in order)
-    seconds = 75.0 if case == "c3_lufs" else 32.0
+    seconds = 75.0 if case.startswith("c3_lufs") else 32.0
     x = _track(seconds, case)
-    one = ShardedTrack(FS, 2, CASES[case], x.shape[0], 0, 1, quantum=512)
+    one = ShardedTrack(RATE.get(case, FS), 2, CASES[case], x.shape[0], 0, 1, quantum=512)
     y1 = one.step(torch.from_numpy(np.ascontiguousarray(x)).cuda()).cpu().numpy()
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(2, _port(), case, seconds, d), nprocs=2, join=True)
@@ -94,7 +100,7 @@ def test_two_ranks_match_one(gpu, case):
     y2 = np.concatenate(parts)
     assert fast[0] == fast[1]
     # the loud case must exercise the rank-to-rank sequential limiter
-    assert fast[0] == (case == "c3_lufs"), "limiter fast path %s" % fast[0]
+    assert fast[0] == case.startswith("c3_lufs"), "limiter fast path %s" % fast[0]
     assert y2.shape == y1.shape
     diff = np.abs(y2.astype(np.int32) - y1.astype(np.int32))
     assert diff.max() == 0, "max |diff| %d LSB at %s (limiter fast path %s)" % (

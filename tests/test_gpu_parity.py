@@ -437,3 +437,35 @@ def test_front1_variants_vs_oracle(gpu, oracle_mod, monkeypatch, env):
     out, _ = _chunk_chain(x16, fs, settings, cuts, seg_frames=128)
     ref = np.concatenate([oracle_mod.chunk(x16[s:s + m], fs, settings) for s, m in cuts])
     _cmp(out, ref, "front1 %s" % env)
+
+
+@pytest.mark.parametrize("fs,env", [
+    (44100, {}), (44100, {"AMX_UP_POLY": "0"}), (88200, {}), (176400, {}), (32000, {}), (64000, {}),
+    (24000, {}),
+], ids=["44k1-poly", "44k1-slow", "88k2-poly", "176k4-poly", "32k-poly", "64k-poly", "24k-slow"])
+def test_loudness_192k_rates_vs_oracle(gpu, oracle_mod, monkeypatch, fs, env):
+    """the 192 kHz measurement at the rates without the unrolled k_up: k_up_poly's forms
+    (amx_loud192.hip AMX_UP_POLY_FORMS) and k_up_slow (AMX_UP_POLY = 0, and 24 kHz, whose
+    form is not built) -- histograms, 192 kHz sample peaks bit for bit, the statistics"""
+    import torch
+    from amx import synth
+    from amx.engine import MasteringJob
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    n = fs * 7 + 1234
+    x16 = oracle_mod.quantize(synth.music_like(n, fs, 2, seed=fs % 1000, peak_dbfs=-2.0))
+    job = MasteringJob(fs, 2, dict(lufs=-14.0), [n], input_s16=True, chunks=[(0, 0, n)])
+    job.run_chunks(torch.from_numpy(x16).cuda())
+    job.loudness_pass1()
+    job.loudness_pass2(carry=False)
+    job.histograms()
+    hist = job.hist.cpu().numpy().view(np.uint64)[0]
+    st = job.st_hist.cpu().numpy().view(np.uint64)[0]
+    out = job.out[:n].cpu().numpy()
+    oh, ost, opk, _ = oracle_mod.ebur128_192k(out, fs)
+    assert hist.sum() == oh.sum() and st.sum() == ost.sum()
+    assert np.abs(hist.astype(np.int64) - oh.astype(np.int64)).sum() <= 2
+    assert np.abs(st.astype(np.int64) - ost.astype(np.int64)).sum() <= 2
+    np.testing.assert_array_equal(job.peak.cpu().numpy()[0][:2], opk)
+    job.decide()
+    assert job.fetch_report(raise_dynamic=False)["stats"][0] == oracle_mod.loudnorm_measure(out, fs)
