@@ -416,6 +416,11 @@ __device__ __forceinline__ void analog_load8(const float *src, int64_t f, int64_
     }
 }
 
+// FLAT: the workgroups stride over the 4096-frame blocks of all chunks in one sequence
+// (block b of the job -> its chunk by a scalar walk over the chunk list, monotone per
+// workgroup), so a chunk's last, partial round of blocks does not leave most workgroups
+// idle before the next chunk starts (C3: 352 blocks per chunk over 256 workgroups)
+template <bool FLAT>
 __global__ void __launch_bounds__(1024) k_analog_h(const ChainDev *__restrict__ cdp,
                                                    const ChunkDev *__restrict__ chunks, int n_chunks,
                                                    const float *__restrict__ in,
@@ -425,52 +430,96 @@ __global__ void __launch_bounds__(1024) k_analog_h(const ChainDev *__restrict__ 
     for (int i = threadIdx.x; i < AMX_HALF_LUT; i += 1024) s_tab[i] = lut_half[i];
     __syncthreads();
     const ChainDev &cd = *cdp;
-    const int64_t stride = (int64_t)gridDim.x * 1024 * 4;
-    for (int c = 0; c < n_chunks; c++) {
-        const ChunkDev ch = chunks[c];
-        const bool vin = (ch.in_off & 1) == 0, vout = (ch.loc_off & 3) == 0;
-        int64_t f = ((int64_t)blockIdx.x * 1024 + threadIdx.x) * 4;
-        if (f >= ch.n) continue;
-        auto work = [&](const float (&x)[8], int64_t ff) {
-            float t[8];
+    auto work = [&](const ChunkDev &ch, const float (&x)[8], int64_t ff) {
+        float t[8];
 #pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const int q = (int)q_f32_to_s16_ffmpeg(x[e]);
-                // tanh(s) = sign(s) half[|s|]: half[] >= +0, so the sign is q's sign bit
-                // OR-ed into the value's (the plan checked lut[-s] == -lut[s] bit for bit)
-                const float v = s_tab[abs(q)];
-                t[e] = __int_as_float(__float_as_int(v) | (q & (int)0x80000000));
-            }
-            uint32_t o[4];
+        for (int e = 0; e < 8; e++) {
+            const int q = (int)q_f32_to_s16_ffmpeg(x[e]);
+            // tanh(s) = sign(s) half[|s|]: half[] >= +0, so the sign is q's sign bit
+            // OR-ed into the value's (the plan checked lut[-s] == -lut[s] bit for bit)
+            const float v = s_tab[abs(q)];
+            t[e] = __int_as_float(__float_as_int(v) | (q & (int)0x80000000));
+        }
+        uint32_t o[4];
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                int16_t l, r;
-                analog_shelves(cd, t[2 * i], t[2 * i + 1], l, r);
-                o[i] = pack2(l, r);
-            }
-            uint32_t *dst = a16 + ch.loc_off + ff;
-            if (ff + 4 <= ch.n && vout) {
-                *reinterpret_cast<uint4 *>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
-            } else {
+        for (int i = 0; i < 4; i++) {
+            int16_t l, r;
+            analog_shelves(cd, t[2 * i], t[2 * i + 1], l, r);
+            o[i] = pack2(l, r);
+        }
+        uint32_t *dst = a16 + ch.loc_off + ff;
+        if (ff + 4 <= ch.n && (ch.loc_off & 3) == 0) {
+            *reinterpret_cast<uint4 *>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {
 #pragma unroll
-                for (int i = 0; i < 4; i++)
-                    if (ff + i < ch.n) dst[i] = o[i];
+            for (int i = 0; i < 4; i++)
+                if (ff + i < ch.n) dst[i] = o[i];
+        }
+    };
+    if constexpr (FLAT) {
+        constexpr int64_t BF = 1024 * 4;                   // frames per block
+        int c = 0;
+        int64_t cb0 = 0;                                    // first block of chunk c
+        ChunkDev ch = chunks[0];
+        int64_t nb = (ch.n + BF - 1) / BF;
+        auto seek = [&](int64_t b) -> bool {                // workgroup-uniform
+            while (b >= cb0 + nb) {
+                cb0 += nb;
+                if (++c >= n_chunks) return false;
+                ch = chunks[c];
+                nb = (ch.n + BF - 1) / BF;
             }
+            return true;
         };
-        // two register sets: the next group's input is in flight while one is computed
+        int64_t b = blockIdx.x;
+        if (!seek(b)) return;
+        ChunkDev cc = ch;
+        int64_t f = (b - cb0) * BF + threadIdx.x * 4;
+        // two register sets: the next block's input is in flight while one is computed
         float xa[8], xb[8];
-        analog_load8(in + (ch.in_off + f) * 2, f, ch.n, vin, xa);
+        analog_load8(in + (cc.in_off + f) * 2, f, cc.n, (cc.in_off & 1) == 0, xa);
         for (;;) {
-            int64_t fn = f + stride;
-            if (fn < ch.n) analog_load8(in + (ch.in_off + fn) * 2, fn, ch.n, vin, xb);
-            work(xa, f);
-            if (fn >= ch.n) break;
+            b += gridDim.x;
+            const bool more = seek(b);
+            const ChunkDev cn = ch;
+            const int64_t fn = (b - cb0) * BF + threadIdx.x * 4;
+            if (more) analog_load8(in + (cn.in_off + fn) * 2, fn, cn.n, (cn.in_off & 1) == 0, xb);
+            if (f < cc.n) work(cc, xa, f);
+            if (!more) break;
+            cc = cn;
             f = fn;
-            fn = f + stride;
-            if (fn < ch.n) analog_load8(in + (ch.in_off + fn) * 2, fn, ch.n, vin, xa);
-            work(xb, f);
-            if (fn >= ch.n) break;
-            f = fn;
+            b += gridDim.x;
+            const bool more2 = seek(b);
+            const ChunkDev cn2 = ch;
+            const int64_t fn2 = (b - cb0) * BF + threadIdx.x * 4;
+            if (more2) analog_load8(in + (cn2.in_off + fn2) * 2, fn2, cn2.n, (cn2.in_off & 1) == 0, xa);
+            if (f < cc.n) work(cc, xb, f);
+            if (!more2) break;
+            cc = cn2;
+            f = fn2;
+        }
+    } else {
+        const int64_t stride = (int64_t)gridDim.x * 1024 * 4;
+        for (int c = 0; c < n_chunks; c++) {
+            const ChunkDev ch = chunks[c];
+            const bool vin = (ch.in_off & 1) == 0;
+            int64_t f = ((int64_t)blockIdx.x * 1024 + threadIdx.x) * 4;
+            if (f >= ch.n) continue;
+            // two register sets: the next group's input is in flight while one is computed
+            float xa[8], xb[8];
+            analog_load8(in + (ch.in_off + f) * 2, f, ch.n, vin, xa);
+            for (;;) {
+                int64_t fn = f + stride;
+                if (fn < ch.n) analog_load8(in + (ch.in_off + fn) * 2, fn, ch.n, vin, xb);
+                work(ch, xa, f);
+                if (fn >= ch.n) break;
+                f = fn;
+                fn = f + stride;
+                if (fn < ch.n) analog_load8(in + (ch.in_off + fn) * 2, fn, ch.n, vin, xa);
+                work(ch, xb, f);
+                if (fn >= ch.n) break;
+                f = fn;
+            }
         }
     }
 }
@@ -896,8 +945,12 @@ static hipError_t front1s_t(const Launch &l, const uint32_t *in, const float *lu
                 const int64_t quads = (l.max_chunk_n + 3) / 4;
                 const int64_t wgs = (quads * (int64_t)l.n_chunks + 1023) / 1024;
                 const dim3 gh((unsigned)(wgs < cu_count() ? (wgs > 0 ? wgs : 1) : cu_count()));
-                hipLaunchKernelGGL(k_analog_h, gh, dim3(1024), 0, l.stream, l.cd, l.chunks, l.n_chunks,
-                                   reinterpret_cast<const float *>(in), l.lut_half, a16);
+                if (l.analog_flat)
+                    hipLaunchKernelGGL(k_analog_h<true>, gh, dim3(1024), 0, l.stream, l.cd, l.chunks, l.n_chunks,
+                                       reinterpret_cast<const float *>(in), l.lut_half, a16);
+                else
+                    hipLaunchKernelGGL(k_analog_h<false>, gh, dim3(1024), 0, l.stream, l.cd, l.chunks, l.n_chunks,
+                                       reinterpret_cast<const float *>(in), l.lut_half, a16);
             } else {
                 const dim3 ga((unsigned)((l.max_chunk_n + 4 * AMX_BLOCK - 1) / (4 * AMX_BLOCK)),
                               (unsigned)l.n_chunks);

@@ -242,6 +242,7 @@ struct amx_plan {
     int Le = 1024, warm = 2304, rounds = 2;   // compressor envelope segments (amx_dyn.hip)
     int env_wg = 1, env_pin = 0, env_il = 0;  // k_env0 placement (amx_dyn.hip launch_env)
     int f1_mode = AMX_F1_SPLIT;               // pass-1 form for float32 stereo + analog
+    int analog_flat = 1;                      // k_analog_h over all chunks' blocks (AMX_ANALOG_FLAT)
     int n_es = 0;
     std::vector<SegDev> esegs;
     std::vector<int> eseg0, neseg;
@@ -1012,6 +1013,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         // whose k_analog_h reads the half table from LDS -- AMX_F1_LDS = 0: k_analog, the
         // global table)
         if (const char *ev = std::getenv("AMX_F1")) p->f1_mode = std::atoi(ev);
+        if (const char *ev = std::getenv("AMX_ANALOG_FLAT")) p->analog_flat = std::atoi(ev) != 0;
         if (p->f1_mode == AMX_F1_HALF && !odd) p->f1_mode = AMX_F1_FULL;
         bool half_for_split = p->f1_mode == AMX_F1_SPLIT && odd;
         if (const char *ev = std::getenv("AMX_F1_LDS")) half_for_split = half_for_split && std::atoi(ev) != 0;
@@ -1127,7 +1129,7 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     if (p->n_seg == 0) return AMX_OK;
     hipStream_t st = (hipStream_t)stream;
     amx::Launch l{p->d_cd, p->d_chunks, p->d_segs, p->n_chunks, p->n_seg, p->L, st, p->d_lut_half,
-                  p->f1_mode, p->max_chunk_n};
+                  p->f1_mode, p->max_chunk_n, p->analog_flat};
     int16_t *a16 = wsp<int16_t>(d_ws, p->o_a16);
     double *e = wsp<double>(d_ws, p->o_e), *s = wsp<double>(d_ws, p->o_s);
     int16_t *p16 = p->mb ? wsp<int16_t>(d_ws, p->o_p16) : nullptr;

@@ -420,12 +420,13 @@ def test_tp_decision_at_192k(gpu, oracle_mod, fs):
         assert (want is None or mode == want) and rep["modes"] == [mode], (target, mode, rep["modes"])
 
 
-@pytest.mark.parametrize("env", [{"AMX_F1_LDS": "0"}, {"AMX_F1": "1"}, {"AMX_F1": "2"}],
-                         ids=["split-global-table", "front1h", "front1s"])
+@pytest.mark.parametrize("env", [{"AMX_F1_LDS": "0"}, {"AMX_F1": "1"}, {"AMX_F1": "2"}, {"AMX_ANALOG_FLAT": "0"}],
+                         ids=["split-global-table", "front1h", "front1s", "analog-per-chunk"])
 def test_front1_variants_vs_oracle(gpu, oracle_mod, monkeypatch, env):
     """every form of the analog + EQ front (amx_chain.hip front1s_t) gives the default's
     result: k_analog (the tanh table in global memory, the form an even table would
-    take), the fused k_front1h (half table in LDS) and k_front1s (full table)"""
+    take), the fused k_front1h (half table in LDS) and k_front1s (full table), and
+    k_analog_h walking the chunks one at a time instead of as one block sequence"""
     from amx import synth
     for k, v in env.items():
         monkeypatch.setenv(k, v)
