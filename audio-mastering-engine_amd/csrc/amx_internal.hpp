@@ -10,7 +10,9 @@
 #define AMX_BLOCK 256
 #define AMX_HIST_BINS 1000
 #define AMX_TF_FRAMES 16  // LDS tile frames (AMX_TF in amx_dev.hpp)
+#ifndef AMX_SCAN_S
 #define AMX_SCAN_S 16     // segments per scan block
+#endif
 #define AMX_SCAN_PW 6     // window powers staged in LDS by the down sweep (more: read from memory)
 #define AMX_CTL_FAST 1    // k_decide control word: limiter provably idle
 #define AMX_STATS 16      // doubles per track written by k_decide
