@@ -197,6 +197,27 @@ def other_configs(args):
     return out
 
 
+def other_rates(args):
+    """C3 settings on one 5-minute track at 44.1 kHz: the rate whose 192 kHz measurement
+    takes k_up_poly (M > 1) instead of k_up<4> -- not a BASELINE config, reported beside
+    them; the same captured-graph step, timed over >= 1 s"""
+    import gc
+    import torch
+    from amx.dist import ShardedTrack
+    out = {}
+    for fs in (44100,):
+        n = int(CONFIG_SECONDS["c3"] * fs)
+        runner = ShardedTrack(fs, 2, CONFIGS["c3"], n, 0, 1, quantum=512, seg_frames=args.seg_frames)
+        d_in = torch.from_numpy(synth_input(runner.local_frames, fs, 0)).cuda()
+        ms, steps = time_graph(runner, d_in, 2, 0.5, 1.0)
+        out[str(fs)] = {"settings": "c3", "seconds": CONFIG_SECONDS["c3"], "ms_per_step": round(ms, 4),
+                        "steps": steps, "value": round(2 * n / (ms / 1e3) / 1e6, 3), "unit": "Msamples/s"}
+        del runner, d_in
+        gc.collect()
+        torch.cuda.empty_cache()
+    return out
+
+
 def load_traffic(config):
     """Per-launch HBM bytes from the committed PMC summary (profiles/traffic_<config>.json,
     scripts/gpu_traffic.sh: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, separate passes)."""
@@ -459,6 +480,7 @@ def main():
         line.update(cpu_leg(args, runner, x, fs, settings, job, batch))
     if rank == 0 and world == 1 and args.config == "c3" and not args.no_other_configs:
         line["other_configs"] = other_configs(args)
+        line["other_rates"] = other_rates(args)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
