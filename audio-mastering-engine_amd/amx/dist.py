@@ -214,8 +214,12 @@ class ShardedTrack:
     """
 
     def __init__(self, sample_rate, channels_in, settings, track_frames, rank, world, *,
-                 quantum=None, input_s16=False, seg_frames=128, group=None):
+                 quantum=None, input_s16=False, seg_frames=128, group=None, force_exchange=False):
         self.rank, self.world, self.group = rank, world, group
+        # force_exchange: run the N > 1 step (graph segments, every collective, the
+        # carry kernels) even at world 1 -- an RCCL rehearsal on one GPU, since RCCL
+        # refuses two ranks on one device; the output must equal the bypass path's
+        self.xchg = world > 1 or bool(force_exchange)
         fs = int(sample_rate)
         if quantum is None:
             quantum = packet_frames(channels_in * (2 if input_s16 else 4))
@@ -235,7 +239,7 @@ class ShardedTrack:
         self.job = MasteringJob(fs, channels_in, settings, [self.local_frames], chunks=chunks,
                                 track_frame0=[self.tframe0], track_total=[self.ttotal],
                                 input_s16=input_s16, seg_frames=seg_frames)
-        if world > 1:
+        if self.xchg:
             frames_after = [sum(self.span_frames[q + 1:rank]) for q in range(rank)]
             self.job.plan.kw_carry_setup(frames_after)
             dev = self.job.device
@@ -328,7 +332,7 @@ class ShardedTrack:
           G4  histograms + decision + the limiter on the device's decision;
         then the host reads the decision and, only if the limiter can engage, hands
         its state rank to rank."""
-        if self.world == 1:
+        if not self.xchg:
             return self.job.capture(d_in)
         job = self.job
         lufs_on = job.dd.lufs_on
@@ -358,7 +362,7 @@ class ShardedTrack:
         return self._g
 
     def replay(self):
-        if self.world == 1:
+        if not self.xchg:
             return self.job.replay()
         from . import capi
         job = self.job
@@ -390,7 +394,7 @@ class ShardedTrack:
         """One pass of the whole path over this rank's chunks (input resident)."""
         from . import capi
         job = self.job
-        if self.world == 1:
+        if not self.xchg:
             return job.run(d_in)
         job.run_chunks(d_in)
         self.exchange_edges()

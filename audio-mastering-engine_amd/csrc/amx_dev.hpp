@@ -44,6 +44,35 @@ __device__ __forceinline__ uint32_t pack2(int16_t a, int16_t b) {
 __device__ __forceinline__ int16_t lo16(uint32_t v) { return (int16_t)(v & 0xffff); }
 __device__ __forceinline__ int16_t hi16(uint32_t v) { return (int16_t)(v >> 16); }
 
+// libswresample's linear float kernel (resample.asm, FMA3) for the rates whose 192 kHz
+// phase step is not an integer (22.05 / 11.025 kHz: 1024 phases): the dots with rows h
+// (phase ph) and h2 (ph + 1) as two sets of 8 fused chains over taps k, k+8, k+16, k+24;
+// each set folded to 4 lanes (a[k] + a[k+4]); per lane val + (v2 - val) wf as one FMA
+// (wf = (float)frac * (1.0f / src_incr), the plan's table); then the common kernel's
+// horizontal sum.  oracle/amx_oracle.c swr_dot_lin is the same sequence.
+__device__ __forceinline__ float swr_dot_lin(const float *w, const float *__restrict__ h,
+                                             const float *__restrict__ h2, float wf) {
+    float a[8], c[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        float acc = __builtin_fmaf(w[k], h[k], 0.0f), acc2 = __builtin_fmaf(w[k], h2[k], 0.0f);
+#pragma unroll
+        for (int q = 8; q < 32; q += 8) {
+            acc = __builtin_fmaf(w[k + q], h[k + q], acc);
+            acc2 = __builtin_fmaf(w[k + q], h2[k + q], acc2);
+        }
+        a[k] = acc;
+        c[k] = acc2;
+    }
+    float e[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const float b = a[k] + a[k + 4], d = (c[k] + c[k + 4]) - b;
+        e[k] = __builtin_fmaf(d, wf, b);
+    }
+    return (e[0] + e[2]) + (e[1] + e[3]);
+}
+
 // lfilter DF-II-T biquad step (scipy _linear_filter order, fused)
 __device__ __forceinline__ double lf_step(const double *c, double &z0, double &z1, double x) {
     double y = fma(c[0], x, z0);

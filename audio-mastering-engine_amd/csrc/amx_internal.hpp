@@ -219,9 +219,11 @@ struct UpArgs {
     const float *bankn;       // k_up_poly: [Lout][32] the bank rows in output order
     int hop;
     const int32_t *obase, *oph;   // per output n < Lout: input frame (segment-relative), phase
+    const float *owt;             // per output: interpolation weight (lin)
+    int lin;                      // libswresample's linear kernel: rows oph, oph + 1 (1024 phases)
     const int32_t *slow;          // segments k_up_slow takes (NULL: all, when static_l == 0)
     int64_t n_slow;
-    const float *bank;            // [L][32] float32 polyphase bank
+    const float *bank;            // [pc + 1][32] float32 polyphase bank (row pc = row 0 one tap on)
     const uint32_t *x, *edge;     // d_out (stereo s16 dwords); edge [tracks][2][AMX_UP_EDGE]
     const double *G;              // rows C A^n, n < Lout (the K filter's free response)
     const double *qh, *qt;        // Gram matrices of those rows: head sums [Lout+1][16], tail sums
@@ -296,11 +298,20 @@ struct LpArgs {
     int16_t *y;                   // [n][2] output
     double *summary;              // [16]
 };
-hipError_t launch_loudnorm(const LnArgs &a, const LpArgs &p, const uint32_t *x, int64_t n_in, int L,
-                           int M, const float *bank, hipStream_t st);
+// the 192 kHz resampler's geometry (amx_plan.cpp swr_*): output j sits at phase
+// position j dst / src (units of 1 / pc input frame); lin: interpolate rows ph, ph + 1
+struct SwrDev {
+    int pc, lin;
+    int64_t src, dst;
+    const float *bank;            // [pc + 1][32]
+};
+hipError_t launch_loudnorm(const LnArgs &a, const LpArgs &p, const uint32_t *x, int64_t n_in,
+                           const SwrDev &r, hipStream_t st);
 #define AMX_LN_GATED(g) ((g) && (((g)[0] >> 4) & 15) != 3)   // k_decide mode 3 = dynamic
 hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent_t fork, hipEvent_t join);
 int swr_geometry(int in_rate, int out_rate, int *L, int *M);   // host (amx_plan.cpp)
+int swr_phases(int in_rate, int out_rate);
+int swr_incr(int in_rate, int out_rate, int64_t *src_incr, int64_t *dst_incr);
 int swr_bank(int in_rate, int out_rate, float *bank);
 hipError_t launch_up2(const UpArgs &a, hipStream_t st);
 // finalize

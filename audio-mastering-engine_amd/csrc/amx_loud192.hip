@@ -383,7 +383,8 @@ __global__ void __launch_bounds__(AMX_UP_BLOCK) k_up_slow(UpArgs a) {
             cur++;
         }
         const int ph = a.oph[n];
-        const float u = (a.static_l > 0 && ph == 0) ? w[UP_C] : up_dot(w, a.bank + ph * UP_TAPS);
+        const float u = a.lin ? swr_dot_lin(w, a.bank + ph * UP_TAPS, a.bank + (ph + 1) * UP_TAPS, a.owt[n])
+                        : (a.static_l > 0 && ph == 0) ? w[UP_C] : up_dot(w, a.bank + ph * UP_TAPS);
         acc.add(n, u, w[UP_C]);
     }
     acc_store(a, acc, j, ch);
@@ -417,7 +418,8 @@ __global__ void __launch_bounds__(64) k_up_edge(UpArgs a) {
         float w[UP_TAPS];
 #pragma unroll
         for (int k = 0; k < UP_TAPS; k++) w[k] = up_sample(fr[kb + k], ch);
-        const float u = (a.static_l > 0 && ph == 0) ? w[UP_C] : up_dot(w, a.bank + ph * UP_TAPS);
+        const float u = a.lin ? swr_dot_lin(w, a.bank + ph * UP_TAPS, a.bank + (ph + 1) * UP_TAPS, a.owt[n])
+                        : (a.static_l > 0 && ph == 0) ? w[UP_C] : up_dot(w, a.bank + ph * UP_TAPS);
         us[i] = u;
         if (n < len) {
             pk = fmaxf(pk, fabsf(u));

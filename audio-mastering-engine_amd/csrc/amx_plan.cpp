@@ -157,17 +157,41 @@ namespace amx {
 // 192 kHz stream (what ffmpeg inserts ahead of af_loudnorm in dynamic mode, :229).
 // Restated from resample.c resample_init / build_filter with swresample's defaults:
 // filter_size 32, phase_shift 10, exact_rational 1, cutoff 0.97, Kaiser beta 9, FLTP
-// (float32 bank, scale 1).  Upsampling only (factor 1); L = out/gcd phases (<= 1024,
-// else exact_rational does not apply and the rate is unsupported), M = in/gcd.
+// (float32 bank, scale 1).  Upsampling only (factor 1); L / M = out / in reduced (output j
+// sits at input position j M / L).  The bank has L phases when L <= 1024 (exact_rational)
+// and 1024 otherwise (22.05 / 11.025 kHz): the position then falls between two phases and
+// libswresample's linear kernel interpolates (amx_dev.hpp swr_dot_lin).
 int swr_geometry(int in_rate, int out_rate, int *L, int *M) {
     if (in_rate <= 0 || out_rate <= 0) return -1;
     int64_t a = in_rate, b = out_rate;
     while (b) { int64_t t = a % b; a = b; b = t; }
     const int64_t l = out_rate / a, m = in_rate / a;
-    if (l > 1024) return -1;
     if ((double)out_rate * 0.97 / in_rate < 1.0 && !(l == 1 && m == 1)) return -1;
     *L = (int)l;
     *M = (int)m;
+    return 0;
+}
+
+// resample_init: phase_count 1 << phase_shift (1024), replaced by the exact out / gcd
+// when that is <= 1024 (exact_rational)
+int swr_phases(int in_rate, int out_rate) {
+    int L, M;
+    if (swr_geometry(in_rate, out_rate, &L, &M)) return -1;
+    return L <= 1024 ? L : 1024;
+}
+
+// resample_init: av_reduce(&src_incr, &dst_incr, out_rate, in_rate * phase_count), both
+// doubled while below 2^20; output j sits at phase position j dst_incr / src_incr
+int swr_incr(int in_rate, int out_rate, int64_t *src_incr, int64_t *dst_incr) {
+    const int pc = swr_phases(in_rate, out_rate);
+    if (pc < 0) return -1;
+    int64_t a = out_rate, b = (int64_t)in_rate * pc, x = a, y = b;
+    while (y) { int64_t t = x % y; x = y; y = t; }
+    a /= x;
+    b /= x;
+    while (b < (1 << 20) && a < (1 << 20)) { a *= 2; b *= 2; }
+    *src_incr = a;
+    *dst_incr = b;
     return 0;
 }
 
@@ -189,9 +213,8 @@ static double swr_bessel(double x) {
 }
 
 int swr_bank(int in_rate, int out_rate, float *bank) {
-    int L, M;
-    if (swr_geometry(in_rate, out_rate, &L, &M)) return -1;
-    const int pc = L, taps = 32, center = 15;
+    const int pc = swr_phases(in_rate, out_rate), taps = 32, center = 15;
+    if (pc < 0) return -1;
     const int ph_nb = pc % 2 ? pc : pc / 2 + 1;
     std::vector<double> sin_lut(ph_nb), tab(taps);
     double norm = 0;
@@ -225,7 +248,13 @@ struct amx_plan {
     // the track already is at 192 kHz (the measurement runs on d_out itself)
     int resamp = 0, upL = 1, upM = 1, upLin = 0, upLout = 0, up_static = 0, up_ok = 1;
     int meas_native = 0;    // no 192 kHz resampler for this rate: peaks only, no loudnorm
+    // libswresample's phase count (L, or 1024 when L > 1024), phase step dst / src per
+    // output; up_lin: the step is not an integer, every output interpolates between rows
+    // ph and ph + 1 (bank row pc = row 0 one tap later) with weight owt[n]
+    int up_pc = 1, up_lin = 0;
+    int64_t up_src = 1, up_dst = 1;
     int32_t *d_obase = nullptr, *d_oph = nullptr;
+    float *d_owt = nullptr;
     int32_t *d_slow = nullptr;   // K segments k_up_edge takes (static / poly path); n_slow of them
     int up_poly = 0;             // k_up_poly's form (AMX_UP_POLY) when the rate has one
     int32_t *d_fcnt = nullptr;   // k_up_poly: outputs per segment frame
@@ -374,14 +403,15 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     int kfs = AMX_MEAS_RATE;
     std::vector<float> bank;
     std::vector<int32_t> obase, oph, fcnt;
+    std::vector<float> owt;
     std::vector<float> bankn;
     if (fs != kfs) {
         p->resamp = 1;
         if (amx::swr_geometry(fs, kfs, &p->upL, &p->upM) != 0) {
-            // no exact-rational resampler (192000 / gcd > 1024 phases: 22.05 / 11.025 kHz):
-            // libswresample's inexact 1024-phase path is not restated.  The plan measures
-            // at the track's own rate, which gives the limiter its peaks (the only
-            // measurement lufs=None needs); amx_loudness_decide refuses loudnorm on it.
+            // an input above 192 kHz / 0.97: libswresample would downsample (a longer,
+            // narrower filter), which is not restated.  The plan measures at the track's
+            // own rate, which gives the limiter its peaks (the only measurement lufs=None
+            // needs); amx_loudness_decide refuses loudnorm on it.
             p->up_ok = 0;
             p->resamp = 0;
             p->meas_native = 1;
@@ -393,6 +423,9 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             const int hop192 = (kfs + 5) / 10;
             int target = 480;                 // (AMX_UP_LOUT overrides, for measurements)
             if (const char *ev = std::getenv("AMX_UP_LOUT")) target = std::max(16, std::atoi(ev));
+            p->up_pc = amx::swr_phases(fs, kfs);
+            amx::swr_incr(fs, kfs, &p->up_src, &p->up_dst);
+            p->up_lin = (p->up_dst % p->up_src) != 0;
             int kk = std::max(1, (target + p->upL / 2) / p->upL);
             for (int d = 0; d <= kk; d++) {
                 if (kk - d >= 1 && hop192 % (p->upL * (kk - d)) == 0 && (p->upM * (kk - d)) % 8 == 0) { kk -= d; break; }
@@ -400,12 +433,15 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             }
             p->upLin = p->upM * kk;
             p->upLout = p->upL * kk;
-            bank.assign((size_t)p->upL * 32, 0.0f);
+            bank.assign((size_t)(p->up_pc + 1) * 32, 0.0f);
             amx::swr_bank(fs, kfs, bank.data());
+            // build_filter's extra row pc: row 0 one tap later (the interpolation partner
+            // of the last phase)
+            for (int i = 0; i < 32; i++) bank[(size_t)p->up_pc * 32 + i] = bank[(i + 31) % 32];
             // M == 1: the unrolled kernels (phase pattern static, phase 0 the identity)
             bool ident0 = bank[15] == 1.0f;
             for (int i = 0; i < 32; i++) ident0 = ident0 && (i == 15 || bank[i] == 0.0f);
-            p->up_static = (p->upM == 1 && (p->upL == 2 || p->upL == 4) && ident0 &&
+            p->up_static = (p->upM == 1 && (p->upL == 2 || p->upL == 4) && ident0 && !p->up_lin &&
                             p->upLin % 8 == 0) ? p->upL : 0;
         }
     } else {
@@ -717,9 +753,11 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     // of chain frames [f0, f0 + n) of its track owns outputs [J(f0), J(f0 + n)),
     // J(f) = ceil(f L / M); segment q = chain frames f0 + q Lin + [0, Lin) = outputs
     // J(f0) + q Lout + [0, Lout)
-    const int64_t uL = p->upL, uM = p->upM;
+    const int64_t uL = p->upL, uM = p->upM, uS = p->up_src, uD = p->up_dst, uP = p->up_pc;
     auto J = [&](int64_t f) { return (f * uL + uM - 1) / uM; };
-    int64_t pattern = -1;     // (J(f0) M - f0 L): the phase pattern, equal for all spans
+    // (J(f0) dst - f0 pc src): the phase pattern -- output J(f0)'s position past frame f0
+    // in units of 1 / (pc src) frame (exact rates: (J(f0) M - f0 L) src) -- equal for all spans
+    int64_t pattern = -1;
     for (int t = 0; t < n_tracks; t++) {
         SpanDev &sp = p->spans[t];
         sp.tframe0 = track_frame0 ? track_frame0[t] : 0;
@@ -731,7 +769,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             sp.m_tframe0 = J(sp.tframe0);
             sp.m_n = J(sp.tframe0 + sp.out_n) - sp.m_tframe0;
             sp.m_total = J(sp.ttotal);
-            const int64_t pat = sp.m_tframe0 * uM - sp.tframe0 * uL;
+            const int64_t pat = sp.m_tframe0 * uD - sp.tframe0 * uP * uS;
             if (sp.out_n > 0) {
                 if (pattern >= 0 && pat != pattern) {
                     delete p;
@@ -769,13 +807,17 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         if (pattern < 0) pattern = 0;
         obase.resize(p->upLout);
         oph.resize(p->upLout);
+        owt.resize(p->upLout);
+        const float inv = 1.0f / (float)uS;          // the float reciprocal resample.asm forms
         for (int64_t n = 0; n < p->upLout; n++) {
-            const int64_t idx = pattern + n * uM;     // (J0 + n) M - f0 L
-            obase[n] = (int32_t)(idx / uL);
-            oph[n] = (int32_t)(idx % uL);
+            const int64_t pos = pattern + n * uD;     // (J0 + n) dst - f0 pc src
+            const int64_t idx = pos / uS;
+            obase[n] = (int32_t)(idx / uP);
+            oph[n] = (int32_t)(idx % uP);
+            owt[n] = (float)(pos % uS) * inv;
         }
         if (p->up_static && pattern != 0) p->up_static = 0;
-        if (!p->up_static) {
+        if (!p->up_static && !p->up_lin) {
             // k_up_poly: frame f of a segment is the base of the outputs n with obase[n]
             // == f (consecutive n; every frame has one when L >= M); the form is (min,
             // max count, a block of TB frames dividing Lin)
@@ -987,6 +1029,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     UP(p->d_qh, qh.data(), qh.size());
     UP(p->d_qt, qt.data(), qt.size());
     UP(p->d_oph, oph.data(), oph.size());
+    UP(p->d_owt, owt.data(), owt.size());
     if (!slow.empty()) UP(p->d_slow, slow.data(), slow.size());
     UP(p->d_bank, bank.data(), bank.size());
     if (p->up_poly) {
@@ -1084,7 +1127,7 @@ void amx_plan_free(amx_plan *p) {
                     p->d_bounds, p->d_tailpow, p->d_lut, p->d_energies, p->d_carryP,
                     p->d_esegs, p->d_eseg0, p->d_neseg, p->d_pcnt, p->d_ppart,
                     p->lim.seg_state, p->lim.cnt, p->d_obase, p->d_oph, p->d_bank,
-                    p->d_qh, p->d_qt, p->d_slow, p->d_lut_half, p->d_fcnt, p->d_bankn};
+                    p->d_qh, p->d_qt, p->d_slow, p->d_lut_half, p->d_fcnt, p->d_bankn, p->d_owt};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     if (p->up_fork) (void)hipEventDestroy(p->up_fork);
@@ -1226,6 +1269,8 @@ amx::UpArgs up_args(const amx_plan *p, const int16_t *d_out, const int16_t *d_ed
     a.hop = p->hop;
     a.obase = p->d_obase;
     a.oph = p->d_oph;
+    a.owt = p->d_owt;
+    a.lin = p->up_lin;
     a.slow = p->d_slow;
     a.n_slow = p->n_slow;
     a.bank = p->d_bank;
@@ -1291,7 +1336,7 @@ LnLayout ln_layout(int64_t n192) {
 // itself when it already is 192 kHz)
 int ln_frames(const amx_plan *p, int32_t track, int64_t *n192) {
     if (p->meas_native || (p->resamp && !p->up_ok))
-        return fail(AMX_ERANGE, "loudnorm's 192 kHz modes need an exact-rational 192 kHz resampler");
+        return fail(AMX_ERANGE, "loudnorm's 192 kHz modes need a 192 kHz upsampler (input above 192 kHz)");
     const SpanDev &sp = p->spans[track];
     *n192 = p->resamp ? (sp.out_n * p->upL + p->upM - 1) / p->upM : sp.out_n;
     return AMX_OK;
@@ -1313,7 +1358,7 @@ int amx_loudness_pass1_part(amx_plan *p, int32_t part, const int16_t *d_out, con
         return fail(AMX_EINVAL, "null argument");
     if (part != 0 && part != 1) return fail(AMX_EINVAL, "bad part %d", part);
     if (p->resamp && !p->up_ok)
-        return fail(AMX_ERANGE, "%d Hz has no exact-rational 192 kHz resampler (loudnorm pass 1)",
+        return fail(AMX_ERANGE, "%d Hz has no 192 kHz upsampler (loudnorm pass 1)",
                     p->cd.fs);
     if (int rc = check_edges(p, d_edge)) return rc;
     hipStream_t st = (hipStream_t)stream;
@@ -1458,8 +1503,9 @@ int amx_loudnorm_192k_ex(amx_plan *p, int32_t track, const amx_loudnorm_desc *d,
     a.lp_recG = q.recG;
     a.lp_Fs = q.Fs;
     a.lp_J = q.J;
-    HIPCHK(amx::launch_loudnorm(a, q, reinterpret_cast<const uint32_t *>(d_out) + sp.out_off, sp.out_n, p->upL,
-                                p->upM, p->d_bank, (hipStream_t)stream));
+    amx::SwrDev r{p->up_pc, p->up_lin, p->up_src, p->up_dst, p->d_bank};
+    HIPCHK(amx::launch_loudnorm(a, q, reinterpret_cast<const uint32_t *>(d_out) + sp.out_off, sp.out_n, r,
+                                (hipStream_t)stream));
     return AMX_OK;
 }
 
@@ -1509,7 +1555,7 @@ int amx_loudness_pass2(amx_plan *p, const int16_t *d_out, const int16_t *d_edge,
     if (!p || !d_hops || max_hops <= 0 || (p->n_kseg > 0 && (!d_out || !d_ws)))
         return fail(AMX_EINVAL, "null argument");
     if (p->resamp && !p->up_ok)
-        return fail(AMX_ERANGE, "%d Hz has no exact-rational 192 kHz resampler (loudnorm pass 1)",
+        return fail(AMX_ERANGE, "%d Hz has no 192 kHz upsampler (loudnorm pass 1)",
                     p->cd.fs);
     if (max_hops < p->max_hops) return fail(AMX_EINVAL, "max_hops %lld < %lld", (long long)max_hops,
                                             (long long)p->max_hops);
@@ -1622,9 +1668,8 @@ int amx_loudness_decide(amx_plan *p, const amx_decide_desc *dd, const amx_final_
         (dd->lufs_on && (!d_hist || !d_st_hist)))
         return fail(AMX_EINVAL, "null argument");
     if (dd->lufs_on && p->meas_native)
-        return fail(AMX_ERANGE, "%d Hz: loudnorm measures the track resampled to 192 kHz and this rate "
-                    "has no exact-rational resampler (libswresample's 1024-phase path is not "
-                    "restated); lufs=None works", p->cd.fs);
+        return fail(AMX_ERANGE, "%d Hz: loudnorm measures the track resampled to 192 kHz, which "
+                    "downsamples this rate (not restated); lufs=None works", p->cd.fs);
     amx::DecideArgs a{};
     a.n_tracks = p->n_tracks;
     a.lufs_on = dd->lufs_on ? 1 : 0;

@@ -254,6 +254,9 @@ def main():
                     help="nccl (= RCCL on ROCm); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--one-device", action="store_true",
                     help="every rank on cuda:0 (rehearsal with --dist-backend gloo)")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="run the N > 1 step (graph segments + every collective) even at one rank: "
+                         "an RCCL rehearsal on one GPU")
     args = ap.parse_args()
 
     import numpy as np
@@ -265,8 +268,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_dist = world > 1 or args.force_exchange
+    if use_dist:
         torch.cuda.set_device(0 if args.one_device else local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         dist.init_process_group(args.dist_backend)
     fs = CONFIG_FS[args.config]
     if args.seconds is None:
@@ -286,13 +294,13 @@ def main():
     else:
         total = per_track if args.strong else per_track * world
         runner = ShardedTrack(fs, 2, settings, total, rank, world, quantum=512,
-                              seg_frames=args.seg_frames)
+                              seg_frames=args.seg_frames, force_exchange=args.force_exchange)
         x = synth_input(runner.local_frames, fs, rank)
     d_in = torch.from_numpy(x).cuda()
     job = runner.job
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -326,7 +334,7 @@ def main():
         run()
     barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -436,7 +444,8 @@ def main():
                    "tracks_per_gpu": len(runner.tracks) if batch else 1,
                    "seg_frames": args.seg_frames,
                    "parallelism": ("track-shard x%d" if batch else "chunk-shard x%d") % world,
-                   "launch": ("hipGraph replay" if world == 1 or batch else
+                   "exchanges": ("%s collectives" % dist.get_backend()) if use_dist and not batch else None,
+                   "launch": ("hipGraph replay" if (world == 1 and not args.force_exchange) or batch else
                               "hipGraph segments + eager collectives") if graph else "eager"},
         "timed_region_s": round(elapsed, 4), "soak": {"seconds": round(soak_s, 3), "replays": n_soak},
         "roofline": {"bound": "hbm", "kernel": kern, "stage": dom, "achieved": round(achieved, 2),
@@ -483,7 +492,7 @@ def main():
         line["other_rates"] = other_rates(args)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -545,24 +545,50 @@ static double swr_bessel(double x) {
 
 static int64_t gcd64(int64_t a, int64_t b) { while (b) { int64_t t = a % b; a = b; b = t; } return a; }
 
-/* L = out/g phases, M = in/g phase step; 0 = supported (exact rational, L <= 1024,
- * upsampling), else -1 */
+/* L / M = out_rate / in_rate reduced (output j sits at input position j M / L); 0 =
+ * supported (upsampling), else -1.  The filter bank has orc_swr_phases() rows: L when
+ * L <= 1024 (exact_rational: phase_count = L), else 1024 (libswresample's default
+ * phase_shift 10; the position then falls between phases and the linear path
+ * interpolates, see swr_block) */
 EXPORT int orc_swr_geometry(int in_rate, int out_rate, int *L, int *M) {
     if (in_rate <= 0 || out_rate <= 0) return -1;
     int64_t g = gcd64(in_rate, out_rate);
     int64_t l = out_rate / g, m = in_rate / g;
-    if (l > 1024) return -1;
     if ((double)out_rate * 0.97 / in_rate < 1.0 && !(l == 1 && m == 1)) return -1;   /* downsampling */
     *L = (int)l;
     *M = (int)m;
     return 0;
 }
 
-/* build_filter (factor 1: upsampling, Kaiser, FLTP, scale 1): bank[ph][i], ph < L */
-EXPORT int orc_swr_bank(int in_rate, int out_rate, float *bank) {
+/* resample_init: phase_count = 1 << phase_shift (1024), replaced by the exact
+ * out / gcd when that is <= 1024 */
+EXPORT int orc_swr_phases(int in_rate, int out_rate) {
     int L, M;
     if (orc_swr_geometry(in_rate, out_rate, &L, &M)) return -1;
-    const int pc = L, tap_count = SWR_TAPS, center = SWR_CENTER;
+    return L <= 1024 ? L : 1024;
+}
+
+/* resample_init: av_reduce(&src_incr, &dst_incr, out_rate, in_rate * phase_count,
+ * INT32_MAX / 2), both doubled while below 2^20.  Per output the phase index moves by
+ * dst_incr / src_incr (integer part dst_incr_div, fraction frac in units of 1/src_incr) */
+EXPORT int orc_swr_incr(int in_rate, int out_rate, int64_t *src_incr, int64_t *dst_incr) {
+    const int pc = orc_swr_phases(in_rate, out_rate);
+    if (pc < 0) return -1;
+    int64_t a = out_rate, b = (int64_t)in_rate * pc;
+    const int64_t g = gcd64(a, b);
+    a /= g;
+    b /= g;
+    while (b < (1 << 20) && a < (1 << 20)) { a *= 2; b *= 2; }
+    *src_incr = a;
+    *dst_incr = b;
+    return 0;
+}
+
+/* build_filter (factor 1: upsampling, Kaiser, FLTP, scale 1): bank[ph][i], ph < pc */
+EXPORT int orc_swr_bank(int in_rate, int out_rate, float *bank) {
+    const int pc = orc_swr_phases(in_rate, out_rate);
+    if (pc < 0) return -1;
+    const int tap_count = SWR_TAPS, center = SWR_CENTER;
     const int ph_nb = pc % 2 ? pc : pc / 2 + 1;
     const double factor = 1.0, beta = 9.0;
     double tab[SWR_TAPS];
@@ -621,30 +647,97 @@ static inline float swr_dot(const float *w, const float *h) {
     return (b0 + b2) + (b1 + b3);
 }
 
-/* output frames [j0, j1) of the 192 kHz stream, interleaved doubles */
-static void swr_block(const int16_t *x, int64_t n, int channels, int L, int M, const float *bank,
+/* resample_linear_float (resample.asm, FMA3): the dot products with rows ph (h) and
+ * ph + 1 (h2) run as two sets of 8 fused chains in the same loop; each set is folded
+ * to 4 lanes (a[k] + a[k + 4]); per lane val += (v2 - val) * wf as one FMA, wf =
+ * (float)frac * (1.0f / src_incr) (cvtsi2ss, a float reciprocal formed once); then
+ * the horizontal sum of the common kernel.  PARITY UNPINNED: our reading of the
+ * published assembly, no ffmpeg here to check it against */
+static inline float swr_dot_lin(const float *w, const float *h, const float *h2, float wf) {
+    float a[8], c[8];
+    for (int k = 0; k < 8; k++) {
+        float acc = fmaf(w[k], h[k], 0.0f), acc2 = fmaf(w[k], h2[k], 0.0f);
+        for (int q = 8; q < 32; q += 8) {
+            acc = fmaf(w[k + q], h[k + q], acc);
+            acc2 = fmaf(w[k + q], h2[k + q], acc2);
+        }
+        a[k] = acc;
+        c[k] = acc2;
+    }
+    float e[4];
+    for (int k = 0; k < 4; k++) {
+        const float b = a[k] + a[k + 4], d = (c[k] + c[k + 4]) - b;
+        e[k] = fmaf(d, wf, b);
+    }
+    return (e[0] + e[2]) + (e[1] + e[3]);
+}
+
+/* Resampler geometry for one rate: the bank has pc + 1 rows (row pc = row 0 one tap
+ * later, build_filter's extra row for the interpolation at the last phase) */
+typedef struct {
+    int L, M, pc, lin;
+    int64_t src_incr, dst_incr;
+    float inv;                    /* 1.0f / (float)src_incr */
+    float *bank;
+} Swr;
+
+static int swr_open(Swr *r, int in_rate, int out_rate) {
+    if (orc_swr_geometry(in_rate, out_rate, &r->L, &r->M)) return -1;
+    r->pc = orc_swr_phases(in_rate, out_rate);
+    orc_swr_incr(in_rate, out_rate, &r->src_incr, &r->dst_incr);
+    /* swri_resample: the linear kernel whenever frac or dst_incr_mod is non-zero, i.e.
+     * for every output when the phase step is not an integer; else the common one */
+    r->lin = (r->dst_incr % r->src_incr) != 0;
+    r->inv = 1.0f / (float)r->src_incr;
+    r->bank = (float *)malloc(sizeof(float) * (size_t)(r->pc + 1) * SWR_TAPS);
+    orc_swr_bank(in_rate, out_rate, r->bank);
+    float *ex = r->bank + (size_t)r->pc * SWR_TAPS, *r0 = r->bank;
+    for (int i = 0; i < SWR_TAPS; i++) ex[i] = r0[(i + SWR_TAPS - 1) % SWR_TAPS];
+    return 0;
+}
+
+/* output frames [j0, j1) of the 192 kHz stream, interleaved doubles.  Output j sits at
+ * phase position p = j dst_incr / src_incr (units of 1/pc input sample; exact in
+ * int64): base = floor(p) / pc, phase floor(p) % pc, frac = the remainder */
+static void swr_block(const int16_t *x, int64_t n, int channels, const Swr *r,
                       int64_t j0, int64_t j1, double *out) {
     float w[SWR_TAPS];
     for (int64_t j = j0; j < j1; j++) {
-        const int64_t idx = j * M, base = idx / L;
-        const int ph = (int)(idx % L);
+        const int64_t pos = j * r->dst_incr, idx = pos / r->src_incr, frac = pos % r->src_incr;
+        const int64_t base = idx / r->pc;
+        const int ph = (int)(idx % r->pc);
+        const float wf = (float)frac * r->inv;
         for (int c = 0; c < channels; c++) {
             for (int i = 0; i < SWR_TAPS; i++)
                 w[i] = (float)x[swr_reflect(base - SWR_CENTER + i, n) * channels + c] * (1.0f / 32768.0f);
-            out[(j - j0) * channels + c] = (double)swr_dot(w, bank + (size_t)ph * SWR_TAPS);
+            const float *h = r->bank + (size_t)ph * SWR_TAPS;
+            out[(j - j0) * channels + c] = (double)(r->lin ? swr_dot_lin(w, h, h + SWR_TAPS, wf) : swr_dot(w, h));
         }
     }
+}
+
+/* per-output tables of one period of L outputs (M input frames), for the GPU plan's
+ * checks: base frame, phase row and interpolation weight of output n */
+EXPORT int orc_swr_table(int in_rate, int out_rate, int32_t *obase, int32_t *oph, float *owt) {
+    Swr r;
+    if (swr_open(&r, in_rate, out_rate)) return -1;
+    for (int64_t n = 0; n < r.L; n++) {
+        const int64_t pos = n * r.dst_incr, idx = pos / r.src_incr, frac = pos % r.src_incr;
+        obase[n] = (int32_t)(idx / r.pc);
+        oph[n] = (int32_t)(idx % r.pc);
+        owt[n] = (float)frac * r.inv;
+    }
+    free(r.bank);
+    return r.lin;
 }
 
 /* the upsampled stream itself (tests: small inputs) */
 EXPORT int orc_upsample(const int16_t *x, int64_t n, int channels, int in_rate, int out_rate,
                         double *out) {
-    int L, M;
-    if (orc_swr_geometry(in_rate, out_rate, &L, &M)) return -1;
-    float *bank = (float *)malloc(sizeof(float) * (size_t)L * SWR_TAPS);
-    orc_swr_bank(in_rate, out_rate, bank);
-    swr_block(x, n, channels, L, M, bank, 0, orc_swr_out_frames(n, in_rate, out_rate), out);
-    free(bank);
+    Swr r;
+    if (swr_open(&r, in_rate, out_rate)) return -1;
+    swr_block(x, n, channels, &r, 0, orc_swr_out_frames(n, in_rate, out_rate), out);
+    free(r.bank);
     return 0;
 }
 
@@ -654,10 +747,8 @@ EXPORT int orc_upsample(const int16_t *x, int64_t n, int channels, int in_rate, 
 EXPORT int orc_ebur128_192k(const int16_t *x, int64_t n, int fs, int channels,
                             uint64_t *hist, uint64_t *st_hist, double *peak, int64_t *n_blocks) {
     const int out_rate = 192000;
-    int L, M;
-    if (orc_swr_geometry(fs, out_rate, &L, &M)) return -1;
-    float *bank = (float *)malloc(sizeof(float) * (size_t)L * SWR_TAPS);
-    orc_swr_bank(fs, out_rate, bank);
+    Swr r;
+    if (swr_open(&r, fs, out_rate)) return -1;
     const int64_t n_out = n > 0 ? orc_swr_out_frames(n, fs, out_rate) : 0;
     const int64_t first = (int64_t)out_rate * 3, step = (int64_t)out_rate / 10;
     double *buf = (double *)malloc(sizeof(double) * (size_t)first * channels);
@@ -665,14 +756,14 @@ EXPORT int orc_ebur128_192k(const int16_t *x, int64_t n, int fs, int channels,
     ebur_init(&e, out_rate, channels, hist, st_hist);
     for (int64_t j = 0; j < n_out;) {
         const int64_t take = (j == 0 ? first : step) < n_out - j ? (j == 0 ? first : step) : n_out - j;
-        swr_block(x, n, channels, L, M, bank, j, j + take, buf);
+        swr_block(x, n, channels, &r, j, j + take, buf);
         ebur_add(&e, buf, (size_t)take);
         j += take;
     }
     for (int c = 0; c < channels; c++) peak[c] = e.peak[c];
     *n_blocks = e.nb;
     free(buf);
-    free(bank);
+    free(r.bank);
     free(e.ring);
     return 0;
 }
@@ -1310,10 +1401,8 @@ static int ln_flush(Ln *s, double *tmp, double *dst) {
 EXPORT int64_t orc_loudnorm(const int16_t *x, int64_t n, int fs, int channels,
                             const orc_loudnorm_opts *o, int16_t *out16, double *stats) {
     const int out_rate = 192000;
-    int L, M;
-    if (orc_swr_geometry(fs, out_rate, &L, &M)) return -1;
-    float *bank = (float *)malloc(sizeof(float) * (size_t)L * SWR_TAPS);
-    orc_swr_bank(fs, out_rate, bank);
+    Swr r;
+    if (swr_open(&r, fs, out_rate)) return -1;
     const int64_t n_out = n > 0 ? orc_swr_out_frames(n, fs, out_rate) : 0;
     Ln s;
     ln_init(&s, out_rate, channels, o);
@@ -1324,7 +1413,7 @@ EXPORT int64_t orc_loudnorm(const int16_t *x, int64_t n, int fs, int channels,
     for (int64_t j = 0; j < n_out;) {
         const int64_t want = s.frame_type == LN_FIRST ? first : step;
         const int take = (int)(want < n_out - j ? want : n_out - j);
-        swr_block(x, n, channels, L, M, bank, j, j + take, in);
+        swr_block(x, n, channels, &r, j, j + take, in);
         const int m = ln_filter_frame(&s, in, take, out, 1);
         if (out16)
             for (int64_t i = 0; i < (int64_t)m * channels; i++) {
@@ -1358,7 +1447,7 @@ EXPORT int64_t orc_loudnorm(const int16_t *x, int64_t n, int fs, int channels,
     }
     free(in);
     free(out);
-    free(bank);
+    free(r.bank);
     ln_free(&s);
     return w;
 }

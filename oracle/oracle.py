@@ -294,11 +294,37 @@ def swr_geometry(fs, out_rate=192000):
     return L.value, M.value
 
 
+def swr_phases(fs, out_rate=192000):
+    """the bank's phase count: L (exact rational) or 1024 (libswresample's default)"""
+    pc = lib().orc_swr_phases(ctypes.c_int(fs), ctypes.c_int(out_rate))
+    if pc < 0:
+        raise ValueError("unsupported rate %d" % fs)
+    return pc
+
+
+def swr_incr(fs, out_rate=192000):
+    a, b = ctypes.c_int64(), ctypes.c_int64()
+    if lib().orc_swr_incr(ctypes.c_int(fs), ctypes.c_int(out_rate), ctypes.byref(a), ctypes.byref(b)):
+        raise ValueError("unsupported rate %d" % fs)
+    return a.value, b.value
+
+
 def swr_bank(fs, out_rate=192000):
-    L, _ = swr_geometry(fs, out_rate)
-    bank = np.zeros((L, 32), np.float32)
+    bank = np.zeros((swr_phases(fs, out_rate), 32), np.float32)
     lib().orc_swr_bank(ctypes.c_int(fs), ctypes.c_int(out_rate), _p(bank, _f32p))
     return bank
+
+
+def swr_table(fs, out_rate=192000):
+    """one period (L outputs over M input frames) of the per-output base frame, phase
+    row and interpolation weight; lin = the linear (interpolating) kernel runs"""
+    L, _ = swr_geometry(fs, out_rate)
+    ob = np.zeros(L, np.int32)
+    ph = np.zeros(L, np.int32)
+    wt = np.zeros(L, np.float32)
+    lin = lib().orc_swr_table(ctypes.c_int(fs), ctypes.c_int(out_rate), _p(ob, ctypes.POINTER(ctypes.c_int32)),
+                              _p(ph, ctypes.POINTER(ctypes.c_int32)), _p(wt, _f32p))
+    return ob, ph, wt, bool(lin)
 
 
 def upsample(x16, fs, out_rate=192000):

@@ -105,3 +105,34 @@ def test_two_ranks_match_one(gpu, case):
     diff = np.abs(y2.astype(np.int32) - y1.astype(np.int32))
     assert diff.max() == 0, "max |diff| %d LSB at %s (limiter fast path %s)" % (
         diff.max(), np.argmax(diff.max(axis=1)), fast[0])
+
+
+@pytest.mark.parametrize("case", ["c3_lufs", "square_limiter"])
+def test_rccl_forced_exchange_world1(gpu, case):
+    """RCCL rehearsal on one GPU (RCCL refuses two ranks on one device): a one-rank
+    "nccl" process group with ShardedTrack's exchanges forced on, so the N > 1 step --
+    graph segments, the edge and tail/peak all_gather_into_tensor, the hop all_reduce,
+    the device carry kernels, the limiter on the device's decision -- runs through RCCL.
+    Eager step and graph replay must equal the bypass path bit for bit."""
+    import torch
+    import torch.distributed as dist
+    from amx.dist import ShardedTrack
+    seconds = 75.0 if case == "c3_lufs" else 32.0
+    x = _track(seconds, case)
+    d_in = torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    ref = ShardedTrack(FS, 2, CASES[case], x.shape[0], 0, 1, quantum=512)
+    y_ref = ref.step(d_in).cpu().numpy()
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _port(), rank=0, world_size=1,
+                            timeout=datetime.timedelta(seconds=60))
+    try:
+        assert dist.get_backend() == "nccl"
+        tr = ShardedTrack(FS, 2, CASES[case], x.shape[0], 0, 1, quantum=512, force_exchange=True)
+        y_eager = tr.step(d_in).cpu().numpy()
+        tr.capture(d_in)
+        assert isinstance(tr._g, list) and len(tr._g) == 4      # the N > 1 graph segments ran
+        y_graph = tr.replay().cpu().numpy()
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    np.testing.assert_array_equal(y_eager, y_ref)
+    np.testing.assert_array_equal(y_graph, y_ref)

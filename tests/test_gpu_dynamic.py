@@ -261,12 +261,14 @@ def test_filter_300s_vs_oracle(gpu, oracle_mod):
         _cmp(y, ref, "loudnorm filter 300 s %s" % ("pass 2" if measured else "pass 1"))
 
 
-@pytest.mark.parametrize("seconds,intro", [(12.0, 0.0), (2.0, 0.0), (8.0, 3.5)])
-def test_master_audio_dynamic(gpu, oracle_mod, seconds, intro):
+@pytest.mark.parametrize("seconds,intro,fs", [(12.0, 0.0, 48000), (2.0, 0.0, 48000), (8.0, 3.5, 48000),
+                                              (9.0, 0.0, 22050)])
+def test_master_audio_dynamic(gpu, oracle_mod, seconds, intro, fs):
+    """(22.05 kHz: the filter's 192 kHz input comes from libswresample's interpolating
+    1024-phase kernel, k_ln_upsample's lin form)"""
     import audio_mastering_engine as ame
     from amx import wavio
     from amx.chunking import chunk_bounds, packet_frames
-    fs = 48000
     x = _dynamic_signal(seconds, fs, 11, intro)
     settings = dict(bass_boost=1.0, lufs=-14.0)
     with tempfile.TemporaryDirectory() as dd:

@@ -442,12 +442,14 @@ def test_front1_variants_vs_oracle(gpu, oracle_mod, monkeypatch, env):
 
 @pytest.mark.parametrize("fs,env", [
     (44100, {}), (44100, {"AMX_UP_POLY": "0"}), (88200, {}), (176400, {}), (32000, {}), (64000, {}),
-    (24000, {}),
-], ids=["44k1-poly", "44k1-slow", "88k2-poly", "176k4-poly", "32k-poly", "64k-poly", "24k-slow"])
+    (24000, {}), (22050, {}), (11025, {}),
+], ids=["44k1-poly", "44k1-slow", "88k2-poly", "176k4-poly", "32k-poly", "64k-poly", "24k-slow",
+        "22k05-lin", "11k025-lin"])
 def test_loudness_192k_rates_vs_oracle(gpu, oracle_mod, monkeypatch, fs, env):
     """the 192 kHz measurement at the rates without the unrolled k_up: k_up_poly's forms
     (amx_loud192.hip AMX_UP_POLY_FORMS) and k_up_slow (AMX_UP_POLY = 0, and 24 kHz, whose
-    form is not built) -- histograms, 192 kHz sample peaks bit for bit, the statistics"""
+    form is not built; 22.05 / 11.025 kHz with libswresample's 1024-phase interpolating
+    kernel, swr_dot_lin) -- histograms, 192 kHz sample peaks bit for bit, the statistics"""
     import torch
     from amx import synth
     from amx.engine import MasteringJob

@@ -247,6 +247,49 @@ def test_upsampler_is_the_polyphase_fir(oracle_mod, fs):
         np.testing.assert_array_equal(u[::L], xf)
 
 
+@pytest.mark.parametrize("fs", [22050, 11025])
+def test_upsampler_inexact_rates(oracle_mod, fs):
+    """22.05 / 11.025 kHz: 192000 / gcd > 1024, so libswresample keeps phase_count 1024
+    and steps dst_incr / src_incr phases per output (resample_init); the linear kernel
+    interpolates between rows ph and ph + 1 (row 1024 = row 0 one tap later).  Checked
+    against a plain float64 restatement: (1 - w) row_ph . x + w row_ph+1 . x, with the
+    phase position of output j = j dst_incr / src_incr exactly."""
+    from amx import synth
+    L, M = oracle_mod.swr_geometry(fs)
+    pc = oracle_mod.swr_phases(fs)
+    src, dst = oracle_mod.swr_incr(fs)
+    assert L > 1024 and pc == 1024
+    # the phase step averages pc in_rate / out_rate; one period of L outputs is M frames
+    assert dst * 192000 == src * fs * pc
+    assert L * dst == M * pc * src
+    ob, ph, wt, lin = oracle_mod.swr_table(fs)
+    assert lin and ob[0] == 0 and ph[0] == 0 and wt[0] == 0.0
+    n = 2001
+    x16 = oracle_mod.quantize(synth.music_like(n, fs, 2, seed=5, peak_dbfs=-1.0))
+    u = oracle_mod.upsample(x16, fs)
+    assert u.shape[0] == -(-n * L // M)
+    bank = oracle_mod.swr_bank(fs).astype(np.float64)
+    bank = np.vstack([bank, np.roll(bank[0], 1)[None]])
+    xf = x16.astype(np.float64) / 32768.0
+    idx = lambda k: abs(k) if k < 0 else (2 * n - 1 - k if k >= n else k)
+    for j in list(range(0, 60)) + list(range(u.shape[0] // 2, u.shape[0] // 2 + 40)) + \
+            list(range(u.shape[0] - 60, u.shape[0])):
+        p = j * dst
+        i, fr = p // src, p % src
+        base, phase = i // pc, i % pc
+        w = np.array([xf[idx(base - 15 + k)] for k in range(32)])
+        wgt = fr / src
+        ref = (1 - wgt) * (bank[phase] @ w) + wgt * (bank[phase + 1] @ w)
+        np.testing.assert_allclose(u[j], ref, rtol=0, atol=3e-7)
+    # a band-limited tone comes through (interpolated phases: within ~1e-4 of full scale)
+    t = np.arange(n) / fs
+    tone = np.repeat(np.rint(np.sin(2 * np.pi * 1000.0 * t) * 16000)[:, None], 2, 1).astype(np.int16)
+    ut = oracle_mod.upsample(tone, fs)
+    tt = np.arange(ut.shape[0]) * (fs / 192000.0) / fs
+    ideal = np.sin(2 * np.pi * 1000.0 * tt) * 16000 / 32768.0
+    assert np.abs(ut[400:-400, 0] - ideal[400:-400]).max() < 2e-3
+
+
 def test_ebu3341_at_192k(oracle_mod):
     """EBU Tech 3341 case 1 through the 192 kHz measurement: -23.0 +- 0.1 LUFS; and
     feeding the upsampled stream to the native-rate meter in one call gives the
