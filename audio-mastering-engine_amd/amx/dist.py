@@ -26,7 +26,7 @@ exchange steps are the track-level ones:
 Everything before the limiter runs on the stream without a host round trip; at
 N > 1 the host reads the one-word limiter decision (identical on every rank, it is
 computed from all-reduced data) to choose between the idle path and the
-sequential rank-to-rank chain.
+sequential rank-to-rank chain -- or loudnorm's dynamic mode (ShardedTrack.dynamic).
 """
 import numpy as np
 import torch
@@ -190,14 +190,26 @@ def chain_state_speculative(state, run, is_rest, rank, world, group=None, first_
         dist.send(s, dst=rank + 1, group=group)
 
 
-def _check_linear(ctl):
-    """A chunk-sharded track finalises linear loudnorm only: the device's mode word
-    (k_decide, bits 4..7; 3 = dynamic) is read with the limiter flag each step, so a track
-    that needs dynamic mode raises instead of coming out unnormalised."""
-    if (ctl >> 4) & 15 == 3:
-        from .engine import DynamicModeUnsupported
-        raise DynamicModeUnsupported("chunk-sharded track: loudnorm takes dynamic mode; run it "
-                                     "whole (master_audio / MasteringJob.finish_dynamic)")
+def is_dynamic(ctl):
+    """the device's mode word (k_decide, bits 4..7; 3 = dynamic): loudnorm's pass 2 runs
+    the 192 kHz filter (:240 when the linear conditions fail)"""
+    return (ctl >> 4) & 15 == 3
+
+
+def gather_track(out, n, span_frames, world, group=None):
+    """every rank's span out[:n] (int16 [frames, 2]) all-gathered into the whole track
+    [sum(span_frames), 2] on every rank (spans padded to the longest: one
+    all_gather_into_tensor, one int32 word per stereo frame)"""
+    mx = max(span_frames)
+    buf = torch.zeros((mx, 2), dtype=torch.int16, device=out.device)
+    if n > 0:
+        buf[:n].copy_(out[:n])
+    (w,), st = _staged(group, buf.view(torch.int32).reshape(-1))
+    allw = torch.empty(world * mx, dtype=torch.int32, device=w.device)
+    dist.all_gather_into_tensor(allw, w, group=group)
+    allw = allw.view(world, mx)
+    whole = torch.cat([allw[q, :span_frames[q]] for q in range(world)]).view(torch.int16).reshape(-1, 2)
+    return whole.to(out.device) if st else whole
 
 
 class ShardedTrack:
@@ -317,6 +329,52 @@ class ShardedTrack:
         chain_state_speculative(job.lim_state, lambda: job.finalize(False),
                                 lambda v: is_rest_state(v, job.bs), self.rank, self.world, self.group)
 
+    # ------------------------------------------------- loudnorm dynamic mode
+    def m192(self, f):
+        """the 192 kHz stream position of chain frame f of the track (ceil(f L / M):
+        the first output whose window is centred at or after f)"""
+        import math
+        g = math.gcd(self.job.fs, 192000)
+        L, M = 192000 // g, self.job.fs // g
+        return (f * L + M - 1) // M
+
+    def dynamic_range(self, rank=None):
+        """[P0, P1): the 192 kHz output frames rank `rank` returns in dynamic mode -- the
+        outputs made from its span's chain frames, so the ranks' outputs concatenate to
+        the track's"""
+        r = self.rank if rank is None else rank
+        f0 = sum(self.span_frames[:r])
+        return self.m192(f0), self.m192(f0 + self.span_frames[r])
+
+    def dynamic(self):
+        """loudnorm's dynamic mode on the chunk-sharded track (:240 when the linear
+        conditions fail; :223's alimiter then runs on the 192 kHz stream), replicated
+        form: the spans are all-gathered, the whole track's measurement and 192 kHz path
+        run on every rank (MasteringJob.dynamic_track: both filter runs, pass 1's output
+        measurement, the alimiter), and each rank returns its share of the 192 kHz
+        output, dynamic_range().
+        Returns int16 [P1 - P0, 2]."""
+        job = self.job
+        whole = gather_track(job.out, self.span_frames[self.rank], self.span_frames, self.world, self.group)
+        W = getattr(self, "_whole", None)
+        if W is None:
+            W = MasteringJob(job.fs, 2, {"lufs": job.settings.get("lufs")}, [self.ttotal], input_s16=True,
+                             chunks=[(0, 0, self.ttotal)], device=job.device, measure_only=True)
+            self._whole = W
+        W.out[:self.ttotal].copy_(whole)
+        # the whole track's measurement again (~0.1 ms per 5 minutes): the same hop energies
+        # a one-GPU run forms (the sharded ones differ from them in the last bits of the
+        # hops beside a rank boundary, where the K filter's state came by the carry)
+        W.loudness_pass1(tail=False)
+        W.loudness_pass2(carry=False)
+        W.histograms()
+        W.decide()
+        y, info = W.dynamic_track(0)
+        p0, p1 = self.dynamic_range()
+        self.dyn_info = dict(info, form="replicated")
+        job.report.update(dynamic=self.dyn_info, sample_rate=192000)
+        return y[p0:p1]
+
     # -------------------------------------------------------------- the step
     def capture(self, d_in):
         """Record the step's device work as hipGraphs (torch.cuda.CUDAGraph over HIP
@@ -383,7 +441,8 @@ class ShardedTrack:
         self._ctl_host.copy_(job.ctl[:1], non_blocking=True)
         self._ctl_ev.record()
         self._ctl_ev.synchronize()
-        _check_linear(int(self._ctl_host[0]))
+        if is_dynamic(int(self._ctl_host[0])):
+            return self.dynamic()
         if not (int(self._ctl_host[0]) & capi.CTL_FAST):
             chain_state_speculative(job.lim_state, lambda: job.finalize(False),
                                     lambda v: is_rest_state(v, job.bs), self.rank, self.world,
@@ -408,14 +467,15 @@ class ShardedTrack:
             job.timed("hist", job.histograms)
         job.timed("decide", job.decide)
         ctl = int(job.ctl[0].item())
-        _check_linear(ctl)
+        job.report = {"chunks": len(job.chunks), "segments": job.info.n_segments}
+        if is_dynamic(ctl):
+            return self.dynamic()
         fast = bool(ctl & capi.CTL_FAST)
         if fast:
             job.timed("final", lambda: job.finalize(True))
         else:
             job.lim_state.zero_()
             self.limiter_sequential()
-        job.report = {"chunks": len(job.chunks), "segments": job.info.n_segments}
         return job.y[:job.info.out_frames]
 
 

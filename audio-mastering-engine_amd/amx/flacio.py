@@ -33,20 +33,31 @@ def is_flac(path):
     return head[o:o + 4] == b"fLaC"
 
 
+# samples per byte a FLAC stream can reach at most in practice (constant subframes of
+# the largest blocks: ~65535 samples in ~16 bytes); a STREAMINFO length beyond it is
+# not trusted for the allocation
+_MAX_SAMPLES_PER_BYTE = 4096
+
+
 def decode_flac(data, threads=0, with_blocks=False):
     """(int32 array [frames, channels] left-justified to 32 bits, FlacInfo) of FLAC bytes;
     with_blocks: also the FLAC frames' block sizes in stream order (the demuxer's packets)"""
-    data = bytes(data)
-    data = data[_skip_id3(data):]
+    # the decoder reads the caller's bytes in place (no copy): a numpy view of them
+    raw = np.frombuffer(data, np.uint8)
+    o = _skip_id3(raw[:10].tobytes())
+    size = raw.size - o
+    if size <= 0:
+        raise capi.AmxError("not a FLAC stream (empty)")
+    buf = ctypes.c_void_p(raw.ctypes.data + o)
     L = capi.load()
-    buf = ctypes.create_string_buffer(data, len(data))
     info = capi.FlacInfo()
-    rc = L.amx_flac_info(buf, len(data), ctypes.byref(info))
+    rc = L.amx_flac_info(buf, size, ctypes.byref(info))
     if rc != capi.AMX_OK:
         raise capi.AmxError("not a FLAC stream (amx_flac_info %d)" % rc)
     n = ctypes.c_int64(info.total_frames)
-    if n.value <= 0:     # STREAMINFO without the length: a size query first
-        rc = L.amx_flac_decode(buf, len(data), None, 0, ctypes.byref(n), int(threads), None, 0, None)
+    if n.value <= 0 or n.value > size * _MAX_SAMPLES_PER_BYTE:
+        # STREAMINFO without the length, or one the file cannot hold: a size query first
+        rc = L.amx_flac_decode(buf, size, None, 0, ctypes.byref(n), int(threads), None, 0, None)
         if rc != capi.AMX_OK:
             raise capi.AmxError("corrupt FLAC stream (amx_flac_decode %d)" % rc)
     out = np.empty((n.value, info.channels), np.int32)
@@ -55,7 +66,7 @@ def decode_flac(data, threads=0, with_blocks=False):
     max_blocks = n.value // 16 + 2
     blocks = np.zeros(max_blocks, np.int32)
     nb = ctypes.c_int64(0)
-    rc = L.amx_flac_decode(buf, len(data), out.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(got),
+    rc = L.amx_flac_decode(buf, size, out.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(got),
                            int(threads), blocks.ctypes.data_as(ctypes.c_void_p), max_blocks, ctypes.byref(nb))
     if rc != capi.AMX_OK or got.value != n.value:
         raise capi.AmxError("corrupt FLAC stream (amx_flac_decode %d)" % rc)

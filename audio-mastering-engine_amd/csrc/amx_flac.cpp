@@ -266,16 +266,19 @@ bool subframe(BitReader &br, int block, int bps, int64_t *s) {
         if (order > block) return false;
         for (int i = 0; i < order; i++) s[i] = br.sbits(eb);
         if (!residual(br, block, order, s)) return false;
+        // the predictors in wrapping uint64 arithmetic: a hostile stream's residuals can
+        // push them past int64 (undefined for signed); a valid stream never wraps
         for (int i = order; i < block; i++) {
-            int64_t pred = 0;
+            uint64_t pred = 0;
+            const uint64_t a = (uint64_t)s[i - 1];
             switch (order) {
-            case 1: pred = s[i - 1]; break;
-            case 2: pred = 2 * s[i - 1] - s[i - 2]; break;
-            case 3: pred = 3 * s[i - 1] - 3 * s[i - 2] + s[i - 3]; break;
-            case 4: pred = 4 * s[i - 1] - 6 * s[i - 2] + 4 * s[i - 3] - s[i - 4]; break;
+            case 1: pred = a; break;
+            case 2: pred = 2 * a - (uint64_t)s[i - 2]; break;
+            case 3: pred = 3 * a - 3 * (uint64_t)s[i - 2] + (uint64_t)s[i - 3]; break;
+            case 4: pred = 4 * a - 6 * (uint64_t)s[i - 2] + 4 * (uint64_t)s[i - 3] - (uint64_t)s[i - 4]; break;
             default: break;
             }
-            s[i] += pred;
+            s[i] = (int64_t)((uint64_t)s[i] + pred);
         }
     } else if (type >= 32) {
         const int order = type - 31;
@@ -289,9 +292,9 @@ bool subframe(BitReader &br, int block, int bps, int64_t *s) {
         for (int i = 0; i < order; i++) c[i] = br.sbits(prec);
         if (!residual(br, block, order, s)) return false;
         for (int i = order; i < block; i++) {
-            int64_t acc = 0;
-            for (int k = 0; k < order; k++) acc += c[k] * s[i - 1 - k];
-            s[i] += acc >> shift;
+            uint64_t acc = 0;                           // wrapping, as above
+            for (int k = 0; k < order; k++) acc += (uint64_t)c[k] * (uint64_t)s[i - 1 - k];
+            s[i] = (int64_t)((uint64_t)s[i] + (uint64_t)((int64_t)acc >> shift));
         }
     } else {
         return false;

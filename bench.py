@@ -120,6 +120,11 @@ PER_STEP = {"k_envfix": 2}
 PIPELINE_PREFIX = "k_"
 
 
+def synth_generator(frames, fs):
+    """the generator synth_input uses for this length (named in the bench line's data)"""
+    return "amx.synth.mix_tiled(block_seconds=60)" if frames > 600 * fs else "amx.synth.mix_like"
+
+
 def synth_input(frames, fs, seed):
     """the seeded synthetic program; inputs longer than 10 minutes repeat a 60 s block
     (amx.synth.mix_tiled: mix_like costs ~1 s of host time per 20 s of audio)"""
@@ -188,6 +193,7 @@ def other_configs(args):
         samples = sum(runner.span_frames) * 2
         rep = runner.job.fetch_report()
         out[cfg] = {"workload": WORKLOAD[cfg], "ms_per_step": round(ms, 4), "steps": steps,
+                    "data": synth_generator(per_track, fs),
                     "value": round(samples / (ms / 1e3) / 1e6, 3), "unit": "Msamples/s",
                     "chain_frac": round(CHAIN_BYTES * samples / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                     "loudnorm_mode": rep.get("modes"), "limiter_fast": rep.get("limiter_fast")}
@@ -437,7 +443,8 @@ def main():
         "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (amx.synth.mix_like, seeded per rank / track)",
+        "data": "synthetic (%s, seeded per rank / track)" % synth_generator(
+            per_track if batch else runner.local_frames, fs),
         "config": {"workload": (WORKLOAD_STRONG.get(args.config, WORKLOAD[args.config]) if args.strong
                                 else WORKLOAD[args.config]), "sample_rate": fs,
                    "settings": args.config, "seconds_per_track": args.seconds,

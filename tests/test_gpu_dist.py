@@ -29,13 +29,16 @@ CASES = {
     # outputs), so its resampler segments run with a non-zero phase pattern (k_up_poly)
     "c3_lufs_44k1": dict(bass_boost=-1.0, mid_cut=2.0, presence_boost=2.5, treble_boost=1.0,
                          lufs=-14.0, width=1.3, analog_character=40.0, **MB),
+    # quiet programme with sparse full-scale transients: TP + offset > -1.5 dBTP, so
+    # loudnorm's pass 2 takes dynamic mode and the output is the 192 kHz stream
+    "dynamic": dict(bass_boost=1.0, lufs=-14.0),
 }
 RATE = {"c3_lufs_44k1": 44100}
 
 
 # input gain per case: the loud case drives 0.1 % of the frames over the limit, so the final
 # alimiter (limit 0.98) must engage and the ranks hand its state along
-GAIN = {"c3_lufs": 1.0, "loud_limiter": 1.3, "square_limiter": 1.0, "c3_lufs_44k1": 1.0}
+GAIN = {"c3_lufs": 1.0, "loud_limiter": 1.3, "square_limiter": 1.0, "c3_lufs_44k1": 1.0, "dynamic": 1.0}
 
 
 def _track(seconds, case):
@@ -44,6 +47,12 @@ def _track(seconds, case):
     n = int(fs * seconds)
     if case == "square_limiter":
         return synth.square(n, fs, 2, freq=110.0, amp=1.0)
+    if case == "dynamic":
+        x = synth.mix_like(n, fs, 2, seed=11) * 0.12
+        rng = np.random.default_rng(11)
+        for k in rng.integers(0, n - 200, max(2, int(seconds * 2))):
+            x[k:k + 50] += rng.uniform(-0.9, 0.9, (50, 2))
+        return np.clip(x, -1.0, 1.0).astype(np.float32)
     return (synth.mix_like(n, fs, 2, seed=3) * np.float32(GAIN[case])).astype(np.float32)
 
 
@@ -89,10 +98,17 @@ def test_two_ranks_match_one(gpu, case):
     from amx.dist import ShardedTrack
     # 3 chunks -> ranks own 2 + 1; the sequential-limiter case 2 chunks (that path walks
     # every frame in order)
-    seconds = 75.0 if case.startswith("c3_lufs") else 32.0
+    seconds = 75.0 if case.startswith("c3_lufs") or case == "dynamic" else 32.0
     x = _track(seconds, case)
-    one = ShardedTrack(RATE.get(case, FS), 2, CASES[case], x.shape[0], 0, 1, quantum=512)
-    y1 = one.step(torch.from_numpy(np.ascontiguousarray(x)).cuda()).cpu().numpy()
+    if case == "dynamic":
+        # the one-GPU reference: the whole track through master_array (dynamic_track)
+        from amx.engine import master_array
+        y1, rep = master_array(torch.from_numpy(np.ascontiguousarray(x)), FS, CASES[case], quantum=512)
+        assert rep["modes"][0] == "dynamic" and rep["sample_rate"] == 192000
+        y1 = y1.cpu().numpy()
+    else:
+        one = ShardedTrack(RATE.get(case, FS), 2, CASES[case], x.shape[0], 0, 1, quantum=512)
+        y1 = one.step(torch.from_numpy(np.ascontiguousarray(x)).cuda()).cpu().numpy()
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(2, _port(), case, seconds, d), nprocs=2, join=True)
         parts = [np.load(os.path.join(d, "y%d.npy" % r)) for r in range(2)]
@@ -100,7 +116,8 @@ def test_two_ranks_match_one(gpu, case):
     y2 = np.concatenate(parts)
     assert fast[0] == fast[1]
     # the loud case must exercise the rank-to-rank sequential limiter
-    assert fast[0] == case.startswith("c3_lufs"), "limiter fast path %s" % fast[0]
+    if case != "dynamic":
+        assert fast[0] == case.startswith("c3_lufs"), "limiter fast path %s" % fast[0]
     assert y2.shape == y1.shape
     diff = np.abs(y2.astype(np.int32) - y1.astype(np.int32))
     assert diff.max() == 0, "max |diff| %d LSB at %s (limiter fast path %s)" % (
