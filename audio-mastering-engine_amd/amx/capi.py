@@ -96,7 +96,8 @@ EXPORTS = ("amx_abi_version", "amx_last_error", "amx_build_id", "amx_plan_create
            "amx_kw_propagate", "amx_loudness_pass2", "amx_loudness_histograms",
            "amx_limiter_geometry", "amx_limiter_prepare", "amx_loudness_decide", "amx_kw_carry_setup", "amx_kw_carry",
            "amx_finalize", "amx_env_counters", "amx_pcm_to_s16", "amx_loudnorm_192k_size",
-           "amx_loudnorm_192k", "amx_loudnorm_192k_ex", "amx_flac_info", "amx_flac_decode")
+           "amx_loudnorm_192k", "amx_loudnorm_192k_ex", "amx_flac_info", "amx_flac_decode",
+           "amx_plan_set_gate")
 PCM_FORMATS = {"u8": 0, "s16": 1, "s24": 2, "s32": 3, "f32": 4, "f64": 5,
                "s8": 6, "s16be": 7, "s24be": 8, "s32be": 9, "f32be": 10, "f64be": 11}
 
@@ -129,6 +130,7 @@ def load(path=None):
     L.amx_loudness_pass1_part.argtypes = [vp, ctypes.c_int32, vp, vp, vp, vp, vp, vp]
     L.amx_pcm_to_s16.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, vp, vp]
     L.amx_env_counters.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]
+    L.amx_plan_set_gate.argtypes = [vp, vp]
     L.amx_kw_propagate.argtypes = [vp, ctypes.c_int64, c_double_p, c_double_p]
     L.amx_loudness_pass2.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int64, vp, vp]
     L.amx_loudness_histograms.argtypes = [vp, vp, ctypes.c_int64, vp, vp, vp, vp]
@@ -227,6 +229,10 @@ class Plan:
         n = len(frames_after)
         arr = (ctypes.c_int64 * max(1, n))(*[int(f) for f in frames_after])
         check(load().amx_kw_carry_setup(self.h, n, arr), "amx_kw_carry_setup")
+
+    def set_gate(self, d_word):
+        """amx_plan_set_gate: a device int32 tensor (its first word), or None"""
+        check(load().amx_plan_set_gate(self.h, ptr(d_word) if d_word is not None else None), "amx_plan_set_gate")
 
     def limiter_geometry(self, fd):
         bs, halo, sd = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()

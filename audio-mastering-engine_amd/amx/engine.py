@@ -343,6 +343,10 @@ class MasteringJob:
         step's decision was dynamic."""
         if self.dd.lufs_on and self._dyn_sides is None:
             self._dyn_sides = [self._job192(t, cached=False) for t in range(self.n_tracks)]
+            # the side plan's 192 kHz measurement passes and alimiter return at once for a
+            # track whose decision is not dynamic (ADVICE r03: a linear batch paid them)
+            for t, (_, job2, _, _) in enumerate(self._dyn_sides):
+                job2.plan.set_gate(self.ctl[t:t + 1])
 
     def dynamic_output(self, t, stream=None):
         """after a step with prepare_dynamic(): (int16 [n192, 2], info) of track t if its

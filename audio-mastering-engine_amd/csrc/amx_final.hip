@@ -638,11 +638,13 @@ __device__ void limiter_block(const LimArgs &a, int bx, int nbx, double *lim_lds
 struct FinalArgs {
     LimArgs lim;
     int fast_cols, gen_cols;
+    const int32_t *gate;      // amx_plan_set_gate (a 192 kHz side plan in a captured step)
 };
 
 template <bool UNIT>
 __global__ void __launch_bounds__(AMX_BLOCK, 8) k_final(FinalArgs fa) {
     extern __shared__ double lim_lds[];               // general columns: 3 B + 4 x 64 doubles
+    if (AMX_LN_GATED(fa.gate)) return;
     const LimArgs &a = fa.lim;
     const int t = blockIdx.y;
     const bool fast = a.ctl ? (a.ctl[t] & AMX_CTL_FAST) != 0 : a.fast != 0;
@@ -682,6 +684,7 @@ hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, co
     a.state = state; a.state_doubles = state_doubles;
     a.y = reinterpret_cast<uint32_t *>(y);
     fa.fast_cols = (ctl != nullptr || fast) ? (int)((max_span + per - 1) / per) : 0;
+    fa.gate = ls.gate;
     size_t lds = 0;
     if (general) {
         lds = limiter_lds_bytes(buffer_size);

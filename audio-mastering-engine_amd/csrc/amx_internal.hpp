@@ -189,12 +189,13 @@ hipError_t launch_gain_overlay(const DynLaunch &d, const uint16_t *m, const doub
                                const int16_t *bands, int16_t *out, int64_t max_chunk_out,
                                const int64_t *n1tab, const int *act);
 // loudness
+// gate (amx_plan_set_gate): the kernel returns at once unless the word says dynamic
 hipError_t launch_kw1(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L,
                       const int16_t *x, const double *G, double *e, uint32_t *pk,
-                      hipStream_t st);
+                      const int32_t *gate, hipStream_t st);
 hipError_t launch_kw2(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L, int hop,
                       const int16_t *x, const double *s, double *parts, int64_t *part_hop,
-                      int aligned, hipStream_t st);
+                      int aligned, const int32_t *gate, hipStream_t st);
 hipError_t launch_hops(const SpanDev *spans, int n_tracks, const KwSegDev *ks, int L, int hop,
                        const double *parts, const int64_t *part_hop, double *hops,
                        int64_t max_hops, hipStream_t st);
@@ -325,6 +326,7 @@ struct LimScratch {
     unsigned *cnt = nullptr;       // [tracks], zero between launches
     int seg_frames = 0, warm_frames = 0, max_segs = 0, buffer_size = 0;
     int64_t warm_cap = 0;          // furthest warm-up start before a segment, frames
+    const int32_t *gate = nullptr; // amx_plan_set_gate: k_final returns unless dynamic
 };
 size_t limiter_lds_bytes(int buffer_size);
 hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, const int16_t *x,

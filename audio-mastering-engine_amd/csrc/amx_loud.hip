@@ -14,7 +14,9 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_kw1(const KwSegDev *__restrict__ 
                                                    int L, const uint32_t *__restrict__ x,
                                                    const double *__restrict__ G,
                                                    double *__restrict__ e,
-                                                   uint32_t *__restrict__ pk) {
+                                                   uint32_t *__restrict__ pk,
+                                                   const int32_t *__restrict__ gate) {
+    if (AMX_LN_GATED(gate)) return;
     __shared__ uint32_t s_in[Tile<1>::WORDS];
     __shared__ int64_t rb[AMX_BLOCK];
     __shared__ int rlo[AMX_BLOCK], rhi[AMX_BLOCK];
@@ -148,7 +150,9 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_kw2(const ChainDev *__restrict__ 
                                                    const uint32_t *__restrict__ x,
                                                    const double *__restrict__ s,
                                                    double *__restrict__ parts,
-                                                   int64_t *__restrict__ part_hop) {
+                                                   int64_t *__restrict__ part_hop,
+                                                   const int32_t *__restrict__ gate) {
+    if (AMX_LN_GATED(gate)) return;
     constexpr int ROWS = AMX_BLOCK / 2;
     __shared__ uint32_t s_in[ROWS * AMX_KW2_PITCH];
     __shared__ int64_t rb[ROWS];
@@ -293,26 +297,26 @@ __global__ void __launch_bounds__(AMX_HIST_THREADS) k_hist(const SpanDev *__rest
 // ================================================================ launchers
 hipError_t launch_kw1(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L,
                       const int16_t *x, const double *G, double *e, uint32_t *pk,
-                      hipStream_t st) {
+                      const int32_t *gate, hipStream_t st) {
     (void)cd;
     if (n_kseg <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_kw1, grid1(n_kseg), dim3(AMX_BLOCK), 0, st, ks, n_kseg, L,
-                       reinterpret_cast<const uint32_t *>(x), G, e, pk);
+                       reinterpret_cast<const uint32_t *>(x), G, e, pk, gate);
     return hipGetLastError();
 }
 
 hipError_t launch_kw2(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L, int hop,
                       const int16_t *x, const double *s, double *parts, int64_t *part_hop,
-                      int aligned, hipStream_t st) {
+                      int aligned, const int32_t *gate, hipStream_t st) {
     if (n_kseg <= 0) return hipSuccess;
     if (L > AMX_KW2_TILES * AMX_TF || L % AMX_TF) return hipErrorInvalidValue;
     const dim3 grid((unsigned)((n_kseg + AMX_BLOCK / 2 - 1) / (AMX_BLOCK / 2)));
     if (aligned)
         hipLaunchKernelGGL(k_kw2<true>, grid, dim3(AMX_BLOCK), 0, st, cd, ks, n_kseg, L, hop,
-                           reinterpret_cast<const uint32_t *>(x), s, parts, part_hop);
+                           reinterpret_cast<const uint32_t *>(x), s, parts, part_hop, gate);
     else
         hipLaunchKernelGGL(k_kw2<false>, grid, dim3(AMX_BLOCK), 0, st, cd, ks, n_kseg, L, hop,
-                           reinterpret_cast<const uint32_t *>(x), s, parts, part_hop);
+                           reinterpret_cast<const uint32_t *>(x), s, parts, part_hop, gate);
     return hipGetLastError();
 }
 

@@ -146,6 +146,8 @@ struct LnShared {
     double red[LN_NW];
     double oe[30];                     // r128_out: the last 30 frames' energies
     int first[LN_NW];
+    double sbuf[1001];                 // ln_seq_sum
+    int scan[LN_NW + 1];
 };
 
 __device__ __forceinline__ int ln_find_bin(const double *B, double e) {
@@ -157,12 +159,58 @@ __device__ __forceinline__ int ln_find_bin(const double *B, double e) {
     return lo;
 }
 
+// libebur128's sum over the bins j >= lo of hist[j] * E[j], in its sequential order
+// (ebur128_gated_loudness's loop; k_decide's wave_seq_sum does the same): thread t owns
+// bins [PER t, PER t + PER), the non-empty ones are compacted in bin order into sbuf
+// (an empty bin adds 0.0, exactly) and thread 0 adds them one by one.  Every thread
+// gets the sum.  sbuf: 1000 doubles; scan: NT / 64 + 1 ints.
+template <int NT>
+__device__ double ln_seq_sum(const unsigned *hist, const double *E, int lo, double *sbuf, int *scan) {
+    constexpr int PER = (1000 + NT - 1) / NT;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int mine = 0;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int j = tid * PER + q;
+        mine += (j < 1000 && j >= lo && hist[j] != 0u) ? 1 : 0;
+    }
+    int incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int up = __shfl_up(incl, o);
+        if (lane >= o) incl += up;
+    }
+    __syncthreads();
+    if (lane == 63) scan[w] = incl;
+    __syncthreads();
+    int off = incl - mine, tot = 0;
+    for (int v = 0; v < NT / 64; v++) {
+        off += v < w ? scan[v] : 0;
+        tot += scan[v];
+    }
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int j = tid * PER + q;
+        if (j < 1000 && j >= lo && hist[j] != 0u) sbuf[off++] = (double)hist[j] * E[j];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double acc = 0.0;
+        for (int k = 0; k < tot; k++) acc += sbuf[k];
+        sbuf[1000] = acc;
+    }
+    __syncthreads();
+    const double r = sbuf[1000];
+    __syncthreads();
+    return r;
+}
+
 // ebur128 gated loudness + relative threshold of the histogram (every thread)
 __device__ void ln_global(LnShared &L, double &global, double &rel_thr) {
     const int tid = threadIdx.x;
-    double s = 0.0, c = 0.0;
-    for (int j = tid; j < 1000; j += LN_NT) { s += (double)L.hist[j] * L.E[j]; c += (double)L.hist[j]; }
-    s = ln_bsum(s, L.red);
+    double c = 0.0;
+    for (int j = tid; j < 1000; j += LN_NT) c += (double)L.hist[j];
+    const double s = ln_seq_sum<LN_NT>(L.hist, L.E, 0, L.sbuf, L.scan);
     c = ln_bsum(c, L.red);
     if (c == 0.0) {
         global = -HUGE_VAL;
@@ -178,9 +226,9 @@ __device__ void ln_global(LnShared &L, double &global, double &rel_thr) {
         start = ln_find_bin(L.B, rel);
         if (rel > L.E[start]) ++start;
     }
-    double g = 0.0, a = 0.0;
-    for (int j = start + tid; j < 1000; j += LN_NT) { g += (double)L.hist[j] * L.E[j]; a += (double)L.hist[j]; }
-    g = ln_bsum(g, L.red);
+    double a = 0.0;
+    for (int j = start + tid; j < 1000; j += LN_NT) a += (double)L.hist[j];
+    const double g = ln_seq_sum<LN_NT>(L.hist, L.E, start, L.sbuf, L.scan);
     a = ln_bsum(a, L.red);
     global = a == 0.0 ? -HUGE_VAL : 10 * log10(g / a) - 0.691;
 }
@@ -837,7 +885,8 @@ __device__ __forceinline__ double lp_shortterm(const double *hops, int64_t k, do
 // frame by frame its block, the gated loudness, the short-term loudness, the value
 __global__ void __launch_bounds__(LP_STAT_NT) k_lp_stats(LpArgs a) {
     __shared__ unsigned hist[1000];
-    __shared__ double E[1000], B[1001], red[LP_STAT_NT / 64];
+    __shared__ double E[1000], B[1001], red[LP_STAT_NT / 64], sbuf[1001];
+    __shared__ int scan[LP_STAT_NT / 64 + 1];
     const int tid = threadIdx.x;
     const double mi = a.measured_src ? a.measured_src[4] : a.measured_i;
     const double mt = a.measured_src ? a.measured_src[7] : a.measured_thresh;
@@ -885,10 +934,11 @@ __global__ void __launch_bounds__(LP_STAT_NT) k_lp_stats(LpArgs a) {
             if (en >= B[0]) hist[ln_find_bin(B, en)] += 1u;
         }
         __syncthreads();
-        // ebur128 gated loudness and relative threshold (ln_global's arithmetic)
-        double s = 0.0, c = 0.0;
-        for (int q = tid; q < 1000; q += LP_STAT_NT) { s += (double)hist[q] * E[q]; c += (double)hist[q]; }
-        s = lp_bsum(s, red);
+        // ebur128 gated loudness and relative threshold (ln_global's arithmetic: the energy
+        // sums in libebur128's sequential bin order, ln_seq_sum)
+        double c = 0.0;
+        for (int q = tid; q < 1000; q += LP_STAT_NT) c += (double)hist[q];
+        const double s = ln_seq_sum<LP_STAT_NT>(hist, E, 0, sbuf, scan);
         c = lp_bsum(c, red);
         double global = -HUGE_VAL, rel_thr = -70.0;
         if (c != 0.0) {
@@ -901,9 +951,9 @@ __global__ void __launch_bounds__(LP_STAT_NT) k_lp_stats(LpArgs a) {
                 start = ln_find_bin(B, rel);
                 if (rel > E[start]) ++start;
             }
-            double g = 0.0, ab = 0.0;
-            for (int q = start + tid; q < 1000; q += LP_STAT_NT) { g += (double)hist[q] * E[q]; ab += (double)hist[q]; }
-            g = lp_bsum(g, red);
+            double ab = 0.0;
+            for (int q = start + tid; q < 1000; q += LP_STAT_NT) ab += (double)hist[q];
+            const double g = ln_seq_sum<LP_STAT_NT>(hist, E, start, sbuf, scan);
             ab = lp_bsum(ab, red);
             global = ab == 0.0 ? -HUGE_VAL : 10 * log10(g / ab) - 0.691;
         }

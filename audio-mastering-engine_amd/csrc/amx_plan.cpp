@@ -248,6 +248,7 @@ struct amx_plan {
     // the track already is at 192 kHz (the measurement runs on d_out itself)
     int resamp = 0, upL = 1, upM = 1, upLin = 0, upLout = 0, up_static = 0, up_ok = 1;
     int meas_native = 0;    // no 192 kHz resampler for this rate: peaks only, no loudnorm
+    const int32_t *gate = nullptr;   // amx_plan_set_gate: the per-sample kernels' mode word
     // libswresample's phase count (L, or 1024 when L > 1024), phase step dst / src per
     // output; up_lin: the step is not an integer, every output interpolates between rows
     // ph and ph + 1 (bank row pc = row 0 one tap later) with weight owt[n]
@@ -1372,7 +1373,7 @@ int amx_loudness_pass1_part(amx_plan *p, int32_t part, const int16_t *d_out, con
         if (p->resamp)
             HIPCHK(amx::launch_up1(up_args(p, d_out, d_edge, d_ws), st, p->up_aux, p->up_fork, p->up_join));
         else if (!p->fuse_kw)  // else the GEMV + per-segment peaks were made by k_front2 (amx_run_chunks)
-            HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e, pk, st));
+            HIPCHK(amx::launch_kw1(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, d_out, p->d_Gkw, e, pk, p->gate, st));
         return AMX_OK;
     }
     // k_peak_reduce writes every track's peak; only tracks without a K segment (empty
@@ -1525,6 +1526,12 @@ int amx_pcm_to_s16(const void *d_raw, int64_t frames, int32_t channels, int32_t 
     return AMX_OK;
 }
 
+int amx_plan_set_gate(amx_plan *p, const int32_t *d_gate) {
+    if (!p) return fail(AMX_EINVAL, "null plan");
+    p->gate = d_gate;
+    return AMX_OK;
+}
+
 int amx_env_counters(const amx_plan *p, const void *d_ws, int32_t *out, int32_t n) {
     if (!p || !out || n < 0) return fail(AMX_EINVAL, "null argument");
     const int32_t have = AMX_ENV_MAX_ROUNDS * AMX_ENV_NCTR;
@@ -1574,7 +1581,7 @@ int amx_loudness_pass2(amx_plan *p, const int16_t *d_out, const int16_t *d_edge,
         HIPCHK(amx::launch_up2(up_args(p, d_out, d_edge, d_ws), st));
     else
         HIPCHK(amx::launch_kw2(p->d_cd, p->d_ksegs, p->n_kseg, p->Lkw, p->hop, d_out, s, parts, phop,
-                               p->kw_aligned, st));
+                               p->kw_aligned, p->gate, st));
     HIPCHK(amx::launch_hops(p->d_spans, p->n_tracks, p->d_ksegs, p->resamp ? p->upLout : p->Lkw,
                             p->hop, parts, phop, d_hops, max_hops, st));
     return AMX_OK;
@@ -1745,6 +1752,7 @@ int amx_finalize(amx_plan *p, const amx_final_desc *fd, const int16_t *d_x,
         rc = amx_limiter_prepare(p, fd, 0, -1);
         if (rc) return rc;
     }
+    p->lim.gate = p->gate;
     HIPCHK(amx::launch_final(p->d_spans, p->n_tracks, p->max_span, d_x, d_halo, halo, d_gains, d_ctl,
                              fast ? 1 : 0, p->cd.fs, fd->level_in, level, fd->level_out, fd->limit,
                              fd->release_ms / 1000.0, bs, d_lim_state, sd, p->lim, d_y, st));

@@ -231,10 +231,20 @@ AMX_API int amx_flac_decode(const uint8_t *data, int64_t size, int32_t *out, int
  * call it outside graph capture.  Replaces no reference line. */
 AMX_API int amx_env_counters(const amx_plan *plan, const void *d_ws, int32_t *out, int32_t n);
 
+/* Gate a plan's per-sample kernels on a device word: with d_gate set, the K-weighting
+ * passes (amx_loudness_pass1 / _pass2 at the plan's own rate) and amx_finalize's kernel
+ * return at once unless (*d_gate >> 4) & 15 == 3 -- the chain track's k_decide mode
+ * word says dynamic.  For the 192 kHz side plan of loudnorm's dynamic path held in a
+ * captured step (MasteringJob.prepare_dynamic): a linear track's step then skips its
+ * 192 kHz measurement passes and alimiter.  NULL removes the gate.  Replaces no
+ * reference line (the reference only runs the 192 kHz pass 2 when it is needed, :240). */
+AMX_API int amx_plan_set_gate(amx_plan *plan, const int32_t *d_gate);
+
 /* Loudness pass 1 over d_out as ffmpeg's loudnorm pass 1 measures it (:229): with no
  * measured_* values af_loudnorm runs in dynamic mode, which takes 192 kHz input, so
  * the track is measured on libswresample's 192 kHz upsampling of it (recomputed on
- * the fly, never stored; exact-rational rates only, else AMX_ERANGE) -- libebur128's
+ * the fly, never stored; libswresample's 1024-phase interpolating kernel where the
+ * phase step is not an integer, 22.05 / 11.025 kHz) -- libebur128's
  * K filter, 400 ms / 3 s blocks and sample peak at 192 kHz.
  * K-filter zero-state GEMV per segment + exact scan + sample peaks.
  * d_edge [n_tracks][2][16][2] int16: the 16 output frames before and after a span

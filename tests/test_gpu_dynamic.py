@@ -218,6 +218,40 @@ def test_graph_step_with_dynamic(gpu, oracle_mod):
     _cmp(want[1], ref, "graph step, dynamic track")
 
 
+def test_graph_step_dynamic_gate_linear_batch(gpu):
+    """capture(dynamic=True) on a batch whose tracks all stay linear: the 192 kHz side
+    plans' measurement passes and alimiter are gated on each track's decision
+    (amx_plan_set_gate), so a replay costs about what the dynamic=False graph costs
+    (ADVICE r03: ungated, every step paid two 192 kHz passes and the alimiter per track);
+    the outputs are the same bit for bit"""
+    import time
+    import torch
+    from amx import synth
+    from amx.engine import MasteringJob
+    fs = 48000
+    settings = dict(mid_cut=2.0, lufs=-14.0)
+    xs = [synth.mix_like(fs * 60, fs, 2, seed=70 + k) for k in range(2)]
+    d_in = torch.from_numpy(np.ascontiguousarray(np.concatenate(xs))).cuda()
+    n = [x.shape[0] for x in xs]
+    times, outs = {}, {}
+    for dyn in (False, True):
+        job = MasteringJob(fs, 2, settings, n, quantum=512)
+        job.capture(d_in, dynamic=dyn)
+        for _ in range(3):
+            job.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            job.replay()
+        torch.cuda.synchronize()
+        times[dyn] = (time.perf_counter() - t0) / 20
+        assert job.fetch_report(raise_dynamic=False)["modes"] == ["linear", "linear"]
+        outs[dyn] = job.y[:job.info.out_frames].cpu().numpy()
+    print("linear batch step: dynamic=False %.3f ms, dynamic=True %.3f ms" % (times[False] * 1e3, times[True] * 1e3))
+    assert np.array_equal(outs[False], outs[True])
+    assert times[True] <= 1.25 * times[False] + 0.2e-3, times
+
+
 @pytest.mark.timeout(900)
 def test_filter_300s_vs_oracle(gpu, oracle_mod):
     """a 5-minute track (the C2/C3 length) through the parallel form of dynamic mode
