@@ -119,8 +119,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_front1(const ChainDev *__restrict
 // t: 16-B column t % 8 of rows t / 8 + 32 m), issued one tile ahead; only a
 // workgroup with a partial (chunk-final) segment clamps addresses (PART).
 #define AMX_F1_PITCH (2 * AMX_TF + 2)   // dwords per LDS row: 8-B aligned, conflict-free
-// HT: lut is the odd-symmetric half table in LDS (k_front1h): tanh(s) = sign(s) lut[|s|]
-template <int D, bool AN, bool PART, bool HT = false>
+template <int D, bool AN, bool PART>
 __device__ __forceinline__ void front1s_run(const ChainDev &cd, const float *__restrict__ lut,
                                             const uint32_t *__restrict__ const *ip,
                                             const int *ilen, uint32_t *const *op,
@@ -175,14 +174,8 @@ __device__ __forceinline__ void front1s_run(const ChainDev &cd, const float *__r
                 const int f = 2 * i + half;
                 const int q0 = (int)q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f]));
                 const int q1 = (int)q_f32_to_s16_ffmpeg(__uint_as_float(rp[2 * f + 1]));
-                if constexpr (HT) {
-                    const float v0 = lut[q0 < 0 ? -q0 : q0], v1 = lut[q1 < 0 ? -q1 : q1];
-                    t0[i] = q0 < 0 ? -v0 : v0;
-                    t1[i] = q1 < 0 ? -v1 : v1;
-                } else {
-                    t0[i] = lut[q0 + 32768];
-                    t1[i] = lut[q1 + 32768];
-                }
+                t0[i] = lut[q0 + 32768];
+                t1[i] = lut[q1 + 32768];
             }
 #pragma unroll
             for (int i = 0; i < AMX_TF / 2; i++) {
@@ -288,122 +281,18 @@ __global__ void __launch_bounds__(AMX_BLOCK, 4) k_front1s(const ChainDev *__rest
                                   G, sG, eo);
 }
 
-// k_front1s<D, true> with the tanh table in LDS.  numpy's float32 tanh table is odd
-// (the plan checks every pair bit for bit, amx_plan.cpp), so its 32 769-entry half
-// (128 KB) fits the 160 KB LDS beside the tile buffers: one workgroup per CU, persistent
-// over the segment blocks, loads the half table once; a lookup is an LDS read instead of
-// a gather from the 256 KB global table through the texture path.
-template <int D>
-__global__ void __launch_bounds__(AMX_BLOCK, 1) k_front1h(const ChainDev *__restrict__ cdp,
-                                                          const ChunkDev *__restrict__ chunks,
-                                                          const SegDev *__restrict__ segs,
-                                                          int n_seg, int L,
-                                                          const uint32_t *__restrict__ in,
-                                                          const float *__restrict__ lut_half,
-                                                          uint32_t *__restrict__ a16,
-                                                          const double *__restrict__ G,
-                                                          double *__restrict__ e) {
-    constexpr int ROWS = AMX_BLOCK / 2;
-    constexpr int H = D / 2;
-    __shared__ float s_tab[AMX_HALF_LUT];
-    __shared__ uint32_t s_in[ROWS * AMX_F1_PITCH];
-    __shared__ uint32_t s_out[ROWS * (AMX_TF + 1)];
-    __shared__ __attribute__((aligned(16))) double sG[AMX_TF * (D > 0 ? D : 2)];
-    __shared__ int64_t rb_in[ROWS], rb_out[ROWS];
-    __shared__ int rl[ROWS];
-    static_assert(AMX_TF * D / 2 <= AMX_BLOCK, "one 16-B piece of the G tile per thread");
-    static_assert(D % 2 == 0, "state split in halves");
-    for (int i = threadIdx.x; i < AMX_HALF_LUT; i += AMX_BLOCK) s_tab[i] = lut_half[i];
-    const ChainDev &cd = *cdp;
-    const int t = threadIdx.x, row = t >> 1, half = t & 1;
-    const int nblk = (n_seg + ROWS - 1) / ROWS;
-    for (int b = blockIdx.x; b < nblk; b += gridDim.x) {
-        __syncthreads();                       // the previous block's rb / rl reads are done
-        const int j = b * ROWS + row;
-        const bool valid = j < n_seg;
-        const SegDev sg = segs[valid ? j : n_seg - 1];
-        const ChunkDev ch = chunks[sg.chunk];
-        const int len = valid ? sg.len : 0;
-        if (half == 0) {
-            rb_in[row] = valid ? (ch.in_off + sg.pos) * 2 : 0;
-            rb_out[row] = valid ? ch.loc_off + sg.pos : 0;
-            rl[row] = len;
-        }
-        const int part = __syncthreads_or(len < L);
-        const int c4 = t & 7, rg = t >> 3;
-        const uint32_t *ip[4];
-        int ilen[4];
-        uint32_t *op[4];
-#pragma unroll
-        for (int m = 0; m < 4; m++) {
-            ip[m] = in + rb_in[rg + 32 * m] + 4 * c4;
-            ilen[m] = rl[rg + 32 * m];
-            op[m] = a16 + rb_out[rg + 32 * m] + 2 * c4;
-        }
-        double *eo = (D > 0 && valid && !sg.last) ? e + (int64_t)j * 2 * D + half * H : nullptr;
-        if (part)
-            front1s_run<D, true, true, true>(cd, s_tab, ip, ilen, op, c4, rg, s_in, s_out, row, half, L,
-                                             len, G, sG, eo);
-        else
-            front1s_run<D, true, false, true>(cd, s_tab, ip, ilen, op, c4, rg, s_in, s_out, row, half, L,
-                                              len, G, sG, eo);
-    }
-}
-
 // ----------------------------------- analog character as its own elementwise pass
 // Float32 stereo input with the analog stage (:258-266): quantise (A.1), the tanh
 // table, the two channel-axis shelves -> the chain's s16 input a16.  Every frame is
-// independent (the shelves filter along the channel axis), so a thread takes 4 frames of
-// one chunk (two 16-B loads, one 16-B store) and the launch has a wave per 256 frames:
-// thousands of waves in flight hide the table gathers that stalled the segment kernel,
-// which did this work on 2 waves per 64 segments beside its GEMV.  The EQ GEMV then runs
-// over a16 (k_gemv16).
-__global__ void __launch_bounds__(AMX_BLOCK) k_analog(const ChainDev *__restrict__ cdp,
-                                                      const ChunkDev *__restrict__ chunks,
-                                                      const float *__restrict__ in,
-                                                      const float *__restrict__ lut,
-                                                      uint32_t *__restrict__ a16) {
-    const ChainDev &cd = *cdp;
-    const ChunkDev ch = chunks[blockIdx.y];
-    const int64_t f = ((int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x) * 4;
-    if (f >= ch.n) return;
-    const float *src = in + (ch.in_off + f) * 2;
-    uint32_t *dst = a16 + ch.loc_off + f;
-    const bool full = f + 4 <= ch.n;
-    float x[8];
-    if (full && (ch.in_off & 1) == 0) {
-        const float4 u0 = *reinterpret_cast<const float4 *>(src);
-        const float4 u1 = *reinterpret_cast<const float4 *>(src + 4);
-        x[0] = u0.x; x[1] = u0.y; x[2] = u0.z; x[3] = u0.w;
-        x[4] = u1.x; x[5] = u1.y; x[6] = u1.z; x[7] = u1.w;
-    } else {
-#pragma unroll
-        for (int e = 0; e < 8; e++) x[e] = f + e / 2 < ch.n ? src[e] : 0.0f;
-    }
-    float t[8];
-#pragma unroll
-    for (int e = 0; e < 8; e++) t[e] = lut[(int)q_f32_to_s16_ffmpeg(x[e]) + 32768];
-    uint32_t o[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        int16_t l, r;
-        analog_shelves(cd, t[2 * i], t[2 * i + 1], l, r);
-        o[i] = pack2(l, r);
-    }
-    if (full && (ch.loc_off & 3) == 0) {
-        *reinterpret_cast<uint4 *>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-            if (f + i < ch.n) dst[i] = o[i];
-    }
-}
-
-// k_analog with the tanh table in LDS (measured: the global-table form is bound by the
-// L2 -> L1 traffic of its scattered table reads, 105 us at C3).  numpy's float32 tanh
-// table is odd (the plan checks every pair bit for bit), so the 32 769-entry half table
-// (128 KB) sits in the LDS of one 1024-thread workgroup per CU (4 waves per SIMD), loaded
-// once; the workgroups then stride over every chunk's 4-frame groups.
+// independent (the shelves filter along the channel axis), so the launch has a wave per
+// 256 frames: thousands of waves in flight, where the segment kernel did this work on 2
+// waves per 64 segments beside its GEMV.  The EQ GEMV then runs over a16 (k_gemv16).
+// The tanh table sits in LDS (measured: a global-table form is bound by the L2 -> L1
+// traffic of its scattered table reads, 105 us at C3; a segment kernel holding the table
+// in LDS, 150 us -- DESIGN.md §3.4).  numpy's float32 tanh table is odd (the plan checks
+// every pair bit for bit), so the 32 769-entry half table (128 KB) sits in the LDS of one
+// 1024-thread workgroup per CU (4 waves per SIMD), loaded once; the workgroups then
+// stride over every chunk's 4-frame groups.
 __device__ __forceinline__ void analog_load8(const float *src, int64_t f, int64_t n, bool vin, float (&x)[8]) {
     if (f + 4 <= n && vin) {
         const float4 u0 = *reinterpret_cast<const float4 *>(src);
@@ -416,11 +305,11 @@ __device__ __forceinline__ void analog_load8(const float *src, int64_t f, int64_
     }
 }
 
-// FLAT: the workgroups stride over the 4096-frame blocks of all chunks in one sequence
-// (block b of the job -> its chunk by a scalar walk over the chunk list, monotone per
+// The workgroups stride over the 4096-frame blocks of all chunks in one sequence (block
+// b of the job -> its chunk by a scalar walk over the chunk list, monotone per
 // workgroup), so a chunk's last, partial round of blocks does not leave most workgroups
-// idle before the next chunk starts (C3: 352 blocks per chunk over 256 workgroups)
-template <bool FLAT>
+// idle before the next chunk starts (C3: 352 blocks per chunk over 256 workgroups;
+// striding chunk by chunk measured 52.6 against 49.4 us)
 __global__ void __launch_bounds__(1024) k_analog_h(const ChainDev *__restrict__ cdp,
                                                    const ChunkDev *__restrict__ chunks, int n_chunks,
                                                    const float *__restrict__ in,
@@ -456,75 +345,50 @@ __global__ void __launch_bounds__(1024) k_analog_h(const ChainDev *__restrict__ 
                 if (ff + i < ch.n) dst[i] = o[i];
         }
     };
-    if constexpr (FLAT) {
-        constexpr int64_t BF = 1024 * 4;                   // frames per block
-        int c = 0;
-        int64_t cb0 = 0;                                    // first block of chunk c
-        ChunkDev ch = chunks[0];
-        int64_t nb = (ch.n + BF - 1) / BF;
-        auto seek = [&](int64_t b) -> bool {                // workgroup-uniform
-            while (b >= cb0 + nb) {
-                cb0 += nb;
-                if (++c >= n_chunks) return false;
-                ch = chunks[c];
-                nb = (ch.n + BF - 1) / BF;
-            }
-            return true;
-        };
-        int64_t b = blockIdx.x;
-        if (!seek(b)) return;
-        ChunkDev cc = ch;
-        int64_t f = (b - cb0) * BF + threadIdx.x * 4;
-        // two register sets: the next block's input is in flight while one is computed
-        float xa[8], xb[8];
-        analog_load8(in + (cc.in_off + f) * 2, f, cc.n, (cc.in_off & 1) == 0, xa);
-        for (;;) {
-            b += gridDim.x;
-            const bool more = seek(b);
-            const ChunkDev cn = ch;
-            const int64_t fn = (b - cb0) * BF + threadIdx.x * 4;
-            if (more) analog_load8(in + (cn.in_off + fn) * 2, fn, cn.n, (cn.in_off & 1) == 0, xb);
-            if (f < cc.n) work(cc, xa, f);
-            if (!more) break;
-            cc = cn;
-            f = fn;
-            b += gridDim.x;
-            const bool more2 = seek(b);
-            const ChunkDev cn2 = ch;
-            const int64_t fn2 = (b - cb0) * BF + threadIdx.x * 4;
-            if (more2) analog_load8(in + (cn2.in_off + fn2) * 2, fn2, cn2.n, (cn2.in_off & 1) == 0, xa);
-            if (f < cc.n) work(cc, xb, f);
-            if (!more2) break;
-            cc = cn2;
-            f = fn2;
+    constexpr int64_t BF = 1024 * 4;                   // frames per block
+    int c = 0;
+    int64_t cb0 = 0;                                    // first block of chunk c
+    ChunkDev ch = chunks[0];
+    int64_t nb = (ch.n + BF - 1) / BF;
+    auto seek = [&](int64_t b) -> bool {                // workgroup-uniform
+        while (b >= cb0 + nb) {
+            cb0 += nb;
+            if (++c >= n_chunks) return false;
+            ch = chunks[c];
+            nb = (ch.n + BF - 1) / BF;
         }
-    } else {
-        const int64_t stride = (int64_t)gridDim.x * 1024 * 4;
-        for (int c = 0; c < n_chunks; c++) {
-            const ChunkDev ch = chunks[c];
-            const bool vin = (ch.in_off & 1) == 0;
-            int64_t f = ((int64_t)blockIdx.x * 1024 + threadIdx.x) * 4;
-            if (f >= ch.n) continue;
-            // two register sets: the next group's input is in flight while one is computed
-            float xa[8], xb[8];
-            analog_load8(in + (ch.in_off + f) * 2, f, ch.n, vin, xa);
-            for (;;) {
-                int64_t fn = f + stride;
-                if (fn < ch.n) analog_load8(in + (ch.in_off + fn) * 2, fn, ch.n, vin, xb);
-                work(ch, xa, f);
-                if (fn >= ch.n) break;
-                f = fn;
-                fn = f + stride;
-                if (fn < ch.n) analog_load8(in + (ch.in_off + fn) * 2, fn, ch.n, vin, xa);
-                work(ch, xb, f);
-                if (fn >= ch.n) break;
-                f = fn;
-            }
-        }
+        return true;
+    };
+    int64_t b = blockIdx.x;
+    if (!seek(b)) return;
+    ChunkDev cc = ch;
+    int64_t f = (b - cb0) * BF + threadIdx.x * 4;
+    // two register sets: the next block's input is in flight while one is computed
+    float xa[8], xb[8];
+    analog_load8(in + (cc.in_off + f) * 2, f, cc.n, (cc.in_off & 1) == 0, xa);
+    for (;;) {
+        b += gridDim.x;
+        const bool more = seek(b);
+        const ChunkDev cn = ch;
+        const int64_t fn = (b - cb0) * BF + threadIdx.x * 4;
+        if (more) analog_load8(in + (cn.in_off + fn) * 2, fn, cn.n, (cn.in_off & 1) == 0, xb);
+        if (f < cc.n) work(cc, xa, f);
+        if (!more) break;
+        cc = cn;
+        f = fn;
+        b += gridDim.x;
+        const bool more2 = seek(b);
+        const ChunkDev cn2 = ch;
+        const int64_t fn2 = (b - cb0) * BF + threadIdx.x * 4;
+        if (more2) analog_load8(in + (cn2.in_off + fn2) * 2, fn2, cn2.n, (cn2.in_off & 1) == 0, xa);
+        if (f < cc.n) work(cc, xb, f);
+        if (!more2) break;
+        cc = cn2;
+        f = fn2;
     }
 }
 
-// EQ pass 1 over the s16 stereo chain input a16 (after k_analog): the GEMV of
+// EQ pass 1 over the s16 stereo chain input a16 (after k_analog_h): the GEMV of
 // k_front1s without the input conversion -- two threads per segment, each holding both
 // channels' accumulators for half of the D state components, G tiles through LDS.  A
 // row's 16-frame tile is 64 B: lane t loads 16-B piece t % 4 of rows t / 4 + 64 m
@@ -939,35 +803,18 @@ static hipError_t front1s_t(const Launch &l, const uint32_t *in, const float *lu
                             const double *G, double *e) {
     const int rows = AMX_BLOCK / 2;
     if constexpr (AN) {
-        if (l.f1_mode == AMX_F1_SPLIT) {
-            // analog as an elementwise pass, then the GEMV over its s16 output
-            if (l.lut_half) {
-                const int64_t quads = (l.max_chunk_n + 3) / 4;
-                const int64_t wgs = (quads * (int64_t)l.n_chunks + 1023) / 1024;
-                const dim3 gh((unsigned)(wgs < cu_count() ? (wgs > 0 ? wgs : 1) : cu_count()));
-                if (l.analog_flat)
-                    hipLaunchKernelGGL(k_analog_h<true>, gh, dim3(1024), 0, l.stream, l.cd, l.chunks, l.n_chunks,
-                                       reinterpret_cast<const float *>(in), l.lut_half, a16);
-                else
-                    hipLaunchKernelGGL(k_analog_h<false>, gh, dim3(1024), 0, l.stream, l.cd, l.chunks, l.n_chunks,
-                                       reinterpret_cast<const float *>(in), l.lut_half, a16);
-            } else {
-                const dim3 ga((unsigned)((l.max_chunk_n + 4 * AMX_BLOCK - 1) / (4 * AMX_BLOCK)),
-                              (unsigned)l.n_chunks);
-                hipLaunchKernelGGL(k_analog, ga, dim3(AMX_BLOCK), 0, l.stream, l.cd, l.chunks,
-                                   reinterpret_cast<const float *>(in), lut, a16);
-            }
+        if (l.f1_mode == AMX_F1_SPLIT && l.lut_half) {
+            // analog as an elementwise pass (the half table in LDS), then the GEMV over its
+            // s16 output; else (a tanh table that is not odd) k_front1s with the full table
+            const int64_t quads = (l.max_chunk_n + 3) / 4;
+            const int64_t wgs = (quads * (int64_t)l.n_chunks + 1023) / 1024;
+            const dim3 gh((unsigned)(wgs < cu_count() ? (wgs > 0 ? wgs : 1) : cu_count()));
+            hipLaunchKernelGGL(k_analog_h, gh, dim3(1024), 0, l.stream, l.cd, l.chunks, l.n_chunks,
+                               reinterpret_cast<const float *>(in), l.lut_half, a16);
             if constexpr (D > 0) {
                 hipLaunchKernelGGL((k_gemv16<D>), dim3((unsigned)((l.n_seg + rows - 1) / rows)), dim3(AMX_BLOCK), 0,
                                    l.stream, l.cd, l.chunks, l.segs, l.n_seg, l.L, a16, G, e);
             }
-            return hipGetLastError();
-        }
-        if (l.f1_mode == AMX_F1_HALF && l.lut_half) {
-            const int nblk = (l.n_seg + rows - 1) / rows;
-            dim3 grid((unsigned)(nblk < cu_count() ? nblk : cu_count()));
-            hipLaunchKernelGGL((k_front1h<D>), grid, dim3(AMX_BLOCK), 0, l.stream, l.cd, l.chunks, l.segs,
-                               l.n_seg, l.L, in, l.lut_half, a16, G, e);
             return hipGetLastError();
         }
     }

@@ -132,10 +132,10 @@ struct SpanDev {
 
 // ---------------------------------------------------------------- launchers
 namespace amx {
-// pass 1 for float32 stereo input with the analog stage: k_analog(_h) + k_gemv16 (default),
-// k_front1h (tanh half table in LDS), k_front1s (global table) -- AMX_F1 = 0 / 1 / 2
+// pass 1 for float32 stereo input with the analog stage: k_analog_h + k_gemv16 (the odd
+// tanh table's half in LDS; default), or k_front1s with the full table in global memory
+// (a table that is not odd; AMX_F1 = 2 forces it, for tests)
 #define AMX_F1_SPLIT 0
-#define AMX_F1_HALF 1
 #define AMX_F1_FULL 2
 struct Launch {
     const ChainDev *cd;
@@ -143,10 +143,9 @@ struct Launch {
     const SegDev *segs;
     int32_t n_chunks, n_seg, L;
     hipStream_t stream;
-    const float *lut_half = nullptr;   // odd tanh table's half (k_front1h, k_analog_h), NULL: the full table
+    const float *lut_half = nullptr;   // odd tanh table's half (k_analog_h), NULL: the full table
     int f1_mode = AMX_F1_SPLIT;        // float32 stereo + analog: which pass-1 form (amx_chain.hip)
     int64_t max_chunk_n = 0;           // frames of the longest chunk (elementwise grids)
-    int analog_flat = 1;               // k_analog_h strides over all chunks' blocks in one sequence
 };
 struct ScanPlan {
     int D, n_blk, K;

@@ -272,7 +272,6 @@ struct amx_plan {
     int Le = 1024, warm = 2304, rounds = 2;   // compressor envelope segments (amx_dyn.hip)
     int env_wg = 1, env_pin = 0, env_il = 0;  // k_env0 placement (amx_dyn.hip launch_env)
     int f1_mode = AMX_F1_SPLIT;               // pass-1 form for float32 stereo + analog
-    int analog_flat = 1;                      // k_analog_h over all chunks' blocks (AMX_ANALOG_FLAT)
     int n_es = 0;
     std::vector<SegDev> esegs;
     std::vector<int> eseg0, neseg;
@@ -311,7 +310,7 @@ struct amx_plan {
     int n_prev = 0;
     double *d_tailpow = nullptr;
     float *d_lut = nullptr;
-    float *d_lut_half = nullptr;   // the odd tanh table's half [0, 32768] (k_front1h), or NULL
+    float *d_lut_half = nullptr;   // the odd tanh table's half [0, 32768] (k_analog_h), or NULL
     unsigned int *d_pcnt = nullptr;   // k_peak_reduce's per-track block counter (self re-arming)
     int *d_ppart = nullptr;           // its per-block partial maxima
     int any_empty_span = 0;           // a span with no K segment: its peak is zeroed directly
@@ -1053,15 +1052,11 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         const uint32_t *b = reinterpret_cast<const uint32_t *>(desc->tanh_lut);
         bool odd = true;
         for (int k = 1; k < 32768 && odd; k++) odd = b[32768 - k] == (b[32768 + k] ^ 0x80000000u);
-        // (measurements: AMX_F1 = 1 runs k_front1h, 2 k_front1s; default the split form,
-        // whose k_analog_h reads the half table from LDS -- AMX_F1_LDS = 0: k_analog, the
-        // global table)
-        if (const char *ev = std::getenv("AMX_F1")) p->f1_mode = std::atoi(ev);
-        if (const char *ev = std::getenv("AMX_ANALOG_FLAT")) p->analog_flat = std::atoi(ev) != 0;
-        if (p->f1_mode == AMX_F1_HALF && !odd) p->f1_mode = AMX_F1_FULL;
-        bool half_for_split = p->f1_mode == AMX_F1_SPLIT && odd;
-        if (const char *ev = std::getenv("AMX_F1_LDS")) half_for_split = half_for_split && std::atoi(ev) != 0;
-        if (p->f1_mode == AMX_F1_HALF || half_for_split) {
+        // (tests: AMX_F1 = 2 runs the full-table form k_front1s, the path a table that is
+        // not odd takes)
+        if (const char *ev = std::getenv("AMX_F1")) p->f1_mode = std::atoi(ev) == AMX_F1_FULL ? AMX_F1_FULL : AMX_F1_SPLIT;
+        if (!odd) p->f1_mode = AMX_F1_FULL;
+        if (p->f1_mode == AMX_F1_SPLIT) {
             std::vector<float> half(32769);
             for (int k = 0; k < 32768; k++) half[k] = desc->tanh_lut[32768 + k];
             half[32768] = -desc->tanh_lut[0];
@@ -1173,7 +1168,7 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     if (p->n_seg == 0) return AMX_OK;
     hipStream_t st = (hipStream_t)stream;
     amx::Launch l{p->d_cd, p->d_chunks, p->d_segs, p->n_chunks, p->n_seg, p->L, st, p->d_lut_half,
-                  p->f1_mode, p->max_chunk_n, p->analog_flat};
+                  p->f1_mode, p->max_chunk_n};
     int16_t *a16 = wsp<int16_t>(d_ws, p->o_a16);
     double *e = wsp<double>(d_ws, p->o_e), *s = wsp<double>(d_ws, p->o_s);
     int16_t *p16 = p->mb ? wsp<int16_t>(d_ws, p->o_p16) : nullptr;
