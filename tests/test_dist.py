@@ -249,11 +249,32 @@ def test_batch_split_gloo_world2(frames):
 
 def test_sharded_track_mode_word():
     """A chunk-sharded step reads k_decide's control word (bit 0 limiter idle, bits 4..7
-    loudnorm mode): dynamic mode (3) raises rather than leaving the track unnormalised."""
-    from amx.engine import DynamicModeUnsupported
+    loudnorm mode): mode 3 sends the track to loudnorm's dynamic path
+    (ShardedTrack.dynamic) instead of the linear finalisation."""
     for mode in (0, 1, 2):
         for fast in (0, 1):
-            adist._check_linear((mode << 4) | fast)
+            assert not adist.is_dynamic((mode << 4) | fast)
     for fast in (0, 1):
-        with pytest.raises(DynamicModeUnsupported):
-            adist._check_linear((3 << 4) | fast)
+        assert adist.is_dynamic((3 << 4) | fast)
+
+
+def _gather_worker(rank, world, port, spans):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        whole = torch.arange(2 * sum(spans), dtype=torch.int32).to(torch.int16).reshape(-1, 2)
+        f0 = sum(spans[:rank])
+        out = torch.zeros((spans[rank] + 7, 2), dtype=torch.int16)    # a span buffer with a tail
+        out[:spans[rank]] = whole[f0:f0 + spans[rank]]
+        got = adist.gather_track(out, spans[rank], spans, world)
+        assert torch.equal(got, whole)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("spans", [[5, 3], [1, 9], [4, 4]])
+def test_gather_track_gloo_world2(spans):
+    """dynamic mode's span gather (ShardedTrack.dynamic): spans of different lengths are
+    padded to the longest for one all_gather_into_tensor and reassembled in rank order"""
+    mp.spawn(_gather_worker, args=(2, _free_port(), spans), nprocs=2, join=True)
