@@ -69,26 +69,27 @@ __device__ __forceinline__ float ln_dot(const float *w, const float *__restrict_
 __global__ void __launch_bounds__(AMX_BLOCK) k_ln_upsample(const uint32_t *__restrict__ x, int64_t n_in,
                                                            SwrDev r, int64_t n192, float *__restrict__ u,
                                                            const int32_t *__restrict__ gate) {
-    const int64_t j = (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x;
-    if (j >= n192 || AMX_LN_GATED(gate)) return;
-    const int64_t pos = j * r.dst, idx = pos / r.src;
-    const int64_t base = idx / r.pc;
-    const int ph = (int)(idx % r.pc);
-    float w0[LN_TAPS], w1[LN_TAPS];
+    if (AMX_LN_GATED(gate)) return;
+    for (int64_t j = (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x; j < n192; j += (int64_t)gridDim.x * AMX_BLOCK) {
+        const int64_t pos = j * r.dst, idx = pos / r.src;
+        const int64_t base = idx / r.pc;
+        const int ph = (int)(idx % r.pc);
+        float w0[LN_TAPS], w1[LN_TAPS];
 #pragma unroll
-    for (int i = 0; i < LN_TAPS; i++) {
-        const uint32_t v = x[ln_reflect(base - LN_C + i, n_in)];
-        w0[i] = (float)lo16(v) * (1.0f / 32768.0f);
-        w1[i] = (float)hi16(v) * (1.0f / 32768.0f);
-    }
-    const float *h = r.bank + (int64_t)ph * LN_TAPS;
-    if (r.lin) {
-        const float wf = (float)(pos - idx * r.src) * (1.0f / (float)r.src);
-        u[2 * j] = swr_dot_lin(w0, h, h + LN_TAPS, wf);
-        u[2 * j + 1] = swr_dot_lin(w1, h, h + LN_TAPS, wf);
-    } else {
-        u[2 * j] = ln_dot(w0, h);
-        u[2 * j + 1] = ln_dot(w1, h);
+        for (int i = 0; i < LN_TAPS; i++) {
+            const uint32_t v = x[ln_reflect(base - LN_C + i, n_in)];
+            w0[i] = (float)lo16(v) * (1.0f / 32768.0f);
+            w1[i] = (float)hi16(v) * (1.0f / 32768.0f);
+        }
+        const float *h = r.bank + (int64_t)ph * LN_TAPS;
+        if (r.lin) {
+            const float wf = (float)(pos - idx * r.src) * (1.0f / (float)r.src);
+            u[2 * j] = swr_dot_lin(w0, h, h + LN_TAPS, wf);
+            u[2 * j + 1] = swr_dot_lin(w1, h, h + LN_TAPS, wf);
+        } else {
+            u[2 * j] = ln_dot(w0, h);
+            u[2 * j + 1] = ln_dot(w1, h);
+        }
     }
 }
 
@@ -1612,7 +1613,10 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
 hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x, int64_t n_in,
                            const SwrDev &r, hipStream_t st) {
     if (ln.n192 <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ln_upsample, dim3((unsigned)((ln.n192 + AMX_BLOCK - 1) / AMX_BLOCK)), dim3(AMX_BLOCK),
+    // grid-stride over at most 8192 workgroups: a gated (linear) track's launch then
+    // dispatches a bounded number of workgroups that return at once
+    const int64_t nb = (ln.n192 + AMX_BLOCK - 1) / AMX_BLOCK;
+    hipLaunchKernelGGL(k_ln_upsample, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(AMX_BLOCK),
                        0, st, x, n_in, r, ln.n192, ln.u, lp.gate);
     hipLaunchKernelGGL(k_lp_stats, dim3(1 + (lp.T + LP_STAT_F - 1) / LP_STAT_F), dim3(LP_STAT_NT), 0, st, lp);
     hipLaunchKernelGGL(k_ln_dyn, dim3(1), dim3(LN_NT), 0, st, ln, 0);
