@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
     if (base >= ch.n) return;                          // block-uniform
     const uint32_t *x = bands + b * nloc + ch.loc_off;
     uint16_t *mo = mi + b * nloc + ch.loc_off;
-    const int64_t rowlen = (ch.n + 63) / 64 * 64;     // the chunk row (64-frame aligned)
+    const int64_t rowlen = (ch.n + 15) / 16 * 16;     // the chunk row (16-frame aligned)
     // LDS slot k holds frame base - LP + k
     const int64_t f0 = base - LP;
     const int t = threadIdx.x;
@@ -392,70 +392,40 @@ __device__ __forceinline__ double env_step3_raw(double att, double m, double inc
     return att <= m ? up : dn;
 }
 
-// the wave's 64 rows of a tile are quiet -- every r below rq, the first table index with
-// m != 0 -- so every m is 0 and every lane's state is held through the tile
-typedef unsigned short us2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ bool env_tile_quiet(const u2v (&I)[4], uint32_t rq) {
-    us2v a = __builtin_bit_cast(us2v, I[0][0]);
-    a = __builtin_elementwise_max(a, __builtin_bit_cast(us2v, I[0][1]));
-#pragma unroll
-    for (int i = 1; i < 4; i++) {
-        a = __builtin_elementwise_max(a, __builtin_bit_cast(us2v, I[i][0]));
-        a = __builtin_elementwise_max(a, __builtin_bit_cast(us2v, I[i][1]));
-    }
-    const uint32_t mx = a.x > a.y ? a.x : a.y;
-    return __ballot(mx >= rq) == 0ull;
-}
-
-// QS: quiet tiles (env_tile_quiet, wave-uniform) skip their gathers, staging and steps;
-// qf carries the flag of the tile whose m sits in G (tile q on entry, q + 2 on exit)
-template <bool RCP, bool QS>
-__device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, double (&G)[16], bool &qf,
+template <bool RCP>
+__device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, double (&G)[16],
                                           u2v (&Islot)[4], const u2v (&Inext)[4],
-                                          const uint16_t *const (&irow)[4], const double *mt,
-                                          uint32_t rq, int q,
+                                          const uint16_t *const (&irow)[4], const double *mt, int q,
                                           int ntile, int nwarm, int64_t start, int64_t end,
                                           double *ckr, double &att, double &s_spec, bool &any) {
     const int lane = threadIdx.x & 63;
-    const bool quiet = QS && qf;
     // stage tile q's m (gathered two tiles ago)
-    if (!quiet) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            double *d = sm + ((lane >> 2) + 16 * i) * AMX_ENV_MP + 4 * (lane & 3);
-            *reinterpret_cast<d2v *>(d) = d2v{G[4 * i], G[4 * i + 1]};
-            *reinterpret_cast<d2v *>(d + 2) = d2v{G[4 * i + 2], G[4 * i + 3]};
-        }
+    for (int i = 0; i < 4; i++) {
+        double *d = sm + ((lane >> 2) + 16 * i) * AMX_ENV_MP + 4 * (lane & 3);
+        *reinterpret_cast<d2v *>(d) = d2v{G[4 * i], G[4 * i + 1]};
+        *reinterpret_cast<d2v *>(d + 2) = d2v{G[4 * i + 2], G[4 * i + 3]};
     }
     __builtin_amdgcn_wave_barrier();
     {
         // this ring slot (tile q's r, gathered already) takes tile q + PF (past the
         // end: re-read, unused); then the gathers of tile q + 2
         const int qn = (q + AMX_ENV_PF < ntile ? q + AMX_ENV_PF : q) * AMX_ENV_TF;
-        bool qn2 = false;
-        if constexpr (QS) qn2 = env_tile_quiet(Inext, rq);
-        qf = qn2;
 #pragma unroll
         for (int i = 0; i < 4; i++) Islot[i] = *reinterpret_cast<const u2v *>(irow[i] + qn);
-        if (!qn2) env_gather(mt, Inext, G);
+        env_gather(mt, Inext, G);
     }
     const int64_t f0 = start + (int64_t)q * AMX_ENV_TF;
     const bool in = f0 >= 0 && f0 < end;           // whole tile in (else held)
     double mv[AMX_ENV_TF];
-    if (!quiet) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const d2v v = *reinterpret_cast<const d2v *>(sm + lane * AMX_ENV_MP + 2 * i);
-            mv[2 * i] = v.x;
-            mv[2 * i + 1] = v.y;
-        }
+    for (int i = 0; i < 8; i++) {
+        const d2v v = *reinterpret_cast<const d2v *>(sm + lane * AMX_ENV_MP + 2 * i);
+        mv[2 * i] = v.x;
+        mv[2 * i + 1] = v.y;
     }
     __builtin_amdgcn_wave_barrier();
     if (q == nwarm) s_spec = att;
-    if (quiet) {
-        if (in && q >= nwarm) ckr[f0 / AMX_ENV_TF] = att;
-        return;
-    }
     // a tile outside the chunk / segment holds the state: it is skipped rather than
     // fed zeros (the same state; no per-frame selects on the common path)
     if (in) {
@@ -488,17 +458,16 @@ __device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, double
 }
 
 // Launch: W = 1, 2 or 4 waves per workgroup (a workgroup's waves go to
-// distinct SIMDs) with enough dynamic LDS that a CU holds one workgroup, and no more
-// workgroups than CUs.  The staging (gathers, LDS) is the CU's shared path, so a step
-// costs about W times the single-wave cost; the plan picks Le so that all segments fit
-// one resident wave set, which also shrinks the warm-up share (W + Le) / Le.
-// IL (band-interleaved, W = 3): wave w of a workgroup runs band w of the same 64
-// segments, so a CU holds one wave per band; quiet tiles (QS) are skipped, and a band
-// below its threshold leaves its SIMD -- and the CU's gather path -- to the other two.
+// distinct SIMDs) of one band, with enough dynamic LDS that a CU holds one workgroup,
+// and no more workgroups than CUs.  The plan picks Le so that all segments fit one
+// resident wave set.  What caps a CU is its memory pipeline, not the step's fp64
+// arithmetic (scripts/env_mb.hip, profiles/r04_env_mb.txt): each wave-frame's m gather
+// refills L1 lines of the 256 KB table from L2 (~55 CU cycles) beside the LDS staging
+// (~45), while the step costs ~62 cycles of its own SIMD; a CU holding more waves, or
+// band-interleaved waves, does not step more frames.
 #define AMX_ENV_WG 4
-#define AMX_ENV_WGT 8                    // k_env0t: most waves per workgroup
 #define AMX_ENV_LDS_PIN (48 * 1024)      // + 36 KB static: > 80 KB, one workgroup per CU
-template <bool RCP, bool IL>
+template <bool RCP>
 __global__ void __launch_bounds__(64 * AMX_ENV_WG) k_env0(const ChainDev *__restrict__ cdp,
                                              const ChunkDev *__restrict__ chunks,
                                              const SegDev *__restrict__ es, int n_es,
@@ -510,15 +479,14 @@ __global__ void __launch_bounds__(64 * AMX_ENV_WG) k_env0(const ChainDev *__rest
                                              int Le, int *__restrict__ flags) {
     __shared__ __attribute__((aligned(16))) double sm_all[AMX_ENV_WG][64 * AMX_ENV_MP];
     const ChainDev &cd = *cdp;
-    // (the wave index as a scalar: the band's table base stays an SGPR pair under IL)
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double *sm = sm_all[wv];
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < AMX_ENV_MAX_ROUNDS) flags[threadIdx.x] = 0;
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) {
         for (int k = lane; k < AMX_ENV_MAX_ROUNDS * AMX_ENV_NCTR; k += 64) flags[AMX_ENV_MAX_ROUNDS + k] = 0;
     }
-    const int j = IL ? blockIdx.x * 64 + lane : (blockIdx.x * (blockDim.x >> 6) + wv) * 64 + lane;
-    const int b = IL ? wv : blockIdx.y;
+    const int j = (blockIdx.x * (blockDim.x >> 6) + wv) * 64 + lane;
+    const int b = blockIdx.y;
     const bool valid = j < n_es;
     const SegDev sg = es[valid ? j : n_es - 1];
     const ChunkDev ch = chunks[sg.chunk];
@@ -540,14 +508,8 @@ __global__ void __launch_bounds__(64 * AMX_ENV_WG) k_env0(const ChainDev *__rest
 #pragma unroll
         for (int i = 0; i < 4; i++) I[u][i] = *reinterpret_cast<const u2v *>(irow[i] + u * AMX_ENV_TF);
     double G[2][16];
-    const uint32_t rq = (uint32_t)cd.rq[b];
-    bool qf[2] = {false, false};
-    if constexpr (IL) {
-        qf[0] = env_tile_quiet(I[0], rq);
-        qf[1] = env_tile_quiet(I[1], rq);
-    }
-    if (!qf[0]) env_gather(mt, I[0], G[0]);
-    if (!qf[1]) env_gather(mt, I[1], G[1]);
+    env_gather(mt, I[0], G[0]);
+    env_gather(mt, I[1], G[1]);
     // the warm-up's start guess: a chunk's first frames start from 0 (exact: the
     // reference starts every chunk there); elsewhere m of the warm-up's first frame --
     // inside a compressed stretch the state sits at or near m, and trajectories meet
@@ -558,186 +520,8 @@ __global__ void __launch_bounds__(64 * AMX_ENV_WG) k_env0(const ChainDev *__rest
     for (int q0 = 0; q0 < ntile; q0 += AMX_ENV_PF) {
 #pragma unroll
         for (int u = 0; u < AMX_ENV_PF; u++)
-            env0_tile<RCP, IL>(cd, sm, G[u & 1], qf[u & 1], I[u], I[(u + 2) % AMX_ENV_PF], irow, mt, rq,
-                               q0 + u, ntile, nwarm, start, end, ckr, att, s_spec, any);
-    }
-    if (valid) {
-        sv[(int64_t)b * n_es + j] = s_spec;
-        ev[(int64_t)b * n_es + j] = att;
-        act[(int64_t)b * n_es + j] = any ? 1 : 0;
-    }
-}
-
-// ----------------------------------- round 0, row-tiled gathers (round 4)
-// The same speculation as k_env0, laid out for the CU's memory pipeline, which is what
-// capped k_env0 (scripts/env_mb.hip, profiles/r04_env_mb.txt): a CU steps no more frames
-// when it holds more waves because every wave-frame costs ~55 CU cycles of m gathers --
-// k_env0's gather instruction covers 16 segments x 4 frames, 16+ table lines -- and ~45
-// of LDS staging, while the fp64 step itself costs ~62 cycles of one SIMD only.  Here a
-// gather instruction covers RK segments x TF = 64 / RK consecutive frames: the rms index
-// changes slowly frame to frame, so the 64 lanes touch a few table lines.
-//   r: a tile of 64 segments x TF frames arrives by TF / 8 16-B loads per lane (2 tiles
-//      ahead), is staged in LDS (sr) and read back one u16 per lane per gather;
-//   m: gathered one tile ahead, written to LDS by (segment, frame) and read back by each
-//      lane as its own segment's TF values (TF / 2 ds_read_b128);
-//   quiet tiles (every r of the wave's 64 segments below rq: m = 0 everywhere, the state
-//      held) skip the staging, the gathers and the step;
-//   a workgroup's waves take the three bands in turn (wave v: band v % 3), so a CU holds
-//      waves of different bands and a quiet band's waves leave its memory pipeline to
-//      the others (C3's high band is below its threshold throughout).
-// Everything else -- the warm-up start guess, the recorded s, e, act and checkpoints,
-// and the exact operation sequence per frame -- is k_env0's.
-template <int RK>
-struct EnvTile {
-    static constexpr int TF = 64 / RK;       // frames per tile
-    static constexpr int NL = TF / 8;        // 16-B r loads per lane per tile
-    static constexpr int RPL = 64 / NL;      // segments per r load
-    static constexpr int SMP = TF + 2;       // m row pitch (doubles): 16-B aligned rows
-    static constexpr int LDS = 64 * SMP * 8 + 64 * TF * 2;   // bytes per wave
-};
-
-template <bool RCP, int RK>
-__global__ void __launch_bounds__(64 * AMX_ENV_WGT) k_env0t(const ChainDev *__restrict__ cdp,
-                                                          const ChunkDev *__restrict__ chunks,
-                                                          const SegDev *__restrict__ es, int n_es,
-                                                          const uint16_t *__restrict__ mi,
-                                                          const double *__restrict__ tabs,
-                                                          double *__restrict__ ck,
-                                                          double *__restrict__ sv, double *__restrict__ ev,
-                                                          int *__restrict__ act, int64_t nloc, int warm,
-                                                          int Le, int *__restrict__ flags, int ngroups) {
-    using T = EnvTile<RK>;
-    constexpr int TF = T::TF, NL = T::NL, RPL = T::RPL, SMP = T::SMP;
-    extern __shared__ __attribute__((aligned(16))) double env_lds[];
-    const ChainDev &cd = *cdp;
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int v = blockIdx.x * (blockDim.x >> 6) + wv;        // wave: band v % 3, group v / 3
-    if (v == 0) {
-        for (int k = lane; k < AMX_ENV_MAX_ROUNDS; k += 64) flags[k] = 0;
-        for (int k = lane; k < AMX_ENV_MAX_ROUNDS * AMX_ENV_NCTR; k += 64) flags[AMX_ENV_MAX_ROUNDS + k] = 0;
-    }
-    const int b = v % 3, grp = v / 3;
-    if (grp >= ngroups) return;                                // wave-uniform; wave barriers only
-    double *sm = env_lds + (size_t)wv * (T::LDS / 8);
-    uint16_t *sr = reinterpret_cast<uint16_t *>(sm + 64 * SMP);
-    const int j = grp * 64 + lane;
-    const bool valid = j < n_es;
-    const SegDev sg = es[valid ? j : n_es - 1];
-    const ChunkDev ch = chunks[sg.chunk];
-    const int64_t rowoff = b * nloc + ch.loc_off;
-    const int64_t start = sg.pos - warm;
-    const int64_t end = valid ? sg.pos + sg.len : sg.pos;
-    double *ckr = ck + rowoff / AMX_ENV_TF;
-    const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
-    const uint32_t rq = (uint32_t)cd.rq[b];
-    const int ntile = (warm + Le) / TF, nwarm = warm / TF;
-    // r load i of a tile: segment i RPL + lane / NL, frames 8 (lane % NL) .. + 7
-    const uint16_t *src[NL];
-#pragma unroll
-    for (int i = 0; i < NL; i++)
-        src[i] = mi + __shfl(rowoff + start, i * RPL + lane / NL) + 8 * (lane % NL);
-    u4v R[2][NL];
-#pragma unroll
-    for (int i = 0; i < NL; i++) {
-        R[0][i] = *reinterpret_cast<const u4v *>(src[i]);
-        R[1][i] = *reinterpret_cast<const u4v *>(src[i] + TF);
-    }
-    // quiet: every r of the tile (all 64 segments) below rq
-    auto quiet_of = [&](const u4v (&Rt)[NL]) -> bool {
-        us2v a = __builtin_bit_cast(us2v, Rt[0][0]);
-#pragma unroll
-        for (int i = 0; i < NL; i++)
-#pragma unroll
-            for (int e = 0; e < 4; e++) a = __builtin_elementwise_max(a, __builtin_bit_cast(us2v, Rt[i][e]));
-        const uint32_t mx = a.x > a.y ? a.x : a.y;
-        return __ballot(mx >= rq) == 0ull;
-    };
-    double G[TF];
-    // stage tile Rt's r in LDS and gather its m: instruction k covers segments
-    // k RK .. k RK + RK - 1, lane l frame l % TF of segment k RK + l / TF
-    auto stage_gather = [&](const u4v (&Rt)[NL]) {
-#pragma unroll
-        for (int i = 0; i < NL; i++)
-            *reinterpret_cast<u4v *>(sr + (i * RPL + lane / NL) * TF + 8 * (lane % NL)) = Rt[i];
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int k = 0; k < TF; k++) G[k] = mt[sr[(k * RK + lane / TF) * TF + (lane % TF)]];
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    };
-    // the warm-up's start guess (k_env0)
-    double att = 0.0, s_spec = 0.0;
-    if (cd.env_guess && start >= 0) att = mt[mi[rowoff + start]];
-    bool any = false;
-    bool qc = quiet_of(R[0]);
-    if (!qc) stage_gather(R[0]);
-    auto tile = [&](int q, int slot) {
-        // tile q's m (gathered last tile) through LDS to its segment's lane
-        double mv[TF];
-        if (!qc) {
-#pragma unroll
-            for (int k = 0; k < TF; k++) sm[(k * RK + lane / TF) * SMP + (lane % TF)] = G[k];
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int i = 0; i < TF / 2; i++) {
-                const d2v x = *reinterpret_cast<const d2v *>(sm + lane * SMP + 2 * i);
-                mv[2 * i] = x.x;
-                mv[2 * i + 1] = x.y;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-        }
-        // tile q + 1: its r is in slot ^ 1; stage + gather unless quiet; then tile q + 2's r
-        const bool qn = quiet_of(R[slot ^ 1]);
-        if (!qn) stage_gather(R[slot ^ 1]);
-        {
-            const int64_t o = (int64_t)(q + 2 < ntile ? q + 2 : q) * TF;
-#pragma unroll
-            for (int i = 0; i < NL; i++) R[slot][i] = *reinterpret_cast<const u4v *>(src[i] + o);
-        }
-        if (q == nwarm) s_spec = att;
-        const int64_t f0 = start + (int64_t)q * TF;
-        const bool in = f0 >= 0 && f0 < end;                   // whole tile in (else held)
-        if (in && q >= nwarm) {
-#pragma unroll
-            for (int h = 0; h < TF / AMX_ENV_TF; h++) {
-                // the checkpoint before frame f0 + 16 h: written before the tile's step
-                // for h = 0; the later ones inside the step below
-                if (h == 0 || qc) ckr[(f0 + AMX_ENV_TF * h) / AMX_ENV_TF] = att;
-            }
-        }
-        if (!qc && in) {
-            if (q >= nwarm) {
-                uint32_t hh = 0, ll = 0;
-#pragma unroll
-                for (int f = 0; f < TF; f++) {
-                    const unsigned long long x = (unsigned long long)__double_as_longlong(mv[f]);
-                    hh |= (uint32_t)(x >> 32);
-                    ll |= (uint32_t)x;
-                }
-                any |= ((hh & 0x7fffffffu) | ll) != 0u;
-            }
-#pragma unroll
-            for (int h = 0; h < TF / AMX_ENV_TF; h++) {
-                if (h > 0 && q >= nwarm) ckr[(f0 + AMX_ENV_TF * h) / AMX_ENV_TF] = att;
-                double iv[AMX_ENV_TF], dv[AMX_ENV_TF];
-#pragma unroll
-                for (int f = 0; f < AMX_ENV_TF; f++) {
-                    iv[f] = env_div<RCP>(mv[AMX_ENV_TF * h + f], cd.env_A, cd.env_rA);
-                    dv[f] = env_div<RCP>(mv[AMX_ENV_TF * h + f], cd.env_R, cd.env_rR);
-                }
-#pragma unroll
-                for (int f = 0; f < AMX_ENV_TF; f++)
-                    att = env_step3_raw(att, mv[AMX_ENV_TF * h + f], iv[f], dv[f]);
-            }
-        }
-        qc = qn;
-    };
-    for (int q = 0; q < ntile; q += 2) {
-        tile(q, 0);
-        tile(q + 1, 1);
+            env0_tile<RCP>(cd, sm, G[u & 1], I[u], I[(u + 2) % AMX_ENV_PF], irow, mt,
+                           q0 + u, ntile, nwarm, start, end, ckr, att, s_spec, any);
     }
     if (valid) {
         sv[(int64_t)b * n_es + j] = s_spec;
@@ -1113,33 +897,10 @@ template <bool RCP>
 static void env_launch_t(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,
                          int *act, int *prev, int *flags, int rounds, int part) {
     const dim3 gw((unsigned)((d.n_es + 63) / 64), 3);
-    if (part == 0 && d.env_rk) {
-        // k_env0t: waves v = (group v / 3, band v % 3), env_wg per workgroup, one
-        // workgroup per CU (LDS past half the CU's)
-        const int ngroups = (d.n_es + 63) / 64;
-        const int nw = d.env_wg >= 1 && d.env_wg <= AMX_ENV_WGT ? d.env_wg : 3;
-        const dim3 g0((unsigned)((3 * ngroups + nw - 1) / nw));
-        size_t lds = (size_t)nw * (d.env_rk == 4 ? EnvTile<4>::LDS : EnvTile<2>::LDS);
-        if (lds > 160 * 1024) return;
-        if (lds < 81 * 1024) lds = 81 * 1024;
-        if (d.env_rk == 4)
-            hipLaunchKernelGGL((k_env0t<RCP, 4>), g0, dim3(64 * nw), lds, d.st, d.cd, d.chunks, d.es, d.n_es, m,
-                               d.tabs, ck, sv, ev, act, d.nloc, d.warm, d.Le, flags, ngroups);
-        else
-            hipLaunchKernelGGL((k_env0t<RCP, 2>), g0, dim3(64 * nw), lds, d.st, d.cd, d.chunks, d.es, d.n_es, m,
-                               d.tabs, ck, sv, ev, act, d.nloc, d.warm, d.Le, flags, ngroups);
-        return;
-    }
     if (part == 0) {
         const int wg = d.env_wg >= 1 && d.env_wg <= AMX_ENV_WG ? d.env_wg : 1;
-        if (d.env_il) {     // band-interleaved: one wave per band of 64 segments
-            const dim3 g0((unsigned)((d.n_es + 63) / 64), 1);
-            hipLaunchKernelGGL((k_env0<RCP, true>), g0, dim3(192), d.env_pin ? AMX_ENV_LDS_PIN : 0, d.st, d.cd,
-                               d.chunks, d.es, d.n_es, m, d.tabs, ck, sv, ev, act, d.nloc, d.warm, d.Le, flags);
-            return;
-        }
         const dim3 g0((unsigned)((d.n_es + 64 * wg - 1) / (64 * wg)), 3);
-        hipLaunchKernelGGL((k_env0<RCP, false>), g0, dim3(64 * wg), d.env_pin ? AMX_ENV_LDS_PIN : 0, d.st, d.cd,
+        hipLaunchKernelGGL((k_env0<RCP>), g0, dim3(64 * wg), d.env_pin ? AMX_ENV_LDS_PIN : 0, d.st, d.cd,
                            d.chunks, d.es, d.n_es, m, d.tabs, ck, sv, ev, act, d.nloc, d.warm, d.Le, flags);
         return;
     }

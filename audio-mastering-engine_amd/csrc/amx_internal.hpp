@@ -174,8 +174,6 @@ struct DynLaunch {
     const double *tabs;
     hipStream_t st;
     int env_wg, env_pin;         // k_env0: waves per workgroup, one workgroup per CU
-    int env_il;                  // k_env0: band-interleaved workgroups (3 waves, one per band)
-    int env_rk;                  // k_env0t (row-tiled gathers): segments per gather (2 / 4), 0: k_env0
 };
 hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m);
 // input decode: PCM of any supported format -> stereo s16 frames (amx_io.hip)

@@ -270,8 +270,7 @@ struct amx_plan {
     int lev_eq = 0, lev_x = 0, lev_kw = 0;
     int mb = 0;
     int Le = 1024, warm = 2304, rounds = 2;   // compressor envelope segments (amx_dyn.hip)
-    int env_wg = 1, env_pin = 0, env_il = 0;  // k_env0 placement (amx_dyn.hip launch_env)
-    int env_rk = 0;                           // k_env0t's gather rows (AMX_ENV_RK), 0: k_env0
+    int env_wg = 1, env_pin = 0;              // k_env0 placement (amx_dyn.hip launch_env)
     int f1_mode = AMX_F1_SPLIT;               // pass-1 form for float32 stereo + analog
     int n_es = 0;
     std::vector<SegDev> esegs;
@@ -659,45 +658,16 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         if (const char *ev = std::getenv("AMX_ENV_WG")) wg = std::atoi(ev);
         int64_t le_min = 1024;                                   // (measurements: AMX_ENV_LEMIN)
         if (const char *ev = std::getenv("AMX_ENV_LEMIN")) le_min = std::max(128, std::atoi(ev)) / 128 * 128;
-        if (const char *ev = std::getenv("AMX_ENV_IL")) p->env_il = std::atoi(ev) != 0;
-        if (const char *ev = std::getenv("AMX_ENV_RK")) p->env_rk = std::atoi(ev) == 4 ? 4 : (std::atoi(ev) == 2 ? 2 : 0);
-        if (p->env_rk) {
-            // k_env0t: wg waves per workgroup of mixed bands, one workgroup per CU
-            wg = 4;
-            if (const char *ev = std::getenv("AMX_ENV_WG")) wg = std::max(1, std::min(p->env_rk == 2 ? 6 : 8, std::atoi(ev)));
-            p->env_il = 0;
-        }
-        if (wg > 0 && p->env_rk) {
-            p->env_wg = wg;
+        if (wg > 0) {
+            p->env_wg = std::min(wg, 4);
             p->env_pin = 1;
             if (!env_le) {
                 int dev = 0, ncu = 0;
                 if (hipGetDevice(&dev) != hipSuccess ||
                     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 3)
                     ncu = 256;
-                // segments per band: ncu * wg waves hold 3 bands' groups of 64
-                const int64_t fit = (int64_t)ncu * wg / 3 * 64;
-                int64_t total = 0;
-                for (int c = 0; c < n_chunks; c++) total += chunks[c].frames;
-                int64_t Le = std::max<int64_t>(le_min, (total / fit + 127) / 128 * 128);
-                for (;; Le += 128) {
-                    int64_t ne = 0;
-                    for (int c = 0; c < n_chunks; c++) ne += (chunks[c].frames + Le - 1) / Le;
-                    if (ne <= fit || Le >= (int64_t)1 << 24) break;
-                }
-                p->Le = (int)Le;
-            }
-        } else if (wg > 0) {
-            p->env_wg = p->env_il ? 3 : std::min(wg, 4);
-            p->env_pin = 1;
-            if (!env_le) {
-                int dev = 0, ncu = 0;
-                if (hipGetDevice(&dev) != hipSuccess ||
-                    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 3)
-                    ncu = 256;
-                // segments per band: W waves of one band per CU, or (W = 3, band-interleaved)
-                // one wave per band of the same 64 segments per CU
-                const int64_t fit = p->env_il ? (int64_t)ncu * 64 : (int64_t)(ncu / 3) * 64 * p->env_wg;
+                // segments per band: W waves of one band per CU
+                const int64_t fit = (int64_t)(ncu / 3) * 64 * p->env_wg;
                 int64_t total = 0;
                 for (int c = 0; c < n_chunks; c++) total += chunks[c].frames;
                 int64_t Le = std::max<int64_t>(le_min, (total / fit + 127) / 128 * 128);
@@ -764,7 +734,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         p->n1tab.push_back(n1);
         p->max_chunk_out = n2 > p->max_chunk_out ? n2 : p->max_chunk_out;
         p->max_chunk_n = ch.n > p->max_chunk_n ? ch.n : p->max_chunk_n;
-        loc += (ch.n + 63) / 64 * 64;   // chunk rows of per-frame scratch start 64-frame aligned
+        loc += (ch.n + 15) / 16 * 16;   // chunk rows of per-frame scratch start 16-frame aligned
         outo += n2;
     }
     if (loc >= ((int64_t)1 << 31) || outo >= ((int64_t)1 << 31)) {
@@ -1213,7 +1183,7 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     amx::DynLaunch dl{p->d_cd,    p->d_chunks, p->n_chunks, p->d_esegs, p->n_es,
                       p->d_eseg0, p->d_neseg,  p->nloc,     p->max_chunk_n, p->cd.look,
                       p->warm,    p->Le,       p->cd.env_rcp, p->d_tabs, st,
-                      p->env_wg,  p->env_pin,  p->env_il, p->env_rk};
+                      p->env_wg,  p->env_pin};
     switch (stage) {
     case AMX_STAGE_FRONT1:
         if (p->mono16) {

@@ -104,24 +104,6 @@ def test_compressor_fixup_paths(gpu, oracle_mod, warm, rounds, signal):
     _cmp(out, ref, "compressor warm=%d rounds=%d %s" % (warm, rounds, signal), exact_min=1.0, tol=0)
 
 
-@pytest.mark.parametrize("rk", ["2", "4"])
-@pytest.mark.parametrize("warm,rounds", [(0, 0), (64, 2), (-1, -1)])
-def test_compressor_row_tiled_speculation(gpu, oracle_mod, monkeypatch, rk, warm, rounds):
-    """k_env0t (AMX_ENV_RK = 2 / 4: row-tiled gathers, mixed-band workgroups, quiet tiles
-    skipped) in place of k_env0: the envelope is exact whatever the work split, the high
-    band of this programme is quiet (its tiles skipped), the chunks are uneven"""
-    from amx import synth
-    monkeypatch.setenv("AMX_ENV_RK", rk)
-    fs = 48000
-    n = int(fs * 9.7)
-    x16 = oracle_mod.quantize(synth.mix_like(n, fs, 2, seed=17))
-    settings = dict(C3, _env_warm=warm, _env_rounds=rounds)
-    chunks = [(0, n // 2 + 3), (n // 2 + 3, n - (n // 2 + 3))]
-    out, _ = _chunk_chain(x16, fs, settings, chunks)
-    ref = np.concatenate([oracle_mod.chunk(x16[s:s + m], fs, C3) for s, m in chunks])
-    _cmp(out, ref, "k_env0t rk=%s warm=%d rounds=%d" % (rk, warm, rounds), exact_min=1.0, tol=0)
-
-
 def test_mono_and_f32_quantise(gpu, oracle_mod):
     import torch
     from amx import synth
