@@ -196,6 +196,19 @@ def is_dynamic(ctl):
     return (ctl >> 4) & 15 == 3
 
 
+def shard_segments(K, k_fin, world):
+    """The parallel loudnorm filter's segments (amx_loudnorm_192k_segments) split over
+    the ranks for the sharded dynamic mode: contiguous [(kb, ke)], [0, k_fin) in near
+    equal runs (the first k_fin % world one longer) and the last rank also takes the
+    FINAL flush frame's segments [k_fin, K) (FINAL re-bases the ring: its walk cannot
+    cross ranks).  None when there are fewer pre-FINAL segments than ranks."""
+    if world < 1 or k_fin < world or K < k_fin:
+        return None
+    out = shard_ranges(k_fin, world)
+    out[-1] = (out[-1][0], K)
+    return out
+
+
 def gather_track(out, n, span_frames, world, group=None):
     """every rank's span out[:n] (int16 [frames, 2]) all-gathered into the whole track
     [sum(span_frames), 2] on every rank (spans padded to the longest: one
@@ -226,8 +239,13 @@ class ShardedTrack:
     """
 
     def __init__(self, sample_rate, channels_in, settings, track_frames, rank, world, *,
-                 quantum=None, input_s16=False, seg_frames=128, group=None, force_exchange=False):
+                 quantum=None, input_s16=False, seg_frames=128, group=None, force_exchange=False,
+                 dynamic=False):
         self.rank, self.world, self.group = rank, world, group
+        # dynamic: at one rank, hold loudnorm's dynamic path in the step (prepare_dynamic:
+        # gated on the device) and return the 192 kHz output when the track takes it; at
+        # N > 1 the step always handles it (dynamic())
+        self.dyn = bool(dynamic)
         # force_exchange: run the N > 1 step (graph segments, every collective, the
         # carry kernels) even at world 1 -- an RCCL rehearsal on one GPU, since RCCL
         # refuses two ranks on one device; the output must equal the bypass path's
@@ -252,18 +270,23 @@ class ShardedTrack:
                                 track_frame0=[self.tframe0], track_total=[self.ttotal],
                                 input_s16=input_s16, seg_frames=seg_frames)
         if self.xchg:
-            frames_after = [sum(self.span_frames[q + 1:rank]) for q in range(rank)]
-            self.job.plan.kw_carry_setup(frames_after)
-            dev = self.job.device
-            self.tails_all = torch.zeros((world, 2, 4), dtype=torch.float64, device=dev)
-            from . import capi
-            self.ne = capi.UP_EDGE                                  # frames after the span start
-            self.nl = max(capi.UP_EDGE, self.job.halo_frames)       # frames before the span end
-            fw = (4 * (self.ne + self.nl) + 7) // 8                 # doubles holding them
-            self._ebuf = torch.zeros(fw, dtype=torch.float64, device=dev)
-            self._eall = torch.zeros(world * fw, dtype=torch.float64, device=dev)
-            self._xbuf = torch.zeros(12, dtype=torch.float64, device=dev)
-            self._xall = torch.zeros(world * 12, dtype=torch.float64, device=dev)
+            self._setup_exchange()
+
+    def _setup_exchange(self):
+        """the K-filter carry transitions and the exchange buffers of the N > 1 step"""
+        rank, world = self.rank, self.world
+        frames_after = [sum(self.span_frames[q + 1:rank]) for q in range(rank)]
+        self.job.plan.kw_carry_setup(frames_after)
+        dev = self.job.device
+        self.tails_all = torch.zeros((world, 2, 4), dtype=torch.float64, device=dev)
+        from . import capi
+        self.ne = capi.UP_EDGE                                  # frames after the span start
+        self.nl = max(capi.UP_EDGE, self.job.halo_frames)       # frames before the span end
+        fw = (4 * (self.ne + self.nl) + 7) // 8                 # doubles holding them
+        self._ebuf = torch.zeros(fw, dtype=torch.float64, device=dev)
+        self._eall = torch.zeros(world * fw, dtype=torch.float64, device=dev)
+        self._xbuf = torch.zeros(12, dtype=torch.float64, device=dev)
+        self._xall = torch.zeros(world * 12, dtype=torch.float64, device=dev)
 
     # -------------------------------------------------------------- exchanges
     def _all_gather(self, out, inp):
@@ -346,13 +369,127 @@ class ShardedTrack:
         f0 = sum(self.span_frames[:r])
         return self.m192(f0), self.m192(f0 + self.span_frames[r])
 
-    def dynamic(self):
+    def _ln_split(self, W):
+        """the filter's segments, this rank's share and the hand-off buffers (once per
+        whole-track plan): None when the track has too few segments to split"""
+        import ctypes
+        from . import capi
+        L = capi.load()
+        K, kf, rd, co = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        capi.check(L.amx_loudnorm_192k_segments(W.plan.h, 0, None, 0, ctypes.byref(K), ctypes.byref(kf),
+                                                ctypes.byref(rd), ctypes.byref(co)), "amx_loudnorm_192k_segments")
+        starts = (ctypes.c_int64 * (K.value + 1))()
+        capi.check(L.amx_loudnorm_192k_segments(W.plan.h, 0, starts, K.value + 1, ctypes.byref(K), None, None,
+                                                None), "amx_loudnorm_192k_segments")
+        ranges = shard_segments(K.value, kf.value, self.world)
+        if ranges is None:
+            return None
+        dev = W.device
+        return {"starts": list(starts), "ranges": ranges, "ctl": co.value,
+                "rec_in": torch.zeros(rd.value, dtype=torch.float64, device=dev),
+                "rec_out": torch.zeros(rd.value, dtype=torch.float64, device=dev),
+                "flag": torch.zeros(1, dtype=torch.int32, device=dev)}
+
+    def _filter_sharded(self, W, side, desc, measured, offset_i):
+        """one dynamic-mode filter run of the track, its segments sharded over the ranks
+        (amx_loudnorm_192k_shard): part 0 (this rank's 192 kHz stream, every frame's
+        statistics), part 1 (gains, the segments [kb, ke) from guessed states), then the
+        walks in rank order: each rank receives the true limiter state at kb from
+        rank - 1 (one record), walks its boundaries and sends the state at ke on.  This
+        rank's output: job2.out[start(kb), start(ke)).
+        A quiet start or a walk that cannot go on (the frame-by-frame path: one
+        sequence over the whole track) runs the whole filter on every rank instead;
+        every rank takes the same branch (the control word comes from the same hop
+        energies; the walk's fallback is all-reduced)."""
+        import ctypes
+        from . import capi
+        n192, job2, ws2, summ = side
+        L = capi.load()
+        sp = self._split
+
+        def whole():
+            W.loudnorm_192k(0, desc, job2, ws2, summ, measured=measured, offset_i=offset_i)
+            self._forms.append("replicated")
+
+        kb, ke = sp["ranges"][self.rank]
+        rank, world = self.rank, self.world
+
+        def part(p):
+            sh = capi.LnShard(p, kb, ke, 0, -1, -1, capi.ptr(sp["rec_in"]) if rank > 0 else None,
+                              capi.ptr(sp["rec_out"]) if rank < world - 1 else None)
+            capi.check(L.amx_loudnorm_192k_shard(
+                W.plan.h, 0, ctypes.byref(desc), capi.ptr(measured), capi.ptr(offset_i), ctypes.byref(sh),
+                capi.ptr(W.out), capi.ptr(W.hops), int(W.max_hops), capi.ptr(W.peak), capi.ptr(job2.out),
+                capi.ptr(summ), capi.ptr(ws2), None), "amx_loudnorm_192k_shard")
+
+        ctl = ws2[sp["ctl"]:sp["ctl"] + 4].view(torch.int32)
+        part(0)
+        if int(ctl.item()) != 0:
+            return whole()
+        part(1)
+        if rank > 0:
+            (s,), st = _staged(self.group, sp["rec_in"])
+            dist.recv(s, src=rank - 1, group=self.group)
+            if st:
+                sp["rec_in"].copy_(s)
+        part(2)
+        if rank < world - 1:
+            (s,), _ = _staged(self.group, sp["rec_out"])
+            dist.send(s, dst=rank + 1, group=self.group)
+        flag = sp["flag"]
+        flag.copy_(ctl[0:1] == 2)
+        (f,), st = _staged(self.group, flag)
+        dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+        if int(f.item()) != 0:
+            return whole()
+        self._forms.append("sharded")
+
+    def _dynamic_sharded(self, W):
+        """_dyn_enqueue's sequence with the 192 kHz stream split over the ranks by the
+        filter's segments: filter pass 1 (sharded), the loudness of its output measured
+        from the ranks' runs (Span192: K-filter carry, hop energies all-reduced) ->
+        target_offset, filter pass 2 (sharded), its peaks (max over ranks) and the
+        alimiter over the runs (halo + state hand-off).  Returns (this rank's run of the
+        192 kHz output, info)."""
+        from . import capi, loudness
+        from .settings import LOUDNORM_LRA, LOUDNORM_TP
+        sp = self._split
+        side = W._job192(0, cached=True)
+        job2 = side[1]
+        kb, ke = sp["ranges"][self.rank]
+        starts = sp["starts"]
+        s0, s1 = starts[kb], starts[ke]
+        S = sp.get("span")
+        if S is None:
+            lens = [starts[b] - starts[a] for a, b in sp["ranges"]]
+            S = sp["span"] = Span192(lens, self.rank, self.world, self.group, W.settings.get("lufs"), W.device)
+        target = float(W.settings["lufs"])
+        d1 = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
+        self._filter_sharded(W, side, d1, None, None)
+        S.job.out[:s1 - s0].copy_(job2.out[s0:s1])
+        S.measure(True)
+        W._i_out[0:1].copy_(S.job.stats[0, 0:1])             # pass 1's output loudness
+        d2 = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
+        self._filter_sharded(W, side, d2, W.stats[0], W._i_out[0:1])
+        S.job.out[:s1 - s0].copy_(job2.out[s0:s1])
+        S.measure(False)                                     # the limiter's input bound
+        y = S.limit()
+        i_out = float(W._i_out[0].item())
+        info = {"target_offset": loudness._fmt(target - i_out), "pass1_output_i": i_out,
+                "sample_rate": 192000, "limiter_fast": S.fast}
+        return y, info
+
+    def dynamic(self, sharded=True):
         """loudnorm's dynamic mode on the chunk-sharded track (:240 when the linear
-        conditions fail; :223's alimiter then runs on the 192 kHz stream), replicated
-        form: the spans are all-gathered, the whole track's measurement and 192 kHz path
-        run on every rank (MasteringJob.dynamic_track: both filter runs, pass 1's output
-        measurement, the alimiter), and each rank returns its share of the 192 kHz
-        output, dynamic_range().
+        conditions fail; :223's alimiter then runs on the 192 kHz stream).  The spans are
+        all-gathered and every rank measures the whole track again (the filter's gains
+        come from those hop energies).  Sharded form (_dynamic_sharded): the 192 kHz
+        stream is split over the ranks by the filter's segments -- both filter runs, the
+        measurement of pass 1's output and the alimiter run on each rank's run with the
+        limiter-state records, K-filter tails, hop energies and alimiter state crossing
+        ranks; each rank returns its run, self.dyn_range.  Replicated form (a track
+        with fewer filter segments than ranks, or sharded=False): every rank runs the
+        whole 192 kHz path (MasteringJob.dynamic_track) and returns dynamic_range().
         Returns int16 [P1 - P0, 2]."""
         job = self.job
         whole = gather_track(job.out, self.span_frames[self.rank], self.span_frames, self.world, self.group)
@@ -361,6 +498,7 @@ class ShardedTrack:
             W = MasteringJob(job.fs, 2, {"lufs": job.settings.get("lufs")}, [self.ttotal], input_s16=True,
                              chunks=[(0, 0, self.ttotal)], device=job.device, measure_only=True)
             self._whole = W
+            self._split = self._ln_split(W) if self.world > 1 else None
         W.out[:self.ttotal].copy_(whole)
         # the whole track's measurement again (~0.1 ms per 5 minutes): the same hop energies
         # a one-GPU run forms (the sharded ones differ from them in the last bits of the
@@ -369,11 +507,20 @@ class ShardedTrack:
         W.loudness_pass2(carry=False)
         W.histograms()
         W.decide()
-        y, info = W.dynamic_track(0)
-        p0, p1 = self.dynamic_range()
-        self.dyn_info = dict(info, form="replicated")
+        self._forms = []
+        if sharded and self._split is not None:
+            y, info = self._dynamic_sharded(W)
+            kb, ke = self._split["ranges"][self.rank]
+            self.dyn_range = (self._split["starts"][kb], self._split["starts"][ke])
+            form = "sharded" if self._forms == ["sharded"] * 2 else "+".join(self._forms)
+        else:
+            y, info = W.dynamic_track(0)
+            self.dyn_range = self.dynamic_range()
+            y = y[self.dyn_range[0]:self.dyn_range[1]]
+            form = "replicated"
+        self.dyn_info = dict(info, form=form)
         job.report.update(dynamic=self.dyn_info, sample_rate=192000)
-        return y[p0:p1]
+        return y
 
     # -------------------------------------------------------------- the step
     def capture(self, d_in):
@@ -391,13 +538,16 @@ class ShardedTrack:
         then the host reads the decision and, only if the limiter can engage, hands
         its state rank to rank."""
         if not self.xchg:
-            return self.job.capture(d_in)
+            return self.job.capture(d_in, dynamic=self.dyn)
         job = self.job
         lufs_on = job.dd.lufs_on
 
         def seg(*fns):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # thread_local: the process group's watchdog thread polls the events of
+            # finished collectives; in the default (global) mode that poll invalidates a
+            # capture running at the same time
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 for fn in fns:
                     fn()
             return g
@@ -419,9 +569,16 @@ class ShardedTrack:
         self._ctl_ev = torch.cuda.Event()
         return self._g
 
+    def _one_rank_dynamic(self, y):
+        d = self.job.dynamic_output(0) if self.dyn else None
+        if d is None:
+            return y
+        self.dyn_info = dict(d[1], form="one rank")
+        return d[0]
+
     def replay(self):
         if not self.xchg:
-            return self.job.replay()
+            return self._one_rank_dynamic(self.job.replay())
         from . import capi
         job = self.job
         g1, g2, g3, g4 = self._g
@@ -454,7 +611,9 @@ class ShardedTrack:
         from . import capi
         job = self.job
         if not self.xchg:
-            return job.run(d_in)
+            if self.dyn:
+                job.prepare_dynamic()
+            return self._one_rank_dynamic(job.run(d_in))
         job.run_chunks(d_in)
         self.exchange_edges()
         job.timed("up", lambda: job.loudness_pass1(tail=True, part=0))
@@ -477,6 +636,54 @@ class ShardedTrack:
             job.lim_state.zero_()
             self.limiter_sequential()
         return job.y[:job.info.out_frames]
+
+
+class Span192(ShardedTrack):
+    """This rank's run of a chunk-sharded track's 192 kHz stream in loudnorm's dynamic
+    mode (ShardedTrack._dynamic_sharded): a measure-only job over the frames of its
+    filter segments with ShardedTrack's exchanges -- edges (the alimiter's halo),
+    K-filter tails + sample peaks (all-gather), hop energies (all-reduce), the
+    alimiter's state hand-off (chain_state_speculative)."""
+
+    def __init__(self, spans, rank, world, group, lufs, device):
+        self.rank, self.world, self.group = rank, world, group
+        self.xchg, self.dyn = True, False
+        self.span_frames = [int(v) for v in spans]
+        self.tframe0 = sum(self.span_frames[:rank])
+        self.ttotal = sum(self.span_frames)
+        n = self.span_frames[rank]
+        self.job = MasteringJob(192000, 2, {"lufs": lufs}, [n], input_s16=True, chunks=[(0, 0, n)],
+                                track_frame0=[self.tframe0], track_total=[self.ttotal], device=device,
+                                measure_only=True, seg_frames=1024)    # the K scan's window at 192 kHz
+        self.fast = None
+        self._setup_exchange()
+
+    def measure(self, lufs_on):
+        """the stream's loudness (lufs_on) and peaks from the runs, as ShardedTrack.step
+        measures the chain output: every rank ends with the same statistics row"""
+        job = self.job
+        self.exchange_edges()
+        job.loudness_pass1(tail=True)
+        self.exchange_carry_peaks()
+        job.dd.lufs_on = 1 if lufs_on else 0
+        if lufs_on:
+            job.loudness_pass2(carry=True)
+            reduce_loudness(job.hops, None, self.group)
+            job.histograms()
+        job.decide()
+
+    def limit(self):
+        """the alimiter (:223) over the runs: the device's decision (the same on every
+        rank) picks the idle path or the rank-to-rank state hand-off"""
+        from . import capi
+        job = self.job
+        self.fast = bool(int(job.ctl[0].item()) & capi.CTL_FAST)
+        if self.fast:
+            job.finalize(True)
+        else:
+            job.lim_state.zero_()
+            self.limiter_sequential()
+        return job.y[:self.span_frames[self.rank]]
 
 
 class ShardedBatch:

@@ -233,17 +233,17 @@ class MasteringJob:
             capi.ptr(self.out), capi.ptr(self.hops), int(self.max_hops), capi.ptr(self.peak), capi.ptr(job2.out),
             capi.ptr(summ), capi.ptr(ws2), self._s(stream)), "amx_loudnorm_192k")
 
-    def dynamic_track(self, t, stats=None, stream=None):
+    def dynamic_track(self, t, stats=None, stream=None, filt=None):
         """loudnorm's dynamic mode for track t (:240 when the linear conditions fail), as
         the reference's two ffmpeg passes run it: pass 1's filter with the measured_*
         defaults, whose output loudness gives target_offset; pass 2's filter with the
         pass-1 strings; then the alimiter (:223) at 192 kHz.  Returns (int16 [n192, 2] at
         192 kHz, info).  Every step is on the device, without a host round trip (the
         "%.2f" strings pass 2 parses are formed there); the host reads the result."""
-        run = self._dyn_enqueue(t, self._job192(t, cached=True), stream)
+        run = self._dyn_enqueue(t, self._job192(t, cached=True), stream, filt=filt)
         return self._dyn_result(run, stream)
 
-    def _dyn_enqueue(self, t, side, stream, gate=False):
+    def _dyn_enqueue(self, t, side, stream, gate=False, filt=None):
         """Both passes of the dynamic path for track t, enqueued on `stream`: pass 1's
         filter with the measured_* defaults and the 192 kHz measurement of its output
         (its integrated loudness is pass 1's target_offset); pass 2's filter with the
@@ -252,12 +252,17 @@ class MasteringJob:
         side: the 192 kHz set of _job192 (made beforehand: a plan's creation synchronises
         the device).  gate: every loudnorm kernel first checks the track's control word
         and returns unless it says dynamic (a captured step holds the path for whichever
-        tracks need it)."""
+        tracks need it).  filt(desc, measured, offset_i): the filter run in place of
+        amx_loudnorm_192k_ex (ShardedTrack's segment-sharded run)."""
         n192, job2, ws2, summ = side
+        if filt is None:
+            def filt(desc, measured, offset_i):
+                self.loudnorm_192k(t, desc, job2, ws2, summ, stream, measured=measured, offset_i=offset_i,
+                                   gate=g)
         target = float(self.settings["lufs"])
         g = self.ctl[t:t + 1] if gate else None
         d1 = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
-        self.loudnorm_192k(t, d1, job2, ws2, summ, stream, gate=g)
+        filt(d1, None, None)
         job2.loudness_pass1(stream, tail=False)
         job2.loudness_pass2(stream, carry=False)
         job2.histograms(stream)
@@ -266,8 +271,7 @@ class MasteringJob:
         with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
             self._i_out[t:t + 1].copy_(job2.stats[0, 0:1])       # pass 1's output loudness
         d2 = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
-        self.loudnorm_192k(t, d2, job2, ws2, summ, stream, measured=self.stats[t], offset_i=self._i_out[t:t + 1],
-                           gate=g)
+        filt(d2, self.stats[t], self._i_out[t:t + 1])
         job2.loudness_pass1(stream, tail=False)            # the limiter's input bound
         job2.dd.lufs_on = 0
         job2.decide(stream)
@@ -374,7 +378,8 @@ class MasteringJob:
             self.run(d_in)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local: other threads (a process group's watchdog) may query events meanwhile
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self.run(d_in)
         self._graph = g
         return g

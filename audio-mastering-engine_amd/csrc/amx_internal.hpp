@@ -296,6 +296,12 @@ struct LpArgs {
                                   // 4 offset (dB)
     int16_t *y;                   // [n][2] output
     double *summary;              // [16]
+    // a chunk-sharded track's share (amx_loudnorm_192k_shard): k_lp_seg runs the segments
+    // [kb, ke), k_lp_walk walks their boundaries from rec_in (NULL: from the track start)
+    // and leaves the true state at ke in rec_out (NULL: none); whole track: 0, K, NULL, NULL
+    int kb, ke;
+    const double *rec_in;
+    double *rec_out;
 };
 // the 192 kHz resampler's geometry (amx_plan.cpp swr_*): output j sits at phase
 // position j dst / src (units of 1 / pc input frame); lin: interpolate rows ph, ph + 1
@@ -306,6 +312,8 @@ struct SwrDev {
 };
 hipError_t launch_loudnorm(const LnArgs &a, const LpArgs &p, const uint32_t *x, int64_t n_in,
                            const SwrDev &r, hipStream_t st);
+hipError_t launch_loudnorm_shard(const LnArgs &a, const LpArgs &p, const uint32_t *x, int64_t n_in,
+                                 const SwrDev &r, int64_t u_lo, int64_t u_hi, int part, hipStream_t st);
 #define AMX_LN_GATED(g) ((g) && (((g)[0] >> 4) & 15) != 3)   // k_decide mode 3 = dynamic
 hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent_t fork, hipEvent_t join);
 int swr_geometry(int in_rate, int out_rate, int *L, int *M);   // host (amx_plan.cpp)

@@ -64,13 +64,13 @@ __device__ __forceinline__ float ln_dot(const float *w, const float *__restrict_
     return (b0 + b2) + (b1 + b3);
 }
 
-// one thread per 192 kHz frame: both channels.  Output j sits at phase position
-// j dst / src past input frame 0 (exact rates: j M / L, frac 0)
+// one thread per 192 kHz frame: both channels, frames [j0, j1).  Output j sits at phase
+// position j dst / src past input frame 0 (exact rates: j M / L, frac 0)
 __global__ void __launch_bounds__(AMX_BLOCK) k_ln_upsample(const uint32_t *__restrict__ x, int64_t n_in,
-                                                           SwrDev r, int64_t n192, float *__restrict__ u,
+                                                           SwrDev r, int64_t j0, int64_t j1, float *__restrict__ u,
                                                            const int32_t *__restrict__ gate) {
     if (AMX_LN_GATED(gate)) return;
-    for (int64_t j = (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x; j < n192; j += (int64_t)gridDim.x * AMX_BLOCK) {
+    for (int64_t j = j0 + (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x; j < j1; j += (int64_t)gridDim.x * AMX_BLOCK) {
         const int64_t pos = j * r.dst, idx = pos / r.src;
         const int64_t base = idx / r.pc;
         const int ph = (int)(idx % r.pc);
@@ -1482,7 +1482,7 @@ __global__ void __launch_bounds__(64) k_lp_seg(LpArgs a) {
     LpWave W;
     lp_wave_init(a, W, reinterpret_cast<double2 *>(a.rings) + (int64_t)blockIdx.x * LP_RS, flags, st);
     const int NF = a.T + 1 + LP_NFIN;
-    for (int k = blockIdx.x; k < a.K; k += gridDim.x) {
+    for (int k = a.kb + blockIdx.x; k < a.ke; k += gridDim.x) {
         if (k < kh) continue;
         const int ak = lp_seg_start(a, k), bk = k + 1 < a.K ? lp_seg_start(a, k + 1) : NF;
         if (k == kh && kh > 0) {
@@ -1522,6 +1522,9 @@ __global__ void __launch_bounds__(64) k_lp_seg(LpArgs a) {
 // active where FINAL re-bases the ring, FINAL runs here from that state.  A true state
 // with a multiplied slot outside its window (never expected) hands the whole track
 // to k_ln_dyn (ctl[0] = 2).
+// A shard (a.rec_in, chunk-sharded tracks): the walk covers the boundaries [kb, ke) from
+// the true state at kb that the previous rank's walker made, and leaves the true state at
+// ke in a.rec_out for the next rank (marked dirty when this walk fell back).
 __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
     if (a.ctl[0] != 0 && a.ctl[0] != 4) return;
     const int kh = a.ctl[0] == 4 ? a.ctl[4] : 0;
@@ -1530,16 +1533,16 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
     LpWave W;
     lp_wave_init(a, W, reinterpret_cast<double2 *>(a.wring), flags, st);
     const int lane = threadIdx.x;
-    const int NF = a.T + 1 + LP_NFIN, kS0 = a.J + 1;
-    const double *cur = a.recE + (int64_t)kh * LP_REC;
-    bool k4 = true;
+    const int NF = a.T + 1 + LP_NFIN, kS0 = a.J + 1, ke = a.ke;
+    const double *cur = a.rec_in ? a.rec_in : a.recE + (int64_t)kh * LP_REC;
+    bool k4 = a.rec_in == nullptr;
     int toggle = 0, reruns = 0, fin = 0, fallback = 0;
-    int k = kh + 1;
-    while (k < a.K) {
+    int k = a.rec_in ? a.kb : kh + 1;
+    while (k < ke) {
         if (k4) {
-            while (k < a.K) {
+            while (k < ke) {
                 const int j = k + lane;
-                const bool stop = j >= a.K || j == kS0 || a.match[j] == 0;
+                const bool stop = j >= ke || j == kS0 || a.match[j] == 0;
                 const unsigned long long m = __ballot(stop);
                 if (m) {
                     k += __ffsll((long long)m) - 1;
@@ -1547,8 +1550,8 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
                 }
                 k += 64;
             }
-            if (k >= a.K) break;
             cur = a.recE + (int64_t)(k - 1) * LP_REC;
+            if (k >= ke) break;
         }
         if (cur[LP_DIRTY] != 0.0) {
             fallback = 1;
@@ -1595,6 +1598,12 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
         }
         k++;
     }
+    if (a.rec_out && ke < a.K) {
+        // the true state at boundary ke for the next rank's walk
+        for (int q = lane; q < LP_REC; q += 64) a.rec_out[q] = cur[q];
+        __syncthreads();
+        if (lane == 0 && fallback) a.rec_out[LP_DIRTY] = 1.0;
+    }
     if (lane == 0) {
         if (fallback) a.ctl[0] = 2;
         a.ctl[1] = reruns;
@@ -1617,7 +1626,7 @@ hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x
     // dispatches a bounded number of workgroups that return at once
     const int64_t nb = (ln.n192 + AMX_BLOCK - 1) / AMX_BLOCK;
     hipLaunchKernelGGL(k_ln_upsample, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(AMX_BLOCK),
-                       0, st, x, n_in, r, ln.n192, ln.u, lp.gate);
+                       0, st, x, n_in, r, (int64_t)0, ln.n192, ln.u, lp.gate);
     hipLaunchKernelGGL(k_lp_stats, dim3(1 + (lp.T + LP_STAT_F - 1) / LP_STAT_F), dim3(LP_STAT_NT), 0, st, lp);
     hipLaunchKernelGGL(k_ln_dyn, dim3(1), dim3(LN_NT), 0, st, ln, 0);
     hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
@@ -1630,6 +1639,35 @@ hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x
     hipLaunchKernelGGL(k_lp_seg, dim3(lp.P), dim3(64), 0, st, lp);
     hipLaunchKernelGGL(k_lp_walk, dim3(1), dim3(64), 0, st, lp);
     hipLaunchKernelGGL(k_ln_dyn, dim3(1), dim3(LN_NT), 0, st, ln, 1);
+    return hipGetLastError();
+}
+
+// a chunk-sharded track's share of one filter run (amx_loudnorm_192k_shard), in three
+// parts the host puts the rank-to-rank hand-off between: 0 -- the 192 kHz stream over
+// [u_lo, u_hi) and every frame's statistics (the host then reads lp.ctl[0]: 0 = the
+// parallel form runs, else the whole track must run frame by frame); 1 -- deltas, gains
+// and the segments [kb, ke); 2 -- the walk over their boundaries from lp.rec_in
+hipError_t launch_loudnorm_shard(const LnArgs &ln, const LpArgs &lp, const uint32_t *x, int64_t n_in,
+                                 const SwrDev &r, int64_t u_lo, int64_t u_hi, int part, hipStream_t st) {
+    if (ln.n192 <= 0) return hipSuccess;
+    if (part == 0) {
+        const int64_t nb = (u_hi - u_lo + AMX_BLOCK - 1) / AMX_BLOCK;
+        if (nb > 0)
+            hipLaunchKernelGGL(k_ln_upsample, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(AMX_BLOCK), 0, st, x,
+                               n_in, r, u_lo, u_hi, ln.u, lp.gate);
+        hipLaunchKernelGGL(k_lp_stats, dim3(1 + (lp.T + LP_STAT_F - 1) / LP_STAT_F), dim3(LP_STAT_NT), 0, st, lp);
+    } else if (part == 1) {
+        hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
+        const int gb = max((lp.T + 1 + 255) / 256, (LP_FR + 255) / 256);
+        hipLaunchKernelGGL(k_lp_gains, dim3(gb), dim3(256), 0, st, lp);
+        hipError_t e = hipMemsetAsync(lp.cnt, 0, sizeof(int) * (size_t)(lp.K + 1), st);
+        if (e != hipSuccess) return e;
+        e = hipMemsetAsync(lp.match, 0, sizeof(int) * (size_t)(lp.K + 1), st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_lp_seg, dim3(lp.P), dim3(64), 0, st, lp);
+    } else {
+        hipLaunchKernelGGL(k_lp_walk, dim3(1), dim3(64), 0, st, lp);
+    }
     return hipGetLastError();
 }
 

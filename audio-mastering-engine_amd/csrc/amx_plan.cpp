@@ -1335,6 +1335,13 @@ int ln_frames(const amx_plan *p, int32_t track, int64_t *n192) {
     *n192 = p->resamp ? (sp.out_n * p->upL + p->upM - 1) / p->upM : sp.out_n;
     return AMX_OK;
 }
+// the first output position of segment k: its frame (k_lp_*'s lp_seg_start) and that
+// frame's base (lp_frame: INNER frames from 0, FINAL's from S0)
+int64_t ln_seg_base(const LnLayout &lo, int64_t n192, int k) {
+    const int phi = k == 0 ? 0 : (k <= lo.J ? 1 + k * lo.Fs : lo.T + 1 + (k - lo.J - 1) * lo.Fs);
+    const int64_t S0 = n192 - (LN_FIRST_FRAMES - 19200);
+    return phi <= lo.T ? (int64_t)19200 * phi : S0 + (int64_t)19200 * (phi - lo.T - 1);
+}
 int check_edges(const amx_plan *p, const int16_t *d_edge) {
     if (!p->resamp || d_edge) return AMX_OK;
     for (const SpanDev &sp : p->spans)
@@ -1403,12 +1410,16 @@ int amx_loudnorm_192k_size(const amx_plan *p, int32_t track, int64_t *frames, in
     return AMX_OK;
 }
 
-int amx_loudnorm_192k_ex(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const double *d_measured,
-                         const double *d_offset_i, const int32_t *d_gate, const int16_t *d_out, const double *d_hops,
-                         int64_t max_hops, const double *d_peak, int16_t *d_y192, double *d_summary,
-                         void *d_ws2, void *stream) {
+}  // extern "C"
+
+namespace {
+// the kernels' arguments of one filter run of track `track` (amx_loudnorm_192k_ex / _shard)
+int ln_args(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const double *d_measured,
+            const double *d_offset_i, const int32_t *d_gate, const int16_t *d_out, const double *d_hops,
+            int64_t max_hops, const double *d_peak, int16_t *d_y192, double *d_summary, void *d_ws2,
+            amx::LnArgs &a, amx::LpArgs &q, int64_t &n192) {
     if (!p || track < 0 || track >= p->n_tracks) return fail(AMX_EINVAL, "bad argument");
-    int64_t n192 = 0;
+    n192 = 0;
     if (int rc = ln_frames(p, track, &n192)) return rc;
     if (!d || !d_out || !d_hops || !d_peak || !d_y192 || !d_summary || !d_ws2)
         return fail(AMX_EINVAL, "null argument");
@@ -1418,7 +1429,7 @@ int amx_loudnorm_192k_ex(amx_plan *p, int32_t track, const amx_loudnorm_desc *d,
     if (max_hops < n192 / 19200 + 1) return fail(AMX_EINVAL, "d_hops holds %lld hops", (long long)max_hops);
     const LnLayout lo = ln_layout(n192);
     char *w = reinterpret_cast<char *>(d_ws2);
-    amx::LnArgs a{};
+    a = amx::LnArgs{};
     a.n192 = n192;
     a.u = reinterpret_cast<float *>(w + lo.o_u);
     a.ring = reinterpret_cast<double *>(w + lo.o_ring);
@@ -1450,7 +1461,7 @@ int amx_loudnorm_192k_ex(amx_plan *p, int32_t track, const amx_loudnorm_desc *d,
         for (int i = 0; i < 21; i++) a.weights[i] *= adjust;
     }
     for (int k = 0; k < 5; k++) { a.kb[k] = p->kdf_b[k]; a.ka[k] = p->kdf_a[k]; }
-    amx::LpArgs q{};
+    q = amx::LpArgs{};
     q.n = n192;
     q.S0 = n192 - (LN_FIRST_FRAMES - 19200);
     q.T = lo.T;
@@ -1497,9 +1508,79 @@ int amx_loudnorm_192k_ex(amx_plan *p, int32_t track, const amx_loudnorm_desc *d,
     a.lp_recG = q.recG;
     a.lp_Fs = q.Fs;
     a.lp_J = q.J;
+    q.kb = 0;
+    q.ke = q.K;
+    return AMX_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int amx_loudnorm_192k_ex(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const double *d_measured,
+                         const double *d_offset_i, const int32_t *d_gate, const int16_t *d_out, const double *d_hops,
+                         int64_t max_hops, const double *d_peak, int16_t *d_y192, double *d_summary,
+                         void *d_ws2, void *stream) {
+    amx::LnArgs a;
+    amx::LpArgs q;
+    int64_t n192 = 0;
+    if (int rc = ln_args(p, track, d, d_measured, d_offset_i, d_gate, d_out, d_hops, max_hops, d_peak, d_y192,
+                         d_summary, d_ws2, a, q, n192))
+        return rc;
+    const SpanDev &sp = p->spans[track];
     amx::SwrDev r{p->up_pc, p->up_lin, p->up_src, p->up_dst, p->d_bank};
     HIPCHK(amx::launch_loudnorm(a, q, reinterpret_cast<const uint32_t *>(d_out) + sp.out_off, sp.out_n, r,
                                 (hipStream_t)stream));
+    return AMX_OK;
+}
+
+int amx_loudnorm_192k_shard(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const double *d_measured,
+                            const double *d_offset_i, const amx_ln_shard *sh, const int16_t *d_out,
+                            const double *d_hops, int64_t max_hops, const double *d_peak, int16_t *d_y192,
+                            double *d_summary, void *d_ws2, void *stream) {
+    if (!sh || sh->part < 0 || sh->part > 2) return fail(AMX_EINVAL, "bad shard");
+    amx::LnArgs a;
+    amx::LpArgs q;
+    int64_t n192 = 0;
+    if (int rc = ln_args(p, track, d, d_measured, d_offset_i, nullptr, d_out, d_hops, max_hops, d_peak, d_y192,
+                         d_summary, d_ws2, a, q, n192))
+        return rc;
+    if (sh->kb < 0 || sh->ke > q.K || sh->kb > sh->ke) return fail(AMX_EINVAL, "segments [%d, %d) of %d", sh->kb, sh->ke, q.K);
+    int64_t u_lo = sh->u_lo, u_hi = sh->u_hi;
+    if (u_lo < 0) {
+        // what segments [kb, ke) read: from Wf + 2 frames before the first one's start
+        // (its warm-up) to a ring and two frames past the last one's end
+        const LnLayout lo = ln_layout(n192);
+        u_lo = std::max<int64_t>(0, ln_seg_base(lo, n192, sh->kb) - (int64_t)19200 * (lo.Wf + 2));
+        u_hi = sh->ke < lo.K ? std::min<int64_t>(n192, ln_seg_base(lo, n192, sh->ke) + AMX_LN_RING + 2 * 19200) : n192;
+    }
+    if (u_hi > n192 || u_lo > u_hi) return fail(AMX_EINVAL, "bad 192 kHz range");
+    if (sh->part == 2 && sh->kb > 0 && !sh->d_rec_in) return fail(AMX_EINVAL, "segment %d needs the true state", sh->kb);
+    q.kb = sh->kb;
+    q.ke = sh->ke;
+    q.rec_in = sh->kb > 0 ? sh->d_rec_in : nullptr;
+    q.rec_out = sh->ke < q.K ? sh->d_rec_out : nullptr;
+    const SpanDev &sp = p->spans[track];
+    amx::SwrDev r{p->up_pc, p->up_lin, p->up_src, p->up_dst, p->d_bank};
+    HIPCHK(amx::launch_loudnorm_shard(a, q, reinterpret_cast<const uint32_t *>(d_out) + sp.out_off, sp.out_n, r,
+                                      u_lo, u_hi, sh->part, (hipStream_t)stream));
+    return AMX_OK;
+}
+
+int amx_loudnorm_192k_segments(const amx_plan *p, int32_t track, int64_t *starts, int32_t cap, int32_t *K,
+                               int32_t *k_fin, int32_t *rec_doubles, int64_t *ctl_offset) {
+    if (!p || track < 0 || track >= p->n_tracks || !K) return fail(AMX_EINVAL, "bad argument");
+    int64_t n192 = 0;
+    if (int rc = ln_frames(p, track, &n192)) return rc;
+    const LnLayout lo = ln_layout(n192);
+    *K = lo.K;
+    if (k_fin) *k_fin = lo.J + 1;
+    if (rec_doubles) *rec_doubles = AMX_LN_REC;
+    if (ctl_offset) *ctl_offset = lo.o_ctl;
+    if (starts) {
+        if (cap < lo.K + 1) return fail(AMX_EINVAL, "starts holds %d, needs %d", cap, lo.K + 1);
+        for (int k = 0; k < lo.K; k++) starts[k] = ln_seg_base(lo, n192, k);
+        starts[lo.K] = n192;
+    }
     return AMX_OK;
 }
 

@@ -125,13 +125,24 @@ def synth_generator(frames, fs):
     return "amx.synth.mix_tiled(block_seconds=60)" if frames > 600 * fs else "amx.synth.mix_like"
 
 
-def synth_input(frames, fs, seed):
+def synth_input(frames, fs, seed, kind="mix"):
     """the seeded synthetic program; inputs longer than 10 minutes repeat a 60 s block
-    (amx.synth.mix_tiled: mix_like costs ~1 s of host time per 20 s of audio)"""
+    (amx.synth.mix_tiled: mix_like costs ~1 s of host time per 20 s of audio).
+    kind "dynamic": the programme at -18 dB with two 50-frame full-scale bursts per
+    second -- true peak + offset above -1.5 dBTP, so loudnorm takes dynamic mode"""
+    import numpy as np
     from amx import synth
     if frames > 600 * fs:
-        return synth.mix_tiled(frames, fs, 2, seed=seed)
-    return synth.mix_like(frames, fs, 2, seed=seed)
+        x = synth.mix_tiled(frames, fs, 2, seed=seed)
+    else:
+        x = synth.mix_like(frames, fs, 2, seed=seed)
+    if kind == "dynamic":
+        x *= np.float32(0.12)
+        rng = np.random.default_rng(seed + 11)
+        for k in rng.integers(0, max(1, frames - 200), max(2, int(frames / fs * 2))):
+            x[k:k + 50] += rng.uniform(-0.9, 0.9, (min(50, frames - k), 2)).astype(np.float32)
+        np.clip(x, -1.0, 1.0, out=x)
+    return x
 
 
 def load_flops(config):
@@ -260,6 +271,9 @@ def main():
                     help="nccl (= RCCL on ROCm); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--one-device", action="store_true",
                     help="every rank on cuda:0 (rehearsal with --dist-backend gloo)")
+    ap.add_argument("--input", default="mix", choices=("mix", "dynamic"),
+                    help="dynamic: a quiet programme with full-scale bursts, so loudnorm takes "
+                         "dynamic mode (the 192 kHz path; chunk-sharded at N > 1)")
     ap.add_argument("--force-exchange", action="store_true",
                     help="run the N > 1 step (graph segments + every collective) even at one rank: "
                          "an RCCL rehearsal on one GPU")
@@ -300,8 +314,9 @@ def main():
     else:
         total = per_track if args.strong else per_track * world
         runner = ShardedTrack(fs, 2, settings, total, rank, world, quantum=512,
-                              seg_frames=args.seg_frames, force_exchange=args.force_exchange)
-        x = synth_input(runner.local_frames, fs, rank)
+                              seg_frames=args.seg_frames, force_exchange=args.force_exchange,
+                              dynamic=args.input == "dynamic")
+        x = synth_input(runner.local_frames, fs, rank, args.input)
     d_in = torch.from_numpy(x).cuda()
     job = runner.job
 
@@ -405,7 +420,7 @@ def main():
     per_stage = {k: v / n_ev for k, v in per_stage.items()}
     job.stage_events = None
     env_ctr = job.env_counters() if settings.get("multiband") else None
-    report = job.fetch_report()
+    report = job.fetch_report(raise_dynamic=False)
     frames = runner.local_frames
     mb = bool(settings.get("multiband"))
     # dominant kernel: the slowest single-kernel stage
@@ -492,7 +507,11 @@ def main():
         "loudnorm": report.get("stats"),
         "loudnorm_mode": report.get("modes"),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if args.input == "dynamic":
+        # value counts the chain's input-rate samples; the step ends in the 192 kHz stream
+        line["dynamic"] = dict(getattr(runner, "dyn_info", None) or {}, input=args.input)
+        line["data"] += "; quiet programme with full-scale bursts (loudnorm dynamic mode)"
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.input == "mix":
         line.update(cpu_leg(args, runner, x, fs, settings, job, batch))
     if rank == 0 and world == 1 and args.config == "c3" and not args.no_other_configs:
         line["other_configs"] = other_configs(args)

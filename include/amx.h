@@ -305,6 +305,38 @@ AMX_API int amx_loudnorm_192k_ex(amx_plan *plan, int32_t track, const amx_loudno
                                  const int32_t *d_gate, const int16_t *d_out, const double *d_hops, int64_t max_hops,
                                  const double *d_peak, int16_t *d_y192, double *d_summary, void *d_ws2,
                                  void *stream);
+/* A chunk-sharded track's share of one dynamic-mode filter run (:240 in dynamic mode on a
+ * track split over ranks).  plan: a measure-only plan of the WHOLE track (d_out the whole
+ * chain output, gathered from the ranks); every rank forms every frame's AGC gain from the
+ * whole-track hop energies and runs the parallel form's segments [kb, ke) only; the
+ * rank-to-rank hand-off is the limiter's true state at a segment boundary, one record of
+ * rec_doubles doubles (amx_loudnorm_192k_segments).  part 0: the 192 kHz stream over
+ * [u_lo, u_hi) (u_lo < 0: the range segments [kb, ke) read) and the frame statistics -- then read the int32 at ctl_offset of d_ws2: 0
+ * means the parallel form runs, anything else (a quiet start, a track under 3 s) means the
+ * whole track must run frame by frame (amx_loudnorm_192k_ex on one rank's whole data);
+ * part 1: gains and the segments; part 2: the walk over [kb, ke) from d_rec_in (the true
+ * state at kb, made by the previous rank's part 2; NULL on the rank holding segment 0),
+ * which writes the true state at ke to d_rec_out (NULL on the last rank; a record whose
+ * [7] is non-zero means the walk could not go on: the whole track must run frame by
+ * frame).  Outputs: d_y192 frames [start(kb), start(ke)) (whole-track positions).
+ * Replaces no single reference line: the reference runs the filter on one process. */
+typedef struct amx_ln_shard {
+    int32_t part, kb, ke, pad_;
+    int64_t u_lo, u_hi;
+    const double *d_rec_in;
+    double *d_rec_out;
+} amx_ln_shard;
+AMX_API int amx_loudnorm_192k_shard(amx_plan *plan, int32_t track, const amx_loudnorm_desc *desc,
+                                    const double *d_measured, const double *d_offset_i, const amx_ln_shard *sh,
+                                    const int16_t *d_out, const double *d_hops, int64_t max_hops,
+                                    const double *d_peak, int16_t *d_y192, double *d_summary, void *d_ws2,
+                                    void *stream);
+/* The parallel form's segments of the track's 192 kHz filter run: starts[k] (k < *K, cap
+ * entries) = the output frame segment k starts at (starts[*K] = the frame count); *k_fin
+ * = the first segment of the FINAL flush frame (one rank must hold [k_fin, K)); the
+ * record size in doubles; the byte offset in d_ws2 of the int32 control words. */
+AMX_API int amx_loudnorm_192k_segments(const amx_plan *plan, int32_t track, int64_t *starts, int32_t cap,
+                                       int32_t *K, int32_t *k_fin, int32_t *rec_doubles, int64_t *ctl_offset);
 /* Host helper for chunk-sharded tracks: out8 = A^frames * in8 (per channel 4x4 K-filter
  * transition at the measurement rate; frames of the measurement stream), so
  * carry(r+1) = A^{len_r} carry(r) + tail(r). */

@@ -278,3 +278,23 @@ def test_gather_track_gloo_world2(spans):
     """dynamic mode's span gather (ShardedTrack.dynamic): spans of different lengths are
     padded to the longest for one all_gather_into_tensor and reassembled in rank order"""
     mp.spawn(_gather_worker, args=(2, _free_port(), spans), nprocs=2, join=True)
+
+
+@pytest.mark.parametrize("K,k_fin,world", [(188, 181, 2), (188, 181, 8), (9, 2, 2), (12, 5, 4), (40, 33, 3)])
+def test_shard_segments(K, k_fin, world):
+    """the sharded dynamic mode's segment split: contiguous runs tiling [0, K), every rank
+    non-empty, no boundary inside the FINAL flush frame's segments [k_fin, K)"""
+    r = adist.shard_segments(K, k_fin, world)
+    assert len(r) == world and r[0][0] == 0 and r[-1][1] == K
+    assert all(r[i][1] == r[i + 1][0] for i in range(world - 1))
+    assert all(b > a for a, b in r)
+    assert all(b <= k_fin for a, b in r[:-1]) and r[-1][0] < k_fin
+    pre = [min(b, k_fin) - a for a, b in r]
+    assert max(pre) - min(pre) <= 1
+
+
+def test_shard_segments_short_track():
+    """fewer pre-FINAL segments than ranks: no split (every rank runs the filter whole)"""
+    assert adist.shard_segments(30, 1, 2) is None
+    assert adist.shard_segments(35, 7, 8) is None
+    assert adist.shard_segments(36, 8, 8) is not None

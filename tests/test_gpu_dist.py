@@ -32,13 +32,19 @@ CASES = {
     # quiet programme with sparse full-scale transients: TP + offset > -1.5 dBTP, so
     # loudnorm's pass 2 takes dynamic mode and the output is the 192 kHz stream
     "dynamic": dict(bass_boost=1.0, lufs=-14.0),
+    # the same with one-frame filter segments and no warm-up (AMX_LN_SEG=1, AMX_LN_WARM=0):
+    # most segments start from a wrong guess, so the limiter state rank 0's walk hands
+    # rank 1 decides rank 1's first segment
+    "dynamic_nowarm": dict(bass_boost=1.0, lufs=-14.0),
 }
+ENV = {"dynamic_nowarm": {"AMX_LN_SEG": "1", "AMX_LN_WARM": "0"}}
 RATE = {"c3_lufs_44k1": 44100}
 
 
 # input gain per case: the loud case drives 0.1 % of the frames over the limit, so the final
 # alimiter (limit 0.98) must engage and the ranks hand its state along
-GAIN = {"c3_lufs": 1.0, "loud_limiter": 1.3, "square_limiter": 1.0, "c3_lufs_44k1": 1.0, "dynamic": 1.0}
+GAIN = {"c3_lufs": 1.0, "loud_limiter": 1.3, "square_limiter": 1.0, "c3_lufs_44k1": 1.0, "dynamic": 1.0,
+        "dynamic_nowarm": 1.0}
 
 
 def _track(seconds, case):
@@ -47,7 +53,7 @@ def _track(seconds, case):
     n = int(fs * seconds)
     if case == "square_limiter":
         return synth.square(n, fs, 2, freq=110.0, amp=1.0)
-    if case == "dynamic":
+    if case.startswith("dynamic"):
         x = synth.mix_like(n, fs, 2, seed=11) * 0.12
         rng = np.random.default_rng(11)
         for k in rng.integers(0, n - 200, max(2, int(seconds * 2))):
@@ -62,6 +68,7 @@ def _worker(rank, world, port, case, seconds, outdir):
     from amx.dist import ShardedTrack
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ.update(ENV.get(case, {}))
     dist.init_process_group("gloo", rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=60))
     try:
@@ -79,6 +86,9 @@ def _worker(rank, world, port, case, seconds, outdir):
         np.save(os.path.join(outdir, "y%d.npy" % rank), y_eager)
         fast = bool(int(tr.job.ctl[0].item()) & 1)
         np.save(os.path.join(outdir, "fast%d.npy" % rank), np.array([fast]))
+        if case.startswith("dynamic"):
+            with open(os.path.join(outdir, "form%d.txt" % rank), "w") as f:
+                f.write(tr.dyn_info["form"])
     finally:
         dist.destroy_process_group()
 
@@ -98,9 +108,9 @@ def test_two_ranks_match_one(gpu, case):
     from amx.dist import ShardedTrack
     # 3 chunks -> ranks own 2 + 1; the sequential-limiter case 2 chunks (that path walks
     # every frame in order)
-    seconds = 75.0 if case.startswith("c3_lufs") or case == "dynamic" else 32.0
+    seconds = 75.0 if case.startswith("c3_lufs") or case.startswith("dynamic") else 32.0
     x = _track(seconds, case)
-    if case == "dynamic":
+    if case.startswith("dynamic"):
         # the one-GPU reference: the whole track through master_array (dynamic_track)
         from amx.engine import master_array
         y1, rep = master_array(torch.from_numpy(np.ascontiguousarray(x)), FS, CASES[case], quantum=512)
@@ -113,10 +123,15 @@ def test_two_ranks_match_one(gpu, case):
         mp.spawn(_worker, args=(2, _port(), case, seconds, d), nprocs=2, join=True)
         parts = [np.load(os.path.join(d, "y%d.npy" % r)) for r in range(2)]
         fast = [bool(np.load(os.path.join(d, "fast%d.npy" % r))[0]) for r in range(2)]
+        forms = [open(os.path.join(d, "form%d.txt" % r)).read() if case.startswith("dynamic") else None
+                 for r in range(2)]
     y2 = np.concatenate(parts)
     assert fast[0] == fast[1]
+    if case.startswith("dynamic"):
+        # both filter runs split over the ranks by segments, with the limiter-state hand-off
+        assert forms == ["sharded"] * 2, forms
     # the loud case must exercise the rank-to-rank sequential limiter
-    if case != "dynamic":
+    if not case.startswith("dynamic"):
         assert fast[0] == case.startswith("c3_lufs"), "limiter fast path %s" % fast[0]
     assert y2.shape == y1.shape
     diff = np.abs(y2.astype(np.int32) - y1.astype(np.int32))
