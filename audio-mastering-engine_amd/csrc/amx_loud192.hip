@@ -53,6 +53,9 @@ namespace amx {
 #ifndef AMX_UP_WAVES
 #define AMX_UP_WAVES 4     // waves per SIMD the register budget must allow
 #endif
+#ifndef AMX_UP_PF
+#define AMX_UP_PF 1        // k_up_poly: the next output's bank and C A^n rows loaded one output ahead
+#endif
 
 __device__ __forceinline__ float up_sample(uint32_t w, int ch) {
     return (float)(ch ? hi16(w) : lo16(w)) * (1.0f / 32768.0f);
@@ -134,8 +137,10 @@ struct UpAcc {
     int split, len;
     const double *wc;            // rows C A^n (plan table)
     __device__ __forceinline__ void add(int n, float u, float xc) {
+        add_row(n, u, xc, wc + (int64_t)n * AMX_KW_DIM);              // wave-uniform row
+    }
+    __device__ __forceinline__ void add_row(int n, float u, float xc, const double *r) {
         const double ud = (double)u;
-        const double *r = wc + (int64_t)n * AMX_KW_DIM;              // wave-uniform row
         if constexpr (FAST) {
             const double a = bq_step(c1, v[0], v[1], ud);
             const double y = hp_step(c2, v[2], v[3], a);
@@ -313,6 +318,17 @@ k_up_poly(UpArgs a) {
     for (int i = 0; i < W; i++) w[i] = up_sample(xp[i], ch);
     const int nblk = a.Lin / TB;
     int n = 0;                                                 // next output (wave-uniform)
+#if AMX_UP_PF
+    // the rows of output n (bank row, C A^n row) are loaded while output n - 1 computes:
+    // 40 scalar registers in flight instead of a scalar-cache miss on every output (the
+    // 640 rows of 44.1 kHz are 80 KB)
+    float h[UP_TAPS];
+    double r[AMX_KW_DIM];
+#pragma unroll
+    for (int i = 0; i < UP_TAPS; i++) h[i] = a.bankn[i];
+#pragma unroll
+    for (int d = 0; d < AMX_KW_DIM; d++) r[d] = a.G[d];
+#endif
     for (int b = 0; b < nblk; b++) {
         uint32_t nx[TB];
         const int o0 = (b + 1 < nblk ? (b + 1) * TB : b * TB) + (W - TB);
@@ -326,7 +342,24 @@ k_up_poly(UpArgs a) {
             for (int o = 0; o < CMAX; o++) {
                 if (o < CMIN || o < c) {
                     __builtin_amdgcn_sched_barrier(AMX_UP_SB);
+#if AMX_UP_PF
+                    const int nn = n + 1 < a.Lout ? n + 1 : n;
+                    float hn[UP_TAPS];
+                    double rn[AMX_KW_DIM];
+                    const float *hp = a.bankn + (int64_t)nn * UP_TAPS;
+                    const double *rp = a.G + (int64_t)nn * AMX_KW_DIM;
+#pragma unroll
+                    for (int i = 0; i < UP_TAPS; i++) hn[i] = hp[i];
+#pragma unroll
+                    for (int d = 0; d < AMX_KW_DIM; d++) rn[d] = rp[d];
+                    acc.add_row(n, UP_DOT(w + kb, h), w[kb + UP_C], r);
+#pragma unroll
+                    for (int i = 0; i < UP_TAPS; i++) h[i] = hn[i];
+#pragma unroll
+                    for (int d = 0; d < AMX_KW_DIM; d++) r[d] = rn[d];
+#else
                     acc.add(n, UP_DOT(w + kb, a.bankn + (int64_t)n * UP_TAPS), w[kb + UP_C]);
+#endif
                     n++;
                 }
             }
