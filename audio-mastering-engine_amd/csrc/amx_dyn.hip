@@ -944,125 +944,6 @@ hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m) {
     return hipGetLastError();
 }
 
-// The same speculation with the band's m table in LDS (one 160 KiB workgroup per CU):
-// slot 0 holds 0 (r < rq: below the threshold), slot s >= 1 holds m(rq + s - 1) for the
-// AMX_ENV_NT - 1 indices from rq, the first with m != 0.  A lane reads its own 16-frame
-// row of r (two 16-B loads, AMX_ENV_PF tiles in flight) and looks up m in LDS: no L1
-// line refills of the 256 KB table and no LDS staging.  An r past the table's end (the
-// loudest frames, r > rq + AMX_ENV_NT - 2) is gathered from the global table for that
-// tile (a wave-uniform test, rare).
-#define AMX_ENV_NT 20480
-#define AMX_ENV_LDS_TAB (AMX_ENV_NT * 8)
-template <bool RCP>
-__global__ void __launch_bounds__(64 * AMX_ENV_WG) k_env0l(const ChainDev *__restrict__ cdp,
-                                              const ChunkDev *__restrict__ chunks,
-                                              const SegDev *__restrict__ es, int n_es,
-                                              const uint16_t *__restrict__ mi,
-                                              const double *__restrict__ tabs,
-                                              double *__restrict__ ck,
-                                              double *__restrict__ sv, double *__restrict__ ev,
-                                              int *__restrict__ act, int64_t nloc, int warm,
-                                              int Le, int *__restrict__ flags) {
-    extern __shared__ double tl[];
-    const ChainDev &cd = *cdp;
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < AMX_ENV_MAX_ROUNDS) flags[threadIdx.x] = 0;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) {
-        for (int k = lane; k < AMX_ENV_MAX_ROUNDS * AMX_ENV_NCTR; k += 64) flags[AMX_ENV_MAX_ROUNDS + k] = 0;
-    }
-    const int b = blockIdx.y;
-    const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
-    const int rq = cd.rq[b];
-    for (int s = threadIdx.x; s < AMX_ENV_NT; s += blockDim.x) {
-        const int r = rq + s - 1;
-        tl[s] = (s > 0 && r <= 32768) ? mt[r] : 0.0;
-    }
-    __syncthreads();
-    const int j = (blockIdx.x * (blockDim.x >> 6) + wv) * 64 + lane;
-    const bool valid = j < n_es;
-    const SegDev sg = es[valid ? j : n_es - 1];
-    const ChunkDev ch = chunks[sg.chunk];
-    const int64_t rowoff = b * nloc + ch.loc_off;       // this lane's chunk row
-    const int64_t start = sg.pos - warm;                // frame of step 0 (may be < 0)
-    const int64_t end = valid ? sg.pos + sg.len : sg.pos;
-    double *ckr = ck + rowoff / AMX_ENV_TF;             // checkpoint k: before frame 16 k
-    const int ntile = (warm + Le) / AMX_ENV_TF, nwarm = warm / AMX_ENV_TF;
-    const uint16_t *row = mi + rowoff + start;
-    u4v R[AMX_ENV_PF][2];
-#pragma unroll
-    for (int u = 0; u < AMX_ENV_PF; u++) {
-        R[u][0] = *reinterpret_cast<const u4v *>(row + u * AMX_ENV_TF);
-        R[u][1] = *reinterpret_cast<const u4v *>(row + u * AMX_ENV_TF + 8);
-    }
-    double att = 0.0, s_spec = 0.0;
-    if (cd.env_guess && start >= 0) att = mt[mi[rowoff + start]];
-    bool any = false;
-    for (int q0 = 0; q0 < ntile; q0 += AMX_ENV_PF) {
-#pragma unroll
-        for (int u = 0; u < AMX_ENV_PF; u++) {
-            const int q = q0 + u;
-            const u4v a0 = R[u][0], a1 = R[u][1];
-            {
-                const int qn = (q + AMX_ENV_PF < ntile ? q + AMX_ENV_PF : q) * AMX_ENV_TF;
-                R[u][0] = *reinterpret_cast<const u4v *>(row + qn);
-                R[u][1] = *reinterpret_cast<const u4v *>(row + qn + 8);
-            }
-            const int64_t f0 = start + (int64_t)q * AMX_ENV_TF;
-            const bool in = f0 >= 0 && f0 < end;
-            if (q == nwarm) s_spec = att;
-            if (in) {
-                uint32_t rr[AMX_ENV_TF];
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    rr[2 * e] = a0[e] & 0xffffu;
-                    rr[2 * e + 1] = a0[e] >> 16;
-                    rr[8 + 2 * e] = a1[e] & 0xffffu;
-                    rr[8 + 2 * e + 1] = a1[e] >> 16;
-                }
-                double mv[AMX_ENV_TF];
-                bool far = false;
-#pragma unroll
-                for (int f = 0; f < AMX_ENV_TF; f++) {
-                    const int s = (int)rr[f] - rq + 1;
-                    far |= s >= AMX_ENV_NT;
-                    mv[f] = tl[s < 0 ? 0 : (s < AMX_ENV_NT ? s : 0)];
-                }
-                if (__ballot(far)) {
-#pragma unroll
-                    for (int f = 0; f < AMX_ENV_TF; f++) {
-                        const int s = (int)rr[f] - rq + 1;
-                        if (s >= AMX_ENV_NT) mv[f] = m_of(mt, rr[f]);
-                    }
-                }
-                if (q >= nwarm) {
-                    ckr[f0 / AMX_ENV_TF] = att;
-                    uint32_t h = 0, l = 0;
-#pragma unroll
-                    for (int f = 0; f < AMX_ENV_TF; f++) {
-                        const unsigned long long x = (unsigned long long)__double_as_longlong(mv[f]);
-                        h |= (uint32_t)(x >> 32);
-                        l |= (uint32_t)x;
-                    }
-                    any |= ((h & 0x7fffffffu) | l) != 0u;
-                }
-                double iv[AMX_ENV_TF], dv[AMX_ENV_TF];
-#pragma unroll
-                for (int f = 0; f < AMX_ENV_TF; f++) {
-                    iv[f] = env_div<RCP>(mv[f], cd.env_A, cd.env_rA);
-                    dv[f] = env_div<RCP>(mv[f], cd.env_R, cd.env_rR);
-                }
-#pragma unroll
-                for (int f = 0; f < AMX_ENV_TF; f++) att = env_step3_raw(att, mv[f], iv[f], dv[f]);
-            }
-        }
-    }
-    if (valid) {
-        sv[(int64_t)b * n_es + j] = s_spec;
-        ev[(int64_t)b * n_es + j] = att;
-        act[(int64_t)b * n_es + j] = any ? 1 : 0;
-    }
-}
-
 // part 0: the speculation (k_env0); part 1: the parallel fix-up rounds (k_envfix)
 template <bool RCP>
 static void env_launch_t(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,
@@ -1071,12 +952,8 @@ static void env_launch_t(const DynLaunch &d, const uint16_t *m, double *ck, doub
     if (part == 0) {
         const int wg = d.env_wg >= 1 && d.env_wg <= AMX_ENV_WG ? d.env_wg : 1;
         const dim3 g0((unsigned)((d.n_es + 64 * wg - 1) / (64 * wg)), 3);
-        if (d.env_lds)
-            hipLaunchKernelGGL((k_env0l<RCP>), g0, dim3(64 * wg), AMX_ENV_LDS_TAB, d.st, d.cd,
-                               d.chunks, d.es, d.n_es, m, d.tabs, ck, sv, ev, act, d.nloc, d.warm, d.Le, flags);
-        else
-            hipLaunchKernelGGL((k_env0<RCP>), g0, dim3(64 * wg), d.env_pin ? AMX_ENV_LDS_PIN : 0, d.st, d.cd,
-                               d.chunks, d.es, d.n_es, m, d.tabs, ck, sv, ev, act, d.nloc, d.warm, d.Le, flags);
+        hipLaunchKernelGGL((k_env0<RCP>), g0, dim3(64 * wg), d.env_pin ? AMX_ENV_LDS_PIN : 0, d.st, d.cd,
+                           d.chunks, d.es, d.n_es, m, d.tabs, ck, sv, ev, act, d.nloc, d.warm, d.Le, flags);
         return;
     }
     // rounds == 0: only prev[] (everything is left to k_envseq)

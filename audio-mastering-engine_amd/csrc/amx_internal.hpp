@@ -174,7 +174,6 @@ struct DynLaunch {
     const double *tabs;
     hipStream_t st;
     int env_wg, env_pin;         // k_env0: waves per workgroup, one workgroup per CU
-    int env_lds;                 // k_env0l: the m table in LDS
 };
 hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m);
 // input decode: PCM of any supported format -> stereo s16 frames (amx_io.hip)

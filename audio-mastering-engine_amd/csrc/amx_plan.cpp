@@ -271,7 +271,6 @@ struct amx_plan {
     int mb = 0;
     int Le = 1024, warm = 2304, rounds = 2;   // compressor envelope segments (amx_dyn.hip)
     int env_wg = 1, env_pin = 0;              // k_env0 placement (amx_dyn.hip launch_env)
-    int env_lds = 0;                          // k_env0l: the m table in LDS
     int f1_mode = AMX_F1_SPLIT;               // pass-1 form for float32 stereo + analog
     int n_es = 0;
     std::vector<SegDev> esegs;
@@ -659,8 +658,6 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         if (const char *ev = std::getenv("AMX_ENV_WG")) wg = std::atoi(ev);
         int64_t le_min = 1024;                                   // (measurements: AMX_ENV_LEMIN)
         if (const char *ev = std::getenv("AMX_ENV_LEMIN")) le_min = std::max(128, std::atoi(ev)) / 128 * 128;
-        if (const char *ev = std::getenv("AMX_ENV_LDS")) p->env_lds = std::atoi(ev) != 0;
-        if (p->env_lds && wg < 1) wg = 2;
         if (wg > 0) {
             p->env_wg = std::min(wg, 4);
             p->env_pin = 1;
@@ -1186,7 +1183,7 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     amx::DynLaunch dl{p->d_cd,    p->d_chunks, p->n_chunks, p->d_esegs, p->n_es,
                       p->d_eseg0, p->d_neseg,  p->nloc,     p->max_chunk_n, p->cd.look,
                       p->warm,    p->Le,       p->cd.env_rcp, p->d_tabs, st,
-                      p->env_wg,  p->env_pin,  p->env_lds};
+                      p->env_wg,  p->env_pin};
     switch (stage) {
     case AMX_STAGE_FRONT1:
         if (p->mono16) {
