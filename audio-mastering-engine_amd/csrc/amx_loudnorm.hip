@@ -64,6 +64,48 @@ __device__ __forceinline__ float ln_dot(const float *w, const float *__restrict_
     return (b0 + b2) + (b1 + b3);
 }
 
+// The M == 1 rates (192 kHz / L: 48 kHz L = 4, 96 kHz 2, 64 kHz 3, 32 kHz 6, 192 kHz 1):
+// output j = frame j / L, phase j % L.  One thread per input frame: its 32-frame window
+// once, then the L outputs with the bank rows as wave-uniform operands (k_ln_upsample's
+// generic form pays two 64-bit divisions and a per-lane bank row for every output).
+template <int L>
+__global__ void __launch_bounds__(AMX_BLOCK) k_ln_up_static(const uint32_t *__restrict__ x, int64_t n_in,
+                                                            const float *__restrict__ bank, int64_t j0, int64_t j1,
+                                                            float *__restrict__ u, const int32_t *__restrict__ gate) {
+    if (AMX_LN_GATED(gate)) return;
+    const int64_t f0 = j0 / L, f1 = (j1 + L - 1) / L;
+    for (int64_t f = f0 + (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x; f < f1; f += (int64_t)gridDim.x * AMX_BLOCK) {
+        float w0[LN_TAPS], w1[LN_TAPS];
+        const int64_t g = f - LN_C;
+        if (g >= 0 && g + LN_TAPS <= n_in) {
+#pragma unroll
+            for (int i = 0; i < LN_TAPS; i++) {
+                const uint32_t v = x[g + i];
+                w0[i] = (float)lo16(v) * (1.0f / 32768.0f);
+                w1[i] = (float)hi16(v) * (1.0f / 32768.0f);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < LN_TAPS; i++) {
+                const uint32_t v = x[ln_reflect(g + i, n_in)];
+                w0[i] = (float)lo16(v) * (1.0f / 32768.0f);
+                w1[i] = (float)hi16(v) * (1.0f / 32768.0f);
+            }
+        }
+#pragma unroll
+        for (int ph = 0; ph < L; ph++) {
+            const int64_t j = f * L + ph;
+            const float *h = bank + ph * LN_TAPS;
+            const float a = ln_dot(w0, h), b = ln_dot(w1, h);
+            if (j >= j0 && j < j1) *reinterpret_cast<float2 *>(u + 2 * j) = make_float2(a, b);
+        }
+    }
+}
+
+// dispatch: the static form for M == 1 rates, else the generic one
+static void ln_upsample(const uint32_t *x, int64_t n_in, const SwrDev &r, int64_t j0, int64_t j1, float *u,
+                        const int32_t *gate, hipStream_t st);
+
 // one thread per 192 kHz frame: both channels, frames [j0, j1).  Output j sits at phase
 // position j dst / src past input frame 0 (exact rates: j M / L, frac 0)
 __global__ void __launch_bounds__(AMX_BLOCK) k_ln_upsample(const uint32_t *__restrict__ x, int64_t n_in,
@@ -1124,7 +1166,7 @@ __device__ __forceinline__ void lp_clear_range(LpWave &W, int lo, int hi) {   //
 }
 
 // the fill at the start of frame phi: the slots it refills lose their flags
-__device__ void lp_refill(const LpArgs &a, LpWave &W, int phi) {
+__device__ __forceinline__ void lp_refill(const LpArgs &a, LpWave &W, int phi) {
     int s0 = 0, cnt = LP_RS;
     if (phi != 0 && phi != a.T + 1) {
         if (phi <= a.T) {
@@ -1145,20 +1187,32 @@ __device__ void lp_refill(const LpArgs &a, LpWave &W, int phi) {
     __syncthreads();
 }
 
-// multiply k slots from e0 by env(i) (af_loudnorm's envelope loops)
+// multiply k slots from e0 by env(i) (af_loudnorm's envelope loops).  The k slots are
+// distinct, so the values of 4 groups of 64 are loaded before any of them is written
+// (one memory round trip per 256 slots)
 template <class F>
 __device__ __forceinline__ void lp_env(const LpArgs &a, LpWave &W, int e0, int k, F env) {
-    for (int i0 = 0; i0 < k; i0 += 64) {
-        const int i = i0 + (int)threadIdx.x;
-        if (i < k) {
-            int s = e0 + i;
-            if (s >= LP_RS) s -= LP_RS;
-            double2 v = lp_val(a, W, s);
-            const double g = env(i);
-            v.x = v.x * g;
-            v.y = v.y * g;
-            W.ring[s] = v;
-            atomicOr(&W.flags[s >> 5], 1u << (s & 31));
+    for (int i00 = 0; i00 < k; i00 += 256) {
+        double2 v[4];
+        int s[4];
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            const int i = i00 + 64 * p + (int)threadIdx.x;
+            int ss = e0 + i;
+            if (ss >= LP_RS) ss -= LP_RS;
+            s[p] = ss;
+            v[p] = i < k ? lp_val(a, W, ss) : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            const int i = i00 + 64 * p + (int)threadIdx.x;
+            if (i < k) {
+                const double g = env(i);
+                v[p].x = v[p].x * g;
+                v[p].y = v[p].y * g;
+                W.ring[s[p]] = v[p];
+                atomicOr(&W.flags[s[p] >> 5], 1u << (s[p] & 31));
+            }
         }
         __syncthreads();
     }
@@ -1169,11 +1223,25 @@ __device__ __forceinline__ int lp_env_end(int e0, int k) {
     return e >= LP_RS ? e - LP_RS : e;
 }
 
+#define LP_PD 4                  // lp_detect: groups of 64 positions loaded ahead
+// one group's values: 64 positions from slot s0, and the 12 after them (lanes < 12)
+__device__ __forceinline__ void lp_grp(const LpArgs &a, const LpWave &W, int s0, int lane, double2 &v,
+                                       double2 &v2) {
+    int s = s0 + lane;
+    while (s >= LP_RS) s -= LP_RS;
+    v = lp_val(a, W, s);
+    v2 = make_double2(0.0, 0.0);
+    if (lane < 12) {
+        int s2 = s0 + 64 + lane;
+        while (s2 >= LP_RS) s2 -= LP_RS;
+        v2 = lp_val(a, W, s2);
+    }
+}
 // detect_peak from offset smp over count positions: peak_delta or -1; the peak's |x|
 // and slot.  64 positions per step: the first one that is a candidate with its
 // previous sample as predecessor is found by a ballot; only from there on is the scan
 // serial (a candidate that fails the 10-sample look-ahead keeps the older predecessor)
-__device__ int lp_detect(const LpArgs &a, LpWave &W, int smp, int count, double &peak_value,
+__device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, int count, double &peak_value,
                          int &peak_slot) {
     const int lane = threadIdx.x;
     int slot0 = W.f.lbi + smp + LP_ATT;
@@ -1181,17 +1249,21 @@ __device__ int lp_detect(const LpArgs &a, LpWave &W, int smp, int count, double 
     const double ceiling = a.ceiling;
     double pv0 = 0.0, pv1 = 0.0;               // n = 0 never qualifies (n > 0)
     double *st0 = W.st, *st1 = W.st + 80;
-    for (int nb0 = 0; nb0 < count; nb0 += 64) {
+    // the groups' values are loaded LP_PD groups ahead of the one being scanned (the scan
+    // only reads the ring, so a value loaded early is the value then): one memory round
+    // trip per LP_PD groups instead of one per group.  Loads past count read slots of the
+    // same ring window, in bounds, unused.
+    double2 q[LP_PD], q2[LP_PD];
+#pragma unroll
+    for (int p = 0; p < LP_PD; p++) lp_grp(a, W, slot0 + p * 64, lane, q[p], q2[p]);
+    for (int nb00 = 0; nb00 < count; nb00 += 64 * LP_PD)
+#pragma unroll
+    for (int p = 0; p < LP_PD; p++) {
+        const int nb0 = nb00 + 64 * p;
+        if (nb0 >= count) break;
         {
-            int s = slot0 + nb0 + lane;
-            if (s >= LP_RS) s -= LP_RS;
-            const double2 v = lp_val(a, W, s);
-            double2 v2 = make_double2(0.0, 0.0);
-            if (lane < 12) {
-                int s2 = slot0 + nb0 + 64 + lane;
-                if (s2 >= LP_RS) s2 -= LP_RS;
-                v2 = lp_val(a, W, s2);
-            }
+            const double2 v = q[p], v2 = q2[p];
+            lp_grp(a, W, slot0 + nb0 + 64 * LP_PD, lane, q[p], q2[p]);
             __syncthreads();                   // the previous group's serial reads are done
             st0[lane] = fabs(v.x);
             st1[lane] = fabs(v.y);
@@ -1248,9 +1320,10 @@ __device__ int lp_detect(const LpArgs &a, LpWave &W, int smp, int count, double 
 }
 
 // the output of the frame: the ring from its first slot, clamped to the ceiling, s16
-__device__ void lp_emit(const LpArgs &a, const LpWave &W) {
+__device__ __forceinline__ void lp_emit(const LpArgs &a, const LpWave &W) {
     const double ceiling = a.ceiling;
     uint32_t *y = reinterpret_cast<uint32_t *>(a.y);
+#pragma unroll 4
     for (int i0 = 0; i0 < W.f.nb; i0 += 64) {
         const int i = i0 + (int)threadIdx.x;
         if (i < W.f.nb) {
@@ -1266,7 +1339,7 @@ __device__ void lp_emit(const LpArgs &a, const LpWave &W) {
 }
 
 // true_peak_limiter on frame W.f (af_loudnorm), then its output when emit
-__device__ void lp_call(const LpArgs &a, LpWave &W, bool emit) {
+__device__ __forceinline__ void lp_call(const LpArgs &a, LpWave &W, bool emit) {
     const int nb = W.f.nb;
     const double ceiling = a.ceiling;
     if (W.f.phi == 0) {
@@ -1365,7 +1438,7 @@ __device__ void lp_call(const LpArgs &a, LpWave &W, bool emit) {
     if (emit) lp_emit(a, W);
 }
 
-__device__ void lp_rest(LpWave &W) {        // af_loudnorm's initial limiter state
+__device__ __forceinline__ void lp_rest(LpWave &W) {        // af_loudnorm's initial limiter state
     W.mode = LO_OUT;
     W.env_cnt = 0;
     W.env_index = 0;
@@ -1378,7 +1451,7 @@ __device__ void lp_rest(LpWave &W) {        // af_loudnorm's initial limiter sta
 
 // the state at the start of frame W.f (after its fill): scalars and the values of
 // the 2048 slots from the frame's first; [LP_DIRTY] = a flag outside those slots
-__device__ void lp_snapshot(const LpArgs &a, const LpWave &W, double *rec) {
+__device__ __forceinline__ void lp_snapshot(const LpArgs &a, const LpWave &W, double *rec) {
     const int lane = threadIdx.x;
     const int w0 = W.f.lbi;
     bool out = false;
@@ -1416,7 +1489,7 @@ __device__ void lp_snapshot(const LpArgs &a, const LpWave &W, double *rec) {
 }
 
 // the same state back into a wave (every window slot flagged with its recorded value)
-__device__ void lp_restore(const LpArgs &a, LpWave &W, const double *rec, int phi) {
+__device__ __forceinline__ void lp_restore(const LpArgs &a, LpWave &W, const double *rec, int phi) {
     W.f = lp_frame(a, phi);
     W.mode = (int)rec[0];
     W.env_cnt = (int)rec[1];
@@ -1442,7 +1515,7 @@ __device__ __forceinline__ bool lp_bits_eq(double x, double y) {
 // two states at the same frame lead to the same future: equal scalars (only the mode
 // when both are at rest: OUT re-initialises the rest) and equal window values, and
 // neither has a multiplied slot outside the window
-__device__ bool lp_same(const double *A, const double *B) {
+__device__ __forceinline__ bool lp_same(const double *A, const double *B) {
     bool diff = A[LP_DIRTY] != 0.0 || B[LP_DIRTY] != 0.0 || (int)A[0] != (int)B[0];
     if ((int)A[0] != LO_OUT || (int)B[0] != LO_OUT)
         for (int q = 0; q < 6; q++) diff |= !lp_bits_eq(A[q], B[q]);
@@ -1452,7 +1525,7 @@ __device__ bool lp_same(const double *A, const double *B) {
 
 // boundary j: the later of segment j-1 (its end state) and segment j (its guess) to
 // arrive compares them
-__device__ void lp_arrive(const LpArgs &a, int j) {
+__device__ __forceinline__ void lp_arrive(const LpArgs &a, int j) {
     __threadfence();
     int old = 0;
     if (threadIdx.x == 0) old = atomicAdd(&a.cnt[j], 1);
@@ -1619,14 +1692,32 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
     }
 }
 
+static void ln_upsample(const uint32_t *x, int64_t n_in, const SwrDev &r, int64_t j0, int64_t j1, float *u,
+                        const int32_t *gate, hipStream_t st) {
+    if (j1 <= j0) return;
+    // grid-stride over at most 8192 workgroups: a gated (linear) track's launch then
+    // dispatches a bounded number of workgroups that return at once
+    auto grid = [](int64_t n) {
+        const int64_t nb = (n + AMX_BLOCK - 1) / AMX_BLOCK;
+        return dim3((unsigned)(nb < 8192 ? nb : 8192));
+    };
+    if (!r.lin && r.src == r.dst) {
+        const int64_t nf = (j1 + r.pc - 1) / r.pc - j0 / r.pc;
+        switch (r.pc) {
+#define LN_UPS(LL) \
+        case LL: hipLaunchKernelGGL(k_ln_up_static<LL>, grid(nf), dim3(AMX_BLOCK), 0, st, x, n_in, r.bank, j0, j1, u, gate); return;
+        LN_UPS(1) LN_UPS(2) LN_UPS(3) LN_UPS(4) LN_UPS(6)
+#undef LN_UPS
+        default: break;
+        }
+    }
+    hipLaunchKernelGGL(k_ln_upsample, grid(j1 - j0), dim3(AMX_BLOCK), 0, st, x, n_in, r, j0, j1, u, gate);
+}
+
 hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x, int64_t n_in,
                            const SwrDev &r, hipStream_t st) {
     if (ln.n192 <= 0) return hipSuccess;
-    // grid-stride over at most 8192 workgroups: a gated (linear) track's launch then
-    // dispatches a bounded number of workgroups that return at once
-    const int64_t nb = (ln.n192 + AMX_BLOCK - 1) / AMX_BLOCK;
-    hipLaunchKernelGGL(k_ln_upsample, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(AMX_BLOCK),
-                       0, st, x, n_in, r, (int64_t)0, ln.n192, ln.u, lp.gate);
+    ln_upsample(x, n_in, r, 0, ln.n192, ln.u, lp.gate, st);
     hipLaunchKernelGGL(k_lp_stats, dim3(1 + (lp.T + LP_STAT_F - 1) / LP_STAT_F), dim3(LP_STAT_NT), 0, st, lp);
     hipLaunchKernelGGL(k_ln_dyn, dim3(1), dim3(LN_NT), 0, st, ln, 0);
     hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
@@ -1651,10 +1742,7 @@ hipError_t launch_loudnorm_shard(const LnArgs &ln, const LpArgs &lp, const uint3
                                  const SwrDev &r, int64_t u_lo, int64_t u_hi, int part, hipStream_t st) {
     if (ln.n192 <= 0) return hipSuccess;
     if (part == 0) {
-        const int64_t nb = (u_hi - u_lo + AMX_BLOCK - 1) / AMX_BLOCK;
-        if (nb > 0)
-            hipLaunchKernelGGL(k_ln_upsample, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(AMX_BLOCK), 0, st, x,
-                               n_in, r, u_lo, u_hi, ln.u, lp.gate);
+        ln_upsample(x, n_in, r, u_lo, u_hi, ln.u, lp.gate, st);
         hipLaunchKernelGGL(k_lp_stats, dim3(1 + (lp.T + LP_STAT_F - 1) / LP_STAT_F), dim3(LP_STAT_NT), 0, st, lp);
     } else if (part == 1) {
         hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);

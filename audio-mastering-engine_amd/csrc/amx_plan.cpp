@@ -1304,7 +1304,9 @@ LnLayout ln_layout(int64_t n192) {
     l.J = t_ok >= 1 + l.Fs ? (t_ok - 1) / l.Fs : 0;
     l.M = (29 + l.Fs - 1) / l.Fs;
     l.K = 1 + l.J + l.M;
-    l.P = std::min(l.K, 1024);
+    int pmax = 1024;                       // persistent k_lp_seg waves (measurements: AMX_LN_P)
+    if (const char *ev = std::getenv("AMX_LN_P")) pmax = std::max(1, std::atoi(ev));
+    l.P = std::min(l.K, pmax);
     int64_t o = 0;
     auto take = [&](int64_t bytes) { const int64_t at = o; o += ((bytes + 255) / 256) * 256; return at; };
     l.o_u = take(n192 * 2 * (int64_t)sizeof(float));

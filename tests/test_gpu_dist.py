@@ -36,15 +36,18 @@ CASES = {
     # most segments start from a wrong guess, so the limiter state rank 0's walk hands
     # rank 1 decides rank 1's first segment
     "dynamic_nowarm": dict(bass_boost=1.0, lufs=-14.0),
+    # 44.1 kHz: the ranks' 192 kHz ranges of the filter come from the generic (M > 1)
+    # resampler form, each rank upsampling only what its segments read
+    "dynamic_44k1": dict(bass_boost=1.0, lufs=-14.0),
 }
 ENV = {"dynamic_nowarm": {"AMX_LN_SEG": "1", "AMX_LN_WARM": "0"}}
-RATE = {"c3_lufs_44k1": 44100}
+RATE = {"c3_lufs_44k1": 44100, "dynamic_44k1": 44100}
 
 
 # input gain per case: the loud case drives 0.1 % of the frames over the limit, so the final
 # alimiter (limit 0.98) must engage and the ranks hand its state along
 GAIN = {"c3_lufs": 1.0, "loud_limiter": 1.3, "square_limiter": 1.0, "c3_lufs_44k1": 1.0, "dynamic": 1.0,
-        "dynamic_nowarm": 1.0}
+        "dynamic_nowarm": 1.0, "dynamic_44k1": 1.0}
 
 
 def _track(seconds, case):
@@ -113,7 +116,8 @@ def test_two_ranks_match_one(gpu, case):
     if case.startswith("dynamic"):
         # the one-GPU reference: the whole track through master_array (dynamic_track)
         from amx.engine import master_array
-        y1, rep = master_array(torch.from_numpy(np.ascontiguousarray(x)), FS, CASES[case], quantum=512)
+        y1, rep = master_array(torch.from_numpy(np.ascontiguousarray(x)), RATE.get(case, FS), CASES[case],
+                               quantum=512)
         assert rep["modes"][0] == "dynamic" and rep["sample_rate"] == 192000
         y1 = y1.cpu().numpy()
     else:
