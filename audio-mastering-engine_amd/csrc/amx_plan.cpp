@@ -1288,24 +1288,30 @@ struct LnLayout {
     int64_t o_u = 0, o_ring = 0, o_ctl = 0, o_dctl = 0, o_v = 0, o_hold = 0, o_D = 0, o_G = 0, o_ramp = 0;
     int64_t o_recG = 0, o_recE = 0, o_wrec = 0, o_cnt = 0, o_match = 0, o_rings = 0, o_wring = 0, total = 0;
 };
-// INNER frames, segments of Fs frames (AMX_LN_SEG, default 4) each warmed up Wf frames
-// (AMX_LN_WARM, default 3) before its start, waves of k_lp_seg
+// INNER frames, segments of Fs frames each warmed up Wf frames (AMX_LN_WARM, default 2)
+// before its start, at most P persistent k_lp_seg waves (AMX_LN_P, default 2048: two per
+// SIMD).  Fs (AMX_LN_SEG overrides) is the smallest >= 2 whose segments fit the P waves: a
+// wave then runs one segment, Fs + Wf frames (r04m: a 5-min track 11.9 -> 9.1 ms per
+// dynamic step from Fs 4 / Wf 3 / 1024 waves); a longer track takes longer segments, so
+// the warm-up share Wf / Fs shrinks instead of waves running several segments each.
 LnLayout ln_layout(int64_t n192) {
     LnLayout l;
-    if (const char *ev = std::getenv("AMX_LN_SEG")) l.Fs = std::max(1, std::atoi(ev));
-    if (const char *ev = std::getenv("AMX_LN_WARM")) l.Wf = std::max(0, std::atoi(ev));
+    l.Wf = 2;
+    int pmax = 2048;
+    if (const char *ev = std::getenv("AMX_LN_P")) pmax = std::max(64, std::atoi(ev));
     if (n192 >= LN_FIRST_FRAMES) {
         l.T = (int)((n192 - LN_FIRST_FRAMES + 19199) / 19200);
         l.nb_last = l.T > 0 ? (int)(n192 - LN_FIRST_FRAMES - 19200LL * (l.T - 1)) : 0;
     }
+    l.Fs = std::max(2, (l.T + (pmax - 32) - 1) / (pmax - 32));
+    if (const char *ev = std::getenv("AMX_LN_SEG")) l.Fs = std::max(1, std::atoi(ev));
+    if (const char *ev = std::getenv("AMX_LN_WARM")) l.Wf = std::max(0, std::atoi(ev));
     // boundaries only at full INNER frames (a partial last frame's wrap reads reach the
     // frame before it), at FINAL's start and inside FINAL
     const int t_ok = (l.T > 0 && l.nb_last == 19200) ? l.T : l.T - 1;
     l.J = t_ok >= 1 + l.Fs ? (t_ok - 1) / l.Fs : 0;
     l.M = (29 + l.Fs - 1) / l.Fs;
     l.K = 1 + l.J + l.M;
-    int pmax = 1024;                       // persistent k_lp_seg waves (measurements: AMX_LN_P)
-    if (const char *ev = std::getenv("AMX_LN_P")) pmax = std::max(1, std::atoi(ev));
     l.P = std::min(l.K, pmax);
     int64_t o = 0;
     auto take = [&](int64_t bytes) { const int64_t at = o; o += ((bytes + 255) / 256) * 256; return at; };
