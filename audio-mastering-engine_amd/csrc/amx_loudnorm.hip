@@ -1130,29 +1130,33 @@ __device__ __forceinline__ int64_t lp_pos(const LpFrame &f, int s) {
     return f.F - LP_RS + d;
 }
 
-// the fill value of a position (af_loudnorm filter_frame: FIRST, INNER, FINAL)
-__device__ __forceinline__ double2 lp_fill(const LpArgs &a, const LpWave &W, int64_t pos) {
-    if (W.f.fin) {
-        if (pos >= a.n) return make_double2(0.0, 0.0);
-        const float2 x = reinterpret_cast<const float2 *>(a.u)[pos];
-        const double g = a.G[a.T];
-        return make_double2(((double)x.x * g) * W.off, ((double)x.y * g) * W.off);
-    }
-    const float2 x = reinterpret_cast<const float2 *>(a.u)[pos];
-    if (pos < LP_RS) return make_double2(((double)x.x * W.d0) * W.off, ((double)x.y * W.d0) * W.off);
-    const int64_t q = pos - LP_RS;
-    const int t = (int)(q / LP_FR), i = (int)(q - (int64_t)t * LP_FR);
-    const double r = (t < a.T - 1 || a.nb_last == LP_FR) ? a.ramp[i] : (double)i / (double)a.nb_last;
-    const double g0 = a.G[t], g1 = a.G[t + 1];
-    const double g = g0 + (r * (g1 - g0));
-    return make_double2(((double)x.x * g) * W.off, ((double)x.y * g) * W.off);
-}
-
 __device__ __forceinline__ bool lp_flag(const LpWave &W, int s) { return (W.flags[s >> 5] >> (s & 31)) & 1u; }
 
+// the value a slot holds: the multiplied value if flagged, else its position's fill
+// (af_loudnorm filter_frame: FIRST u d0 offset, INNER u (gain ramp) offset, FINAL
+// u G_T offset, 0 past the track).  No control flow around the loads (a load inside a
+// divergent branch made the compiler wait for every outstanding load at the join, which
+// undid the scans' loads ahead): every operand is loaded -- an unflagged slot's ring
+// value from slot 0 (one line for the whole wave), the gain rows clamped in range -- and
+// the value selected
 __device__ __forceinline__ double2 lp_val(const LpArgs &a, const LpWave &W, int s) {
-    if (lp_flag(W, s)) return W.ring[s];
-    return lp_fill(a, W, lp_pos(W.f, s));
+    const bool fl = lp_flag(W, s);
+    const double2 rv = W.ring[fl ? s : 0];
+    const int64_t pos = lp_pos(W.f, s);
+    const bool fin = W.f.fin != 0;
+    const bool past = fin && pos >= a.n;
+    const float2 x = reinterpret_cast<const float2 *>(a.u)[past ? 0 : pos];
+    const int64_t q = pos - LP_RS > 0 ? pos - LP_RS : 0;
+    const int t = (int)(q / LP_FR), i = (int)(q - (int64_t)t * LP_FR);
+    const int tc = t < a.T - 1 ? t : a.T - 1;
+    const double r0 = a.ramp[i], g0 = a.G[tc], g1 = a.G[tc + 1], gT = a.G[a.T];
+    double r = r0;
+    if (!(t < a.T - 1 || a.nb_last == LP_FR)) r = (double)i / (double)a.nb_last;
+    const double gi = g0 + (r * (g1 - g0));
+    const double g = fin ? gT : (pos < LP_RS ? W.d0 : gi);
+    double2 v = make_double2(((double)x.x * g) * W.off, ((double)x.y * g) * W.off);
+    if (past) v = make_double2(0.0, 0.0);
+    return fl ? rv : v;
 }
 
 __device__ __forceinline__ void lp_clear_range(LpWave &W, int lo, int hi) {   // slots [lo, hi)
@@ -1201,7 +1205,7 @@ __device__ __forceinline__ void lp_env(const LpArgs &a, LpWave &W, int e0, int k
             int ss = e0 + i;
             if (ss >= LP_RS) ss -= LP_RS;
             s[p] = ss;
-            v[p] = i < k ? lp_val(a, W, ss) : make_double2(0.0, 0.0);
+            v[p] = lp_val(a, W, ss);                       // (i >= k: read, unused)
         }
 #pragma unroll
         for (int p = 0; p < 4; p++) {
@@ -1319,21 +1323,31 @@ __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, in
     return -1;
 }
 
-// the output of the frame: the ring from its first slot, clamped to the ceiling, s16
+// the output of the frame: the ring from its first slot, clamped to the ceiling, s16.
+// Four groups' values are loaded before any output is stored (the stores could alias
+// the loads for the compiler, which would otherwise wait out one load per group)
 __device__ __forceinline__ void lp_emit(const LpArgs &a, const LpWave &W) {
     const double ceiling = a.ceiling;
     uint32_t *y = reinterpret_cast<uint32_t *>(a.y);
-#pragma unroll 4
-    for (int i0 = 0; i0 < W.f.nb; i0 += 64) {
-        const int i = i0 + (int)threadIdx.x;
-        if (i < W.f.nb) {
+    const int nb = W.f.nb;
+    for (int i00 = 0; i00 < nb; i00 += 256) {
+        double2 v[4];
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            const int i = i00 + 64 * p + (int)threadIdx.x;
             int s = W.f.lbi + i;
-            if (s >= LP_RS) s -= LP_RS;
-            const double2 v = lp_val(a, W, s);
-            double o0 = v.x, o1 = v.y;
-            if (fabs(o0) > ceiling) o0 = ceiling * (o0 < 0 ? -1 : 1);
-            if (fabs(o1) > ceiling) o1 = ceiling * (o1 < 0 ? -1 : 1);
-            y[W.f.base + i] = pack2(ln_s16(o0), ln_s16(o1));
+            while (s >= LP_RS) s -= LP_RS;
+            v[p] = lp_val(a, W, s);                        // (i >= nb: read, unused)
+        }
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            const int i = i00 + 64 * p + (int)threadIdx.x;
+            if (i < nb) {
+                double o0 = v[p].x, o1 = v[p].y;
+                if (fabs(o0) > ceiling) o0 = ceiling * (o0 < 0 ? -1 : 1);
+                if (fabs(o1) > ceiling) o1 = ceiling * (o1 < 0 ? -1 : 1);
+                y[W.f.base + i] = pack2(ln_s16(o0), ln_s16(o1));
+            }
         }
     }
 }
@@ -1547,7 +1561,7 @@ __device__ __forceinline__ void lp_wave_init(const LpArgs &a, LpWave &W, double2
 }
 
 // every segment at once (persistent waves): from rest Wf frames before its start
-__global__ void __launch_bounds__(64) k_lp_seg(LpArgs a) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_lp_seg(LpArgs a) {
     if (a.ctl[0] != 0 && a.ctl[0] != 4) return;
     const int kh = a.ctl[0] == 4 ? a.ctl[4] : 0;     // a quiet start: k_ln_dyn ran segments < kh
     __shared__ unsigned flags[LP_FW];
