@@ -259,43 +259,6 @@ __device__ __forceinline__ uint32_t gain_frame(const ChainDev &cd, uint32_t v, d
     return gain_apply(v, gain_factor(cd, att));
 }
 
-// gain_frame for K frames at once with their operations interleaved step by step (the
-// same operation sequence per frame): K independent exp10 chains in one instruction
-// stream, where the frame-at-a-time form left each chain's dependent latency exposed
-// (k_gain_overlay waited on dependencies 53 % of its cycles, r03)
-template <int K>
-__device__ __forceinline__ void gain_frames(const ChainDev &cd, const uint32_t *v, const double *att,
-                                            uint32_t *g) {
-    const double *E = cd.exc;
-    double q[K], x[K], k[K], r[K], u[K], p[K];
-#pragma unroll
-    for (int i = 0; i < K; i++) q[i] = -att[i] * E[15];
-#pragma unroll
-    for (int i = 0; i < K; i++) x[i] = fma(fma(-q[i], 20.0, -att[i]), E[15], q[i]);
-#pragma unroll
-    for (int i = 0; i < K; i++) k[i] = rint(x[i] * E[0]);
-#pragma unroll
-    for (int i = 0; i < K; i++) r[i] = fma(E[1], k[i], x[i]);
-#pragma unroll
-    for (int i = 0; i < K; i++) r[i] = fma(E[2], k[i], r[i]);
-#pragma unroll
-    for (int i = 0; i < K; i++) u[i] = r[i] * E[3];
-#pragma unroll
-    for (int i = 0; i < K; i++) u[i] = fma(E[4], r[i], u[i]);
-#pragma unroll
-    for (int i = 0; i < K; i++) p[i] = fma(E[5], u[i], E[6]);
-#pragma unroll
-    for (int j = 7; j < 15; j++)
-#pragma unroll
-        for (int i = 0; i < K; i++) p[i] = fma(u[i], p[i], E[j]);
-#pragma unroll
-    for (int i = 0; i < K; i++) p[i] = fma(u[i], p[i], 1.0);
-#pragma unroll
-    for (int i = 0; i < K; i++) p[i] = fma(u[i], p[i], 1.0);
-#pragma unroll
-    for (int i = 0; i < K; i++) g[i] = gain_apply(v[i], ldexp(p[i], (int)k[i]));
-}
-
 #define AMX_ENV_TF_ 16   // checkpoint spacing (frames)
 
 // lane i's value of a double, as a wave-uniform (scalar) operand
@@ -763,9 +726,6 @@ __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
 // the wave's loads still cover one contiguous 2 KB) and gathers m = mt[r] --
 // neighbouring threads hold neighbouring frames, so a gather touches few table lines.
 #define AMX_GO_XP 20       // sample / output row pitch in dwords (80 B)
-#ifndef AMX_GO_ILP
-#define AMX_GO_ILP 1       // frames whose gain chains run interleaved (1: frame at a time)
-#endif
 #define AMX_GO_WAVES (AMX_BLOCK / 64)
 template <bool RCP>
 __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__restrict__ cdp,
@@ -871,23 +831,11 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
                 for (int f = 0; f < AMX_ENV_TF_; f++) gv[f] = gain_apply(xv[f], g);
             }
         } else {
-#if AMX_GO_ILP > 1
-            // the attenuations first (the recurrence), then the gains AMX_GO_ILP frames at a time
-            double at[AMX_ENV_TF_];
-#pragma unroll
-            for (int f = 0; f < AMX_ENV_TF_; f++) {
-                att = env_step<RCP>(cd, att, mv[f]);
-                at[f] = att;
-            }
-#pragma unroll
-            for (int f = 0; f < AMX_ENV_TF_; f += AMX_GO_ILP) gain_frames<AMX_GO_ILP>(cd, xv + f, at + f, gv + f);
-#else
 #pragma unroll
             for (int f = 0; f < AMX_ENV_TF_; f++) {
                 att = env_step<RCP>(cd, att, mv[f]);
                 gv[f] = gain_frame(cd, xv[f], att);
             }
-#endif
         }
 #pragma unroll
         for (int f = 0; f < AMX_ENV_TF_; f++) {

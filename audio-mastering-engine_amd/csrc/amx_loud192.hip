@@ -53,9 +53,6 @@ namespace amx {
 #ifndef AMX_UP_WAVES
 #define AMX_UP_WAVES 4     // waves per SIMD the register budget must allow
 #endif
-#ifndef AMX_UP_PF
-#define AMX_UP_PF 1        // k_up_poly: the next output's bank and C A^n rows loaded one output ahead
-#endif
 
 __device__ __forceinline__ float up_sample(uint32_t w, int ch) {
     return (float)(ch ? hi16(w) : lo16(w)) * (1.0f / 32768.0f);
@@ -318,7 +315,6 @@ k_up_poly(UpArgs a) {
     for (int i = 0; i < W; i++) w[i] = up_sample(xp[i], ch);
     const int nblk = a.Lin / TB;
     int n = 0;                                                 // next output (wave-uniform)
-#if AMX_UP_PF
     // the rows of output n (bank row, C A^n row) are loaded while output n - 1 computes:
     // 40 scalar registers in flight instead of a scalar-cache miss on every output (the
     // 640 rows of 44.1 kHz are 80 KB)
@@ -328,7 +324,6 @@ k_up_poly(UpArgs a) {
     for (int i = 0; i < UP_TAPS; i++) h[i] = a.bankn[i];
 #pragma unroll
     for (int d = 0; d < AMX_KW_DIM; d++) r[d] = a.G[d];
-#endif
     for (int b = 0; b < nblk; b++) {
         uint32_t nx[TB];
         const int o0 = (b + 1 < nblk ? (b + 1) * TB : b * TB) + (W - TB);
@@ -342,7 +337,6 @@ k_up_poly(UpArgs a) {
             for (int o = 0; o < CMAX; o++) {
                 if (o < CMIN || o < c) {
                     __builtin_amdgcn_sched_barrier(AMX_UP_SB);
-#if AMX_UP_PF
                     const int nn = n + 1 < a.Lout ? n + 1 : n;
                     float hn[UP_TAPS];
                     double rn[AMX_KW_DIM];
@@ -357,9 +351,6 @@ k_up_poly(UpArgs a) {
                     for (int i = 0; i < UP_TAPS; i++) h[i] = hn[i];
 #pragma unroll
                     for (int d = 0; d < AMX_KW_DIM; d++) r[d] = rn[d];
-#else
-                    acc.add(n, UP_DOT(w + kb, a.bankn + (int64_t)n * UP_TAPS), w[kb + UP_C]);
-#endif
                     n++;
                 }
             }
