@@ -1147,7 +1147,15 @@ __device__ __forceinline__ double2 lp_val(const LpArgs &a, const LpWave &W, int 
     const bool past = fin && pos >= a.n;
     const float2 x = reinterpret_cast<const float2 *>(a.u)[past ? 0 : pos];
     const int64_t q = pos - LP_RS > 0 ? pos - LP_RS : 0;
-    const int t = (int)(q / LP_FR), i = (int)(q - (int64_t)t * LP_FR);
+    int t, i;
+    if (a.n < ((int64_t)1 << 31)) {             // wave-uniform: 32-bit quotient (tracks < 3.1 h)
+        const uint32_t q32 = (uint32_t)q;
+        t = (int)(q32 / (uint32_t)LP_FR);
+        i = (int)(q32 - (uint32_t)t * (uint32_t)LP_FR);
+    } else {
+        t = (int)(q / LP_FR);
+        i = (int)(q - (int64_t)t * LP_FR);
+    }
     const int tc = t < a.T - 1 ? t : a.T - 1;
     const double r0 = a.ramp[i], g0 = a.G[tc], g1 = a.G[tc + 1], gT = a.G[a.T];
     double r = r0;
@@ -1228,18 +1236,11 @@ __device__ __forceinline__ int lp_env_end(int e0, int k) {
 }
 
 #define LP_PD 4                  // lp_detect: groups of 64 positions loaded ahead
-// one group's values: 64 positions from slot s0, and the 12 after them (lanes < 12)
-__device__ __forceinline__ void lp_grp(const LpArgs &a, const LpWave &W, int s0, int lane, double2 &v,
-                                       double2 &v2) {
+// one group's values: 64 positions from slot s0
+__device__ __forceinline__ double2 lp_grp(const LpArgs &a, const LpWave &W, int s0, int lane) {
     int s = s0 + lane;
     while (s >= LP_RS) s -= LP_RS;
-    v = lp_val(a, W, s);
-    v2 = make_double2(0.0, 0.0);
-    if (lane < 12) {
-        int s2 = s0 + 64 + lane;
-        while (s2 >= LP_RS) s2 -= LP_RS;
-        v2 = lp_val(a, W, s2);
-    }
+    return lp_val(a, W, s);
 }
 // detect_peak from offset smp over count positions: peak_delta or -1; the peak's |x|
 // and slot.  64 positions per step: the first one that is a candidate with its
@@ -1257,17 +1258,19 @@ __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, in
     // only reads the ring, so a value loaded early is the value then): one memory round
     // trip per LP_PD groups instead of one per group.  Loads past count read slots of the
     // same ring window, in bounds, unused.
-    double2 q[LP_PD], q2[LP_PD];
+    // (the 12 positions after a group, for its look-ahead, are the next group's first 12:
+    // already loaded, LP_PD >= 2)
+    double2 q[LP_PD];
 #pragma unroll
-    for (int p = 0; p < LP_PD; p++) lp_grp(a, W, slot0 + p * 64, lane, q[p], q2[p]);
+    for (int p = 0; p < LP_PD; p++) q[p] = lp_grp(a, W, slot0 + p * 64, lane);
     for (int nb00 = 0; nb00 < count; nb00 += 64 * LP_PD)
 #pragma unroll
     for (int p = 0; p < LP_PD; p++) {
         const int nb0 = nb00 + 64 * p;
         if (nb0 >= count) break;
         {
-            const double2 v = q[p], v2 = q2[p];
-            lp_grp(a, W, slot0 + nb0 + 64 * LP_PD, lane, q[p], q2[p]);
+            const double2 v = q[p], v2 = q[(p + 1) % LP_PD];
+            q[p] = lp_grp(a, W, slot0 + nb0 + 64 * LP_PD, lane);
             __syncthreads();                   // the previous group's serial reads are done
             st0[lane] = fabs(v.x);
             st1[lane] = fabs(v.y);
