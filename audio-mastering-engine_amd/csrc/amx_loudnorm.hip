@@ -64,6 +64,25 @@ __device__ __forceinline__ float ln_dot(const float *w, const float *__restrict_
     return (b0 + b2) + (b1 + b3);
 }
 
+typedef float ln_f2 __attribute__((ext_vector_type(2)));
+
+// ln_dot with the 8 chains as 4 packed pairs (v_pk_fma_f32 / v_pk_add_f32): the same
+// operations lane by lane, the first term a fused multiply-add onto 0 as in ln_dot
+__device__ __forceinline__ float ln_dot2(const float *w, const float *__restrict__ h) {
+    ln_f2 acc4[4];
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {
+        ln_f2 acc = __builtin_elementwise_fma(ln_f2{w[k], w[k + 1]}, ln_f2{h[k], h[k + 1]}, ln_f2{0.0f, 0.0f});
+        acc = __builtin_elementwise_fma(ln_f2{w[k + 8], w[k + 9]}, ln_f2{h[k + 8], h[k + 9]}, acc);
+        acc = __builtin_elementwise_fma(ln_f2{w[k + 16], w[k + 17]}, ln_f2{h[k + 16], h[k + 17]}, acc);
+        acc = __builtin_elementwise_fma(ln_f2{w[k + 24], w[k + 25]}, ln_f2{h[k + 24], h[k + 25]}, acc);
+        acc4[k >> 1] = acc;
+    }
+    const ln_f2 b01 = acc4[0] + acc4[2], b23 = acc4[1] + acc4[3];
+    const ln_f2 c = b01 + b23;
+    return c.x + c.y;
+}
+
 // The M == 1 rates (192 kHz / L: 48 kHz L = 4, 96 kHz 2, 64 kHz 3, 32 kHz 6, 192 kHz 1):
 // output j = frame j / L, phase j % L.  One thread per input frame: its 32-frame window
 // once, then the L outputs with the bank rows as wave-uniform operands (k_ln_upsample's
@@ -96,7 +115,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_ln_up_static(const uint32_t *__re
         for (int ph = 0; ph < L; ph++) {
             const int64_t j = f * L + ph;
             const float *h = bank + ph * LN_TAPS;
-            const float a = ln_dot(w0, h), b = ln_dot(w1, h);
+            const float a = ln_dot2(w0, h), b = ln_dot2(w1, h);
             if (j >= j0 && j < j1) *reinterpret_cast<float2 *>(u + 2 * j) = make_float2(a, b);
         }
     }
@@ -897,7 +916,7 @@ __global__ void __launch_bounds__(LN_NT) k_ln_dyn(LnArgs a0, int phase) {
 #define LP_REC AMX_LN_REC
 #define LP_WIN AMX_LN_WIN
 #define LP_STAT_NT 256
-#define LP_STAT_F 16             // INNER frames per k_lp_stats workgroup
+#define LP_STAT_F 4              // INNER frames per k_lp_stats workgroup (16: 135 us per run at C3)
 #define LP_DIRTY 7               // record slot: 1 = a flagged slot lies outside the window
 
 enum { LO_OUT = 0, LO_ATTACK, LO_SUSTAIN, LO_RELEASE };
