@@ -416,3 +416,72 @@ def test_batch_several_dynamic(gpu, oracle_mod):
         x16 = oracle_mod.quantize(x)
         ref, rinfo = oracle_mod.pipeline(x16, fs, settings, chunk_bounds(x16.shape[0], fs, 512))
         _cmp(job.track_output(t).cpu().numpy(), ref, "several-dynamic batch track %d (%s)" % (t, rinfo["mode"]))
+
+
+@pytest.mark.parametrize("ranks,seg,warm", [(3, None, None), (3, 1, 0), (2, 2, 1)])
+def test_shard_parts_vs_oracle(gpu, oracle_mod, monkeypatch, ranks, seg, warm):
+    """amx_loudnorm_192k_segments / amx_loudnorm_192k_shard through the C ABI, the
+    ranks simulated in order in one process, each with its own scratch: part 0 (its
+    192 kHz range + every frame's statistics), part 1 (its segments from guessed
+    states), part 2 (its walk from the state record the previous one left).  The runs
+    of the 192 kHz output, concatenated, must be the oracle's filter output -- with
+    one-frame segments and no warm-up most guesses are wrong, so the records decide."""
+    import ctypes
+    import torch
+    from amx import capi
+    from amx.dist import shard_segments
+    from amx.engine import MasteringJob
+    if seg is not None:
+        monkeypatch.setenv("AMX_LN_SEG", str(seg))
+        monkeypatch.setenv("AMX_LN_WARM", str(warm))
+    fs = 48000
+    x = _dynamic_signal(20.0, fs, 17)
+    x16 = oracle_mod.quantize(x)
+    st = oracle_mod.loudnorm_measure(x16, fs)
+    job = MasteringJob(fs, 2, {"lufs": -14.0}, [x16.shape[0]], input_s16=True,
+                       chunks=[(0, 0, x16.shape[0])], measure_only=True)
+    job.out[:x16.shape[0]].copy_(torch.from_numpy(x16))
+    job.loudness_pass1(tail=False)
+    job.loudness_pass2(carry=False)
+    job.histograms()
+    job.decide()
+    n192, job2, _, summ = job._job192(0, cached=False)[0:4]
+    L = capi.load()
+    K, kf, rd, co = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+    capi.check(L.amx_loudnorm_192k_segments(job.plan.h, 0, None, 0, ctypes.byref(K), ctypes.byref(kf),
+                                            ctypes.byref(rd), ctypes.byref(co)), "segments")
+    starts = (ctypes.c_int64 * (K.value + 1))()
+    capi.check(L.amx_loudnorm_192k_segments(job.plan.h, 0, starts, K.value + 1, ctypes.byref(K), None, None,
+                                            None), "segments")
+    starts = list(starts)
+    assert starts[0] == 0 and starts[-1] == n192 and all(a < b for a, b in zip(starts, starts[1:]))
+    assert 0 < kf.value <= K.value
+    # a starts array too small is refused
+    small = (ctypes.c_int64 * K.value)()
+    assert L.amx_loudnorm_192k_segments(job.plan.h, 0, small, K.value, ctypes.byref(K), None, None, None) != 0
+    ranges = shard_segments(K.value, kf.value, ranks)
+    nb, wsb = ctypes.c_int64(), ctypes.c_int64()
+    capi.check(L.amx_loudnorm_192k_size(job.plan.h, 0, ctypes.byref(nb), ctypes.byref(wsb)), "size")
+    ws2s = [torch.empty(wsb.value, dtype=torch.uint8, device=job.device) for _ in range(ranks)]
+    recs = [torch.zeros(rd.value, dtype=torch.float64, device=job.device) for _ in range(ranks)]
+    for offset in (0.0, 9.0):
+        d = capi.LoudnormDesc(-14.0, 11.0, -1.5, float(st["input_i"]), float(st["input_lra"]),
+                              float(st["input_tp"]), float(st["input_thresh"]), offset)
+        job2.out.zero_()
+        for r, (kb, ke) in enumerate(ranges):
+            for part in (0, 1, 2):
+                sh = capi.LnShard(part, kb, ke, 0, -1, -1, capi.ptr(recs[r - 1]) if r > 0 else None,
+                                  capi.ptr(recs[r]) if r < ranks - 1 else None)
+                capi.check(L.amx_loudnorm_192k_shard(
+                    job.plan.h, 0, ctypes.byref(d), None, None, ctypes.byref(sh), capi.ptr(job.out),
+                    capi.ptr(job.hops), int(job.max_hops), capi.ptr(job.peak), capi.ptr(job2.out),
+                    capi.ptr(summ), capi.ptr(ws2s[r]), None), "shard")
+                ctl = int(ws2s[r][co.value:co.value + 4].view(torch.int32).item())
+                assert ctl == 0, (r, part, ctl)          # the parallel form ran, no fallback
+        ref, _ = oracle_mod.loudnorm(x16, fs, -14.0, measured=st, offset=offset)
+        _cmp(job2.out[:n192].cpu().numpy(), ref, "shard parts x%d Fs=%s Wf=%s offset %.1f" % (ranks, seg, warm, offset))
+    # a walk past the first segment without the previous state is refused
+    sh = capi.LnShard(2, ranges[1][0], ranges[1][1], 0, -1, -1, None, None)
+    assert L.amx_loudnorm_192k_shard(job.plan.h, 0, ctypes.byref(d), None, None, ctypes.byref(sh), capi.ptr(job.out),
+                                     capi.ptr(job.hops), int(job.max_hops), capi.ptr(job.peak), capi.ptr(job2.out),
+                                     capi.ptr(summ), capi.ptr(ws2s[1]), None) != 0
