@@ -1254,7 +1254,10 @@ __device__ __forceinline__ int lp_env_end(int e0, int k) {
     return e >= LP_RS ? e - LP_RS : e;
 }
 
-#define LP_PD 4                  // lp_detect: groups of 64 positions loaded ahead
+#ifndef AMX_LP_PD
+#define AMX_LP_PD 4              // (measurement builds: scripts/build_var.py)
+#endif
+#define LP_PD AMX_LP_PD          // lp_detect: groups of 64 positions loaded ahead
 // one group's values: 64 positions from slot s0
 __device__ __forceinline__ double2 lp_grp(const LpArgs &a, const LpWave &W, int s0, int lane) {
     int s = s0 + lane;
