@@ -1136,6 +1136,9 @@ struct LpWave {
     double2 *ring;         // [LP_RS] the multiplied slots' values (HBM)
     unsigned *flags;       // [LP_FW] LDS: slot multiplied since its last fill
     double *st;            // [2][80] LDS: |x| of a peak-scan group
+    double *gl;            // [8] LDS: G[tb .. tb + 7] (clamped to T), the gain rows the frame's slots use
+    int tb;
+    double gT;             // G[T] (FINAL's gain)
     LpFrame f;
     int mode, env_cnt, env_index, attack_length;
     double gr0, gr1;
@@ -1176,7 +1179,11 @@ __device__ __forceinline__ double2 lp_val(const LpArgs &a, const LpWave &W, int 
         i = (int)(q - (int64_t)t * LP_FR);
     }
     const int tc = t < a.T - 1 ? t : a.T - 1;
-    const double r0 = a.ramp[i], g0 = a.G[tc], g1 = a.G[tc + 1], gT = a.G[a.T];
+    // the gain rows from the frame's LDS copy (a slot of frame f holds a position of one of
+    // the <= 4 INNER frames from tb, lp_gload): LDS reads instead of 3 vector loads
+    int k = tc - W.tb;
+    k = k < 0 ? 0 : (k > 6 ? 6 : k);
+    const double r0 = a.ramp[i], g0 = W.gl[k], g1 = W.gl[k + 1], gT = W.gT;
     double r = r0;
     if (!(t < a.T - 1 || a.nb_last == LP_FR)) r = (double)i / (double)a.nb_last;
     const double gi = g0 + (r * (g1 - g0));
@@ -1184,6 +1191,17 @@ __device__ __forceinline__ double2 lp_val(const LpArgs &a, const LpWave &W, int 
     double2 v = make_double2(((double)x.x * g) * W.off, ((double)x.y * g) * W.off);
     if (past) v = make_double2(0.0, 0.0);
     return fl ? rv : v;
+}
+
+// the frame's gain rows into LDS: positions [F - LP_RS, F) fall in INNER frames
+// t = (pos - LP_RS) / LP_FR >= tb; the caller synchronises before lp_val reads them
+__device__ __forceinline__ void lp_gload(const LpArgs &a, LpWave &W) {
+    const int64_t q = W.f.F - 2 * (int64_t)LP_RS;
+    W.tb = q > 0 ? (int)(q / LP_FR) : 0;
+    if (threadIdx.x < 8) {
+        const int t = W.tb + (int)threadIdx.x;
+        W.gl[threadIdx.x] = a.G[t < a.T ? t : a.T];
+    }
 }
 
 __device__ __forceinline__ void lp_clear_range(LpWave &W, int lo, int hi) {   // slots [lo, hi)
@@ -1215,6 +1233,7 @@ __device__ __forceinline__ void lp_refill(const LpArgs &a, LpWave &W, int phi) {
         lp_clear_range(W, s0, min(s0 + cnt, LP_RS));
         if (s0 + cnt > LP_RS) lp_clear_range(W, 0, s0 + cnt - LP_RS);
     }
+    lp_gload(a, W);
     __syncthreads();
 }
 
@@ -1530,6 +1549,7 @@ __device__ __forceinline__ void lp_snapshot(const LpArgs &a, const LpWave &W, do
 // the same state back into a wave (every window slot flagged with its recorded value)
 __device__ __forceinline__ void lp_restore(const LpArgs &a, LpWave &W, const double *rec, int phi) {
     W.f = lp_frame(a, phi);
+    lp_gload(a, W);
     W.mode = (int)rec[0];
     W.env_cnt = (int)rec[1];
     W.env_index = (int)rec[2];
@@ -1581,6 +1601,9 @@ __device__ __forceinline__ void lp_wave_init(const LpArgs &a, LpWave &W, double2
     W.ring = ring;
     W.flags = flags;
     W.st = st;
+    W.gl = st + 160;
+    W.tb = 0;
+    W.gT = a.G[a.T];
     W.d0 = a.dctl[0];
     W.off = a.dctl[1];
 }
@@ -1590,7 +1613,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     if (a.ctl[0] != 0 && a.ctl[0] != 4) return;
     const int kh = a.ctl[0] == 4 ? a.ctl[4] : 0;     // a quiet start: k_ln_dyn ran segments < kh
     __shared__ unsigned flags[LP_FW];
-    __shared__ double st[160];
+    __shared__ double st[168];
     LpWave W;
     lp_wave_init(a, W, reinterpret_cast<double2 *>(a.rings) + (int64_t)blockIdx.x * LP_RS, flags, st);
     const int NF = a.T + 1 + LP_NFIN;
@@ -1641,7 +1664,7 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
     if (a.ctl[0] != 0 && a.ctl[0] != 4) return;
     const int kh = a.ctl[0] == 4 ? a.ctl[4] : 0;
     __shared__ unsigned flags[LP_FW];
-    __shared__ double st[160];
+    __shared__ double st[168];
     LpWave W;
     lp_wave_init(a, W, reinterpret_cast<double2 *>(a.wring), flags, st);
     const int lane = threadIdx.x;
