@@ -643,7 +643,9 @@ class Span192(ShardedTrack):
     mode (ShardedTrack._dynamic_sharded): a measure-only job over the frames of its
     filter segments with ShardedTrack's exchanges -- edges (the alimiter's halo),
     K-filter tails + sample peaks (all-gather), hop energies (all-reduce), the
-    alimiter's state hand-off (chain_state_speculative)."""
+    alimiter's state hand-off (chain_state_speculative).  Only those exchange methods
+    and measure() / limit() are used on it: it has no chunks, so ShardedTrack's
+    step / capture / replay do not apply."""
 
     def __init__(self, spans, rank, world, group, lufs, device):
         self.rank, self.world, self.group = rank, world, group
