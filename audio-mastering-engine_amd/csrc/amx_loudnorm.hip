@@ -1609,7 +1609,11 @@ __device__ __forceinline__ void lp_wave_init(const LpArgs &a, LpWave &W, double2
 }
 
 // every segment at once (persistent waves): from rest Wf frames before its start
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_lp_seg(LpArgs a) {
+#ifndef AMX_LP_WPE
+#define AMX_LP_WPE 3             // k_lp_seg waves per SIMD the register budget allows (168
+                                 // VGPRs, a 300-B spill; 2: C5 dynamic 43.0 vs 40.9 ms)
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AMX_LP_WPE))) k_lp_seg(LpArgs a) {
     if (a.ctl[0] != 0 && a.ctl[0] != 4) return;
     const int kh = a.ctl[0] == 4 ? a.ctl[4] : 0;     // a quiet start: k_ln_dyn ran segments < kh
     __shared__ unsigned flags[LP_FW];
