@@ -39,6 +39,10 @@ CASES = {
     # 44.1 kHz: the ranks' 192 kHz ranges of the filter come from the generic (M > 1)
     # resampler form, each rank upsampling only what its segments read
     "dynamic_44k1": dict(bass_boost=1.0, lufs=-14.0),
+    # a quiet 6 s intro: the filter starts below measured_thresh (above_threshold 0), a
+    # feedback loop the parallel form does not split -- every rank runs both filter runs
+    # whole, the 192 kHz measurement and alimiter still over the ranks' runs
+    "dynamic_quiet": dict(bass_boost=1.0, lufs=-14.0),
 }
 ENV = {"dynamic_nowarm": {"AMX_LN_SEG": "1", "AMX_LN_WARM": "0"}}
 RATE = {"c3_lufs_44k1": 44100, "dynamic_44k1": 44100}
@@ -47,7 +51,7 @@ RATE = {"c3_lufs_44k1": 44100, "dynamic_44k1": 44100}
 # input gain per case: the loud case drives 0.1 % of the frames over the limit, so the final
 # alimiter (limit 0.98) must engage and the ranks hand its state along
 GAIN = {"c3_lufs": 1.0, "loud_limiter": 1.3, "square_limiter": 1.0, "c3_lufs_44k1": 1.0, "dynamic": 1.0,
-        "dynamic_nowarm": 1.0, "dynamic_44k1": 1.0}
+        "dynamic_nowarm": 1.0, "dynamic_44k1": 1.0, "dynamic_quiet": 1.0}
 
 
 def _track(seconds, case):
@@ -61,6 +65,8 @@ def _track(seconds, case):
         rng = np.random.default_rng(11)
         for k in rng.integers(0, n - 200, max(2, int(seconds * 2))):
             x[k:k + 50] += rng.uniform(-0.9, 0.9, (50, 2))
+        if case == "dynamic_quiet":
+            x[:int(6 * fs)] *= 0.0005
         return np.clip(x, -1.0, 1.0).astype(np.float32)
     return (synth.mix_like(n, fs, 2, seed=3) * np.float32(GAIN[case])).astype(np.float32)
 
@@ -133,7 +139,9 @@ def test_two_ranks_match_one(gpu, case):
     assert fast[0] == fast[1]
     if case.startswith("dynamic"):
         # both filter runs split over the ranks by segments, with the limiter-state hand-off
-        assert forms == ["sharded"] * 2, forms
+        # (a quiet start: both run whole on every rank)
+        want = "replicated+replicated" if case == "dynamic_quiet" else "sharded"
+        assert forms == [want] * 2, forms
     # the loud case must exercise the rank-to-rank sequential limiter
     if not case.startswith("dynamic"):
         assert fast[0] == case.startswith("c3_lufs"), "limiter fast path %s" % fast[0]
