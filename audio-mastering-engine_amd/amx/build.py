@@ -63,18 +63,51 @@ def needs_build():
     return built_hash() != source_hash()
 
 
+def _obj_key(src):
+    """cache key of one object: the source, the shared headers and the flags"""
+    h = hashlib.sha256()
+    for p in [src] + [os.path.join(CSRC, f) for f in HEADERS] + [HEADER]:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()[:24]
+
+
 def build(force=False, verbose=False):
+    """Compile every source to an object (in parallel, objects cached by content under
+    build/amx_obj/), then link libamx.so.  Only amx_plan.cpp carries the stamp, so a
+    change to one kernel file recompiles that file and the stamp's object."""
     if not force and not needs_build():
         return OUT
+    from concurrent.futures import ThreadPoolExecutor
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    obj_dir = os.path.join(PKG, "..", "build", "amx_obj")
+    os.makedirs(obj_dir, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = ([hipcc] + FLAGS + ['-DAMX_SRC_HASH="%s"' % source_hash()] +
-           [os.path.join(CSRC, s) for s in SOURCES] + ["-o", OUT + ".tmp"])
-    r = subprocess.run(cmd, capture_output=True, text=True)
+    cflags = [f for f in FLAGS if f != "-shared"]
+    stamp = source_hash()
+
+    def compile_one(s):
+        src = os.path.join(CSRC, s)
+        extra = ['-DAMX_SRC_HASH="%s"' % stamp] if s == "amx_plan.cpp" else []
+        key = _obj_key(src) + ("-" + stamp[:16] if extra else "")
+        obj = os.path.join(obj_dir, "%s.%s.o" % (s, key))
+        if force or not os.path.exists(obj):
+            r = subprocess.run([hipcc] + cflags + extra + ["-c", src, "-o", obj + ".tmp"],
+                               capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError("hipcc failed on %s:\n%s%s" % (s, r.stdout, r.stderr))
+            if verbose and (r.stdout or r.stderr):
+                print(r.stdout + r.stderr)
+            os.replace(obj + ".tmp", obj)
+        return obj
+
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 1), 16))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    r = subprocess.run([hipcc] + FLAGS + objs + ["-o", OUT + ".tmp"], capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
-    if verbose and (r.stdout or r.stderr):
-        print(r.stdout + r.stderr)
+        raise RuntimeError("hipcc link failed:\n" + r.stdout + r.stderr)
     os.replace(OUT + ".tmp", OUT)
     return OUT
 

@@ -420,7 +420,7 @@ class ShardedTrack:
             capi.check(L.amx_loudnorm_192k_shard(
                 W.plan.h, 0, ctypes.byref(desc), capi.ptr(measured), capi.ptr(offset_i), ctypes.byref(sh),
                 capi.ptr(W.out), capi.ptr(W.hops), int(W.max_hops), capi.ptr(W.peak), capi.ptr(job2.out),
-                capi.ptr(summ), capi.ptr(ws2), None), "amx_loudnorm_192k_shard")
+                capi.ptr(summ), capi.ptr(ws2), W._s(None)), "amx_loudnorm_192k_shard")
 
         ctl = ws2[sp["ctl"]:sp["ctl"] + 4].view(torch.int32)
         part(0)

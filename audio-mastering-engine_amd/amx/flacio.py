@@ -33,10 +33,12 @@ def is_flac(path):
     return head[o:o + 4] == b"fLaC"
 
 
-# samples per byte a FLAC stream can reach at most in practice (constant subframes of
-# the largest blocks: ~65535 samples in ~16 bytes); a STREAMINFO length beyond it is
-# not trusted for the allocation
-_MAX_SAMPLES_PER_BYTE = 4096
+# samples per byte a FLAC stream can reach at most: a frame of the largest block
+# (65535 samples) is at least ~11 bytes (a 6-byte header + the 16-bit block size, one
+# constant subframe of 2 bytes, the CRC-16), i.e. <= ~5958 samples per byte; a
+# STREAMINFO length beyond 6144 per byte is not trusted for the allocation (a size
+# query decides it first), so valid streams -- long silence included -- decode once
+_MAX_SAMPLES_PER_BYTE = 6144
 
 
 def decode_flac(data, threads=0, with_blocks=False):

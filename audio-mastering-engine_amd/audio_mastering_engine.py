@@ -69,6 +69,24 @@ def _device_input(path):
     return d_in, info.sample_rate, frames, 2, True, info
 
 
+def _normalize(job):
+    """normalize_loudness_on_disk_with_ffmpeg (:227-242) on the device: the rest of pass
+    1's measurement, the statistics and decision; dynamic mode (:240 when the linear
+    conditions fail) runs the 192 kHz path and returns its (output, info), linear
+    mode (and the -inf skip, :238) returns None -- the gain rides in amx_finalize."""
+    job.loudness_pass2(carry=False)
+    job.histograms()
+    job.decide()
+    report = job.fetch_report(raise_dynamic=False)
+    mode = report["modes"][0] if report["modes"] else "off"
+    if mode == "skip":
+        logging.warning("Measured loudness is -inf (silent audio). Skipping normalization.")
+    if mode == "dynamic":
+        # loudnorm pass 2 in dynamic mode (:240): 192 kHz AGC + true-peak limiter
+        return job.dynamic_track(0, report["stats"][0])
+    return None
+
+
 def master_audio(settings, status_callback=None, progress_callback=None):
     import torch
     from amx.engine import MasteringJob
@@ -99,21 +117,26 @@ def master_audio(settings, status_callback=None, progress_callback=None):
     status("Re-assembling processed chunks with concat filter...")           # :205
     progress(num_chunks + 1, total_steps)                                     # :206
     status("Concatenation complete.")                                         # :213
+    # the sample peaks the limiter's path decision needs (and, with lufs, the first
+    # half of loudnorm's 192 kHz measurement)
     job.loudness_pass1()
+    dyn = None
     if settings.get("lufs") is not None:                                      # :216
         status("Normalizing final loudness...")                               # :217
         progress(num_chunks + 2, total_steps)                                 # :218
-        job.loudness_pass2(carry=False)
-        job.histograms()
-    job.decide()
-    report = job.fetch_report(raise_dynamic=False)
-    mode = report["modes"][0] if report["modes"] else "off"
-    if mode == "skip":
-        logging.warning("Measured loudness is -inf (silent audio). Skipping normalization.")
-    dyn = None
-    if mode == "dynamic":
-        # loudnorm pass 2 in dynamic mode (:240): 192 kHz AGC + true-peak limiter
-        dyn = job.dynamic_track(0, report["stats"][0])
+        try:
+            dyn = _normalize(job)
+        except Exception as e:                                                # :243-246
+            # the reference logs any normalisation error and carries on with a copy of
+            # the unnormalised track: here the track is finalised without the gain
+            logging.exception("Error during disk-based normalization.")
+            if isinstance(e, subprocess.CalledProcessError):
+                logging.error(f"FFMPEG STDERR:\n{e.stderr}")
+            dyn = None
+            job.dd.lufs_on = 0
+            job.decide()
+    else:
+        job.decide()
     status("Applying final limiting and exporting...")                        # :221
     progress(num_chunks + 3, total_steps)                                     # :222
     if dyn is None:

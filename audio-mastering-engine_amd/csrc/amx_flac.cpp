@@ -267,19 +267,22 @@ bool subframe(BitReader &br, int block, int bps, int64_t *s) {
         for (int i = 0; i < order; i++) s[i] = br.sbits(eb);
         if (!residual(br, block, order, s)) return false;
         // the predictors in wrapping uint64 arithmetic: a hostile stream's residuals can
-        // push them past int64 (undefined for signed); a valid stream never wraps
-        for (int i = order; i < block; i++) {
-            uint64_t pred = 0;
-            const uint64_t a = (uint64_t)s[i - 1];
-            switch (order) {
-            case 1: pred = a; break;
-            case 2: pred = 2 * a - (uint64_t)s[i - 2]; break;
-            case 3: pred = 3 * a - 3 * (uint64_t)s[i - 2] + (uint64_t)s[i - 3]; break;
-            case 4: pred = 4 * a - 6 * (uint64_t)s[i - 2] + 4 * (uint64_t)s[i - 3] - (uint64_t)s[i - 4]; break;
-            default: break;
+        // push them past int64 (undefined for signed); a valid stream never wraps.
+        // Order 0 predicts 0: the samples are the residuals (and s[i - 1] would read
+        // before the subframe at i = 0 -- found by the host ASan build, test_sanitize.py)
+        if (order > 0)
+            for (int i = order; i < block; i++) {
+                uint64_t pred = 0;
+                const uint64_t a = (uint64_t)s[i - 1];
+                switch (order) {
+                case 1: pred = a; break;
+                case 2: pred = 2 * a - (uint64_t)s[i - 2]; break;
+                case 3: pred = 3 * a - 3 * (uint64_t)s[i - 2] + (uint64_t)s[i - 3]; break;
+                case 4: pred = 4 * a - 6 * (uint64_t)s[i - 2] + 4 * (uint64_t)s[i - 3] - (uint64_t)s[i - 4]; break;
+                default: break;
+                }
+                s[i] = (int64_t)((uint64_t)s[i] + pred);
             }
-            s[i] = (int64_t)((uint64_t)s[i] + pred);
-        }
     } else if (type >= 32) {
         const int order = type - 31;
         if (order > block) return false;

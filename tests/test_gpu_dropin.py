@@ -125,6 +125,54 @@ def test_master_audio_rates_inexact_192k_resampler(gpu, oracle_mod, fs, lufs):
         assert rep["stats"][0] == rinfo["stats"], (rep["stats"][0], rinfo["stats"])
 
 
+@pytest.mark.parametrize("stage", ["loudness_pass2", "histograms", "dynamic_track"])
+def test_master_audio_normalization_failure_fallback(gpu, oracle_mod, monkeypatch, caplog, stage):
+    """:243-246: any error inside the loudness normalisation is logged and the
+    unnormalised track goes on to the alimiter -- the output equals the oracle's
+    pipeline with lufs=None, and the status / progress sequence is the reference's
+    (with the "Normalizing final loudness..." step, which ran and failed)."""
+    import logging
+    import audio_mastering_engine as ame
+    from amx import capi, engine, synth, wavio
+    from amx.chunking import chunk_bounds, packet_frames
+    fs = 48000
+    n = int(fs * 34.0)
+    x = synth.mix_like(n, fs, 2, seed=34)
+    if stage == "dynamic_track":
+        # a quiet programme with full-scale bursts: loudnorm takes dynamic mode
+        x = x * np.float32(0.12)
+        rng = np.random.default_rng(3)
+        for k in rng.integers(0, n - 200, 60):
+            x[k:k + 50] += rng.uniform(-0.9, 0.9, (50, 2)).astype(np.float32)
+        x = np.clip(x, -1.0, 1.0).astype(np.float32)
+
+    def boom(*a, **k):
+        raise capi.AmxError("injected failure in %s" % stage)
+    monkeypatch.setattr(engine.MasteringJob, stage, boom)
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "in.wav"), os.path.join(d, "out.wav")
+        wavio.write_wav_f32(src, x, fs)
+        st, pr = [], []
+        with caplog.at_level(logging.ERROR):
+            out = ame.master_audio(dict(C3, input_file=src, output_file=dst), st.append,
+                                   lambda a, b: pr.append((a, b)))
+        assert out == dst
+        y, info = wavio.read_wav_native(dst)
+        bounds = chunk_bounds(n, fs, packet_frames(8))
+    assert "Error during disk-based normalization." in caplog.text
+    want_st, want_pr = _expected_calls(len(bounds), True)
+    assert st == want_st and pr == want_pr
+    x16 = oracle_mod.quantize(x)
+    if stage == "dynamic_track":
+        _, rinfo = oracle_mod.pipeline(x16, fs, C3, bounds)
+        assert rinfo["mode"] == "dynamic", rinfo.get("stats")
+    ref, _ = oracle_mod.pipeline(x16, fs, dict(C3, lufs=None), bounds)
+    assert info.sample_rate == fs
+    assert y.shape == ref.shape
+    dd = np.abs(y.astype(np.int32) - ref.astype(np.int32))
+    assert dd.max() == 0, "max |diff| %d LSB" % dd.max()
+
+
 def test_master_audio_192k_dynamic(gpu, oracle_mod):
     """a 192 kHz input that loudnorm sends to dynamic mode: ffmpeg inserts no resampler
     (only s16 -> dbl), the filter and the alimiter run at the input rate"""
