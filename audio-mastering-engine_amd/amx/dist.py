@@ -525,18 +525,20 @@ class ShardedTrack:
     # -------------------------------------------------------------- the step
     def capture(self, d_in):
         """Record the step's device work as hipGraphs (torch.cuda.CUDAGraph over HIP
-        stream capture).  One rank: the whole step (MasteringJob.capture).  N ranks:
-        the stretches between the step's three collectives, each one graph:
-          G1  chunk chain, packing the span's edge frames;
+        stream capture).  One rank: the whole step (MasteringJob.capture).  N ranks over
+        RCCL: the whole step as ONE graph with its three collectives captured as nodes:
+          chunk chain, packing the span's edge frames;
           all-gather of the edges;
-          G2  unpacking them, loudness pass 1 (GEMV + scan from rest + tail + peaks),
-              packing tail and peaks;
+          unpacking them, loudness pass 1 (GEMV + scan from rest + tail + peaks),
+          packing tail and peaks;
           all-gather of tails and peaks;
-          G3  carry (amx_kw_carry), peak = max over ranks, loudness pass 2;
+          carry (amx_kw_carry), peak = max over ranks, loudness pass 2;
           all-reduce(SUM) of the hop energies (loudnorm on);
-          G4  histograms + decision + the limiter on the device's decision;
+          histograms + decision + the limiter on the device's decision, and the
+          decision word copied to pinned host memory;
         then the host reads the decision and, only if the limiter can engage, hands
-        its state rank to rank."""
+        its state rank to rank.  Over gloo (host-staged collectives) the four stretches
+        between the collectives are four graphs and the collectives run eagerly."""
         if not self.xchg:
             return self.job.capture(d_in, dynamic=self.dyn)
         job = self.job
@@ -552,21 +554,46 @@ class ShardedTrack:
                     fn()
             return g
 
-        torch.cuda.synchronize()
-        g1 = seg(lambda: job.run_chunks(d_in), self._pack_edges)
-        g2 = seg(self._unpack_edges, lambda: job.loudness_pass1(tail=True), self._pack_x)
-        g3 = seg(self._unpack_x, lambda: job.loudness_pass2(carry=True)) if lufs_on else seg(self._unpack_x)
-
         # the limiter state is zeroed in the graph, so when the device picks the general
         # limiter the in-graph run IS the speculative from-rest run of
         # chain_state_speculative: replay() then only hands the end states along
         def fin():
             job.lim_state.zero_()
             job.finalize(None)
-        g4 = seg(job.histograms, job.decide, fin) if lufs_on else seg(job.decide, fin)
-        self._g = [g1, g2, g3, g4]
+
         self._ctl_host = torch.zeros(1, dtype=torch.int32).pin_memory()
         self._ctl_ev = torch.cuda.Event()
+        torch.cuda.synchronize()
+        if dist.get_backend(self.group) == "nccl":
+            # RCCL collectives are captured into the graph with the kernels around them
+            # (scripts/rccl_capture_probe.py): the whole step is ONE graph launch, its
+            # three collectives graph nodes on RCCL's stream -- no host launch between
+            # the stretches, and the decision word lands in pinned memory at the end
+            def whole():
+                job.run_chunks(d_in)
+                self._pack_edges()
+                self._all_gather(self._eall, self._ebuf)
+                self._unpack_edges()
+                job.loudness_pass1(tail=True)
+                self._pack_x()
+                self._all_gather(self._xall, self._xbuf)
+                self._unpack_x()
+                if lufs_on:
+                    job.loudness_pass2(carry=True)
+                    reduce_loudness(job.hops, None, self.group)
+                    job.histograms()
+                job.decide()
+                fin()
+                self._ctl_host.copy_(job.ctl[:1], non_blocking=True)
+            self._g = [seg(whole)]
+            return self._g
+        # gloo (the N-rank rehearsal on one GPU) stages every collective through host
+        # copies, which a graph cannot hold: the stretches between them are the graphs
+        g1 = seg(lambda: job.run_chunks(d_in), self._pack_edges)
+        g2 = seg(self._unpack_edges, lambda: job.loudness_pass1(tail=True), self._pack_x)
+        g3 = seg(self._unpack_x, lambda: job.loudness_pass2(carry=True)) if lufs_on else seg(self._unpack_x)
+        g4 = seg(job.histograms, job.decide, fin) if lufs_on else seg(job.decide, fin)
+        self._g = [g1, g2, g3, g4]
         return self._g
 
     def _one_rank_dynamic(self, y):
@@ -581,23 +608,28 @@ class ShardedTrack:
             return self._one_rank_dynamic(self.job.replay())
         from . import capi
         job = self.job
-        g1, g2, g3, g4 = self._g
-        g1.replay()
-        self._all_gather(self._eall, self._ebuf)
-        g2.replay()
-        self._all_gather(self._xall, self._xbuf)
-        g3.replay()
-        if job.dd.lufs_on:
-            reduce_loudness(job.hops, None, self.group)
-        g4.replay()
+        if len(self._g) == 1:
+            self._g[0].replay()                 # the whole step, collectives included
+        else:
+            g1, g2, g3, g4 = self._g
+            g1.replay()
+            self._all_gather(self._eall, self._ebuf)
+            g2.replay()
+            self._all_gather(self._xall, self._xbuf)
+            g3.replay()
+            if job.dd.lufs_on:
+                reduce_loudness(job.hops, None, self.group)
+            g4.replay()
+            self._ctl_host.copy_(job.ctl[:1], non_blocking=True)
         # The one host read of the step: RCCL operations are enqueued by the host, so
         # only the host can decide whether the limiter's rank-to-rank hand-off runs.
         # The word is the same on every rank (computed from all-reduced data); when it
         # says "idle" (the common case) the step is already complete on the device.
-        # Only this 4-byte copy is waited for, on the launch stream.
-        self._ctl_host.copy_(job.ctl[:1], non_blocking=True)
+        # Only this 4-byte copy is waited for: an event on the launch stream, polled
+        # (a blocking event wait sleeps and wakes late)
         self._ctl_ev.record()
-        self._ctl_ev.synchronize()
+        while not self._ctl_ev.query():
+            pass
         if is_dynamic(int(self._ctl_host[0])):
             return self.dynamic()
         if not (int(self._ctl_host[0]) & capi.CTL_FAST):

@@ -262,20 +262,26 @@ class MasteringJob:
         target = float(self.settings["lufs"])
         g = self.ctl[t:t + 1] if gate else None
         d1 = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
-        filt(d1, None, None)
-        job2.loudness_pass1(stream, tail=False)
-        job2.loudness_pass2(stream, carry=False)
-        job2.histograms(stream)
-        job2.dd.lufs_on = 1
-        job2.decide(stream)
-        with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
-            self._i_out[t:t + 1].copy_(job2.stats[0, 0:1])       # pass 1's output loudness
+        self.timed("ln_filter1", lambda: filt(d1, None, None), stream)
+
+        def measure1():
+            job2.loudness_pass1(stream, tail=False)
+            job2.loudness_pass2(stream, carry=False)
+            job2.histograms(stream)
+            job2.dd.lufs_on = 1
+            job2.decide(stream)
+            with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
+                self._i_out[t:t + 1].copy_(job2.stats[0, 0:1])       # pass 1's output loudness
+        self.timed("ln_measure1", measure1, stream)
         d2 = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
-        filt(d2, self.stats[t], self._i_out[t:t + 1])
-        job2.loudness_pass1(stream, tail=False)            # the limiter's input bound
-        job2.dd.lufs_on = 0
-        job2.decide(stream)
-        job2.finalize(None, stream)
+        self.timed("ln_filter2", lambda: filt(d2, self.stats[t], self._i_out[t:t + 1]), stream)
+
+        def limit():
+            job2.loudness_pass1(stream, tail=False)            # the limiter's input bound
+            job2.dd.lufs_on = 0
+            job2.decide(stream)
+            job2.finalize(None, stream)
+        self.timed("ln_limit192", limit, stream)
         return {"t": t, "n192": n192, "job2": job2, "ws2": ws2, "summ": summ}
 
     def _dyn_result(self, run, stream):

@@ -302,6 +302,10 @@ struct LpArgs {
     int kb, ke;
     const double *rec_in;
     double *rec_out;
+    // [n / 64 + 2] the largest |unlimited value| per 64 positions (k_lp_fill); non-NULL:
+    // k_lp_fill writes every position's unlimited output first, lp_detect skips blocks
+    // below the ceiling and k_lp_seg emits only the multiplied slots
+    double *bm;
 };
 // the 192 kHz resampler's geometry (amx_plan.cpp swr_*): output j sits at phase
 // position j dst / src (units of 1 / pc input frame); lin: interpolate rows ph, ph + 1
@@ -313,7 +317,8 @@ struct SwrDev {
 hipError_t launch_loudnorm(const LnArgs &a, const LpArgs &p, const uint32_t *x, int64_t n_in,
                            const SwrDev &r, hipStream_t st);
 hipError_t launch_loudnorm_shard(const LnArgs &a, const LpArgs &p, const uint32_t *x, int64_t n_in,
-                                 const SwrDev &r, int64_t u_lo, int64_t u_hi, int part, hipStream_t st);
+                                 const SwrDev &r, int64_t u_lo, int64_t u_hi, int64_t y_lo, int64_t y_hi, int part,
+                                 hipStream_t st);
 #define AMX_LN_GATED(g) ((g) && (((g)[0] >> 4) & 15) != 3)   // k_decide mode 3 = dynamic
 hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent_t fork, hipEvent_t join);
 int swr_geometry(int in_rate, int out_rate, int *L, int *M);   // host (amx_plan.cpp)

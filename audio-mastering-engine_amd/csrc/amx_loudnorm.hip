@@ -1276,17 +1276,38 @@ __device__ __forceinline__ int lp_env_end(int e0, int k) {
 #ifndef AMX_LP_PD
 #define AMX_LP_PD 4              // (measurement builds: scripts/build_var.py)
 #endif
-#define LP_PD AMX_LP_PD          // lp_detect: groups of 64 positions loaded ahead
+#define LP_PD AMX_LP_PD          // lp_detect: groups of 64 positions loaded together
 // one group's values: 64 positions from slot s0
 __device__ __forceinline__ double2 lp_grp(const LpArgs &a, const LpWave &W, int s0, int lane) {
     int s = s0 + lane;
     while (s >= LP_RS) s -= LP_RS;
     return lp_val(a, W, s);
 }
+// any slot of [s0, s0 + len) (mod LP_RS, len <= 64) multiplied since its fill
+__device__ __forceinline__ bool lp_flags_any(const LpWave &W, int s0, int len) {
+    bool any = false;
+#pragma unroll
+    for (int part = 0; part < 2; part++) {
+        const int lo = part == 0 ? s0 : 0;
+        const int hi = part == 0 ? min(s0 + len, LP_RS) : max(s0 + len - LP_RS, 0);
+        for (int w = lo >> 5; w <= ((hi - 1) >> 5) && hi > lo; w++) {
+            const int b0 = w * 32;
+            const int x0 = max(lo, b0) - b0, x1 = min(hi, b0 + 32) - b0;
+            const unsigned m = (x1 - x0 == 32) ? 0xffffffffu : (((1u << (x1 - x0)) - 1u) << x0);
+            any |= (W.flags[w] & m) != 0u;
+        }
+    }
+    return any;
+}
 // detect_peak from offset smp over count positions: peak_delta or -1; the peak's |x|
 // and slot.  64 positions per step: the first one that is a candidate with its
 // previous sample as predecessor is found by a ballot; only from there on is the scan
-// serial (a candidate that fails the 10-sample look-ahead keeps the older predecessor)
+// serial (a candidate that fails the 10-sample look-ahead keeps the older predecessor).
+// A candidate needs |x| > ceiling.  Outside FINAL, a slot's value is its position's
+// fill (a function of the position alone, k_lp_fill) or a multiplied value (flagged;
+// the limiter only multiplies by gains <= 1): so a group whose positions' fill maxima
+// (a.bm, 64-position blocks) are <= ceiling and whose slots carry no flag holds no
+// candidate and is skipped without loading a value -- 64 groups per ballot
 __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, int count, double &peak_value,
                          int &peak_slot) {
     const int lane = threadIdx.x;
@@ -1295,23 +1316,63 @@ __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, in
     const double ceiling = a.ceiling;
     double pv0 = 0.0, pv1 = 0.0;               // n = 0 never qualifies (n > 0)
     double *st0 = W.st, *st1 = W.st + 80;
-    // the groups' values are loaded LP_PD groups ahead of the one being scanned (the scan
-    // only reads the ring, so a value loaded early is the value then): one memory round
-    // trip per LP_PD groups instead of one per group.  Loads past count read slots of the
-    // same ring window, in bounds, unused.
-    // (the 12 positions after a group, for its look-ahead, are the next group's first 12:
-    // already loaded, LP_PD >= 2)
-    double2 q[LP_PD];
+    const bool skip = a.bm != nullptr && !W.f.fin;
+    // outside FINAL the positions of consecutive slots from slot0 are consecutive
+    const int64_t pos0 = lp_pos(W.f, slot0);
+    unsigned long long mask = 0ull;
+    int mask_base = -1;
+    bool stale = false;
+    int nb00 = 0;
+    while (nb00 < count) {
+        if (skip) {
+            if (mask_base < 0 || nb00 >= mask_base + 64 * 64) {
+                // lane j: may group nb00 + 64 j hold a candidate?
+                const int g0 = nb00 + 64 * lane;
+                bool may = false;
+                if (g0 < count) {
+                    const int64_t p = pos0 + g0;
+                    int s = slot0 + g0;
+                    while (s >= LP_RS) s -= LP_RS;
+                    may = a.bm[p >> 6] > ceiling || a.bm[(p + 63) >> 6] > ceiling || lp_flags_any(W, s, 64);
+                }
+                mask = __ballot(may);
+                mask_base = nb00;
+            }
+            const unsigned long long m = mask >> ((nb00 - mask_base) >> 6);
+            if (m == 0ull) {
+                nb00 = mask_base + 64 * 64;
+                mask_base = -1;
+                stale = true;
+                continue;
+            }
+            const int d = __ffsll((long long)m) - 1;
+            if (d > 0) {
+                nb00 += 64 * d;
+                stale = true;
+                if (nb00 >= count) break;
+            }
+            if (stale) {
+                // the predecessor: the value just before the group (skipped, so <= ceiling)
+                int s = slot0 + nb00 - 1;
+                while (s >= LP_RS) s -= LP_RS;
+                const double2 v = lp_val(a, W, s);
+                pv0 = fabs(v.x);
+                pv1 = fabs(v.y);
+                stale = false;
+            }
+        }
+        // LP_PD groups from nb00 and the next one's first 12 positions (the look-ahead),
+        // loaded together: one memory round trip per LP_PD groups.  Loads past count read
+        // slots of the same ring window, in bounds, unused.
+        double2 q[LP_PD + 1];
 #pragma unroll
-    for (int p = 0; p < LP_PD; p++) q[p] = lp_grp(a, W, slot0 + p * 64, lane);
-    for (int nb00 = 0; nb00 < count; nb00 += 64 * LP_PD)
+        for (int p = 0; p <= LP_PD; p++) q[p] = lp_grp(a, W, slot0 + nb00 + p * 64, lane);
 #pragma unroll
     for (int p = 0; p < LP_PD; p++) {
         const int nb0 = nb00 + 64 * p;
         if (nb0 >= count) break;
         {
-            const double2 v = q[p], v2 = q[(p + 1) % LP_PD];
-            q[p] = lp_grp(a, W, slot0 + nb0 + 64 * LP_PD, lane);
+            const double2 v = q[p], v2 = q[p + 1];
             __syncthreads();                   // the previous group's serial reads are done
             st0[lane] = fabs(v.x);
             st1[lane] = fabs(v.y);
@@ -1364,6 +1425,8 @@ __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, in
             }
         }
     }
+        nb00 += 64 * LP_PD;
+    }
     return -1;
 }
 
@@ -1396,8 +1459,56 @@ __device__ __forceinline__ void lp_emit(const LpArgs &a, const LpWave &W) {
     }
 }
 
-// true_peak_limiter on frame W.f (af_loudnorm), then its output when emit
-__device__ __forceinline__ void lp_call(const LpArgs &a, LpWave &W, bool emit) {
+#define LP_SPARSE_MAX 4096       // multiplied slots in a frame above which lp_emit_sparse emits densely
+// the bits of flag word w inside slots [lo, lo + len) mod LP_RS
+__device__ __forceinline__ unsigned lp_range_bits(int w, int lo, int len) {
+    unsigned m = 0u;
+#pragma unroll
+    for (int part = 0; part < 2; part++) {
+        const int a0 = part == 0 ? lo : 0;
+        const int a1 = part == 0 ? min(lo + len, LP_RS) : max(lo + len - LP_RS, 0);
+        const int b0 = w * 32;
+        const int x0 = max(a0, b0) - b0, x1 = min(a1, b0 + 32) - b0;
+        if (x1 > x0) m |= (x1 - x0 == 32) ? 0xffffffffu : (((1u << (x1 - x0)) - 1u) << x0);
+    }
+    return m;
+}
+
+// the output of the frame where k_lp_fill already wrote every position's unlimited
+// value: only the slots the limiter multiplied differ -- their ring values, clamped, s16
+// (a frame with many of them emits densely)
+__device__ __forceinline__ void lp_emit_sparse(const LpArgs &a, const LpWave &W) {
+    const int nb = W.f.nb, lbi = W.f.lbi;
+    int cnt = 0;
+    for (int w = threadIdx.x; w < LP_FW; w += 64) cnt += __popc(W.flags[w] & lp_range_bits(w, lbi, nb));
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) cnt += __shfl_xor(cnt, o);
+    if (cnt == 0) return;
+    if (cnt > LP_SPARSE_MAX) {
+        lp_emit(a, W);
+        return;
+    }
+    const double ceiling = a.ceiling;
+    uint32_t *y = reinterpret_cast<uint32_t *>(a.y);
+    for (int w = threadIdx.x; w < LP_FW; w += 64) {
+        unsigned m = W.flags[w] & lp_range_bits(w, lbi, nb);
+        while (m) {
+            const int s = 32 * w + __ffs(m) - 1;
+            m &= m - 1u;
+            int i = s - lbi;
+            if (i < 0) i += LP_RS;
+            const double2 v = W.ring[s];
+            double o0 = v.x, o1 = v.y;
+            if (fabs(o0) > ceiling) o0 = ceiling * (o0 < 0 ? -1 : 1);
+            if (fabs(o1) > ceiling) o1 = ceiling * (o1 < 0 ? -1 : 1);
+            y[W.f.base + i] = pack2(ln_s16(o0), ln_s16(o1));
+        }
+    }
+}
+
+// true_peak_limiter on frame W.f (af_loudnorm), then its output: emit 0 none, 1 sparse
+// (over k_lp_fill's output), 2 dense
+__device__ __forceinline__ void lp_call(const LpArgs &a, LpWave &W, int emit) {
     const int nb = W.f.nb;
     const double ceiling = a.ceiling;
     if (W.f.phi == 0) {
@@ -1493,7 +1604,8 @@ __device__ __forceinline__ void lp_call(const LpArgs &a, LpWave &W, bool emit) {
             }
         }
     } while (smp < nb);
-    if (emit) lp_emit(a, W);
+    if (emit == 1) lp_emit_sparse(a, W);
+    else if (emit == 2) lp_emit(a, W);
 }
 
 __device__ __forceinline__ void lp_rest(LpWave &W) {        // af_loudnorm's initial limiter state
@@ -1608,6 +1720,61 @@ __device__ __forceinline__ void lp_wave_init(const LpArgs &a, LpWave &W, double2
     W.off = a.dctl[1];
 }
 
+// Every output position's unlimited value, before the limiter runs (the gains are known,
+// fact 1 above): y = s16(clamp(fill)) over the positions [y_lo, y_hi) the segments emit,
+// so k_lp_seg only writes the slots its limiter multiplied (lp_emit_sparse); and bm[b],
+// the largest |fill| of positions [64 b, 64 b + 64) as a frame outside FINAL reads them
+// (lp_val's unflagged value), for lp_detect's skip -- +inf for a block with a position
+// outside [u_lo, u_hi) or past the track.  The fill is lp_val's expression term for
+// term: u (gain ramp) offset for INNER positions, u d0 offset below the ring's first
+// fill, u G_T offset for the positions FINAL emits.  One wave per 64-position block.
+__global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t y_hi, int64_t u_lo, int64_t u_hi) {
+    if ((a.ctl[0] != 0 && a.ctl[0] != 4) || a.T < 1) return;
+    if (a.ctl[0] == 4) {
+        // a quiet start: k_ln_dyn wrote the frames before the hand-over segment
+        const int phi = lp_seg_start(a, a.ctl[4]);
+        const int64_t b = phi <= a.T ? (int64_t)LP_FR * phi : a.S0 + (int64_t)LP_FR * (phi - a.T - 1);
+        y_lo = y_lo > b ? y_lo : b;
+    }
+    const double d0 = a.dctl[0], off = a.dctl[1], gT = a.G[a.T], ceiling_inf = HUGE_VAL;
+    const int lane = threadIdx.x & 63;
+    const int64_t b_lo = u_lo >> 6, b_hi = (u_hi + 63) >> 6;
+    uint32_t *y = reinterpret_cast<uint32_t *>(a.y);
+    const float2 *u = reinterpret_cast<const float2 *>(a.u);
+    for (int64_t b = b_lo + (((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6); b < b_hi;
+         b += ((int64_t)gridDim.x * 256) >> 6) {
+        const int64_t pos = 64 * b + lane;
+        const bool in = pos >= u_lo && pos < u_hi && pos < a.n;
+        double mx = in ? 0.0 : ceiling_inf;
+        if (in) {
+            const float2 x = u[pos];
+            const int64_t q = pos - LP_RS > 0 ? pos - LP_RS : 0;
+            const int t = (int)(q / LP_FR), i = (int)(q - (int64_t)t * LP_FR);
+            const int tc = t < a.T - 1 ? t : a.T - 1;
+            double r = a.ramp[i];
+            if (!(t < a.T - 1 || a.nb_last == LP_FR)) r = (double)i / (double)a.nb_last;
+            const double g0 = a.G[tc], g1 = a.G[tc + 1];
+            const double gi = g0 + (r * (g1 - g0));
+            const double g = pos < LP_RS ? d0 : gi;
+            const double v0 = ((double)x.x * g) * off, v1 = ((double)x.y * g) * off;
+            mx = fmax(fabs(v0), fabs(v1));
+            if (pos >= y_lo && pos < y_hi) {
+                double o0 = v0, o1 = v1;
+                if (pos >= a.S0) {                     // FINAL emits it: u G_T offset
+                    o0 = ((double)x.x * gT) * off;
+                    o1 = ((double)x.y * gT) * off;
+                }
+                if (fabs(o0) > a.ceiling) o0 = a.ceiling * (o0 < 0 ? -1 : 1);
+                if (fabs(o1) > a.ceiling) o1 = a.ceiling * (o1 < 0 ? -1 : 1);
+                y[pos] = pack2(ln_s16(o0), ln_s16(o1));
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) mx = fmax(mx, __shfl_xor(mx, o));
+        if (lane == 0) a.bm[b] = mx;
+    }
+}
+
 // every segment at once (persistent waves): from rest Wf frames before its start
 #ifndef AMX_LP_WPE
 #define AMX_LP_WPE 3             // k_lp_seg waves per SIMD the register budget allows (168
@@ -1632,7 +1799,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AMX_LP_
                     W.f = lp_frame(a, phi);
                     lp_refill(a, W, phi);
                 }
-                lp_call(a, W, true);
+                lp_call(a, W, a.bm ? 1 : 2);
             }
         } else {
             const int w = ak - a.Wf > 0 ? ak - a.Wf : 0;
@@ -1644,7 +1811,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AMX_LP_
                     lp_snapshot(a, W, a.recG + (int64_t)k * LP_REC);
                     if (k > kh) lp_arrive(a, k);
                 }
-                lp_call(a, W, phi >= ak);
+                lp_call(a, W, phi >= ak ? (a.bm ? 1 : 2) : 0);
             }
         }
         if (k + 1 < a.K) {
@@ -1703,7 +1870,7 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
                     W.f = lp_frame(a, phi);
                     lp_refill(a, W, phi);
                 }
-                lp_call(a, W, true);
+                lp_call(a, W, 2);
             }
             fin = 1;
             break;
@@ -1722,7 +1889,7 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
                 W.f = lp_frame(a, phi);
                 lp_refill(a, W, phi);
             }
-            lp_call(a, W, true);
+            lp_call(a, W, 2);
         }
         reruns++;
         if (k + 1 < a.K) {
@@ -1758,6 +1925,15 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
     }
 }
 
+static void lp_fill(const LpArgs &lp, int64_t y_lo, int64_t y_hi, int64_t u_lo, int64_t u_hi, hipStream_t st) {
+    const int64_t blocks = ((u_hi + 63) >> 6) - (u_lo >> 6);
+    if (blocks <= 0) return;
+    // grid-stride over at most 4096 workgroups (a gated track's launch returns at once)
+    const int64_t g = (blocks + 3) / 4;
+    hipLaunchKernelGGL(k_lp_fill, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, lp, y_lo, y_hi, u_lo,
+                       u_hi);
+}
+
 static void ln_upsample(const uint32_t *x, int64_t n_in, const SwrDev &r, int64_t j0, int64_t j1, float *u,
                         const int32_t *gate, hipStream_t st) {
     if (j1 <= j0) return;
@@ -1789,6 +1965,7 @@ hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x
     hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
     const int gb = max((lp.T + 1 + 255) / 256, (LP_FR + 255) / 256);
     hipLaunchKernelGGL(k_lp_gains, dim3(gb), dim3(256), 0, st, lp);
+    if (lp.bm) lp_fill(lp, 0, ln.n192, 0, ln.n192, st);
     hipError_t e = hipMemsetAsync(lp.cnt, 0, sizeof(int) * (size_t)(lp.K + 1), st);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(lp.match, 0, sizeof(int) * (size_t)(lp.K + 1), st);
@@ -1805,7 +1982,8 @@ hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x
 // parallel form runs, else the whole track must run frame by frame); 1 -- deltas, gains
 // and the segments [kb, ke); 2 -- the walk over their boundaries from lp.rec_in
 hipError_t launch_loudnorm_shard(const LnArgs &ln, const LpArgs &lp, const uint32_t *x, int64_t n_in,
-                                 const SwrDev &r, int64_t u_lo, int64_t u_hi, int part, hipStream_t st) {
+                                 const SwrDev &r, int64_t u_lo, int64_t u_hi, int64_t y_lo, int64_t y_hi, int part,
+                                 hipStream_t st) {
     if (ln.n192 <= 0) return hipSuccess;
     if (part == 0) {
         ln_upsample(x, n_in, r, u_lo, u_hi, ln.u, lp.gate, st);
@@ -1814,6 +1992,7 @@ hipError_t launch_loudnorm_shard(const LnArgs &ln, const LpArgs &lp, const uint3
         hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
         const int gb = max((lp.T + 1 + 255) / 256, (LP_FR + 255) / 256);
         hipLaunchKernelGGL(k_lp_gains, dim3(gb), dim3(256), 0, st, lp);
+        if (lp.bm) lp_fill(lp, y_lo, y_hi, u_lo, u_hi, st);
         hipError_t e = hipMemsetAsync(lp.cnt, 0, sizeof(int) * (size_t)(lp.K + 1), st);
         if (e != hipSuccess) return e;
         e = hipMemsetAsync(lp.match, 0, sizeof(int) * (size_t)(lp.K + 1), st);

@@ -1286,7 +1286,8 @@ amx::UpArgs up_args(const amx_plan *p, const int16_t *d_out, const int16_t *d_ed
 struct LnLayout {
     int T = 0, nb_last = 0, Fs = 4, Wf = 3, J = 0, M = 0, K = 0, P = 0;
     int64_t o_u = 0, o_ring = 0, o_ctl = 0, o_dctl = 0, o_v = 0, o_hold = 0, o_D = 0, o_G = 0, o_ramp = 0;
-    int64_t o_recG = 0, o_recE = 0, o_wrec = 0, o_cnt = 0, o_match = 0, o_rings = 0, o_wring = 0, total = 0;
+    int64_t o_recG = 0, o_recE = 0, o_wrec = 0, o_cnt = 0, o_match = 0, o_rings = 0, o_wring = 0, o_bm = 0;
+    int64_t total = 0;
 };
 // INNER frames, segments of Fs frames each warmed up Wf frames (AMX_LN_WARM, default 2)
 // before its start, at most P persistent k_lp_seg waves (AMX_LN_P, default 3072: three per
@@ -1331,6 +1332,7 @@ LnLayout ln_layout(int64_t n192) {
     l.o_match = take((int64_t)(l.K + 1) * sizeof(int));
     l.o_rings = take((int64_t)l.P * AMX_LN_RING * 2 * sizeof(double));
     l.o_wring = take((int64_t)AMX_LN_RING * 2 * sizeof(double));
+    l.o_bm = take((n192 / 64 + 2) * (int64_t)sizeof(double));
     l.total = o;
     return l;
 }
@@ -1518,6 +1520,10 @@ int ln_args(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const double
     a.lp_J = q.J;
     q.kb = 0;
     q.ke = q.K;
+    // k_lp_fill + the skipping scan + the sparse emit (AMX_LP_FILL=0: the dense form, for
+    // A/B measurements)
+    const char *fe = std::getenv("AMX_LP_FILL");
+    q.bm = (fe && std::atoi(fe) == 0) ? nullptr : reinterpret_cast<double *>(w + lo.o_bm);
     return AMX_OK;
 }
 }  // namespace
@@ -1569,8 +1575,11 @@ int amx_loudnorm_192k_shard(amx_plan *p, int32_t track, const amx_loudnorm_desc 
     q.rec_out = sh->ke < q.K ? sh->d_rec_out : nullptr;
     const SpanDev &sp = p->spans[track];
     amx::SwrDev r{p->up_pc, p->up_lin, p->up_src, p->up_dst, p->d_bank};
+    // the positions segments [kb, ke) emit
+    const LnLayout lo = ln_layout(n192);
+    const int64_t y_lo = ln_seg_base(lo, n192, sh->kb), y_hi = sh->ke < lo.K ? ln_seg_base(lo, n192, sh->ke) : n192;
     HIPCHK(amx::launch_loudnorm_shard(a, q, reinterpret_cast<const uint32_t *>(d_out) + sp.out_off, sp.out_n, r,
-                                      u_lo, u_hi, sh->part, (hipStream_t)stream));
+                                      u_lo, u_hi, y_lo, y_hi, sh->part, (hipStream_t)stream));
     return AMX_OK;
 }
 

@@ -180,13 +180,64 @@ def time_graph(runner, d_in, warmup, soak_s, min_s):
     return (time.perf_counter() - t0) * 1e3 / steps, steps
 
 
+def _oracle():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    return oracle
+
+
+def _threads():
+    return max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1, 16))
+
+
+def oracle_tracks(tracks, fs, settings, ex):
+    """The C oracle's whole pipeline (:171-226) over [(x16 track, chunk bounds)]: chunk
+    chains on the thread pool `ex` (ctypes drops the GIL), loudness + alimiter serial per
+    track as in the reference, the tracks themselves side by side.  Test infrastructure:
+    the checker of the GPU output, never the thing measured."""
+    import numpy as np
+    oracle = _oracle()
+
+    def one(xb):
+        xt, bounds = xb
+        outs = [oracle.chunk(xt[s:s + n], fs, settings) for s, n in bounds] if len(tracks) > 1 else \
+            list(ex.map(lambda sn: oracle.chunk(xt[sn[0]:sn[0] + sn[1]], fs, settings), bounds))
+        cat = np.concatenate(outs, axis=0)
+        yy = cat
+        if settings.get("lufs") is not None:
+            mode, g = oracle.loudnorm_linear_gain(oracle.loudnorm_measure(cat, fs), float(settings["lufs"]))
+            if mode == "linear":
+                yy = oracle.linear_gain(cat, g)
+        return oracle.alimiter(yy, fs)
+    if len(tracks) == 1:
+        return [one(tracks[0])]
+    return list(ex.map(one, tracks))
+
+
+def parity(ys, refs, what):
+    """max |diff| (LSB) and the exact fraction of the GPU outputs against the oracle's"""
+    import numpy as np
+    mx, ex_n, n_all = 0, 0, 0
+    for t, (y, ref) in enumerate(zip(ys, refs)):
+        if y.shape != ref.shape:
+            return {"shape_mismatch": [list(y.shape), list(ref.shape)], "track": t}
+        d = np.abs(y.astype(np.int32) - ref.astype(np.int32))
+        mx = max(mx, int(d.max()) if d.size else 0)
+        ex_n += int((d == 0).sum())
+        n_all += d.size
+    return {"max_abs_lsb": mx, "exact_frac": ex_n / max(1, n_all), "tracks": len(refs), "what": what}
+
+
 def other_configs(args):
     """C2, C4, C5 on this GPU (N = 1): the same step as their own bench lines (hipGraph
     replay of the whole pipeline on HBM-resident synthetic input), timed over >= 1 s;
-    no CPU leg, no per-stage events"""
+    then each config's whole workload through the C oracle (thread pool), compared with
+    the GPU output bit for bit (parity_vs_oracle); no per-stage events"""
     import gc
+    from concurrent.futures import ThreadPoolExecutor
     import torch
     from amx.dist import ShardedBatch, ShardedTrack
+    oracle = _oracle()
     out = {}
     for cfg in ("c2", "c4", "c5"):
         fs = CONFIG_FS[cfg]
@@ -194,21 +245,91 @@ def other_configs(args):
         if cfg == "c4":
             frames = [per_track] * CONFIG_TRACKS[cfg]
             runner = ShardedBatch(fs, 2, CONFIGS[cfg], frames, 0, 1, quantum=512, seg_frames=args.seg_frames)
-            x = np.concatenate([synth_input(frames[t], fs, 1000 + t) for t in runner.tracks], axis=0)
+            xs = [synth_input(frames[t], fs, 1000 + t) for t in runner.tracks]
+            x = np.concatenate(xs, axis=0)
         else:
             runner = ShardedTrack(fs, 2, CONFIGS[cfg], per_track, 0, 1, quantum=512, seg_frames=args.seg_frames)
             x = synth_input(runner.local_frames, fs, 0)
+            xs = [x]
         d_in = torch.from_numpy(x).cuda()
         del x
         ms, steps = time_graph(runner, d_in, 2, 0.5, 1.0)
         samples = sum(runner.span_frames) * 2
         rep = runner.job.fetch_report()
-        out[cfg] = {"workload": WORKLOAD[cfg], "ms_per_step": round(ms, 4), "steps": steps,
-                    "data": synth_generator(per_track, fs),
-                    "value": round(samples / (ms / 1e3) / 1e6, 3), "unit": "Msamples/s",
-                    "chain_frac": round(CHAIN_BYTES * samples / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                    "loudnorm_mode": rep.get("modes"), "limiter_fast": rep.get("limiter_fast")}
+        o = {"workload": WORKLOAD[cfg], "ms_per_step": round(ms, 4), "steps": steps,
+             "data": synth_generator(per_track, fs),
+             "value": round(samples / (ms / 1e3) / 1e6, 3), "unit": "Msamples/s",
+             "chain_frac": round(CHAIN_BYTES * samples / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+             "loudnorm_mode": rep.get("modes"), "limiter_fast": rep.get("limiter_fast")}
+        if not args.no_cpu_baseline:
+            if cfg == "c4":
+                ys = [runner.job.track_output(t).cpu().numpy() for t in range(len(runner.tracks))]
+                tracks = [(oracle.quantize(xt), runner.track_bounds[t]) for xt, t in zip(xs, runner.tracks)]
+            else:
+                ys = [runner.job.y[:runner.job.info.out_frames].cpu().numpy()]
+                tracks = [(oracle.quantize(xs[0]), [(s - runner.in0, n) for s, n in runner.bounds])]
+            del xs
+            t0 = time.perf_counter()
+            with ThreadPoolExecutor(_threads()) as ex:
+                refs = oracle_tracks(tracks, fs, CONFIGS[cfg], ex)
+            o["parity_vs_oracle"] = dict(parity(ys, refs, "whole workload, bit for bit"),
+                                         oracle_seconds=round(time.perf_counter() - t0, 2))
+            del ys, refs, tracks
+        out[cfg] = o
         del runner, d_in
+        gc.collect()
+        torch.cuda.empty_cache()
+    return out
+
+
+def other_inputs(args):
+    """loudnorm's dynamic mode (:240 when the linear conditions fail: the 192 kHz AGC,
+    true-peak limiter and the alimiter at 192 kHz) on the default bench's own step: a
+    quiet programme with full-scale bursts (synth_input kind "dynamic").  C3 settings on
+    one 5-min 48 kHz track (per-stage times, and the whole 192 kHz output against the C
+    oracle's pipeline) and C5 strong (one 60-min 96 kHz track).  The step is the same
+    captured graph with the dynamic path gated on the device, replayed; the host reads
+    the decision and the 192 kHz output's size back each step."""
+    import gc
+    import torch
+    from amx.chunking import chunk_bounds
+    from amx.dist import ShardedTrack
+    out = {}
+    for cfg, fs, seconds in (("c3", 48000, 300.0), ("c5_strong", 96000, 3600.0)):
+        settings = CONFIGS["c3"]
+        n = int(seconds * fs)
+        runner = ShardedTrack(fs, 2, settings, n, 0, 1, quantum=512, seg_frames=args.seg_frames, dynamic=True)
+        x = synth_input(runner.local_frames, fs, 0, "dynamic")
+        d_in = torch.from_numpy(x).cuda()
+        ms, steps = time_graph(runner, d_in, 1, 0.5, 1.0)
+        y = runner.replay()
+        info = dict(getattr(runner, "dyn_info", None) or {})
+        o = {"settings": "c3", "sample_rate": fs, "seconds": seconds, "ms_per_step": round(ms, 4), "steps": steps,
+             "value": round(2 * n / (ms / 1e3) / 1e6, 3), "unit": "Msamples/s (input rate)",
+             "output_sample_rate": info.get("sample_rate"), "dynamic": info,
+             "data": "synthetic: %s at -18 dB with two 50-frame full-scale bursts per second" %
+                     synth_generator(n, fs)}
+        job = runner.job
+        if cfg == "c3":
+            job.stage_events = []
+            for _ in range(3):
+                runner.step(d_in)
+            torch.cuda.synchronize()
+            st = {}
+            for name, a, b in job.stage_events:
+                st[name] = st.get(name, 0.0) + a.elapsed_time(b) / 3
+            job.stage_events = None
+            o["stages_ms"] = {k: round(v, 4) for k, v in st.items()}
+            if not args.no_cpu_baseline:
+                oracle = _oracle()
+                y = runner.replay().cpu().numpy()
+                t0 = time.perf_counter()
+                ref, rinfo = oracle.pipeline(oracle.quantize(x), fs, settings, chunk_bounds(n, fs, 512))
+                o["parity_vs_oracle"] = dict(parity([y], [ref], "the whole 192 kHz output, bit for bit"),
+                                             oracle_mode=rinfo.get("mode"),
+                                             oracle_seconds=round(time.perf_counter() - t0, 2))
+        out[cfg] = o
+        del runner, d_in, x, y
         gc.collect()
         torch.cuda.empty_cache()
     return out
@@ -468,7 +589,8 @@ def main():
                    "parallelism": ("track-shard x%d" if batch else "chunk-shard x%d") % world,
                    "exchanges": ("%s collectives" % dist.get_backend()) if use_dist and not batch else None,
                    "launch": ("hipGraph replay" if (world == 1 and not args.force_exchange) or batch else
-                              "hipGraph segments + eager collectives") if graph else "eager"},
+                              ("one hipGraph, RCCL collectives captured" if args.dist_backend == "nccl" else
+                               "hipGraph segments + eager (host-staged) collectives")) if graph else "eager"},
         "timed_region_s": round(elapsed, 4), "soak": {"seconds": round(soak_s, 3), "replays": n_soak},
         "roofline": {"bound": "hbm", "kernel": kern, "stage": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -516,6 +638,7 @@ def main():
     if rank == 0 and world == 1 and args.config == "c3" and not args.no_other_configs:
         line["other_configs"] = other_configs(args)
         line["other_rates"] = other_rates(args)
+        line["other_inputs"] = {"dynamic": other_inputs(args)}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if use_dist:
@@ -541,17 +664,7 @@ def cpu_leg(args, runner, x, fs, settings, job, batch):
             off += n
     else:
         tracks = [(x16, [(s - runner.in0, n) for s, n in runner.bounds])]
-    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1, 16))
-
-    def pipeline_threaded(xt, bounds, ex):
-        outs = list(ex.map(lambda sn: oracle.chunk(xt[sn[0]:sn[0] + sn[1]], fs, settings), bounds))
-        cat = np.concatenate(outs, axis=0)
-        yy = cat
-        if settings.get("lufs") is not None:
-            mode, g = oracle.loudnorm_linear_gain(oracle.loudnorm_measure(cat, fs), float(settings["lufs"]))
-            if mode == "linear":
-                yy = oracle.linear_gain(cat, g)
-        return oracle.alimiter(yy, fs)
+    threads = _threads()
 
     # 1 core on a bounded sample: whole chunks of the first track, up to ~20 s of audio
     # per... as many chunks as fit ~10-30 s of CPU (the whole 5-min track at C2/C3)
@@ -576,7 +689,7 @@ def cpu_leg(args, runner, x, fs, settings, job, batch):
     # serial per track, as in the reference) -- also the parity reference
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:
-        refs = [pipeline_threaded(xt, b, ex) for xt, b in tracks]
+        refs = oracle_tracks(tracks, fs, settings, ex)
     dtp = time.perf_counter() - t0
     tot = sum(xt.shape[0] for xt, _ in tracks)
     out["cpu_baseline"]["all_cores"] = {
@@ -584,18 +697,8 @@ def cpu_leg(args, runner, x, fs, settings, job, batch):
         "what": "the whole workload: chunk chains on a thread pool, loudness + alimiter serial"}
     if nch == len(b0):
         out["cpu_baseline"]["all_cores"]["same_output_as_1_core"] = bool(np.array_equal(refs[0], ref1))
-    mx, ex_n, n_all = 0, 0, 0
-    for t, ref in enumerate(refs):
-        y = (job.track_output(t) if batch else job.y[:job.info.out_frames]).cpu().numpy()
-        if y.shape != ref.shape:
-            out["parity_vs_oracle"] = {"shape_mismatch": [list(y.shape), list(ref.shape)], "track": t}
-            return out
-        d = np.abs(y.astype(np.int32) - ref.astype(np.int32))
-        mx = max(mx, int(d.max()))
-        ex_n += int((d == 0).sum())
-        n_all += d.size
-    out["parity_vs_oracle"] = {"max_abs_lsb": mx, "exact_frac": ex_n / max(1, n_all),
-                               "tracks": len(refs), "what": "whole workload, bit for bit"}
+    ys = [(job.track_output(t) if batch else job.y[:job.info.out_frames]).cpu().numpy() for t in range(len(refs))]
+    out["parity_vs_oracle"] = parity(ys, refs, "whole workload, bit for bit")
     return out
 
 

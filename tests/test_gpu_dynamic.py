@@ -109,6 +109,48 @@ def test_parallel_splits_vs_oracle(gpu, oracle_mod, monkeypatch, seg, warm):
         _cmp(job2.out[:n192].cpu().numpy(), ref, "parallel split Fs=%d Wf=%d offset %.1f" % (seg, warm, offset))
 
 
+@pytest.mark.parametrize("seg,warm,intro", [(None, None, 0.0), (1, 0, 0.0), (None, None, 6.0), (2, 1, 12.5)])
+def test_fill_prepass_equals_dense_form(gpu, oracle_mod, monkeypatch, seg, warm, intro):
+    """k_lp_fill + the skipping peak scan + the sparse emit (the default) against the
+    dense form (AMX_LP_FILL=0: every position's value loaded in the scans, every output
+    written by k_lp_seg), bit for bit, on an output buffer poisoned before each run (a
+    position neither form writes would show); quiet (+0 dB) and busy (+9 dB) limiters,
+    one-frame segments without warm-up (re-runs), and quiet starts (the hand-over)"""
+    import torch
+    from amx import capi
+    from amx.engine import MasteringJob
+    if seg is not None:
+        monkeypatch.setenv("AMX_LN_SEG", str(seg))
+        monkeypatch.setenv("AMX_LN_WARM", str(warm))
+    fs = 48000
+    x = _dynamic_signal(24.0, fs, 23, intro)
+    x16 = oracle_mod.quantize(x)
+    st = oracle_mod.loudnorm_measure(x16, fs)
+    job = MasteringJob(fs, 2, {"lufs": -14.0}, [x16.shape[0]], input_s16=True,
+                       chunks=[(0, 0, x16.shape[0])], measure_only=True)
+    job.out[:x16.shape[0]].copy_(torch.from_numpy(x16))
+    job.loudness_pass1(tail=False)
+    job.loudness_pass2(carry=False)
+    job.histograms()
+    job.decide()
+    n192, job2, ws2, summ = job._job192(0, cached=False)[0:4]
+    for offset in (0.0, 9.0):
+        d = capi.LoudnormDesc(-14.0, 11.0, -1.5, float(st["input_i"]), float(st["input_lra"]),
+                              float(st["input_tp"]), float(st["input_thresh"]), offset)
+        outs = []
+        for fill in ("0", "1"):
+            monkeypatch.setenv("AMX_LP_FILL", fill)
+            job2.out.fill_(12345)
+            job.loudnorm_192k(0, d, job2, ws2, summ)
+            outs.append(job2.out[:n192].cpu().numpy())
+        s = summ.cpu().numpy()
+        print("fill pre-pass, offset %.1f: %d segments, %d re-run, FINAL re-run %d, handed over at %d" %
+              (offset, s[12], s[10], s[11], s[14]))
+        np.testing.assert_array_equal(outs[1], outs[0])
+        ref, _ = oracle_mod.loudnorm(x16, fs, -14.0, measured=st, offset=offset)
+        _cmp(outs[1], ref, "fill pre-pass offset %.1f" % offset)
+
+
 @pytest.mark.parametrize("seg,warm,intro", [(4, 3, 6.0), (1, 0, 6.0), (4, 3, 12.5)])
 def test_quiet_start_handover_vs_oracle(gpu, oracle_mod, monkeypatch, seg, warm, intro):
     """a quiet intro (the first 3 s below measured_thresh: above_threshold 0, so the
