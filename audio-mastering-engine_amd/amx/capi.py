@@ -79,7 +79,7 @@ class LoudnormDesc(ctypes.Structure):
 
 
 class LnShard(ctypes.Structure):
-    _fields_ = [("part", ctypes.c_int32), ("kb", ctypes.c_int32), ("ke", ctypes.c_int32), ("pad_", ctypes.c_int32),
+    _fields_ = [("part", ctypes.c_int32), ("kb", ctypes.c_int32), ("ke", ctypes.c_int32), ("windowed", ctypes.c_int32),
                 ("u_lo", ctypes.c_int64), ("u_hi", ctypes.c_int64), ("d_rec_in", ctypes.c_void_p),
                 ("d_rec_out", ctypes.c_void_p)]
 
@@ -103,7 +103,8 @@ EXPORTS = ("amx_abi_version", "amx_last_error", "amx_build_id", "amx_plan_create
            "amx_limiter_geometry", "amx_limiter_prepare", "amx_loudness_decide", "amx_kw_carry_setup", "amx_kw_carry",
            "amx_finalize", "amx_env_counters", "amx_pcm_to_s16", "amx_loudnorm_192k_size",
            "amx_loudnorm_192k", "amx_loudnorm_192k_ex", "amx_flac_info", "amx_flac_decode",
-           "amx_plan_set_gate", "amx_loudnorm_192k_shard", "amx_loudnorm_192k_segments")
+           "amx_plan_set_gate", "amx_loudnorm_192k_shard", "amx_loudnorm_192k_segments",
+           "amx_loudnorm_192k_shard_window")
 PCM_FORMATS = {"u8": 0, "s16": 1, "s24": 2, "s32": 3, "f32": 4, "f64": 5,
                "s8": 6, "s16be": 7, "s24be": 8, "s32be": 9, "f32be": 10, "f64be": 11}
 
@@ -157,6 +158,8 @@ def load(path=None):
                                        ctypes.c_int64, vp, vp, vp, vp, vp]
     L.amx_loudnorm_192k_shard.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(LoudnormDesc), vp, vp,
                                           ctypes.POINTER(LnShard), vp, vp, ctypes.c_int64, vp, vp, vp, vp, vp]
+    L.amx_loudnorm_192k_shard_window.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                 ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     L.amx_loudnorm_192k_segments.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                                              ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]

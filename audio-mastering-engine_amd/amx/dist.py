@@ -266,9 +266,12 @@ class ShardedTrack:
         self.tframe0 = sum(self.out_n[:c0])
         self.ttotal = sum(self.out_n)
         chunks = [(0, s - self.in0, n) for s, n in self.bounds[c0:c1]]
-        self.job = MasteringJob(fs, channels_in, settings, [self.local_frames], chunks=chunks,
-                                track_frame0=[self.tframe0], track_total=[self.ttotal],
-                                input_s16=input_s16, seg_frames=seg_frames)
+        self._job_args = ((fs, channels_in, settings, [self.local_frames]),
+                          dict(chunks=chunks, track_frame0=[self.tframe0], track_total=[self.ttotal],
+                               input_s16=input_s16, seg_frames=seg_frames))
+        self.job = MasteringJob(*self._job_args[0], **self._job_args[1])
+        self._slots = None         # the pipelined replay's two buffer sets (capture)
+        self._pending = None
         if self.xchg:
             self._setup_exchange()
 
@@ -481,16 +484,41 @@ class ShardedTrack:
 
     def dynamic(self, sharded=True):
         """loudnorm's dynamic mode on the chunk-sharded track (:240 when the linear
-        conditions fail; :223's alimiter then runs on the 192 kHz stream).  The spans are
-        all-gathered and every rank measures the whole track again (the filter's gains
-        come from those hop energies).  Sharded form (_dynamic_sharded): the 192 kHz
-        stream is split over the ranks by the filter's segments -- both filter runs, the
-        measurement of pass 1's output and the alimiter run on each rank's run with the
-        limiter-state records, K-filter tails, hop energies and alimiter state crossing
-        ranks; each rank returns its run, self.dyn_range.  Replicated form (a track
-        with fewer filter segments than ranks, or sharded=False): every rank runs the
-        whole 192 kHz path (MasteringJob.dynamic_track) and returns dynamic_range().
-        Returns int16 [P1 - P0, 2]."""
+        conditions fail; :223's alimiter then runs on the 192 kHz stream).
+
+        Windowed form (the default at N > 1, _dynamic_windowed): every rank keeps its own
+        part -- the filter's gains come from the step's own all-reduced hop energies and
+        decision, the filter segments are split at the ranks' span boundaries, and a
+        rank holds only its span plus a halo of the neighbours' edge frames (one
+        all-gather), the 192 kHz stream and output of its own segments; the limiter
+        state record goes rank to rank; the 192 kHz measurement and the alimiter run
+        over the ranks' runs (Span192).  Per-rank memory and traffic scale as 1 / N.
+        Replicated form (a track too short to split, a quiet start or a walk fallback
+        -- one sequence over the whole track --, or sharded=False): the spans are
+        all-gathered and every rank runs the whole 192 kHz path.
+        Returns int16 [P1 - P0, 2]: this rank's run of the 192 kHz output."""
+        job = self.job
+        self._forms = []
+        y = info = None
+        if sharded and self.world > 1:
+            wd = self._windows()
+            if wd is not None:
+                r = self._dynamic_windowed(wd)
+                if r is not None:
+                    y, info = r
+                    self.dyn_range = wd["y"][self.rank]
+        if y is None:
+            y, info = self._dynamic_replicated(sharded)
+        fs_ = self._forms or ["replicated"]
+        form = fs_[0] if all(f == fs_[0] for f in fs_) else "+".join(fs_)
+        self.dyn_info = dict(info, form=form)
+        job.report.update(dynamic=self.dyn_info, sample_rate=192000)
+        return y
+
+    def _dynamic_replicated(self, sharded):
+        """the spans all-gathered into a whole-track plan on every rank, measured again,
+        and the 192 kHz path run whole (MasteringJob.dynamic_track), or with the filter's
+        segments split evenly over the ranks (_dynamic_sharded)"""
         job = self.job
         whole = gather_track(job.out, self.span_frames[self.rank], self.span_frames, self.world, self.group)
         W = getattr(self, "_whole", None)
@@ -500,27 +528,189 @@ class ShardedTrack:
             self._whole = W
             self._split = self._ln_split(W) if self.world > 1 else None
         W.out[:self.ttotal].copy_(whole)
-        # the whole track's measurement again (~0.1 ms per 5 minutes): the same hop energies
-        # a one-GPU run forms (the sharded ones differ from them in the last bits of the
-        # hops beside a rank boundary, where the K filter's state came by the carry)
         W.loudness_pass1(tail=False)
         W.loudness_pass2(carry=False)
         W.histograms()
         W.decide()
-        self._forms = []
         if sharded and self._split is not None:
             y, info = self._dynamic_sharded(W)
             kb, ke = self._split["ranges"][self.rank]
             self.dyn_range = (self._split["starts"][kb], self._split["starts"][ke])
-            form = "sharded" if self._forms == ["sharded"] * 2 else "+".join(self._forms)
         else:
             y, info = W.dynamic_track(0)
             self.dyn_range = self.dynamic_range()
             y = y[self.dyn_range[0]:self.dyn_range[1]]
-            form = "replicated"
-        self.dyn_info = dict(info, form=form)
-        job.report.update(dynamic=self.dyn_info, sample_rate=192000)
-        return y
+            self._forms.append("replicated")
+        return y, info
+
+    # ------------------------------------------- dynamic mode, windowed (N > 1)
+    def _windows(self):
+        """(once per track) the filter's segments split at the ranks' span boundaries and
+        each rank's windows (amx_loudnorm_192k_shard_window): chain frames x, 192 kHz
+        stream u, output positions y; the halo sizes of the edge exchange.  None when the
+        track cannot be split so (spans shorter than a halo, a rank without a segment,
+        FINAL not on the last rank)."""
+        if hasattr(self, "_wd"):
+            return self._wd
+        import ctypes
+        from . import capi, design
+        L = capi.load()
+        job, world = self.job, self.world
+        desc, keep = design.chain_desc(job.fs, 2, {"lufs": job.settings.get("lufs")})
+        desc.input_s16 = 1
+        desc.measure_only = 1
+        plan = capi.Plan(desc, [(0, 0, self.ttotal)], None, None, 128)   # geometry only
+        K, kf, rd, co = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        capi.check(L.amx_loudnorm_192k_segments(plan.h, 0, None, 0, ctypes.byref(K), ctypes.byref(kf),
+                                                ctypes.byref(rd), ctypes.byref(co)), "amx_loudnorm_192k_segments")
+        starts = (ctypes.c_int64 * (K.value + 1))()
+        capi.check(L.amx_loudnorm_192k_segments(plan.h, 0, starts, K.value + 1, ctypes.byref(K), None, None, None),
+                   "amx_loudnorm_192k_segments")
+        starts = list(starts)
+        F = [sum(self.span_frames[:q]) for q in range(world + 1)]
+        kbs = [0]
+        for q in range(1, world):
+            p = self.m192(F[q])
+            kbs.append(next((k for k in range(K.value) if starts[k] >= p), K.value))
+        kbs.append(K.value)
+        self._wd = None
+        if any(kbs[q] >= kbs[q + 1] for q in range(world)) or kbs[world - 1] > kf.value:
+            return None
+        xs, us, ys, wsb, ctl = [], [], [], [], []
+        for q in range(world):
+            win = (ctypes.c_int64 * 7)()
+            b = ctypes.c_int64()
+            capi.check(L.amx_loudnorm_192k_shard_window(plan.h, 0, kbs[q], kbs[q + 1], win, ctypes.byref(b)),
+                       "amx_loudnorm_192k_shard_window")
+            xs.append((win[0], win[1]))
+            us.append((win[2], win[3]))
+            ys.append((win[4], win[5]))
+            wsb.append(b.value)
+            ctl.append(win[6])
+        before = [max(0, F[q] - xs[q][0]) for q in range(world)]
+        after = [max(0, xs[q][1] - F[q + 1]) for q in range(world)]
+        if any(before[q] > (self.span_frames[q - 1] if q > 0 else 0) for q in range(world)) or \
+                any(after[q] > (self.span_frames[q + 1] if q + 1 < world else 0) for q in range(world)):
+            return None
+        r = self.rank
+        dev = job.device
+        Hb, Ha = max(before), max(after)
+        wd = {"plan": plan, "keep": keep, "K": K.value, "kb": kbs[r], "ke": kbs[r + 1], "x": xs[r], "u": us[r],
+              "y": ys, "F": F, "Hb": Hb, "Ha": Ha, "ctl": ctl[r], "rec_doubles": rd.value,
+              "ws2": torch.empty(max(1, wsb[r]), dtype=torch.uint8, device=dev),
+              "xwin": torch.zeros((max(1, xs[r][1] - xs[r][0]), 2), dtype=torch.int16, device=dev),
+              "summ": torch.zeros(16, dtype=torch.float64, device=dev),
+              "i_out": torch.zeros(1, dtype=torch.float64, device=dev),
+              "rec_in": torch.zeros(rd.value, dtype=torch.float64, device=dev),
+              "rec_out": torch.zeros(rd.value, dtype=torch.float64, device=dev),
+              "flag": torch.zeros(1, dtype=torch.int32, device=dev),
+              "ebuf": torch.zeros(max(1, Ha + Hb), dtype=torch.int32, device=dev),
+              "eall": torch.zeros(world * max(1, Ha + Hb), dtype=torch.int32, device=dev)}
+        # the 192 kHz runs as a chunk-sharded measure-only track: its output buffer is the
+        # filter's windowed output (no copy)
+        wd["span"] = Span192([y1 - y0 for y0, y1 in ys], r, world, self.group, job.settings.get("lufs"), dev)
+        self._wd = wd
+        return wd
+
+    def _fill_window(self, wd):
+        """the chain frames [x_lo, x_hi) this rank's resampler reads: the previous rank's
+        last frames, its own span, the next rank's first frames (one all-gather of every
+        rank's first Ha and last Hb frames)"""
+        job, r, world = self.job, self.rank, self.world
+        Ha, Hb, F = wd["Ha"], wd["Hb"], wd["F"]
+        n = self.span_frames[r]
+        out32 = job.out[:n].view(torch.int32).reshape(-1)
+        eb = wd["ebuf"]
+        if Ha + Hb > 0:
+            eb.zero_()
+            m = min(Ha, n)
+            eb[:m].copy_(out32[:m])
+            m = min(Hb, n)
+            eb[Ha + Hb - m:Ha + Hb].copy_(out32[n - m:n])
+            self._all_gather(wd["eall"], eb)
+        ea = wd["eall"].view(world, -1)
+        x0, x1 = wd["x"]
+        xw = wd["xwin"].view(torch.int32).reshape(-1)
+        # [x0, F_r): the previous rank's last frames
+        if x0 < F[r]:
+            k = F[r] - x0
+            xw[:k].copy_(ea[r - 1][Ha + Hb - k:Ha + Hb])
+        a, b = max(x0, F[r]), min(x1, F[r + 1])
+        if b > a:
+            xw[a - x0:b - x0].copy_(out32[a - F[r]:b - F[r]])
+        if x1 > F[r + 1]:
+            k = x1 - F[r + 1]
+            xw[x1 - x0 - k:].copy_(ea[r + 1][:k])
+
+    def _filter_windowed(self, wd, desc, measured, offset_i):
+        """one filter run over this rank's segments [kb, ke) in its windows
+        (amx_loudnorm_192k_shard, windowed): part 0 (the 192 kHz stream over the u
+        window, every frame's statistics from the all-reduced hop energies), part 1
+        (gains, the fill pre-pass, the segments from guessed states), then the walks in
+        rank order with the one-record hand-off.  False: the parallel form cannot run
+        this track (a quiet start, a walk fallback) -- every rank takes the same branch."""
+        import ctypes
+        from . import capi
+        L = capi.load()
+        job, rank, world = self.job, self.rank, self.world
+        kb, ke = wd["kb"], wd["ke"]
+        y_out = wd["span"].job.out
+
+        def part(p):
+            sh = capi.LnShard(p, kb, ke, 1, -1, -1, capi.ptr(wd["rec_in"]) if rank > 0 else None,
+                              capi.ptr(wd["rec_out"]) if rank < world - 1 else None)
+            capi.check(L.amx_loudnorm_192k_shard(
+                wd["plan"].h, 0, ctypes.byref(desc), capi.ptr(measured), capi.ptr(offset_i), ctypes.byref(sh),
+                capi.ptr(wd["xwin"]), capi.ptr(job.hops), int(job.max_hops), capi.ptr(job.peak), capi.ptr(y_out),
+                capi.ptr(wd["summ"]), capi.ptr(wd["ws2"]), job._s(None)), "amx_loudnorm_192k_shard")
+
+        ctl = wd["ws2"][wd["ctl"]:wd["ctl"] + 4].view(torch.int32)
+        part(0)
+        if int(ctl.item()) != 0:
+            return False
+        part(1)
+        if rank > 0:
+            (s,), st = _staged(self.group, wd["rec_in"])
+            dist.recv(s, src=rank - 1, group=self.group)
+            if st:
+                wd["rec_in"].copy_(s)
+        part(2)
+        if rank < world - 1:
+            (s,), _ = _staged(self.group, wd["rec_out"])
+            dist.send(s, dst=rank + 1, group=self.group)
+        flag = wd["flag"]
+        flag.copy_(ctl[0:1] == 2)
+        (f,), st = _staged(self.group, flag)
+        dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+        return int(f.item()) == 0
+
+    def _dynamic_windowed(self, wd):
+        """the reference's two loudnorm passes in dynamic mode (:229 / :240) and the
+        alimiter (:223) over the ranks' windows: filter pass 1 -> the loudness of its
+        output measured over the runs (Span192) -> target_offset; filter pass 2 with the
+        step's own statistics row; its peaks and the alimiter over the runs.  None: the
+        parallel form cannot run this track (the replicated form takes it)."""
+        from . import capi, loudness
+        from .settings import LOUDNORM_LRA, LOUDNORM_TP
+        job = self.job
+        S = wd["span"]
+        self._fill_window(wd)
+        target = float(job.settings["lufs"])
+        d1 = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
+        if not self._filter_windowed(wd, d1, None, None):
+            return None
+        S.measure(True)
+        wd["i_out"].copy_(S.job.stats[0, 0:1])                    # pass 1's output loudness
+        d2 = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
+        if not self._filter_windowed(wd, d2, job.stats[0], wd["i_out"]):
+            return None
+        S.measure(False)                                     # the limiter's input bound
+        y = S.limit()
+        i_out = float(wd["i_out"][0].item())
+        self._forms.append("windowed")
+        info = {"target_offset": loudness._fmt(target - i_out), "pass1_output_i": i_out,
+                "sample_rate": 192000, "limiter_fast": S.fast}
+        return y, info
 
     # -------------------------------------------------------------- the step
     def capture(self, d_in):
@@ -561,15 +751,51 @@ class ShardedTrack:
             job.lim_state.zero_()
             job.finalize(None)
 
-        self._ctl_host = torch.zeros(1, dtype=torch.int32).pin_memory()
-        self._ctl_ev = torch.cuda.Event()
         torch.cuda.synchronize()
         if dist.get_backend(self.group) == "nccl":
-            # RCCL collectives are captured into the graph with the kernels around them
-            # (scripts/rccl_capture_probe.py): the whole step is ONE graph launch, its
-            # three collectives graph nodes on RCCL's stream -- no host launch between
-            # the stretches, and the decision word lands in pinned memory at the end
-            def whole():
+            return self._capture_pipelined(d_in, seg)
+        self._ctl_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self._ctl_ev = torch.cuda.Event()
+        # gloo (the N-rank rehearsal on one GPU) stages every collective through host
+        # copies, which a graph cannot hold: the stretches between them are the graphs
+        g1 = seg(lambda: job.run_chunks(d_in), self._pack_edges)
+        g2 = seg(self._unpack_edges, lambda: job.loudness_pass1(tail=True), self._pack_x)
+        g3 = seg(self._unpack_x, lambda: job.loudness_pass2(carry=True)) if lufs_on else seg(self._unpack_x)
+        g4 = seg(job.histograms, job.decide, fin) if lufs_on else seg(job.decide, fin)
+        self._g = [g1, g2, g3, g4]
+        return self._g
+
+    # the pipelined replay's per-slot state: a MasteringJob, its exchange buffers, the
+    # pinned decision word and its event, its graph
+    _SLOT_KEYS = ("job", "tails_all", "_ebuf", "_eall", "_xbuf", "_xall", "_ctl_host", "_ctl_ev", "_g")
+
+    def _use(self, k):
+        for key, v in self._slots[k].items():
+            setattr(self, key, v)
+
+    def _capture_pipelined(self, d_in, seg):
+        """Two buffer sets (slots), each with its own job, exchange buffers and graph: the
+        whole step as ONE graph with its RCCL collectives captured as nodes
+        (scripts/rccl_capture_probe.py), the decision word copied to pinned memory at
+        its end.  replay() alternates them, so step k + 1 is enqueued before the host
+        reads step k's word: the host never stalls the device, and a step whose limiter
+        needs the rank-to-rank hand-off (or dynamic mode) is finished on its own slot,
+        in stream order after step k + 1 (which touches only the other slot's
+        buffers).  Every rank takes the same branch (the word comes from all-reduced
+        data), so RCCL operations stay in the same order on every rank."""
+        lufs_on = self.job.dd.lufs_on
+        slots = []
+        for k in range(2):
+            if k == 1:
+                self.job = MasteringJob(*self._job_args[0], **self._job_args[1])
+                self._setup_exchange()
+                self.step(d_in)                  # the new buffers' first (eager) step
+                torch.cuda.synchronize()
+            job = self.job
+            self._ctl_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+            self._ctl_ev = torch.cuda.Event()
+
+            def whole(job=job):
                 job.run_chunks(d_in)
                 self._pack_edges()
                 self._all_gather(self._eall, self._ebuf)
@@ -583,18 +809,50 @@ class ShardedTrack:
                     reduce_loudness(job.hops, None, self.group)
                     job.histograms()
                 job.decide()
-                fin()
+                # the in-graph limiter run from rest on the device's decision (see fin)
+                job.lim_state.zero_()
+                job.finalize(None)
                 self._ctl_host.copy_(job.ctl[:1], non_blocking=True)
             self._g = [seg(whole)]
-            return self._g
-        # gloo (the N-rank rehearsal on one GPU) stages every collective through host
-        # copies, which a graph cannot hold: the stretches between them are the graphs
-        g1 = seg(lambda: job.run_chunks(d_in), self._pack_edges)
-        g2 = seg(self._unpack_edges, lambda: job.loudness_pass1(tail=True), self._pack_x)
-        g3 = seg(self._unpack_x, lambda: job.loudness_pass2(carry=True)) if lufs_on else seg(self._unpack_x)
-        g4 = seg(job.histograms, job.decide, fin) if lufs_on else seg(job.decide, fin)
-        self._g = [g1, g2, g3, g4]
-        return self._g
+            slots.append({key: getattr(self, key) for key in self._SLOT_KEYS})
+        self._slots = slots
+        self._slot = 0
+        self._pending = None
+        self._use(0)
+        return [sl["_g"][0] for sl in slots]
+
+    def _resolve(self, k):
+        """finish the step that ran on slot k: wait for its decision word and, if the
+        limiter can engage, hand its state along; dynamic mode runs the 192 kHz path.
+        Returns the step's output."""
+        from . import capi
+        cur = {key: getattr(self, key) for key in self._SLOT_KEYS}
+        self._use(k)
+        try:
+            job = self.job
+            while not self._ctl_ev.query():
+                pass
+            ctl = int(self._ctl_host[0])
+            if is_dynamic(ctl):
+                return self.dynamic()
+            if not (ctl & capi.CTL_FAST):
+                chain_state_speculative(job.lim_state, lambda: job.finalize(False),
+                                        lambda v: is_rest_state(v, job.bs), self.rank, self.world,
+                                        self.group, first_run_done=True)
+            return job.y[:job.info.out_frames]
+        finally:
+            for key, v in cur.items():
+                setattr(self, key, v)
+
+    def flush(self):
+        """The output of the last replay(), final (the pipelined replay resolves a step
+        when the next one has been enqueued; call this before reading the last output).
+        None when nothing is pending."""
+        if self._slots is None or self._pending is None:
+            return getattr(self, "_last_out", None)
+        k, self._pending = self._pending, None
+        self._last_out = self._resolve(k)
+        return self._last_out
 
     def _one_rank_dynamic(self, y):
         d = self.job.dynamic_output(0) if self.dyn else None
@@ -604,13 +862,25 @@ class ShardedTrack:
         return d[0]
 
     def replay(self):
+        """One step from the captured graph(s).  Pipelined (N > 1 over RCCL): enqueues
+        the step on the next slot, then resolves the previous step (its decision word,
+        and the rare hand-off / dynamic path on its own slot); returns this step's
+        output buffer, final after the next replay() or flush()."""
         if not self.xchg:
-            return self._one_rank_dynamic(self.job.replay())
+            self._last_out = self._one_rank_dynamic(self.job.replay())
+            return self._last_out
         from . import capi
-        job = self.job
-        if len(self._g) == 1:
+        if self._slots is not None:
+            k = self._slot
+            self._use(k)
             self._g[0].replay()                 # the whole step, collectives included
-        else:
+            self._ctl_ev.record()
+            prev, self._pending, self._slot = self._pending, k, k ^ 1
+            if prev is not None:
+                self._last_out = self._resolve(prev)
+            return self.job.y[:self.job.info.out_frames]
+        job = self.job
+        if len(self._g) == 4:
             g1, g2, g3, g4 = self._g
             g1.replay()
             self._all_gather(self._eall, self._ebuf)
@@ -631,12 +901,14 @@ class ShardedTrack:
         while not self._ctl_ev.query():
             pass
         if is_dynamic(int(self._ctl_host[0])):
-            return self.dynamic()
+            self._last_out = self.dynamic()
+            return self._last_out
         if not (int(self._ctl_host[0]) & capi.CTL_FAST):
             chain_state_speculative(job.lim_state, lambda: job.finalize(False),
                                     lambda v: is_rest_state(v, job.bs), self.rank, self.world,
                                     self.group, first_run_done=True)
-        return job.y[:job.info.out_frames]
+        self._last_out = job.y[:job.info.out_frames]
+        return self._last_out
 
     def step(self, d_in):
         """One pass of the whole path over this rank's chunks (input resident)."""
@@ -760,6 +1032,10 @@ class ShardedBatch:
 
     def replay(self):
         return self.job.replay()
+
+    def flush(self):
+        """ShardedTrack's interface: a batch step needs no host resolution"""
+        return None
 
     def finish_dynamic(self):
         """After a step: finish this rank's tracks that loudnorm sends to dynamic mode

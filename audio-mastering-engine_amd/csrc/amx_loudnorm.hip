@@ -1167,7 +1167,9 @@ __device__ __forceinline__ double2 lp_val(const LpArgs &a, const LpWave &W, int 
     const int64_t pos = lp_pos(W.f, s);
     const bool fin = W.f.fin != 0;
     const bool past = fin && pos >= a.n;
-    const float2 x = reinterpret_cast<const float2 *>(a.u)[past ? 0 : pos];
+    // (a past position reads the track's last one, unused: inside every window that
+    // holds FINAL, amx_ln_shard.windowed)
+    const float2 x = reinterpret_cast<const float2 *>(a.u)[past ? a.n - 1 : pos];
     const int64_t q = pos - LP_RS > 0 ? pos - LP_RS : 0;
     int t, i;
     if (a.n < ((int64_t)1 << 31)) {             // wave-uniform: 32-bit quotient (tracks < 3.1 h)
@@ -1310,6 +1312,9 @@ __device__ __forceinline__ bool lp_flags_any(const LpWave &W, int s0, int len) {
 // candidate and is skipped without loading a value -- 64 groups per ballot
 __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, int count, double &peak_value,
                          int &peak_slot) {
+#ifdef AMX_LPV_NODETECT        // measurement variant: the limiter never engages (wrong output)
+    return -1;
+#endif
     const int lane = threadIdx.x;
     int slot0 = W.f.lbi + smp + LP_ATT;
     if (slot0 >= LP_RS) slot0 -= LP_RS;
@@ -1604,6 +1609,9 @@ __device__ __forceinline__ void lp_call(const LpArgs &a, LpWave &W, int emit) {
             }
         }
     } while (smp < nb);
+#ifdef AMX_LPV_NOEMIT          // measurement variant: no output (wrong output)
+    emit = 0;
+#endif
     if (emit == 1) lp_emit_sparse(a, W);
     else if (emit == 2) lp_emit(a, W);
 }
@@ -1652,7 +1660,11 @@ __device__ __forceinline__ void lp_snapshot(const LpArgs &a, const LpWave &W, do
     for (int j = lane; j < LP_WIN; j += 64) {
         int s = w0 + j;
         if (s >= LP_RS) s -= LP_RS;
+#ifdef AMX_LPV_NOSNAP          // measurement variant: the window's values not loaded (wrong output)
+        const double2 v = make_double2(0.0, 0.0);
+#else
         const double2 v = lp_val(a, W, s);
+#endif
         rec[16 + 2 * j] = v.x;
         rec[17 + 2 * j] = v.y;
     }

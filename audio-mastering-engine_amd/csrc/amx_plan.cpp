@@ -1295,7 +1295,7 @@ struct LnLayout {
 // wave then runs one segment, Fs + Wf frames (r04m: a 5-min track 11.9 -> 9.1 ms per
 // dynamic step from Fs 4 / Wf 3 / 1024 waves); a longer track takes longer segments, so
 // the warm-up share Wf / Fs shrinks instead of waves running several segments each.
-LnLayout ln_layout(int64_t n192) {
+LnLayout ln_layout(int64_t n192, int64_t u_frames = -1, int p_cap = -1) {
     LnLayout l;
     l.Wf = 2;
     int pmax = 3072;
@@ -1314,9 +1314,10 @@ LnLayout ln_layout(int64_t n192) {
     l.M = (29 + l.Fs - 1) / l.Fs;
     l.K = 1 + l.J + l.M;
     l.P = std::min(l.K, pmax);
+    if (p_cap > 0) l.P = std::min(l.P, p_cap);     // a window's segments need no more waves
     int64_t o = 0;
     auto take = [&](int64_t bytes) { const int64_t at = o; o += ((bytes + 255) / 256) * 256; return at; };
-    l.o_u = take(n192 * 2 * (int64_t)sizeof(float));
+    l.o_u = take((u_frames < 0 ? n192 : u_frames) * 2 * (int64_t)sizeof(float));
     l.o_ring = take((2 * 40320 + 64) * (int64_t)sizeof(double));
     l.o_ctl = take(16 * sizeof(int));
     l.o_dctl = take(8 * sizeof(double));
@@ -1427,7 +1428,8 @@ namespace {
 int ln_args(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const double *d_measured,
             const double *d_offset_i, const int32_t *d_gate, const int16_t *d_out, const double *d_hops,
             int64_t max_hops, const double *d_peak, int16_t *d_y192, double *d_summary, void *d_ws2,
-            amx::LnArgs &a, amx::LpArgs &q, int64_t &n192) {
+            amx::LnArgs &a, amx::LpArgs &q, int64_t &n192, int64_t u_lo = 0, int64_t u_frames = -1,
+            int64_t y_lo = 0, int p_cap = -1) {
     if (!p || track < 0 || track >= p->n_tracks) return fail(AMX_EINVAL, "bad argument");
     n192 = 0;
     if (int rc = ln_frames(p, track, &n192)) return rc;
@@ -1437,13 +1439,16 @@ int ln_args(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const double
     if (sp.tframe0 != 0 || sp.ttotal != sp.out_n)
         return fail(AMX_EINVAL, "loudnorm's 192 kHz modes run on whole tracks (one plan holds the track)");
     if (max_hops < n192 / 19200 + 1) return fail(AMX_EINVAL, "d_hops holds %lld hops", (long long)max_hops);
-    const LnLayout lo = ln_layout(n192);
+    const LnLayout lo = ln_layout(n192, u_frames, p_cap);
     char *w = reinterpret_cast<char *>(d_ws2);
     a = amx::LnArgs{};
     a.n192 = n192;
-    a.u = reinterpret_cast<float *>(w + lo.o_u);
+    // a window (amx_ln_shard.windowed): u holds positions [u_lo, ..) and d_y192 starts at
+    // position y_lo; the kernels index whole-track positions, so the bases move back
+    // (only positions inside the windows are ever touched)
+    a.u = reinterpret_cast<float *>(reinterpret_cast<uintptr_t>(w + lo.o_u) - (uintptr_t)u_lo * 2 * sizeof(float));
     a.ring = reinterpret_cast<double *>(w + lo.o_ring);
-    a.y = d_y192;
+    a.y = reinterpret_cast<int16_t *>(reinterpret_cast<uintptr_t>(d_y192) - (uintptr_t)y_lo * 2 * sizeof(int16_t));
     a.summary = d_summary;
     a.hops = d_hops + (int64_t)track * max_hops * 2;
     a.peak = d_peak + (int64_t)track * 4;
@@ -1510,7 +1515,7 @@ int ln_args(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const double
     q.wring = reinterpret_cast<double *>(w + lo.o_wring);
     q.ctl = reinterpret_cast<int *>(w + lo.o_ctl);
     q.dctl = reinterpret_cast<double *>(w + lo.o_dctl);
-    q.y = d_y192;
+    q.y = a.y;
     q.summary = d_summary;
     a.lp_ctl = q.ctl;
     a.lp_dctl = q.dctl;
@@ -1555,18 +1560,19 @@ int amx_loudnorm_192k_shard(amx_plan *p, int32_t track, const amx_loudnorm_desc 
     amx::LnArgs a;
     amx::LpArgs q;
     int64_t n192 = 0;
+    if (!p || track < 0 || track >= p->n_tracks) return fail(AMX_EINVAL, "bad argument");
+    if (int rc = ln_frames(p, track, &n192)) return rc;
+    int64_t win[7] = {0, 0, sh->u_lo, sh->u_hi, 0, 0, 0};
+    if (sh->windowed || sh->u_lo < 0) {
+        int64_t wsb = 0;
+        if (int rc = amx_loudnorm_192k_shard_window(p, track, sh->kb, sh->ke, win, &wsb)) return rc;
+    }
+    const int64_t u_lo = win[2], u_hi = win[3];
     if (int rc = ln_args(p, track, d, d_measured, d_offset_i, nullptr, d_out, d_hops, max_hops, d_peak, d_y192,
-                         d_summary, d_ws2, a, q, n192))
+                         d_summary, d_ws2, a, q, n192, sh->windowed ? u_lo : 0, sh->windowed ? u_hi - u_lo : -1,
+                         sh->windowed ? win[4] : 0, sh->windowed ? sh->ke - sh->kb : -1))
         return rc;
     if (sh->kb < 0 || sh->ke > q.K || sh->kb > sh->ke) return fail(AMX_EINVAL, "segments [%d, %d) of %d", sh->kb, sh->ke, q.K);
-    int64_t u_lo = sh->u_lo, u_hi = sh->u_hi;
-    if (u_lo < 0) {
-        // what segments [kb, ke) read: from Wf + 2 frames before the first one's start
-        // (its warm-up) to a ring and two frames past the last one's end
-        const LnLayout lo = ln_layout(n192);
-        u_lo = std::max<int64_t>(0, ln_seg_base(lo, n192, sh->kb) - (int64_t)19200 * (lo.Wf + 2));
-        u_hi = sh->ke < lo.K ? std::min<int64_t>(n192, ln_seg_base(lo, n192, sh->ke) + AMX_LN_RING + 2 * 19200) : n192;
-    }
     if (u_hi > n192 || u_lo > u_hi) return fail(AMX_EINVAL, "bad 192 kHz range");
     if (sh->part == 2 && sh->kb > 0 && !sh->d_rec_in) return fail(AMX_EINVAL, "segment %d needs the true state", sh->kb);
     q.kb = sh->kb;
@@ -1578,8 +1584,43 @@ int amx_loudnorm_192k_shard(amx_plan *p, int32_t track, const amx_loudnorm_desc 
     // the positions segments [kb, ke) emit
     const LnLayout lo = ln_layout(n192);
     const int64_t y_lo = ln_seg_base(lo, n192, sh->kb), y_hi = sh->ke < lo.K ? ln_seg_base(lo, n192, sh->ke) : n192;
-    HIPCHK(amx::launch_loudnorm_shard(a, q, reinterpret_cast<const uint32_t *>(d_out) + sp.out_off, sp.out_n, r,
-                                      u_lo, u_hi, y_lo, y_hi, sh->part, (hipStream_t)stream));
+    // windowed: d_out holds track frames [x_lo, x_hi) (the base moves back to frame 0)
+    const uint32_t *x = sh->windowed
+                            ? reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(d_out) -
+                                                                 (uintptr_t)win[0] * sizeof(uint32_t))
+                            : reinterpret_cast<const uint32_t *>(d_out) + sp.out_off;
+    HIPCHK(amx::launch_loudnorm_shard(a, q, x, sp.out_n, r, u_lo, u_hi, y_lo, y_hi, sh->part, (hipStream_t)stream));
+    return AMX_OK;
+}
+
+int amx_loudnorm_192k_shard_window(const amx_plan *p, int32_t track, int32_t kb, int32_t ke, int64_t *win,
+                                   int64_t *ws_bytes) {
+    if (!p || track < 0 || track >= p->n_tracks || !win || !ws_bytes) return fail(AMX_EINVAL, "bad argument");
+    int64_t n192 = 0;
+    if (int rc = ln_frames(p, track, &n192)) return rc;
+    const LnLayout lo = ln_layout(n192);
+    if (kb < 0 || ke > lo.K || kb >= ke) return fail(AMX_EINVAL, "segments [%d, %d) of %d", kb, ke, lo.K);
+    // what segments [kb, ke) read: from Wf + 2 frames before the first one's start (its
+    // warm-up) to a ring and two frames past the last one's end
+    const int64_t u_lo = std::max<int64_t>(0, ln_seg_base(lo, n192, kb) - (int64_t)19200 * (lo.Wf + 2));
+    const int64_t u_hi = ke < lo.K ? std::min<int64_t>(n192, ln_seg_base(lo, n192, ke) + AMX_LN_RING + 2 * 19200) : n192;
+    // the chain frames the resampler reads for them: output j's window starts at frame
+    // floor(j M / L) - 15 (32 taps), with a margin; 192 kHz input: the positions themselves
+    const SpanDev &sp = p->spans[track];
+    int64_t x_lo = u_lo, x_hi = u_hi;
+    if (p->resamp) {
+        x_lo = std::max<int64_t>(0, (int64_t)((__int128)u_lo * p->upM / p->upL) - 40);
+        x_hi = std::min<int64_t>(sp.out_n, (int64_t)(((__int128)u_hi * p->upM + p->upL - 1) / p->upL) + 40);
+    }
+    win[0] = x_lo;
+    win[1] = x_hi;
+    win[2] = u_lo;
+    win[3] = u_hi;
+    win[4] = ln_seg_base(lo, n192, kb);
+    win[5] = ke < lo.K ? ln_seg_base(lo, n192, ke) : n192;
+    const LnLayout lw = ln_layout(n192, u_hi - u_lo, ke - kb);
+    win[6] = lw.o_ctl;
+    *ws_bytes = lw.total;
     return AMX_OK;
 }
 

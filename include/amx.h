@@ -321,7 +321,10 @@ AMX_API int amx_loudnorm_192k_ex(amx_plan *plan, int32_t track, const amx_loudno
  * frame).  Outputs: d_y192 frames [start(kb), start(ke)) (whole-track positions).
  * Replaces no single reference line: the reference runs the filter on one process. */
 typedef struct amx_ln_shard {
-    int32_t part, kb, ke, pad_;
+    /* windowed != 0: the rank holds only windows of the track (amx_loudnorm_192k_shard_window):
+     * d_out = track frames [x_lo, x_hi), d_y192 = 192 kHz positions [y_lo, y_hi), d_ws2 of
+     * the window's size with the stream u over [u_lo, u_hi) only (u_lo / u_hi ignored) */
+    int32_t part, kb, ke, windowed;
     int64_t u_lo, u_hi;
     const double *d_rec_in;
     double *d_rec_out;
@@ -331,6 +334,16 @@ AMX_API int amx_loudnorm_192k_shard(amx_plan *plan, int32_t track, const amx_lou
                                     const int16_t *d_out, const double *d_hops, int64_t max_hops,
                                     const double *d_peak, int16_t *d_y192, double *d_summary, void *d_ws2,
                                     void *stream);
+/* The windows a rank running segments [kb, ke) of the track's filter needs when it holds
+ * no whole-track buffer (amx_ln_shard.windowed): win[0..1] = the chain-output frames
+ * [x_lo, x_hi) its resampler reads (its own span plus halos of the neighbours' spans),
+ * win[2..3] = the 192 kHz positions [u_lo, u_hi) its segments read, win[4..5] = the output
+ * positions [y_lo, y_hi) they emit, win[6] = the byte offset in that d_ws2 of the int32
+ * control words; *ws_bytes = the d_ws2 size of the window (the whole-track records stay;
+ * the stream and the limiter waves are the window's).  Per-rank memory and traffic then
+ * scale as 1 / ranks. */
+AMX_API int amx_loudnorm_192k_shard_window(const amx_plan *plan, int32_t track, int32_t kb, int32_t ke,
+                                           int64_t *win, int64_t *ws_bytes);
 /* The parallel form's segments of the track's 192 kHz filter run: starts[k] (k < *K, cap
  * entries) = the output frame segment k starts at (starts[*K] = the frame count); *k_fin
  * = the first segment of the FINAL flush frame (one rank must hold [k_fin, K)); the

@@ -120,12 +120,14 @@ def test_two_ranks_match_one(gpu, case):
     seconds = 75.0 if case.startswith("c3_lufs") or case.startswith("dynamic") else 32.0
     x = _track(seconds, case)
     if case.startswith("dynamic"):
-        # the one-GPU reference: the whole track through master_array (dynamic_track)
-        from amx.engine import master_array
-        y1, rep = master_array(torch.from_numpy(np.ascontiguousarray(x)), RATE.get(case, FS), CASES[case],
-                               quantum=512)
-        assert rep["modes"][0] == "dynamic" and rep["sample_rate"] == 192000
-        y1 = y1.cpu().numpy()
+        # the reference: the oracle's whole pipeline in dynamic mode (the ranks' filter
+        # gains come from the step's own all-reduced hop energies, which equal the
+        # one-GPU sums up to rounding beside a rank boundary: within 3 LSB)
+        import oracle
+        from amx.chunking import chunk_bounds
+        fs = RATE.get(case, FS)
+        y1, rinfo = oracle.pipeline(oracle.quantize(x), fs, CASES[case], chunk_bounds(x.shape[0], fs, 512))
+        assert rinfo["mode"] == "dynamic" and rinfo["sample_rate"] == 192000
     else:
         one = ShardedTrack(RATE.get(case, FS), 2, CASES[case], x.shape[0], 0, 1, quantum=512)
         y1 = one.step(torch.from_numpy(np.ascontiguousarray(x)).cuda()).cpu().numpy()
@@ -138,15 +140,20 @@ def test_two_ranks_match_one(gpu, case):
     y2 = np.concatenate(parts)
     assert fast[0] == fast[1]
     if case.startswith("dynamic"):
-        # both filter runs split over the ranks by segments, with the limiter-state hand-off
-        # (a quiet start: both run whole on every rank)
-        want = "replicated+replicated" if case == "dynamic_quiet" else "sharded"
+        # both filter runs on the ranks' windows, with the limiter-state hand-off (a quiet
+        # start: the whole filter on every rank)
+        want = "replicated" if case == "dynamic_quiet" else "windowed"
         assert forms == [want] * 2, forms
     # the loud case must exercise the rank-to-rank sequential limiter
     if not case.startswith("dynamic"):
         assert fast[0] == case.startswith("c3_lufs"), "limiter fast path %s" % fast[0]
     assert y2.shape == y1.shape
     diff = np.abs(y2.astype(np.int32) - y1.astype(np.int32))
+    if case.startswith("dynamic"):
+        exact = float((diff == 0).mean())
+        print("%s over 2 ranks vs the oracle: max |diff| %d LSB, exact %.7f" % (case, diff.max(), exact))
+        assert diff.max() <= 3 and exact >= 0.999, (int(diff.max()), exact)
+        return
     assert diff.max() == 0, "max |diff| %d LSB at %s (limiter fast path %s)" % (
         diff.max(), np.argmax(diff.max(axis=1)), fast[0])
 
@@ -173,11 +180,17 @@ def test_rccl_forced_exchange_world1(gpu, case):
         tr = ShardedTrack(FS, 2, CASES[case], x.shape[0], 0, 1, quantum=512, force_exchange=True)
         y_eager = tr.step(d_in).cpu().numpy()
         tr.capture(d_in)
-        # the N > 1 step as ONE graph: the RCCL collectives are captured nodes
-        assert isinstance(tr._g, list) and len(tr._g) == 1
-        y_graph = tr.replay().cpu().numpy()
+        # the N > 1 step as ONE graph per slot: the RCCL collectives are captured nodes;
+        # the two slots alternate, a step resolved when the next one is enqueued
+        assert isinstance(tr._g, list) and len(tr._g) == 1 and len(tr._slots) == 2
+        tr.replay()
+        y_graph = tr.flush().cpu().numpy()
+        for _ in range(3):
+            tr.replay()
+        y_graph2 = tr.flush().cpu().numpy()
         torch.cuda.synchronize()
     finally:
         dist.destroy_process_group()
     np.testing.assert_array_equal(y_eager, y_ref)
     np.testing.assert_array_equal(y_graph, y_ref)
+    np.testing.assert_array_equal(y_graph2, y_ref)

@@ -527,3 +527,83 @@ def test_shard_parts_vs_oracle(gpu, oracle_mod, monkeypatch, ranks, seg, warm):
     assert L.amx_loudnorm_192k_shard(job.plan.h, 0, ctypes.byref(d), None, None, ctypes.byref(sh), capi.ptr(job.out),
                                      capi.ptr(job.hops), int(job.max_hops), capi.ptr(job.peak), capi.ptr(job2.out),
                                      capi.ptr(summ), capi.ptr(ws2s[1]), None) != 0
+
+
+@pytest.mark.parametrize("ranks,seg,warm,fs", [(3, None, None, 48000), (3, 1, 0, 48000), (2, None, None, 44100)])
+def test_shard_windows_vs_oracle(gpu, oracle_mod, monkeypatch, ranks, seg, warm, fs):
+    """the windowed shard (amx_loudnorm_192k_shard_window + amx_ln_shard.windowed): each
+    simulated rank holds ONLY its windows -- the chain frames its resampler reads, the
+    192 kHz stream its segments read (a d_ws2 of the window's size) and the output
+    positions they emit -- poisoned outside what it writes; the runs concatenated must be
+    the oracle's filter output (within 3 LSB), and equal the whole-track shard's output"""
+    import ctypes
+    import torch
+    from amx import capi
+    from amx.dist import shard_segments
+    from amx.engine import MasteringJob
+    if seg is not None:
+        monkeypatch.setenv("AMX_LN_SEG", str(seg))
+        monkeypatch.setenv("AMX_LN_WARM", str(warm))
+    x = _dynamic_signal(21.0, fs, 29)
+    x16 = oracle_mod.quantize(x)
+    st = oracle_mod.loudnorm_measure(x16, fs)
+    n = x16.shape[0]
+    job = MasteringJob(fs, 2, {"lufs": -14.0}, [n], input_s16=True, chunks=[(0, 0, n)], measure_only=True)
+    job.out[:n].copy_(torch.from_numpy(x16))
+    job.loudness_pass1(tail=False)
+    job.loudness_pass2(carry=False)
+    job.histograms()
+    job.decide()
+    n192, job2, ws2_whole, summ = job._job192(0, cached=False)[0:4]
+    L = capi.load()
+    K, kf, rd, co = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+    capi.check(L.amx_loudnorm_192k_segments(job.plan.h, 0, None, 0, ctypes.byref(K), ctypes.byref(kf),
+                                            ctypes.byref(rd), ctypes.byref(co)), "segments")
+    ranges = shard_segments(K.value, kf.value, ranks)
+    dev = job.device
+    wins, bufs = [], []
+    for kb, ke in ranges:
+        win, b = (ctypes.c_int64 * 7)(), ctypes.c_int64()
+        capi.check(L.amx_loudnorm_192k_shard_window(job.plan.h, 0, kb, ke, win, ctypes.byref(b)), "window")
+        x0, x1, u0, u1, y0, y1, ctl_off = list(win)
+        assert 0 <= x0 < x1 <= n and 0 <= u0 < u1 <= n192 and u0 <= y0 < y1 <= u1
+        xw = torch.from_numpy(np.ascontiguousarray(x16[x0:x1])).to(dev)
+        bufs.append((xw, torch.empty(b.value, dtype=torch.uint8, device=dev),
+                     torch.empty((y1 - y0, 2), dtype=torch.int16, device=dev)))
+        wins.append((x0, x1, u0, u1, y0, y1, ctl_off))
+    # a window of no segments is refused
+    w0, b0 = (ctypes.c_int64 * 7)(), ctypes.c_int64()
+    assert L.amx_loudnorm_192k_shard_window(job.plan.h, 0, 3, 3, w0, ctypes.byref(b0)) != 0
+    recs = [torch.zeros(rd.value, dtype=torch.float64, device=dev) for _ in range(ranks)]
+    for offset in (0.0, 9.0):
+        d = capi.LoudnormDesc(-14.0, 11.0, -1.5, float(st["input_i"]), float(st["input_lra"]),
+                              float(st["input_tp"]), float(st["input_thresh"]), offset)
+        for r, (kb, ke) in enumerate(ranges):
+            xw, ws2, yw = bufs[r]
+            ws2.fill_(0xA5)
+            yw.fill_(12345)
+            for part in (0, 1, 2):
+                sh = capi.LnShard(part, kb, ke, 1, -1, -1, capi.ptr(recs[r - 1]) if r > 0 else None,
+                                  capi.ptr(recs[r]) if r < ranks - 1 else None)
+                capi.check(L.amx_loudnorm_192k_shard(
+                    job.plan.h, 0, ctypes.byref(d), None, None, ctypes.byref(sh), capi.ptr(xw),
+                    capi.ptr(job.hops), int(job.max_hops), capi.ptr(job.peak), capi.ptr(yw),
+                    capi.ptr(summ), capi.ptr(ws2), None), "shard windowed")
+                c = wins[r][6]
+                ctl = int(ws2[c:c + 4].view(torch.int32).item())
+                assert ctl == 0, (r, part, ctl)
+        y = np.concatenate([b[2].cpu().numpy() for b in bufs])
+        assert y.shape[0] == n192
+        ref, _ = oracle_mod.loudnorm(x16, fs, -14.0, measured=st, offset=offset)
+        _cmp(y, ref, "shard windows x%d Fs=%s Wf=%s %d Hz offset %.1f" % (ranks, seg, warm, fs, offset))
+        # the whole-track buffers' form: the same numbers
+        job2.out.zero_()
+        for r, (kb, ke) in enumerate(ranges):
+            for part in (0, 1, 2):
+                sh = capi.LnShard(part, kb, ke, 0, -1, -1, capi.ptr(recs[r - 1]) if r > 0 else None,
+                                  capi.ptr(recs[r]) if r < ranks - 1 else None)
+                capi.check(L.amx_loudnorm_192k_shard(
+                    job.plan.h, 0, ctypes.byref(d), None, None, ctypes.byref(sh), capi.ptr(job.out),
+                    capi.ptr(job.hops), int(job.max_hops), capi.ptr(job.peak), capi.ptr(job2.out),
+                    capi.ptr(summ), capi.ptr(ws2_whole), None), "shard")
+        np.testing.assert_array_equal(y, job2.out[:n192].cpu().numpy())
