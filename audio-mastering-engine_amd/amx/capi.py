@@ -18,7 +18,7 @@ ABI_VERSION = 3
 CTL_FAST = 1
 MODES = ("off", "skip", "linear", "dynamic")
 STATS = 16
-UP_EDGE = 16      # frames of a neighbour rank the 192 kHz resampler window reaches (amx.h)
+UP_EDGE = 80      # frames of a neighbour rank the 192 kHz resampler window reaches (amx_internal.hpp)
 STAGES = ("front1", "scan_eq", "front2", "scan_xo", "xover", "rms", "env", "fix", "apply")
 
 
@@ -104,7 +104,7 @@ EXPORTS = ("amx_abi_version", "amx_last_error", "amx_build_id", "amx_plan_create
            "amx_finalize", "amx_env_counters", "amx_pcm_to_s16", "amx_loudnorm_192k_size",
            "amx_loudnorm_192k", "amx_loudnorm_192k_ex", "amx_flac_info", "amx_flac_decode",
            "amx_plan_set_gate", "amx_loudnorm_192k_shard", "amx_loudnorm_192k_segments",
-           "amx_loudnorm_192k_shard_window")
+           "amx_loudnorm_192k_shard_window", "amx_publish_ctl")
 PCM_FORMATS = {"u8": 0, "s16": 1, "s24": 2, "s32": 3, "f32": 4, "f64": 5,
                "s8": 6, "s16be": 7, "s24be": 8, "s32be": 9, "f32be": 10, "f64be": 11}
 
@@ -158,6 +158,7 @@ def load(path=None):
                                        ctypes.c_int64, vp, vp, vp, vp, vp]
     L.amx_loudnorm_192k_shard.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(LoudnormDesc), vp, vp,
                                           ctypes.POINTER(LnShard), vp, vp, ctypes.c_int64, vp, vp, vp, vp, vp]
+    L.amx_publish_ctl.argtypes = [vp, vp, ctypes.c_int32, vp]
     L.amx_loudnorm_192k_shard_window.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                                  ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     L.amx_loudnorm_192k_segments.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.c_int32,

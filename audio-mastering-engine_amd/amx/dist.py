@@ -812,7 +812,7 @@ class ShardedTrack:
                 # the in-graph limiter run from rest on the device's decision (see fin)
                 job.lim_state.zero_()
                 job.finalize(None)
-                self._ctl_host.copy_(job.ctl[:1], non_blocking=True)
+                job.publish_ctl(self._ctl_host)
             self._g = [seg(whole)]
             slots.append({key: getattr(self, key) for key in self._SLOT_KEYS})
         self._slots = slots
@@ -832,7 +832,10 @@ class ShardedTrack:
             job = self.job
             while not self._ctl_ev.query():
                 pass
-            ctl = int(self._ctl_host[0])
+            hv = self._ctl_host.numpy()
+            while hv[0] == -1:                  # (the device's store lands with the step's end)
+                pass
+            ctl = int(hv[0])
             if is_dynamic(ctl):
                 return self.dynamic()
             if not (ctl & capi.CTL_FAST):
@@ -873,6 +876,7 @@ class ShardedTrack:
         if self._slots is not None:
             k = self._slot
             self._use(k)
+            self._ctl_host.fill_(-1)            # (this slot's previous word was read)
             self._g[0].replay()                 # the whole step, collectives included
             self._ctl_ev.record()
             prev, self._pending, self._slot = self._pending, k, k ^ 1

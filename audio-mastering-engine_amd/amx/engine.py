@@ -15,6 +15,7 @@ HIP kernel in libamx.so.  There is no CPU fallback: if the library or a GPU is
 missing, construction raises.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -103,6 +104,7 @@ class MasteringJob:
         self.plan.limiter_prepare(self.fd, limiter_seg_frames, limiter_warm_frames)
         self._i_out = torch.zeros((T,), dtype=torch.float64, device=dev)   # pass 1's output I (dynamic)
         self._dyn_sides = None     # per track, the 192 kHz sets run() enqueues (prepare_dynamic)
+        self._graph_dyn = None
         self.report = {}
 
     # ------------------------------------------------------------ device steps
@@ -180,6 +182,13 @@ class MasteringJob:
             self.plan.h, self.dd, self.fd, capi.ptr(self.hist) if lufs_on else None,
             capi.ptr(self.st_hist) if lufs_on else None, capi.ptr(self.peak), capi.ptr(self.stats),
             capi.ptr(self.gains), capi.ptr(self.ctl), self._s(stream)), "amx_loudness_decide")
+
+    def publish_ctl(self, host, stream=None):
+        """the tracks' decision words into the pinned host tensor `host` (amx_publish_ctl:
+        device stores, no copy node), on the stream"""
+        import ctypes
+        capi.check(capi.load().amx_publish_ctl(capi.ptr(self.ctl), ctypes.c_void_p(host.data_ptr()),
+                                               int(self.n_tracks), self._s(stream)), "amx_publish_ctl")
 
     def finalize(self, fast=None, stream=None):
         """fast None: each track takes the limiter path amx_loudness_decide chose."""
@@ -325,10 +334,12 @@ class MasteringJob:
                             "gains": gains, "limiter_fast": all(fast)})
         return self.report
 
-    def run(self, d_in, stream=None):
+    def run(self, d_in, stream=None, dyn=True, ctl_to=None):
         """Whole pipeline for whole tracks on this GPU, fully on the stream (no host
         round trip); returns y (int16 [frames, 2]).  fetch_report() reads the
-        loudness decision afterwards."""
+        loudness decision afterwards.  dyn False: without the gated dynamic path
+        (capture puts it in a graph of its own); ctl_to: a pinned host tensor the
+        decision words are copied to as soon as they are made (before the limiter)."""
         self.run_chunks(d_in, stream)
         self.timed("up", lambda: self.loudness_pass1(stream, tail=False, part=0), stream)
         self.timed("loud1", lambda: self.loudness_pass1(stream, tail=False, part=1), stream)
@@ -336,8 +347,10 @@ class MasteringJob:
             self.timed("loud2", lambda: self.loudness_pass2(stream, carry=False), stream)
             self.timed("hist", lambda: self.histograms(stream), stream)
         self.timed("decide", lambda: self.decide(stream), stream)
+        if ctl_to is not None:
+            self.publish_ctl(ctl_to, stream)
         self.timed("final", lambda: self.finalize(None, stream), stream)
-        if self._dyn_sides:
+        if self._dyn_sides and dyn:
             # the dynamic path of every track, gated on the device by the track's decision
             # (a linear track's kernels return at once): the step needs no host round trip
             # whichever mode loudnorm takes
@@ -376,8 +389,14 @@ class MasteringJob:
         critical path.  run() has no host round trip, so the captured graph is the
         complete step.  dynamic: the graph also holds loudnorm's dynamic path
         (prepare_dynamic), so a track that takes it is finished inside the step too."""
+        self._graph_dyn = None
         if dynamic:
             self.prepare_dynamic()
+        dyn = bool(self._dyn_sides)
+        if os.environ.get("AMX_DYN_INLINE") == "1":
+            dyn = False      # (diagnostics: the gated dynamic path inside the step's graph)
+        if dyn:
+            self._ctl_pin = torch.full((max(1, self.n_tracks),), -1, dtype=torch.int32).pin_memory()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -386,12 +405,35 @@ class MasteringJob:
         g = torch.cuda.CUDAGraph()
         # thread_local: other threads (a process group's watchdog) may query events meanwhile
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            self.run(d_in)
+            self.run(d_in, dyn=not dyn, ctl_to=self._ctl_pin[:self.n_tracks] if dyn else None)
         self._graph = g
+        if dyn:
+            # the dynamic path of every track, gated per track on the device, in a graph of
+            # its own that replay() launches only when some track's word says dynamic: a
+            # linear step pays none of its ~35 nodes per track
+            gd = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gd, capture_error_mode="thread_local"):
+                for t, side in enumerate(self._dyn_sides):
+                    self._dyn_enqueue(t, side, None, gate=True)
+            self._graph_dyn = gd
         return g
 
     def replay(self):
+        """One step from the captured graph.  With the dynamic path (capture(dynamic=True))
+        the host reads the decision words, which the graph copies to pinned memory
+        before its limiter kernel: they land while that kernel still runs, so the next
+        step's launch is not delayed; the dynamic graph follows only when needed."""
+        if self._graph_dyn is None:
+            self._graph.replay()
+            return self.y[:self.info.out_frames]
+        h = self._ctl_pin
+        h.fill_(-1)                 # (the previous step's copy has landed: it was read)
         self._graph.replay()
+        hv = h.numpy()[:self.n_tracks]
+        while (hv == -1).any():
+            pass
+        if any((int(v) >> 4) & 15 == 3 for v in hv):       # k_decide mode 3 = dynamic
+            self._graph_dyn.replay()
         return self.y[:self.info.out_frames]
 
     def finish_dynamic(self, report=None):

@@ -201,7 +201,9 @@ hipError_t launch_hist(const SpanDev *spans, int n_tracks, int hop, const double
                        int64_t max_hops, const double *bounds, unsigned long long *hist,
                        unsigned long long *st_hist, hipStream_t st);
 // loudness at 192 kHz (amx_loud192.hip): the resampled stream is recomputed from d_out
-#define AMX_UP_EDGE 16     // frames of the neighbour rank's output the resampler window needs
+#define AMX_UP_EDGE 80     // frames of the neighbour rank's output the resampler window needs
+                           // (16 for the 32-tap upsampler; up to 67 for 768 kHz's 132 taps)
+#define AMX_SWR_MAX_ALLOC 144   // the widest resampler row (filter_alloc) restated
 #define AMX_UP_BLOCK 64
 // k_up_poly's template form as one code (launch switch, plan)
 #define AMX_UP_POLY(cmin, cmax, tb) ((cmin) * 256 + (cmax) * 16 + (tb))
@@ -222,7 +224,9 @@ struct UpArgs {
     int lin;                      // libswresample's linear kernel: rows oph, oph + 1 (1024 phases)
     const int32_t *slow;          // segments k_up_slow takes (NULL: all, when static_l == 0)
     int64_t n_slow;
-    const float *bank;            // [pc + 1][32] float32 polyphase bank (row pc = row 0 one tap on)
+    const float *bank;            // [pc + 1][alloc] float32 polyphase bank (row pc = row 0 one tap on)
+    int taps, alloc;              // filter_length, filter_alloc: 32, 32 but for downsampling rates
+                                  // (then every segment goes through k_up_wide)
     const uint32_t *x, *edge;     // d_out (stereo s16 dwords); edge [tracks][2][AMX_UP_EDGE]
     const double *G;              // rows C A^n, n < Lout (the K filter's free response)
     const double *qh, *qt;        // Gram matrices of those rows: head sums [Lout+1][16], tail sums
@@ -312,7 +316,8 @@ struct LpArgs {
 struct SwrDev {
     int pc, lin;
     int64_t src, dst;
-    const float *bank;            // [pc + 1][32]
+    const float *bank;            // [pc + 1][alloc]
+    int taps, alloc;              // filter_length, filter_alloc (32, 32 but downsampling)
 };
 hipError_t launch_loudnorm(const LnArgs &a, const LpArgs &p, const uint32_t *x, int64_t n_in,
                            const SwrDev &r, hipStream_t st);
@@ -355,6 +360,7 @@ struct DecideArgs {
     int32_t *ctl;
 };
 hipError_t launch_decide(const DecideArgs &a, hipStream_t st);
+hipError_t launch_publish(const int32_t *ctl, int32_t *host, int n, hipStream_t st);
 hipError_t launch_kw_carry(const double *tails, const double *P, int n_prev, double *carry,
                            hipStream_t st);
 // per-track sample peak: partial maxima per block into part[track][block][2], the last

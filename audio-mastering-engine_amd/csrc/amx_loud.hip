@@ -725,6 +725,20 @@ hipError_t launch_decide(const DecideArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// the decision words stored straight into the caller's pinned host memory (system-scope
+// stores from one small kernel): no copy node, whose completion signalling stalled the
+// stream ~25 us in a captured step
+__global__ void k_publish(const int32_t *__restrict__ ctl, int32_t *host, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        __hip_atomic_store(host + i, ctl[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_publish(const int32_t *ctl, int32_t *host, int n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, ctl, host, n);
+    return hipGetLastError();
+}
+
 // K-filter state entering this rank's span from the other ranks' zero-start tails:
 // carry = sum_q P_q tail_q (P_q = A^{frames between span q's end and this span},
 // host-computed), per channel; one thread per (channel, row).

@@ -524,6 +524,118 @@ __global__ void __launch_bounds__(64) k_up_edge(UpArgs a) {
     }
 }
 
+// the FMA3 kernel's order over a row of `alloc` taps (a multiple of 8: the downsampling
+// filters of inputs above 192 kHz), the window's frames read from LDS: 8 chains over taps
+// k, k + 8, ..., then the common horizontal sum
+__device__ __forceinline__ float up_dot_wide(const uint32_t *fr, int ch, const float *__restrict__ h, int alloc) {
+    float a[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        float acc = up_sample(fr[k], ch) * h[k];
+        for (int q = 8; q < alloc; q += 8) acc = fmaf(up_sample(fr[k + q], ch), h[k + q], acc);
+        a[k] = acc;
+    }
+    const float b0 = a[0] + a[4], b1 = a[1] + a[5], b2 = a[2] + a[6], b3 = a[3] + a[7];
+    return (b0 + b2) + (b1 + b3);
+}
+
+// Every K segment of a downsampling rate (an input above 192 kHz / 0.97: 352.8, 384,
+// 705.6, 768 kHz; the filter has `taps` > 32 taps in rows of `alloc`), one wave per
+// segment as k_up_edge: the segment's frames staged in LDS from g0 - center, the 2 x Lout
+// outputs in parallel, the K filter on one lane per channel, the energy terms reduced
+// over the wave.  The window of output n is frames obase[n] - center .. + alloc - 1 (the
+// row's zero padding multiplies the frames after it, as the x86 kernel does).
+__global__ void __launch_bounds__(64) k_up_wide(UpArgs a) {
+    extern __shared__ uint32_t sh[];
+    const int lane = threadIdx.x;
+    const int64_t j = a.slow ? a.slow[blockIdx.x] : (int64_t)blockIdx.x;
+    const KwSegDev sg = a.ks[j];
+    const SpanDev sp = a.spans[sg.track];
+    const int t = sg.track;
+    const int64_t g0 = sg.out_pos - sp.out_off;
+    const int c = (a.taps - 1) / 2;
+    const int nf = a.Lin + a.alloc;                               // frames g0 - c + [0, nf)
+    uint32_t *fr = sh;
+    float *us = reinterpret_cast<float *>(sh + nf);               // [n][ch]
+    for (int i = lane; i < nf; i += 64) fr[i] = up_word(a.x, a.edge, sp, t, g0 - c + i);
+    __syncthreads();
+    const int len = sg.len;
+    const int ch = lane & 1;
+    float pk = 0.0f, px = 0.0f;
+    for (int i = lane; i < 2 * a.Lout; i += 64) {                 // i & 1 == ch
+        const int n = i >> 1;
+        const int kb = a.obase[n], ph = a.oph[n];
+        const float u = up_dot_wide(fr + kb, ch, a.bank + (int64_t)ph * a.alloc, a.alloc);
+        us[i] = u;
+        if (n < len) {
+            pk = fmaxf(pk, fabsf(u));
+            px = fmaxf(px, fabsf(up_sample(fr[kb + c], ch)));
+        }
+    }
+#pragma unroll
+    for (int o = 2; o < 64; o <<= 1) {                            // max over the channel's lanes
+        pk = fmaxf(pk, __shfl_xor(pk, o));
+        px = fmaxf(px, __shfl_xor(px, o));
+    }
+    __syncthreads();
+    double *ys = reinterpret_cast<double *>(sh + ((nf + 2 * a.Lout + 1) & ~1));   // [n][ch]
+    if (lane < 2) {
+        double c1[5], c2[5];
+#pragma unroll
+        for (int k = 0; k < 3; k++) { c1[k] = a.cd->kw1[k]; c2[k] = a.cd->kw2[k]; }
+        c1[3] = a.cd->kw1[4]; c1[4] = a.cd->kw1[5];
+        c2[3] = a.cd->kw2[4]; c2[4] = a.cd->kw2[5];
+        double v[4] = {0.0, 0.0, 0.0, 0.0};
+        int n = 0;
+        for (; n < len; n++)
+            ys[2 * n + ch] = hp_step(c2, v[2], v[3], bq_step(c1, v[0], v[1], (double)us[2 * n + ch]));
+        for (; n < a.Lout; n++) ys[2 * n + ch] = 0.0;
+        double *o = a.e + (j * 2 + ch) * AMX_KW_DIM;
+#pragma unroll
+        for (int d = 0; d < AMX_KW_DIM; d++) o[d] = v[d];
+        uint32_t *pq = a.pk + j * 4;
+        pq[ch] = __float_as_uint(pk);
+        pq[2 + ch] = (uint32_t)(px * 32768.0f);
+    }
+    __syncthreads();
+    const int64_t h0 = sg.tframe / a.hop;
+    const int split = (int)((h0 + 1) * a.hop - sg.tframe);
+    double acc[2][2][5] = {};                                     // [ch][piece][term]
+    for (int n = lane; n < len; n += 64) {
+        const double *r = a.G + (int64_t)n * AMX_KW_DIM;
+        const int pc = n < split ? 0 : 1;
+#pragma unroll
+        for (int cc = 0; cc < 2; cc++) {
+            const double y = ys[2 * n + cc];
+#pragma unroll
+            for (int p = 0; p < 2; p++) {
+                const double yy = p == pc ? y : 0.0;
+                acc[cc][p][0] = fma(yy, yy, acc[cc][p][0]);
+#pragma unroll
+                for (int d = 0; d < 4; d++) acc[cc][p][1 + d] = fma(yy, r[d], acc[cc][p][1 + d]);
+            }
+        }
+    }
+#pragma unroll
+    for (int cc = 0; cc < 2; cc++)
+#pragma unroll
+        for (int p = 0; p < 2; p++)
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                double x = acc[cc][p][k];
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) x += __shfl_xor(x, o);
+                acc[cc][p][k] = x;
+            }
+    if (lane < 2) {
+        double *te = a.eterms + (j * 2 + ch) * 10;
+#pragma unroll
+        for (int p = 0; p < 2; p++)
+#pragma unroll
+            for (int k = 0; k < 5; k++) te[p * 5 + k] = ch ? acc[1][p][k] : acc[0][p][k];
+    }
+}
+
 // hop pieces' energies from the exact start states: E = sum yz^2 + 2 s.q + s^T Q s,
 // Q the piece's Gram matrix of the rows C A^n (plan tables: head Qh[k] = sum_{n<k},
 // tail Qt[k] = sum_{k<=n<Lout}); one thread per (segment, channel)
@@ -608,6 +720,10 @@ hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent
             hipError_t e = hipStreamWaitEvent(st, join, 0);
             if (e != hipSuccess) return e;
         }
+    } else if (a.taps != UP_TAPS) {
+        const size_t nf = (size_t)a.Lin + a.alloc;
+        hipLaunchKernelGGL(k_up_wide, dim3((unsigned)a.n_slow), dim3(64),
+                           ((nf + 2 * (size_t)a.Lout + 1) & ~(size_t)1) * 4 + (size_t)a.Lout * 16, st, a);
     } else {
         hipLaunchKernelGGL(k_up_slow, dim3((unsigned)((a.n_slow + AMX_UP_BLOCK / 2 - 1) / (AMX_UP_BLOCK / 2))),
                            dim3(AMX_UP_BLOCK), 0, st, a);

@@ -154,6 +154,42 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_ln_upsample(const uint32_t *__res
     }
 }
 
+// a downsampling rate's resampler (r.taps > 32 taps in rows of r.alloc): one thread per
+// 192 kHz frame, both channels, the window x[base - center ..] read from memory (mirrored
+// at the track's ends), the FMA3 kernel's 8 chains over the row
+__global__ void __launch_bounds__(AMX_BLOCK) k_ln_upsample_wide(const uint32_t *__restrict__ x, int64_t n_in,
+                                                                SwrDev r, int64_t j0, int64_t j1,
+                                                                float *__restrict__ u,
+                                                                const int32_t *__restrict__ gate) {
+    if (AMX_LN_GATED(gate)) return;
+    const int c = (r.taps - 1) / 2;
+    for (int64_t j = j0 + (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x; j < j1; j += (int64_t)gridDim.x * AMX_BLOCK) {
+        const int64_t pos = j * r.dst, idx = pos / r.src;
+        const int64_t base = idx / r.pc;
+        const int ph = (int)(idx % r.pc);
+        const float *h = r.bank + (int64_t)ph * r.alloc;
+        float a0[8], a1[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t v = x[ln_reflect(base - c + k, n_in)];
+            a0[k] = __builtin_fmaf((float)lo16(v) * (1.0f / 32768.0f), h[k], 0.0f);
+            a1[k] = __builtin_fmaf((float)hi16(v) * (1.0f / 32768.0f), h[k], 0.0f);
+        }
+        for (int q = 8; q < r.alloc; q += 8) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t v = x[ln_reflect(base - c + q + k, n_in)];
+                a0[k] = __builtin_fmaf((float)lo16(v) * (1.0f / 32768.0f), h[q + k], a0[k]);
+                a1[k] = __builtin_fmaf((float)hi16(v) * (1.0f / 32768.0f), h[q + k], a1[k]);
+            }
+        }
+        const float b0 = a0[0] + a0[4], b1 = a0[1] + a0[5], b2 = a0[2] + a0[6], b3 = a0[3] + a0[7];
+        const float e0 = a1[0] + a1[4], e1 = a1[1] + a1[5], e2 = a1[2] + a1[6], e3 = a1[3] + a1[7];
+        u[2 * j] = (b0 + b2) + (b1 + b3);
+        u[2 * j + 1] = (e0 + e2) + (e1 + e3);
+    }
+}
+
 // ------------------------------------------------------------ block helpers
 // The filter runs on one workgroup of LN_NT threads per track: every thread carries the
 // (block-uniform) scalar state, the per-sample loops are shared out over the block.  One
@@ -1285,31 +1321,17 @@ __device__ __forceinline__ double2 lp_grp(const LpArgs &a, const LpWave &W, int 
     while (s >= LP_RS) s -= LP_RS;
     return lp_val(a, W, s);
 }
-// any slot of [s0, s0 + len) (mod LP_RS, len <= 64) multiplied since its fill
-__device__ __forceinline__ bool lp_flags_any(const LpWave &W, int s0, int len) {
-    bool any = false;
-#pragma unroll
-    for (int part = 0; part < 2; part++) {
-        const int lo = part == 0 ? s0 : 0;
-        const int hi = part == 0 ? min(s0 + len, LP_RS) : max(s0 + len - LP_RS, 0);
-        for (int w = lo >> 5; w <= ((hi - 1) >> 5) && hi > lo; w++) {
-            const int b0 = w * 32;
-            const int x0 = max(lo, b0) - b0, x1 = min(hi, b0 + 32) - b0;
-            const unsigned m = (x1 - x0 == 32) ? 0xffffffffu : (((1u << (x1 - x0)) - 1u) << x0);
-            any |= (W.flags[w] & m) != 0u;
-        }
-    }
-    return any;
-}
 // detect_peak from offset smp over count positions: peak_delta or -1; the peak's |x|
 // and slot.  64 positions per step: the first one that is a candidate with its
 // previous sample as predecessor is found by a ballot; only from there on is the scan
 // serial (a candidate that fails the 10-sample look-ahead keeps the older predecessor).
 // A candidate needs |x| > ceiling.  Outside FINAL, a slot's value is its position's
-// fill (a function of the position alone, k_lp_fill) or a multiplied value (flagged;
-// the limiter only multiplies by gains <= 1): so a group whose positions' fill maxima
-// (a.bm, 64-position blocks) are <= ceiling and whose slots carry no flag holds no
-// candidate and is skipped without loading a value -- 64 groups per ballot
+// fill (a function of the position alone, k_lp_fill) or that fill multiplied by the
+// limiter's envelope gains, which are <= 1 (attack / release ramps between a gain
+// reduction and 1, sustain at the reduction) up to their rounding: so a group whose
+// positions' fill maxima (a.bm, 64-position blocks), raised by a relative 1e-9 margin
+// for that rounding, are <= ceiling holds no candidate -- flagged or not -- and is
+// skipped without loading a value, 64 groups per ballot
 __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, int count, double &peak_value,
                          int &peak_slot) {
 #ifdef AMX_LPV_NODETECT        // measurement variant: the limiter never engages (wrong output)
@@ -1336,9 +1358,7 @@ __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, in
                 bool may = false;
                 if (g0 < count) {
                     const int64_t p = pos0 + g0;
-                    int s = slot0 + g0;
-                    while (s >= LP_RS) s -= LP_RS;
-                    may = a.bm[p >> 6] > ceiling || a.bm[(p + 63) >> 6] > ceiling || lp_flags_any(W, s, 64);
+                    may = fmax(a.bm[p >> 6], a.bm[(p + 63) >> 6]) * (1.0 + 1e-9) > ceiling;
                 }
                 mask = __ballot(may);
                 mask_base = nb00;
@@ -1748,42 +1768,93 @@ __global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t
         const int64_t b = phi <= a.T ? (int64_t)LP_FR * phi : a.S0 + (int64_t)LP_FR * (phi - a.T - 1);
         y_lo = y_lo > b ? y_lo : b;
     }
-    const double d0 = a.dctl[0], off = a.dctl[1], gT = a.G[a.T], ceiling_inf = HUGE_VAL;
+    const double d0 = a.dctl[0], off = a.dctl[1], gT = a.G[a.T], ceiling = a.ceiling;
+    // four consecutive positions per thread (a 64-position block is 16 lanes): 32-B
+    // loads of u, 16-B stores of y
     const int lane = threadIdx.x & 63;
     const int64_t b_lo = u_lo >> 6, b_hi = (u_hi + 63) >> 6;
     uint32_t *y = reinterpret_cast<uint32_t *>(a.y);
-    const float2 *u = reinterpret_cast<const float2 *>(a.u);
-    for (int64_t b = b_lo + (((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6); b < b_hi;
-         b += ((int64_t)gridDim.x * 256) >> 6) {
-        const int64_t pos = 64 * b + lane;
-        const bool in = pos >= u_lo && pos < u_hi && pos < a.n;
-        double mx = in ? 0.0 : ceiling_inf;
-        if (in) {
-            const float2 x = u[pos];
-            const int64_t q = pos - LP_RS > 0 ? pos - LP_RS : 0;
-            const int t = (int)(q / LP_FR), i = (int)(q - (int64_t)t * LP_FR);
-            const int tc = t < a.T - 1 ? t : a.T - 1;
-            double r = a.ramp[i];
-            if (!(t < a.T - 1 || a.nb_last == LP_FR)) r = (double)i / (double)a.nb_last;
-            const double g0 = a.G[tc], g1 = a.G[tc + 1];
-            const double gi = g0 + (r * (g1 - g0));
-            const double g = pos < LP_RS ? d0 : gi;
-            const double v0 = ((double)x.x * g) * off, v1 = ((double)x.y * g) * off;
-            mx = fmax(fabs(v0), fabs(v1));
-            if (pos >= y_lo && pos < y_hi) {
+    const float4 *u4 = reinterpret_cast<const float4 *>(a.u);
+    const bool small = a.n < ((int64_t)1 << 31);          // wave-uniform: 32-bit quotients
+    for (int64_t b = b_lo + (((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4); b < b_hi;
+         b += ((int64_t)gridDim.x * 256) >> 4) {
+        const int64_t p0 = 64 * b + 4 * (lane & 15);
+        const bool whole = p0 >= u_lo && p0 + 4 <= u_hi && p0 + 4 <= a.n;
+        double mx = 0.0;
+        if (whole) {
+            const float4 xa = u4[p0 >> 1], xb = u4[(p0 >> 1) + 1];     // positions p0 .. p0 + 3
+            const float xs[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+            const int64_t q = p0 - LP_RS > 0 ? p0 - LP_RS : 0;
+            int t, i;
+            if (small) {
+                t = (int)((uint32_t)q / (uint32_t)LP_FR);
+                i = (int)((uint32_t)q - (uint32_t)t * (uint32_t)LP_FR);
+            } else {
+                t = (int)(q / LP_FR);
+                i = (int)(q - (int64_t)t * LP_FR);
+            }
+            uint32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int64_t pos = p0 + k;
+                if (k > 0 && pos - LP_RS > 0 && ++i == LP_FR) {            // (positions <= LP_RS: q 0)
+                    i = 0;
+                    t++;
+                }
+                const int tc = t < a.T - 1 ? t : a.T - 1;
+                double r = a.ramp[i];
+                if (!(t < a.T - 1 || a.nb_last == LP_FR)) r = (double)i / (double)a.nb_last;
+                const double g0 = a.G[tc], g1 = a.G[tc + 1];
+                const double gi = g0 + (r * (g1 - g0));
+                const double g = pos < LP_RS ? d0 : gi;
+                const double v0 = ((double)xs[2 * k] * g) * off, v1 = ((double)xs[2 * k + 1] * g) * off;
+                mx = fmax(mx, fmax(fabs(v0), fabs(v1)));
                 double o0 = v0, o1 = v1;
                 if (pos >= a.S0) {                     // FINAL emits it: u G_T offset
+                    o0 = ((double)xs[2 * k] * gT) * off;
+                    o1 = ((double)xs[2 * k + 1] * gT) * off;
+                }
+                if (fabs(o0) > ceiling) o0 = ceiling * (o0 < 0 ? -1 : 1);
+                if (fabs(o1) > ceiling) o1 = ceiling * (o1 < 0 ? -1 : 1);
+                o[k] = pack2(ln_s16(o0), ln_s16(o1));
+            }
+            if (p0 >= y_lo && p0 + 4 <= y_hi) {
+                *reinterpret_cast<uint4 *>(y + p0) = make_uint4(o[0], o[1], o[2], o[3]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (p0 + k >= y_lo && p0 + k < y_hi) y[p0 + k] = o[k];
+            }
+        } else {
+            // a block edge of the window or the track: any position outside holds no fill
+            // (+inf: the scan never skips such a block); inside ones one at a time
+            mx = HUGE_VAL;
+            const float2 *u = reinterpret_cast<const float2 *>(a.u);
+            for (int k = 0; k < 4; k++) {
+                const int64_t pos = p0 + k;
+                if (!(pos >= u_lo && pos < u_hi && pos < a.n)) continue;
+                const float2 x = u[pos];
+                const int64_t q = pos - LP_RS > 0 ? pos - LP_RS : 0;
+                const int t = (int)(q / LP_FR), i = (int)(q - (int64_t)t * LP_FR);
+                const int tc = t < a.T - 1 ? t : a.T - 1;
+                double r = a.ramp[i];
+                if (!(t < a.T - 1 || a.nb_last == LP_FR)) r = (double)i / (double)a.nb_last;
+                const double g0 = a.G[tc], g1 = a.G[tc + 1];
+                const double gi = g0 + (r * (g1 - g0));
+                const double g = pos < LP_RS ? d0 : gi;
+                double o0 = ((double)x.x * g) * off, o1 = ((double)x.y * g) * off;
+                if (pos >= a.S0) {
                     o0 = ((double)x.x * gT) * off;
                     o1 = ((double)x.y * gT) * off;
                 }
-                if (fabs(o0) > a.ceiling) o0 = a.ceiling * (o0 < 0 ? -1 : 1);
-                if (fabs(o1) > a.ceiling) o1 = a.ceiling * (o1 < 0 ? -1 : 1);
-                y[pos] = pack2(ln_s16(o0), ln_s16(o1));
+                if (fabs(o0) > ceiling) o0 = ceiling * (o0 < 0 ? -1 : 1);
+                if (fabs(o1) > ceiling) o1 = ceiling * (o1 < 0 ? -1 : 1);
+                if (pos >= y_lo && pos < y_hi) y[pos] = pack2(ln_s16(o0), ln_s16(o1));
             }
         }
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) mx = fmax(mx, __shfl_xor(mx, o));
-        if (lane == 0) a.bm[b] = mx;
+        for (int o = 1; o < 16; o <<= 1) mx = fmax(mx, __shfl_xor(mx, o));
+        if ((lane & 15) == 0) a.bm[b] = mx;
     }
 }
 
@@ -1940,8 +2011,9 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
 static void lp_fill(const LpArgs &lp, int64_t y_lo, int64_t y_hi, int64_t u_lo, int64_t u_hi, hipStream_t st) {
     const int64_t blocks = ((u_hi + 63) >> 6) - (u_lo >> 6);
     if (blocks <= 0) return;
-    // grid-stride over at most 4096 workgroups (a gated track's launch returns at once)
-    const int64_t g = (blocks + 3) / 4;
+    // grid-stride over at most 4096 workgroups (a gated track's launch returns at once);
+    // a workgroup covers 16 blocks
+    const int64_t g = (blocks + 15) / 16;
     hipLaunchKernelGGL(k_lp_fill, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, lp, y_lo, y_hi, u_lo,
                        u_hi);
 }
@@ -1955,6 +2027,10 @@ static void ln_upsample(const uint32_t *x, int64_t n_in, const SwrDev &r, int64_
         const int64_t nb = (n + AMX_BLOCK - 1) / AMX_BLOCK;
         return dim3((unsigned)(nb < 8192 ? nb : 8192));
     };
+    if (r.taps != LN_TAPS) {
+        hipLaunchKernelGGL(k_ln_upsample_wide, grid(j1 - j0), dim3(AMX_BLOCK), 0, st, x, n_in, r, j0, j1, u, gate);
+        return;
+    }
     if (!r.lin && r.src == r.dst) {
         const int64_t nf = (j1 + r.pc - 1) / r.pc - j0 / r.pc;
         switch (r.pc) {

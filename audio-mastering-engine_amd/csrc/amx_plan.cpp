@@ -165,18 +165,38 @@ int swr_geometry(int in_rate, int out_rate, int *L, int *M) {
     if (in_rate <= 0 || out_rate <= 0) return -1;
     int64_t a = in_rate, b = out_rate;
     while (b) { int64_t t = a % b; a = b; b = t; }
-    const int64_t l = out_rate / a, m = in_rate / a;
-    if ((double)out_rate * 0.97 / in_rate < 1.0 && !(l == 1 && m == 1)) return -1;
-    *L = (int)l;
-    *M = (int)m;
+    *L = (int)(out_rate / a);
+    *M = (int)(in_rate / a);
+    return 0;
+}
+
+// resample_init: factor = min(out_rate * cutoff / in_rate, 1) (cutoff 0.97); filter_length
+// = max(ceil(filter_size / factor), 1) rounded up to even; rows of filter_alloc =
+// FFALIGN(filter_length, 8) floats.  An input above 192 kHz / 0.97 (352.8 / 384 / 705.6 /
+// 768 kHz) is DOWNsampled with the longer, narrower filter.  Equal rates: no resampler
+// (ffmpeg only converts the sample format), the 32-tap identity row.
+int swr_filter(int in_rate, int out_rate, int *taps, int *alloc, double *factor) {
+    if (in_rate <= 0 || out_rate <= 0) return -1;
+    double f = out_rate * 0.97 / in_rate;
+    if (f > 1.0 || in_rate == out_rate) f = 1.0;
+    int t = (int)std::ceil(32 / f);
+    if (t < 1) t = 1;
+    if (t > 1) t = (t + 1) & ~1;
+    const int al = (t + 7) & ~7;
+    if (al > AMX_SWR_MAX_ALLOC) return -1;
+    if (taps) *taps = t;
+    if (alloc) *alloc = al;
+    if (factor) *factor = f;
     return 0;
 }
 
 // resample_init: phase_count 1 << phase_shift (1024), replaced by the exact out / gcd
-// when that is <= 1024 (exact_rational)
+// when that is <= 1024 (exact_rational).  The interpolating (1024-phase) form is restated
+// for the 32-tap filter only.
 int swr_phases(int in_rate, int out_rate) {
-    int L, M;
-    if (swr_geometry(in_rate, out_rate, &L, &M)) return -1;
+    int L, M, t;
+    if (swr_geometry(in_rate, out_rate, &L, &M) || swr_filter(in_rate, out_rate, &t, nullptr, nullptr)) return -1;
+    if (L > 1024 && t != 32) return -1;
     return L <= 1024 ? L : 1024;
 }
 
@@ -212,28 +232,36 @@ static double swr_bessel(double x) {
     return v;
 }
 
+// build_filter (Kaiser beta 9, FLTP, scale 1): pc rows of filter_alloc floats (zeros past
+// filter_length); factor 1 forms sin(x) / x from an alternating sine table, factor < 1
+// from sin(x) itself
 int swr_bank(int in_rate, int out_rate, float *bank) {
-    const int pc = swr_phases(in_rate, out_rate), taps = 32, center = 15;
-    if (pc < 0) return -1;
+    const int pc = swr_phases(in_rate, out_rate);
+    int taps = 0, alloc = 0;
+    double factor = 1.0;
+    if (pc < 0 || swr_filter(in_rate, out_rate, &taps, &alloc, &factor)) return -1;
+    const int center = (taps - 1) / 2;
     const int ph_nb = pc % 2 ? pc : pc / 2 + 1;
     std::vector<double> sin_lut(ph_nb), tab(taps);
     double norm = 0;
-    for (int ph = 0; ph < ph_nb; ph++) sin_lut[ph] = std::sin(M_PI * ph / pc) * (center & 1 ? 1 : -1);
+    std::fill(bank, bank + (size_t)pc * alloc, 0.0f);
+    if (factor == 1.0)
+        for (int ph = 0; ph < ph_nb; ph++) sin_lut[ph] = std::sin(M_PI * ph / pc) * (center & 1 ? 1 : -1);
     for (int ph = 0; ph < ph_nb; ph++) {
-        double sv = sin_lut[ph];
+        double sv = factor == 1.0 ? sin_lut[ph] : 0.0;
         for (int i = 0; i < taps; i++) {
-            const double x = M_PI * ((double)(i - center) - (double)ph / pc) * 1.0;
-            double y = x == 0 ? 1.0 : sv / x;
-            const double w = 2.0 * x / (1.0 * taps * M_PI);
+            const double x = M_PI * ((double)(i - center) - (double)ph / pc) * factor;
+            double y = x == 0 ? 1.0 : (factor == 1.0 ? sv / x : std::sin(x) / x);
+            const double w = 2.0 * x / (factor * taps * M_PI);
             y *= swr_bessel(9.0 * std::sqrt(std::max(1 - w * w, 0.0)));
             tab[i] = y;
             sv = -sv;
             if (!ph) norm += y;
         }
-        for (int i = 0; i < taps; i++) bank[ph * taps + i] = (float)(tab[i] * 1 / norm);
+        for (int i = 0; i < taps; i++) bank[ph * alloc + i] = (float)(tab[i] * 1 / norm);
         if (pc % 2) continue;
         if (pc - ph < pc)
-            for (int i = 0; i < taps; i++) bank[(pc - ph) * taps + taps - 1 - i] = bank[ph * taps + i];
+            for (int i = 0; i < taps; i++) bank[(pc - ph) * alloc + taps - 1 - i] = bank[ph * alloc + i];
     }
     return 0;
 }
@@ -253,6 +281,7 @@ struct amx_plan {
     // output; up_lin: the step is not an integer, every output interpolates between rows
     // ph and ph + 1 (bank row pc = row 0 one tap later) with weight owt[n]
     int up_pc = 1, up_lin = 0;
+    int up_taps = 32, up_alloc = 32;   // filter_length / filter_alloc (> 32: downsampling)
     int64_t up_src = 1, up_dst = 1;
     int32_t *d_obase = nullptr, *d_oph = nullptr;
     float *d_owt = nullptr;
@@ -407,11 +436,11 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     std::vector<float> bankn;
     if (fs != kfs) {
         p->resamp = 1;
-        if (amx::swr_geometry(fs, kfs, &p->upL, &p->upM) != 0) {
-            // an input above 192 kHz / 0.97: libswresample would downsample (a longer,
-            // narrower filter), which is not restated.  The plan measures at the track's
-            // own rate, which gives the limiter its peaks (the only measurement lufs=None
-            // needs); amx_loudness_decide refuses loudnorm on it.
+        if (amx::swr_geometry(fs, kfs, &p->upL, &p->upM) != 0 || amx::swr_phases(fs, kfs) < 0) {
+            // a rate whose resampler is not restated (an interpolating downsampler: L >
+            // 1024 with the longer filter): the plan measures at the track's own rate,
+            // which gives the limiter its peaks (the only measurement lufs=None needs);
+            // amx_loudness_decide refuses loudnorm on it.
             p->up_ok = 0;
             p->resamp = 0;
             p->meas_native = 1;
@@ -424,6 +453,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             int target = 480;                 // (AMX_UP_LOUT overrides, for measurements)
             if (const char *ev = std::getenv("AMX_UP_LOUT")) target = std::max(16, std::atoi(ev));
             p->up_pc = amx::swr_phases(fs, kfs);
+            amx::swr_filter(fs, kfs, &p->up_taps, &p->up_alloc, nullptr);
             amx::swr_incr(fs, kfs, &p->up_src, &p->up_dst);
             p->up_lin = (p->up_dst % p->up_src) != 0;
             int kk = std::max(1, (target + p->upL / 2) / p->upL);
@@ -433,14 +463,15 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             }
             p->upLin = p->upM * kk;
             p->upLout = p->upL * kk;
-            bank.assign((size_t)(p->up_pc + 1) * 32, 0.0f);
+            const int al = p->up_alloc;
+            bank.assign((size_t)(p->up_pc + 1) * al, 0.0f);
             amx::swr_bank(fs, kfs, bank.data());
-            // build_filter's extra row pc: row 0 one tap later (the interpolation partner
-            // of the last phase)
-            for (int i = 0; i < 32; i++) bank[(size_t)p->up_pc * 32 + i] = bank[(i + 31) % 32];
+            // resample_init's extra row pc: row 0 one tap later within the row (the
+            // interpolation partner of the last phase)
+            for (int i = 0; i < al; i++) bank[(size_t)p->up_pc * al + i] = bank[(i + al - 1) % al];
             // M == 1: the unrolled kernels (phase pattern static, phase 0 the identity)
-            bool ident0 = bank[15] == 1.0f;
-            for (int i = 0; i < 32; i++) ident0 = ident0 && (i == 15 || bank[i] == 0.0f);
+            bool ident0 = p->up_taps == 32 && bank[15] == 1.0f;
+            for (int i = 0; i < 32 && ident0; i++) ident0 = ident0 && (i == 15 || bank[i] == 0.0f);
             p->up_static = (p->upM == 1 && (p->upL == 2 || p->upL == 4) && ident0 && !p->up_lin &&
                             p->upLin % 8 == 0) ? p->upL : 0;
         }
@@ -815,7 +846,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             owt[n] = (float)(pos % uS) * inv;
         }
         if (p->up_static && pattern != 0) p->up_static = 0;
-        if (!p->up_static && !p->up_lin) {
+        if (!p->up_static && !p->up_lin && p->up_taps == 32) {
             // k_up_poly: frame f of a segment is the base of the outputs n with obase[n]
             // == f (consecutive n; every frame has one when L >= M); the form is (min,
             // max count, a block of TB frames dividing Lin)
@@ -1268,6 +1299,8 @@ amx::UpArgs up_args(const amx_plan *p, const int16_t *d_out, const int16_t *d_ed
     a.slow = p->d_slow;
     a.n_slow = p->n_slow;
     a.bank = p->d_bank;
+    a.taps = p->up_taps;
+    a.alloc = p->up_alloc;
     a.x = reinterpret_cast<const uint32_t *>(d_out);
     a.edge = reinterpret_cast<const uint32_t *>(d_edge);
     a.G = p->d_Gkw;
@@ -1546,7 +1579,7 @@ int amx_loudnorm_192k_ex(amx_plan *p, int32_t track, const amx_loudnorm_desc *d,
                          d_summary, d_ws2, a, q, n192))
         return rc;
     const SpanDev &sp = p->spans[track];
-    amx::SwrDev r{p->up_pc, p->up_lin, p->up_src, p->up_dst, p->d_bank};
+    amx::SwrDev r{p->up_pc, p->up_lin, p->up_src, p->up_dst, p->d_bank, p->up_taps, p->up_alloc};
     HIPCHK(amx::launch_loudnorm(a, q, reinterpret_cast<const uint32_t *>(d_out) + sp.out_off, sp.out_n, r,
                                 (hipStream_t)stream));
     return AMX_OK;
@@ -1580,7 +1613,7 @@ int amx_loudnorm_192k_shard(amx_plan *p, int32_t track, const amx_loudnorm_desc 
     q.rec_in = sh->kb > 0 ? sh->d_rec_in : nullptr;
     q.rec_out = sh->ke < q.K ? sh->d_rec_out : nullptr;
     const SpanDev &sp = p->spans[track];
-    amx::SwrDev r{p->up_pc, p->up_lin, p->up_src, p->up_dst, p->d_bank};
+    amx::SwrDev r{p->up_pc, p->up_lin, p->up_src, p->up_dst, p->d_bank, p->up_taps, p->up_alloc};
     // the positions segments [kb, ke) emit
     const LnLayout lo = ln_layout(n192);
     const int64_t y_lo = ln_seg_base(lo, n192, sh->kb), y_hi = sh->ke < lo.K ? ln_seg_base(lo, n192, sh->ke) : n192;
@@ -1609,8 +1642,9 @@ int amx_loudnorm_192k_shard_window(const amx_plan *p, int32_t track, int32_t kb,
     const SpanDev &sp = p->spans[track];
     int64_t x_lo = u_lo, x_hi = u_hi;
     if (p->resamp) {
-        x_lo = std::max<int64_t>(0, (int64_t)((__int128)u_lo * p->upM / p->upL) - 40);
-        x_hi = std::min<int64_t>(sp.out_n, (int64_t)(((__int128)u_hi * p->upM + p->upL - 1) / p->upL) + 40);
+        const int64_t m = p->up_alloc + 8;       // the window's reach (center + the row)
+        x_lo = std::max<int64_t>(0, (int64_t)((__int128)u_lo * p->upM / p->upL) - m);
+        x_hi = std::min<int64_t>(sp.out_n, (int64_t)(((__int128)u_hi * p->upM + p->upL - 1) / p->upL) + m);
     }
     win[0] = x_lo;
     win[1] = x_hi;
@@ -1800,6 +1834,12 @@ int amx_limiter_prepare(amx_plan *p, const amx_final_desc *fd, int32_t seg_frame
     return AMX_OK;
 }
 
+int amx_publish_ctl(const int32_t *d_ctl, int32_t *h_ctl, int32_t n, void *stream) {
+    if (n < 0 || (n > 0 && (!d_ctl || !h_ctl))) return fail(AMX_EINVAL, "null argument");
+    HIPCHK(amx::launch_publish(d_ctl, h_ctl, n, (hipStream_t)stream));
+    return AMX_OK;
+}
+
 int amx_loudness_decide(amx_plan *p, const amx_decide_desc *dd, const amx_final_desc *fd,
                         const uint64_t *d_hist, const uint64_t *d_st_hist, const double *d_peak,
                         double *d_stats, double *d_gains, int32_t *d_ctl, void *stream) {
@@ -1807,8 +1847,8 @@ int amx_loudness_decide(amx_plan *p, const amx_decide_desc *dd, const amx_final_
         (dd->lufs_on && (!d_hist || !d_st_hist)))
         return fail(AMX_EINVAL, "null argument");
     if (dd->lufs_on && p->meas_native)
-        return fail(AMX_ERANGE, "%d Hz: loudnorm measures the track resampled to 192 kHz, which "
-                    "downsamples this rate (not restated); lufs=None works", p->cd.fs);
+        return fail(AMX_ERANGE, "%d Hz: loudnorm measures the track resampled to 192 kHz with an "
+                    "interpolating downsampler (not restated); lufs=None works", p->cd.fs);
     amx::DecideArgs a{};
     a.n_tracks = p->n_tracks;
     a.lufs_on = dd->lufs_on ? 1 : 0;

@@ -277,6 +277,26 @@ def other_configs(args):
             o["parity_vs_oracle"] = dict(parity(ys, refs, "whole workload, bit for bit"),
                                          oracle_seconds=round(time.perf_counter() - t0, 2))
             del ys, refs, tracks
+        if cfg == "c4":
+            # the same batch captured with loudnorm's dynamic path held for every track
+            # (MasteringJob.capture(dynamic=True): launched only for a track whose decision
+            # says dynamic -- none here): what a product batch pays to finish loud tracks
+            # in the step
+            job = runner.job
+            job.capture(d_in, dynamic=True)
+            for _ in range(3):
+                job.replay()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            nd = 0
+            while time.perf_counter() - t0 < 1.0 or nd < 5:
+                job.replay()
+                nd += 1
+            torch.cuda.synchronize()
+            msd = (time.perf_counter() - t0) * 1e3 / nd
+            o["dynamic_capture"] = {"ms_per_step": round(msd, 4), "steps": nd,
+                                    "overhead": round(msd / ms - 1.0, 4),
+                                    "what": "capture(dynamic=True): the dynamic path held for every track"}
         out[cfg] = o
         del runner, d_in
         gc.collect()

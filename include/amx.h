@@ -247,9 +247,10 @@ AMX_API int amx_plan_set_gate(amx_plan *plan, const int32_t *d_gate);
  * phase step is not an integer, 22.05 / 11.025 kHz) -- libebur128's
  * K filter, 400 ms / 3 s blocks and sample peak at 192 kHz.
  * K-filter zero-state GEMV per segment + exact scan + sample peaks.
- * d_edge [n_tracks][2][16][2] int16: the 16 output frames before and after a span
+ * d_edge [n_tracks][2][80][2] int16: the 80 output frames before and after a span
  * that does not start / end its track (the neighbour ranks' frames, which the
- * resampler's 32-tap window reaches); NULL when every span is a whole track.
+ * resampler's window reaches: 16 for the 32-tap upsampler, up to 67 for the longer
+ * downsampling filters of inputs above 192 kHz); NULL when every span is a whole track.
  * d_kw_tail [n_tracks][2][4]: K-filter state at each span end assuming the span
  * started from rest (what the NEXT rank of a chunk-sharded track needs, see
  * amx_kw_propagate; NULL = not wanted, e.g. one GPU); d_peak [n_tracks][4]: per
@@ -403,6 +404,12 @@ typedef struct amx_decide_desc {
 AMX_API int amx_loudness_decide(amx_plan *plan, const amx_decide_desc *dd, const amx_final_desc *fd,
                                 const uint64_t *d_hist, const uint64_t *d_st_hist, const double *d_peak,
                                 double *d_stats, double *d_gains, int32_t *d_ctl, void *stream);
+/* The n decision words d_ctl (amx_loudness_decide) stored into pinned host memory h_ctl
+ * (hipHostMalloc'd, device-mapped) by a small kernel on the stream, with system-scope
+ * stores: the host polls them while the step goes on (a captured step's host read,
+ * without a copy node's completion stall).  Replaces no reference line: the reference
+ * reads ffmpeg's printed statistics (:231-237). */
+AMX_API int amx_publish_ctl(const int32_t *d_ctl, int32_t *h_ctl, int32_t n, void *stream);
 
 /* Chunk-sharded tracks: K-filter state entering this plan's (single) span from the
  * zero-start tails of the n_prev spans before it.  Setup (host, once): frames_after[q]

@@ -523,8 +523,9 @@ EXPORT void orc_ebur128(const int16_t *x, int64_t n, int fs, int channels,
  * the phase step is an integer (frac stays 0), so linear interpolation adds 0.
  * PARITY UNPINNED: no ffmpeg binary or fixture exists here; a host without FMA3
  * sums in another order (differences of float32 rounding in the measured values). */
-#define SWR_TAPS 32
+#define SWR_TAPS 32              /* filter_size; the filter of an upsampling rate */
 #define SWR_CENTER 15            /* (taps - 1) / 2 */
+#define SWR_MAX_ALLOC 256        /* the widest bank row restated (factor >= 1 / 8) */
 
 static double swr_bessel(double x) {
     double lastv = 0, t, v;
@@ -546,25 +547,46 @@ static double swr_bessel(double x) {
 static int64_t gcd64(int64_t a, int64_t b) { while (b) { int64_t t = a % b; a = b; b = t; } return a; }
 
 /* L / M = out_rate / in_rate reduced (output j sits at input position j M / L); 0 =
- * supported (upsampling), else -1.  The filter bank has orc_swr_phases() rows: L when
- * L <= 1024 (exact_rational: phase_count = L), else 1024 (libswresample's default
- * phase_shift 10; the position then falls between phases and the linear path
- * interpolates, see swr_block) */
+ * supported, else -1.  The filter bank has orc_swr_phases() rows: L when L <= 1024
+ * (exact_rational: phase_count = L), else 1024 (libswresample's default phase_shift 10;
+ * the position then falls between phases and the linear path interpolates, see
+ * swr_block).  Inputs above 192 kHz / 0.97 (the loudnorm pass-1 resampler then
+ * DOWNsamples: 352.8 / 384 / 705.6 / 768 kHz) take the longer, narrower filter of
+ * orc_swr_filter; the interpolating path is restated for the 32-tap filter only. */
 EXPORT int orc_swr_geometry(int in_rate, int out_rate, int *L, int *M) {
     if (in_rate <= 0 || out_rate <= 0) return -1;
     int64_t g = gcd64(in_rate, out_rate);
     int64_t l = out_rate / g, m = in_rate / g;
-    if ((double)out_rate * 0.97 / in_rate < 1.0 && !(l == 1 && m == 1)) return -1;   /* downsampling */
     *L = (int)l;
     *M = (int)m;
+    return 0;
+}
+
+/* resample_init: factor = min(out_rate * cutoff / in_rate, 1) (cutoff 0.97);
+ * filter_length = max(ceil(filter_size / factor), 1) rounded up to even; the bank rows
+ * are filter_alloc = FFALIGN(filter_length, 8) floats (zeros past filter_length) */
+EXPORT int orc_swr_filter(int in_rate, int out_rate, int *taps, int *alloc, double *factor) {
+    if (in_rate <= 0 || out_rate <= 0) return -1;
+    double f = out_rate * 0.97 / in_rate;
+    if (f > 1.0 || in_rate == out_rate) f = 1.0;   /* equal rates: no resampling (the identity row) */
+    int t = (int)ceil(SWR_TAPS / f);
+    if (t < 1) t = 1;
+    if (t > 1) t = (t + 1) & ~1;
+    const int al = (t + 7) & ~7;
+    if (al > SWR_MAX_ALLOC) return -1;
+    if (taps) *taps = t;
+    if (alloc) *alloc = al;
+    if (factor) *factor = f;
     return 0;
 }
 
 /* resample_init: phase_count = 1 << phase_shift (1024), replaced by the exact
  * out / gcd when that is <= 1024 */
 EXPORT int orc_swr_phases(int in_rate, int out_rate) {
-    int L, M;
+    int L, M, t, al;
     if (orc_swr_geometry(in_rate, out_rate, &L, &M)) return -1;
+    if (orc_swr_filter(in_rate, out_rate, &t, &al, NULL)) return -1;
+    if (L > 1024 && t != SWR_TAPS) return -1;    /* interpolating downsampler: not restated */
     return L <= 1024 ? L : 1024;
 }
 
@@ -584,34 +606,41 @@ EXPORT int orc_swr_incr(int in_rate, int out_rate, int64_t *src_incr, int64_t *d
     return 0;
 }
 
-/* build_filter (factor 1: upsampling, Kaiser, FLTP, scale 1): bank[ph][i], ph < pc */
+/* build_filter (Kaiser, FLTP, scale 1): bank[ph][i] (rows of filter_alloc floats,
+ * zeros past filter_length), ph < pc.  factor 1 (upsampling) forms sin(x) / x from a
+ * sine table alternating in sign; factor < 1 (downsampling) from sin(x) itself */
 EXPORT int orc_swr_bank(int in_rate, int out_rate, float *bank) {
     const int pc = orc_swr_phases(in_rate, out_rate);
-    if (pc < 0) return -1;
-    const int tap_count = SWR_TAPS, center = SWR_CENTER;
+    int tap_count, alloc;
+    double factor;
+    if (pc < 0 || orc_swr_filter(in_rate, out_rate, &tap_count, &alloc, &factor)) return -1;
+    const int center = (tap_count - 1) / 2;
     const int ph_nb = pc % 2 ? pc : pc / 2 + 1;
-    const double factor = 1.0, beta = 9.0;
-    double tab[SWR_TAPS];
+    const double beta = 9.0;
+    double tab[SWR_MAX_ALLOC];
     double *sin_lut = (double *)malloc(sizeof(double) * ph_nb);
     double norm = 0;
-    for (int ph = 0; ph < ph_nb; ph++) sin_lut[ph] = sin(M_PI * ph / pc) * (center & 1 ? 1 : -1);
+    memset(bank, 0, sizeof(float) * (size_t)pc * alloc);
+    if (factor == 1.0)
+        for (int ph = 0; ph < ph_nb; ph++) sin_lut[ph] = sin(M_PI * ph / pc) * (center & 1 ? 1 : -1);
     for (int ph = 0; ph < ph_nb; ph++) {
-        double s = sin_lut[ph];
+        double s = factor == 1.0 ? sin_lut[ph] : 0.0;
         for (int i = 0; i < tap_count; i++) {
             double x = M_PI * ((double)(i - center) - (double)ph / pc) * factor;
             double y;
             if (x == 0) y = 1.0;
-            else y = s / x;                                    /* factor == 1.0 */
+            else if (factor == 1.0) y = s / x;
+            else y = sin(x) / x;
             double w = 2.0 * x / (factor * tap_count * M_PI);
             y *= swr_bessel(beta * sqrt(fmax(1 - w * w, 0)));
             tab[i] = y;
             s = -s;
             if (!ph) norm += y;
         }
-        for (int i = 0; i < tap_count; i++) bank[ph * tap_count + i] = (float)(tab[i] * 1 / norm);
+        for (int i = 0; i < tap_count; i++) bank[ph * alloc + i] = (float)(tab[i] * 1 / norm);
         if (pc % 2) continue;
         for (int i = 0; i < tap_count; i++)
-            if (pc - ph < pc) bank[(pc - ph) * tap_count + tap_count - 1 - i] = bank[ph * tap_count + i];
+            if (pc - ph < pc) bank[(pc - ph) * alloc + tap_count - 1 - i] = bank[ph * alloc + i];
     }
     free(sin_lut);
     return 0;
@@ -633,14 +662,13 @@ static inline int64_t swr_reflect(int64_t k, int64_t n) {
     }
 }
 
-/* the float kernel's order (see above) */
-static inline float swr_dot(const float *w, const float *h) {
+/* the float kernel's order (see above): the ymm loop runs over filter_alloc taps (the
+ * row's zero padding multiplies the samples that follow the window) */
+static inline float swr_dot(const float *w, const float *h, int alloc) {
     float a[8];
     for (int k = 0; k < 8; k++) {
         float acc = fmaf(w[k], h[k], 0.0f);
-        acc = fmaf(w[k + 8], h[k + 8], acc);
-        acc = fmaf(w[k + 16], h[k + 16], acc);
-        acc = fmaf(w[k + 24], h[k + 24], acc);
+        for (int q = 8; q < alloc; q += 8) acc = fmaf(w[k + q], h[k + q], acc);
         a[k] = acc;
     }
     const float b0 = a[0] + a[4], b1 = a[1] + a[5], b2 = a[2] + a[6], b3 = a[3] + a[7];
@@ -676,6 +704,7 @@ static inline float swr_dot_lin(const float *w, const float *h, const float *h2,
  * later, build_filter's extra row for the interpolation at the last phase) */
 typedef struct {
     int L, M, pc, lin;
+    int taps, alloc, center;      /* filter_length, filter_alloc, (taps - 1) / 2 */
     int64_t src_incr, dst_incr;
     float inv;                    /* 1.0f / (float)src_incr */
     float *bank;
@@ -684,15 +713,18 @@ typedef struct {
 static int swr_open(Swr *r, int in_rate, int out_rate) {
     if (orc_swr_geometry(in_rate, out_rate, &r->L, &r->M)) return -1;
     r->pc = orc_swr_phases(in_rate, out_rate);
+    if (r->pc < 0 || orc_swr_filter(in_rate, out_rate, &r->taps, &r->alloc, NULL)) return -1;
+    r->center = (r->taps - 1) / 2;
     orc_swr_incr(in_rate, out_rate, &r->src_incr, &r->dst_incr);
     /* swri_resample: the linear kernel whenever frac or dst_incr_mod is non-zero, i.e.
      * for every output when the phase step is not an integer; else the common one */
     r->lin = (r->dst_incr % r->src_incr) != 0;
     r->inv = 1.0f / (float)r->src_incr;
-    r->bank = (float *)malloc(sizeof(float) * (size_t)(r->pc + 1) * SWR_TAPS);
+    r->bank = (float *)malloc(sizeof(float) * (size_t)(r->pc + 1) * r->alloc);
     orc_swr_bank(in_rate, out_rate, r->bank);
-    float *ex = r->bank + (size_t)r->pc * SWR_TAPS, *r0 = r->bank;
-    for (int i = 0; i < SWR_TAPS; i++) ex[i] = r0[(i + SWR_TAPS - 1) % SWR_TAPS];
+    /* resample_init's extra row pc: row 0 one tap later within the row (filter_alloc) */
+    float *ex = r->bank + (size_t)r->pc * r->alloc, *r0 = r->bank;
+    for (int i = 0; i < r->alloc; i++) ex[i] = r0[(i + r->alloc - 1) % r->alloc];
     return 0;
 }
 
@@ -701,17 +733,18 @@ static int swr_open(Swr *r, int in_rate, int out_rate) {
  * int64): base = floor(p) / pc, phase floor(p) % pc, frac = the remainder */
 static void swr_block(const int16_t *x, int64_t n, int channels, const Swr *r,
                       int64_t j0, int64_t j1, double *out) {
-    float w[SWR_TAPS];
+    float w[SWR_MAX_ALLOC];
     for (int64_t j = j0; j < j1; j++) {
         const int64_t pos = j * r->dst_incr, idx = pos / r->src_incr, frac = pos % r->src_incr;
         const int64_t base = idx / r->pc;
         const int ph = (int)(idx % r->pc);
         const float wf = (float)frac * r->inv;
         for (int c = 0; c < channels; c++) {
-            for (int i = 0; i < SWR_TAPS; i++)
-                w[i] = (float)x[swr_reflect(base - SWR_CENTER + i, n) * channels + c] * (1.0f / 32768.0f);
-            const float *h = r->bank + (size_t)ph * SWR_TAPS;
-            out[(j - j0) * channels + c] = (double)(r->lin ? swr_dot_lin(w, h, h + SWR_TAPS, wf) : swr_dot(w, h));
+            for (int i = 0; i < r->alloc; i++)
+                w[i] = (float)x[swr_reflect(base - r->center + i, n) * channels + c] * (1.0f / 32768.0f);
+            const float *h = r->bank + (size_t)ph * r->alloc;
+            out[(j - j0) * channels + c] =
+                (double)(r->lin ? swr_dot_lin(w, h, h + SWR_TAPS, wf) : swr_dot(w, h, r->alloc));
         }
     }
 }

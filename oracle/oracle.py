@@ -309,8 +309,18 @@ def swr_incr(fs, out_rate=192000):
     return a.value, b.value
 
 
+def swr_filter(fs, out_rate=192000):
+    """resample_init's filter: (filter_length taps, filter_alloc row stride, factor)"""
+    t, al, f = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
+    if lib().orc_swr_filter(ctypes.c_int(fs), ctypes.c_int(out_rate), ctypes.byref(t), ctypes.byref(al),
+                            ctypes.byref(f)):
+        raise ValueError("unsupported rate %d" % fs)
+    return t.value, al.value, f.value
+
+
 def swr_bank(fs, out_rate=192000):
-    bank = np.zeros((swr_phases(fs, out_rate), 32), np.float32)
+    """[phases][filter_alloc] float32 bank (zeros past filter_length)"""
+    bank = np.zeros((swr_phases(fs, out_rate), swr_filter(fs, out_rate)[1]), np.float32)
     lib().orc_swr_bank(ctypes.c_int(fs), ctypes.c_int(out_rate), _p(bank, _f32p))
     return bank
 

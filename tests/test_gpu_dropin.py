@@ -395,3 +395,44 @@ def test_master_audio_flac(gpu, oracle_mod, bps, channels, seconds, variable, se
     assert y.shape == ref.shape
     dd = np.abs(y.astype(np.int32) - ref.astype(np.int32))
     assert dd.max() == 0, "max |diff| %d LSB" % dd.max()
+
+
+@pytest.mark.parametrize("fs", [384000, 352800])
+@pytest.mark.parametrize("kind", ["mix", "dynamic"])
+def test_master_audio_above_192k(gpu, oracle_mod, fs, kind):
+    """inputs above 192 kHz with lufs=-14 (the GUI's default, mastering_gui.py:48): ffmpeg's
+    loudnorm (:229, :240) resamples them DOWN to 192 kHz with libswresample's longer,
+    narrower filter (66 taps at 384 kHz, 62 at 352.8 kHz; restated in the oracle, parity
+    unpinned against ffmpeg itself).  Linear mode keeps the input rate; dynamic mode
+    writes 192 kHz.  The statistics strings equal the oracle's and the output is within
+    3 LSB of it (round 4 refused these rates with ERANGE)."""
+    import audio_mastering_engine as ame
+    from amx import synth, wavio
+    from amx.chunking import chunk_bounds, packet_frames
+    n = int(fs * 9.0)
+    x = synth.mix_like(n, fs, 2, seed=fs % 1000)
+    if kind == "dynamic":
+        x = x * np.float32(0.12)
+        rng = np.random.default_rng(fs % 997)
+        for k in rng.integers(0, n - 2000, 18):
+            x[k:k + 400] += rng.uniform(-0.9, 0.9, (400, 2)).astype(np.float32)
+        x = np.clip(x, -1.0, 1.0).astype(np.float32)
+    settings = dict(bass_boost=1.5, presence_boost=1.0, lufs=-14.0)
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "in.wav"), os.path.join(d, "out.wav")
+        wavio.write_wav_f32(src, x, fs)
+        st = []
+        ame.master_audio(dict(settings, input_file=src, output_file=dst), st.append)
+        y, info = wavio.read_wav_native(dst)
+        bounds = chunk_bounds(n, fs, packet_frames(8))
+    assert "Error" not in " ".join(st)
+    ref, rinfo = oracle_mod.pipeline(oracle_mod.quantize(x), fs, settings, bounds)
+    assert rinfo["mode"] == ("dynamic" if kind == "dynamic" else "linear"), rinfo.get("stats")
+    assert info.sample_rate == rinfo["sample_rate"] == (192000 if kind == "dynamic" else fs)
+    assert y.shape == ref.shape
+    dd = np.abs(y.astype(np.int32) - ref.astype(np.int32))
+    print("%d Hz %s: max |diff| %d LSB, exact %.7f" % (fs, kind, dd.max(), (dd == 0).mean()))
+    assert dd.max() <= 3 and (dd == 0).mean() >= 0.999
+    from amx.engine import master_array
+    _, rep = master_array(np.ascontiguousarray(oracle_mod.quantize(x)), fs, settings, quantum=packet_frames(8))
+    assert rep["stats"][0] == rinfo["stats"], (rep["stats"][0], rinfo["stats"])

@@ -261,12 +261,12 @@ def test_graph_step_with_dynamic(gpu, oracle_mod):
 
 
 def test_graph_step_dynamic_gate_linear_batch(gpu):
-    """capture(dynamic=True) on a batch whose tracks all stay linear: the 192 kHz side
-    plans' measurement passes and alimiter are gated on each track's decision
-    (amx_plan_set_gate), so a replay costs the dynamic=False graph plus the gated nodes'
-    launches -- a fixed ~25 graph nodes per track, not work that grows with the track
-    (ADVICE r03: ungated, every step paid two 192 kHz passes and the alimiter per track);
-    the outputs are the same bit for bit"""
+    """capture(dynamic=True) on a batch whose tracks all stay linear: the dynamic path
+    sits in a graph of its own that replay() launches only when a track's decision word
+    (copied to pinned memory before the limiter kernel) says dynamic, so a linear step
+    costs the dynamic=False graph and one host read that overlaps the limiter: within
+    10 % of it (round 4: +130 %, ~25 gated nodes per track); the outputs are the same
+    bit for bit"""
     import time
     import torch
     from amx import synth
@@ -292,7 +292,7 @@ def test_graph_step_dynamic_gate_linear_batch(gpu):
         outs[dyn] = job.y[:job.info.out_frames].cpu().numpy()
     print("linear batch step: dynamic=False %.3f ms, dynamic=True %.3f ms" % (times[False] * 1e3, times[True] * 1e3))
     assert np.array_equal(outs[False], outs[True])
-    assert times[True] - times[False] <= 0.25e-3 * len(n), times
+    assert times[True] <= 1.10 * times[False], times
 
 
 @pytest.mark.timeout(900)

@@ -316,3 +316,88 @@ def test_measurement_192k_vs_native(oracle_mod):
     assert float(a["input_tp"]) >= float(b["input_tp"])
     _, _, pk192, _ = oracle_mod.ebur128_192k(x16, fs)
     assert pk192.max() >= np.abs(x16.astype(np.int32)).max() / 32768.0
+
+
+def _py_swr_bank_down(fs, out_rate=192000):
+    """libswresample build_filter for factor < 1 (a DOWNsampling resampler: inputs above
+    192 kHz / 0.97), restated again in Python: filter_length = ceil(32 / factor) made
+    even, rows of filter_alloc = FFALIGN(length, 8) floats, y = sin(x) / x times the
+    Kaiser window (beta 9) of w = 2x / (factor length pi), normalised by row 0's sum"""
+    g = math.gcd(fs, out_rate)
+    L = out_rate // g
+    factor = min(out_rate * 0.97 / fs, 1.0)
+    taps = max(int(math.ceil(32 / factor)), 1)
+    taps += taps & 1
+    alloc = (taps + 7) // 8 * 8
+    center = (taps - 1) // 2
+
+    def bessel(x):
+        x = x * x / 4
+        t, v, lastv, i = x, 1 + x, 0.0, 1
+        while v != lastv:
+            t *= x * (1.0 / ((i + 1) * (i + 1)))
+            v += t
+            lastv = v
+            t *= x * (1.0 / ((i + 2) * (i + 2)))
+            v += t
+            i += 2
+        return v
+    rows = np.zeros((L, alloc), np.float64)
+    ph_nb = L if L % 2 else L // 2 + 1
+    norm = 0.0
+    for ph in range(ph_nb):
+        for i in range(taps):
+            x = math.pi * ((i - center) - ph / L) * factor
+            y = 1.0 if x == 0 else math.sin(x) / x
+            w = 2.0 * x / (factor * taps * math.pi)
+            y *= bessel(9.0 * math.sqrt(max(1 - w * w, 0.0)))
+            rows[ph, i] = y
+            if ph == 0:
+                norm += y
+    out = np.zeros((L, alloc), np.float32)
+    for ph in range(ph_nb):
+        out[ph, :taps] = (rows[ph, :taps] * 1 / norm).astype(np.float32)
+        if L % 2 == 0 and 0 < ph:
+            out[L - ph, :taps] = out[ph, :taps][::-1]
+    return out, taps, alloc
+
+
+@pytest.mark.parametrize("fs,taps", [(384000, 66), (352800, 62), (768000, 132), (705600, 122)])
+def test_swr_downsampling_filter(oracle_mod, fs, taps):
+    """loudnorm pass 1 on inputs above 192 kHz (:229, :240): libswresample downsamples to
+    192 kHz with a longer, narrower Kaiser filter (resample_init's factor < 1).  Two
+    restatements of build_filter agree; the FIR passes a 1 kHz tone at unit gain, rejects a
+    tone past the new Nyquist (> 60 dB), and the output count is ceil(n L / M).
+    PARITY UNPINNED (no ffmpeg or fixture): checked against the published algorithm only."""
+    from amx import synth
+    b = oracle_mod.swr_bank(fs)
+    want, t2, alloc = _py_swr_bank_down(fs)
+    t, al, factor = oracle_mod.swr_filter(fs)
+    assert (t, al) == (t2, alloc) == (taps, (taps + 7) // 8 * 8) and factor < 1.0
+    np.testing.assert_array_equal(b, want)
+    assert np.all(b[:, taps:] == 0.0)
+    L, M = oracle_mod.swr_geometry(fs)
+    assert L < M
+    n = 20000
+    tt = np.arange(n) / fs
+    for f0, lo, hi in ((1000.0, 0.999, 1.001), (min(150000.0, 0.45 * fs), 0.0, 1e-3)):
+        x = np.stack([0.5 * np.sin(2 * np.pi * f0 * tt)] * 2, axis=1).astype(np.float32)
+        u = oracle_mod.upsample(oracle_mod.quantize(x), fs)
+        assert u.shape[0] == -(-n * L // M)
+        j = np.arange(u.shape[0] // 4, 3 * u.shape[0] // 4)
+        tj = j * (M / L) / fs                      # output j's time (input frames j M / L)
+        A = np.stack([np.sin(2 * np.pi * f0 * tj), np.cos(2 * np.pi * f0 * tj)], axis=1)
+        coef = np.linalg.lstsq(A, u[j, 0], rcond=None)[0]
+        amp = np.hypot(*coef) / 0.5
+        assert lo <= amp <= hi, (f0, amp)
+    # the FIR itself: output j = row (j M) % L over inputs floor(j M / L) - center ...
+    x16 = oracle_mod.quantize(synth.music_like(3001, fs, 2, seed=6, peak_dbfs=-1.0))
+    u = oracle_mod.upsample(x16, fs)
+    xf = x16.astype(np.float64) / 32768.0
+    nn = x16.shape[0]
+    idx = lambda k: abs(k) if k < 0 else (2 * nn - 1 - k if k >= nn else k)
+    c = (taps - 1) // 2
+    for j in list(range(0, 40)) + list(range(u.shape[0] - 40, u.shape[0])):
+        base, ph = (j * M) // L, (j * M) % L
+        w = np.array([xf[idx(base - c + i)] for i in range(taps)])
+        np.testing.assert_allclose(u[j], b[ph, :taps].astype(np.float64) @ w, rtol=0, atol=4e-7)
