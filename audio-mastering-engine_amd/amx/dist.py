@@ -276,20 +276,48 @@ class ShardedTrack:
             self._setup_exchange()
 
     def _setup_exchange(self):
-        """the K-filter carry transitions and the exchange buffers of the N > 1 step"""
+        """the K-filter carry transitions and the exchange buffers of the N > 1 step.
+        The exchange moves whole buffers with one gather kernel each: the K-filter tail
+        and the peaks ARE the all-gather's input (the job's kw_tail / peak are views of
+        it), the edge frames are one index_select out of the span and one into a buffer
+        the job's resampler edges and limiter halo are views of"""
         rank, world = self.rank, self.world
+        job = self.job
         frames_after = [sum(self.span_frames[q + 1:rank]) for q in range(rank)]
-        self.job.plan.kw_carry_setup(frames_after)
-        dev = self.job.device
+        job.plan.kw_carry_setup(frames_after)
+        dev = job.device
         self.tails_all = torch.zeros((world, 2, 4), dtype=torch.float64, device=dev)
         from . import capi
         self.ne = capi.UP_EDGE                                  # frames after the span start
-        self.nl = max(capi.UP_EDGE, self.job.halo_frames)       # frames before the span end
-        fw = (4 * (self.ne + self.nl) + 7) // 8                 # doubles holding them
-        self._ebuf = torch.zeros(fw, dtype=torch.float64, device=dev)
-        self._eall = torch.zeros(world * fw, dtype=torch.float64, device=dev)
+        self.nl = max(capi.UP_EDGE, job.halo_frames)            # frames before the span end
+        W = self.ne + self.nl                                   # one int32 word per frame
+        self._ebuf = torch.zeros(W, dtype=torch.int32, device=dev)
+        # the gathered words, and one zero word after them (the source of a missing neighbour)
+        self._eall = torch.zeros(world * W + 1, dtype=torch.int32, device=dev)
+        E, h = capi.UP_EDGE, max(1, job.halo_frames)
+        self._edst = torch.zeros(2 * E + h, dtype=torch.int32, device=dev)
+        job.edge = self._edst[:2 * E].view(torch.int16).reshape(1, 2, E, 2)
+        job.halo = self._edst[2 * E:].view(torch.int16).reshape(1, h, 2)
+        zero = world * W
+        src = [zero] * (2 * E + h)
+        if rank > 0:
+            for i in range(E):
+                src[i] = (rank - 1) * W + self.ne + self.nl - E + i
+            for i in range(job.halo_frames):
+                src[2 * E + i] = (rank - 1) * W + self.ne + self.nl - job.halo_frames + i
+        if rank < world - 1:
+            for i in range(E):
+                src[E + i] = (rank + 1) * W + i
+        self._eidx = torch.tensor(src, dtype=torch.int64, device=dev)
+        n = self.span_frames[rank]
+        self._pidx = None
+        if n >= max(self.ne, self.nl):
+            self._pidx = torch.tensor(list(range(self.ne)) + list(range(n - self.nl, n)), dtype=torch.int64,
+                                      device=dev)
         self._xbuf = torch.zeros(12, dtype=torch.float64, device=dev)
         self._xall = torch.zeros(world * 12, dtype=torch.float64, device=dev)
+        job.kw_tail = self._xbuf[0:8].view(1, 2, 4)
+        job.peak = self._xbuf[8:12].view(1, 4)
 
     # -------------------------------------------------------------- exchanges
     def _all_gather(self, out, inp):
@@ -301,40 +329,32 @@ class ShardedTrack:
     def _pack_edges(self):
         """This span's first ne and last nl output frames (zero-padded when shorter)."""
         job, n = self.job, self.span_frames[self.rank]
-        b = self._ebuf.view(torch.uint8)
+        out32 = job.out.view(torch.int32).reshape(-1)
+        if self._pidx is not None:
+            torch.index_select(out32, 0, self._pidx, out=self._ebuf)
+            return
+        b = self._ebuf
         b.zero_()
         m = min(self.ne, n)
         if m > 0:
-            b[:4 * m].copy_(job.out[:m].contiguous().view(torch.uint8).reshape(-1))
+            b[:m].copy_(out32[:m])
         m = min(self.nl, n)
         if m > 0:
-            o = 4 * (self.ne + self.nl - m)
-            b[o:o + 4 * m].copy_(job.out[n - m:n].contiguous().view(torch.uint8).reshape(-1))
+            o = self.ne + self.nl - m
+            b[o:o + m].copy_(out32[n - m:n])
 
     def _unpack_edges(self):
         """Previous rank's last frames -> the resampler's low edge and the limiter halo;
-        next rank's first frames -> the resampler's high edge."""
-        job, r, world = self.job, self.rank, self.world
-        ea = self._eall.view(world, -1).view(torch.uint8)
-        ne, nl, E = self.ne, self.nl, job.edge.shape[2]
-        if r > 0:
-            last = ea[r - 1][4 * ne:4 * (ne + nl)].view(torch.int16).reshape(nl, 2)
-            job.edge[0, 0].copy_(last[nl - E:])
-            h = job.halo_frames
-            if h > 0:
-                job.halo[0, :h].copy_(last[nl - h:])
-        if r < world - 1:
-            job.edge[0, 1].copy_(ea[r + 1][:4 * E].view(torch.int16).reshape(E, 2))
+        next rank's first frames -> the resampler's high edge (one gather)."""
+        torch.index_select(self._eall, 0, self._eidx, out=self._edst)
 
     def exchange_edges(self):
         self._pack_edges()
-        self._all_gather(self._eall, self._ebuf)
+        self._all_gather(self._eall[:-1], self._ebuf)
         self._unpack_edges()
 
     def _pack_x(self):
-        xb, job = self._xbuf, self.job
-        xb[0:8].copy_(job.kw_tail.reshape(-1)[:8])
-        xb[8:12].copy_(job.peak.reshape(-1)[:4])
+        """(nothing to move: the job's kw_tail and peak live in the all-gather's input)"""
 
     def _unpack_x(self):
         from . import capi
@@ -343,7 +363,7 @@ class ShardedTrack:
         self.tails_all.copy_(xa[:, 0:8].reshape(world, 2, 4))
         capi.check(capi.load().amx_kw_carry(job.plan.h, capi.ptr(self.tails_all), capi.ptr(job.kw_carry),
                                             job._s(None)), "amx_kw_carry")
-        job.peak.reshape(-1)[:4].copy_(xa[:, 8:12].amax(0))
+        torch.amax(xa[:, 8:12], 0, out=job.peak.reshape(4))
 
     def exchange_carry_peaks(self):
         self._pack_x()
@@ -767,7 +787,11 @@ class ShardedTrack:
 
     # the pipelined replay's per-slot state: a MasteringJob, its exchange buffers, the
     # pinned decision word and its event, its graph
-    _SLOT_KEYS = ("job", "tails_all", "_ebuf", "_eall", "_xbuf", "_xall", "_ctl_host", "_ctl_ev", "_g")
+    # (every tensor a slot's graph reads or writes stays referenced here: one replaced by
+    # the other slot's _setup_exchange and freed would be re-used while the graph holds
+    # its address -- r05f's index_select fault on the freed gather indices)
+    _SLOT_KEYS = ("job", "tails_all", "_ebuf", "_eall", "_edst", "_eidx", "_pidx", "_xbuf", "_xall", "_ctl_host",
+                  "_ctl_ev", "_g")
 
     def _use(self, k):
         for key, v in self._slots[k].items():
@@ -798,7 +822,7 @@ class ShardedTrack:
             def whole(job=job):
                 job.run_chunks(d_in)
                 self._pack_edges()
-                self._all_gather(self._eall, self._ebuf)
+                self._all_gather(self._eall[:-1], self._ebuf)
                 self._unpack_edges()
                 job.loudness_pass1(tail=True)
                 self._pack_x()
@@ -887,7 +911,7 @@ class ShardedTrack:
         if len(self._g) == 4:
             g1, g2, g3, g4 = self._g
             g1.replay()
-            self._all_gather(self._eall, self._ebuf)
+            self._all_gather(self._eall[:-1], self._ebuf)
             g2.replay()
             self._all_gather(self._xall, self._xbuf)
             g3.replay()

@@ -104,7 +104,7 @@ class MasteringJob:
         self.plan.limiter_prepare(self.fd, limiter_seg_frames, limiter_warm_frames)
         self._i_out = torch.zeros((T,), dtype=torch.float64, device=dev)   # pass 1's output I (dynamic)
         self._dyn_sides = None     # per track, the 192 kHz sets run() enqueues (prepare_dynamic)
-        self._graph_dyn = None
+        self._dyn_eager = False
         self.report = {}
 
     # ------------------------------------------------------------ device steps
@@ -387,9 +387,11 @@ class MasteringJob:
         capture): replay() then re-issues the whole pipeline -- every kernel, same
         buffers -- with one launch, so the host's per-kernel launch cost is off the
         critical path.  run() has no host round trip, so the captured graph is the
-        complete step.  dynamic: the graph also holds loudnorm's dynamic path
-        (prepare_dynamic), so a track that takes it is finished inside the step too."""
-        self._graph_dyn = None
+        complete step.  dynamic: the step also holds loudnorm's dynamic path
+        (prepare_dynamic), so a track that takes it is finished inside the step too --
+        enqueued by replay() after the graph, for the tracks whose published decision
+        word says dynamic (AMX_DYN_INLINE=1: gated inside the graph instead)."""
+        self._dyn_eager = False
         if dynamic:
             self.prepare_dynamic()
         dyn = bool(self._dyn_sides)
@@ -407,33 +409,28 @@ class MasteringJob:
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self.run(d_in, dyn=not dyn, ctl_to=self._ctl_pin[:self.n_tracks] if dyn else None)
         self._graph = g
-        if dyn:
-            # the dynamic path of every track, gated per track on the device, in a graph of
-            # its own that replay() launches only when some track's word says dynamic: a
-            # linear step pays none of its ~35 nodes per track
-            gd = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gd, capture_error_mode="thread_local"):
-                for t, side in enumerate(self._dyn_sides):
-                    self._dyn_enqueue(t, side, None, gate=True)
-            self._graph_dyn = gd
+        self._dyn_eager = dyn
         return g
 
     def replay(self):
         """One step from the captured graph.  With the dynamic path (capture(dynamic=True))
-        the host reads the decision words, which the graph copies to pinned memory
-        before its limiter kernel: they land while that kernel still runs, so the next
-        step's launch is not delayed; the dynamic graph follows only when needed."""
-        if self._graph_dyn is None:
-            self._graph.replay()
+        the graph publishes the decision words to pinned memory before its limiter kernel
+        (device stores: they land while that kernel still runs); the host then enqueues
+        the gated dynamic path, eagerly, only for a track whose word says dynamic, so a
+        linear step pays none of its ~35 launches per track.  (A graph of its own for
+        that path replayed 10-20x slower than the same launches made eagerly, with
+        walker re-runs: profiles/r05_dyn_graph.txt.)"""
+        self._graph.replay()
+        if not getattr(self, "_dyn_eager", False):
             return self.y[:self.info.out_frames]
         h = self._ctl_pin
-        h.fill_(-1)                 # (the previous step's copy has landed: it was read)
-        self._graph.replay()
         hv = h.numpy()[:self.n_tracks]
         while (hv == -1).any():
             pass
-        if any((int(v) >> 4) & 15 == 3 for v in hv):       # k_decide mode 3 = dynamic
-            self._graph_dyn.replay()
+        dyn = [t for t in range(self.n_tracks) if (int(hv[t]) >> 4) & 15 == 3]   # k_decide mode 3
+        h.fill_(-1)                 # (read: the next step's words replace it)
+        for t in dyn:
+            self._dyn_enqueue(t, self._dyn_sides[t], None, gate=True)
         return self.y[:self.info.out_frames]
 
     def finish_dynamic(self, report=None):

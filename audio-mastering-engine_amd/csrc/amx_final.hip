@@ -662,6 +662,18 @@ size_t limiter_lds_bytes(int buffer_size) {
     return ((size_t)3 * buffer_size + 4 * AMX_LIM_BATCH) * sizeof(double);
 }
 
+// a workgroup may declare all of a CU's 160 KiB of LDS on gfx950: the general columns'
+// ring (3 B doubles) then fits a 5 ms attack up to ~670 kHz (B <= 6741; 384 kHz: 3 840)
+hipError_t limiter_allow_lds(size_t bytes) {
+    if (bytes > AMX_LIM_LDS_MAX) return hipErrorInvalidValue;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_final<true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)AMX_LIM_LDS_MAX);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_final<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)AMX_LIM_LDS_MAX);
+    return e;
+}
+
 hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, const int16_t *x,
                         const int16_t *halo, int halo_frames, const double *gains,
                         const int32_t *ctl, int fast, int fs, double level_in, double level,
@@ -688,7 +700,7 @@ hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, co
     size_t lds = 0;
     if (general) {
         lds = limiter_lds_bytes(buffer_size);
-        if (lds > 64 * 1024) return hipErrorInvalidValue;   // B <= 2645: attack <= 13.7 ms at 96 kHz
+        if (lds > AMX_LIM_LDS_MAX) return hipErrorInvalidValue;   // B <= 6741: 5 ms up to ~670 kHz
         if (!ls.seg_state || !ls.cnt || ls.buffer_size != buffer_size || ls.max_segs < 1)
             return hipErrorInvalidValue;
         a.seg_frames = ls.seg_frames; a.warm_frames = ls.warm_frames; a.max_segs = ls.max_segs;

@@ -345,6 +345,8 @@ struct LimScratch {
     const int32_t *gate = nullptr; // amx_plan_set_gate: k_final returns unless dynamic
 };
 size_t limiter_lds_bytes(int buffer_size);
+#define AMX_LIM_LDS_MAX (160 * 1024)   // gfx950: one workgroup may hold a CU's whole LDS
+hipError_t limiter_allow_lds(size_t bytes);   // k_final's dynamic LDS limit raised to it
 hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, const int16_t *x,
                         const int16_t *halo, int halo_frames, const double *gains,
                         const int32_t *ctl, int fast, int fs, double level_in, double level,

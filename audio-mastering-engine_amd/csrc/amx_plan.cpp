@@ -1790,7 +1790,10 @@ int amx_limiter_prepare(amx_plan *p, const amx_final_desc *fd, int32_t seg_frame
     if (seg_frames < 64 || seg_frames < bs / 2)
         return fail(AMX_EINVAL, "limiter segments of %d frames: need >= 64 and >= the ring (%d frames)",
                     seg_frames, bs / 2);
-    if (amx::limiter_lds_bytes(bs) > 64 * 1024) return fail(AMX_EINVAL, "Attack is too large.");
+    if (amx::limiter_lds_bytes(bs) > AMX_LIM_LDS_MAX)
+        return fail(AMX_ERANGE, "Attack is too large: the alimiter's %d-sample look-ahead ring does not fit "
+                    "a CU's LDS (inputs above ~670 kHz)", bs);
+    if (amx::limiter_lds_bytes(bs) > 64 * 1024) HIPCHK(amx::limiter_allow_lds(amx::limiter_lds_bytes(bs)));
     const int64_t max_segs64 = p->max_span > 0 ? (p->max_span + seg_frames - 1) / seg_frames : 1;
     if (max_segs64 > INT32_MAX / 2) return fail(AMX_EINVAL, "limiter: too many segments");
     const int max_segs = (int)max_segs64;
