@@ -286,7 +286,6 @@ class ShardedTrack:
         frames_after = [sum(self.span_frames[q + 1:rank]) for q in range(rank)]
         job.plan.kw_carry_setup(frames_after)
         dev = job.device
-        self.tails_all = torch.zeros((world, 2, 4), dtype=torch.float64, device=dev)
         from . import capi
         self.ne = capi.UP_EDGE                                  # frames after the span start
         self.nl = max(capi.UP_EDGE, job.halo_frames)            # frames before the span end
@@ -358,12 +357,12 @@ class ShardedTrack:
 
     def _unpack_x(self):
         from . import capi
-        job, world = self.job, self.world
-        xa = self._xall.view(world, -1)
-        self.tails_all.copy_(xa[:, 0:8].reshape(world, 2, 4))
-        capi.check(capi.load().amx_kw_carry(job.plan.h, capi.ptr(self.tails_all), capi.ptr(job.kw_carry),
-                                            job._s(None)), "amx_kw_carry")
-        torch.amax(xa[:, 8:12], 0, out=job.peak.reshape(4))
+        job = self.job
+        # the K-filter carry from the previous ranks' tails and the track's peaks (max over
+        # the ranks) straight from the gathered rows: one kernel
+        capi.check(capi.load().amx_kw_carry_rows(job.plan.h, capi.ptr(self._xall), self.world, 12,
+                                                 capi.ptr(job.kw_carry), capi.ptr(job.peak), job._s(None)),
+                   "amx_kw_carry_rows")
 
     def exchange_carry_peaks(self):
         self._pack_x()
@@ -790,7 +789,7 @@ class ShardedTrack:
     # (every tensor a slot's graph reads or writes stays referenced here: one replaced by
     # the other slot's _setup_exchange and freed would be re-used while the graph holds
     # its address -- r05f's index_select fault on the freed gather indices)
-    _SLOT_KEYS = ("job", "tails_all", "_ebuf", "_eall", "_edst", "_eidx", "_pidx", "_xbuf", "_xall", "_ctl_host",
+    _SLOT_KEYS = ("job", "_ebuf", "_eall", "_edst", "_eidx", "_pidx", "_xbuf", "_xall", "_ctl_host",
                   "_ctl_ev", "_g")
 
     def _use(self, k):
@@ -906,7 +905,9 @@ class ShardedTrack:
             prev, self._pending, self._slot = self._pending, k, k ^ 1
             if prev is not None:
                 self._last_out = self._resolve(prev)
-            return self.job.y[:self.job.info.out_frames]
+            out = self.job.y[:self.job.info.out_frames]
+            self._use(0)            # (step(), dynamic() and callers see slot 0's buffers)
+            return out
         job = self.job
         if len(self._g) == 4:
             g1, g2, g3, g4 = self._g
@@ -941,6 +942,8 @@ class ShardedTrack:
     def step(self, d_in):
         """One pass of the whole path over this rank's chunks (input resident)."""
         from . import capi
+        if self._slots is not None and self._pending is not None:
+            self.flush()            # a pipelined step still pending: resolve it first
         job = self.job
         if not self.xchg:
             if self.dyn:

@@ -365,6 +365,8 @@ hipError_t launch_decide(const DecideArgs &a, hipStream_t st);
 hipError_t launch_publish(const int32_t *ctl, int32_t *host, int n, hipStream_t st);
 hipError_t launch_kw_carry(const double *tails, const double *P, int n_prev, double *carry,
                            hipStream_t st);
+hipError_t launch_kw_carry_rows(const double *rows, int world, int ld, const double *P, int n_prev,
+                                double *carry, double *peak, hipStream_t st);
 // per-track sample peak: partial maxima per block into part[track][block][2], the last
 // block of a track (counter cnt[track], zero between launches) writes peak[track][2]
 int peak_reduce_blocks(int64_t max_nkseg);

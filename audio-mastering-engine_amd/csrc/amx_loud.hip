@@ -762,5 +762,34 @@ hipError_t launch_kw_carry(const double *tails, const double *P, int n_prev, dou
     return hipGetLastError();
 }
 
-}  // namespace amx
+// the gathered exchange rows (row q: tail [2][4] at 0, peaks [4] at 8, stride ld):
+// threads 0-7 the carry from the rows q < n_prev, threads 8-11 the peak max over all rows
+__global__ void k_kw_carry_rows(const double *__restrict__ rows, int world, int ld,
+                                const double *__restrict__ P, int n_prev, double *__restrict__ carry,
+                                double *__restrict__ peak) {
+    const int t = threadIdx.x;
+    if (t < 2 * AMX_KW_DIM) {
+        const int c = t / AMX_KW_DIM, i = t % AMX_KW_DIM;
+        double acc = 0.0;
+        for (int q = 0; q < n_prev; q++) {
+            const double *Pq = P + (int64_t)q * AMX_KW_DIM * AMX_KW_DIM;
+            const double *tq = rows + (int64_t)q * ld + c * AMX_KW_DIM;
+#pragma unroll
+            for (int k = 0; k < AMX_KW_DIM; k++) acc = fma(Pq[i * AMX_KW_DIM + k], tq[k], acc);
+        }
+        carry[t] = acc;
+    } else if (t < 2 * AMX_KW_DIM + 4) {
+        const int c = t - 2 * AMX_KW_DIM;
+        double m = rows[2 * AMX_KW_DIM + c];
+        for (int q = 1; q < world; q++) m = fmax(m, rows[(int64_t)q * ld + 2 * AMX_KW_DIM + c]);
+        peak[c] = m;
+    }
+}
 
+hipError_t launch_kw_carry_rows(const double *rows, int world, int ld, const double *P, int n_prev,
+                                double *carry, double *peak, hipStream_t st) {
+    hipLaunchKernelGGL(k_kw_carry_rows, dim3(1), dim3(64), 0, st, rows, world, ld, P, n_prev, carry, peak);
+    return hipGetLastError();
+}
+
+}  // namespace amx

@@ -1902,6 +1902,18 @@ int amx_kw_carry(amx_plan *p, const double *d_tails, double *d_carry, void *stre
     return AMX_OK;
 }
 
+int amx_kw_carry_rows(amx_plan *p, const double *d_rows, int32_t world, int32_t ld, double *d_carry,
+                      double *d_peak, void *stream) {
+    if (!p || !d_rows || !d_carry || !d_peak) return fail(AMX_EINVAL, "null argument");
+    if (!p->d_carryP) return fail(AMX_EINVAL, "amx_kw_carry_rows: call amx_kw_carry_setup first");
+    if (world < 1 || ld < 12 || p->n_prev >= world)
+        return fail(AMX_EINVAL, "amx_kw_carry_rows: %d rows of %d doubles for %d previous spans", world, ld,
+                    p->n_prev);
+    HIPCHK(amx::launch_kw_carry_rows(d_rows, world, ld, p->d_carryP, p->n_prev, d_carry, d_peak,
+                                     (hipStream_t)stream));
+    return AMX_OK;
+}
+
 int amx_finalize(amx_plan *p, const amx_final_desc *fd, const int16_t *d_x,
                  const double *d_gains, const int32_t *d_ctl, int32_t fast,
                  const int16_t *d_halo, int16_t *d_y, double *d_lim_state, void *d_ws,

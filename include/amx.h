@@ -418,6 +418,13 @@ AMX_API int amx_publish_ctl(const int32_t *d_ctl, int32_t *h_ctl, int32_t n, voi
  * stream: d_carry [2][4] = sum_q A^{frames_after[q]} d_tails[q] (d_tails [n_prev][2][4]). */
 AMX_API int amx_kw_carry_setup(amx_plan *plan, int32_t n_prev, const int64_t *frames_after);
 AMX_API int amx_kw_carry(amx_plan *plan, const double *d_tails, double *d_carry, void *stream);
+/* The same from the N > 1 step's gathered exchange rows in place (one kernel instead of
+ * a copy, the carry and a max reduction): d_rows [world][ld] doubles, each rank's row =
+ * its K-filter tail [2][4] at 0 and its sample peaks [4] at 8 (ld >= 12); d_carry as
+ * above from the rows q < n_prev; d_peak [4] = the max over the world rows.  Replaces the
+ * whole-file measurement's peaks of :229 (ebur128 over the concatenated track). */
+AMX_API int amx_kw_carry_rows(amx_plan *plan, const double *d_rows, int32_t world, int32_t ld,
+                              double *d_carry, double *d_peak, void *stream);
 
 /* Finalize: loudnorm linear gain (d_gains[t] <= 0 -> no normalisation, :216) then
  * alimiter (:223) -> d_y int16 [out_frames, 2] (same frame indexing as d_x).
