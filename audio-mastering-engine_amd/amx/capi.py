@@ -75,7 +75,8 @@ class PlanInfo(ctypes.Structure):
 
 class LoudnormDesc(ctypes.Structure):
     _fields_ = [(k, ctypes.c_double) for k in ("target_i", "target_lra", "target_tp", "measured_i",
-                                                 "measured_lra", "measured_tp", "measured_thresh", "offset")]
+                                                 "measured_lra", "measured_tp", "measured_thresh", "offset")] + \
+        [("reuse_stream", ctypes.c_int32)]
 
 
 class LnShard(ctypes.Structure):

@@ -721,6 +721,7 @@ class ShardedTrack:
         S.measure(True)
         wd["i_out"].copy_(S.job.stats[0, 0:1])                    # pass 1's output loudness
         d2 = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
+        d2.reuse_stream = 1          # the same windows: pass 1's stream over u stands
         if not self._filter_windowed(wd, d2, job.stats[0], wd["i_out"]):
             return None
         S.measure(False)                                     # the limiter's input bound

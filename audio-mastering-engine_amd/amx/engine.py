@@ -264,6 +264,7 @@ class MasteringJob:
         tracks need it).  filt(desc, measured, offset_i): the filter run in place of
         amx_loudnorm_192k_ex (ShardedTrack's segment-sharded run)."""
         n192, job2, ws2, summ = side
+        reuse = filt is None
         if filt is None:
             def filt(desc, measured, offset_i):
                 self.loudnorm_192k(t, desc, job2, ws2, summ, stream, measured=measured, offset_i=offset_i,
@@ -283,6 +284,8 @@ class MasteringJob:
                 self._i_out[t:t + 1].copy_(job2.stats[0, 0:1])       # pass 1's output loudness
         self.timed("ln_measure1", measure1, stream)
         d2 = capi.LoudnormDesc(target, LOUDNORM_LRA, LOUDNORM_TP, 0.0, 0.0, 99.0, -70.0, 0.0)
+        # pass 2 filters the same input on the same scratch: pass 1's 192 kHz stream stands
+        d2.reuse_stream = 1 if reuse else 0
         self.timed("ln_filter2", lambda: filt(d2, self.stats[t], self._i_out[t:t + 1]), stream)
 
         def limit():

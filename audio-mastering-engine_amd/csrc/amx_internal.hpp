@@ -319,11 +319,12 @@ struct SwrDev {
     const float *bank;            // [pc + 1][alloc]
     int taps, alloc;              // filter_length, filter_alloc (32, 32 but downsampling)
 };
+// resample false: ln.u already holds the stream (amx_loudnorm_desc.reuse_stream)
 hipError_t launch_loudnorm(const LnArgs &a, const LpArgs &p, const uint32_t *x, int64_t n_in,
-                           const SwrDev &r, hipStream_t st);
+                           const SwrDev &r, bool resample, hipStream_t st);
 hipError_t launch_loudnorm_shard(const LnArgs &a, const LpArgs &p, const uint32_t *x, int64_t n_in,
                                  const SwrDev &r, int64_t u_lo, int64_t u_hi, int64_t y_lo, int64_t y_hi, int part,
-                                 hipStream_t st);
+                                 bool resample, hipStream_t st);
 #define AMX_LN_GATED(g) ((g) && (((g)[0] >> 4) & 15) != 3)   // k_decide mode 3 = dynamic
 hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent_t fork, hipEvent_t join);
 int swr_geometry(int in_rate, int out_rate, int *L, int *M);   // host (amx_plan.cpp)

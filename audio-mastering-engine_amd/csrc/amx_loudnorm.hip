@@ -2045,9 +2045,9 @@ static void ln_upsample(const uint32_t *x, int64_t n_in, const SwrDev &r, int64_
 }
 
 hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x, int64_t n_in,
-                           const SwrDev &r, hipStream_t st) {
+                           const SwrDev &r, bool resample, hipStream_t st) {
     if (ln.n192 <= 0) return hipSuccess;
-    ln_upsample(x, n_in, r, 0, ln.n192, ln.u, lp.gate, st);
+    if (resample) ln_upsample(x, n_in, r, 0, ln.n192, ln.u, lp.gate, st);
     hipLaunchKernelGGL(k_lp_stats, dim3(1 + (lp.T + LP_STAT_F - 1) / LP_STAT_F), dim3(LP_STAT_NT), 0, st, lp);
     hipLaunchKernelGGL(k_ln_dyn, dim3(1), dim3(LN_NT), 0, st, ln, 0);
     hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
@@ -2071,10 +2071,10 @@ hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x
 // and the segments [kb, ke); 2 -- the walk over their boundaries from lp.rec_in
 hipError_t launch_loudnorm_shard(const LnArgs &ln, const LpArgs &lp, const uint32_t *x, int64_t n_in,
                                  const SwrDev &r, int64_t u_lo, int64_t u_hi, int64_t y_lo, int64_t y_hi, int part,
-                                 hipStream_t st) {
+                                 bool resample, hipStream_t st) {
     if (ln.n192 <= 0) return hipSuccess;
     if (part == 0) {
-        ln_upsample(x, n_in, r, u_lo, u_hi, ln.u, lp.gate, st);
+        if (resample) ln_upsample(x, n_in, r, u_lo, u_hi, ln.u, lp.gate, st);
         hipLaunchKernelGGL(k_lp_stats, dim3(1 + (lp.T + LP_STAT_F - 1) / LP_STAT_F), dim3(LP_STAT_NT), 0, st, lp);
     } else if (part == 1) {
         hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);

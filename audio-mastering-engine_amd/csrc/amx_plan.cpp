@@ -1581,7 +1581,7 @@ int amx_loudnorm_192k_ex(amx_plan *p, int32_t track, const amx_loudnorm_desc *d,
     const SpanDev &sp = p->spans[track];
     amx::SwrDev r{p->up_pc, p->up_lin, p->up_src, p->up_dst, p->d_bank, p->up_taps, p->up_alloc};
     HIPCHK(amx::launch_loudnorm(a, q, reinterpret_cast<const uint32_t *>(d_out) + sp.out_off, sp.out_n, r,
-                                (hipStream_t)stream));
+                                d->reuse_stream == 0, (hipStream_t)stream));
     return AMX_OK;
 }
 
@@ -1622,7 +1622,8 @@ int amx_loudnorm_192k_shard(amx_plan *p, int32_t track, const amx_loudnorm_desc 
                             ? reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(d_out) -
                                                                  (uintptr_t)win[0] * sizeof(uint32_t))
                             : reinterpret_cast<const uint32_t *>(d_out) + sp.out_off;
-    HIPCHK(amx::launch_loudnorm_shard(a, q, x, sp.out_n, r, u_lo, u_hi, y_lo, y_hi, sh->part, (hipStream_t)stream));
+    HIPCHK(amx::launch_loudnorm_shard(a, q, x, sp.out_n, r, u_lo, u_hi, y_lo, y_hi, sh->part, d->reuse_stream == 0,
+                                      (hipStream_t)stream));
     return AMX_OK;
 }
 
