@@ -277,10 +277,11 @@ class ShardedTrack:
 
     def _setup_exchange(self):
         """the K-filter carry transitions and the exchange buffers of the N > 1 step.
-        The exchange moves whole buffers with one gather kernel each: the K-filter tail
-        and the peaks ARE the all-gather's input (the job's kw_tail / peak are views of
-        it), the edge frames are one index_select out of the span and one into a buffer
-        the job's resampler edges and limiter halo are views of"""
+        The exchange moves whole buffers with one gather kernel each, and the all-gathers
+        run in place (each rank's input is its own row of the output): the K-filter tail
+        and the peaks ARE that row (the job's kw_tail / peak are views of it), the edge
+        frames are one index_select out of the span into it and one out of the gathered
+        rows into a buffer the job's resampler edges and limiter halo are views of"""
         rank, world = self.rank, self.world
         job = self.job
         frames_after = [sum(self.span_frames[q + 1:rank]) for q in range(rank)]
@@ -290,9 +291,11 @@ class ShardedTrack:
         self.ne = capi.UP_EDGE                                  # frames after the span start
         self.nl = max(capi.UP_EDGE, job.halo_frames)            # frames before the span end
         W = self.ne + self.nl                                   # one int32 word per frame
-        self._ebuf = torch.zeros(W, dtype=torch.int32, device=dev)
-        # the gathered words, and one zero word after them (the source of a missing neighbour)
+        # the gathered words, and one zero word after them (the source of a missing
+        # neighbour); this rank's words are its own row: the all-gathers run in place
+        # (no local copy, none at all at world 1)
         self._eall = torch.zeros(world * W + 1, dtype=torch.int32, device=dev)
+        self._ebuf = self._eall[rank * W:(rank + 1) * W]
         E, h = capi.UP_EDGE, max(1, job.halo_frames)
         self._edst = torch.zeros(2 * E + h, dtype=torch.int32, device=dev)
         job.edge = self._edst[:2 * E].view(torch.int16).reshape(1, 2, E, 2)
@@ -313,8 +316,8 @@ class ShardedTrack:
         if n >= max(self.ne, self.nl):
             self._pidx = torch.tensor(list(range(self.ne)) + list(range(n - self.nl, n)), dtype=torch.int64,
                                       device=dev)
-        self._xbuf = torch.zeros(12, dtype=torch.float64, device=dev)
         self._xall = torch.zeros(world * 12, dtype=torch.float64, device=dev)
+        self._xbuf = self._xall[rank * 12:(rank + 1) * 12]
         job.kw_tail = self._xbuf[0:8].view(1, 2, 4)
         job.peak = self._xbuf[8:12].view(1, 4)
 

@@ -306,6 +306,7 @@ struct amx_plan {
     std::vector<int> eseg0, neseg;
     int fuse_kw = 0;        // loudness pass-1 GEMV + peak run inside k_front2
     int kw_rest_states = 0;
+    int kw_eb_ready = 0;     // the K scan's block sums (o_ebk) are those of the current e
     int kw_aligned = 0;     // K-filter hop pieces split only at 16-frame tile boundaries // the last amx_loudness_pass1 left the K-filter start states from rest
     int n_tracks = 0, n_chunks = 0, n_seg = 0, n_kseg = 0, n_blk = 0, n_kblk = 0;
     int64_t max_nkseg = 0;
@@ -1413,6 +1414,7 @@ int amx_loudness_pass1_part(amx_plan *p, int32_t part, const int16_t *d_out, con
         // the pass over the samples: per K segment the zero-state end state (and, at
         // 192 kHz, the peaks and energy terms; amx_loud192.hip)
         p->kw_rest_states = 0;
+        p->kw_eb_ready = 0;
         if (p->n_kseg == 0) return AMX_OK;
         if (p->resamp)
             HIPCHK(amx::launch_up1(up_args(p, d_out, d_edge, d_ws), st, p->up_aux, p->up_fork, p->up_join));
@@ -1433,6 +1435,7 @@ int amx_loudness_pass1_part(amx_plan *p, int32_t part, const int16_t *d_out, con
                                    p->resamp, st));
     HIPCHK(amx::launch_scan(p->scan_kw(), e, s, nullptr, wsp<double>(d_ws, p->o_ebk), st));
     p->kw_rest_states = 1;   // s = the start states from rest: pass 2 without a carry reuses them
+    p->kw_eb_ready = 1;      // and the block sums: pass 2 with a carry runs the down sweep only
     if (d_kw_tail)
         HIPCHK(amx::launch_kw_tail(p->d_spans, p->n_tracks, s, e, p->d_tailpow, d_kw_tail, st));
     return AMX_OK;
@@ -1742,8 +1745,12 @@ int amx_loudness_pass2(amx_plan *p, const int16_t *d_out, const int16_t *d_edge,
     double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
     double *parts = wsp<double>(d_ws, p->o_parts);
     int64_t *phop = wsp<int64_t>(d_ws, p->o_phop);
-    if (d_kw_carry || !p->kw_rest_states)
-        HIPCHK(amx::launch_scan(p->scan_kw(), e, s, d_kw_carry, wsp<double>(d_ws, p->o_ebk), st));
+    if (d_kw_carry || !p->kw_rest_states) {
+        // the block sums do not depend on the carry: after pass 1 only the down sweep runs
+        HIPCHK(amx::launch_scan(p->scan_kw(), e, s, d_kw_carry, wsp<double>(d_ws, p->o_ebk), st, !p->kw_eb_ready));
+        p->kw_eb_ready = 1;
+        p->kw_rest_states = d_kw_carry ? 0 : 1;
+    }
     if (p->resamp)
         HIPCHK(amx::launch_up2(up_args(p, d_out, d_edge, d_ws), st));
     else

@@ -146,28 +146,31 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_scan_blk(const ScanBlk *__restric
 // ================================================================ launchers
 template <int D, int GP>
 static hipError_t scan_t(const ScanPlan &p, const double *e, double *s, const double *carry,
-                         double *eb, hipStream_t st) {
+                         double *eb, bool up, hipStream_t st) {
     constexpr int GPB = (64 / GP) * (AMX_BLOCK / 64);
     const dim3 gb((unsigned)((2 * (int64_t)p.n_blk + GPB - 1) / GPB));
-    hipLaunchKernelGGL((k_scan_blk<D, GP, false>), gb, dim3(AMX_BLOCK), 0, st, p.blks, p.n_blk, e,
-                       s, p.M, p.Mbk, p.K, carry, eb);
+    if (up)
+        hipLaunchKernelGGL((k_scan_blk<D, GP, false>), gb, dim3(AMX_BLOCK), 0, st, p.blks, p.n_blk, e,
+                           s, p.M, p.Mbk, p.K, carry, eb);
     hipLaunchKernelGGL((k_scan_blk<D, GP, true>), gb, dim3(AMX_BLOCK), 0, st, p.blks, p.n_blk, e,
                        s, p.M, p.Mbk, p.K, carry, eb);
     return hipGetLastError();
 }
 
+// up false: eb already holds the up sweep of these e (the block sums do not depend on
+// the carry), only the down sweep runs
 hipError_t launch_scan(const ScanPlan &p, const double *e, double *s, const double *carry,
-                       double *eb, hipStream_t st) {
+                       double *eb, hipStream_t st, bool up) {
     if (p.n_blk <= 0 || p.D <= 0) return hipSuccess;
     switch (p.D) {
-    case 2: return scan_t<2, 2>(p, e, s, carry, eb, st);
-    case 4: return scan_t<4, 4>(p, e, s, carry, eb, st);
-    case 8: return scan_t<8, 8>(p, e, s, carry, eb, st);
-    case 10: return scan_t<10, 10>(p, e, s, carry, eb, st);
-    case 12: return scan_t<12, 12>(p, e, s, carry, eb, st);
-    case 16: return scan_t<16, 16>(p, e, s, carry, eb, st);
-    case 18: return scan_t<18, 18>(p, e, s, carry, eb, st);
-    case 20: return scan_t<20, 20>(p, e, s, carry, eb, st);
+    case 2: return scan_t<2, 2>(p, e, s, carry, eb, up, st);
+    case 4: return scan_t<4, 4>(p, e, s, carry, eb, up, st);
+    case 8: return scan_t<8, 8>(p, e, s, carry, eb, up, st);
+    case 10: return scan_t<10, 10>(p, e, s, carry, eb, up, st);
+    case 12: return scan_t<12, 12>(p, e, s, carry, eb, up, st);
+    case 16: return scan_t<16, 16>(p, e, s, carry, eb, up, st);
+    case 18: return scan_t<18, 18>(p, e, s, carry, eb, up, st);
+    case 20: return scan_t<20, 20>(p, e, s, carry, eb, up, st);
     }
     return hipErrorInvalidValue;
 }
