@@ -1760,15 +1760,7 @@ __device__ __forceinline__ void lp_wave_init(const LpArgs &a, LpWave &W, double2
 // outside [u_lo, u_hi) or past the track.  The fill is lp_val's expression term for
 // term: u (gain ramp) offset for INNER positions, u d0 offset below the ring's first
 // fill, u G_T offset for the positions FINAL emits.  One wave per 64-position block.
-// XL > 0 (an M == 1 rate, 192 kHz / XL with 4 % XL == 0, libswresample's 32-tap filter):
-// a whole block's stream values are recomputed from the chain output x -- k_ln_up_static's
-// window and dot, operation for operation, so the same floats -- instead of read back
-// from u (8 B per position against 4 / XL B of x: the kernel's traffic 0.7 -> 0.3 GB per
-// 5-min 48 kHz track); edge blocks read u.
-template <int XL>
-__global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t y_hi, int64_t u_lo, int64_t u_hi,
-                                                 const uint32_t *__restrict__ xin, int64_t n_in,
-                                                 const float *__restrict__ bank) {
+__global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t y_hi, int64_t u_lo, int64_t u_hi) {
     if ((a.ctl[0] != 0 && a.ctl[0] != 4) || a.T < 1) return;
     if (a.ctl[0] == 4) {
         // a quiet start: k_ln_dyn wrote the frames before the hand-over segment
@@ -1790,38 +1782,8 @@ __global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t
         const bool whole = p0 >= u_lo && p0 + 4 <= u_hi && p0 + 4 <= a.n;
         double mx = 0.0;
         if (whole) {
-            float xs[8];                                               // positions p0 .. p0 + 3
-            if constexpr (XL > 0) {
-                // frames p0 / XL .. + 4 / XL - 1: their 32-frame windows, loaded once
-                constexpr int NF = 4 / XL, NW = LN_TAPS + NF - 1;
-                float w0[NW], w1[NW];
-                const int64_t g = p0 / XL - LN_C;
-                if (g >= 0 && g + NW <= n_in) {
-#pragma unroll
-                    for (int i = 0; i < NW; i++) {
-                        const uint32_t v = xin[g + i];
-                        w0[i] = (float)lo16(v) * (1.0f / 32768.0f);
-                        w1[i] = (float)hi16(v) * (1.0f / 32768.0f);
-                    }
-                } else {
-#pragma unroll
-                    for (int i = 0; i < NW; i++) {
-                        const uint32_t v = xin[ln_reflect(g + i, n_in)];
-                        w0[i] = (float)lo16(v) * (1.0f / 32768.0f);
-                        w1[i] = (float)hi16(v) * (1.0f / 32768.0f);
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const float *h = bank + (k % XL) * LN_TAPS;
-                    xs[2 * k] = ln_dot2(w0 + k / XL, h);
-                    xs[2 * k + 1] = ln_dot2(w1 + k / XL, h);
-                }
-            } else {
-                const float4 xa = u4[p0 >> 1], xb = u4[(p0 >> 1) + 1];
-                xs[0] = xa.x; xs[1] = xa.y; xs[2] = xa.z; xs[3] = xa.w;
-                xs[4] = xb.x; xs[5] = xb.y; xs[6] = xb.z; xs[7] = xb.w;
-            }
+            const float4 xa = u4[p0 >> 1], xb = u4[(p0 >> 1) + 1];     // positions p0 .. p0 + 3
+            const float xs[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
             const int64_t q = p0 - LP_RS > 0 ? p0 - LP_RS : 0;
             int t, i;
             if (small) {
@@ -2046,22 +2008,14 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
     }
 }
 
-static void lp_fill(const LpArgs &lp, int64_t y_lo, int64_t y_hi, int64_t u_lo, int64_t u_hi, const uint32_t *x,
-                    int64_t n_in, const SwrDev &r, hipStream_t st) {
+static void lp_fill(const LpArgs &lp, int64_t y_lo, int64_t y_hi, int64_t u_lo, int64_t u_hi, hipStream_t st) {
     const int64_t blocks = ((u_hi + 63) >> 6) - (u_lo >> 6);
     if (blocks <= 0) return;
     // grid-stride over at most 4096 workgroups (a gated track's launch returns at once);
     // a workgroup covers 16 blocks
     const int64_t g = (blocks + 15) / 16;
-    const dim3 grid((unsigned)(g < 4096 ? g : 4096));
-    const bool stat = r.taps == LN_TAPS && !r.lin && r.src == r.dst && std::getenv("AMX_LP_FILLX") == nullptr;
-    switch (stat ? r.pc : 0) {
-    case 1: hipLaunchKernelGGL(k_lp_fill<1>, grid, dim3(256), 0, st, lp, y_lo, y_hi, u_lo, u_hi, x, n_in, r.bank); return;
-    case 2: hipLaunchKernelGGL(k_lp_fill<2>, grid, dim3(256), 0, st, lp, y_lo, y_hi, u_lo, u_hi, x, n_in, r.bank); return;
-    case 4: hipLaunchKernelGGL(k_lp_fill<4>, grid, dim3(256), 0, st, lp, y_lo, y_hi, u_lo, u_hi, x, n_in, r.bank); return;
-    default:
-        hipLaunchKernelGGL(k_lp_fill<0>, grid, dim3(256), 0, st, lp, y_lo, y_hi, u_lo, u_hi, x, n_in, r.bank);
-    }
+    hipLaunchKernelGGL(k_lp_fill, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, lp, y_lo, y_hi, u_lo,
+                       u_hi);
 }
 
 static void ln_upsample(const uint32_t *x, int64_t n_in, const SwrDev &r, int64_t j0, int64_t j1, float *u,
@@ -2099,7 +2053,7 @@ hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x
     hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
     const int gb = max((lp.T + 1 + 255) / 256, (LP_FR + 255) / 256);
     hipLaunchKernelGGL(k_lp_gains, dim3(gb), dim3(256), 0, st, lp);
-    if (lp.bm) lp_fill(lp, 0, ln.n192, 0, ln.n192, x, n_in, r, st);
+    if (lp.bm) lp_fill(lp, 0, ln.n192, 0, ln.n192, st);
     hipError_t e = hipMemsetAsync(lp.cnt, 0, sizeof(int) * (size_t)(lp.K + 1), st);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(lp.match, 0, sizeof(int) * (size_t)(lp.K + 1), st);
@@ -2126,7 +2080,7 @@ hipError_t launch_loudnorm_shard(const LnArgs &ln, const LpArgs &lp, const uint3
         hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
         const int gb = max((lp.T + 1 + 255) / 256, (LP_FR + 255) / 256);
         hipLaunchKernelGGL(k_lp_gains, dim3(gb), dim3(256), 0, st, lp);
-        if (lp.bm) lp_fill(lp, y_lo, y_hi, u_lo, u_hi, x, n_in, r, st);
+        if (lp.bm) lp_fill(lp, y_lo, y_hi, u_lo, u_hi, st);
         hipError_t e = hipMemsetAsync(lp.cnt, 0, sizeof(int) * (size_t)(lp.K + 1), st);
         if (e != hipSuccess) return e;
         e = hipMemsetAsync(lp.match, 0, sizeof(int) * (size_t)(lp.K + 1), st);
