@@ -1168,11 +1168,23 @@ __device__ __forceinline__ int lp_seg_start(const LpArgs &a, int k) {
     return a.T + 1 + (k - a.J - 1) * a.Fs;
 }
 
+// The limiter of one segment runs on a workgroup of LP_NT lanes (LP_NW waves): its
+// slot loops (fills, envelopes, output) and its peak scans are LP_NT wide, so a release's
+// 19 200 slots or a frame's scan take 1 / LP_NW of one wave's dependent memory round
+// trips; the scalar state is workgroup-uniform (every lane holds it).
+#ifndef AMX_LP_NT
+#define AMX_LP_NT 128
+#endif
+#define LP_NT AMX_LP_NT
+#define LP_NW (LP_NT / 64)
+#define LP_STW (LP_NT + 16)      // one channel's scan row: a group and its 12-position look-ahead
+
 struct LpWave {
     double2 *ring;         // [LP_RS] the multiplied slots' values (HBM)
     unsigned *flags;       // [LP_FW] LDS: slot multiplied since its last fill
-    double *st;            // [2][80] LDS: |x| of a peak-scan group
+    double *st;            // [2][LP_STW] LDS: |x| of a peak-scan group
     double *gl;            // [8] LDS: G[tb .. tb + 7] (clamped to T), the gain rows the frame's slots use
+    unsigned long long *sv;   // [LP_NW] LDS: the waves' votes
     int tb;
     double gT;             // G[T] (FINAL's gain)
     LpFrame f;
@@ -1180,6 +1192,63 @@ struct LpWave {
     double gr0, gr1;
     double d0, off;
 };
+
+// workgroup votes (uniform control flow only): the waves' ballots through LDS
+__device__ __forceinline__ void lp_vote(const LpWave &W, bool p, unsigned long long (&m)[LP_NW]) {
+    const unsigned long long b = __ballot(p);
+#if LP_NW == 1
+    m[0] = b;
+#else
+    __syncthreads();                       // the previous vote's readers are done
+    if ((threadIdx.x & 63) == 0) W.sv[threadIdx.x >> 6] = b;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < LP_NW; w++) m[w] = W.sv[w];
+#endif
+}
+// the first set bit at index >= from of an LP_NT-bit vote, or -1
+__device__ __forceinline__ int lp_next(const unsigned long long (&m)[LP_NW], int from) {
+#pragma unroll
+    for (int w = 0; w < LP_NW; w++) {
+        if (from >= 64 * (w + 1)) continue;
+        const int sh = from > 64 * w ? from - 64 * w : 0;
+        const unsigned long long x = m[w] >> sh;
+        if (x) return 64 * w + sh + __ffsll((long long)x) - 1;
+    }
+    return -1;
+}
+// the first lane whose p holds, or -1
+__device__ __forceinline__ int lp_first(const LpWave &W, bool p) {
+    unsigned long long m[LP_NW];
+    lp_vote(W, p, m);
+    return lp_next(m, 0);
+}
+// workgroup max / sum (the waves' reductions through the vote scratch)
+__device__ __forceinline__ double lp_wg_max(const LpWave &W, double v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v = fmax(v, __shfl_xor(v, o));
+#if LP_NW > 1
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) W.sv[threadIdx.x >> 6] = (unsigned long long)__double_as_longlong(v);
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < LP_NW; w++) v = fmax(v, __longlong_as_double((long long)W.sv[w]));
+#endif
+    return v;
+}
+__device__ __forceinline__ int lp_wg_sum(const LpWave &W, int v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o);
+#if LP_NW > 1
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) W.sv[threadIdx.x >> 6] = (unsigned long long)(unsigned)v;
+    __syncthreads();
+    v = 0;
+#pragma unroll
+    for (int w = 0; w < LP_NW; w++) v += (int)(unsigned)W.sv[w];
+#endif
+    return v;
+}
 
 // the position a slot holds: the latest filled one with that slot
 __device__ __forceinline__ int64_t lp_pos(const LpFrame &f, int s) {
@@ -1244,7 +1313,7 @@ __device__ __forceinline__ void lp_gload(const LpArgs &a, LpWave &W) {
 
 __device__ __forceinline__ void lp_clear_range(LpWave &W, int lo, int hi) {   // slots [lo, hi)
     if (hi <= lo) return;
-    for (int w = (lo >> 5) + (int)threadIdx.x; w <= ((hi - 1) >> 5); w += 64) {
+    for (int w = (lo >> 5) + (int)threadIdx.x; w <= ((hi - 1) >> 5); w += LP_NT) {
         const int b0 = w * 32;
         const int x0 = max(lo, b0) - b0, x1 = min(hi, b0 + 32) - b0;
         const unsigned m = (x1 - x0 == 32) ? 0xffffffffu : (((1u << (x1 - x0)) - 1u) << x0);
@@ -1266,7 +1335,7 @@ __device__ __forceinline__ void lp_refill(const LpArgs &a, LpWave &W, int phi) {
         }
     }
     if (cnt >= LP_RS) {
-        for (int w = threadIdx.x; w < LP_FW; w += 64) W.flags[w] = 0u;
+        for (int w = threadIdx.x; w < LP_FW; w += LP_NT) W.flags[w] = 0u;
     } else {
         lp_clear_range(W, s0, min(s0 + cnt, LP_RS));
         if (s0 + cnt > LP_RS) lp_clear_range(W, 0, s0 + cnt - LP_RS);
@@ -1276,16 +1345,16 @@ __device__ __forceinline__ void lp_refill(const LpArgs &a, LpWave &W, int phi) {
 }
 
 // multiply k slots from e0 by env(i) (af_loudnorm's envelope loops).  The k slots are
-// distinct, so the values of 4 groups of 64 are loaded before any of them is written
-// (one memory round trip per 256 slots)
+// distinct, so the values of 4 groups of LP_NT are loaded before any of them is written
+// (one memory round trip per 4 LP_NT slots)
 template <class F>
 __device__ __forceinline__ void lp_env(const LpArgs &a, LpWave &W, int e0, int k, F env) {
-    for (int i00 = 0; i00 < k; i00 += 256) {
+    for (int i00 = 0; i00 < k; i00 += 4 * LP_NT) {
         double2 v[4];
         int s[4];
 #pragma unroll
         for (int p = 0; p < 4; p++) {
-            const int i = i00 + 64 * p + (int)threadIdx.x;
+            const int i = i00 + LP_NT * p + (int)threadIdx.x;
             int ss = e0 + i;
             if (ss >= LP_RS) ss -= LP_RS;
             s[p] = ss;
@@ -1293,7 +1362,7 @@ __device__ __forceinline__ void lp_env(const LpArgs &a, LpWave &W, int e0, int k
         }
 #pragma unroll
         for (int p = 0; p < 4; p++) {
-            const int i = i00 + 64 * p + (int)threadIdx.x;
+            const int i = i00 + LP_NT * p + (int)threadIdx.x;
             if (i < k) {
                 const double g = env(i);
                 v[p].x = v[p].x * g;
@@ -1314,16 +1383,16 @@ __device__ __forceinline__ int lp_env_end(int e0, int k) {
 #ifndef AMX_LP_PD
 #define AMX_LP_PD 4              // (measurement builds: scripts/build_var.py)
 #endif
-#define LP_PD AMX_LP_PD          // lp_detect: groups of 64 positions loaded together
-// one group's values: 64 positions from slot s0
+#define LP_PD AMX_LP_PD          // lp_detect: groups of LP_NT positions loaded together
+// one group's values: LP_NT positions from slot s0
 __device__ __forceinline__ double2 lp_grp(const LpArgs &a, const LpWave &W, int s0, int lane) {
     int s = s0 + lane;
     while (s >= LP_RS) s -= LP_RS;
     return lp_val(a, W, s);
 }
 // detect_peak from offset smp over count positions: peak_delta or -1; the peak's |x|
-// and slot.  64 positions per step: the first one that is a candidate with its
-// previous sample as predecessor is found by a ballot; only from there on is the scan
+// and slot.  LP_NT positions per step: the first one that is a candidate with its
+// previous sample as predecessor is found by a vote; only from there on is the scan
 // serial (a candidate that fails the 10-sample look-ahead keeps the older predecessor).
 // A candidate needs |x| > ceiling.  Outside FINAL, a slot's value is its position's
 // fill (a function of the position alone, k_lp_fill) or that fill multiplied by the
@@ -1331,7 +1400,7 @@ __device__ __forceinline__ double2 lp_grp(const LpArgs &a, const LpWave &W, int 
 // reduction and 1, sustain at the reduction) up to their rounding: so a group whose
 // positions' fill maxima (a.bm, 64-position blocks), raised by a relative 1e-9 margin
 // for that rounding, are <= ceiling holds no candidate -- flagged or not -- and is
-// skipped without loading a value, 64 groups per ballot
+// skipped without loading a value, LP_NT groups per vote
 __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, int count, double &peak_value,
                          int &peak_slot) {
 #ifdef AMX_LPV_NODETECT        // measurement variant: the limiter never engages (wrong output)
@@ -1342,37 +1411,41 @@ __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, in
     if (slot0 >= LP_RS) slot0 -= LP_RS;
     const double ceiling = a.ceiling;
     double pv0 = 0.0, pv1 = 0.0;               // n = 0 never qualifies (n > 0)
-    double *st0 = W.st, *st1 = W.st + 80;
+    double *st0 = W.st, *st1 = W.st + LP_STW;
     const bool skip = a.bm != nullptr && !W.f.fin;
     // outside FINAL the positions of consecutive slots from slot0 are consecutive
     const int64_t pos0 = lp_pos(W.f, slot0);
-    unsigned long long mask = 0ull;
+    unsigned long long mask[LP_NW];
+#pragma unroll
+    for (int w = 0; w < LP_NW; w++) mask[w] = 0ull;
     int mask_base = -1;
     bool stale = false;
     int nb00 = 0;
     while (nb00 < count) {
         if (skip) {
-            if (mask_base < 0 || nb00 >= mask_base + 64 * 64) {
-                // lane j: may group nb00 + 64 j hold a candidate?
-                const int g0 = nb00 + 64 * lane;
+            if (mask_base < 0 || nb00 >= mask_base + LP_NT * LP_NT) {
+                // lane j: may group nb00 + LP_NT j hold a candidate?
+                const int g0 = nb00 + LP_NT * lane;
                 bool may = false;
                 if (g0 < count) {
                     const int64_t p = pos0 + g0;
-                    may = fmax(a.bm[p >> 6], a.bm[(p + 63) >> 6]) * (1.0 + 1e-9) > ceiling;
+                    double mx = a.bm[p >> 6];
+#pragma unroll
+                    for (int k = 1; k <= LP_NT / 64; k++) mx = fmax(mx, a.bm[(p + 64 * k - 1) >> 6]);
+                    may = mx * (1.0 + 1e-9) > ceiling;
                 }
-                mask = __ballot(may);
+                lp_vote(W, may, mask);
                 mask_base = nb00;
             }
-            const unsigned long long m = mask >> ((nb00 - mask_base) >> 6);
-            if (m == 0ull) {
-                nb00 = mask_base + 64 * 64;
+            const int d = lp_next(mask, (nb00 - mask_base) / LP_NT) - (nb00 - mask_base) / LP_NT;
+            if (d < 0) {
+                nb00 = mask_base + LP_NT * LP_NT;
                 mask_base = -1;
                 stale = true;
                 continue;
             }
-            const int d = __ffsll((long long)m) - 1;
             if (d > 0) {
-                nb00 += 64 * d;
+                nb00 += LP_NT * d;
                 stale = true;
                 if (nb00 >= count) break;
             }
@@ -1391,10 +1464,10 @@ __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, in
         // slots of the same ring window, in bounds, unused.
         double2 q[LP_PD + 1];
 #pragma unroll
-        for (int p = 0; p <= LP_PD; p++) q[p] = lp_grp(a, W, slot0 + nb00 + p * 64, lane);
+        for (int p = 0; p <= LP_PD; p++) q[p] = lp_grp(a, W, slot0 + nb00 + p * LP_NT, lane);
 #pragma unroll
     for (int p = 0; p < LP_PD; p++) {
-        const int nb0 = nb00 + 64 * p;
+        const int nb0 = nb00 + LP_NT * p;
         if (nb0 >= count) break;
         {
             const double2 v = q[p], v2 = q[p + 1];
@@ -1402,13 +1475,13 @@ __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, in
             st0[lane] = fabs(v.x);
             st1[lane] = fabs(v.y);
             if (lane < 12) {
-                st0[64 + lane] = fabs(v2.x);
-                st1[64 + lane] = fabs(v2.y);
+                st0[LP_NT + lane] = fabs(v2.x);
+                st1[LP_NT + lane] = fabs(v2.y);
             }
             __syncthreads();
         }
         const int n = nb0 + lane;
-        const int last = (count - nb0 < 64 ? count - nb0 : 64) - 1;
+        const int last = (count - nb0 < LP_NT ? count - nb0 : LP_NT) - 1;
         bool cand = false;
         if (n < count && n > 0) {
             const double t0 = st0[lane], t1 = st1[lane];
@@ -1416,13 +1489,12 @@ __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, in
             cand = (p0 <= t0 && st0[lane + 1] <= t0 && t0 > ceiling) ||
                    (p1 <= t1 && st1[lane + 1] <= t1 && t1 > ceiling);
         }
-        const unsigned long long m = __ballot(cand);
-        if (!m) {
+        const int L0 = lp_first(W, cand);
+        if (L0 < 0) {
             pv0 = st0[last];
             pv1 = st1[last];
             continue;
         }
-        const int L0 = __ffsll((long long)m) - 1;
         if (L0 > 0) {
             pv0 = st0[L0 - 1];
             pv1 = st1[L0 - 1];
@@ -1450,7 +1522,7 @@ __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, in
             }
         }
     }
-        nb00 += 64 * LP_PD;
+        nb00 += LP_NT * LP_PD;
     }
     return -1;
 }
@@ -1462,18 +1534,18 @@ __device__ __forceinline__ void lp_emit(const LpArgs &a, const LpWave &W) {
     const double ceiling = a.ceiling;
     uint32_t *y = reinterpret_cast<uint32_t *>(a.y);
     const int nb = W.f.nb;
-    for (int i00 = 0; i00 < nb; i00 += 256) {
+    for (int i00 = 0; i00 < nb; i00 += 4 * LP_NT) {
         double2 v[4];
 #pragma unroll
         for (int p = 0; p < 4; p++) {
-            const int i = i00 + 64 * p + (int)threadIdx.x;
+            const int i = i00 + LP_NT * p + (int)threadIdx.x;
             int s = W.f.lbi + i;
             while (s >= LP_RS) s -= LP_RS;
             v[p] = lp_val(a, W, s);                        // (i >= nb: read, unused)
         }
 #pragma unroll
         for (int p = 0; p < 4; p++) {
-            const int i = i00 + 64 * p + (int)threadIdx.x;
+            const int i = i00 + LP_NT * p + (int)threadIdx.x;
             if (i < nb) {
                 double o0 = v[p].x, o1 = v[p].y;
                 if (fabs(o0) > ceiling) o0 = ceiling * (o0 < 0 ? -1 : 1);
@@ -1505,9 +1577,8 @@ __device__ __forceinline__ unsigned lp_range_bits(int w, int lo, int len) {
 __device__ __forceinline__ void lp_emit_sparse(const LpArgs &a, const LpWave &W) {
     const int nb = W.f.nb, lbi = W.f.lbi;
     int cnt = 0;
-    for (int w = threadIdx.x; w < LP_FW; w += 64) cnt += __popc(W.flags[w] & lp_range_bits(w, lbi, nb));
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) cnt += __shfl_xor(cnt, o);
+    for (int w = threadIdx.x; w < LP_FW; w += LP_NT) cnt += __popc(W.flags[w] & lp_range_bits(w, lbi, nb));
+    cnt = lp_wg_sum(W, cnt);
     if (cnt == 0) return;
     if (cnt > LP_SPARSE_MAX) {
         lp_emit(a, W);
@@ -1515,7 +1586,7 @@ __device__ __forceinline__ void lp_emit_sparse(const LpArgs &a, const LpWave &W)
     }
     const double ceiling = a.ceiling;
     uint32_t *y = reinterpret_cast<uint32_t *>(a.y);
-    for (int w = threadIdx.x; w < LP_FW; w += 64) {
+    for (int w = threadIdx.x; w < LP_FW; w += LP_NT) {
         unsigned m = W.flags[w] & lp_range_bits(w, lbi, nb);
         while (m) {
             const int s = 32 * w + __ffs(m) - 1;
@@ -1538,12 +1609,11 @@ __device__ __forceinline__ void lp_call(const LpArgs &a, LpWave &W, int emit) {
     const double ceiling = a.ceiling;
     if (W.f.phi == 0) {
         double mx = 0.0;
-        for (int i = threadIdx.x; i < LP_ATT; i += 64) {
+        for (int i = threadIdx.x; i < LP_ATT; i += LP_NT) {
             const double2 v = lp_val(a, W, i);
             mx = fmax(mx, fmax(fabs(v.x), fabs(v.y)));
         }
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) mx = fmax(mx, __shfl_xor(mx, o));
+        mx = lp_wg_max(W, mx);
         if (mx > ceiling) {
             W.gr1 = ceiling / mx;
             W.mode = LO_SUSTAIN;
@@ -1643,7 +1713,7 @@ __device__ __forceinline__ void lp_rest(LpWave &W) {        // af_loudnorm's ini
     W.attack_length = LP_ATT;
     W.gr0 = 0.0;
     W.gr1 = 0.0;
-    for (int w = threadIdx.x; w < LP_FW; w += 64) W.flags[w] = 0u;
+    for (int w = threadIdx.x; w < LP_FW; w += LP_NT) W.flags[w] = 0u;
     __syncthreads();
 }
 
@@ -1653,7 +1723,7 @@ __device__ __forceinline__ void lp_snapshot(const LpArgs &a, const LpWave &W, do
     const int lane = threadIdx.x;
     const int w0 = W.f.lbi;
     bool out = false;
-    for (int w = lane; w < LP_FW; w += 64) {
+    for (int w = lane; w < LP_FW; w += LP_NT) {
         unsigned m = W.flags[w];
         // clear the window's bits: slots [w0, w0 + LP_WIN) mod LP_RS
 #pragma unroll
@@ -1666,7 +1736,7 @@ __device__ __forceinline__ void lp_snapshot(const LpArgs &a, const LpWave &W, do
         }
         out |= m != 0u;
     }
-    const bool dirty = __ballot(out) != 0ull;
+    const bool dirty = lp_first(W, out) >= 0;
     if (lane == 0) {
         rec[0] = W.mode;
         rec[1] = W.env_cnt;
@@ -1677,7 +1747,7 @@ __device__ __forceinline__ void lp_snapshot(const LpArgs &a, const LpWave &W, do
         rec[6] = W.f.phi;
         rec[LP_DIRTY] = dirty ? 1.0 : 0.0;
     }
-    for (int j = lane; j < LP_WIN; j += 64) {
+    for (int j = lane; j < LP_WIN; j += LP_NT) {
         int s = w0 + j;
         if (s >= LP_RS) s -= LP_RS;
 #ifdef AMX_LPV_NOSNAP          // measurement variant: the window's values not loaded (wrong output)
@@ -1700,9 +1770,9 @@ __device__ __forceinline__ void lp_restore(const LpArgs &a, LpWave &W, const dou
     W.attack_length = (int)rec[3];
     W.gr0 = rec[4];
     W.gr1 = rec[5];
-    for (int w = threadIdx.x; w < LP_FW; w += 64) W.flags[w] = 0u;
+    for (int w = threadIdx.x; w < LP_FW; w += LP_NT) W.flags[w] = 0u;
     __syncthreads();
-    for (int j = threadIdx.x; j < LP_WIN; j += 64) {
+    for (int j = threadIdx.x; j < LP_WIN; j += LP_NT) {
         int s = W.f.lbi + j;
         if (s >= LP_RS) s -= LP_RS;
         W.ring[s] = make_double2(rec[16 + 2 * j], rec[17 + 2 * j]);
@@ -1718,34 +1788,38 @@ __device__ __forceinline__ bool lp_bits_eq(double x, double y) {
 // two states at the same frame lead to the same future: equal scalars (only the mode
 // when both are at rest: OUT re-initialises the rest) and equal window values, and
 // neither has a multiplied slot outside the window
-__device__ __forceinline__ bool lp_same(const double *A, const double *B) {
+__device__ __forceinline__ bool lp_same(const LpWave &W, const double *A, const double *B) {
     bool diff = A[LP_DIRTY] != 0.0 || B[LP_DIRTY] != 0.0 || (int)A[0] != (int)B[0];
     if ((int)A[0] != LO_OUT || (int)B[0] != LO_OUT)
         for (int q = 0; q < 6; q++) diff |= !lp_bits_eq(A[q], B[q]);
-    for (int j = threadIdx.x; j < 2 * LP_WIN; j += 64) diff |= !lp_bits_eq(A[16 + j], B[16 + j]);
-    return __ballot(diff) == 0ull;
+    for (int j = threadIdx.x; j < 2 * LP_WIN; j += LP_NT) diff |= !lp_bits_eq(A[16 + j], B[16 + j]);
+    return lp_first(W, diff) < 0;
 }
 
 // boundary j: the later of segment j-1 (its end state) and segment j (its guess) to
 // arrive compares them
-__device__ __forceinline__ void lp_arrive(const LpArgs &a, int j) {
+// (every wave's record stores are released -- its own fence -- before lane 0 counts
+// the arrival; the count is broadcast through LDS)
+__device__ __forceinline__ void lp_arrive(const LpArgs &a, const LpWave &W, int j) {
     __threadfence();
-    int old = 0;
-    if (threadIdx.x == 0) old = atomicAdd(&a.cnt[j], 1);
-    old = __shfl(old, 0);
+    __syncthreads();
+    if (threadIdx.x == 0) W.sv[0] = (unsigned long long)(unsigned)atomicAdd(&a.cnt[j], 1);
+    __syncthreads();
+    const int old = (int)(unsigned)W.sv[0];
     if (old == 1) {
         __threadfence();
-        const bool same = lp_same(a.recE + (int64_t)(j - 1) * LP_REC, a.recG + (int64_t)j * LP_REC);
+        const bool same = lp_same(W, a.recE + (int64_t)(j - 1) * LP_REC, a.recG + (int64_t)j * LP_REC);
         if (threadIdx.x == 0) a.match[j] = same ? 1 : 0;
     }
 }
 
 __device__ __forceinline__ void lp_wave_init(const LpArgs &a, LpWave &W, double2 *ring, unsigned *flags,
-                                             double *st) {
+                                             double *st, unsigned long long *sv) {
     W.ring = ring;
     W.flags = flags;
     W.st = st;
-    W.gl = st + 160;
+    W.gl = st + 2 * LP_STW;
+    W.sv = sv;
     W.tb = 0;
     W.gT = a.G[a.T];
     W.d0 = a.dctl[0];
@@ -1863,13 +1937,14 @@ __global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t
 #define AMX_LP_WPE 3             // k_lp_seg waves per SIMD the register budget allows (168
                                  // VGPRs, a 300-B spill; 2: C5 dynamic 43.0 vs 40.9 ms)
 #endif
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AMX_LP_WPE))) k_lp_seg(LpArgs a) {
+__global__ void __launch_bounds__(LP_NT) __attribute__((amdgpu_waves_per_eu(AMX_LP_WPE))) k_lp_seg(LpArgs a) {
     if (a.ctl[0] != 0 && a.ctl[0] != 4) return;
     const int kh = a.ctl[0] == 4 ? a.ctl[4] : 0;     // a quiet start: k_ln_dyn ran segments < kh
     __shared__ unsigned flags[LP_FW];
-    __shared__ double st[168];
+    __shared__ double st[2 * LP_STW + 8];
+    __shared__ unsigned long long sv[LP_NW];
     LpWave W;
-    lp_wave_init(a, W, reinterpret_cast<double2 *>(a.rings) + (int64_t)blockIdx.x * LP_RS, flags, st);
+    lp_wave_init(a, W, reinterpret_cast<double2 *>(a.rings) + (int64_t)blockIdx.x * LP_RS, flags, st, sv);
     const int NF = a.T + 1 + LP_NFIN;
     for (int k = a.kb + blockIdx.x; k < a.ke; k += gridDim.x) {
         if (k < kh) continue;
@@ -1892,7 +1967,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AMX_LP_
                 lp_refill(a, W, phi);
                 if (phi == ak) {
                     lp_snapshot(a, W, a.recG + (int64_t)k * LP_REC);
-                    if (k > kh) lp_arrive(a, k);
+                    if (k > kh) lp_arrive(a, W, k);
                 }
                 lp_call(a, W, phi >= ak ? (a.bm ? 1 : 2) : 0);
             }
@@ -1901,7 +1976,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AMX_LP_
             W.f = lp_frame(a, bk);
             lp_refill(a, W, bk);
             lp_snapshot(a, W, a.recE + (int64_t)k * LP_REC);
-            lp_arrive(a, k + 1);
+            lp_arrive(a, W, k + 1);
         }
     }
 }
@@ -1914,13 +1989,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AMX_LP_
 // A shard (a.rec_in, chunk-sharded tracks): the walk covers the boundaries [kb, ke) from
 // the true state at kb that the previous rank's walker made, and leaves the true state at
 // ke in a.rec_out for the next rank (marked dirty when this walk fell back).
-__global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
+__global__ void __launch_bounds__(LP_NT) k_lp_walk(LpArgs a) {
     if (a.ctl[0] != 0 && a.ctl[0] != 4) return;
     const int kh = a.ctl[0] == 4 ? a.ctl[4] : 0;
     __shared__ unsigned flags[LP_FW];
-    __shared__ double st[168];
+    __shared__ double st[2 * LP_STW + 8];
+    __shared__ unsigned long long sv[LP_NW];
     LpWave W;
-    lp_wave_init(a, W, reinterpret_cast<double2 *>(a.wring), flags, st);
+    lp_wave_init(a, W, reinterpret_cast<double2 *>(a.wring), flags, st, sv);
     const int lane = threadIdx.x;
     const int NF = a.T + 1 + LP_NFIN, kS0 = a.J + 1, ke = a.ke;
     const double *cur = a.rec_in ? a.rec_in : a.recE + (int64_t)kh * LP_REC;
@@ -1932,12 +2008,12 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
             while (k < ke) {
                 const int j = k + lane;
                 const bool stop = j >= ke || j == kS0 || a.match[j] == 0;
-                const unsigned long long m = __ballot(stop);
-                if (m) {
-                    k += __ffsll((long long)m) - 1;
+                const int f = lp_first(W, stop);
+                if (f >= 0) {
+                    k += f;
                     break;
                 }
-                k += 64;
+                k += LP_NT;
             }
             cur = a.recE + (int64_t)(k - 1) * LP_REC;
             if (k >= ke) break;
@@ -1958,7 +2034,7 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
             fin = 1;
             break;
         }
-        const bool ok = k4 ? (a.match[k] != 0) : lp_same(cur, a.recG + (int64_t)k * LP_REC);
+        const bool ok = k4 ? (a.match[k] != 0) : lp_same(W, cur, a.recG + (int64_t)k * LP_REC);
         if (ok) {
             cur = a.recE + (int64_t)k * LP_REC;
             k4 = true;
@@ -1989,7 +2065,7 @@ __global__ void __launch_bounds__(64) k_lp_walk(LpArgs a) {
     }
     if (a.rec_out && ke < a.K) {
         // the true state at boundary ke for the next rank's walk
-        for (int q = lane; q < LP_REC; q += 64) a.rec_out[q] = cur[q];
+        for (int q = lane; q < LP_REC; q += LP_NT) a.rec_out[q] = cur[q];
         __syncthreads();
         if (lane == 0 && fallback) a.rec_out[LP_DIRTY] = 1.0;
     }
@@ -2058,8 +2134,8 @@ hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(lp.match, 0, sizeof(int) * (size_t)(lp.K + 1), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_lp_seg, dim3(lp.P), dim3(64), 0, st, lp);
-    hipLaunchKernelGGL(k_lp_walk, dim3(1), dim3(64), 0, st, lp);
+    hipLaunchKernelGGL(k_lp_seg, dim3(lp.P), dim3(LP_NT), 0, st, lp);
+    hipLaunchKernelGGL(k_lp_walk, dim3(1), dim3(LP_NT), 0, st, lp);
     hipLaunchKernelGGL(k_ln_dyn, dim3(1), dim3(LN_NT), 0, st, ln, 1);
     return hipGetLastError();
 }
@@ -2085,9 +2161,9 @@ hipError_t launch_loudnorm_shard(const LnArgs &ln, const LpArgs &lp, const uint3
         if (e != hipSuccess) return e;
         e = hipMemsetAsync(lp.match, 0, sizeof(int) * (size_t)(lp.K + 1), st);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_lp_seg, dim3(lp.P), dim3(64), 0, st, lp);
+        hipLaunchKernelGGL(k_lp_seg, dim3(lp.P), dim3(LP_NT), 0, st, lp);
     } else {
-        hipLaunchKernelGGL(k_lp_walk, dim3(1), dim3(64), 0, st, lp);
+        hipLaunchKernelGGL(k_lp_walk, dim3(1), dim3(LP_NT), 0, st, lp);
     }
     return hipGetLastError();
 }

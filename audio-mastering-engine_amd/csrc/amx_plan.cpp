@@ -1324,15 +1324,15 @@ struct LnLayout {
     int64_t total = 0;
 };
 // INNER frames, segments of Fs frames each warmed up Wf frames (AMX_LN_WARM, default 2)
-// before its start, at most P persistent k_lp_seg waves (AMX_LN_P, default 3072: three per
-// SIMD, k_lp_seg's register budget).  Fs (AMX_LN_SEG overrides) is the smallest >= 2 whose segments fit the P waves: a
+// before its start, at most P persistent k_lp_seg workgroups of AMX_LP_NT lanes (AMX_LN_P;
+// default 3072 waves: three per SIMD, k_lp_seg's register budget).  Fs (AMX_LN_SEG overrides) is the smallest >= 2 whose segments fit the P waves: a
 // wave then runs one segment, Fs + Wf frames (r04m: a 5-min track 11.9 -> 9.1 ms per
 // dynamic step from Fs 4 / Wf 3 / 1024 waves); a longer track takes longer segments, so
 // the warm-up share Wf / Fs shrinks instead of waves running several segments each.
 LnLayout ln_layout(int64_t n192, int64_t u_frames = -1, int p_cap = -1) {
     LnLayout l;
     l.Wf = 2;
-    int pmax = 3072;
+    int pmax = 3072 / (AMX_LP_NT / 64);
     if (const char *ev = std::getenv("AMX_LN_P")) pmax = std::max(64, std::atoi(ev));
     if (n192 >= LN_FIRST_FRAMES) {
         l.T = (int)((n192 - LN_FIRST_FRAMES + 19199) / 19200);
