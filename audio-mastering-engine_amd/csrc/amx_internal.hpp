@@ -364,6 +364,7 @@ struct DecideArgs {
     double target_i, target_tp, target_lra, level_in, limit;
     double *stats, *gains;
     int32_t *ctl;
+    int32_t *host_ctl;     // amx_plan_set_publish: the words also into pinned host memory
 };
 hipError_t launch_decide(const DecideArgs &a, hipStream_t st);
 hipError_t launch_publish(const int32_t *ctl, int32_t *host, int n, hipStream_t st);

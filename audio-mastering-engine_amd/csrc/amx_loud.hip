@@ -716,7 +716,11 @@ __global__ void __launch_bounds__(128) k_decide(DecideArgs a) {
     o[4] = si; o[5] = stp; o[6] = slra; o[7] = sthr;
     o[8] = (double)mode; o[9] = gain; o[10] = fast ? 1.0 : 0.0; o[11] = pk; o[12] = pk_out;
     a.gains[t] = gain;
-    a.ctl[t] = (fast ? AMX_CTL_FAST : 0) | (mode << 4);
+    const int32_t w = (fast ? AMX_CTL_FAST : 0) | (mode << 4);
+    a.ctl[t] = w;
+    // (amx_plan_set_publish) the word straight into the caller's pinned host memory, a
+    // system-scope store: the host polls it while the limiter runs, no node of its own
+    if (a.host_ctl) __hip_atomic_store(a.host_ctl + t, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 hipError_t launch_decide(const DecideArgs &a, hipStream_t st) {

@@ -1193,6 +1193,15 @@ struct LpWave {
     double d0, off;
 };
 
+// the workgroup barrier after ring stores another wave reads next: every wave's stores
+// have completed (vmcnt) before it arrives
+__device__ __forceinline__ void lp_sync_ring() {
+#if LP_NW > 1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    __syncthreads();
+}
+
 // workgroup votes (uniform control flow only): the waves' ballots through LDS
 __device__ __forceinline__ void lp_vote(const LpWave &W, bool p, unsigned long long (&m)[LP_NW]) {
     const unsigned long long b = __ballot(p);
@@ -1371,7 +1380,7 @@ __device__ __forceinline__ void lp_env(const LpArgs &a, LpWave &W, int e0, int k
                 atomicOr(&W.flags[s[p] >> 5], 1u << (s[p] & 31));
             }
         }
-        __syncthreads();
+        lp_sync_ring();
     }
 }
 
@@ -1778,7 +1787,7 @@ __device__ __forceinline__ void lp_restore(const LpArgs &a, LpWave &W, const dou
         W.ring[s] = make_double2(rec[16 + 2 * j], rec[17 + 2 * j]);
         atomicOr(&W.flags[s >> 5], 1u << (s & 31));
     }
-    __syncthreads();
+    lp_sync_ring();
 }
 
 __device__ __forceinline__ bool lp_bits_eq(double x, double y) {
@@ -2057,7 +2066,7 @@ __global__ void __launch_bounds__(LP_NT) k_lp_walk(LpArgs a) {
             double *r = a.wrec + (int64_t)toggle * LP_REC;
             toggle ^= 1;
             lp_snapshot(a, W, r);
-            __syncthreads();
+            lp_sync_ring();                // (the record's stores, read by every wave next)
             cur = r;
             k4 = false;
         }

@@ -277,6 +277,7 @@ struct amx_plan {
     int resamp = 0, upL = 1, upM = 1, upLin = 0, upLout = 0, up_static = 0, up_ok = 1;
     int meas_native = 0;    // no 192 kHz resampler for this rate: peaks only, no loudnorm
     const int32_t *gate = nullptr;   // amx_plan_set_gate: the per-sample kernels' mode word
+    int32_t *publish = nullptr;      // amx_plan_set_publish: pinned host words k_decide also stores
     // libswresample's phase count (L, or 1024 when L > 1024), phase step dst / src per
     // output; up_lin: the step is not an integer, every output interpolates between rows
     // ph and ph + 1 (bank row pc = row 0 one tap later) with weight owt[n]
@@ -1702,6 +1703,12 @@ int amx_plan_set_gate(amx_plan *p, const int32_t *d_gate) {
     return AMX_OK;
 }
 
+int amx_plan_set_publish(amx_plan *p, int32_t *h_ctl) {
+    if (!p) return fail(AMX_EINVAL, "null plan");
+    p->publish = h_ctl;
+    return AMX_OK;
+}
+
 int amx_env_counters(const amx_plan *p, const void *d_ws, int32_t *out, int32_t n) {
     if (!p || !out || n < 0) return fail(AMX_EINVAL, "null argument");
     const int32_t have = AMX_ENV_MAX_ROUNDS * AMX_ENV_NCTR;
@@ -1876,6 +1883,7 @@ int amx_loudness_decide(amx_plan *p, const amx_decide_desc *dd, const amx_final_
     a.stats = d_stats;
     a.gains = d_gains;
     a.ctl = d_ctl;
+    a.host_ctl = p->publish;
     HIPCHK(amx::launch_decide(a, (hipStream_t)stream));
     return AMX_OK;
 }
