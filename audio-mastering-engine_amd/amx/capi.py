@@ -101,7 +101,7 @@ EXPORTS = ("amx_abi_version", "amx_last_error", "amx_build_id", "amx_plan_create
            "amx_plan_get_info", "amx_plan_track_span", "amx_run_chunks", "amx_run_stage",
            "amx_loudness_pass1", "amx_loudness_pass1_part",
            "amx_kw_propagate", "amx_loudness_pass2", "amx_loudness_histograms",
-           "amx_limiter_geometry", "amx_limiter_prepare", "amx_loudness_decide", "amx_kw_carry_setup", "amx_kw_carry", "amx_kw_carry_rows",
+           "amx_limiter_geometry", "amx_limiter_prepare", "amx_loudness_decide", "amx_kw_carry_setup", "amx_kw_carry", "amx_kw_carry_rows", "amx_plan_set_publish",
            "amx_finalize", "amx_env_counters", "amx_pcm_to_s16", "amx_loudnorm_192k_size",
            "amx_loudnorm_192k", "amx_loudnorm_192k_ex", "amx_flac_info", "amx_flac_decode",
            "amx_plan_set_gate", "amx_loudnorm_192k_shard", "amx_loudnorm_192k_segments",
@@ -150,6 +150,7 @@ def load(path=None):
     L.amx_kw_carry_setup.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]
     L.amx_kw_carry.argtypes = [vp, vp, vp, vp]
     L.amx_kw_carry_rows.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp]
+    L.amx_plan_set_publish.argtypes = [vp, vp]
     L.amx_finalize.argtypes = [vp, ctypes.POINTER(FinalDesc), vp, vp, vp, ctypes.c_int32, vp, vp,
                                vp, vp, vp]
     L.amx_loudnorm_192k_size.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64),
@@ -246,6 +247,12 @@ class Plan:
         n = len(frames_after)
         arr = (ctypes.c_int64 * max(1, n))(*[int(f) for f in frames_after])
         check(load().amx_kw_carry_setup(self.h, n, arr), "amx_kw_carry_setup")
+
+    def set_publish(self, host):
+        """amx_plan_set_publish: a pinned host int32 tensor k_decide also stores the
+        decision words into (None: stop)"""
+        check(load().amx_plan_set_publish(self.h, ctypes.c_void_p(host.data_ptr()) if host is not None else None),
+              "amx_plan_set_publish")
 
     def set_gate(self, d_word):
         """amx_plan_set_gate: a device int32 tensor (its first word), or None"""

@@ -229,9 +229,10 @@ class ShardedTrack:
     """This rank's part of one chunk-sharded track.
 
     A step has three exchanges (every one a single collective over all ranks):
-      1. edges: each rank's first 16 and last max(16, B - 1) output frames, all-gathered
+      1. edges: each rank's first 80 and last max(80, B - 1) output frames, all-gathered
          as raw bytes -- the 192 kHz resampler window of the loudness measurement
-         reaches 16 frames into both neighbours, and the alimiter's look-ahead ring
+         reaches up to 80 frames into both neighbours (16 for the 32-tap filter, more
+         for the downsampling filter above 192 kHz), and the alimiter's look-ahead ring
          needs the previous rank's last B - 1 frames;
       2. K-filter tails (8 doubles) and sample peaks (4 doubles), all-gathered: every
          rank builds its incoming K-filter state (amx_kw_carry) and the track's peaks;
@@ -811,6 +812,7 @@ class ShardedTrack:
         buffers).  Every rank takes the same branch (the word comes from all-reduced
         data), so RCCL operations stay in the same order on every rank."""
         lufs_on = self.job.dd.lufs_on
+        self._lim_rest = torch.zeros_like(self.job.lim_state)
         slots = []
         for k in range(2):
             if k == 1:
@@ -821,6 +823,7 @@ class ShardedTrack:
             job = self.job
             self._ctl_host = torch.zeros(1, dtype=torch.int32).pin_memory()
             self._ctl_ev = torch.cuda.Event()
+            job.plan.set_publish(self._ctl_host)
 
             def whole(job=job):
                 job.run_chunks(d_in)
@@ -835,11 +838,10 @@ class ShardedTrack:
                     job.loudness_pass2(carry=True)
                     reduce_loudness(job.hops, None, self.group)
                     job.histograms()
-                job.decide()
-                # the in-graph limiter run from rest on the device's decision (see fin)
-                job.lim_state.zero_()
-                job.finalize(None)
-                job.publish_ctl(self._ctl_host)
+                job.decide()                   # (k_decide also stores the word to _ctl_host)
+                # the in-graph limiter run from rest on the device's decision (see fin):
+                # its entering state is a buffer of zeros no kernel writes
+                job.finalize(None, state=self._lim_rest)
             self._g = [seg(whole)]
             slots.append({key: getattr(self, key) for key in self._SLOT_KEYS})
         self._slots = slots

@@ -190,12 +190,15 @@ class MasteringJob:
         capi.check(capi.load().amx_publish_ctl(capi.ptr(self.ctl), ctypes.c_void_p(host.data_ptr()),
                                                int(self.n_tracks), self._s(stream)), "amx_publish_ctl")
 
-    def finalize(self, fast=None, stream=None):
-        """fast None: each track takes the limiter path amx_loudness_decide chose."""
+    def finalize(self, fast=None, stream=None, state=None):
+        """fast None: each track takes the limiter path amx_loudness_decide chose.
+        state: the limiter state entering the span (default self.lim_state; a buffer of
+        zeros = from rest, read only)."""
         ctl = capi.ptr(self.ctl) if fast is None else None
+        st = self.lim_state if state is None else state
         capi.check(capi.load().amx_finalize(self.plan.h, self.fd, capi.ptr(self.out), capi.ptr(self.gains),
                                             ctl, 1 if fast else 0, capi.ptr(self.halo), capi.ptr(self.y),
-                                            capi.ptr(self.lim_state), capi.ptr(self.ws), self._s(stream)),
+                                            capi.ptr(st), capi.ptr(self.ws), self._s(stream)),
                    "amx_finalize")
 
     def env_counters(self):
@@ -401,7 +404,10 @@ class MasteringJob:
         if os.environ.get("AMX_DYN_INLINE") == "1":
             dyn = False      # (diagnostics: the gated dynamic path inside the step's graph)
         if dyn:
+            # k_decide stores the decision words here as well (amx_plan_set_publish): the
+            # host reads them while the limiter kernel still runs
             self._ctl_pin = torch.full((max(1, self.n_tracks),), -1, dtype=torch.int32).pin_memory()
+            self.plan.set_publish(self._ctl_pin)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -410,7 +416,7 @@ class MasteringJob:
         g = torch.cuda.CUDAGraph()
         # thread_local: other threads (a process group's watchdog) may query events meanwhile
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            self.run(d_in, dyn=not dyn, ctl_to=self._ctl_pin[:self.n_tracks] if dyn else None)
+            self.run(d_in, dyn=not dyn)
         self._graph = g
         self._dyn_eager = dyn
         return g
@@ -423,15 +429,16 @@ class MasteringJob:
         linear step pays none of its ~35 launches per track.  (A graph of its own for
         that path replayed 10-20x slower than the same launches made eagerly, with
         walker re-runs: profiles/r05_dyn_graph.txt.)"""
-        self._graph.replay()
         if not getattr(self, "_dyn_eager", False):
+            self._graph.replay()
             return self.y[:self.info.out_frames]
         h = self._ctl_pin
+        h.fill_(-1)                 # (the previous step's words were read: its decide has run)
+        self._graph.replay()
         hv = h.numpy()[:self.n_tracks]
         while (hv == -1).any():
             pass
         dyn = [t for t in range(self.n_tracks) if (int(hv[t]) >> 4) & 15 == 3]   # k_decide mode 3
-        h.fill_(-1)                 # (read: the next step's words replace it)
         for t in dyn:
             self._dyn_enqueue(t, self._dyn_sides[t], None, gate=True)
         return self.y[:self.info.out_frames]

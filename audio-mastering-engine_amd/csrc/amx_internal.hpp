@@ -155,8 +155,11 @@ struct ScanPlan {
 };
 hipError_t launch_front1(const Launch &l, int D, int win, bool analog, const float *in,
                          const float *lut, int16_t *a16, const double *G, double *e);
+// tailP / tail (the K filter, D = 4): the down sweep also writes each stream's end state
+// P_t s_last + e_last (k_kw_tail's product) from its last block
 hipError_t launch_scan(const ScanPlan &p, const double *e, double *s, const double *carry,
-                       double *eb, hipStream_t st, bool up = true);
+                       double *eb, hipStream_t st, bool up = true, const double *tailP = nullptr,
+                       double *tail = nullptr);
 hipError_t launch_front2(const Launch &l, int mask, const int16_t *a16, const double *s_eq,
                          int16_t *dst, int to_out, const double *Gx, double *e_x,
                          const double *Gkw, double *e_kw, uint32_t *pk);

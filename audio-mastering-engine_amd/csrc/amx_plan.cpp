@@ -1434,10 +1434,14 @@ int amx_loudness_pass1_part(amx_plan *p, int32_t part, const int16_t *d_out, con
     HIPCHK(amx::launch_peak_reduce(p->d_spans, p->n_tracks, p->max_nkseg, pk, d_peak, p->d_pcnt,
                                    p->d_ppart, p->d_ksegs, p->Lkw, d_out, p->d_Gkw, e, p->fuse_kw,
                                    p->resamp, st));
-    HIPCHK(amx::launch_scan(p->scan_kw(), e, s, nullptr, wsp<double>(d_ws, p->o_ebk), st));
+    // the span tails from the scan's own down sweep unless a span is empty (its tail is 0:
+    // k_kw_tail writes it)
+    const bool tail_fused = d_kw_tail && !p->any_empty_span;
+    HIPCHK(amx::launch_scan(p->scan_kw(), e, s, nullptr, wsp<double>(d_ws, p->o_ebk), st, true,
+                            tail_fused ? p->d_tailpow : nullptr, tail_fused ? d_kw_tail : nullptr));
     p->kw_rest_states = 1;   // s = the start states from rest: pass 2 without a carry reuses them
     p->kw_eb_ready = 1;      // and the block sums: pass 2 with a carry runs the down sweep only
-    if (d_kw_tail)
+    if (d_kw_tail && !tail_fused)
         HIPCHK(amx::launch_kw_tail(p->d_spans, p->n_tracks, s, e, p->d_tailpow, d_kw_tail, st));
     return AMX_OK;
 }

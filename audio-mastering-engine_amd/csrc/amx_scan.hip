@@ -28,7 +28,9 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_scan_blk(const ScanBlk *__restric
                                                         const double *__restrict__ M,
                                                         const double *__restrict__ Mbk, int K,
                                                         const double *__restrict__ carry,
-                                                        double *__restrict__ eb) {
+                                                        double *__restrict__ eb,
+                                                        const double *__restrict__ tailP,
+                                                        double *__restrict__ tail) {
     // GW groups of GP lanes in each wave (a group never straddles waves, so wave
     // barriers order its LDS exchange); lanes past GW GP are idle.  GP = D packs the
     // groups: D = 20 -> 3 groups per wave (60 lanes) instead of 2 of 32.
@@ -111,7 +113,25 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_scan_blk(const ScanBlk *__restric
         if (DOWN) {
             const int64_t jj = (int64_t)bk.seg0 + q;
             if (row) s[(jj * 2 + ch) * D + i] = v;
-            if (q == n - 1) break;                         // the next block has its own B
+            if (q == n - 1) {                              // the next block has its own B
+                if constexpr (D == AMX_KW_DIM) {
+                    // the stream's end state from these start states (k_kw_tail's
+                    // product, same order): P_t s_last + e_last, by the last block
+                    if (tail && bk.last) {
+                        if (lane_ok) my[i] = v;
+                        __builtin_amdgcn_wave_barrier();
+                        double acc = 0.0;
+#pragma unroll
+                        for (int qq = 0; qq < AMX_SCAN_S; qq++) acc = qq == q ? ev[qq] : acc;
+                        const double *Pt = tailP + (int64_t)bk.stream * 16;
+#pragma unroll
+                        for (int k = 0; k < D; k++) acc = fma(Pt[ri * 4 + k], my[k], acc);
+                        if (row) tail[((int64_t)bk.stream * 2 + ch) * D + i] = acc;
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                }
+                break;
+            }
         }
         if (lane_ok) my[i] = v;
         __builtin_amdgcn_wave_barrier();
@@ -146,31 +166,32 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_scan_blk(const ScanBlk *__restric
 // ================================================================ launchers
 template <int D, int GP>
 static hipError_t scan_t(const ScanPlan &p, const double *e, double *s, const double *carry,
-                         double *eb, bool up, hipStream_t st) {
+                         double *eb, bool up, const double *tailP, double *tail, hipStream_t st) {
     constexpr int GPB = (64 / GP) * (AMX_BLOCK / 64);
     const dim3 gb((unsigned)((2 * (int64_t)p.n_blk + GPB - 1) / GPB));
     if (up)
         hipLaunchKernelGGL((k_scan_blk<D, GP, false>), gb, dim3(AMX_BLOCK), 0, st, p.blks, p.n_blk, e,
-                           s, p.M, p.Mbk, p.K, carry, eb);
+                           s, p.M, p.Mbk, p.K, carry, eb, nullptr, nullptr);
     hipLaunchKernelGGL((k_scan_blk<D, GP, true>), gb, dim3(AMX_BLOCK), 0, st, p.blks, p.n_blk, e,
-                       s, p.M, p.Mbk, p.K, carry, eb);
+                       s, p.M, p.Mbk, p.K, carry, eb, tailP, tail);
     return hipGetLastError();
 }
 
 // up false: eb already holds the up sweep of these e (the block sums do not depend on
 // the carry), only the down sweep runs
 hipError_t launch_scan(const ScanPlan &p, const double *e, double *s, const double *carry,
-                       double *eb, hipStream_t st, bool up) {
+                       double *eb, hipStream_t st, bool up, const double *tailP, double *tail) {
     if (p.n_blk <= 0 || p.D <= 0) return hipSuccess;
+    if (tail && p.D != AMX_KW_DIM) return hipErrorInvalidValue;
     switch (p.D) {
-    case 2: return scan_t<2, 2>(p, e, s, carry, eb, up, st);
-    case 4: return scan_t<4, 4>(p, e, s, carry, eb, up, st);
-    case 8: return scan_t<8, 8>(p, e, s, carry, eb, up, st);
-    case 10: return scan_t<10, 10>(p, e, s, carry, eb, up, st);
-    case 12: return scan_t<12, 12>(p, e, s, carry, eb, up, st);
-    case 16: return scan_t<16, 16>(p, e, s, carry, eb, up, st);
-    case 18: return scan_t<18, 18>(p, e, s, carry, eb, up, st);
-    case 20: return scan_t<20, 20>(p, e, s, carry, eb, up, st);
+    case 2: return scan_t<2, 2>(p, e, s, carry, eb, up, tailP, tail, st);
+    case 4: return scan_t<4, 4>(p, e, s, carry, eb, up, tailP, tail, st);
+    case 8: return scan_t<8, 8>(p, e, s, carry, eb, up, tailP, tail, st);
+    case 10: return scan_t<10, 10>(p, e, s, carry, eb, up, tailP, tail, st);
+    case 12: return scan_t<12, 12>(p, e, s, carry, eb, up, tailP, tail, st);
+    case 16: return scan_t<16, 16>(p, e, s, carry, eb, up, tailP, tail, st);
+    case 18: return scan_t<18, 18>(p, e, s, carry, eb, up, tailP, tail, st);
+    case 20: return scan_t<20, 20>(p, e, s, carry, eb, up, tailP, tail, st);
     }
     return hipErrorInvalidValue;
 }

@@ -414,6 +414,10 @@ AMX_API int amx_loudness_decide(amx_plan *plan, const amx_decide_desc *dd, const
  * without a copy node's completion stall).  Replaces no reference line: the reference
  * reads ffmpeg's printed statistics (:231-237). */
 AMX_API int amx_publish_ctl(const int32_t *d_ctl, int32_t *h_ctl, int32_t n, void *stream);
+/* The same words stored by amx_loudness_decide itself (its kernel's last stores; no node
+ * of their own in a captured step): h_ctl = pinned host memory of n_tracks int32 words,
+ * NULL to stop.  The plan keeps the pointer; the caller keeps the memory alive. */
+AMX_API int amx_plan_set_publish(amx_plan *plan, int32_t *h_ctl);
 
 /* Chunk-sharded tracks: K-filter state entering this plan's (single) span from the
  * zero-start tails of the n_prev spans before it.  Setup (host, once): frames_after[q]
