@@ -1193,6 +1193,13 @@ struct LpWave {
     double d0, off;
 };
 
+// a barrier only a multi-wave workgroup needs (one wave's lanes run in lock step)
+__device__ __forceinline__ void lp_wg_barrier() {
+#if LP_NW > 1
+    __syncthreads();
+#endif
+}
+
 // the workgroup barrier after ring stores another wave reads next: every wave's stores
 // have completed (vmcnt) before it arrives
 __device__ __forceinline__ void lp_sync_ring() {
@@ -1332,6 +1339,9 @@ __device__ __forceinline__ void lp_clear_range(LpWave &W, int lo, int hi) {   //
 
 // the fill at the start of frame phi: the slots it refills lose their flags
 __device__ __forceinline__ void lp_refill(const LpArgs &a, LpWave &W, int phi) {
+    // every wave is done with the previous frame's flags and gain rows (its output pass
+    // reads them) before they are rewritten
+    lp_wg_barrier();
     int s0 = 0, cnt = LP_RS;
     if (phi != 0 && phi != a.T + 1) {
         if (phi <= a.T) {
@@ -1716,6 +1726,7 @@ __device__ __forceinline__ void lp_call(const LpArgs &a, LpWave &W, int emit) {
 }
 
 __device__ __forceinline__ void lp_rest(LpWave &W) {        // af_loudnorm's initial limiter state
+    lp_wg_barrier();                       // (the flags' previous readers are done)
     W.mode = LO_OUT;
     W.env_cnt = 0;
     W.env_index = 0;
@@ -1771,6 +1782,7 @@ __device__ __forceinline__ void lp_snapshot(const LpArgs &a, const LpWave &W, do
 
 // the same state back into a wave (every window slot flagged with its recorded value)
 __device__ __forceinline__ void lp_restore(const LpArgs &a, LpWave &W, const double *rec, int phi) {
+    lp_wg_barrier();                       // (the flags', gain rows' and ring's previous readers are done)
     W.f = lp_frame(a, phi);
     lp_gload(a, W);
     W.mode = (int)rec[0];
