@@ -1003,11 +1003,18 @@ class Span192(ShardedTrack):
 
     def measure(self, lufs_on):
         """the stream's loudness (lufs_on) and peaks from the runs, as ShardedTrack.step
-        measures the chain output: every rank ends with the same statistics row"""
+        measures the chain output: every rank ends with the same statistics row.  Without
+        the loudness only the limiter's input bound is needed: the filter's ceiling
+        (engine.ln_output_bound), the same on every rank"""
+        from .engine import ln_output_bound
         job = self.job
         self.exchange_edges()
-        job.loudness_pass1(tail=True)
-        self.exchange_carry_peaks()
+        bound = None if lufs_on else ln_output_bound(self.ttotal)
+        if bound is not None:
+            job.peak.fill_(bound)
+        else:
+            job.loudness_pass1(tail=True)
+            self.exchange_carry_peaks()
         job.dd.lufs_on = 1 if lufs_on else 0
         if lufs_on:
             job.loudness_pass2(carry=True)

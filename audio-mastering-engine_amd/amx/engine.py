@@ -43,6 +43,18 @@ def final_desc(params=ALIMITER):
     return fd
 
 
+def ln_output_bound(n192):
+    """The largest |sample| / 32768 of loudnorm's dynamic-mode output (int16 at 192 kHz):
+    its true-peak limiter clamps every sample to the ceiling 10^(TP / 20) (af_loudnorm's
+    final clamp), and the WAV muxer rounds to s16.  None for a track under 3 s, which
+    takes the linear path (output = input x offset, unclamped)."""
+    import math
+    if n192 < 576000:                   # frame_size(192000, 3000): the linear fallback
+        return None
+    c = 10.0 ** (LOUDNORM_TP / 20.0)
+    return min(math.floor(c * 32768.0 + 0.5), 32767) / 32768.0
+
+
 class MasteringJob:
     def __init__(self, sample_rate, channels_in, settings, track_frames, *, quantum=None,
                  input_s16=False, seg_frames=128, device=None, chunks=None, track_frame0=None,
@@ -292,7 +304,15 @@ class MasteringJob:
         self.timed("ln_filter2", lambda: filt(d2, self.stats[t], self._i_out[t:t + 1]), stream)
 
         def limit():
-            job2.loudness_pass1(stream, tail=False)            # the limiter's input bound
+            # the limiter's input bound: af_loudnorm clamps every limited output sample to
+            # its ceiling, so that is the bound without a pass over the 192 kHz samples
+            # (a track under 3 s takes the unlimited linear path: measured)
+            bound = ln_output_bound(n192)
+            if bound is not None:
+                with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
+                    job2.peak.fill_(bound)
+            else:
+                job2.loudness_pass1(stream, tail=False)
             job2.dd.lufs_on = 0
             job2.decide(stream)
             job2.finalize(None, stream)

@@ -2145,7 +2145,10 @@ hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x
                            const SwrDev &r, bool resample, hipStream_t st) {
     if (ln.n192 <= 0) return hipSuccess;
     if (resample) ln_upsample(x, n_in, r, 0, ln.n192, ln.u, lp.gate, st);
-    hipLaunchKernelGGL(k_lp_stats, dim3(1 + (lp.T + LP_STAT_F - 1) / LP_STAT_F), dim3(LP_STAT_NT), 0, st, lp);
+    // reuse (pass 2 on pass 1's scratch): the frames' statistics depend on the input's hop
+    // energies alone and stand -- only block 0, the resolved options, runs
+    hipLaunchKernelGGL(k_lp_stats, dim3(resample ? 1 + (lp.T + LP_STAT_F - 1) / LP_STAT_F : 1), dim3(LP_STAT_NT), 0,
+                       st, lp);
     hipLaunchKernelGGL(k_ln_dyn, dim3(1), dim3(LN_NT), 0, st, ln, 0);
     hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
     const int gb = max((lp.T + 1 + 255) / 256, (LP_FR + 255) / 256);
@@ -2172,7 +2175,8 @@ hipError_t launch_loudnorm_shard(const LnArgs &ln, const LpArgs &lp, const uint3
     if (ln.n192 <= 0) return hipSuccess;
     if (part == 0) {
         if (resample) ln_upsample(x, n_in, r, u_lo, u_hi, ln.u, lp.gate, st);
-        hipLaunchKernelGGL(k_lp_stats, dim3(1 + (lp.T + LP_STAT_F - 1) / LP_STAT_F), dim3(LP_STAT_NT), 0, st, lp);
+        hipLaunchKernelGGL(k_lp_stats, dim3(resample ? 1 + (lp.T + LP_STAT_F - 1) / LP_STAT_F : 1), dim3(LP_STAT_NT),
+                           0, st, lp);
     } else if (part == 1) {
         hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
         const int gb = max((lp.T + 1 + 255) / 256, (LP_FR + 255) / 256);

@@ -275,9 +275,10 @@ AMX_API int amx_loudness_pass1_part(amx_plan *plan, int32_t part, const int16_t 
 typedef struct amx_loudnorm_desc {
     double target_i, target_lra, target_tp;                     /* I, LRA, TP */
     double measured_i, measured_lra, measured_tp, measured_thresh, offset;   /* pass 1: 0, 0, 99, -70, 0 */
-    /* nonzero: d_ws2 still holds this track's 192 kHz stream from the previous call on
-     * the same d_out and scratch (pass 2 after pass 1: the same input, resampled the same
-     * way) -- the resampler is not run again; 0: the call resamples d_out */
+    /* nonzero: d_ws2 still holds this track's 192 kHz stream and per-frame statistics from
+     * the previous call on the same d_out, hop energies and scratch (pass 2 after pass 1:
+     * the same input, resampled and measured the same way) -- neither is formed again;
+     * 0: the call resamples d_out and forms them */
     int32_t reuse_stream;
 } amx_loudnorm_desc;
 /* output frames (ceil(frames * 192000 / fs)) and the d_ws2 bytes amx_loudnorm_192k needs */
