@@ -111,12 +111,28 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_ln_up_static(const uint32_t *__re
                 w1[i] = (float)hi16(v) * (1.0f / 32768.0f);
             }
         }
+        float o[2 * L];
+#pragma unroll
+        for (int ph = 0; ph < L; ph++) {
+            const float *h = bank + ph * LN_TAPS;
+            o[2 * ph] = ln_dot2(w0, h);
+            o[2 * ph + 1] = ln_dot2(w1, h);
+        }
+        if constexpr (L % 2 == 0) {
+            // the frame's L outputs are 8 L contiguous bytes: 16-B stores (16-B aligned: u
+            // is, and 8 L f is a multiple of 16) when all of them are in range
+            if (f * L >= j0 && f * L + L <= j1) {
+#pragma unroll
+                for (int q = 0; q < L / 2; q++)
+                    *reinterpret_cast<float4 *>(u + 2 * (f * L) + 4 * q) =
+                        make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+                continue;
+            }
+        }
 #pragma unroll
         for (int ph = 0; ph < L; ph++) {
             const int64_t j = f * L + ph;
-            const float *h = bank + ph * LN_TAPS;
-            const float a = ln_dot2(w0, h), b = ln_dot2(w1, h);
-            if (j >= j0 && j < j1) *reinterpret_cast<float2 *>(u + 2 * j) = make_float2(a, b);
+            if (j >= j0 && j < j1) *reinterpret_cast<float2 *>(u + 2 * j) = make_float2(o[2 * ph], o[2 * ph + 1]);
         }
     }
 }
