@@ -84,55 +84,82 @@ __device__ __forceinline__ float ln_dot2(const float *w, const float *__restrict
 }
 
 // The M == 1 rates (192 kHz / L: 48 kHz L = 4, 96 kHz 2, 64 kHz 3, 32 kHz 6, 192 kHz 1):
-// output j = frame j / L, phase j % L.  One thread per input frame: its 32-frame window
-// once, then the L outputs with the bank rows as wave-uniform operands (k_ln_upsample's
+// output j = frame j / L, phase j % L.  One thread per LN_UPF consecutive input frames:
+// one window of 31 + LN_UPF frames (loaded once: 35 loads for 4 frames instead of 128),
+// then every frame's L outputs with the bank rows as wave-uniform operands (k_ln_upsample's
 // generic form pays two 64-bit divisions and a per-lane bank row for every output).
+#define LN_UPF 4
 template <int L>
 __global__ void __launch_bounds__(AMX_BLOCK) k_ln_up_static(const uint32_t *__restrict__ x, int64_t n_in,
                                                             const float *__restrict__ bank, int64_t j0, int64_t j1,
                                                             float *__restrict__ u, const int32_t *__restrict__ gate) {
     if (AMX_LN_GATED(gate)) return;
+    constexpr int NW = LN_TAPS + LN_UPF - 1;
     const int64_t f0 = j0 / L, f1 = (j1 + L - 1) / L;
-    for (int64_t f = f0 + (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x; f < f1; f += (int64_t)gridDim.x * AMX_BLOCK) {
-        float w0[LN_TAPS], w1[LN_TAPS];
-        const int64_t g = f - LN_C;
-        if (g >= 0 && g + LN_TAPS <= n_in) {
+    const int64_t nblk = (f1 - f0 + LN_UPF - 1) / LN_UPF;
+    for (int64_t bi = (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x; bi < nblk; bi += (int64_t)gridDim.x * AMX_BLOCK) {
+        const int64_t fb = f0 + bi * LN_UPF;          // this thread's first frame
+        float w0[NW], w1[NW];
+        const int64_t g = fb - LN_C;
+        static_assert(LN_UPF == 4 && LN_C % 4 == 3, "the 16-B window loads start one frame early");
+        if (g >= 1 && g - 1 + NW + 1 <= n_in && ((reinterpret_cast<uintptr_t>(x + g - 1) & 15) == 0)) {
+            // 16-B loads of frames g - 1 .. g + NW - 1 (g - 1 = fb - 16: 16-B aligned when x is)
+            uint32_t wv[NW + 1];
 #pragma unroll
-            for (int i = 0; i < LN_TAPS; i++) {
+            for (int i = 0; i < (NW + 1) / 4; i++) {
+                const uint4 q = *reinterpret_cast<const uint4 *>(x + g - 1 + 4 * i);
+                wv[4 * i] = q.x; wv[4 * i + 1] = q.y; wv[4 * i + 2] = q.z; wv[4 * i + 3] = q.w;
+            }
+#pragma unroll
+            for (int i = 0; i < NW; i++) {
+                w0[i] = (float)lo16(wv[i + 1]) * (1.0f / 32768.0f);
+                w1[i] = (float)hi16(wv[i + 1]) * (1.0f / 32768.0f);
+            }
+        } else if (g >= 0 && g + NW <= n_in) {
+#pragma unroll
+            for (int i = 0; i < NW; i++) {
                 const uint32_t v = x[g + i];
                 w0[i] = (float)lo16(v) * (1.0f / 32768.0f);
                 w1[i] = (float)hi16(v) * (1.0f / 32768.0f);
             }
         } else {
 #pragma unroll
-            for (int i = 0; i < LN_TAPS; i++) {
+            for (int i = 0; i < NW; i++) {
                 const uint32_t v = x[ln_reflect(g + i, n_in)];
                 w0[i] = (float)lo16(v) * (1.0f / 32768.0f);
                 w1[i] = (float)hi16(v) * (1.0f / 32768.0f);
             }
         }
-        float o[2 * L];
 #pragma unroll
-        for (int ph = 0; ph < L; ph++) {
-            const float *h = bank + ph * LN_TAPS;
-            o[2 * ph] = ln_dot2(w0, h);
-            o[2 * ph + 1] = ln_dot2(w1, h);
-        }
-        if constexpr (L % 2 == 0) {
-            // the frame's L outputs are 8 L contiguous bytes: 16-B stores (16-B aligned: u
-            // is, and 8 L f is a multiple of 16) when all of them are in range
-            if (f * L >= j0 && f * L + L <= j1) {
+        for (int k = 0; k < LN_UPF; k++) {
+            const int64_t f = fb + k;
+            if (f >= f1) break;
+            float o[2 * L];
 #pragma unroll
-                for (int q = 0; q < L / 2; q++)
-                    *reinterpret_cast<float4 *>(u + 2 * (f * L) + 4 * q) =
-                        make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-                continue;
+            for (int ph = 0; ph < L; ph++) {
+                const float *h = bank + ph * LN_TAPS;
+                o[2 * ph] = ln_dot2(w0 + k, h);
+                o[2 * ph + 1] = ln_dot2(w1 + k, h);
             }
-        }
+            bool done = false;
+            if constexpr (L % 2 == 0) {
+                // the frame's L outputs are 8 L contiguous bytes: 16-B stores when all are
+                // in range
+                if (f * L >= j0 && f * L + L <= j1) {
 #pragma unroll
-        for (int ph = 0; ph < L; ph++) {
-            const int64_t j = f * L + ph;
-            if (j >= j0 && j < j1) *reinterpret_cast<float2 *>(u + 2 * j) = make_float2(o[2 * ph], o[2 * ph + 1]);
+                    for (int q = 0; q < L / 2; q++)
+                        *reinterpret_cast<float4 *>(u + 2 * (f * L) + 4 * q) =
+                            make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+                    done = true;
+                }
+            }
+            if (!done) {
+#pragma unroll
+                for (int ph = 0; ph < L; ph++) {
+                    const int64_t j = f * L + ph;
+                    if (j >= j0 && j < j1) *reinterpret_cast<float2 *>(u + 2 * j) = make_float2(o[2 * ph], o[2 * ph + 1]);
+                }
+            }
         }
     }
 }
@@ -2145,7 +2172,7 @@ static void ln_upsample(const uint32_t *x, int64_t n_in, const SwrDev &r, int64_
         return;
     }
     if (!r.lin && r.src == r.dst) {
-        const int64_t nf = (j1 + r.pc - 1) / r.pc - j0 / r.pc;
+        const int64_t nf = ((j1 + r.pc - 1) / r.pc - j0 / r.pc + LN_UPF - 1) / LN_UPF;   // frame blocks
         switch (r.pc) {
 #define LN_UPS(LL) \
         case LL: hipLaunchKernelGGL(k_ln_up_static<LL>, grid(nf), dim3(AMX_BLOCK), 0, st, x, n_in, r.bank, j0, j1, u, gate); return;
