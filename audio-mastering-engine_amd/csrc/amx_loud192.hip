@@ -707,6 +707,7 @@ hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent
             }
         }
         switch (a.static_l > 0 ? a.static_l : a.poly) {
+        case 1: hipLaunchKernelGGL(k_up<1>, dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a); break;
         case 2: hipLaunchKernelGGL(k_up<2>, dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a); break;
         case 4: hipLaunchKernelGGL(k_up<4>, dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a); break;
 #define AMX_UP_POLY_CASE(c0, c1, t)                                                                  \

@@ -474,15 +474,29 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
             // M == 1: the unrolled kernels (phase pattern static, phase 0 the identity)
             bool ident0 = p->up_taps == 32 && bank[15] == 1.0f;
             for (int i = 0; i < 32 && ident0; i++) ident0 = ident0 && (i == 15 || bank[i] == 0.0f);
-            p->up_static = (p->upM == 1 && (p->upL == 2 || p->upL == 4) && ident0 && !p->up_lin &&
+            p->up_static = (p->upM == 1 && (p->upL == 1 || p->upL == 2 || p->upL == 4) && ident0 && !p->up_lin &&
                             p->upLin % 8 == 0) ? p->upL : 0;
         }
     } else {
         // already 192 kHz: ffmpeg inserts no resampler ahead of af_loudnorm, only the s16
         // -> dbl conversion x / 32768; a one-phase bank that is the unit impulse makes
-        // k_ln_upsample produce exactly that (every other tap adds 0)
+        // k_ln_upsample produce exactly that (every other tap adds 0).  The measurement
+        // takes the resampler path with that identity (L = M = 1, k_up<1>): one pass over
+        // the samples -- K filter, peaks and the hop pieces' energy terms -- where the
+        // native path ran the GEMV and then the filter again (k_kw1 + k_kw2).
+        // AMX_K192_NATIVE=1 keeps the native path (measurements).
         bank.assign(32, 0.0f);
         bank[15] = 1.0f;
+        if (std::getenv("AMX_K192_NATIVE") == nullptr) {
+            p->resamp = 1;
+            p->upL = p->upM = 1;
+            p->up_pc = 1;
+            p->up_taps = p->up_alloc = 32;
+            p->up_src = p->up_dst = 1;
+            p->up_lin = 0;
+            p->upLin = p->upLout = 480;            // 40 K segments per 100 ms hop
+            p->up_static = 1;
+        }
     }
     p->hop = (kfs + 5) / 10;                   // libebur128 samples_in_100ms at 192 kHz
     {
