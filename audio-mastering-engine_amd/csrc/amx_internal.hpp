@@ -272,7 +272,7 @@ struct LnArgs {
 #define AMX_LN_WIN 2048            // ring frames compared at a segment boundary
 #define AMX_LN_REC (16 + 2 * AMX_LN_WIN)   // doubles of one boundary state record
 #ifndef AMX_LP_NT
-#define AMX_LP_NT 128    // lanes of a k_lp_seg / k_lp_walk workgroup (amx_loudnorm.hip)
+#define AMX_LP_NT 256    // lanes of a k_lp_seg / k_lp_walk workgroup (amx_loudnorm.hip)
 #endif
 struct LpArgs {
     int64_t n;                    // 192 kHz frames

@@ -1216,7 +1216,7 @@ __device__ __forceinline__ int lp_seg_start(const LpArgs &a, int k) {
 // 19 200 slots or a frame's scan take 1 / LP_NW of one wave's dependent memory round
 // trips; the scalar state is workgroup-uniform (every lane holds it).
 #ifndef AMX_LP_NT
-#define AMX_LP_NT 128
+#define AMX_LP_NT 256
 #endif
 #define LP_NT AMX_LP_NT
 #define LP_NW (LP_NT / 64)
