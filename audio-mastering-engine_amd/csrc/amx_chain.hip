@@ -699,7 +699,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_xover2(const ChainDev *__restrict
                                                       const SegDev *__restrict__ segs, int n_seg,
                                                       int L, const uint32_t *__restrict__ p16,
                                                       const double *__restrict__ s_x,
-                                                      uint32_t *__restrict__ bands, int64_t nloc) {
+                                                      uint32_t *__restrict__ bands, int64_t nloc,
+                                                      int *__restrict__ bact) {
     constexpr int WV = AMX_BLOCK / 64;
     __shared__ __attribute__((aligned(16))) uint32_t s_in[WV][32 * AMX_VT_PITCH];
     __shared__ __attribute__((aligned(16))) uint32_t s_b[WV][2][32 * AMX_VT_PITCH];
@@ -709,6 +710,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_xover2(const ChainDev *__restrict
     const int j = blockIdx.x * (AMX_BLOCK / 2) + wv * 32 + row;
     if (t < 12) s_c[t] = cd.xlo[t];
     else if (t < 24) s_c[t] = cd.xhi[t - 12];
+    // the step's band-activity words start clear (k_rms sets them; amx_dyn.hip)
+    if (blockIdx.x == 0 && t < 3) bact[t] = 0;
     double z[AMX_XO_DIM];
 #pragma unroll
     for (int d = 0; d < AMX_XO_DIM; d++) z[d] = 0.0;
@@ -886,13 +889,13 @@ hipError_t launch_front2(const Launch &l, int mask, const int16_t *a16, const do
 }
 
 hipError_t launch_xover2(const Launch &l, const int16_t *p16, const double *s_x,
-                         int16_t *bands, int64_t nloc) {
+                         int16_t *bands, int64_t nloc, int *bact) {
     if (l.n_seg <= 0) return hipSuccess;
     const int rows = AMX_BLOCK / 2;
     dim3 grid((unsigned)((l.n_seg + rows - 1) / rows));
     hipLaunchKernelGGL(k_xover2, grid, dim3(AMX_BLOCK), 0, l.stream, l.cd, l.chunks, l.segs,
                        l.n_seg, l.L, reinterpret_cast<const uint32_t *>(p16), s_x,
-                       reinterpret_cast<uint32_t *>(bands), nloc);
+                       reinterpret_cast<uint32_t *>(bands), nloc, bact);
     return hipGetLastError();
 }
 

@@ -77,7 +77,8 @@ template <int LP>
 __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ cdp,
                                                    const ChunkDev *__restrict__ chunks,
                                                    const uint32_t *__restrict__ bands,
-                                                   uint16_t *__restrict__ mi, int64_t nloc) {
+                                                   uint16_t *__restrict__ mi, int64_t nloc,
+                                                   int *bact) {
     constexpr int N = AMX_RMS_N;
     constexpr int F = N - LP;                          // frames out per workgroup
     constexpr int PER = N / AMX_BLOCK;                 // 16 slots per thread
@@ -155,19 +156,30 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ 
         const uint32_t cnt = head ? 2u * (uint32_t)i : cfull;
         return rms_floor(S, cnt, head ? 1.0 / (double)cnt : rfull);
     };
+    // band activity: a frame whose m may be nonzero (r >= rq; every r below rq has m = 0)
+    const uint32_t rq = (uint32_t)cdp->rq[b];
+    bool hot = false;
     if (whole) {
 #pragma unroll
-        for (int k = 0; k < OUT; k++) mo[base + t + k * AMX_BLOCK] = (uint16_t)rms_at(k);
+        for (int k = 0; k < OUT; k++) {
+            const uint32_t rms = rms_at(k);
+            hot |= rms >= rq;
+            mo[base + t + k * AMX_BLOCK] = (uint16_t)rms;
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < OUT; k++) {
             const int64_t i = base + t + k * AMX_BLOCK;
             const uint32_t rms = rms_at(k);
+            hot |= i < ch.n && rms >= rq;
             // the row's tail past the chunk (to the 16-frame boundary) gets r = 0, m = 0:
             // k_env0 feeds a chunk's partial last tile without masking
             if (i < rowlen) mo[i] = i < ch.n ? (uint16_t)rms : (uint16_t)0;
         }
     }
+    // one word per band, cleared by k_xover2; set once (read first, so the later
+    // workgroups of an active band do not all store to the one line)
+    if (__syncthreads_or(hot) && t == 0 && bact[b] == 0) bact[b] = 1;
 }
 
 // m of table index r.  Rows hold r only where a chunk has frames: the padding and a
@@ -354,6 +366,34 @@ __device__ double env_rerun_wave(const ChainDev &cd, const uint16_t *m, const do
 // read in bounds.  W and Le are multiples of 16 AMX_ENV_PF and chunk rows start
 // 16-frame aligned, so the warm-up / main boundary is tile-uniform, every vector is
 // aligned and checkpoints fall on tile starts.
+// The bands k_rms found active (a frame over the threshold) and the segment table of
+// their count (ChainDev::etab).  An inactive band has m = 0 on every frame, so its
+// attenuation stays at the chunk start's 0 throughout: the envelope kernels skip it
+// and k_gain_overlay passes it through unread.  Slot s (k_env0's blockIdx.y) runs the
+// s-th active band, so t active bands share the CUs.
+struct EnvBands {
+    int mask;                    // bit b: band b active (wave-uniform)
+    int nb;
+    __device__ __forceinline__ bool act(int b) const { return (mask >> b) & 1; }
+};
+__device__ __forceinline__ EnvBands env_bands(const int *bact) {
+    EnvBands e;
+    e.mask = 0;
+#pragma unroll
+    for (int b = 0; b < 3; b++) e.mask |= (__builtin_amdgcn_readfirstlane(bact[b]) != 0) << b;
+    e.nb = __builtin_popcount(e.mask);
+    return e;
+}
+// the band of slot s: the position of the (s + 1)-th set bit of the mask
+__device__ __forceinline__ int env_slot_band(const EnvBands &e, int s) {
+    int m = e.mask;
+    for (int k = 0; k < s; k++) m &= m - 1;
+    return __builtin_ctz(m | 8);
+}
+
+#ifndef AMX_ENV_FIXBANDS
+#define AMX_ENV_FIXBANDS 1   // (measurement variant 0: the fix-up ignores the band flags; 3-band table only)
+#endif
 #define AMX_ENV_TF 16
 #define AMX_ENV_MP 18      // m tile pitch in doubles (144 B)
 #define AMX_ENV_PF 8       // r tiles in flight
@@ -476,7 +516,7 @@ __global__ void __launch_bounds__(64 * AMX_ENV_WG) k_env0(const ChainDev *__rest
                                              double *__restrict__ ck,
                                              double *__restrict__ sv, double *__restrict__ ev,
                                              int *__restrict__ act, int64_t nloc, int warm,
-                                             int Le, int *__restrict__ flags) {
+                                             int *__restrict__ flags) {
     __shared__ __attribute__((aligned(16))) double sm_all[AMX_ENV_WG][64 * AMX_ENV_MP];
     const ChainDev &cd = *cdp;
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -485,8 +525,14 @@ __global__ void __launch_bounds__(64 * AMX_ENV_WG) k_env0(const ChainDev *__rest
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) {
         for (int k = lane; k < AMX_ENV_MAX_ROUNDS * AMX_ENV_NCTR; k += 64) flags[AMX_ENV_MAX_ROUNDS + k] = 0;
     }
+    const EnvBands eb = env_bands(flags + AMX_ENV_BACT);
+    if ((int)blockIdx.y >= eb.nb) return;                 // workgroup-uniform
+    const int b = env_slot_band(eb, blockIdx.y);
+    es += cd.etab[eb.nb].es_off;
+    n_es = cd.etab[eb.nb].n_es;
+    const int Le = cd.etab[eb.nb].Le, ld = cd.es_ld;
+    if ((int)(blockIdx.x * (blockDim.x >> 6)) * 64 >= n_es) return;
     const int j = (blockIdx.x * (blockDim.x >> 6) + wv) * 64 + lane;
-    const int b = blockIdx.y;
     const bool valid = j < n_es;
     const SegDev sg = es[valid ? j : n_es - 1];
     const ChunkDev ch = chunks[sg.chunk];
@@ -524,9 +570,9 @@ __global__ void __launch_bounds__(64 * AMX_ENV_WG) k_env0(const ChainDev *__rest
                            q0 + u, ntile, nwarm, start, end, ckr, att, s_spec, any);
     }
     if (valid) {
-        sv[(int64_t)b * n_es + j] = s_spec;
-        ev[(int64_t)b * n_es + j] = att;
-        act[(int64_t)b * n_es + j] = any ? 1 : 0;
+        sv[(int64_t)b * ld + j] = s_spec;
+        ev[(int64_t)b * ld + j] = att;
+        act[(int64_t)b * ld + j] = any ? 1 : 0;
     }
 }
 
@@ -571,15 +617,25 @@ __global__ void __launch_bounds__(64) k_envfix(const ChainDev *__restrict__ cdp,
                                                int *flags, int round, int fix) {
     if (round > 0 && __builtin_amdgcn_readfirstlane(flags[round - 1]) == 0) return;
     const ChainDev &cd = *cdp;
+    const int b = blockIdx.y;
+#if AMX_ENV_FIXBANDS
+    const EnvBands eb = env_bands(flags + AMX_ENV_BACT);
+    if (!eb.act(b)) return;
+    const int tb = eb.nb;
+#else
+    const int tb = 3;
+#endif
+    es += cd.etab[tb].es_off;
+    n_es = cd.etab[tb].n_es;
+    if ((int)blockIdx.x * 64 >= n_es) return;
     // per-round counters after the round flags: segments re-run, the most re-runs in
     // one wave (its chain of dependent fixes), waves with work, look-back steps
     int *ctr = flags + AMX_ENV_MAX_ROUNDS + round * AMX_ENV_NCTR;
     const int lane = threadIdx.x;
     const int w0 = blockIdx.x * 64;
     const int j = w0 + lane;
-    const int b = blockIdx.y;
     const bool valid = j < n_es;
-    const int64_t bo = (int64_t)b * n_es;
+    const int64_t bo = (int64_t)b * cd.es_ld;
     const int jc = valid ? j : n_es - 1;
     const SegDev sg = es[jc];
     const bool a = valid && act[bo + jc] != 0;
@@ -673,10 +729,19 @@ __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
     if (fl >= 0 && __builtin_amdgcn_readfirstlane(flags[fl]) == 0) return;
     const ChainDev &cd = *cdp;
     const int c = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
-    const int s0 = eseg0[c], s1 = s0 + neseg[c];
+#if AMX_ENV_FIXBANDS
+    const EnvBands eb = env_bands(flags + AMX_ENV_BACT);
+    if (!eb.act(b)) return;
+    const int tb = eb.nb;
+#else
+    const int tb = 3;
+#endif
+    es += cd.etab[tb].es_off;
+    const int s0 = eseg0[cd.etab[tb].ch_off + c], s1 = s0 + neseg[cd.etab[tb].ch_off + c];
     const ChunkDev ch = chunks[c];
-    double *S = sv + (int64_t)b * n_es, *E = ev + (int64_t)b * n_es;
-    const int *A = act + (int64_t)b * n_es, *Pv = prev + (int64_t)b * n_es;
+    const int64_t ld = cd.es_ld;
+    double *S = sv + (int64_t)b * ld, *E = ev + (int64_t)b * ld;
+    const int *A = act + (int64_t)b * ld, *Pv = prev + (int64_t)b * ld;
     const int64_t ro = b * nloc + ch.loc_off;
     int cur = s0;
     while (cur < s1) {
@@ -740,7 +805,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
                                                             const int *__restrict__ act,
                                                             const int *__restrict__ eseg0,
                                                             const int *__restrict__ neseg,
-                                                            int n_es, int seg_tiles) {
+                                                            int use_act, const int *__restrict__ bact) {
     __shared__ __attribute__((aligned(16))) uint32_t sx_all[AMX_GO_WAVES][64 * AMX_GO_XP];
     const ChainDev &cd = *cdp;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -762,14 +827,20 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
         const int64_t f = wbase + 4 * (64 * i + lane);
         xo[i] = ch.loc_off + (f < rowlen ? f : 0);
     }
-    // seg_tiles (= Le, a multiple of this wave's 1024 frames): a band whose envelope segment has no
-    // over-threshold frame (act == 0) has m = 0 on the whole tile -- its r is not read
-    bool mzero[3] = {false, false, false};
-    const int jt = seg_tiles ? (int)(wbase / seg_tiles) : 0;   // the envelope segment holding the wave
-    if (seg_tiles && jt < neseg[c]) {
-        const int js = eseg0[c] + jt;
+    // an inactive band (k_rms) has m = 0 and att = 0 everywhere: neither its r nor its
+    // checkpoints are read.  With Le (the table's) a multiple of this wave's 1024 frames,
+    // a band whose envelope segment has no over-threshold frame (act == 0) has m = 0 on
+    // the whole tile -- its r is not read
+    const EnvBands eb = env_bands(bact);
+    bool mzero[3];
 #pragma unroll
-        for (int b = 0; b < 3; b++) mzero[b] = act[(int64_t)b * n_es + js] == 0;
+    for (int b = 0; b < 3; b++) mzero[b] = !eb.act(b);
+    const int seg_tiles = use_act && cd.etab[eb.nb].Le % (64 * AMX_ENV_TF_) == 0 ? cd.etab[eb.nb].Le : 0;
+    const int jt = seg_tiles ? (int)(wbase / seg_tiles) : 0;   // the envelope segment holding the wave
+    if (seg_tiles && jt < neseg[cd.etab[eb.nb].ch_off + c]) {
+        const int js = eseg0[cd.etab[eb.nb].ch_off + c] + jt;
+#pragma unroll
+        for (int b = 0; b < 3; b++) mzero[b] = mzero[b] || act[(int64_t)b * cd.es_ld + js] == 0;
     }
     u4v Mp[2];
     u4v Xp[4];
@@ -813,7 +884,7 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
             xv[4 * k] = v.x; xv[4 * k + 1] = v.y; xv[4 * k + 2] = v.z; xv[4 * k + 3] = v.w;
         }
         __builtin_amdgcn_wave_barrier();
-        double att = i0 < n ? ck[(b * nloc + ch.loc_off + i0) / AMX_ENV_TF_] : 0.0;
+        double att = i0 < n && eb.act(b) ? ck[(b * nloc + ch.loc_off + i0) / AMX_ENV_TF_] : 0.0;
         // m = 0 on every frame of the wave (below the threshold) holds each lane's att,
         // so its gain is one value: formed once instead of per frame.  With att = 0 as
         // well every frame passes unchanged (the reference's "att != 0" test)
@@ -876,19 +947,19 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
 
 // ---------------------------------------------------------------- launchers
 template <int LP>
-static void rms_t(const DynLaunch &d, const int16_t *bands, uint16_t *m) {
+static void rms_t(const DynLaunch &d, const int16_t *bands, uint16_t *m, int *bact) {
     constexpr int F = AMX_RMS_N - LP;
     dim3 g((unsigned)((d.max_chunk_n + F - 1) / F), (unsigned)d.n_chunks, 3);
     if (empty(g)) return;
     hipLaunchKernelGGL(k_rms<LP>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks,
-                       reinterpret_cast<const uint32_t *>(bands), m, d.nloc);
+                       reinterpret_cast<const uint32_t *>(bands), m, d.nloc, bact);
 }
 
-hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m) {
+hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m, int *bact) {
     if (d.look > AMX_RMS_MAXLOOK) return hipErrorInvalidValue;
-    if (d.look <= 256) rms_t<256>(d, bands, m);
-    else if (d.look <= 512) rms_t<512>(d, bands, m);
-    else rms_t<1024>(d, bands, m);
+    if (d.look <= 256) rms_t<256>(d, bands, m, bact);
+    else if (d.look <= 512) rms_t<512>(d, bands, m, bact);
+    else rms_t<1024>(d, bands, m, bact);
     return hipGetLastError();
 }
 
@@ -901,7 +972,7 @@ static void env_launch_t(const DynLaunch &d, const uint16_t *m, double *ck, doub
         const int wg = d.env_wg >= 1 && d.env_wg <= AMX_ENV_WG ? d.env_wg : 1;
         const dim3 g0((unsigned)((d.n_es + 64 * wg - 1) / (64 * wg)), 3);
         hipLaunchKernelGGL((k_env0<RCP>), g0, dim3(64 * wg), d.env_pin ? AMX_ENV_LDS_PIN : 0, d.st, d.cd,
-                           d.chunks, d.es, d.n_es, m, d.tabs, ck, sv, ev, act, d.nloc, d.warm, d.Le, flags);
+                           d.chunks, d.es, d.n_es, m, d.tabs, ck, sv, ev, act, d.nloc, d.warm, flags);
         return;
     }
     // rounds == 0: only prev[] (everything is left to k_envseq)
@@ -936,20 +1007,19 @@ hipError_t launch_envseq(const DynLaunch &d, const uint16_t *m, double *ck, doub
 
 hipError_t launch_gain_overlay(const DynLaunch &d, const uint16_t *m, const double *ck,
                                const int16_t *bands, int16_t *out, int64_t max_chunk_out,
-                               const int64_t *n1tab, const int *act) {
+                               const int64_t *n1tab, const int *act, const int *bact) {
     dim3 g((unsigned)((max_chunk_out + AMX_ENV_TF_ * AMX_BLOCK - 1) / (AMX_ENV_TF_ * AMX_BLOCK)),
            (unsigned)d.n_chunks);
     if (empty(g)) return hipSuccess;
     const uint32_t *x = reinterpret_cast<const uint32_t *>(bands);
     uint32_t *o = reinterpret_cast<uint32_t *>(out);
-    // a wave's 1024 frames lie in one envelope segment when Le is a multiple of 1024
-    const int seg_tiles = (act && d.Le % (64 * AMX_ENV_TF_) == 0) ? d.Le : 0;
+    // (a wave's 1024 frames lie in one envelope segment when the table's Le is a multiple of 1024)
     if (d.rcp)
         hipLaunchKernelGGL(k_gain_overlay<true>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, m, d.tabs, ck,
-                           x, o, d.nloc, n1tab, act, d.eseg0, d.neseg, d.n_es, seg_tiles);
+                           x, o, d.nloc, n1tab, act, d.eseg0, d.neseg, act ? 1 : 0, bact);
     else
         hipLaunchKernelGGL(k_gain_overlay<false>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, m, d.tabs, ck,
-                           x, o, d.nloc, n1tab, act, d.eseg0, d.neseg, d.n_es, seg_tiles);
+                           x, o, d.nloc, n1tab, act, d.eseg0, d.neseg, act ? 1 : 0, bact);
     return hipGetLastError();
 }
 

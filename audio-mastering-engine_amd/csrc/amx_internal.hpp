@@ -18,6 +18,7 @@
 #define AMX_STATS 16      // doubles per track written by k_decide
 #define AMX_ENV_MAX_ROUNDS 16  // k_envfix rounds (one flag word each)
 #define AMX_ENV_NCTR 4         // k_envfix diagnostic counters per round (after the flags)
+#define AMX_ENV_BACT (AMX_ENV_MAX_ROUNDS * (1 + AMX_ENV_NCTR))  // band-activity words after the counters
 #define AMX_EQC 64        // compact EQ coefficient block (see ChainDev::eqc)
 #define AMX_MEAS_RATE 192000  // loudnorm pass 1 measures at 192 kHz (af_loudnorm dynamic mode)
 #ifndef AMX_PCM_U8        // input PCM formats (include/amx.h amx_pcm_to_s16)
@@ -77,6 +78,14 @@ struct ChainDev {
     // k_env0's warm-up start guess: 1 = m of the warm-up's first frame, 0 = att = 0
     // 
     int32_t env_guess;
+    // envelope segment tables by active-band count (amx_dyn.hip): table t (1..3) cuts
+    // the chunks into segments of Le frames so that t bands' segments fill the CUs as
+    // one resident wave set; k_rms flags the bands with a frame over the threshold and
+    // the envelope kernels take the table of that count.  Offsets index the plan's
+    // concatenated segment array and per-chunk (first, count) arrays; the per-band
+    // segment arrays (s, e, act, prev) have stride es_ld = the largest n_es
+    int32_t es_ld;
+    struct { int32_t es_off, n_es, ch_off, Le; } etab[4];
     // exp10 constants of the gain (amx_dyn.hip exp10_gain): read through the plan so
     // they are scalar operands of the FMAs (a 64-bit literal is not encodable)
     double exc[16];
@@ -164,13 +173,13 @@ hipError_t launch_front2(const Launch &l, int mask, const int16_t *a16, const do
                          int16_t *dst, int to_out, const double *Gx, double *e_x,
                          const double *Gkw, double *e_kw, uint32_t *pk);
 hipError_t launch_xover2(const Launch &l, const int16_t *p16, const double *s_x,
-                         int16_t *bands, int64_t nloc);
+                         int16_t *bands, int64_t nloc, int *bact);
 struct DynLaunch {
     const ChainDev *cd;
     const ChunkDev *chunks;
     int n_chunks;
-    const SegDev *es;            // envelope segments (Le frames, per chunk)
-    int n_es;
+    const SegDev *es;            // envelope segments: the tables of ChainDev::etab, concatenated
+    int n_es;                    // the largest table's segment count (= ChainDev::es_ld)
     const int *eseg0, *neseg;    // per chunk: first envelope segment, count
     int64_t nloc, max_chunk_n;
     int look, warm, Le, rcp;
@@ -178,7 +187,7 @@ struct DynLaunch {
     hipStream_t st;
     int env_wg, env_pin;         // k_env0: waves per workgroup, one workgroup per CU
 };
-hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m);
+hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m, int *bact);
 // input decode: PCM of any supported format -> stereo s16 frames (amx_io.hip)
 hipError_t launch_pcm_to_s16(const void *raw, int64_t frames, int channels, int fmt, int16_t *out,
                              hipStream_t st);
@@ -188,7 +197,7 @@ hipError_t launch_envseq(const DynLaunch &d, const uint16_t *m, double *ck, doub
                          const int *act, const int *prev, const int *flags, int rounds);
 hipError_t launch_gain_overlay(const DynLaunch &d, const uint16_t *m, const double *ck,
                                const int16_t *bands, int16_t *out, int64_t max_chunk_out,
-                               const int64_t *n1tab, const int *act);
+                               const int64_t *n1tab, const int *act, const int *bact);
 // loudness
 // gate (amx_plan_set_gate): the kernel returns at once unless the word says dynamic
 hipError_t launch_kw1(const ChainDev *cd, const KwSegDev *ks, int n_kseg, int L,

@@ -300,6 +300,7 @@ struct amx_plan {
     int lev_eq = 0, lev_x = 0, lev_kw = 0;
     int mb = 0;
     int Le = 1024, warm = 2304, rounds = 2;   // compressor envelope segments (amx_dyn.hip)
+    int Le_t[4] = {0, 0, 0, 0};               // segment length of the table for t active bands
     int env_wg = 1, env_pin = 0;              // k_env0 placement (amx_dyn.hip launch_env)
     int f1_mode = AMX_F1_SPLIT;               // pass-1 form for float32 stereo + analog
     int n_es = 0;
@@ -713,19 +714,32 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
                 if (hipGetDevice(&dev) != hipSuccess ||
                     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 3)
                     ncu = 256;
-                // segments per band: W waves of one band per CU
-                const int64_t fit = (int64_t)(ncu / 3) * 64 * p->env_wg;
+                // segments per band: W waves of one band per CU, the CUs shared by the t
+                // bands that are active (t = 3: every band; the tables for 1 and 2 active
+                // bands have shorter segments, floor 512 frames; AMX_ENV_BANDTAB=0 keeps
+                // the 3-band table for every count)
+                int bandtab = 1;
+                if (const char *ev = std::getenv("AMX_ENV_BANDTAB")) bandtab = std::atoi(ev);
                 int64_t total = 0;
                 for (int c = 0; c < n_chunks; c++) total += chunks[c].frames;
-                int64_t Le = std::max<int64_t>(le_min, (total / fit + 127) / 128 * 128);
-                for (;; Le += 128) {
-                    int64_t ne = 0;
-                    for (int c = 0; c < n_chunks; c++) ne += (chunks[c].frames + Le - 1) / Le;
-                    if (ne <= fit || Le >= (int64_t)1 << 24) break;
+                for (int t = 3; t >= 1; t--) {
+                    const int64_t fit = (int64_t)(ncu / t) * 64 * p->env_wg;
+                    int64_t lo = (t == 3 || std::getenv("AMX_ENV_LEMIN")) ? le_min : 512;
+                    if (const char *ev = std::getenv("AMX_ENV_LEMIN2"))           // (measurements)
+                        if (t < 3) lo = std::max(128, std::atoi(ev)) / 128 * 128;
+                    int64_t Le = std::max<int64_t>(lo, (total / fit + 127) / 128 * 128);
+                    for (;; Le += 128) {
+                        int64_t ne = 0;
+                        for (int c = 0; c < n_chunks; c++) ne += (chunks[c].frames + Le - 1) / Le;
+                        if (ne <= fit || Le >= (int64_t)1 << 24) break;
+                    }
+                    p->Le_t[t] = (t == 3 || bandtab) ? (int)Le : p->Le_t[3];
                 }
-                p->Le = (int)Le;
+                p->Le = p->Le_t[3];
             }
         }
+        for (int t = 1; t <= 3; t++)
+            if (p->Le_t[t] == 0) p->Le_t[t] = p->Le;
     }
     int64_t loc = 0, outo = 0;
     p->spans.assign(n_tracks, SpanDev{});
@@ -748,20 +762,6 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         int64_t ns = (ch.n + p->L - 1) / p->L;
         ch.nseg = (int32_t)ns;
         add_blocks(p->blks, ch.seg0, (int32_t)ns, c);
-        if (p->mb) {   // envelope segments of the compressor (Le frames)
-            const int64_t ne = (ch.n + p->Le - 1) / p->Le;
-            p->eseg0.push_back((int)p->esegs.size());
-            p->neseg.push_back((int)ne);
-            for (int64_t k = 0; k < ne; k++) {
-                SegDev e{};
-                e.pos = k * p->Le;
-                e.chunk = c;
-                e.len = (int32_t)((ch.n - e.pos) < p->Le ? (ch.n - e.pos) : p->Le);
-                e.first = p->eseg0.back();
-                e.last = (k == ne - 1) ? 1 : 0;
-                p->esegs.push_back(e);
-            }
-        }
         for (int64_t k = 0; k < ns; k++) {
             SegDev s{};
             s.pos = k * p->L;
@@ -790,7 +790,43 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
                     (long long)std::max(loc, outo));
     }
     p->nloc = loc;
-    p->n_es = (int)p->esegs.size();
+    if (p->mb) {
+        // envelope segment tables (ChainDev::etab): per table the chunks cut into Le_t-frame
+        // segments; segment indices (SegDev::first, eseg0) are table-relative
+        int ld = 0;
+        for (int t = 3; t >= 1; t--) {
+            if (t < 3 && p->Le_t[t] == p->Le_t[3]) {
+                p->cd.etab[t] = p->cd.etab[3];
+                continue;
+            }
+            const int Le = p->Le_t[t];
+            const int es_off = (int)p->esegs.size(), ch_off = (int)p->eseg0.size();
+            for (int c = 0; c < n_chunks; c++) {
+                const int64_t n = p->chunks[c].n;
+                const int64_t ne = (n + Le - 1) / Le;
+                p->eseg0.push_back((int)p->esegs.size() - es_off);
+                p->neseg.push_back((int)ne);
+                for (int64_t k = 0; k < ne; k++) {
+                    SegDev e{};
+                    e.pos = k * Le;
+                    e.chunk = c;
+                    e.len = (int32_t)((n - e.pos) < Le ? (n - e.pos) : Le);
+                    e.first = p->eseg0.back();
+                    e.last = (k == ne - 1) ? 1 : 0;
+                    p->esegs.push_back(e);
+                }
+            }
+            const int n_es = (int)p->esegs.size() - es_off;
+            p->cd.etab[t].es_off = es_off;
+            p->cd.etab[t].n_es = n_es;
+            p->cd.etab[t].ch_off = ch_off;
+            p->cd.etab[t].Le = Le;
+            ld = std::max(ld, n_es);
+        }
+        p->cd.etab[0] = p->cd.etab[3];
+        p->cd.es_ld = ld;
+        p->n_es = ld;
+    }
     p->out_frames = outo;
     p->n_seg = (int)p->segs.size();
     // K-weighting segments per track span, on the measurement stream: output j of
@@ -1130,7 +1166,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         p->o_m = (size_t)align_up(off, (3 * nl + 2 * mpad) * 2) + mpad * 2;   // u16 r
         p->o_esv = (size_t)align_up(off, 3 * ne * 8);
         p->o_ee0 = (size_t)align_up(off, 3 * ne * 8);
-        p->o_eflags = (size_t)align_up(off, AMX_ENV_MAX_ROUNDS * (1 + AMX_ENV_NCTR) * 4);
+        p->o_eflags = (size_t)align_up(off, (AMX_ENV_BACT + 4) * 4);   // + band-activity words
         p->o_eact = (size_t)align_up(off, 3 * ne * 4);
         p->o_eprev = (size_t)align_up(off, 3 * ne * 4);
     }
@@ -1261,10 +1297,10 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
             HIPCHK(amx::launch_scan(p->scan_xo(), ex, sx, nullptr, wsp<double>(d_ws, p->o_ebx), st));
         break;
     case AMX_STAGE_XOVER:
-        if (p->mb) HIPCHK(amx::launch_xover2(l, p16, sx, bands, p->nloc));
+        if (p->mb) HIPCHK(amx::launch_xover2(l, p16, sx, bands, p->nloc, eflags + AMX_ENV_BACT));
         break;
     case AMX_STAGE_RMS:
-        if (p->mb) HIPCHK(amx::launch_rms(dl, bands, mframe));
+        if (p->mb) HIPCHK(amx::launch_rms(dl, bands, mframe, eflags + AMX_ENV_BACT));
         break;
     case AMX_STAGE_ENV:
         if (p->mb)
@@ -1278,7 +1314,8 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
         break;
     case AMX_STAGE_APPLY:
         if (p->mb)
-            HIPCHK(amx::launch_gain_overlay(dl, mframe, ck, bands, d_out, p->max_chunk_out, p->d_n1, eact));
+            HIPCHK(amx::launch_gain_overlay(dl, mframe, ck, bands, d_out, p->max_chunk_out, p->d_n1, eact,
+                                            eflags + AMX_ENV_BACT));
         break;
     }
     return AMX_OK;

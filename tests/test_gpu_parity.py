@@ -104,6 +104,26 @@ def test_compressor_fixup_paths(gpu, oracle_mod, warm, rounds, signal):
     _cmp(out, ref, "compressor warm=%d rounds=%d %s" % (warm, rounds, signal), exact_min=1.0, tol=0)
 
 
+@pytest.mark.parametrize("active", ["111", "110", "101", "010", "001", "000"])
+def test_compressor_active_bands(gpu, oracle_mod, active):
+    """Bands with no frame over their threshold (threshold 0 dBFS: no rms exceeds it) are
+    skipped by the envelope kernels, and the active ones (threshold -40 dBFS) run on the
+    segment table of their count (amx_dyn.hip env_bands, ChainDev::etab): bit-exact to
+    the oracle for every pattern of active bands."""
+    from amx import synth
+    fs = 48000
+    n = int(fs * 7.3)
+    x16 = oracle_mod.quantize(synth.music_like(n, fs, 2, seed=11, peak_dbfs=-2.0))
+    mb = dict(MB)
+    for k, name in zip(active, ("low", "mid", "high")):
+        mb[name + "_thresh"] = 0.0 if k == "0" else -40.0
+    settings = dict(VOCAL, lufs=-14.0, width=1.3, analog_character=40.0, **mb)
+    chunks = [(0, n // 3), (n // 3, n - n // 3)]
+    out, _ = _chunk_chain(x16, fs, settings, chunks)
+    ref = np.concatenate([oracle_mod.chunk(x16[s:s + m], fs, settings) for s, m in chunks])
+    _cmp(out, ref, "compressor active bands %s" % active, exact_min=1.0, tol=0)
+
+
 def test_mono_and_f32_quantise(gpu, oracle_mod):
     import torch
     from amx import synth
