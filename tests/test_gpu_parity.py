@@ -63,8 +63,9 @@ def test_golden_chunk_bitexact(gpu, path):
     (48000, C2, 7.3), (48000, C3, 7.3), (44100, dict(bass_boost=3.0, treble_boost=3.0), 5.0),
     (96000, C3, 4.1), (48000, dict(VOCAL, analog_character=100.0, width=0.0), 3.0),
     (44100, dict(bass_boost=-2.0, treble_boost=-4.0, mid_cut=3.0, presence_boost=-2.0, **MB), 3.3),
+    (192000, C3, 1.3), (32000, C3, 6.1),
 ])
-@pytest.mark.parametrize("seg_frames", [256, 1000])
+@pytest.mark.parametrize("seg_frames", [128, 256, 1000])
 def test_multichunk_chain_vs_oracle(gpu, oracle_mod, fs, settings, seconds, seg_frames):
     from amx import synth
     n = int(fs * seconds)
@@ -119,7 +120,7 @@ def test_compressor_active_bands(gpu, oracle_mod, active):
         mb[name + "_thresh"] = 0.0 if k == "0" else -40.0
     settings = dict(VOCAL, lufs=-14.0, width=1.3, analog_character=40.0, **mb)
     chunks = [(0, n // 3), (n // 3, n - n // 3)]
-    out, _ = _chunk_chain(x16, fs, settings, chunks)
+    out, _ = _chunk_chain(x16, fs, settings, chunks, seg_frames=128)
     ref = np.concatenate([oracle_mod.chunk(x16[s:s + m], fs, settings) for s, m in chunks])
     _cmp(out, ref, "compressor active bands %s" % active, exact_min=1.0, tol=0)
 
