@@ -16,11 +16,11 @@
 //     earlier (the trajectories of this recurrence coincide after clamp events, so
 //     the warm-up usually lands exactly on the true state) and writes its start guess
 //     s_j, end state e_j, an over-threshold flag and a checkpoint every 16 frames;
-//   k_envfix rounds: segment j takes its true start from the end of the nearest
-//     earlier segment that has any over-threshold frame (below-threshold frames hold
-//     the state: m = 0 makes both steps the identity), and if it differs from s_j the
-//     wave re-runs the segment from it, rewriting checkpoints until the new state
-//     meets a stored one (the trajectories have coincided);
+//   k_envheads / k_envchain: segment j's true start is the end of segment j - 1 (0 at
+//     a chunk's start).  A segment whose stored start differs while its predecessor's
+//     holds heads a chain; one wave per chain re-runs the head from the true start,
+//     rewriting checkpoints until the new state meets a stored one (the trajectories
+//     have coincided), and walks on while the next segment's start is now wrong;
 //   k_envseq: a final in-order walk per (chunk, band) fixes whatever is still
 //     inconsistent, so the result is exact whatever the signal;
 //   k_gain_overlay: every frame's attenuation from the checkpoint before it, the
@@ -391,9 +391,6 @@ __device__ __forceinline__ int env_slot_band(const EnvBands &e, int s) {
     return __builtin_ctz(m | 8);
 }
 
-#ifndef AMX_ENV_FIXBANDS
-#define AMX_ENV_FIXBANDS 1   // (measurement variant 0: the fix-up ignores the band flags; 3-band table only)
-#endif
 #define AMX_ENV_TF 16
 #define AMX_ENV_MP 18      // m tile pitch in doubles (144 B)
 #define AMX_ENV_PF 8       // r tiles in flight
@@ -524,6 +521,7 @@ __global__ void __launch_bounds__(64 * AMX_ENV_WG) k_env0(const ChainDev *__rest
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < AMX_ENV_MAX_ROUNDS) flags[threadIdx.x] = 0;
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) {
         for (int k = lane; k < AMX_ENV_MAX_ROUNDS * AMX_ENV_NCTR; k += 64) flags[AMX_ENV_MAX_ROUNDS + k] = 0;
+        if (lane < 2) flags[AMX_ENV_LIST + lane] = 0;   // the chain list's length, k_envseq's flag
     }
     const EnvBands eb = env_bands(flags + AMX_ENV_BACT);
     if ((int)blockIdx.y >= eb.nb) return;                 // workgroup-uniform
@@ -591,128 +589,126 @@ __device__ __forceinline__ double env_fix_segment(const ChainDev &cd, const uint
     return env_rerun_wave<RCP>(cd, mrow, mt, ckr, pos, pos + len, ns, old_end);
 }
 
-// ------------------------------------------------ rounds: parallel fix-up
-// A wave per 64 consecutive segments of one band, updating s and e in place.
-// Segment j's true start is the end of prev[j], the nearest earlier segment of its
-// chunk with an over-threshold frame (below-threshold frames hold the state), or 0.
-// Round 0 derives prev[j] (ballot of the act flags within the wave, a wave-uniform
-// look-back over earlier waves for the lanes of the wave's first chunk that have
-// none) and stores it for the later rounds and k_envseq.  Lanes whose start differs
-// from their stored start s_j are fixed in index order by the whole wave; a fixed
-// segment's new end is handed at once to the lanes of the same wave that start from
-// it, so a run of dependent segments within one wave settles in one round.  flags[r]
-// records that round r fixed anything: a round (and k_envseq) after a round that
-// fixed nothing has nothing to do and returns at once.  Waves of one round may read
-// a predecessor's end before or after another wave rewrites it; either is an end
-// of its segment from some start, and k_envseq checks every link at the end.
+// ------------------------------------------------ parallel fix-up: chains
+// The link j - 1 -> j holds when segment j's stored start equals segment j - 1's stored
+// end (a chunk's first segment: 0, where every chunk starts).  k_env0's speculation
+// breaks few links.  A segment whose link is broken while its predecessor's link holds
+// is a chain head: its predecessor is exact, so its true start is known.  k_envheads
+// marks the heads and lists them (one atomicAdd per wave); k_envchain gives each head
+// its own wave (a fixed grid looping over the list).  The wave re-runs the head from
+// the true start (env_fix_segment: an inactive segment only takes the held state) and
+// walks on to the next segment while that one's stored start differs from the new
+// end.  It stops at the chunk's end, at a link that holds, or at another head, which
+// has its own wave.  A head's wave may have read its predecessor's end before another
+// chain rewrote it; the walker that reaches such a head with a changed end sets a flag,
+// and k_envseq then checks every link in order.  Independent chains run in parallel
+// (round 4's k_envfix re-ran all of a 64-segment wave's segments in turn).
+#define AMX_ENV_CHAIN_WAVES 2048    // k_envchain grid (waves loop over the head list)
 template <bool RCP>
-__global__ void __launch_bounds__(64) k_envfix(const ChainDev *__restrict__ cdp,
-                                               const ChunkDev *__restrict__ chunks,
-                                               const SegDev *__restrict__ es, int n_es,
-                                               const uint16_t *__restrict__ mm,
-                                               const double *__restrict__ tabs,
-                                               double *__restrict__ ck, double *sv, double *ev,
-                                               const int *__restrict__ act,
-                                               int *__restrict__ prev, int64_t nloc,
-                                               int *flags, int round, int fix) {
-    if (round > 0 && __builtin_amdgcn_readfirstlane(flags[round - 1]) == 0) return;
+__global__ void __launch_bounds__(64) k_envheads(const ChainDev *__restrict__ cdp,
+                                                 const SegDev *__restrict__ es, int n_es,
+                                                 const double *__restrict__ sv,
+                                                 const double *__restrict__ ev,
+                                                 int *flags, int *__restrict__ list,
+                                                 int *__restrict__ hmark) {
     const ChainDev &cd = *cdp;
-    const int b = blockIdx.y;
-#if AMX_ENV_FIXBANDS
+    const int b = blockIdx.y, lane = threadIdx.x;
     const EnvBands eb = env_bands(flags + AMX_ENV_BACT);
     if (!eb.act(b)) return;
-    const int tb = eb.nb;
-#else
-    const int tb = 3;
-#endif
-    es += cd.etab[tb].es_off;
-    n_es = cd.etab[tb].n_es;
+    es += cd.etab[eb.nb].es_off;
+    n_es = cd.etab[eb.nb].n_es;
     if ((int)blockIdx.x * 64 >= n_es) return;
-    // per-round counters after the round flags: segments re-run, the most re-runs in
-    // one wave (its chain of dependent fixes), waves with work, look-back steps
-    int *ctr = flags + AMX_ENV_MAX_ROUNDS + round * AMX_ENV_NCTR;
-    const int lane = threadIdx.x;
-    const int w0 = blockIdx.x * 64;
-    const int j = w0 + lane;
-    const bool valid = j < n_es;
+    const int j = blockIdx.x * 64 + lane;
     const int64_t bo = (int64_t)b * cd.es_ld;
-    const int jc = valid ? j : n_es - 1;
-    const SegDev sg = es[jc];
-    const bool a = valid && act[bo + jc] != 0;
-    int p;
-    if (round == 0) {
-        const unsigned long long am = __ballot(a);
-        const unsigned long long below = lane ? am & (~0ull >> (64 - lane)) : 0ull;
-        p = below ? w0 + 63 - __clzll((long long)below) : -1;
-        if (p < sg.first) p = -1;
-        const bool lb = valid && p < 0 && sg.first < w0;
-        if (__ballot(lb)) {
-            // the wave's first chunk: last active segment before w0 (uniform)
-            const int first0 = __shfl(sg.first, 0);
-            int last = -1, steps = 0;
-            for (int base = w0 - 64; base + 63 >= first0; base -= 64) {
-                const int jj = base + lane;
-                steps++;
-                const unsigned long long mk = __ballot(jj >= first0 && act[bo + jj] != 0);
-                if (mk) { last = base + 63 - __clzll((long long)mk); break; }
+    bool head = false;
+    if (j < n_es) {
+        const int first = es[j].first;
+        const bool need = !(sv[bo + j] == (j == first ? 0.0 : ev[bo + j - 1]));
+        bool needp = false;
+        if (j > first) needp = !(sv[bo + j - 1] == (j - 1 == first ? 0.0 : ev[bo + j - 2]));
+        head = need && !needp;
+        hmark[bo + j] = head ? 1 : 0;
+    }
+    const unsigned long long hm = __ballot(head);
+    if (hm) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(flags + AMX_ENV_LIST, __popcll(hm));
+        base = __shfl(base, 0);
+        const unsigned long long below = lane ? hm & (~0ull >> (64 - lane)) : 0ull;
+        if (head) list[base + __popcll(below)] = (int)(bo + j);
+    }
+}
+
+template <bool RCP>
+__global__ void __launch_bounds__(64) k_envchain(const ChainDev *__restrict__ cdp,
+                                                 const ChunkDev *__restrict__ chunks,
+                                                 const SegDev *__restrict__ es,
+                                                 const uint16_t *__restrict__ mm,
+                                                 const double *__restrict__ tabs,
+                                                 double *__restrict__ ck, double *sv, double *ev,
+                                                 const int *__restrict__ act, int *flags,
+                                                 const int *__restrict__ list,
+                                                 const int *__restrict__ hmark, int64_t nloc) {
+    const int count = __builtin_amdgcn_readfirstlane(flags[AMX_ENV_LIST]);
+    if ((int)blockIdx.x >= count) return;
+    const ChainDev &cd = *cdp;
+    const int lane = threadIdx.x;
+    const EnvBands eb = env_bands(flags + AMX_ENV_BACT);
+    const SegDev *et = es + cd.etab[eb.nb].es_off;
+    const int ld = cd.es_ld;
+    // per-round counters after the round flags (amx_env_counters): segments re-run,
+    // the longest walk, chains, 0
+    int *ctr = flags + AMX_ENV_MAX_ROUNDS;
+    int runs = 0, longest = 0, chains = 0;
+    bool stale = false;
+    for (int i = blockIdx.x; i < count; i += gridDim.x) {
+        const int k = __builtin_amdgcn_readfirstlane(list[i]);
+        const int b = k / ld, j = k - b * ld;
+        const int64_t bo = (int64_t)b * ld;
+        const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
+        SegDev sg = et[j];
+        double state = j == sg.first ? 0.0 : ev[bo + j - 1];
+        int cur = j, walked = 0;
+        while (true) {
+            const bool a = act[bo + cur] != 0;
+            const double old_end = ev[bo + cur];
+            const int64_t ro = b * nloc + chunks[sg.chunk].loc_off;
+            const double r = env_fix_segment<RCP>(cd, mm + ro, mt, ck + ro / AMX_ENV_TF_, sg.pos, sg.len, a,
+                                                  state, old_end);
+            walked++;
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) {
+                sv[bo + cur] = state;
+                ev[bo + cur] = r;
             }
-            if (lb) p = last;
-            if (lane == 0) atomicMax(ctr + 3, steps);
+            if (sg.last) break;                          // the chunk's end
+            const int nx = cur + 1;
+            if (hmark[bo + nx]) {                        // another chain's head
+                stale = stale || !(r == old_end);
+                break;
+            }
+            if (sv[bo + nx] == r) break;                 // the link holds: the rest stands
+            state = r;
+            cur = nx;
+            sg = et[cur];
         }
-        if (!valid) p = -1;
-        if (valid) prev[bo + j] = p;
-    } else {
-        p = valid ? prev[bo + j] : -1;
+        runs += walked;
+        longest = walked > longest ? walked : longest;
+        chains++;
     }
-    if (!fix) return;
-    double ns = 0.0, os = 0.0, en = 0.0;
-    bool need = false;
-    if (valid) {
-        ns = p >= 0 ? ev[bo + p] : 0.0;
-        os = sv[bo + j];
-        en = ev[bo + j];
-        need = !(ns == os);
-    }
-    unsigned long long work = __ballot(need);
-    if (!work) return;
-    if (lane == 0) flags[round] = 1;
-    int nfix = 0;
-    const int64_t loc = chunks[sg.chunk].loc_off;
-    bool fixed = false;
-    while (work) {
-        const int w = __ffsll((long long)work) - 1;
-        const int64_t posw = __shfl(sg.pos, w), locw = __shfl(loc, w);
-        const int lenw = __shfl(sg.len, w);
-        const bool aw = __shfl((int)a, w) != 0;
-        const double nsw = __shfl(ns, w), enw = __shfl(en, w);
-        const int64_t ro = b * nloc + locw;
-        const double r = env_fix_segment<RCP>(cd, mm + ro, tabs + (int64_t)b * 3 * AMX_TAB,
-                                              ck + ro / AMX_ENV_TF_, posw, lenw, aw, nsw, enw);
-        if (lane == w) { en = r; fixed = true; }
-        nfix++;
-        // lanes starting from segment w0 + w take its new end now
-        if (lane > w && valid && p == w0 + w) {
-            ns = r;
-            need = !(ns == os);
-        }
-        work = __ballot(need) & (w == 63 ? 0ull : ~0ull << (w + 1));
-    }
-    if (fixed) {
-        ev[bo + j] = en;
-        sv[bo + j] = ns;
-    }
-    if (lane == 0) {                      // diagnostics (amx_env_counters)
-        atomicAdd(ctr + 0, nfix);
-        atomicMax(ctr + 1, nfix);
-        atomicAdd(ctr + 2, 1);
+    if (lane == 0) {
+        if (stale) flags[AMX_ENV_LIST + 1] = 1;          // k_envseq must check the links
+        atomicAdd(ctr + 0, runs);
+        atomicMax(ctr + 1, longest);
+        atomicAdd(ctr + 2, chains);
     }
 }
 
 // --------------------------------------- final in-order walk (exactness net)
 // One wave per (chunk, band): find the first segment whose start disagrees with
 // its predecessor's end (64 at a time) and fix it with the whole wave, continue
-// after it.  Nothing to do when the last round fixed nothing (flags[fl] == 0; fl < 0:
-// no rounds ran, always walk).
+// after it.  Nothing to do when no chain walker reported a head it may have raced
+// (flags[fl] == 0; fl < 0: no fix-up ran, always walk).
 template <bool RCP>
 __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
                                                const ChunkDev *__restrict__ chunks,
@@ -723,25 +719,20 @@ __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
                                                const double *__restrict__ tabs,
                                                double *__restrict__ ck,
                                                double *__restrict__ sv, double *__restrict__ ev,
-                                               const int *__restrict__ act,
-                                               const int *__restrict__ prev, int64_t nloc,
+                                               const int *__restrict__ act, int64_t nloc,
                                                const int *__restrict__ flags, int fl) {
     if (fl >= 0 && __builtin_amdgcn_readfirstlane(flags[fl]) == 0) return;
     const ChainDev &cd = *cdp;
     const int c = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
-#if AMX_ENV_FIXBANDS
     const EnvBands eb = env_bands(flags + AMX_ENV_BACT);
     if (!eb.act(b)) return;
     const int tb = eb.nb;
-#else
-    const int tb = 3;
-#endif
     es += cd.etab[tb].es_off;
     const int s0 = eseg0[cd.etab[tb].ch_off + c], s1 = s0 + neseg[cd.etab[tb].ch_off + c];
     const ChunkDev ch = chunks[c];
     const int64_t ld = cd.es_ld;
     double *S = sv + (int64_t)b * ld, *E = ev + (int64_t)b * ld;
-    const int *A = act + (int64_t)b * ld, *Pv = prev + (int64_t)b * ld;
+    const int *A = act + (int64_t)b * ld;
     const int64_t ro = b * nloc + ch.loc_off;
     int cur = s0;
     while (cur < s1) {
@@ -749,18 +740,13 @@ __global__ void __launch_bounds__(64) k_envseq(const ChainDev *__restrict__ cdp,
         for (int base = cur; base < s1; base += 64) {
             const int j = base + lane;
             bool bad = false;
-            if (j < s1) {
-                const int p = Pv[j];
-                const double ns = p >= 0 ? E[p] : 0.0;
-                bad = !(ns == S[j]);
-            }
+            if (j < s1) bad = !((j == s0 ? 0.0 : E[j - 1]) == S[j]);
             const unsigned long long mk = __ballot(bad);
             if (mk) { found = base + __ffsll((long long)mk) - 1; break; }
         }
         if (found >= s1) break;
         const SegDev sg = es[found];
-        const int p = Pv[found];
-        const double ns = p >= 0 ? E[p] : 0.0;
+        const double ns = found == s0 ? 0.0 : E[found - 1];
         const double r = env_fix_segment<RCP>(cd, mm + ro, tabs + (int64_t)b * 3 * AMX_TAB,
                                               ck + ro / AMX_ENV_TF_, sg.pos, sg.len, A[found] != 0,
                                               ns, E[found]);
@@ -963,11 +949,10 @@ hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m, int
     return hipGetLastError();
 }
 
-// part 0: the speculation (k_env0); part 1: the parallel fix-up rounds (k_envfix)
+// part 0: the speculation (k_env0); part 1: the parallel fix-up (k_envheads + k_envchain)
 template <bool RCP>
 static void env_launch_t(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,
-                         int *act, int *prev, int *flags, int rounds, int part) {
-    const dim3 gw((unsigned)((d.n_es + 63) / 64), 3);
+                         int *act, int *list, int *hmark, int *flags, int rounds, int part) {
     if (part == 0) {
         const int wg = d.env_wg >= 1 && d.env_wg <= AMX_ENV_WG ? d.env_wg : 1;
         const dim3 g0((unsigned)((d.n_es + 64 * wg - 1) / (64 * wg)), 3);
@@ -975,33 +960,35 @@ static void env_launch_t(const DynLaunch &d, const uint16_t *m, double *ck, doub
                            d.chunks, d.es, d.n_es, m, d.tabs, ck, sv, ev, act, d.nloc, d.warm, flags);
         return;
     }
-    // rounds == 0: only prev[] (everything is left to k_envseq)
-    for (int k = 0; k < (rounds > 0 ? rounds : 1); k++)
-        hipLaunchKernelGGL(k_envfix<RCP>, gw, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es, m,
-                           d.tabs, ck, sv, ev, act, prev, d.nloc, flags, k, rounds > 0 ? 1 : 0);
+    if (rounds <= 0) return;                             // everything is left to k_envseq
+    hipLaunchKernelGGL(k_envheads<RCP>, dim3((unsigned)((d.n_es + 63) / 64), 3), dim3(64), 0, d.st, d.cd, d.es,
+                       d.n_es, sv, ev, flags, list, hmark);
+    hipLaunchKernelGGL(k_envchain<RCP>, dim3(AMX_ENV_CHAIN_WAVES), dim3(64), 0, d.st, d.cd, d.chunks, d.es, m,
+                       d.tabs, ck, sv, ev, act, flags, list, hmark, d.nloc);
 }
 
 hipError_t launch_env(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,
-                      int *act, int *prev, int *flags, int rounds, int part) {
+                      int *act, int *list, int *hmark, int *flags, int rounds, int part) {
     if (d.n_es <= 0) return hipSuccess;
     if (d.warm % (AMX_ENV_TF * AMX_ENV_PF) || d.Le % (AMX_ENV_TF * AMX_ENV_PF))
         return hipErrorInvalidValue;
     if (rounds < 0 || rounds > AMX_ENV_MAX_ROUNDS) return hipErrorInvalidValue;
-    if (d.rcp) env_launch_t<true>(d, m, ck, sv, ev, act, prev, flags, rounds, part);
-    else env_launch_t<false>(d, m, ck, sv, ev, act, prev, flags, rounds, part);
+    if (d.rcp) env_launch_t<true>(d, m, ck, sv, ev, act, list, hmark, flags, rounds, part);
+    else env_launch_t<false>(d, m, ck, sv, ev, act, list, hmark, flags, rounds, part);
     return hipGetLastError();
 }
 
 hipError_t launch_envseq(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,
-                         const int *act, const int *prev, const int *flags, int rounds) {
+                         const int *act, const int *flags, int rounds) {
     if (d.n_es <= 0) return hipSuccess;
     const dim3 gr((unsigned)d.n_chunks, 3);
+    const int fl = rounds > 0 ? AMX_ENV_LIST + 1 : -1;
     if (d.rcp)
         hipLaunchKernelGGL(k_envseq<true>, gr, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es,
-                           d.eseg0, d.neseg, m, d.tabs, ck, sv, ev, act, prev, d.nloc, flags, rounds - 1);
+                           d.eseg0, d.neseg, m, d.tabs, ck, sv, ev, act, d.nloc, flags, fl);
     else
         hipLaunchKernelGGL(k_envseq<false>, gr, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es,
-                           d.eseg0, d.neseg, m, d.tabs, ck, sv, ev, act, prev, d.nloc, flags, rounds - 1);
+                           d.eseg0, d.neseg, m, d.tabs, ck, sv, ev, act, d.nloc, flags, fl);
     return hipGetLastError();
 }
 
