@@ -216,13 +216,14 @@ class MasteringJob:
     def env_counters(self):
         """Compressor fix-up diagnostics of the last step (amx_env_counters): segments
         re-run by the chain walkers, the longest walk (segments re-run one after
-        another by one wave), chains.  Synchronous."""
+        another by one wave), chains, and the segments of the optimistic parallel
+        pass before them.  Synchronous."""
         import ctypes
         n = 16 * 4
         buf = (ctypes.c_int32 * n)()
         capi.check(capi.load().amx_env_counters(self.plan.h, capi.ptr(self.ws), buf, n), "amx_env_counters")
-        rows = [list(buf[4 * r:4 * r + 3]) for r in range(16)]
-        keys = ("reruns", "max_chain", "chains")
+        rows = [list(buf[4 * r:4 * r + 4]) for r in range(16)]
+        keys = ("reruns", "max_chain", "chains", "wide")
         return [dict(zip(keys, r)) for r in rows if any(r)]
 
     # --------------------------------------------- loudnorm dynamic mode (192 kHz)

@@ -521,7 +521,7 @@ __global__ void __launch_bounds__(64 * AMX_ENV_WG) k_env0(const ChainDev *__rest
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < AMX_ENV_MAX_ROUNDS) flags[threadIdx.x] = 0;
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) {
         for (int k = lane; k < AMX_ENV_MAX_ROUNDS * AMX_ENV_NCTR; k += 64) flags[AMX_ENV_MAX_ROUNDS + k] = 0;
-        if (lane < 2) flags[AMX_ENV_LIST + lane] = 0;   // the chain list's length, k_envseq's flag
+        if (lane < 3) flags[AMX_ENV_LIST + lane] = 0;   // the two lists' lengths, k_envseq's flag
     }
     const EnvBands eb = env_bands(flags + AMX_ENV_BACT);
     if ((int)blockIdx.y >= eb.nb) return;                 // workgroup-uniform
@@ -598,12 +598,109 @@ __device__ __forceinline__ double env_fix_segment(const ChainDev &cd, const uint
 // its own wave (a fixed grid looping over the list).  The wave re-runs the head from
 // the true start (env_fix_segment: an inactive segment only takes the held state) and
 // walks on to the next segment while that one's stored start differs from the new
-// end.  It stops at the chunk's end, at a link that holds, or at another head, which
-// has its own wave.  A head's wave may have read its predecessor's end before another
+// end (runs of inactive segments, which hold the state, 64 at a time).  It stops at
+// the chunk's end, at a link that holds, or at another head, which has its own wave.  A head's wave may have read its predecessor's end before another
 // chain rewrote it; the walker that reaches such a head with a changed end sets a flag,
 // and k_envseq then checks every link in order.  Independent chains run in parallel
 // (round 4's k_envfix re-ran all of a 64-segment wave's segments in turn).
+// Before the chains, one optimistic parallel pass (k_envneed + k_envwide): every
+// segment whose start differs from the end of its nearest earlier active segment
+// (below-threshold segments hold the state, so that end is its true start) is listed
+// and re-run at once by its own wave from that end as it stands.  Most such re-runs are
+// independent (C4: 254 in a step, at most 2 in a row), and a re-run whose trajectory
+// meets the old one keeps the old end exact; the chains then fix only the links that
+// are still broken.
+template <bool RCP>
+__global__ void __launch_bounds__(64) k_envneed(const ChainDev *__restrict__ cdp,
+                                                const SegDev *__restrict__ es, int n_es,
+                                                const double *__restrict__ sv,
+                                                const double *__restrict__ ev,
+                                                const int *__restrict__ act, int *flags,
+                                                int *__restrict__ prev, int *__restrict__ list) {
+    const ChainDev &cd = *cdp;
+    const int b = blockIdx.y, lane = threadIdx.x;
+    const EnvBands eb = env_bands(flags + AMX_ENV_BACT);
+    if (!eb.act(b)) return;
+    es += cd.etab[eb.nb].es_off;
+    n_es = cd.etab[eb.nb].n_es;
+    const int w0 = blockIdx.x * 64;
+    if (w0 >= n_es) return;
+    const int j = w0 + lane;
+    const bool valid = j < n_es;
+    const int64_t bo = (int64_t)b * cd.es_ld;
+    const SegDev sg = es[valid ? j : n_es - 1];
+    const bool a = valid && act[bo + j] != 0;
+    // p: the nearest earlier active segment of the chunk (a ballot in the wave, then a
+    // wave-uniform look-back over earlier segments for the lanes that have none here)
+    const unsigned long long am = __ballot(a);
+    const unsigned long long below = lane ? am & (~0ull >> (64 - lane)) : 0ull;
+    int p = below ? w0 + 63 - __clzll((long long)below) : -1;
+    if (p < sg.first) p = -1;
+    const bool lb = valid && p < 0 && sg.first < w0;
+    if (__ballot(lb)) {
+        const int first0 = __shfl(sg.first, 0);
+        int last = -1;
+        for (int base = w0 - 64; base + 63 >= first0; base -= 64) {
+            const int jj = base + lane;
+            const unsigned long long mk = __ballot(jj >= first0 && act[bo + jj] != 0);
+            if (mk) { last = base + 63 - __clzll((long long)mk); break; }
+        }
+        if (lb) p = last;
+    }
+    bool need = false;
+    if (valid) {
+        prev[bo + j] = p;
+        need = !((p >= 0 ? ev[bo + p] : 0.0) == sv[bo + j]);
+    }
+    const unsigned long long nm = __ballot(need);
+    if (nm) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(flags + AMX_ENV_LIST, __popcll(nm));
+        base = __shfl(base, 0);
+        const unsigned long long lt = lane ? ~0ull >> (64 - lane) : 0ull;
+        if (need) list[base + __popcll(nm & lt)] = (int)(bo + j);
+    }
+}
+
+template <bool RCP>
+__global__ void __launch_bounds__(64) k_envwide(const ChainDev *__restrict__ cdp,
+                                                const ChunkDev *__restrict__ chunks,
+                                                const SegDev *__restrict__ es,
+                                                const uint16_t *__restrict__ mm,
+                                                const double *__restrict__ tabs,
+                                                double *__restrict__ ck, double *sv, double *ev,
+                                                const int *__restrict__ act, int *flags,
+                                                const int *__restrict__ prev,
+                                                const int *__restrict__ list, int64_t nloc) {
+    const int count = __builtin_amdgcn_readfirstlane(flags[AMX_ENV_LIST]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) flags[AMX_ENV_MAX_ROUNDS + 3] = count;   // (amx_env_counters)
+    if ((int)blockIdx.x >= count) return;
+    const ChainDev &cd = *cdp;
+    const int lane = threadIdx.x;
+    const EnvBands eb = env_bands(flags + AMX_ENV_BACT);
+    const SegDev *et = es + cd.etab[eb.nb].es_off;
+    const int ld = cd.es_ld;
+    for (int i = blockIdx.x; i < count; i += gridDim.x) {
+        const int k = __builtin_amdgcn_readfirstlane(list[i]);
+        const int b = k / ld, j = k - b * ld;
+        const int64_t bo = (int64_t)b * ld;
+        const SegDev sg = et[j];
+        const int p = prev[bo + j];
+        const double ns = p >= 0 ? ev[bo + p] : 0.0;
+        const int64_t ro = b * nloc + chunks[sg.chunk].loc_off;
+        const double r = env_fix_segment<RCP>(cd, mm + ro, tabs + (int64_t)b * 3 * AMX_TAB, ck + ro / AMX_ENV_TF_,
+                                              sg.pos, sg.len, act[bo + j] != 0, ns, ev[bo + j]);
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+            sv[bo + j] = ns;
+            ev[bo + j] = r;
+        }
+    }
+}
+
+#ifndef AMX_ENV_CHAIN_WAVES
 #define AMX_ENV_CHAIN_WAVES 2048    // k_envchain grid (waves loop over the head list)
+#endif
 template <bool RCP>
 __global__ void __launch_bounds__(64) k_envheads(const ChainDev *__restrict__ cdp,
                                                  const SegDev *__restrict__ es, int n_es,
@@ -632,7 +729,7 @@ __global__ void __launch_bounds__(64) k_envheads(const ChainDev *__restrict__ cd
     const unsigned long long hm = __ballot(head);
     if (hm) {
         int base = 0;
-        if (lane == 0) base = atomicAdd(flags + AMX_ENV_LIST, __popcll(hm));
+        if (lane == 0) base = atomicAdd(flags + AMX_ENV_LIST + 1, __popcll(hm));
         base = __shfl(base, 0);
         const unsigned long long below = lane ? hm & (~0ull >> (64 - lane)) : 0ull;
         if (head) list[base + __popcll(below)] = (int)(bo + j);
@@ -649,7 +746,7 @@ __global__ void __launch_bounds__(64) k_envchain(const ChainDev *__restrict__ cd
                                                  const int *__restrict__ act, int *flags,
                                                  const int *__restrict__ list,
                                                  const int *__restrict__ hmark, int64_t nloc) {
-    const int count = __builtin_amdgcn_readfirstlane(flags[AMX_ENV_LIST]);
+    const int count = __builtin_amdgcn_readfirstlane(flags[AMX_ENV_LIST + 1]);
     if ((int)blockIdx.x >= count) return;
     const ChainDev &cd = *cdp;
     const int lane = threadIdx.x;
@@ -661,43 +758,84 @@ __global__ void __launch_bounds__(64) k_envchain(const ChainDev *__restrict__ cd
     int *ctr = flags + AMX_ENV_MAX_ROUNDS;
     int runs = 0, longest = 0, chains = 0;
     bool stale = false;
+    const int n_es = cd.etab[eb.nb].n_es;
     for (int i = blockIdx.x; i < count; i += gridDim.x) {
         const int k = __builtin_amdgcn_readfirstlane(list[i]);
         const int b = k / ld, j = k - b * ld;
         const int64_t bo = (int64_t)b * ld;
         const double *mt = tabs + (int64_t)b * 3 * AMX_TAB;
         SegDev sg = et[j];
+        const int64_t ro = b * nloc + chunks[sg.chunk].loc_off;
+        double *ckr = ck + ro / AMX_ENV_TF_;
         double state = j == sg.first ? 0.0 : ev[bo + j - 1];
         int cur = j, walked = 0;
-        while (true) {
+        bool done = false;
+        while (!done) {
             const bool a = act[bo + cur] != 0;
-            const double old_end = ev[bo + cur];
-            const int64_t ro = b * nloc + chunks[sg.chunk].loc_off;
-            const double r = env_fix_segment<RCP>(cd, mm + ro, mt, ck + ro / AMX_ENV_TF_, sg.pos, sg.len, a,
-                                                  state, old_end);
+            double old_end = ev[bo + cur];
+            const double r = env_fix_segment<RCP>(cd, mm + ro, mt, ckr, sg.pos, sg.len, a, state, old_end);
             walked++;
             __builtin_amdgcn_wave_barrier();
             if (lane == 0) {
                 sv[bo + cur] = state;
                 ev[bo + cur] = r;
             }
-            if (sg.last) break;                          // the chunk's end
-            const int nx = cur + 1;
-            if (hmark[bo + nx]) {                        // another chain's head
-                stale = stale || !(r == old_end);
+            if (sg.last) break;                              // the chunk's end
+            // the segments after it, 64 at a time: inactive ones whose start is wrong
+            // take the held state r in bulk (their checkpoints too); the walk goes on at
+            // the first segment that is active, another chain's head, past the chunk,
+            // or already starts at r
+            int nx = cur + 1;
+            while (true) {
+                const int kk = nx + lane;
+                const bool inch = kk < n_es && et[kk < n_es ? kk : n_es - 1].first == sg.first;
+                bool hk = false, ak = false, st = true;
+                double svk = 0.0, evk = 0.0;
+                if (inch) {
+                    hk = hmark[bo + kk] != 0;
+                    ak = act[bo + kk] != 0;
+                    svk = sv[bo + kk];
+                    evk = ev[bo + kk];
+                    st = hk || ak || svk == r;
+                }
+                const unsigned long long mk = __ballot(st);
+                const int f = mk ? __ffsll((long long)mk) - 1 : 64;
+                if (f > 0) {
+                    const SegDev s0 = et[nx], s1 = et[nx + f - 1];
+                    const int64_t k0 = s0.pos / AMX_ENV_TF_, k1 = (s1.pos + s1.len + AMX_ENV_TF_ - 1) / AMX_ENV_TF_;
+                    for (int64_t q = k0 + lane; q < k1; q += 64) ckr[q] = r;
+                    if (lane < f) {
+                        sv[bo + kk] = r;
+                        ev[bo + kk] = r;
+                    }
+                    old_end = __shfl(evk, f - 1);            // the old end before the stop
+                    walked += f;
+                }
+                if (f == 64) {
+                    nx += 64;
+                    continue;
+                }
+                const bool ins = __shfl((int)inch, f) != 0, hs = __shfl((int)hk, f) != 0;
+                const double ss = __shfl(svk, f);
+                if (!ins) { done = true; break; }            // past the chunk
+                if (hs) {                                    // another chain's head
+                    stale = stale || !(r == old_end);
+                    done = true;
+                    break;
+                }
+                if (ss == r) { done = true; break; }         // the link holds: the rest stands
+                state = r;                                   // an active segment to re-run
+                cur = nx + f;
+                sg = et[cur];
                 break;
             }
-            if (sv[bo + nx] == r) break;                 // the link holds: the rest stands
-            state = r;
-            cur = nx;
-            sg = et[cur];
         }
         runs += walked;
         longest = walked > longest ? walked : longest;
         chains++;
     }
     if (lane == 0) {
-        if (stale) flags[AMX_ENV_LIST + 1] = 1;          // k_envseq must check the links
+        if (stale) flags[AMX_ENV_LIST + 2] = 1;          // k_envseq must check the links
         atomicAdd(ctr + 0, runs);
         atomicMax(ctr + 1, longest);
         atomicAdd(ctr + 2, chains);
@@ -952,7 +1090,8 @@ hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m, int
 // part 0: the speculation (k_env0); part 1: the parallel fix-up (k_envheads + k_envchain)
 template <bool RCP>
 static void env_launch_t(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,
-                         int *act, int *list, int *hmark, int *flags, int rounds, int part) {
+                         int *act, int *list, int *hmark, int *prev, int *list0, int *flags, int rounds,
+                         int part) {
     if (part == 0) {
         const int wg = d.env_wg >= 1 && d.env_wg <= AMX_ENV_WG ? d.env_wg : 1;
         const dim3 g0((unsigned)((d.n_es + 64 * wg - 1) / (64 * wg)), 3);
@@ -961,6 +1100,10 @@ static void env_launch_t(const DynLaunch &d, const uint16_t *m, double *ck, doub
         return;
     }
     if (rounds <= 0) return;                             // everything is left to k_envseq
+    const dim3 gs((unsigned)((d.n_es + 63) / 64), 3);
+    hipLaunchKernelGGL(k_envneed<RCP>, gs, dim3(64), 0, d.st, d.cd, d.es, d.n_es, sv, ev, act, flags, prev, list0);
+    hipLaunchKernelGGL(k_envwide<RCP>, dim3(AMX_ENV_CHAIN_WAVES), dim3(64), 0, d.st, d.cd, d.chunks, d.es, m,
+                       d.tabs, ck, sv, ev, act, flags, prev, list0, d.nloc);
     hipLaunchKernelGGL(k_envheads<RCP>, dim3((unsigned)((d.n_es + 63) / 64), 3), dim3(64), 0, d.st, d.cd, d.es,
                        d.n_es, sv, ev, flags, list, hmark);
     hipLaunchKernelGGL(k_envchain<RCP>, dim3(AMX_ENV_CHAIN_WAVES), dim3(64), 0, d.st, d.cd, d.chunks, d.es, m,
@@ -968,13 +1111,14 @@ static void env_launch_t(const DynLaunch &d, const uint16_t *m, double *ck, doub
 }
 
 hipError_t launch_env(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,
-                      int *act, int *list, int *hmark, int *flags, int rounds, int part) {
+                      int *act, int *list, int *hmark, int *prev, int *list0, int *flags, int rounds,
+                      int part) {
     if (d.n_es <= 0) return hipSuccess;
     if (d.warm % (AMX_ENV_TF * AMX_ENV_PF) || d.Le % (AMX_ENV_TF * AMX_ENV_PF))
         return hipErrorInvalidValue;
     if (rounds < 0 || rounds > AMX_ENV_MAX_ROUNDS) return hipErrorInvalidValue;
-    if (d.rcp) env_launch_t<true>(d, m, ck, sv, ev, act, list, hmark, flags, rounds, part);
-    else env_launch_t<false>(d, m, ck, sv, ev, act, list, hmark, flags, rounds, part);
+    if (d.rcp) env_launch_t<true>(d, m, ck, sv, ev, act, list, hmark, prev, list0, flags, rounds, part);
+    else env_launch_t<false>(d, m, ck, sv, ev, act, list, hmark, prev, list0, flags, rounds, part);
     return hipGetLastError();
 }
 
@@ -982,7 +1126,7 @@ hipError_t launch_envseq(const DynLaunch &d, const uint16_t *m, double *ck, doub
                          const int *act, const int *flags, int rounds) {
     if (d.n_es <= 0) return hipSuccess;
     const dim3 gr((unsigned)d.n_chunks, 3);
-    const int fl = rounds > 0 ? AMX_ENV_LIST + 1 : -1;
+    const int fl = rounds > 0 ? AMX_ENV_LIST + 2 : -1;
     if (d.rcp)
         hipLaunchKernelGGL(k_envseq<true>, gr, dim3(64), 0, d.st, d.cd, d.chunks, d.es, d.n_es,
                            d.eseg0, d.neseg, m, d.tabs, ck, sv, ev, act, d.nloc, flags, fl);

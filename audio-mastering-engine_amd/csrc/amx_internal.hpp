@@ -19,7 +19,7 @@
 #define AMX_ENV_MAX_ROUNDS 16  // envelope fix-up flag words (k_env0 clears them)
 #define AMX_ENV_NCTR 4         // fix-up diagnostic counters per round (after the flags; k_envchain)
 #define AMX_ENV_BACT (AMX_ENV_MAX_ROUNDS * (1 + AMX_ENV_NCTR))  // band-activity words after the counters
-#define AMX_ENV_LIST (AMX_ENV_BACT + 4)  // chain-head list length, then k_envseq's "links may be stale" flag
+#define AMX_ENV_LIST (AMX_ENV_BACT + 4)  // re-run list length, chain-head list length, k_envseq's flag
 #define AMX_EQC 64        // compact EQ coefficient block (see ChainDev::eqc)
 #define AMX_MEAS_RATE 192000  // loudnorm pass 1 measures at 192 kHz (af_loudnorm dynamic mode)
 #ifndef AMX_PCM_U8        // input PCM formats (include/amx.h amx_pcm_to_s16)
@@ -193,7 +193,8 @@ hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m, int
 hipError_t launch_pcm_to_s16(const void *raw, int64_t frames, int channels, int fmt, int16_t *out,
                              hipStream_t st);
 hipError_t launch_env(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,
-                      int *act, int *list, int *hmark, int *flags, int rounds, int part);
+                      int *act, int *list, int *hmark, int *prev, int *list0, int *flags, int rounds,
+                      int part);
 hipError_t launch_envseq(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,
                          const int *act, const int *flags, int rounds);
 hipError_t launch_gain_overlay(const DynLaunch &d, const uint16_t *m, const double *ck,

@@ -350,7 +350,7 @@ struct amx_plan {
     // workspace offsets
     size_t ws_bytes = 0;
     size_t o_a16, o_e, o_s, o_p16, o_ex, o_sx, o_bands, o_r, o_m, o_gain, o_esv, o_ee0, o_eflags, o_eact,
-        o_ehead, o_elist;
+        o_ehead, o_elist, o_eprev, o_elist0;
     size_t o_ekw, o_skw, o_parts, o_phop, o_eterms = 0;
     size_t o_eb, o_ebx, o_ebk, o_pk, o_dup = 0;
     amx::ScanPlan scan_eq() const { return {D, n_blk, lev_eq, d_blks, d_M, d_Mp}; }
@@ -1166,10 +1166,12 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         p->o_m = (size_t)align_up(off, (3 * nl + 2 * mpad) * 2) + mpad * 2;   // u16 r
         p->o_esv = (size_t)align_up(off, 3 * ne * 8);
         p->o_ee0 = (size_t)align_up(off, 3 * ne * 8);
-        p->o_eflags = (size_t)align_up(off, (AMX_ENV_LIST + 2) * 4);   // + band words, chain list length, flag
+        p->o_eflags = (size_t)align_up(off, (AMX_ENV_LIST + 3) * 4);   // + band words, list lengths, flag
         p->o_eact = (size_t)align_up(off, 3 * ne * 4);
         p->o_ehead = (size_t)align_up(off, 3 * ne * 4);   // chain-head marks
         p->o_elist = (size_t)align_up(off, 3 * ne * 4);   // chain-head list
+        p->o_eprev = (size_t)align_up(off, 3 * ne * 4);   // nearest earlier active segment
+        p->o_elist0 = (size_t)align_up(off, 3 * ne * 4);  // the optimistic re-run list
     }
     if (p->mono16) p->o_dup = (size_t)align_up(off, (size_t)p->in_frames * 4);
     const size_t nb = (size_t)p->n_blk, nkb = (size_t)p->n_kblk;
@@ -1265,6 +1267,8 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     int *eact = p->mb ? wsp<int>(d_ws, p->o_eact) : nullptr;
     int *ehead = p->mb ? wsp<int>(d_ws, p->o_ehead) : nullptr;
     int *elist = p->mb ? wsp<int>(d_ws, p->o_elist) : nullptr;
+    int *eprev = p->mb ? wsp<int>(d_ws, p->o_eprev) : nullptr;
+    int *elist0 = p->mb ? wsp<int>(d_ws, p->o_elist0) : nullptr;
     amx::DynLaunch dl{p->d_cd,    p->d_chunks, p->n_chunks, p->d_esegs, p->n_es,
                       p->d_eseg0, p->d_neseg,  p->nloc,     p->max_chunk_n, p->cd.look,
                       p->warm,    p->Le,       p->cd.env_rcp, p->d_tabs, st,
@@ -1306,11 +1310,11 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
         break;
     case AMX_STAGE_ENV:
         if (p->mb)
-            HIPCHK(amx::launch_env(dl, mframe, ck, esv, ee0, eact, elist, ehead, eflags, p->rounds, 0));
+            HIPCHK(amx::launch_env(dl, mframe, ck, esv, ee0, eact, elist, ehead, eprev, elist0, eflags, p->rounds, 0));
         break;
     case AMX_STAGE_FIX:
         if (p->mb) {
-            HIPCHK(amx::launch_env(dl, mframe, ck, esv, ee0, eact, elist, ehead, eflags, p->rounds, 1));
+            HIPCHK(amx::launch_env(dl, mframe, ck, esv, ee0, eact, elist, ehead, eprev, elist0, eflags, p->rounds, 1));
             HIPCHK(amx::launch_envseq(dl, mframe, ck, esv, ee0, eact, eflags, p->rounds));
         }
         break;
