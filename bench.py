@@ -115,7 +115,7 @@ def front2_flops(frames, settings, mb):
 STAGE_KERNEL = {"front1": "k_front1s", "front2": "k_front2", "xover": "k_xover2", "rms": "k_rms",
                 "env": "k_env0", "apply": "k_gain_overlay", "final": "k_final", "up": "k_up"}
 # launches per step of kernels that run more than once (the envelope fix rounds)
-PER_STEP = {"k_envfix": 2}
+PER_STEP = {}   # kernels launched more than once per step (none since round 5)
 # the pipeline's kernels (runtime copy / torch helper kernels excluded from step traffic)
 PIPELINE_PREFIX = "k_"
 
