@@ -6,6 +6,7 @@ limiter -- and the concatenated rank outputs must equal the one-rank run of the
 same track bit for bit (the chunking, loudness decision and limiter are all
 track-level, so sharding must not change a sample)."""
 import datetime
+import gc
 import os
 import socket
 import tempfile
@@ -175,6 +176,7 @@ def test_rccl_forced_exchange_world1(gpu, case):
     y_ref = ref.step(d_in).cpu().numpy()
     dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _port(), rank=0, world_size=1,
                             timeout=datetime.timedelta(seconds=60))
+    tr = None
     try:
         assert dist.get_backend() == "nccl"
         tr = ShardedTrack(FS, 2, CASES[case], x.shape[0], 0, 1, quantum=512, force_exchange=True)
@@ -190,6 +192,11 @@ def test_rccl_forced_exchange_world1(gpu, case):
         y_graph2 = tr.flush().cpu().numpy()
         torch.cuda.synchronize()
     finally:
+        # the slots' graphs hold RCCL nodes of this group's communicator: free them (and
+        # everything they reference) before the group, not at some later collection
+        tr = None
+        gc.collect()
+        torch.cuda.synchronize()
         dist.destroy_process_group()
     np.testing.assert_array_equal(y_eager, y_ref)
     np.testing.assert_array_equal(y_graph, y_ref)
