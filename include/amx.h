@@ -225,10 +225,10 @@ AMX_API int amx_flac_decode(const uint8_t *data, int64_t size, int32_t *out, int
                             int64_t *n_blocks);
 
 /* Diagnostics of the compressor envelope's fix-up (AMX_STAGE_FIX) of the last step run
- * on d_ws: per round r, out[4r..4r+3] = segments re-run, the most re-runs in one wave
- * (the length of its chain of dependent fixes), waves with work, and the longest
- * look-back (in 64-segment steps) of round 0's link search.  Synchronous (hipMemcpy):
- * call it outside graph capture.  Replaces no reference line. */
+ * on d_ws: out[0..3] = segments the chain walkers re-ran, the longest walk (segments one
+ * wave re-ran in turn), chains, and segments of the optimistic parallel pass before them
+ * (out[4..] are 0).  Synchronous (hipMemcpy): call it outside graph capture.  Replaces no
+ * reference line. */
 AMX_API int amx_env_counters(const amx_plan *plan, const void *d_ws, int32_t *out, int32_t n);
 
 /* Gate a plan's per-sample kernels on a device word: with d_gate set, the K-weighting
