@@ -302,12 +302,21 @@ __device__ double env_rerun_wave(const ChainDev &cd, const uint16_t *m, const do
     const int lane = threadIdx.x & 63;
     const bool ckl = (lane & (AMX_ENV_TF_ - 1)) == 0;
     double c = ns;
-    double ml = f0 + lane < f1 ? m_of(mt, m[f0 + lane]) : 0.0;
-    double ol = ckl && f0 + lane < f1 ? ckr[(f0 + lane) / AMX_ENV_TF_] : 0.0;
+    // the loads run ahead of the chain: r indices three windows ahead, their table
+    // gathers (and the stored checkpoints) two, so a window's dependent index -> table
+    // load pair is never waited for (one window ahead left ~2 load latencies per
+    // window exposed against ~0.5 us of steps)
+    auto ridx = [&](int64_t f) -> uint32_t { return f < f1 ? (uint32_t)m[f] : 0xffffffffu; };
+    auto gath = [&](uint32_t r) -> double { return r == 0xffffffffu ? 0.0 : m_of(mt, r); };
+    auto ckld = [&](int64_t f) -> double { return ckl && f < f1 ? ckr[f / AMX_ENV_TF_] : 0.0; };
+    double ml = gath(ridx(f0 + lane));
+    uint32_t ib = ridx(f0 + 128 + lane);
+    double m1 = gath(ridx(f0 + 64 + lane));
+    double ol = ckld(f0 + lane), o1 = ckld(f0 + 64 + lane);
     for (int64_t base = f0; base < f1; base += 64) {
-        const int64_t fn = base + 64 + lane;
-        const double mn = fn < f1 ? m_of(mt, m[fn]) : 0.0;
-        const double on = ckl && fn < f1 ? ckr[fn / AMX_ENV_TF_] : 0.0;
+        const uint32_t ic = ridx(base + 192 + lane);
+        const double m2 = gath(ib);
+        const double o2 = ckld(base + 128 + lane);
         s_m[lane] = ml;
         s_i[lane] = env_div<RCP>(ml, cd.env_A, cd.env_rA);
         s_d[lane] = env_div<RCP>(ml, cd.env_R, cd.env_rR);
@@ -336,8 +345,11 @@ __device__ double env_rerun_wave(const ChainDev &cd, const uint16_t *m, const do
         __builtin_amdgcn_wave_barrier();                  // LDS reads done before the next writes
         if (ckl && (lane >> 4) < stop && base + lane < f1) ckr[(base + lane) / AMX_ENV_TF_] = mine;
         if (stop < 4) return old_end;
-        ml = mn;
-        ol = on;
+        ml = m1;
+        m1 = m2;
+        ib = ic;
+        ol = o1;
+        o1 = o2;
     }
     return c;
 }

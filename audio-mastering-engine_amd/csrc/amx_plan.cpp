@@ -740,6 +740,10 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         }
         for (int t = 1; t <= 3; t++)
             if (p->Le_t[t] == 0) p->Le_t[t] = p->Le;
+        // the warm-up: since the fix-up re-runs broken segments in parallel (round 5), a
+        // shorter warm-up pays where it is most of a lane's frames (C3: Le 1 408 / 896,
+        // C4: 8.5 k); a 60-min track's long segments keep 2 304
+        if (desc->env_warm_frames < 0 && p->Le_t[3] <= 16384) p->warm = 1536;
     }
     int64_t loc = 0, outo = 0;
     p->spans.assign(n_tracks, SpanDev{});
