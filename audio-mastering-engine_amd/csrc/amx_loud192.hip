@@ -262,16 +262,129 @@ __device__ __forceinline__ bool up_fast_seg(const UpArgs &a, const KwSegDev &sg,
            split >= a.Lout;
 }
 
+// k_up_edge's work in chunks of AMX_UPE_CH outputs, for the first workgroups of k_up
+// (below): a left-over segment's frames in LDS, the resampled samples and the K filter's
+// outputs of one chunk at a time (5 KB instead of k_up_edge's 12 KB, so the fast
+// kernel's own workgroups keep their occupancy).  Every sum keeps k_up_edge's order:
+// lane l still accumulates outputs l, l + 64, ... in turn (chunks are multiples of 64),
+// and the K filter runs on, serially, from chunk to chunk.  A k_up_edge beside k_up
+// needed a fork and a join in the step's graph; the join alone cost ~10 us.
+#define AMX_UPE_CH 128
+#define AMX_UPE_NF 544            // frames staged: Lin + 32 <= 544 (static paths: Lin <= 480)
+__device__ __forceinline__ void up_edge_chunked(const UpArgs &a, int64_t j, uint32_t *fr, float *us,
+                                                double *ys) {
+    const int lane = threadIdx.x & 63;
+    const KwSegDev sg = a.ks[j];
+    const SpanDev sp = a.spans[sg.track];
+    const int t = sg.track;
+    const int64_t g0 = sg.out_pos - sp.out_off;
+    const int nf = a.Lin + UP_TAPS;                               // frames g0 - 15 + [0, nf)
+    for (int i = lane; i < nf; i += 64) fr[i] = up_word(a.x, a.edge, sp, t, g0 - UP_C + i);
+    __syncthreads();
+    const int len = sg.len;
+    const int ch = lane & 1;
+    float pk = 0.0f, px = 0.0f;
+    double c1[5], c2[5];
+#pragma unroll
+    for (int k = 0; k < 3; k++) { c1[k] = a.cd->kw1[k]; c2[k] = a.cd->kw2[k]; }
+    c1[3] = a.cd->kw1[4]; c1[4] = a.cd->kw1[5];
+    c2[3] = a.cd->kw2[4]; c2[4] = a.cd->kw2[5];
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    const int64_t h0 = sg.tframe / a.hop;
+    const int split = (int)((h0 + 1) * a.hop - sg.tframe);
+    double acc[2][2][5] = {};                                     // [ch][piece][term]
+    for (int n0 = 0; n0 < a.Lout; n0 += AMX_UPE_CH) {
+        const int nc = a.Lout - n0 < AMX_UPE_CH ? a.Lout - n0 : AMX_UPE_CH;
+        for (int i = lane; i < 2 * nc; i += 64) {                 // i & 1 == ch
+            const int n = n0 + (i >> 1);
+            const int kb = a.obase[n], ph = a.oph[n];
+            float w[UP_TAPS];
+#pragma unroll
+            for (int k = 0; k < UP_TAPS; k++) w[k] = up_sample(fr[kb + k], ch);
+            const float u = (a.static_l > 0 && ph == 0) ? w[UP_C] : up_dot(w, a.bank + ph * UP_TAPS);
+            us[i] = u;
+            if (n < len) {
+                pk = fmaxf(pk, fabsf(u));
+                px = fmaxf(px, fabsf(w[UP_C]));
+            }
+        }
+        __syncthreads();
+        // the K filter recursion, one lane per channel, on from the previous chunk
+        if (lane < 2) {
+            for (int k = 0; k < nc; k++) {
+                const int n = n0 + k;
+                ys[2 * k + ch] = n < len ? hp_step(c2, v[2], v[3], bq_step(c1, v[0], v[1], (double)us[2 * k + ch]))
+                                         : 0.0;
+            }
+        }
+        __syncthreads();
+        for (int k = lane; k < nc; k += 64) {
+            const int n = n0 + k;
+            if (n >= len) continue;
+            const double *r = a.G + (int64_t)n * AMX_KW_DIM;
+            const int pc = n < split ? 0 : 1;
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                const double y = ys[2 * k + c];
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const double yy = q == pc ? y : 0.0;
+                    acc[c][q][0] = fma(yy, yy, acc[c][q][0]);
+#pragma unroll
+                    for (int d = 0; d < 4; d++) acc[c][q][1 + d] = fma(yy, r[d], acc[c][q][1 + d]);
+                }
+            }
+        }
+        __syncthreads();                                          // us / ys are rewritten next chunk
+    }
+#pragma unroll
+    for (int o = 2; o < 64; o <<= 1) {                            // max over the channel's lanes
+        pk = fmaxf(pk, __shfl_xor(pk, o));
+        px = fmaxf(px, __shfl_xor(px, o));
+    }
+#pragma unroll
+    for (int c = 0; c < 2; c++)
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                double x = acc[c][q][k];
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) x += __shfl_xor(x, o);
+                acc[c][q][k] = x;
+            }
+    if (lane < 2) {
+        double *o = a.e + (j * 2 + ch) * AMX_KW_DIM;
+#pragma unroll
+        for (int d = 0; d < AMX_KW_DIM; d++) o[d] = v[d];
+        uint32_t *pq = a.pk + j * 4;
+        pq[ch] = __float_as_uint(pk);
+        pq[2 + ch] = (uint32_t)(px * 32768.0f);
+        double *te = a.eterms + (j * 2 + ch) * 10;
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+#pragma unroll
+            for (int k = 0; k < 5; k++) te[q * 5 + k] = ch ? acc[1][q][k] : acc[0][q][k];
+    }
+}
+
 // one lane per (segment, channel); lanes of segments k_up_slow owns return at once
 template <int STATIC>
 __global__ void __launch_bounds__(AMX_UP_BLOCK) __attribute__((amdgpu_waves_per_eu(AMX_UP_WAVES)))
-k_up(UpArgs a) {
+k_up(UpArgs a, int n_edge) {
     __shared__ int zp[2];
     const int lane = threadIdx.x;
+    if ((int)blockIdx.x < n_edge) {                      // the left-over segments first
+        __shared__ __attribute__((aligned(16))) uint32_t fr[AMX_UPE_NF];
+        __shared__ __attribute__((aligned(16))) float us[2 * AMX_UPE_CH];
+        __shared__ __attribute__((aligned(16))) double ys[2 * AMX_UPE_CH];
+        up_edge_chunked(a, a.slow[blockIdx.x], fr, us, ys);
+        return;
+    }
     if (lane < 2) zp[lane] = 0;
     __syncthreads();
     const int ch = lane & 1;
-    const int64_t j = (int64_t)blockIdx.x * (AMX_UP_BLOCK / 2) + (lane >> 1);
+    const int64_t j = (int64_t)(blockIdx.x - n_edge) * (AMX_UP_BLOCK / 2) + (lane >> 1);
     if (j >= a.n_kseg) return;
     const KwSegDev sg = a.ks[j];
     const SpanDev sp = a.spans[sg.track];
@@ -687,7 +800,17 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_up_energy(UpArgs a) {
 hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
     if (a.n_kseg <= 0) return hipSuccess;
     const unsigned nblk = (unsigned)((a.n_kseg + AMX_UP_BLOCK / 2 - 1) / (AMX_UP_BLOCK / 2));
-    if (a.static_l > 0 || a.poly > 0) {
+    if (a.static_l > 0 && !a.lin && a.Lin + UP_TAPS <= AMX_UPE_NF && a.n_slow < (1 << 20)) {
+        // the left-over segments are k_up's first workgroups (dispatched first, so their
+        // serial K filter overlaps the fast segments): no second stream, no join
+        const unsigned ne = (unsigned)a.n_slow;
+        switch (a.static_l) {
+        case 1: hipLaunchKernelGGL(k_up<1>, dim3(ne + nblk), dim3(AMX_UP_BLOCK), 0, st, a, (int)ne); break;
+        case 2: hipLaunchKernelGGL(k_up<2>, dim3(ne + nblk), dim3(AMX_UP_BLOCK), 0, st, a, (int)ne); break;
+        case 4: hipLaunchKernelGGL(k_up<4>, dim3(ne + nblk), dim3(AMX_UP_BLOCK), 0, st, a, (int)ne); break;
+        default: return hipErrorInvalidValue;
+        }
+    } else if (a.static_l > 0 || a.poly > 0) {
         // the left-over segments' kernel is latency-bound (a serial K-filter lane per
         // channel): it runs on the plan's second stream beside the fast kernel
         const bool side = a.n_slow > 0 && aux && fork && join;
@@ -707,9 +830,9 @@ hipError_t launch_up1(const UpArgs &a, hipStream_t st, hipStream_t aux, hipEvent
             }
         }
         switch (a.static_l > 0 ? a.static_l : a.poly) {
-        case 1: hipLaunchKernelGGL(k_up<1>, dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a); break;
-        case 2: hipLaunchKernelGGL(k_up<2>, dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a); break;
-        case 4: hipLaunchKernelGGL(k_up<4>, dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a); break;
+        case 1: hipLaunchKernelGGL(k_up<1>, dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a, 0); break;
+        case 2: hipLaunchKernelGGL(k_up<2>, dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a, 0); break;
+        case 4: hipLaunchKernelGGL(k_up<4>, dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a, 0); break;
 #define AMX_UP_POLY_CASE(c0, c1, t)                                                                  \
         case AMX_UP_POLY(c0, c1, t):                                                                 \
             hipLaunchKernelGGL((k_up_poly<c0, c1, t>), dim3(nblk), dim3(AMX_UP_BLOCK), 0, st, a); break;
