@@ -424,23 +424,36 @@ __global__ void __launch_bounds__(AMX_PEAK_THREADS) k_peak_reduce(const SpanDev 
     // finish (counter) reduces the slots and writes the peak, then re-arms the
     // counter -- no zeroing pass before, no atomics on the result
     __shared__ bool last;
+    const int nb = (int)((sp.nkseg + (int64_t)AMX_PEAK_THREADS * AMX_PEAK_PER_THREAD - 1) /
+                         ((int64_t)AMX_PEAK_THREADS * AMX_PEAK_PER_THREAD));
     if (threadIdx.x == 0) {
         int mm[4] = {0, 0, 0, 0};
         for (int w = 0; w < AMX_PEAK_THREADS / 64; w++)
             for (int c = 0; c < 4; c++) mm[c] = max(mm[c], red[c][w]);
-        const int nb = (int)((sp.nkseg + (int64_t)AMX_PEAK_THREADS * AMX_PEAK_PER_THREAD - 1) /
-                             ((int64_t)AMX_PEAK_THREADS * AMX_PEAK_PER_THREAD));
         int *pt = part + ((int64_t)t * gridDim.x + blockIdx.x) * 4;
         for (int c = 0; c < 4; c++) pt[c] = mm[c];
         __threadfence();
         last = atomicAdd(cnt + t, 1u) == (unsigned)(nb - 1);
-        if (last) {
-            __threadfence();
+    }
+    __syncthreads();
+    if (last) {
+        // the slots in parallel (a thread per slot and channel word, then the block's max),
+        // not one thread's chain of dependent volatile loads
+        __threadfence();
+        int v = 0;
+        for (int k = threadIdx.x; k < 4 * nb; k += AMX_PEAK_THREADS) {
+            const volatile int *q = part + (int64_t)t * gridDim.x * 4 + k;
+            v = max(v, *q);
+        }
+        // threads with the same k % 4 hold the same channel word: fold over the block
+        for (int o = 4; o < 64; o <<= 1) v = max(v, __shfl_xor(v, o));
+        __syncthreads();                                 // red[] of the first pass was read
+        if ((threadIdx.x & 63) < 4) red[threadIdx.x & 3][threadIdx.x >> 6] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
             int ma[4] = {0, 0, 0, 0};
-            for (int k = 0; k < nb; k++) {
-                const volatile int *q = part + ((int64_t)t * gridDim.x + k) * 4;
-                for (int c = 0; c < 4; c++) ma[c] = max(ma[c], q[c]);
-            }
+            for (int w = 0; w < AMX_PEAK_THREADS / 64; w++)
+                for (int c = 0; c < 4; c++) ma[c] = max(ma[c], red[c][w]);
             // peak[t][4]: the measured stream's sample peak (loudnorm's input_tp) per
             // channel, then the chain output's own sample peak (the limiter's input bound)
             double *pp = peak + 4 * t;
