@@ -219,6 +219,22 @@ __device__ __forceinline__ double env_step3(double att, double m, double inc, do
     return att <= m ? up : dn;
 }
 
+// v_min_f64 without the operand canonicalisation the compiler adds for fmin (IEEE
+// mode quiets signalling NaNs; m is a table value, never a NaN): the instruction fmin
+// compiles to, one fp64 operation per frame fewer
+__device__ __forceinline__ double min_f64_raw(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// env_step3 with that min (k_env0's speculation, the re-runs' chain)
+__device__ __forceinline__ double env_step3_raw(double att, double m, double inc, double dec) {
+    const double up = min_f64_raw(att + inc, m);
+    const double dn = fmax(att - dec, 0.0);
+    return att <= m ? up : dn;
+}
+
 template <bool RCP>
 __device__ __forceinline__ double env_step(const ChainDev &cd, double att, double m) {
     return env_step3(att, m, env_div<RCP>(m, cd.env_A, cd.env_rA), env_div<RCP>(m, cd.env_R, cd.env_rR));
@@ -340,7 +356,7 @@ __device__ double env_rerun_wave(const ChainDev &cd, const uint16_t *m, const do
             if (__builtin_amdgcn_readfirstlane((int)same)) { stop = t; break; }
             mine = lane == 16 * t ? c : mine;            // state before frame base + 16 t
 #pragma unroll
-            for (int q = 0; q < 16; q++) c = env_step3(c, mv[q], iv[q], dv[q]);
+            for (int q = 0; q < 16; q++) c = env_step3_raw(c, mv[q], iv[q], dv[q]);
         }
         __builtin_amdgcn_wave_barrier();                  // LDS reads done before the next writes
         if (ckl && (lane >> 4) < stop && base + lane < f1) ckr[(base + lane) / AMX_ENV_TF_] = mine;
@@ -423,22 +439,6 @@ __device__ __forceinline__ void env_gather(const double *__restrict__ mt, const 
             G[4 * i + e] = mt[r];
         }
     }
-}
-
-// v_min_f64 without the operand canonicalisation the compiler adds for fmin (IEEE
-// mode quiets signalling NaNs; m is a table value, never a NaN): the instruction fmin
-// compiles to, one fp64 operation per frame fewer
-__device__ __forceinline__ double min_f64_raw(double a, double b) {
-    double r;
-    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-
-// env_step3 with that min (k_env0's speculation)
-__device__ __forceinline__ double env_step3_raw(double att, double m, double inc, double dec) {
-    const double up = min_f64_raw(att + inc, m);
-    const double dn = fmax(att - dec, 0.0);
-    return att <= m ? up : dn;
 }
 
 template <bool RCP>
