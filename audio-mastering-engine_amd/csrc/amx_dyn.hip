@@ -209,16 +209,6 @@ __device__ __forceinline__ double env_div(double m, double a, double ra) {
     }
 }
 
-// pydub envelope step, exact, branch-free (both candidates, then select).  The
-// reference's condition is (over and att <= m); over can be dropped: when m == 0
-// (not over) and att == 0 the attack branch gives min(0 + 0, 0) = 0 = att, and
-// att > 0 takes the release branch anyway.
-__device__ __forceinline__ double env_step3(double att, double m, double inc, double dec) {
-    const double up = fmin(att + inc, m);          // attenuation += inc; min(., max_att)
-    const double dn = fmax(att - dec, 0.0);        // attenuation -= dec; max(., 0)
-    return att <= m ? up : dn;
-}
-
 // v_min_f64 without the operand canonicalisation the compiler adds for fmin (IEEE
 // mode quiets signalling NaNs; m is a table value, never a NaN): the instruction fmin
 // compiles to, one fp64 operation per frame fewer
@@ -228,8 +218,12 @@ __device__ __forceinline__ double min_f64_raw(double a, double b) {
     return r;
 }
 
-// env_step3 with that min (k_env0's speculation, the re-runs' chain)
-__device__ __forceinline__ double env_step3_raw(double att, double m, double inc, double dec) {
+// pydub envelope step, exact, branch-free (both candidates, then select): attenuation
+// += inc, min(., max_att) or attenuation -= dec, max(., 0).  The reference's condition
+// is (over and att <= m); over can be dropped: when m == 0 (not over) and att == 0 the
+// attack branch gives min(0 + 0, 0) = 0 = att, and att > 0 takes the release branch
+// anyway.  Every envelope kernel uses it (k_env0, the re-runs, k_gain_overlay).
+__device__ __forceinline__ double env_step3(double att, double m, double inc, double dec) {
     const double up = min_f64_raw(att + inc, m);
     const double dn = fmax(att - dec, 0.0);
     return att <= m ? up : dn;
@@ -356,7 +350,7 @@ __device__ double env_rerun_wave(const ChainDev &cd, const uint16_t *m, const do
             if (__builtin_amdgcn_readfirstlane((int)same)) { stop = t; break; }
             mine = lane == 16 * t ? c : mine;            // state before frame base + 16 t
 #pragma unroll
-            for (int q = 0; q < 16; q++) c = env_step3_raw(c, mv[q], iv[q], dv[q]);
+            for (int q = 0; q < 16; q++) c = env_step3(c, mv[q], iv[q], dv[q]);
         }
         __builtin_amdgcn_wave_barrier();                  // LDS reads done before the next writes
         if (ckl && (lane >> 4) < stop && base + lane < f1) ckr[(base + lane) / AMX_ENV_TF_] = mine;
@@ -502,7 +496,7 @@ __device__ __forceinline__ void env0_tile(const ChainDev &cd, double *sm, double
         // (no scheduling barrier: the scheduler may start the recurrence while later
         // quotients are still being formed; measured 206 -> 201 us at C3)
 #pragma unroll
-        for (int f = 0; f < AMX_ENV_TF; f++) att = env_step3_raw(att, mv[f], iv[f], dv[f]);
+        for (int f = 0; f < AMX_ENV_TF; f++) att = env_step3(att, mv[f], iv[f], dv[f]);
     }
 }
 
