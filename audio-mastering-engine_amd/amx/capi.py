@@ -14,7 +14,7 @@ c_double_p = ctypes.POINTER(ctypes.c_double)
 c_float_p = ctypes.POINTER(ctypes.c_float)
 
 AMX_OK, AMX_EINVAL, AMX_EHIP, AMX_ENOMEM, AMX_ERANGE = 0, -1, -2, -3, -4
-ABI_VERSION = 3
+ABI_VERSION = 4
 CTL_FAST = 1
 MODES = ("off", "skip", "linear", "dynamic")
 STATS = 16
@@ -54,7 +54,7 @@ class FinalDesc(ctypes.Structure):
     _fields_ = [("limit", ctypes.c_double), ("attack_ms", ctypes.c_double),
                 ("release_ms", ctypes.c_double), ("level_in", ctypes.c_double),
                 ("level_out", ctypes.c_double), ("auto_level", ctypes.c_int32),
-                ("pad_", ctypes.c_int32)]
+                ("from_rest", ctypes.c_int32)]
 
 
 class DecideDesc(ctypes.Structure):

@@ -33,7 +33,7 @@ import torch
 import torch.distributed as dist
 
 from .chunking import chunk_bounds, packet_frames
-from .engine import MasteringJob
+from .engine import MasteringJob, wait_host_word
 
 
 def overlay_len(n, fs):
@@ -768,12 +768,11 @@ class ShardedTrack:
                     fn()
             return g
 
-        # the limiter state is zeroed in the graph, so when the device picks the general
+        # the limiter runs from rest in the graph, so when the device picks the general
         # limiter the in-graph run IS the speculative from-rest run of
         # chain_state_speculative: replay() then only hands the end states along
         def fin():
-            job.lim_state.zero_()
-            job.finalize(None)
+            job.finalize(None, from_rest=True)
 
         torch.cuda.synchronize()
         if dist.get_backend(self.group) == "nccl":
@@ -812,7 +811,6 @@ class ShardedTrack:
         buffers).  Every rank takes the same branch (the word comes from all-reduced
         data), so RCCL operations stay in the same order on every rank."""
         lufs_on = self.job.dd.lufs_on
-        self._lim_rest = torch.zeros_like(self.job.lim_state)
         slots = []
         for k in range(2):
             if k == 1:
@@ -840,8 +838,11 @@ class ShardedTrack:
                     job.histograms()
                 job.decide()                   # (k_decide also stores the word to _ctl_host)
                 # the in-graph limiter run from rest on the device's decision (see fin):
-                # its entering state is a buffer of zeros no kernel writes
-                job.finalize(None, state=self._lim_rest)
+                # from_rest ignores the carried state, and the span's end state lands in
+                # this slot's own job.lim_state, which _resolve hands to the next rank
+                # (a shared zero buffer was overwritten by the first engaged
+                # step, and lim_state was never written in the graph)
+                job.finalize(None, from_rest=True)
             self._g = [seg(whole)]
             slots.append({key: getattr(self, key) for key in self._SLOT_KEYS})
         self._slots = slots
@@ -859,11 +860,10 @@ class ShardedTrack:
         self._use(k)
         try:
             job = self.job
-            while not self._ctl_ev.query():
-                pass
+            wait_host_word(self._ctl_ev.query, "the step's end event")
             hv = self._ctl_host.numpy()
-            while hv[0] == -1:                  # (the device's store lands with the step's end)
-                pass
+            # (the device's store lands with the step's end)
+            wait_host_word(lambda: hv[0] != -1, "the step's decision word")
             ctl = int(hv[0])
             if is_dynamic(ctl):
                 return self.dynamic()
@@ -933,8 +933,7 @@ class ShardedTrack:
         # Only this 4-byte copy is waited for: an event on the launch stream, polled
         # (a blocking event wait sleeps and wakes late)
         self._ctl_ev.record()
-        while not self._ctl_ev.query():
-            pass
+        wait_host_word(self._ctl_ev.query, "the decision word's copy")
         if is_dynamic(int(self._ctl_host[0])):
             self._last_out = self.dynamic()
             return self._last_out
@@ -944,6 +943,49 @@ class ShardedTrack:
                                     self.group, first_run_done=True)
         self._last_out = job.y[:job.info.out_frames]
         return self._last_out
+
+    def close(self):
+        """Free what this rank's step holds, graphs first: the captured graphs (at N > 1
+        over RCCL their nodes use the process group's communicator), then the slots'
+        jobs, the dynamic-mode side jobs and plans.  Call it before
+        dist.destroy_process_group -- or use `with ShardedTrack(...) as tr:` -- so no
+        graph holding RCCL nodes outlives its communicator (the round-5 hipGraphLaunch
+        segfault's suspect: such graphs freed at a later garbage collection).
+        Idempotent; the object is unusable afterwards."""
+        import gc
+        if getattr(self, "_closed", False):
+            return
+        self._closed = True
+        torch.cuda.synchronize()
+        self._pending = None
+        jobs = [self.job]
+        for sl in (self._slots or []):
+            sl["_g"] = None
+            jobs.append(sl["job"])
+        self._slots = None
+        self._g = None
+        wd = getattr(self, "_wd", None)
+        if wd:
+            jobs.append(wd["span"].job)
+            wd["plan"].close()
+        sp = getattr(self, "_split", None)
+        if sp and sp.get("span") is not None:
+            jobs.append(sp["span"].job)
+        if getattr(self, "_whole", None) is not None:
+            jobs.append(self._whole)
+        seen = set()
+        for j in jobs:
+            if id(j) not in seen:
+                seen.add(id(j))
+                j.close()
+        gc.collect()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
 
     def step(self, d_in):
         """One pass of the whole path over this rank's chunks (input resident)."""
@@ -1080,6 +1122,17 @@ class ShardedBatch:
     def flush(self):
         """ShardedTrack's interface: a batch step needs no host resolution"""
         return None
+
+    def close(self):
+        """MasteringJob.close on this rank's job (graph first, then the plan)"""
+        self.job.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
 
     def finish_dynamic(self):
         """After a step: finish this rank's tracks that loudnorm sends to dynamic mode

@@ -55,6 +55,24 @@ def ln_output_bound(n192):
     return min(math.floor(c * 32768.0 + 0.5), 32767) / 32768.0
 
 
+def wait_host_word(ready, what, timeout_s=None):
+    """Spin until ready() (a pinned-memory word the device stores, or an event query),
+    for at most timeout_s seconds (AMX_WAIT_TIMEOUT_S, default 120): a faulted kernel
+    or a hung collective then raises instead of spinning forever."""
+    import time
+    if ready():
+        return
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("AMX_WAIT_TIMEOUT_S", "120"))
+    t_end = time.monotonic() + timeout_s
+    n = 0
+    while not ready():
+        n += 1
+        if n & 1023 == 0 and time.monotonic() > t_end:
+            raise RuntimeError("amx: %s not ready after %.0f s (a device fault or a hung "
+                               "collective?)" % (what, timeout_s))
+
+
 class MasteringJob:
     def __init__(self, sample_rate, channels_in, settings, track_frames, *, quantum=None,
                  input_s16=False, seg_frames=128, device=None, chunks=None, track_frame0=None,
@@ -202,13 +220,20 @@ class MasteringJob:
         capi.check(capi.load().amx_publish_ctl(capi.ptr(self.ctl), ctypes.c_void_p(host.data_ptr()),
                                                int(self.n_tracks), self._s(stream)), "amx_publish_ctl")
 
-    def finalize(self, fast=None, stream=None, state=None):
+    def finalize(self, fast=None, stream=None, state=None, from_rest=False):
         """fast None: each track takes the limiter path amx_loudness_decide chose.
-        state: the limiter state entering the span (default self.lim_state; a buffer of
-        zeros = from rest, read only)."""
+        state: the limiter state buffer (default self.lim_state): read as the state
+        entering the span, and the span's end state written back to it.  from_rest:
+        the entering state is not read -- every span starts from rest with its halo
+        (amx_final_desc.from_rest: the speculative first run of the rank-to-rank
+        hand-off, with no zero fill before it)."""
         ctl = capi.ptr(self.ctl) if fast is None else None
         st = self.lim_state if state is None else state
-        capi.check(capi.load().amx_finalize(self.plan.h, self.fd, capi.ptr(self.out), capi.ptr(self.gains),
+        fd = self.fd
+        if from_rest:
+            fd = capi.FinalDesc.from_buffer_copy(self.fd)
+            fd.from_rest = 1
+        capi.check(capi.load().amx_finalize(self.plan.h, fd, capi.ptr(self.out), capi.ptr(self.gains),
                                             ctl, 1 if fast else 0, capi.ptr(self.halo), capi.ptr(self.y),
                                             capi.ptr(st), capi.ptr(self.ws), self._s(stream)),
                    "amx_finalize")
@@ -457,8 +482,7 @@ class MasteringJob:
         h.fill_(-1)                 # (the previous step's words were read: its decide has run)
         self._graph.replay()
         hv = h.numpy()[:self.n_tracks]
-        while (hv == -1).any():
-            pass
+        wait_host_word(lambda: not (hv == -1).any(), "the step's decision words")
         dyn = [t for t in range(self.n_tracks) if (int(hv[t]) >> 4) & 15 == 3]   # k_decide mode 3
         for t in dyn:
             self._dyn_enqueue(t, self._dyn_sides[t], None, gate=True)
@@ -492,6 +516,35 @@ class MasteringJob:
                 cur.wait_stream(st)
                 self.dyn_out[run["t"]] = (y.clone(), info)
         return {t: v[1] for t, v in self.dyn_out.items()}
+
+    def close(self):
+        """Release what the job holds on the device, the captured graph first (its nodes
+        use the plan's tables and the job's buffers), then the 192 kHz side jobs and the
+        plan.  Idempotent; the job is unusable afterwards.  `with MasteringJob(...) as
+        job:` calls it."""
+        if getattr(self, "_closed", False):
+            return
+        self._closed = True
+        torch.cuda.synchronize(self.device)
+        self._graph = None
+        self._dyn_eager = False
+        side_jobs = [side[1] for side in (self._dyn_sides or [])]     # (n192, job2, ws2, summ)
+        j192 = getattr(self, "_j192", None)                            # (key, job2, ws2, summ)
+        if j192 is not None:
+            side_jobs.append(j192[1])
+        self._dyn_sides = self._j192 = None
+        for job2 in side_jobs:
+            job2.close()
+        if getattr(self, "_ctl_pin", None) is not None and self.plan.h:
+            self.plan.set_publish(None)
+        self.plan.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
 
     def track_output(self, t):
         """track t's output: its slot of y, or its 192 kHz output after finish_dynamic"""

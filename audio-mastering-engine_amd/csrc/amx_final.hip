@@ -164,6 +164,7 @@ struct LimArgs {
     const SpanDev *spans;
     const uint32_t *x, *halo;
     int halo_frames, fs, bs, seg_frames, warm_frames, max_segs, fast;
+    int from_rest;          // amx_final_desc.from_rest: every span starts fresh, `state` is out only
     int64_t warm_cap;
     const double *gains;
     const int32_t *ctl;
@@ -181,6 +182,7 @@ struct Lim {
     int64_t n, tframe0;
     double g, level_in, level, level_out, limit, release;
     int fs, bs, halo, P0;
+    bool from_rest;             // the carried state is not read (LimArgs.from_rest)
     double *buffer, *nextdelta, *nextposd, *inb, *outb;   // LDS
     double att, delta;          // scalar state, identical in every lane between batches
     int nextiter, nextlen;
@@ -230,7 +232,7 @@ __device__ void lim_set_idle(Lim &L) {
 // span that starts inside it (limiter assumed idle there).
 __device__ void lim_init_span(Lim &L, const double *S) {
     const int lane = threadIdx.x & 63;
-    const bool fresh = L.tframe0 == 0 || S[5] == 0.0;
+    const bool fresh = L.tframe0 == 0 || L.from_rest || S[5] == 0.0;
     for (int k = lane; k < L.bs; k += 64) {
         L.buffer[k] = fresh ? 0.0 : S[8 + k];
         L.nextdelta[k] = fresh ? 0.0 : S[8 + L.bs + k];
@@ -251,8 +253,8 @@ __device__ void lim_init_span(Lim &L, const double *S) {
     }
     amx_wave_sync();
 }
-__device__ __forceinline__ int lim_p0(const SpanDev &sp, const double *S, int halo, int bs) {
-    const bool fresh = sp.tframe0 == 0 || S[5] == 0.0;
+__device__ __forceinline__ int lim_p0(const SpanDev &sp, const double *S, int halo, int bs, bool from_rest) {
+    const bool fresh = sp.tframe0 == 0 || from_rest || S[5] == 0.0;
     return fresh ? (sp.tframe0 != 0 ? (2 * halo) % bs : 0) : (int)S[2];
 }
 __device__ __forceinline__ int lim_wrap(int v, int bs) { return v >= bs ? v - bs : v; }
@@ -534,10 +536,11 @@ __device__ void limiter_block(const LimArgs &a, int bx, int nbx, double *lim_lds
     L.level_in = a.level_in; L.level = a.level; L.level_out = a.level_out;
     L.limit = a.limit; L.release = a.release;
     L.fs = a.fs; L.bs = a.bs; L.halo = a.halo_frames;
+    L.from_rest = a.from_rest != 0;
     L.buffer = lim_lds; L.nextdelta = lim_lds + a.bs; L.nextposd = lim_lds + 2 * a.bs;
     L.inb = lim_lds + 3 * a.bs; L.outb = L.inb + 2 * AMX_LIM_BATCH;
     double *S = a.state + (int64_t)t * a.state_doubles;
-    L.P0 = lim_p0(sp, S, a.halo_frames, a.bs);
+    L.P0 = lim_p0(sp, S, a.halo_frames, a.bs, L.from_rest);
     const int LS = a.seg_frames;
     const int nseg = (int)((sp.out_n + LS - 1) / LS);
     const int64_t sd = a.state_doubles;
@@ -678,8 +681,8 @@ hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, co
                         const int16_t *halo, int halo_frames, const double *gains,
                         const int32_t *ctl, int fast, int fs, double level_in, double level,
                         double level_out, double limit, double release, int buffer_size,
-                        double *state, int64_t state_doubles, const LimScratch &ls, int16_t *y,
-                        hipStream_t st) {
+                        double *state, int64_t state_doubles, int from_rest, const LimScratch &ls,
+                        int16_t *y, hipStream_t st) {
     if (n_tracks <= 0) return hipSuccess;
     const int64_t per = (int64_t)AMX_BLOCK * AMX_FINAL_FPT;
     const bool unit = level_in == 1.0 && level_out == 1.0 && limit * 32768.0 <= 32767.0;
@@ -693,7 +696,7 @@ hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, co
     a.gains = gains; a.ctl = ctl;
     a.level_in = level_in; a.level = level; a.level_out = level_out; a.limit = limit;
     a.release = release;
-    a.state = state; a.state_doubles = state_doubles;
+    a.state = state; a.state_doubles = state_doubles; a.from_rest = from_rest;
     a.y = reinterpret_cast<uint32_t *>(y);
     fa.fast_cols = (ctl != nullptr || fast) ? (int)((max_span + per - 1) / per) : 0;
     fa.gate = ls.gate;

@@ -369,8 +369,8 @@ hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, co
                         const int16_t *halo, int halo_frames, const double *gains,
                         const int32_t *ctl, int fast, int fs, double level_in, double level,
                         double level_out, double limit, double release, int buffer_size,
-                        double *state, int64_t state_doubles, const LimScratch &ls, int16_t *y,
-                        hipStream_t st);
+                        double *state, int64_t state_doubles, int from_rest, const LimScratch &ls,
+                        int16_t *y, hipStream_t st);
 struct DecideArgs {
     int n_tracks, lufs_on;
     const unsigned long long *hist, *st_hist;

@@ -2023,7 +2023,7 @@ int amx_finalize(amx_plan *p, const amx_final_desc *fd, const int16_t *d_x,
     p->lim.gate = p->gate;
     HIPCHK(amx::launch_final(p->d_spans, p->n_tracks, p->max_span, d_x, d_halo, halo, d_gains, d_ctl,
                              fast ? 1 : 0, p->cd.fs, fd->level_in, level, fd->level_out, fd->limit,
-                             fd->release_ms / 1000.0, bs, d_lim_state, sd, p->lim, d_y, st));
+                             fd->release_ms / 1000.0, bs, d_lim_state, sd, fd->from_rest, p->lim, d_y, st));
     return AMX_OK;
 }
 

@@ -13,6 +13,10 @@ writes) stays in HBM.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--strong]
 
+--gpus N > 1 without a launcher starts the N ranks itself (a child
+`python -m torch.distributed.run --nproc-per-node N`, one process per GPU); under a
+launcher WORLD_SIZE must equal N (else exit 2).
+
 c2 = configs[1] (EQ + loudnorm + alimiter), c4 = configs[3] (8 whole 4-minute tracks
 per GPU, track-sharded, no exchange), c5 = configs[4] (60 min at 96 kHz per GPU).
 --strong: ONE track of the config's length split over the N ranks (configs[4] as
@@ -298,6 +302,7 @@ def other_configs(args):
                                     "overhead": round(msd / ms - 1.0, 4),
                                     "what": "capture(dynamic=True): the dynamic path held for every track"}
         out[cfg] = o
+        runner.close()
         del runner, d_in
         gc.collect()
         torch.cuda.empty_cache()
@@ -351,6 +356,7 @@ def other_inputs(args):
                                              oracle_mode=rinfo.get("mode"),
                                              oracle_seconds=round(time.perf_counter() - t0, 2))
         out[cfg] = o
+        runner.close()
         del runner, d_in, x, y
         gc.collect()
         torch.cuda.empty_cache()
@@ -372,6 +378,7 @@ def other_rates(args):
         ms, steps = time_graph(runner, d_in, 2, 0.5, 1.0)
         out[str(fs)] = {"settings": "c3", "seconds": CONFIG_SECONDS["c3"], "ms_per_step": round(ms, 4),
                         "steps": steps, "value": round(2 * n / (ms / 1e3) / 1e6, 3), "unit": "Msamples/s"}
+        runner.close()
         del runner, d_in
         gc.collect()
         torch.cuda.empty_cache()
@@ -386,6 +393,43 @@ def load_traffic(config):
         return json.load(open(path))["kernels"]
     except (OSError, ValueError, KeyError):
         return None
+
+
+def launch_plan(gpus, env, argv=None, port=None):
+    """How this invocation runs its --gpus N ranks (decided before any GPU call):
+      ("run", None)       -- one process per rank already: WORLD_SIZE == --gpus (a launcher
+                             started us), or N = 1 with no launcher;
+      ("spawn", cmd)      -- N > 1 and no launcher: start N ranks as a child
+                             `python -m torch.distributed.run --nproc-per-node N` on
+                             127.0.0.1 with the same arguments, and exit with its code;
+      ("refuse", message) -- a launcher's WORLD_SIZE disagrees with --gpus, or N < 1.
+    A bare `python bench.py --gpus 8` therefore measures 8 ranks, never one rank labelled
+    n_gpus 1."""
+    if gpus < 1:
+        return ("refuse", "--gpus must be >= 1 (got %d)" % gpus)
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        try:
+            w = int(world)
+        except ValueError:
+            return ("refuse", "WORLD_SIZE=%r is not an integer" % world)
+        if w != gpus:
+            return ("refuse", "launched with WORLD_SIZE=%d but --gpus %d: the world size must equal "
+                              "--gpus" % (w, gpus))
+        return ("run", None)
+    if gpus == 1:
+        return ("run", None)
+    if port is None:
+        import socket
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + argv
+    return ("spawn", cmd)
 
 
 def main():
@@ -422,6 +466,24 @@ def main():
                          "an RCCL rehearsal on one GPU")
     args = ap.parse_args()
 
+    # N ranks before anything touches the GPU: spawn them, or refuse a mismatched launch
+    how, what = launch_plan(args.gpus, os.environ)
+    if how == "refuse":
+        print("bench.py: %s" % what, file=sys.stderr, flush=True)
+        sys.exit(2)
+    if how == "spawn":
+        if not args.one_device:
+            import torch
+            have = torch.cuda.device_count()          # (counts devices without initialising them)
+            if have < args.gpus:
+                print("bench.py: --gpus %d but %d GPU(s) visible (--one-device --dist-backend gloo "
+                      "rehearses N ranks on one)" % (args.gpus, have), file=sys.stderr, flush=True)
+                sys.exit(2)
+        import subprocess
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        sys.exit(subprocess.call(what, env=env))
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -429,6 +491,7 @@ def main():
     from amx.dist import ShardedBatch, ShardedTrack
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    assert world == args.gpus, (world, args.gpus)     # (launch_plan)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_dist = world > 1 or args.force_exchange
@@ -691,6 +754,8 @@ def main():
         line["other_inputs"] = {"dynamic": other_inputs(args)}
     if rank == 0:
         print(json.dumps(line), flush=True)
+    # the captured graphs (RCCL nodes at N > 1) go before the process group
+    runner.close()
     if use_dist:
         dist.destroy_process_group()
 

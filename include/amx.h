@@ -43,7 +43,11 @@ extern "C" {
 #define AMX_ENOMEM -3     /* host allocation failed */
 #define AMX_ERANGE -4     /* a size or filter is outside what the plan supports */
 
-#define AMX_ABI_VERSION 3
+/* ABI history.  3 -> 4 (round 6): amx_loudnorm_desc gained reuse_stream (the struct
+ * grew), amx_ln_shard.pad_ became `windowed`, d_edge went from [2][16][2] to [2][80][2]
+ * frames per track, amx_final_desc.pad_ became `from_rest`.  A caller built against
+ * an older header must be rebuilt: amx_abi_version() tells it which layout it gets. */
+#define AMX_ABI_VERSION 4
 
 #if defined(__GNUC__)
 #define AMX_API __attribute__((visibility("default")))
@@ -114,7 +118,9 @@ typedef struct amx_final_desc {
     double release_ms;            /* 50 */
     double level_in, level_out;   /* 1, 1 */
     int32_t auto_level;           /* 1 (alimiter default) */
-    int32_t pad_;
+    int32_t from_rest;            /* amx_finalize: != 0 -> every span starts from rest (its halo
+                                   * ring, limiter idle) and d_lim_state is written, never read:
+                                   * the speculative first run of a rank-to-rank hand-off (ABI 4) */
 } amx_final_desc;
 
 typedef struct amx_plan amx_plan;

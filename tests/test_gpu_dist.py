@@ -99,6 +99,16 @@ def _worker(rank, world, port, case, seconds, outdir):
         if case.startswith("dynamic"):
             with open(os.path.join(outdir, "form%d.txt" % rank), "w") as f:
                 f.write(tr.dyn_info["form"])
+        elif not fast:
+            # the in-graph limiter runs from rest (amx_final_desc.from_rest)
+            # while the state buffer holds the previous step's valid end state; a changed
+            # input must still give the eager step's output, hand-off included
+            d_in.neg_()
+            y_graph2 = tr.replay().cpu().numpy()
+            y_eager2 = tr.step(d_in).cpu().numpy()
+            np.testing.assert_array_equal(y_graph2, y_eager2)
+            assert not np.array_equal(y_graph2, y_graph)
+        tr.close()
     finally:
         dist.destroy_process_group()
 
@@ -191,13 +201,35 @@ def test_rccl_forced_exchange_world1(gpu, case):
             tr.replay()
         y_graph2 = tr.flush().cpu().numpy()
         torch.cuda.synchronize()
+        # each slot's in-graph limiter run writes its end state into
+        # that slot's own lim_state (what _resolve hands to the next rank), and a changed
+        # input between replays gives the eager output
+        lim_slots = [sl["job"].lim_state.clone() for sl in tr._slots]
+        d_in.neg_()
+        tr.replay()
+        tr.replay()
+        y_graph3 = tr.flush().cpu().numpy()
+        ref2 = ShardedTrack(FS, 2, CASES[case], x.shape[0], 0, 1, quantum=512)
+        y_ref3 = ref2.step(d_in).cpu().numpy()
+        lim_ref3 = ref2.job.lim_state.clone()
+        lim_slots3 = [sl["job"].lim_state.clone() for sl in tr._slots]
+        ref2.close()
     finally:
         # the slots' graphs hold RCCL nodes of this group's communicator: free them (and
         # everything they reference) before the group, not at some later collection
+        if tr is not None:
+            tr.close()
         tr = None
         gc.collect()
         torch.cuda.synchronize()
         dist.destroy_process_group()
+    ref.close()
     np.testing.assert_array_equal(y_eager, y_ref)
     np.testing.assert_array_equal(y_graph, y_ref)
     np.testing.assert_array_equal(y_graph2, y_ref)
+    np.testing.assert_array_equal(y_graph3, y_ref3)
+    assert not np.array_equal(y_graph3, y_graph)
+    if case == "square_limiter":            # the general limiter engaged: its end state
+        for k in range(2):
+            assert float(lim_slots[k][0, 5]) == 1.0          # written (valid) by the graph
+            np.testing.assert_array_equal(lim_slots3[k].cpu().numpy(), lim_ref3.cpu().numpy())
