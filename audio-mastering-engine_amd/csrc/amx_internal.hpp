@@ -190,6 +190,7 @@ struct DynLaunch {
 };
 hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m, int *bact);
 // input decode: PCM of any supported format -> stereo s16 frames (amx_io.hip)
+hipError_t launch_zero(void *p, size_t bytes, hipStream_t st);   // a kernel, never a memset node
 hipError_t launch_pcm_to_s16(const void *raw, int64_t frames, int channels, int fmt, int16_t *out,
                              hipStream_t st);
 hipError_t launch_env(const DynLaunch &d, const uint16_t *m, double *ck, double *sv, double *ev,

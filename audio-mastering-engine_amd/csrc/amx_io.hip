@@ -115,4 +115,24 @@ hipError_t launch_pcm_to_s16(const void *raw, int64_t frames, int channels, int 
     }
 }
 
+// Zero fill as a kernel node.  Every zeroing on a path that may be captured into a
+// hipGraph goes through this instead of hipMemsetAsync: round 6 measured the runtime's
+// fill node (a captured hipMemsetAsync) leaving a 1.2 KB counter array full of
+// pointer-like words on the second replay of the dynamic path's graph (scripts/
+// dyn_graph_probe.py, profiles/r06b_dyn_graph_probe.log), so the filter's boundary
+// votes never matched and its walker re-ran 150 segments.
+__global__ void __launch_bounds__(256) k_zero32(uint32_t *p, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0u;
+}
+
+hipError_t launch_zero(void *p, size_t bytes, hipStream_t st) {
+    if (bytes == 0) return hipSuccess;
+    if (!p || (bytes & 3) || (reinterpret_cast<uintptr_t>(p) & 3)) return hipErrorInvalidValue;
+    const int64_t n = (int64_t)(bytes / 4);
+    const int64_t g = (n + 255) / 256;
+    hipLaunchKernelGGL(k_zero32, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, st,
+                       reinterpret_cast<uint32_t *>(p), n);
+    return hipGetLastError();
+}
+
 }  // namespace amx

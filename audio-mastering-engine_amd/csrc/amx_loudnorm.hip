@@ -2197,9 +2197,9 @@ hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x
     const int gb = max((lp.T + 1 + 255) / 256, (LP_FR + 255) / 256);
     hipLaunchKernelGGL(k_lp_gains, dim3(gb), dim3(256), 0, st, lp);
     if (lp.bm) lp_fill(lp, 0, ln.n192, 0, ln.n192, st);
-    hipError_t e = hipMemsetAsync(lp.cnt, 0, sizeof(int) * (size_t)(lp.K + 1), st);
+    hipError_t e = launch_zero(lp.cnt, sizeof(int) * (size_t)(lp.K + 1), st);
     if (e != hipSuccess) return e;
-    e = hipMemsetAsync(lp.match, 0, sizeof(int) * (size_t)(lp.K + 1), st);
+    e = launch_zero(lp.match, sizeof(int) * (size_t)(lp.K + 1), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lp_seg, dim3(lp.P), dim3(LP_NT), 0, st, lp);
     hipLaunchKernelGGL(k_lp_walk, dim3(1), dim3(LP_NT), 0, st, lp);
@@ -2225,9 +2225,9 @@ hipError_t launch_loudnorm_shard(const LnArgs &ln, const LpArgs &lp, const uint3
         const int gb = max((lp.T + 1 + 255) / 256, (LP_FR + 255) / 256);
         hipLaunchKernelGGL(k_lp_gains, dim3(gb), dim3(256), 0, st, lp);
         if (lp.bm) lp_fill(lp, y_lo, y_hi, u_lo, u_hi, st);
-        hipError_t e = hipMemsetAsync(lp.cnt, 0, sizeof(int) * (size_t)(lp.K + 1), st);
+        hipError_t e = launch_zero(lp.cnt, sizeof(int) * (size_t)(lp.K + 1), st);
         if (e != hipSuccess) return e;
-        e = hipMemsetAsync(lp.match, 0, sizeof(int) * (size_t)(lp.K + 1), st);
+        e = launch_zero(lp.match, sizeof(int) * (size_t)(lp.K + 1), st);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_lp_seg, dim3(lp.P), dim3(LP_NT), 0, st, lp);
     } else {

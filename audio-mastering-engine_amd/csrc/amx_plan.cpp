@@ -1487,9 +1487,9 @@ int amx_loudness_pass1_part(amx_plan *p, int32_t part, const int16_t *d_out, con
     // k_peak_reduce writes every track's peak; only tracks without a K segment (empty
     // spans) need the zero written here
     if (p->any_empty_span || p->n_kseg == 0)
-        HIPCHK(hipMemsetAsync(d_peak, 0, sizeof(double) * 4 * (size_t)p->n_tracks, st));
+        HIPCHK(amx::launch_zero(d_peak, sizeof(double) * 4 * (size_t)p->n_tracks, st));
     if (p->n_kseg == 0) {
-        if (d_kw_tail) HIPCHK(hipMemsetAsync(d_kw_tail, 0, sizeof(double) * 8 * (size_t)p->n_tracks, st));
+        if (d_kw_tail) HIPCHK(amx::launch_zero(d_kw_tail, sizeof(double) * 8 * (size_t)p->n_tracks, st));
         return AMX_OK;
     }
     HIPCHK(amx::launch_peak_reduce(p->d_spans, p->n_tracks, p->max_nkseg, pk, d_peak, p->d_pcnt,
@@ -1811,7 +1811,7 @@ int amx_loudness_pass2(amx_plan *p, const int16_t *d_out, const int16_t *d_edge,
     if (int rc = check_edges(p, d_edge)) return rc;
     hipStream_t st = (hipStream_t)stream;
     if (p->n_kseg == 0) {
-        HIPCHK(hipMemsetAsync(d_hops, 0, sizeof(double) * 2 * (size_t)max_hops * p->n_tracks, st));
+        HIPCHK(amx::launch_zero(d_hops, sizeof(double) * 2 * (size_t)max_hops * p->n_tracks, st));
         return AMX_OK;
     }
     double *e = wsp<double>(d_ws, p->o_ekw), *s = wsp<double>(d_ws, p->o_skw);
