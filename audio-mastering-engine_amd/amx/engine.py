@@ -434,7 +434,7 @@ class MasteringJob:
         n192, job2, ws2, summ = self._dyn_sides[t]
         return self._dyn_result({"t": t, "n192": n192, "job2": job2, "ws2": ws2, "summ": summ}, stream)
 
-    def capture(self, d_in, dynamic=False):
+    def capture(self, d_in, dynamic=False, dyn_graph=None):
         """Record run(d_in) as one hipGraph (torch.cuda.CUDAGraph over the HIP stream
         capture): replay() then re-issues the whole pipeline -- every kernel, same
         buffers -- with one launch, so the host's per-kernel launch cost is off the
@@ -442,8 +442,18 @@ class MasteringJob:
         complete step.  dynamic: the step also holds loudnorm's dynamic path
         (prepare_dynamic), so a track that takes it is finished inside the step too --
         enqueued by replay() after the graph, for the tracks whose published decision
-        word says dynamic (AMX_DYN_INLINE=1: gated inside the graph instead)."""
+        word says dynamic (AMX_DYN_INLINE=1: gated inside the graph instead).
+        dyn_graph (default AMX_DYN_GRAPH, off): that path of each track is captured into
+        a graph of its own as well, and replay() launches the track's graph instead of
+        the ~35 eager launches.  (Round 5 measured such a graph 10-20x slower with walker
+        re-runs: a captured hipMemsetAsync's fill node left the filter's boundary
+        counters full of garbage on some replays.  The library zeroes with kernels since
+        round 6, and the graph then equals the eager launches bit for bit and in time,
+        profiles/r06c_dyn_graph_probe_zero_kernel.log.)"""
         self._dyn_eager = False
+        self._dyn_graphs = None
+        if dyn_graph is None:
+            dyn_graph = os.environ.get("AMX_DYN_GRAPH") == "1"
         if dynamic:
             self.prepare_dynamic()
         dyn = bool(self._dyn_sides)
@@ -465,6 +475,20 @@ class MasteringJob:
             self.run(d_in, dyn=not dyn)
         self._graph = g
         self._dyn_eager = dyn
+        if dyn and dyn_graph:
+            # the gated dynamic path of each track as a graph of its own (warmed up on
+            # the side stream first, as torch's capture wants)
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for t in range(self.n_tracks):
+                    self._dyn_enqueue(t, self._dyn_sides[t], None, gate=True)
+            torch.cuda.current_stream().wait_stream(s)
+            self._dyn_graphs = []
+            for t in range(self.n_tracks):
+                gt = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gt, capture_error_mode="thread_local"):
+                    self._dyn_enqueue(t, self._dyn_sides[t], None, gate=True)
+                self._dyn_graphs.append(gt)
         return g
 
     def replay(self):
@@ -485,7 +509,10 @@ class MasteringJob:
         wait_host_word(lambda: not (hv == -1).any(), "the step's decision words")
         dyn = [t for t in range(self.n_tracks) if (int(hv[t]) >> 4) & 15 == 3]   # k_decide mode 3
         for t in dyn:
-            self._dyn_enqueue(t, self._dyn_sides[t], None, gate=True)
+            if self._dyn_graphs is not None:
+                self._dyn_graphs[t].replay()
+            else:
+                self._dyn_enqueue(t, self._dyn_sides[t], None, gate=True)
         return self.y[:self.info.out_frames]
 
     def finish_dynamic(self, report=None):
@@ -527,6 +554,7 @@ class MasteringJob:
         self._closed = True
         torch.cuda.synchronize(self.device)
         self._graph = None
+        self._dyn_graphs = None
         self._dyn_eager = False
         side_jobs = [side[1] for side in (self._dyn_sides or [])]     # (n192, job2, ws2, summ)
         j192 = getattr(self, "_j192", None)                            # (key, job2, ws2, summ)

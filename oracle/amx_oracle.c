@@ -328,6 +328,176 @@ EXPORT int64_t orc_chunk(const orc_chunk_t *p, const int16_t *in16, int64_t n, i
     return nout;
 }
 
+/* ------------------------------------------- more than two channels (round 6) */
+/* A chunk with C > 2 channels (the file's own layout after the ffmpeg split; :190
+ * duplicates only mono).  audio_segment_to_float_array reshapes only when channels == 2
+ * (:252), so every array stage runs on ONE interleaved 1-D stream of n*C samples:
+ *  - analog character (:258-266): tanh, then both shelves' lfilter along the stream
+ *    (axis -1 of a 1-D array), f64 -> int16;
+ *  - EQ (:272-276): _apply_eq_to_channel on the whole stream; its result is NOT stored
+ *    back into a float32 column (the 1-D branch rebinds `samples`), so it stays float64
+ *    when a stage ran -- float_array_to_audio_segment then clips and scales in float64;
+ *    with every stage skipped it is the float32 input;
+ *  - width (:268) returns a 1-D array unchanged;
+ *  - the crossover (:303) sosfilt's axis 0 of the 1-D stream;
+ *  - pydub's compressor and overlay work on frames of C samples. */
+EXPORT void orc_analog_stream(const int16_t *in, int64_t m, const float *tanh_lut,
+                              const double *b_lo, const double *a_lo, double g_lo,
+                              const double *b_hi, const double *a_hi, double g_hi,
+                              int16_t *out) {
+    const double glo1 = g_lo - 1.0, ghi1 = g_hi - 1.0;
+    lf_state s = {0.0, 0.0}, t = {0.0, 0.0};
+    for (int64_t i = 0; i < m; i++) {
+        const double x = (double)tanh_lut[(int)in[i] + 32768];
+        const double y = lf_step(b_lo, a_lo, &s, x);
+        const double u = x + (y - x) * glo1;
+        const double v = lf_step(b_hi, a_hi, &t, u);
+        out[i] = f64_to_s16(u + (v - u) * ghi1);
+    }
+}
+
+/* the EQ over the stream; returns 1 if a stage ran (out = its float64 result), else 0
+ * (out = the float32 input, widened) */
+EXPORT int orc_eq_stream(const float *in, int64_t m, const orc_eq_t *eq, double *out) {
+    lf_state ls[4];
+    double zs[4][4][2];
+    memset(ls, 0, sizeof(ls));
+    memset(zs, 0, sizeof(zs));
+    int any = 0;
+    for (int st = 0; st < 4; st++) any |= eq->kind[st] != 0;
+    for (int64_t i = 0; i < m; i++) {
+        const float xf = in[i];
+        double x = (double)xf;
+        int first = 1;
+        for (int st = 0; st < 4; st++) {
+            const int k = eq->kind[st];
+            if (k == 0) continue;
+            const double *c = eq->coef[st];
+            if (k == 1) {
+                const double y = lf_step(c, c + 3, &ls[st], x);
+                const double g = eq->g[st];
+                if (eq->gain_db[st] > 0) {
+                    x = x + (y - x) * (g - 1.0);
+                } else {
+                    const double xg = first ? (double)(xf * (float)g) : x * g;
+                    x = xg + (y - xg);
+                }
+            } else {
+                double y = x;
+                for (int q = 0; q < 4; q++) y = sos_step(c + 6 * q, zs[st][q], y);
+                x = x + y * (eq->g[st] - 1.0);
+            }
+            first = 0;
+        }
+        out[i] = x;
+    }
+    return any;
+}
+
+/* pydub compress_dynamic_range on frames of C samples: audioop.rms over the window's
+ * C (i - lo) samples, the gain on all C samples of the frame (orc_compress is C = 2) */
+EXPORT void orc_compress_mc(const int16_t *in, int64_t n, int C, int fs, double threshold,
+                            double ratio, int16_t *out, double *att_trace) {
+    const double thr = 32768.0 * pow(10.0, threshold / 20.0);
+    const int64_t L = (int64_t)(5.0 * (fs / 1000.0));
+    const double A = 5.0 * (fs / 1000.0), R = 50.0 * (fs / 1000.0);
+    const double k = 1.0 - (1.0 / ratio);
+    const double ln10 = log(10.0);
+    int64_t S = 0;
+    double att = 0.0;
+    for (int64_t i = 0; i < n; i++) {
+        if (i > 0)
+            for (int c = 0; c < C; c++) { const int64_t a = in[C * (i - 1) + c]; S += a * a; }
+        if (i - L - 1 >= 0)
+            for (int c = 0; c < C; c++) { const int64_t a = in[C * (i - L - 1) + c]; S -= a * a; }
+        const int64_t lo = i - L < 0 ? 0 : i - L;
+        const int64_t cnt = (int64_t)C * (i - lo);
+        const unsigned int rms = cnt ? (unsigned int)sqrt((double)S / (double)cnt) : 0u;
+        double over = 0.0;
+        if (rms != 0) {
+            const double db = 20 * (log((double)rms / thr) / ln10);
+            over = db > 0 ? db : (db == 0 ? db : 0.0);
+        }
+        const double m = k * over;
+        const double inc = m / A, dec = m / R;
+        if ((double)rms > thr && att <= m) {
+            att += inc;
+            att = att < m ? att : m;
+        } else {
+            att -= dec;
+            att = att > 0 ? att : 0.0;
+        }
+        if (att_trace) att_trace[i] = att;
+        if (att != 0.0) {
+            const double f = pow(10.0, (-att) / 20.0);
+            for (int c = 0; c < C; c++) out[C * i + c] = audioop_mul16(in[C * i + c], f);
+        } else {
+            for (int c = 0; c < C; c++) out[C * i + c] = in[C * i + c];
+        }
+    }
+}
+
+/* orc_overlay3 on frames of C samples */
+EXPORT int64_t orc_overlay3_mc(const int16_t *lo, const int16_t *mid, const int16_t *hi,
+                               int64_t n, int C, int fs, int16_t *out) {
+    const int64_t n1 = orc_overlay_len(n, fs);
+    const int64_t n2 = orc_overlay_len(n1, fs);
+    const int64_t nn = n1 < n ? n1 : n;
+    for (int64_t i = 0; i < C * nn; i++) out[i] = sat16((int)lo[i] + (int)mid[i]);
+    for (int64_t i = C * nn; i < C * n1; i++) out[i] = 0;
+    for (int64_t i = C * n1; i < C * n2; i++) out[i] = 0;
+    const int64_t mm = n2 < n ? n2 : n;
+    for (int64_t i = 0; i < C * mm; i++) out[i] = sat16((int)out[i] + (int)hi[i]);
+    return n2;
+}
+
+/* the chunk body (:189-197) on an s16 chunk of C > 2 channels [n][C]; `out` holds
+ * C (max(n, overlay_len(n)) + 8) samples.  Returns output frames.  p->width_on is
+ * ignored (:268). */
+EXPORT int64_t orc_chunk_mc(const orc_chunk_t *p, const int16_t *in16, int64_t n, int C, int16_t *out) {
+    const int64_t m = n * (int64_t)C;
+    int16_t *a16 = (int16_t *)malloc(sizeof(int16_t) * (m + 1));
+    float *f = (float *)malloc(sizeof(float) * (m + 1));
+    double *y = (double *)malloc(sizeof(double) * (m + 1));
+    const int16_t *src = in16;
+    if (p->analog_on) {
+        orc_analog_stream(in16, m, p->tanh_lut, p->an_b_lo, p->an_a_lo, p->an_g_lo,
+                          p->an_b_hi, p->an_a_hi, p->an_g_hi, a16);
+        src = a16;
+    }
+    for (int64_t i = 0; i < m; i++) f[i] = (float)src[i] / 32768.0f;
+    const int any = orc_eq_stream(f, m, &p->eq, y);
+    int16_t *p16 = p->mb_on ? a16 : out;
+    for (int64_t i = 0; i < m; i++) p16[i] = any ? f64_to_s16(y[i]) : f32_to_s16(f[i]);
+    int64_t nout = n;
+    if (p->mb_on) {
+        int16_t *b = (int16_t *)malloc(sizeof(int16_t) * 6 * (m + 1));
+        int16_t *lo = b, *mi = b + (m + 1), *hi = b + 2 * (m + 1);
+        int16_t *loc = b + 3 * (m + 1), *mic = b + 4 * (m + 1), *hic = b + 5 * (m + 1);
+        double zl[2][2] = {{0, 0}, {0, 0}}, zh[2][2] = {{0, 0}, {0, 0}};
+        for (int64_t i = 0; i < m; i++) {
+            const float xf = (float)p16[i] / 32768.0f;
+            const double x = (double)xf;
+            double l = x, h = x;
+            for (int q = 0; q < 2; q++) l = sos_step(p->xlo + 6 * q, zl[q], l);
+            for (int q = 0; q < 2; q++) h = sos_step(p->xhi + 6 * q, zh[q], h);
+            const double md = (x - l) - h;
+            lo[i] = f64_to_s16(l);
+            mi[i] = f64_to_s16(md);
+            hi[i] = f64_to_s16(h);
+        }
+        orc_compress_mc(lo, n, C, p->fs, p->thr_db[0], p->ratio[0], loc, NULL);
+        orc_compress_mc(mi, n, C, p->fs, p->thr_db[1], p->ratio[1], mic, NULL);
+        orc_compress_mc(hi, n, C, p->fs, p->thr_db[2], p->ratio[2], hic, NULL);
+        nout = orc_overlay3_mc(loc, mic, hic, n, C, p->fs, out);
+        free(b);
+    }
+    free(a16);
+    free(f);
+    free(y);
+    return nout;
+}
+
 /* ========================================================================
  * ffmpeg stages -- restated from the published FFmpeg sources (not in the
  * container).  PARITY UNPINNED: no ffmpeg binary and no reference fixtures.

@@ -57,6 +57,8 @@ def lib():
         L.orc_overlay_len.restype = _i64
         L.orc_overlay3.restype = _i64
         L.orc_chunk.restype = _i64
+        L.orc_chunk_mc.restype = _i64
+        L.orc_overlay3_mc.restype = _i64
         L.orc_swr_out_frames.restype = _i64
         _lib = L
     return _lib
@@ -186,6 +188,16 @@ def compress(band16, fs, threshold, ratio, trace=False):
     return (out, att) if trace else out
 
 
+def compress_mc(band16, fs, threshold, ratio):
+    """orc_compress_mc: pydub's compressor on frames of C samples (band16 [n, C])"""
+    band16 = np.ascontiguousarray(band16, np.int16)
+    out = np.empty_like(band16)
+    lib().orc_compress_mc(_p(band16, _i16p), _i64(band16.shape[0]), ctypes.c_int(band16.shape[1]),
+                          ctypes.c_int(fs), ctypes.c_double(threshold), ctypes.c_double(ratio),
+                          _p(out, _i16p), None)
+    return out
+
+
 def overlay_len(n, fs):
     return int(lib().orc_overlay_len(_i64(n), ctypes.c_int(fs)))
 
@@ -244,6 +256,19 @@ def chunk(in16, fs, settings):
     p, keep = chunk_struct(fs, settings)
     out = np.zeros((max(n, overlay_len(n, fs) if n else 0) + 8, 2), np.int16)
     m = lib().orc_chunk(ctypes.byref(p), _p(in16, _i16p), _i64(n), _p(out, _i16p))
+    del keep
+    return out[:m]
+
+
+def chunk_mc(in16, fs, settings):
+    """The chunk body (:189-197) on an s16 chunk [n, C] with C > 2 channels: one
+    interleaved 1-D stream through analog / EQ / crossover, no width (:252, :268),
+    the compressor and overlay on C-sample frames.  Returns int16 [n', C]."""
+    in16 = np.ascontiguousarray(in16, np.int16)
+    n, C = in16.shape
+    p, keep = chunk_struct(fs, settings)
+    out = np.zeros(((max(n, overlay_len(n, fs) if n else 0) + 8), C), np.int16)
+    m = lib().orc_chunk_mc(ctypes.byref(p), _p(in16, _i16p), _i64(n), ctypes.c_int(C), _p(out, _i16p))
     del keep
     return out[:m]
 

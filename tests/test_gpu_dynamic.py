@@ -224,10 +224,14 @@ def test_parallel_final_rerun_vs_oracle(gpu, oracle_mod, monkeypatch, warm):
     _cmp(job2.out[:n192].cpu().numpy(), ref, "loud tail, FINAL re-run, Wf=%d" % warm)
 
 
-def test_graph_step_with_dynamic(gpu, oracle_mod):
+@pytest.mark.parametrize("dyn_graph", [False, True], ids=["eager_dynamic", "graph_dynamic"])
+def test_graph_step_with_dynamic(gpu, oracle_mod, dyn_graph):
     """capture(dynamic=True): one hipGraph holds the whole step of a two-track batch, one
     track linear and one that loudnorm sends to dynamic mode; replays give the eager
-    outputs bit for bit, and the dynamic track matches the oracle's pipeline"""
+    outputs bit for bit, and the dynamic track matches the oracle's pipeline.
+    graph_dynamic: the dynamic path replayed from its own graph (it
+    used to re-run walker segments the eager launches never did) -- every replay gives
+    the eager run's output and the eager walker's counters"""
     import torch
     from amx import synth
     from amx.chunking import chunk_bounds
@@ -244,8 +248,9 @@ def test_graph_step_with_dynamic(gpu, oracle_mod):
     eager.finish_dynamic(rep)
     want = [eager.track_output(t).cpu().numpy() for t in range(2)]
     job = MasteringJob(fs, 2, settings, [xa.shape[0], xb.shape[0]], quantum=512)
-    job.capture(d_in, dynamic=True)
-    for _ in range(2):
+    job.capture(d_in, dynamic=True, dyn_graph=dyn_graph)
+    assert (job._dyn_graphs is not None) == dyn_graph
+    for _ in range(4 if dyn_graph else 2):
         job.replay()
         torch.cuda.synchronize()
         rep2 = job.fetch_report(raise_dynamic=False)
@@ -253,6 +258,8 @@ def test_graph_step_with_dynamic(gpu, oracle_mod):
         assert job.dynamic_output(0) is None
         y1, info = job.dynamic_output(1)
         assert info["target_offset"] == eager.dyn_out[1][1]["target_offset"]
+        assert info.get("pass2_parallel") == eager.dyn_out[1][1].get("pass2_parallel"), \
+            (info.get("pass2_parallel"), eager.dyn_out[1][1].get("pass2_parallel"))
         assert np.array_equal(job.track_output(0).cpu().numpy(), want[0])
         assert np.array_equal(y1.cpu().numpy(), want[1])
     ref, rinfo = oracle_mod.pipeline(oracle_mod.quantize(xb), fs, settings, chunk_bounds(xb.shape[0], fs, 512))

@@ -244,3 +244,24 @@ def test_aiff_ext80_rates():
     from amx import aiffio
     for fs in (8000, 22050, 44100, 48000, 88200, 96000, 192000):
         assert aiffio._ext80(aiffio._to_ext80(fs)) == fs
+
+
+def test_pipelined_slots_keep_every_exchange_tensor():
+    """r05f's hipErrorLaunchFailure: a slot's captured graph read gather indices that the
+    other slot's _setup_exchange had replaced (and the allocator had reused).  Every
+    attribute _setup_exchange assigns must be kept per slot (ShardedTrack._SLOT_KEYS)."""
+    import ast
+    import inspect
+    import textwrap
+    from amx.dist import ShardedTrack
+    src = textwrap.dedent(inspect.getsource(ShardedTrack._setup_exchange))
+    names = set()
+    for node in ast.walk(ast.parse(src)):
+        if isinstance(node, ast.Assign):
+            for t in node.targets:
+                if isinstance(t, ast.Attribute) and isinstance(t.value, ast.Name) and t.value.id == "self":
+                    names.add(t.attr)
+    names -= {"ne", "nl"}                 # plain ints, the same for both slots
+    assert names, "no attributes found"
+    missing = names - set(ShardedTrack._SLOT_KEYS)
+    assert not missing, "exchange tensors not kept per slot: %s" % sorted(missing)

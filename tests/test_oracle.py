@@ -14,7 +14,10 @@ import pytest
 
 from conftest import GOLDEN
 
-FILES = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+ALL_FILES = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+# chunks with more than two channels (round 6: one interleaved stream, :252)
+MC_FILES = [p for p in ALL_FILES if os.path.basename(p).startswith("mc")]
+FILES = [p for p in ALL_FILES if p not in MC_FILES]
 
 
 def test_golden_present():
@@ -48,6 +51,30 @@ def test_oracle_matches_reference_golden(oracle_mod, path):
                                       d["out16"])
     x16 = d["x16"] if d["x16"].shape[1] == 2 else np.repeat(d["x16"], 2, axis=1)
     np.testing.assert_array_equal(O.chunk(x16, fs, s), d["out16"])
+
+
+@pytest.mark.parametrize("path", MC_FILES, ids=lambda p: os.path.basename(p)[:-4])
+def test_oracle_multichannel_matches_reference_golden(oracle_mod, path):
+    """C > 2 channels: the reference's own chunk body ran on the interleaved 1-D stream
+    (make_golden.py); the oracle's stream restatement must give its every band, every
+    compressed band and the chunk output bit for bit"""
+    O = oracle_mod
+    d = np.load(path)
+    meta = json.loads(str(d["meta"]))
+    s, fs, C = meta["settings"], meta["fs"], meta["channels"]
+    assert C > 2 and d["in16"].shape[1] == C and d["out16"].shape[1] == C
+    assert d["eq32"].ndim == 1                          # the reference's 1-D stream
+    if "width32" in d:                                  # :268 leaves a 1-D array alone
+        np.testing.assert_array_equal(d["width32"], d["eq32"])
+    if s.get("multiband"):
+        for b in ("low", "mid", "high"):
+            np.testing.assert_array_equal(
+                O.compress_mc(d[b + "16"], fs, s[b + "_thresh"], s[b + "_ratio"]), d[b + "c16"])
+    np.testing.assert_array_equal(O.chunk_mc(d["x16"], fs, s), d["out16"])
+
+
+def test_golden_multichannel_present():
+    assert len(MC_FILES) >= 6
 
 
 def test_audioop_known_answers(oracle_mod):
