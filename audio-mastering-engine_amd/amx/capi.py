@@ -42,6 +42,7 @@ class ChainDesc(ctypes.Structure):
         ("comp_threshold_db", ctypes.c_double * 3), ("comp_ratio", ctypes.c_double * 3),
         ("comp_m_table", c_double_p * 3),
         ("env_warm_frames", ctypes.c_int32), ("env_rounds", ctypes.c_int32),
+        ("stream_chain", ctypes.c_int32), ("pad_sc_", ctypes.c_int32), ("eq_in_lut", c_float_p),
     ]
 
 
@@ -105,7 +106,9 @@ EXPORTS = ("amx_abi_version", "amx_last_error", "amx_build_id", "amx_plan_create
            "amx_finalize", "amx_env_counters", "amx_pcm_to_s16", "amx_loudnorm_192k_size",
            "amx_loudnorm_192k", "amx_loudnorm_192k_ex", "amx_flac_info", "amx_flac_decode",
            "amx_plan_set_gate", "amx_loudnorm_192k_shard", "amx_loudnorm_192k_segments",
-           "amx_loudnorm_192k_shard_window", "amx_publish_ctl")
+           "amx_loudnorm_192k_shard_window", "amx_publish_ctl", "amx_plan_set_limiter_trace",
+           "amx_mc_plan_create", "amx_mc_plan_free", "amx_mc_plan_get_info", "amx_mc_run_chunks",
+           "amx_mc_split_pairs", "amx_mc_loudness_combine", "amx_mc_peak_pick", "amx_mc_limiter_out")
 PCM_FORMATS = {"u8": 0, "s16": 1, "s24": 2, "s32": 3, "f32": 4, "f64": 5,
                "s8": 6, "s16be": 7, "s24be": 8, "s32be": 9, "f32be": 10, "f64be": 11}
 
@@ -139,6 +142,17 @@ def load(path=None):
     L.amx_pcm_to_s16.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, vp, vp]
     L.amx_env_counters.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]
     L.amx_plan_set_gate.argtypes = [vp, vp]
+    L.amx_plan_set_limiter_trace.argtypes = [vp, vp]
+    L.amx_mc_plan_create.argtypes = [ctypes.POINTER(ChainDesc), ctypes.POINTER(Chunk), ctypes.c_int32,
+                                     ctypes.c_int32, ctypes.POINTER(vp)]
+    L.amx_mc_plan_free.argtypes = [vp]
+    L.amx_mc_plan_free.restype = None
+    L.amx_mc_plan_get_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+    L.amx_mc_run_chunks.argtypes = [vp, vp, vp, vp, vp]
+    L.amx_mc_split_pairs.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, vp, vp]
+    L.amx_mc_loudness_combine.argtypes = [vp, ctypes.c_int64, vp, ctypes.c_int32, vp, vp, vp]
+    L.amx_mc_peak_pick.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, vp, vp, vp]
+    L.amx_mc_limiter_out.argtypes = [vp, ctypes.POINTER(FinalDesc), vp, ctypes.c_int32, vp, vp, vp, vp, vp]
     L.amx_kw_propagate.argtypes = [vp, ctypes.c_int64, c_double_p, c_double_p]
     L.amx_loudness_pass2.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int64, vp, vp]
     L.amx_loudness_histograms.argtypes = [vp, vp, ctypes.c_int64, vp, vp, vp, vp]
@@ -274,6 +288,35 @@ class Plan:
     def close(self):
         if getattr(self, "h", None):
             load().amx_plan_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class McPlan:
+    """Owns an amx_mc_plan* (a file with 3..8 channels; include/amx.h)."""
+
+    def __init__(self, desc, chunks, seg_frames=128):
+        L = load()
+        arr = (Chunk * max(1, len(chunks)))()
+        for i, (t, off, n) in enumerate(chunks):
+            arr[i].track, arr[i].in_offset, arr[i].frames = int(t), int(off), int(n)
+        h = ctypes.c_void_p()
+        self._desc = desc
+        check(L.amx_mc_plan_create(ctypes.byref(desc), arr, len(chunks), int(seg_frames), ctypes.byref(h)),
+              "amx_mc_plan_create")
+        self.h = h
+        ws, nout = ctypes.c_int64(), ctypes.c_int64()
+        check(L.amx_mc_plan_get_info(h, ctypes.byref(ws), ctypes.byref(nout)), "amx_mc_plan_get_info")
+        self.workspace_bytes, self.out_frames = ws.value, nout.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().amx_mc_plan_free(self.h)
             self.h = None
 
     def __del__(self):

@@ -583,6 +583,146 @@ class MasteringJob:
         return self.y[s.out_offset:s.out_offset + s.out_frames]
 
 
+class MultiChannelJob:
+    """One whole track with 3..8 channels (missing item 1).
+
+    The reference keeps such a chunk as ONE interleaved 1-D stream
+    (audio_segment_to_float_array reshapes only stereo, :252): analog character, EQ and
+    crossover run along it (:264-265, :274, :303), width leaves it alone (:268), and
+    pydub's compressor and overlay work on frames of C samples (:306-309); then ffmpeg
+    concatenates, measures loudness over the C channels (libebur128's default channel
+    map) and limits them together (:216-223).  On the GPU:
+      amx_mc_run_chunks      -- the chain (stream sub-plans + C-sample compressor);
+      amx_mc_split_pairs     -- the output's channel pairs as the tracks of a stereo
+                                measure plan (loudness pass 1 / 2 per channel);
+      amx_mc_loudness_combine -- one track's hop energies with the channel weights, and
+                                its peaks; histograms and the decision on a one-track plan;
+      amx_mc_peak_pick + amx_finalize (att trace) + amx_mc_limiter_out -- the alimiter:
+                                its state depends only on each frame's largest |sample|.
+    Loudnorm's dynamic mode (:240 when the linear conditions fail) is not run for C > 2:
+    finish() raises DynamicModeUnsupported.  Parity: the chain is pinned bit-exact to the
+    reference's own chunk body (tests/golden/mc*.npz); the measurement's channel weights
+    and the C-channel alimiter are parity unpinned (ffmpeg is absent), checked against
+    the oracle's restatement (oracle/amx_oracle.c)."""
+
+    def __init__(self, sample_rate, channels, settings, frames, *, quantum=None, input_s16=False,
+                 seg_frames=128, device=None, chunks=None, limiter=ALIMITER):
+        if not torch.cuda.is_available():
+            raise RuntimeError("amx needs a ROCm GPU (torch.cuda.is_available() is False)")
+        C = int(channels)
+        if not 3 <= C <= 8:
+            raise ValueError("MultiChannelJob takes 3..8 channels (%d): MasteringJob takes 1 or 2" % C)
+        self.device = torch.device(device or "cuda")
+        self.fs, self.C = int(sample_rate), C
+        self.settings = dict(settings)
+        self.input_s16 = bool(input_s16)
+        self.desc, self._keep = design.chain_desc(self.fs, C, self.settings)
+        self.desc.input_s16 = 1 if input_s16 else 0
+        if quantum is None:
+            quantum = packet_frames(C * (2 if input_s16 else 4))
+        self.frames = int(frames)
+        self.chunks = chunks if chunks is not None else plan_tracks([self.frames], self.fs, quantum)
+        self.plan = capi.McPlan(self.desc, self.chunks, seg_frames)
+        n = self.out_frames = int(self.plan.out_frames)
+        dev = self.device
+        self.ws = torch.empty(max(1, self.plan.workspace_bytes), dtype=torch.uint8, device=dev)
+        self.out = torch.empty((max(1, n), C), dtype=torch.int16, device=dev)
+        self.y = torch.empty_like(self.out)
+        P = (C + 1) // 2
+        lufs = self.settings.get("lufs")
+        m = max(1, n)
+        self.meas = MasteringJob(self.fs, 2, {"lufs": lufs}, [m] * P, input_s16=True,
+                                 chunks=[(p, p * m, m) for p in range(P)], device=dev, measure_only=True,
+                                 limiter=limiter)
+        self.one = MasteringJob(self.fs, 2, {"lufs": lufs}, [m], input_s16=True, chunks=[(0, 0, m)],
+                                device=dev, measure_only=True, limiter=limiter)
+        assert self.meas.max_hops == self.one.max_hops
+        self.att = torch.ones(m, dtype=torch.float64, device=dev)
+        capi.check(capi.load().amx_plan_set_limiter_trace(self.one.plan.h, capi.ptr(self.att)),
+                   "amx_plan_set_limiter_trace")
+        self.report = {}
+
+    _s = staticmethod(MasteringJob._s)
+
+    def run_chunks(self, d_in, stream=None):
+        """:185-214 -- every chunk's chain, the concat in self.out [out_frames, C]"""
+        want = torch.int16 if self.input_s16 else torch.float32
+        if d_in.dtype != want or not d_in.is_contiguous() or d_in.device.type != "cuda":
+            raise TypeError("d_in must be a contiguous %s CUDA tensor" % want)
+        need = max((off + k for (_, off, k) in self.chunks), default=0)
+        if d_in.numel() < need * self.C:
+            raise ValueError("d_in holds %d samples, plan needs %d" % (d_in.numel(), need * self.C))
+        capi.check(capi.load().amx_mc_run_chunks(self.plan.h, capi.ptr(d_in), capi.ptr(self.out),
+                                                 capi.ptr(self.ws), self._s(stream)), "amx_mc_run_chunks")
+
+    def measure(self, stream=None, lufs_on=None):
+        """loudnorm pass 1's measurement (:229) over the C channels: every channel's 192 kHz
+        K-weighted hop energies and peaks (the pairs as tracks), combined with the channel
+        weights into the one-track plan; its histograms (lufs on) and decision"""
+        L = capi.load()
+        s = self._s(stream)
+        n = self.out_frames
+        one, meas = self.one, self.meas
+        if lufs_on is None:
+            lufs_on = one.dd.lufs_on
+        one.dd.lufs_on = 1 if lufs_on else 0
+        capi.check(L.amx_mc_split_pairs(capi.ptr(self.out), n, self.C, capi.ptr(meas.out), s),
+                   "amx_mc_split_pairs")
+        meas.loudness_pass1(stream, tail=False)
+        if lufs_on:
+            meas.loudness_pass2(stream, carry=False)
+        capi.check(L.amx_mc_loudness_combine(capi.ptr(meas.hops), int(meas.max_hops), capi.ptr(meas.peak),
+                                             self.C, capi.ptr(one.hops), capi.ptr(one.peak), s),
+                   "amx_mc_loudness_combine")
+        if lufs_on:
+            one.histograms(stream)
+        one.decide(stream)
+
+    def finalize(self, stream=None):
+        """:240's linear gain and :223's alimiter on the C channels -> self.y"""
+        L = capi.load()
+        s = self._s(stream)
+        one = self.one
+        capi.check(L.amx_mc_peak_pick(capi.ptr(self.out), self.out_frames, self.C, capi.ptr(one.gains),
+                                      capi.ptr(one.out), s), "amx_mc_peak_pick")
+        one.finalize(None, stream)
+        capi.check(L.amx_mc_limiter_out(one.plan.h, one.fd, capi.ptr(self.out), self.C, capi.ptr(one.gains),
+                                        capi.ptr(one.ctl), capi.ptr(self.att), capi.ptr(self.y), s),
+                   "amx_mc_limiter_out")
+        return self.y[:self.out_frames]
+
+    def fetch_report(self, raise_dynamic=True):
+        rep = self.one.fetch_report(raise_dynamic=False)
+        if raise_dynamic and rep["modes"] and rep["modes"][0] == "dynamic":
+            raise DynamicModeUnsupported(
+                "loudnorm takes dynamic mode for these measurements %s; the 192 kHz dynamic path "
+                "runs on 1- and 2-channel files only" % (rep["stats"],))
+        self.report = dict(rep, channels=self.C)
+        return self.report
+
+    def run(self, d_in, stream=None):
+        """the whole pipeline (:171-226) on the stream; returns y int16 [frames, C]"""
+        self.run_chunks(d_in, stream)
+        self.measure(stream)
+        return self.finalize(stream)
+
+    def close(self):
+        if getattr(self, "_closed", False):
+            return
+        self._closed = True
+        torch.cuda.synchronize(self.device)
+        self.meas.close()
+        self.one.close()
+        self.plan.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+
 def master_array(x, sample_rate, settings, *, quantum=None, seg_frames=128, limiter_seg_frames=0,
                  limiter_warm_frames=-1):
     """In-memory twin of master_audio: float32 [frames, C] (C = 1/2,
@@ -597,6 +737,14 @@ def master_array(x, sample_rate, settings, *, quantum=None, seg_frames=128, limi
         s16 = False
         x = x.to(torch.float32)
     x = x.contiguous().to("cuda")
+    if x.shape[1] > 2:
+        # 3..8 channels: one interleaved stream through the chain (:252)
+        job = MultiChannelJob(sample_rate, x.shape[1], settings, x.shape[0], quantum=quantum,
+                              input_s16=s16, seg_frames=seg_frames)
+        y = job.run(x)
+        job.fetch_report(raise_dynamic=True)
+        job.report.update(sample_rate=job.fs, job=job)
+        return y, job.report
     job = MasteringJob(sample_rate, x.shape[1], settings, [x.shape[0]], quantum=quantum,
                        input_s16=s16, seg_frames=seg_frames, limiter_seg_frames=limiter_seg_frames,
                        limiter_warm_frames=limiter_warm_frames)

@@ -54,12 +54,21 @@ def _device_input(path):
     import torch
     from amx import capi
     raw, info, code = wavio.read_audio_raw(path)          # WAV, AIFF / AIFF-C or FLAC
-    if info.channels not in (1, 2):
-        raise ValueError("only mono and stereo inputs are supported (%d channels)" % info.channels)
+    if not 1 <= info.channels <= 8:
+        raise ValueError("1 to 8 channels are supported (%d channels)" % info.channels)
     frames = raw.size // info.block_align
     d_raw = torch.from_numpy(raw.copy()).to("cuda")
     if code == "f32":
         return d_raw.view(torch.float32), info.sample_rate, frames, info.channels, False, info
+    if info.channels > 2:
+        # 3..8 channels: s16 [frames][C] as the split writes them (no duplication, :190)
+        if code == "s16":
+            return d_raw.view(torch.int16), info.sample_rate, frames, info.channels, True, info
+        d_in = torch.empty((max(1, frames), info.channels), dtype=torch.int16, device="cuda")
+        capi.check(capi.load().amx_pcm_to_s16(capi.ptr(d_raw), frames, info.channels,
+                                              capi.PCM_FORMATS[code], capi.ptr(d_in),
+                                              capi.ptr_stream()), "amx_pcm_to_s16")
+        return d_in, info.sample_rate, frames, info.channels, True, info
     if code == "s16" and info.channels == 2:
         return d_raw.view(torch.int16), info.sample_rate, frames, 2, True, info
     d_in = torch.empty((max(1, frames), 2), dtype=torch.int16, device="cuda")
@@ -103,6 +112,9 @@ def master_audio(settings, status_callback=None, progress_callback=None):
     status("Splitting complete.")                                             # :180
     num_chunks = len(bounds)
     total_steps = num_chunks + 4                                              # :184
+    if ch_in > 2:
+        return _master_multichannel(settings, status, progress, d_in, fs, frames, ch_in, s16, bounds,
+                                    output_file)
     job = MasteringJob(fs, ch_in, settings, [frames], input_s16=s16,
                        chunks=[(0, s, n) for s, n in bounds])
     # every chunk's chain runs in the same launches (chunks are independent,
@@ -148,6 +160,44 @@ def master_audio(settings, status_callback=None, progress_callback=None):
     wavio.write_wav_s16(output_file, y, out_fs)
     progress(total_steps, total_steps)                                        # :224
     logging.info(f"Finished GPU pipeline, exported to {output_file}")
+    return output_file
+
+
+def _master_multichannel(settings, status, progress, d_in, fs, frames, channels, s16, bounds, output_file):
+    """master_audio for a file with 3..8 channels: the chain over the interleaved stream
+    (:252), the measurement over the C channels and the C-channel alimiter
+    (amx.engine.MultiChannelJob), with the same status strings and progress sequence.
+    Loudnorm's dynamic mode is not run for such a file (DynamicModeUnsupported)."""
+    import torch
+    from amx.engine import MultiChannelJob
+    num_chunks = len(bounds)
+    total_steps = num_chunks + 4
+    job = MultiChannelJob(fs, channels, settings, frames, input_s16=s16, chunks=[(0, s, n) for s, n in bounds])
+    if num_chunks:
+        job.run_chunks(d_in)
+    for i in range(num_chunks):
+        status(f"Processing chunk {i+1} of {num_chunks}...")                  # :186
+        progress(i + 1, total_steps)                                          # :187
+    torch.cuda.current_stream().synchronize()
+    status("Re-assembling processed chunks with concat filter...")           # :205
+    progress(num_chunks + 1, total_steps)                                     # :206
+    status("Concatenation complete.")                                         # :213
+    if settings.get("lufs") is not None:                                      # :216
+        status("Normalizing final loudness...")                               # :217
+        progress(num_chunks + 2, total_steps)                                 # :218
+        job.measure(lufs_on=True)
+        rep = job.fetch_report(raise_dynamic=True)
+        if rep["modes"] and rep["modes"][0] == "skip":
+            logging.warning("Measured loudness is -inf (silent audio). Skipping normalization.")
+    else:
+        job.measure(lufs_on=False)
+    status("Applying final limiting and exporting...")                        # :221
+    progress(num_chunks + 3, total_steps)                                     # :222
+    y = job.finalize().cpu().numpy()
+    wavio.write_wav_s16(output_file, y, fs)
+    progress(total_steps, total_steps)                                        # :224
+    logging.info(f"Finished GPU pipeline, exported to {output_file}")
+    job.close()
     return output_file
 
 

@@ -40,7 +40,10 @@ __device__ __forceinline__ void decode_in(const ChainDev &cd, const uint32_t *ro
 // unrolled by 2 only, so at most two G rows (2 x D doubles) are live in SGPRs: a
 // full unroll spills SGPRs to VGPR lanes.  (A thread per (segment, channel) halves
 // the reuse of each scalar-loaded G value and measured 35 % slower.)
-template <int D, int WIN, bool AN>
+// SC (a stream chain, amx_chain_desc.stream_chain): the input enters the EQ as
+// lut[s + 32768] when a table is given (the analog character's tanh of a C > 2 stream),
+// else as s / 32768
+template <int D, int WIN, bool AN, bool SC = false>
 __global__ void __launch_bounds__(AMX_BLOCK) k_front1(const ChainDev *__restrict__ cdp,
                                                       const ChunkDev *__restrict__ chunks,
                                                       const SegDev *__restrict__ segs, int n_seg,
@@ -88,8 +91,14 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_front1(const ChainDev *__restrict
             orow[f] = pack2(l, r);
             if constexpr (D > 0) {
                 const double *g = G + (int64_t)(k + f) * D;   // wave-uniform row
-                const double x0 = (double)((float)l / 32768.0f);
-                const double x1 = (double)((float)r / 32768.0f);
+                double x0, x1;
+                if constexpr (SC) {
+                    x0 = lut ? (double)lut[(int)l + 32768] : (double)((float)l / 32768.0f);
+                    x1 = lut ? (double)lut[(int)r + 32768] : (double)((float)r / 32768.0f);
+                } else {
+                    x0 = (double)((float)l / 32768.0f);
+                    x1 = (double)((float)r / 32768.0f);
+                }
 #pragma unroll
                 for (int d = 0; d < D; d++) {
                     e0[d] = fma(g[d], x0, e0[d]);
@@ -552,7 +561,10 @@ __device__ __forceinline__ VRows vt_rows(int32_t base, int len) {
     return vr;
 }
 
-template <int MASK, bool MB, bool KW>
+// SC: a stream chain (amx_chain_desc.stream_chain; no width): the input through slut
+// when given (as k_front1), and the EQ's float64 result clipped and scaled in float64
+// (:273-275 keep a 1-D stream's float64 result; float32 only when no stage ran)
+template <int MASK, bool MB, bool KW, bool SC = false>
 __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const ChainDev *__restrict__ cdp,
                                                       const ChunkDev *__restrict__ chunks,
                                                       const SegDev *__restrict__ segs, int n_seg,
@@ -563,7 +575,8 @@ __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const 
                                                       double *__restrict__ e_x,
                                                       const double *__restrict__ Gkw,
                                                       double *__restrict__ e_kw,
-                                                      uint32_t *__restrict__ pk) {
+                                                      uint32_t *__restrict__ pk,
+                                                      const float *__restrict__ slut) {
     constexpr int D = EqDim<MASK>::v;
     constexpr int ROWS = AMX_BLOCK / 2;
     constexpr int WV = AMX_BLOCK / 64;
@@ -625,7 +638,9 @@ __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const 
 #pragma unroll
             for (int f = 0; f < AMX_EQ_F; f++) {
                 const uint32_t p = rp[f0 + f];
-                xf[f] = (float)(chn ? hi16(p) : lo16(p)) / 32768.0f;
+                const int16_t sv = chn ? hi16(p) : lo16(p);
+                if constexpr (SC) xf[f] = slut ? slut[(int)sv + 32768] : (float)sv / 32768.0f;
+                else xf[f] = (float)sv / 32768.0f;
                 x[f] = (double)xf[f];
             }
             // cd.pad0_ == 0: the offset makes the coefficient address depend on the
@@ -633,12 +648,17 @@ __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const 
             eq_tile<MASK, AMX_EQ_F>(negm, cd.eqc + (f0 & cd.pad0_), est, x, xf);
 #pragma unroll
             for (int f = 0; f < AMX_EQ_F; f++) {
-                float v = MASK ? (float)x[f] : xf[f];
-                if (won) {
-                    const float o = pair_swap(v);
-                    v = width_one(w, chn ? o : v, chn ? v : o, chn);
+                int16_t qv;
+                if constexpr (SC) {
+                    qv = MASK ? f64_to_s16(x[f]) : f32_to_s16(xf[f]);
+                } else {
+                    float v = MASK ? (float)x[f] : xf[f];
+                    if (won) {
+                        const float o = pair_swap(v);
+                        v = width_one(w, chn ? o : v, chn ? v : o, chn);
+                    }
+                    qv = f32_to_s16(v);
                 }
-                const int16_t qv = f32_to_s16(v);
                 const int other = __builtin_amdgcn_update_dpp(0, (int)qv, 0xB1, 0xF, 0xF, false);
                 if (chn == 0) op[f0 + f] = pack2(qv, (int16_t)other);
                 if constexpr (MB) {
@@ -782,10 +802,10 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_xover2(const ChainDev *__restrict
 }
 
 // ================================================================ launchers
-template <int D, int WIN, bool AN>
+template <int D, int WIN, bool AN, bool SC = false>
 static hipError_t front1_t(const Launch &l, const uint32_t *in, const float *lut, uint32_t *a16,
                            const double *G, double *e) {
-    hipLaunchKernelGGL((k_front1<D, WIN, AN>), grid1(l.n_seg), dim3(AMX_BLOCK), 0, l.stream, l.cd,
+    hipLaunchKernelGGL((k_front1<D, WIN, AN, SC>), grid1(l.n_seg), dim3(AMX_BLOCK), 0, l.stream, l.cd,
                        l.chunks, l.segs, l.n_seg, l.L, in, lut, a16, G, e);
     return hipGetLastError();
 }
@@ -840,13 +860,15 @@ static hipError_t front1_an(const Launch &l, bool an, const uint32_t *in, const 
 }
 
 hipError_t launch_front1(const Launch &l, int D, int win, bool analog, const float *in,
-                         const float *lut, int16_t *a16, const double *G, double *e) {
+                         const float *lut, int16_t *a16, const double *G, double *e, bool sc) {
     if (l.n_seg <= 0) return hipSuccess;
     if (analog && !lut) return hipErrorInvalidValue;
+    if (sc && (analog || win != 1)) return hipErrorInvalidValue;   // a stream chain reads int16 pairs
     const uint32_t *i32 = reinterpret_cast<const uint32_t *>(in);
     uint32_t *a = reinterpret_cast<uint32_t *>(a16);
 #define F1(DD)                                                                   \
     case DD:                                                                     \
+        if (sc) return front1_t<DD, 1, false, true>(l, i32, lut, a, G, e);       \
         return win == 2 ? front1_an<DD, 2>(l, analog, i32, lut, a, G, e)         \
                         : front1_an<DD, 1>(l, analog, i32, lut, a, G, e);
     switch (D) { F1(0) F1(2) F1(4) F1(8) F1(10) F1(12) F1(16) F1(18) F1(20) }
@@ -854,15 +876,15 @@ hipError_t launch_front1(const Launch &l, int D, int win, bool analog, const flo
     return hipErrorInvalidValue;
 }
 
-template <int MASK, bool MB, bool KW>
+template <int MASK, bool MB, bool KW, bool SC = false>
 static hipError_t front2_t(const Launch &l, const uint32_t *a16, const double *s_eq,
                            uint32_t *dst, int to_out, const double *Gx, double *e_x,
-                           const double *Gkw, double *e_kw, uint32_t *pk) {
+                           const double *Gkw, double *e_kw, uint32_t *pk, const float *slut = nullptr) {
     const int rows = AMX_BLOCK / 2;
     dim3 grid((unsigned)((l.n_seg + rows - 1) / rows));
-    hipLaunchKernelGGL((k_front2<MASK, MB, KW>), grid, dim3(AMX_BLOCK), 0, l.stream, l.cd,
+    hipLaunchKernelGGL((k_front2<MASK, MB, KW, SC>), grid, dim3(AMX_BLOCK), 0, l.stream, l.cd,
                        l.chunks, l.segs, l.n_seg, l.L, a16, s_eq, dst, to_out, Gx, e_x, Gkw, e_kw,
-                       pk);
+                       pk, slut);
     return hipGetLastError();
 }
 
@@ -870,15 +892,18 @@ static hipError_t front2_t(const Launch &l, const uint32_t *a16, const double *s
 
 hipError_t launch_front2(const Launch &l, int mask, const int16_t *a16, const double *s_eq,
                          int16_t *dst, int to_out, const double *Gx, double *e_x,
-                         const double *Gkw, double *e_kw, uint32_t *pk) {
+                         const double *Gkw, double *e_kw, uint32_t *pk, bool sc, const float *slut) {
     if (l.n_seg <= 0) return hipSuccess;
     const uint32_t *a = reinterpret_cast<const uint32_t *>(a16);
     uint32_t *d = reinterpret_cast<uint32_t *>(dst);
     const bool mb = Gx != nullptr, kw = Gkw != nullptr;
     if (mb && kw) return hipErrorInvalidValue;
+    if (sc && kw) return hipErrorInvalidValue;          // a stream chain measures elsewhere
     switch (mask) {
 #define C2(M)                                                                           \
     case M:                                                                             \
+        if (sc) return mb ? front2_t<M, true, false, true>(l, a, s_eq, d, to_out, Gx, e_x, Gkw, e_kw, pk, slut) \
+                          : front2_t<M, false, false, true>(l, a, s_eq, d, to_out, Gx, e_x, Gkw, e_kw, pk, slut); \
         return mb ? front2_t<M, true, false>(l, a, s_eq, d, to_out, Gx, e_x, Gkw, e_kw, pk) \
              : kw ? front2_t<M, false, true>(l, a, s_eq, d, to_out, Gx, e_x, Gkw, e_kw, pk) \
                   : front2_t<M, false, false>(l, a, s_eq, d, to_out, Gx, e_x, Gkw, e_kw, pk);

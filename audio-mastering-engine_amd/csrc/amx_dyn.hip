@@ -1075,6 +1075,177 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_gain_overlay(const ChainDev *__re
     }
 }
 
+// ------------------------------------------ more than two channels (round 6)
+// pydub's compressor on frames of C samples (a C > 2 file, :306-308).  The bands come
+// from a stream sub-plan (pseudo-stereo int16 pairs: the stream in lo16, R = 0), whose
+// chunk k holds chunk k's frames as n * C stream samples (frame i, channel c = stream
+// sample i C + c); r, the checkpoints and the envelope segments belong to a stereo plan
+// over the chunks' real frames (its k_env0 / fix-up kernels run on them unchanged).
+// k_mc_rms: audioop.rms over the window's C (i - lo) samples, exactly as k_rms does for
+// C = 2 (the same block prefix sums, S < 2^44 for C <= 8).
+template <int LP>
+__global__ void __launch_bounds__(AMX_BLOCK) k_mc_rms(const ChainDev *__restrict__ cdp,
+                                                      const ChunkDev *__restrict__ chunks,
+                                                      const ChunkDev *__restrict__ schunks,
+                                                      const uint32_t *__restrict__ bands, int64_t snloc,
+                                                      int C, uint16_t *__restrict__ mi, int64_t nloc,
+                                                      int *bact) {
+    constexpr int N = AMX_RMS_N;
+    constexpr int F = N - LP;
+    constexpr int PER = N / AMX_BLOCK;
+    __shared__ unsigned long long P[N + N / 16];
+    __shared__ unsigned long long wsum[AMX_BLOCK / 64];
+    const int look = cdp->look;
+    const int c = blockIdx.y, b = blockIdx.z;
+    const ChunkDev ch = chunks[c];
+    const int64_t base = (int64_t)blockIdx.x * F;
+    if (base >= ch.n) return;                          // block-uniform
+    const uint32_t *x = bands + b * snloc + schunks[c].loc_off;
+    uint16_t *mo = mi + b * nloc + ch.loc_off;
+    const int64_t rowlen = (ch.n + 15) / 16 * 16;
+    const int64_t f0 = base - LP;
+    const int t = threadIdx.x;
+    unsigned long long v[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int64_t f = f0 + t * PER + q;
+        unsigned long long e = 0;
+        if (f >= 0 && f < ch.n) {
+            const uint32_t *row = x + f * C;
+            for (int k = 0; k < C; k++) {
+                const int32_t a = lo16(row[k]);
+                e += (unsigned long long)(uint32_t)(a * a);
+            }
+        }
+        v[q] = e;
+    }
+    unsigned long long run = 0;
+#pragma unroll
+    for (int q = 0; q < PER; q++) run += v[q];
+    unsigned long long incl = run;
+    const int lane = t & 63, w = t >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long up = __shfl_up(incl, o);
+        if (lane >= o) incl += up;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    unsigned long long pp = incl - run;
+    for (int q = 0; q < w; q++) pp += wsum[q];
+    const int s0 = rms_slot(t * PER);
+#pragma unroll
+    for (int q = 0; q < PER; q++) { pp += v[q]; P[s0 + q] = pp; }
+    __syncthreads();
+    constexpr int OUT = F / AMX_BLOCK;
+    const uint32_t cfull = (uint32_t)C * (uint32_t)look;
+    const double rfull = 1.0 / (double)cfull;
+    const uint32_t rq = (uint32_t)cdp->rq[b];
+    bool hot = false;
+#pragma unroll
+    for (int k = 0; k < OUT; k++) {
+        const uint32_t nn = (uint32_t)t + (uint32_t)k * AMX_BLOCK;
+        const uint32_t e1 = nn + (LP - 1), e0 = e1 - (uint32_t)look;
+        const uint64_t S = P[e1 + (e1 >> 4)] - P[e0 + (e0 >> 4)];
+        const int64_t i = base + nn;
+        const bool head = i < look;
+        const uint32_t cnt = head ? (uint32_t)C * (uint32_t)i : cfull;
+        const uint32_t rms = rms_floor(S, cnt, head ? 1.0 / (double)cnt : rfull);
+        hot |= i < ch.n && rms >= rq;
+        if (i < rowlen) mo[i] = i < ch.n ? (uint16_t)rms : (uint16_t)0;
+    }
+    if (__syncthreads_or(hot) && t == 0 && bact[b] == 0) bact[b] = 1;
+}
+
+// every frame's attenuation from the checkpoint before it (k_gain_overlay's sequence),
+// the gain on the frame's C samples (audioop.mul) and the 3-band overlay with pydub's
+// ms-rounded lengths, into the C-channel output [frames][C].  A thread per 16 frames.
+template <bool RCP>
+__global__ void __launch_bounds__(AMX_BLOCK) k_mc_gain_overlay(const ChainDev *__restrict__ cdp,
+                                                               const ChunkDev *__restrict__ chunks,
+                                                               const ChunkDev *__restrict__ schunks,
+                                                               const uint16_t *__restrict__ mm,
+                                                               const double *__restrict__ tabs,
+                                                               const double *__restrict__ ck,
+                                                               const uint32_t *__restrict__ bands,
+                                                               int64_t snloc, int64_t nloc, int C,
+                                                               const int64_t *__restrict__ n1tab,
+                                                               const int *__restrict__ bact,
+                                                               int16_t *__restrict__ out) {
+    const ChainDev &cd = *cdp;
+    const int c = blockIdx.y;
+    const ChunkDev ch = chunks[c];
+    const int64_t i0 = ((int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x) * AMX_ENV_TF_;
+    const int64_t n = ch.n, n2 = ch.out_n, n1 = n1tab[c];
+    if (i0 >= n2) return;
+    const EnvBands eb = env_bands(bact);
+    const uint32_t *xb = bands + schunks[c].loc_off;
+    double att[3];
+#pragma unroll
+    for (int b = 0; b < 3; b++)
+        att[b] = (i0 < n && eb.act(b)) ? ck[(b * nloc + ch.loc_off + i0) / AMX_ENV_TF_] : 0.0;
+    for (int f = 0; f < AMX_ENV_TF_; f++) {
+        const int64_t i = i0 + f;
+        if (i >= n2) break;
+        double fac[3];
+#pragma unroll
+        for (int b = 0; b < 3; b++) {
+            const bool on = i < n && eb.act(b);
+            const double m = on ? m_of(tabs + (int64_t)b * 3 * AMX_TAB, mm[b * nloc + ch.loc_off + i]) : 0.0;
+            att[b] = env_step<RCP>(cd, att[b], m);
+            fac[b] = gain_factor(cd, att[b]);
+        }
+        int16_t *o = out + (ch.out_off + i) * C;
+        for (int k = 0; k < C; k++) {
+            int16_t v = 0;
+            if (i < n) {
+                const int64_t q = i * C + k;
+                const int g0 = mul16(lo16(xb[q]), fac[0]);
+                const int g1 = mul16(lo16(xb[snloc + q]), fac[1]);
+                const int g2 = mul16(lo16(xb[2 * snloc + q]), fac[2]);
+                const int lm = i < n1 ? (int)sat16(g0 + g1) : 0;     // the first overlay's length
+                v = sat16(lm + g2);
+            }
+            o[k] = v;
+        }
+    }
+}
+
+hipError_t launch_mc_rms(const DynLaunch &d, const ChunkDev *schunks, const int16_t *bands, int64_t snloc,
+                         int C, uint16_t *m, int *bact) {
+    if (d.look > AMX_RMS_MAXLOOK || C < 1 || C > 8) return hipErrorInvalidValue;
+    hipError_t e = launch_zero(bact, 3 * sizeof(int), d.st);       // (k_xover2 clears them for C = 2)
+    if (e != hipSuccess) return e;
+    const uint32_t *x = reinterpret_cast<const uint32_t *>(bands);
+#define MCR(LPV)                                                                                   \
+    {                                                                                              \
+        constexpr int F = AMX_RMS_N - LPV;                                                         \
+        dim3 g((unsigned)((d.max_chunk_n + F - 1) / F), (unsigned)d.n_chunks, 3);                  \
+        if (!empty(g))                                                                             \
+            hipLaunchKernelGGL(k_mc_rms<LPV>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, schunks, x, \
+                               snloc, C, m, d.nloc, bact);                                         \
+    }
+    if (d.look <= 256) MCR(256) else if (d.look <= 512) MCR(512) else MCR(1024)
+#undef MCR
+    return hipGetLastError();
+}
+
+hipError_t launch_mc_gain_overlay(const DynLaunch &d, const ChunkDev *schunks, const uint16_t *m,
+                                  const double *ck, const int16_t *bands, int64_t snloc, int C,
+                                  int64_t max_chunk_out, const int64_t *n1tab, const int *bact, int16_t *out) {
+    dim3 g((unsigned)((max_chunk_out + AMX_ENV_TF_ * AMX_BLOCK - 1) / (AMX_ENV_TF_ * AMX_BLOCK)),
+           (unsigned)d.n_chunks);
+    if (empty(g)) return hipSuccess;
+    const uint32_t *x = reinterpret_cast<const uint32_t *>(bands);
+    if (d.rcp)
+        hipLaunchKernelGGL(k_mc_gain_overlay<true>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, schunks, m,
+                           d.tabs, ck, x, snloc, d.nloc, C, n1tab, bact, out);
+    else
+        hipLaunchKernelGGL(k_mc_gain_overlay<false>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks, schunks, m,
+                           d.tabs, ck, x, snloc, d.nloc, C, n1tab, bact, out);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- launchers
 template <int LP>
 static void rms_t(const DynLaunch &d, const int16_t *bands, uint16_t *m, int *bact) {

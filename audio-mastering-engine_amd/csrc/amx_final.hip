@@ -165,6 +165,7 @@ struct LimArgs {
     const uint32_t *x, *halo;
     int halo_frames, fs, bs, seg_frames, warm_frames, max_segs, fast;
     int from_rest;          // amx_final_desc.from_rest: every span starts fresh, `state` is out only
+    double *att;            // [out frames] each output frame's att (amx_plan_set_limiter_trace), or NULL
     int64_t warm_cap;
     const double *gains;
     const int32_t *ctl;
@@ -179,6 +180,7 @@ struct LimArgs {
 struct Lim {
     const uint32_t *xs, *hl;    // span input (x + out_off), the track's halo row
     uint32_t *ys;
+    double *as;                 // the span's att trace (LimArgs.att), or NULL
     int64_t n, tframe0;
     double g, level_in, level, level_out, limit, release;
     int fs, bs, halo, P0;
@@ -277,7 +279,7 @@ __device__ __forceinline__ double lim_readlane(double v, int k) {
 // frame k's dst in o0, o1.  Stops after the first frame that leaves the state
 // IDLE (nowidle).  Returns the frames done.
 __device__ int lim_seq(Lim &L, int nb, int pos, double s0v, double s1v, double d0v, double d1v,
-                       double &o0, double &o1, bool &nowidle) {
+                       double &o0, double &o1, double &oa, bool &nowidle) {
     const int lane = threadIdx.x & 63;
     const int bs = L.bs, channels = 2;
     const double limit = L.limit;
@@ -355,6 +357,7 @@ __device__ int lim_seq(Lim &L, int nb, int pos, double s0v, double s1v, double d
         peak = fmax(fmax(0.0, fabs(b0)), fabs(b1));
         att += delta;
         const double dst0 = b0 * att, dst1 = b1 * att;
+        const double att_used = att;
         if (bp == head) {
             amx_wave_sync();
             delta = nextdelta[nextiter];
@@ -378,6 +381,7 @@ __device__ int lim_seq(Lim &L, int nb, int pos, double s0v, double s1v, double d
         if (lane == k) {
             o0 = dst0;
             o1 = dst1;
+            oa = att_used;
         }
         pos = bp;
         k++;
@@ -451,6 +455,7 @@ __device__ void lim_run(Lim &L, int64_t f, int64_t fend, bool idle) {
                         v1 = L.buffer[r + 1];
                     }
                     L.ys[i] = pack2(lim_out(L, v0 * 1.0), lim_out(L, v1 * 1.0));
+                    if (L.as) L.as[i] = 1.0;
                 }
                 if (bal) { tgt = stop; break; }
             }
@@ -477,9 +482,12 @@ __device__ void lim_run(Lim &L, int64_t f, int64_t fend, bool idle) {
                 }
             }
             bool nowidle = false;
-            double o0 = 0.0, o1 = 0.0;
-            const int kd = lim_seq(L, nb, lim_pos(L, f), s0, s1, d0, d1, o0, o1, nowidle);
-            if (OUT && lane < kd) L.ys[f + lane] = pack2(lim_out(L, o0), lim_out(L, o1));
+            double o0 = 0.0, o1 = 0.0, oa = 1.0;
+            const int kd = lim_seq(L, nb, lim_pos(L, f), s0, s1, d0, d1, o0, o1, oa, nowidle);
+            if (OUT && lane < kd) {
+                L.ys[f + lane] = pack2(lim_out(L, o0), lim_out(L, o1));
+                if (L.as) L.as[f + lane] = oa;
+            }
             f += kd;
             idle = nowidle;
         }
@@ -530,6 +538,7 @@ __device__ void limiter_block(const LimArgs &a, int bx, int nbx, double *lim_lds
     L.xs = a.x + sp.out_off;
     L.hl = a.halo + (int64_t)t * a.halo_frames;
     L.ys = a.y + sp.out_off;
+    L.as = a.att ? a.att + sp.out_off : nullptr;
     L.n = sp.out_n;
     L.tframe0 = sp.tframe0;
     L.g = a.gains[t];
@@ -677,6 +686,70 @@ hipError_t limiter_allow_lds(size_t bytes) {
     return e;
 }
 
+// ------------------------------------------------ more than two channels (round 6)
+// af_alimiter's state (att, delta, the pending-peak list) evolves from each frame's
+// largest |gained sample| alone: the peak over the channels when a frame enters, and
+// that of the delayed frame (the ring only ever holds input samples; its list entries
+// are compared through their frames' peaks).  So a stereo run over a "peak signal" --
+// per frame the sample of the loudest channel in both channels -- goes through the same
+// states, and its att trace (amx_plan_set_limiter_trace) gives every channel's output.
+__global__ void __launch_bounds__(AMX_BLOCK) k_mc_peak_pick(const int16_t *__restrict__ y, int64_t frames,
+                                                           int C, const double *__restrict__ gain,
+                                                           uint32_t *__restrict__ syn) {
+    const int64_t f = (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x;
+    if (f >= frames) return;
+    const double g = gain[0];
+    const int16_t *row = y + f * C;
+    int16_t best = row[0];
+    int bv = abs((int)gain16(best, g));
+    for (int k = 1; k < C; k++) {
+        const int16_t v = row[k];
+        const int a = abs((int)gain16(v, g));
+        if (a > bv) { bv = a; best = v; }
+    }
+    syn[f] = pack2(best, best);
+}
+
+// out[f][c] = the limiter output of channel c's gained sample B - 1 frames earlier (0
+// before the track) x att[f] -- the operations of lim_run / af_alimiter per channel
+__global__ void __launch_bounds__(AMX_BLOCK) k_mc_limiter_out(const int16_t *__restrict__ y, int64_t frames,
+                                                             int C, int halo, const double *__restrict__ gains,
+                                                             const int32_t *__restrict__ ctl,
+                                                             const double *__restrict__ att, double level_in,
+                                                             double level, double level_out, double limit,
+                                                             int16_t *__restrict__ out) {
+    const int64_t f = (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x;
+    if (f >= frames) return;
+    const double g = gains[0];
+    const bool fast = (ctl[0] & AMX_CTL_FAST) != 0;
+    const double a = fast ? 1.0 : att[f];
+    const int64_t src = f - halo;
+    for (int k = 0; k < C; k++) {
+        const double b = src >= 0 ? ((double)gain16(y[src * C + k], g) * (1.0 / 32768.0)) * level_in : 0.0;
+        double v = b * a;
+        v = v < -limit ? -limit : (v > limit ? limit : v);
+        v = v * level * level_out;
+        out[f * C + k] = clip_llrint(v * 32768.0);
+    }
+}
+
+hipError_t launch_mc_peak_pick(const int16_t *y, int64_t frames, int C, const double *gain, int16_t *syn,
+                               hipStream_t st) {
+    if (frames <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mc_peak_pick, dim3((unsigned)((frames + AMX_BLOCK - 1) / AMX_BLOCK)), dim3(AMX_BLOCK), 0,
+                       st, y, frames, C, gain, reinterpret_cast<uint32_t *>(syn));
+    return hipGetLastError();
+}
+
+hipError_t launch_mc_limiter_out(const int16_t *y, int64_t frames, int C, int halo_frames, const double *gains,
+                                 const int32_t *ctl, const double *att, double level_in, double level,
+                                 double level_out, double limit, int16_t *out, hipStream_t st) {
+    if (frames <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mc_limiter_out, dim3((unsigned)((frames + AMX_BLOCK - 1) / AMX_BLOCK)), dim3(AMX_BLOCK),
+                       0, st, y, frames, C, halo_frames, gains, ctl, att, level_in, level, level_out, limit, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, const int16_t *x,
                         const int16_t *halo, int halo_frames, const double *gains,
                         const int32_t *ctl, int fast, int fs, double level_in, double level,
@@ -700,6 +773,7 @@ hipError_t launch_final(const SpanDev *spans, int n_tracks, int64_t max_span, co
     a.y = reinterpret_cast<uint32_t *>(y);
     fa.fast_cols = (ctl != nullptr || fast) ? (int)((max_span + per - 1) / per) : 0;
     fa.gate = ls.gate;
+    a.att = ls.att;
     size_t lds = 0;
     if (general) {
         lds = limiter_lds_bytes(buffer_size);

@@ -164,7 +164,7 @@ struct ScanPlan {
     const double *Mbk;   // (A^{L S})^k, k = 1 .. K-1
 };
 hipError_t launch_front1(const Launch &l, int D, int win, bool analog, const float *in,
-                         const float *lut, int16_t *a16, const double *G, double *e);
+                         const float *lut, int16_t *a16, const double *G, double *e, bool sc = false);
 // tailP / tail (the K filter, D = 4): the down sweep also writes each stream's end state
 // P_t s_last + e_last (k_kw_tail's product) from its last block
 hipError_t launch_scan(const ScanPlan &p, const double *e, double *s, const double *carry,
@@ -172,7 +172,8 @@ hipError_t launch_scan(const ScanPlan &p, const double *e, double *s, const doub
                        double *tail = nullptr);
 hipError_t launch_front2(const Launch &l, int mask, const int16_t *a16, const double *s_eq,
                          int16_t *dst, int to_out, const double *Gx, double *e_x,
-                         const double *Gkw, double *e_kw, uint32_t *pk);
+                         const double *Gkw, double *e_kw, uint32_t *pk, bool sc = false,
+                         const float *slut = nullptr);
 hipError_t launch_xover2(const Launch &l, const int16_t *p16, const double *s_x,
                          int16_t *bands, int64_t nloc, int *bact);
 struct DynLaunch {
@@ -189,6 +190,23 @@ struct DynLaunch {
     int env_wg, env_pin;         // k_env0: waves per workgroup, one workgroup per CU
 };
 hipError_t launch_rms(const DynLaunch &d, const int16_t *bands, uint16_t *m, int *bact);
+// C > 2 channels (round 6): the bands of a stream sub-plan (schunks, snloc), r / the
+// checkpoints / the output on the real frames of the plan in d
+hipError_t launch_mc_rms(const DynLaunch &d, const ChunkDev *schunks, const int16_t *bands, int64_t snloc,
+                         int C, uint16_t *m, int *bact);
+hipError_t launch_mc_gain_overlay(const DynLaunch &d, const ChunkDev *schunks, const uint16_t *m,
+                                  const double *ck, const int16_t *bands, int64_t snloc, int C,
+                                  int64_t max_chunk_out, const int64_t *n1tab, const int *bact, int16_t *out);
+hipError_t launch_mc_pack(const void *in, int64_t samples, int in_s16, uint32_t *pairs, hipStream_t st);
+hipError_t launch_mc_unpack(const uint32_t *pairs, int64_t samples, int16_t *out, hipStream_t st);
+hipError_t launch_mc_split_pairs(const int16_t *y, int64_t frames, int C, int16_t *pairs, hipStream_t st);
+hipError_t launch_mc_loudness_combine(const double *hops, int64_t max_hops, const double *peak, int C,
+                                      double *hops1, double *peak1, hipStream_t st);
+hipError_t launch_mc_peak_pick(const int16_t *y, int64_t frames, int C, const double *gain, int16_t *syn,
+                               hipStream_t st);
+hipError_t launch_mc_limiter_out(const int16_t *y, int64_t frames, int C, int halo_frames, const double *gains,
+                                 const int32_t *ctl, const double *att, double level_in, double level,
+                                 double level_out, double limit, int16_t *out, hipStream_t st);
 // input decode: PCM of any supported format -> stereo s16 frames (amx_io.hip)
 hipError_t launch_zero(void *p, size_t bytes, hipStream_t st);   // a kernel, never a memset node
 hipError_t launch_pcm_to_s16(const void *raw, int64_t frames, int channels, int fmt, int16_t *out,
@@ -362,6 +380,7 @@ struct LimScratch {
     int seg_frames = 0, warm_frames = 0, max_segs = 0, buffer_size = 0;
     int64_t warm_cap = 0;          // furthest warm-up start before a segment, frames
     const int32_t *gate = nullptr; // amx_plan_set_gate: k_final returns unless dynamic
+    double *att = nullptr;         // amx_plan_set_limiter_trace: per output frame att, or NULL
 };
 size_t limiter_lds_bytes(int buffer_size);
 #define AMX_LIM_LDS_MAX (160 * 1024)   // gfx950: one workgroup may hold a CU's whole LDS

@@ -80,12 +80,29 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_pcm_to_s16(const uint8_t *__restr
     }
 }
 
+// a file with C > 2 channels: every sample to s16 in place of its layout ([frames][C],
+// no duplication), what ffmpeg's split writes for it
+template <int FMT>
+__global__ void __launch_bounds__(AMX_BLOCK) k_pcm_to_s16_flat(const uint8_t *__restrict__ raw,
+                                                               int64_t samples,
+                                                               int16_t *__restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * AMX_BLOCK;
+    for (int64_t i = (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x; i < samples; i += stride)
+        out[i] = pcm_sample<FMT>(raw, i);
+}
+
 template <int FMT>
 static hipError_t pcm_t(const uint8_t *raw, int64_t frames, int channels, uint32_t *out,
                         hipStream_t st) {
     const int64_t want = (frames + AMX_BLOCK - 1) / AMX_BLOCK;
     const unsigned g = (unsigned)(want < 8192 ? (want > 0 ? want : 1) : 8192);
-    if (channels == 2)
+    if (channels > 2) {
+        const int64_t ns = frames * channels;
+        const int64_t wf = (ns + AMX_BLOCK - 1) / AMX_BLOCK;
+        const unsigned gf = (unsigned)(wf < 8192 ? (wf > 0 ? wf : 1) : 8192);
+        hipLaunchKernelGGL(k_pcm_to_s16_flat<FMT>, dim3(gf), dim3(AMX_BLOCK), 0, st, raw, ns,
+                           reinterpret_cast<int16_t *>(out));
+    } else if (channels == 2)
         hipLaunchKernelGGL((k_pcm_to_s16<FMT, 2>), dim3(g), dim3(AMX_BLOCK), 0, st, raw, frames, out);
     else
         hipLaunchKernelGGL((k_pcm_to_s16<FMT, 1>), dim3(g), dim3(AMX_BLOCK), 0, st, raw, frames, out);
@@ -95,7 +112,7 @@ static hipError_t pcm_t(const uint8_t *raw, int64_t frames, int channels, uint32
 hipError_t launch_pcm_to_s16(const void *raw, int64_t frames, int channels, int fmt, int16_t *out,
                              hipStream_t st) {
     if (frames <= 0) return hipSuccess;
-    if (channels != 1 && channels != 2) return hipErrorInvalidValue;
+    if (channels < 1 || channels > 8) return hipErrorInvalidValue;
     const uint8_t *r = reinterpret_cast<const uint8_t *>(raw);
     uint32_t *o = reinterpret_cast<uint32_t *>(out);
     switch (fmt) {
@@ -123,6 +140,98 @@ hipError_t launch_pcm_to_s16(const void *raw, int64_t frames, int channels, int 
 // votes never matched and its walker re-ran 150 segments.
 __global__ void __launch_bounds__(256) k_zero32(uint32_t *p, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0u;
+}
+
+// ----------------------------------------- more than two channels (round 6)
+// The C-channel file as ONE interleaved stream (:252) in the L channel of pseudo-stereo
+// int16 pairs (R = 0): stream sample q = input sample q.  float32 input takes ffmpeg's
+// s16 conversion (A.1) per sample.
+__global__ void __launch_bounds__(256) k_mc_pack(const void *__restrict__ in, int64_t samples, int in_s16,
+                                                 uint32_t *__restrict__ pairs) {
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < samples; q += (int64_t)gridDim.x * 256) {
+        const int16_t v = in_s16 ? reinterpret_cast<const int16_t *>(in)[q]
+                                 : q_f32_to_s16_ffmpeg(reinterpret_cast<const float *>(in)[q]);
+        pairs[q] = (uint32_t)(uint16_t)v;
+    }
+}
+__global__ void __launch_bounds__(256) k_mc_unpack(const uint32_t *__restrict__ pairs, int64_t samples,
+                                                   int16_t *__restrict__ out) {
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < samples; q += (int64_t)gridDim.x * 256)
+        out[q] = (int16_t)(uint16_t)(pairs[q] & 0xffffu);
+}
+// channel pairs (0,1), (2,3), ... of y [frames][C] as stereo tracks [P][frames][2]
+__global__ void __launch_bounds__(256) k_mc_split_pairs(const int16_t *__restrict__ y, int64_t frames, int C,
+                                                        int16_t *__restrict__ pairs) {
+    const int P = (C + 1) / 2;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < frames * P; q += (int64_t)gridDim.x * 256) {
+        const int p = (int)(q / frames);
+        const int64_t f = q - (int64_t)p * frames;
+        const int16_t l = y[f * C + 2 * p];
+        const int16_t r = 2 * p + 1 < C ? y[f * C + 2 * p + 1] : (int16_t)0;
+        reinterpret_cast<uint32_t *>(pairs)[q] = pack2(l, r);
+    }
+}
+// libebur128's default channel map (ebur128_init_channel_map): 4 channels L R Ls Rs, 5
+// L R C Ls Rs, otherwise L R C unused Ls Rs, later channels unused; the surrounds
+// (Mp110 / Mm110) weigh 1.41 (ebur128_calc_gating_block)
+__device__ __forceinline__ double ebur_weight(int C, int c) {
+    if (C == 4) return c < 2 ? 1.0 : 1.41;
+    if (C == 5) return c < 3 ? 1.0 : 1.41;
+    return c < 3 ? 1.0 : (c == 3 ? 0.0 : (c < 6 ? 1.41 : 0.0));
+}
+__global__ void __launch_bounds__(256) k_mc_loudness_combine(const double *__restrict__ hops, int64_t max_hops,
+                                                             const double *__restrict__ peak, int C,
+                                                             double *__restrict__ hops1, double *__restrict__ peak1) {
+    const int P = (C + 1) / 2;
+    for (int64_t h = (int64_t)blockIdx.x * 256 + threadIdx.x; h < max_hops; h += (int64_t)gridDim.x * 256) {
+        double sum = 0.0;
+        for (int c = 0; c < C; c++) {
+            const double w = ebur_weight(C, c);
+            if (w == 0.0) continue;                           // FF_EBUR128_UNUSED
+            double e = hops[((int64_t)(c >> 1) * max_hops + h) * 2 + (c & 1)];
+            if (w != 1.0) e *= w;
+            sum += e;
+        }
+        hops1[2 * h] = sum;
+        hops1[2 * h + 1] = 0.0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        double m192 = 0.0, mout = 0.0;
+        for (int p = 0; p < P; p++) {
+            m192 = fmax(m192, fmax(peak[4 * p], peak[4 * p + 1]));
+            mout = fmax(mout, fmax(peak[4 * p + 2], peak[4 * p + 3]));
+        }
+        peak1[0] = peak1[1] = m192;
+        peak1[2] = peak1[3] = mout;
+    }
+}
+
+static dim3 grid_stride(int64_t n) {
+    const int64_t g = (n + 255) / 256;
+    return dim3((unsigned)(g < 4096 ? (g > 0 ? g : 1) : 4096));
+}
+hipError_t launch_mc_pack(const void *in, int64_t samples, int in_s16, uint32_t *pairs, hipStream_t st) {
+    if (samples <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mc_pack, grid_stride(samples), dim3(256), 0, st, in, samples, in_s16, pairs);
+    return hipGetLastError();
+}
+hipError_t launch_mc_unpack(const uint32_t *pairs, int64_t samples, int16_t *out, hipStream_t st) {
+    if (samples <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mc_unpack, grid_stride(samples), dim3(256), 0, st, pairs, samples, out);
+    return hipGetLastError();
+}
+hipError_t launch_mc_split_pairs(const int16_t *y, int64_t frames, int C, int16_t *pairs, hipStream_t st) {
+    if (frames <= 0) return hipSuccess;
+    if (C < 1 || C > 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_mc_split_pairs, grid_stride(frames * ((C + 1) / 2)), dim3(256), 0, st, y, frames, C, pairs);
+    return hipGetLastError();
+}
+hipError_t launch_mc_loudness_combine(const double *hops, int64_t max_hops, const double *peak, int C,
+                                      double *hops1, double *peak1, hipStream_t st) {
+    if (C < 1 || C > 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_mc_loudness_combine, grid_stride(max_hops), dim3(256), 0, st, hops, max_hops, peak, C,
+                       hops1, peak1);
+    return hipGetLastError();
 }
 
 hipError_t launch_zero(void *p, size_t bytes, hipStream_t st) {

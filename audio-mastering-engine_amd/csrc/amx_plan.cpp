@@ -342,6 +342,9 @@ struct amx_plan {
     int n_prev = 0;
     double *d_tailpow = nullptr;
     float *d_lut = nullptr;
+    float *d_in_lut = nullptr;     // a stream chain's input table (amx_chain_desc.eq_in_lut), or NULL
+    int sc = 0;                    // a stream chain (amx_chain_desc.stream_chain)
+    double *lim_att = nullptr;     // amx_plan_set_limiter_trace
     float *d_lut_half = nullptr;   // the odd tanh table's half [0, 32768] (k_analog_h), or NULL
     unsigned int *d_pcnt = nullptr;   // k_peak_reduce's per-track block counter (self re-arming)
     int *d_ppart = nullptr;           // its per-block partial maxima
@@ -416,10 +419,13 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         return fail(AMX_EINVAL, "channels_in must be 1 or 2");
     if (desc->analog_on && !desc->tanh_lut)
         return fail(AMX_EINVAL, "analog character needs the float32 tanh table (tanh_lut)");
+    if (desc->stream_chain && (desc->analog_on || desc->width_on || !desc->input_s16 || desc->channels_in != 2))
+        return fail(AMX_EINVAL, "a stream chain takes int16 pairs, without analog character or width");
     *out = nullptr;
     amx_plan *p = new (std::nothrow) amx_plan();
     if (!p) return fail(AMX_ENOMEM, "out of memory");
     p->desc = *desc;
+    p->sc = desc->stream_chain ? 1 : 0;
     const int fs = desc->sample_rate;
     if (desc->env_warm_frames >= 0) p->warm = (desc->env_warm_frames + 127) / 128 * 128;   // whole ring of k_env0 tiles
     if (desc->env_rounds >= 0) p->rounds = desc->env_rounds;
@@ -952,7 +958,8 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
     // the K-filter segment grid equals the chain's when there is no multiband
     // (output frames == input frames) and every chunk but a span's last is whole
     // segments long: k_front2 then does loudness pass 1 on the output it writes
-    p->fuse_kw = (!p->resamp && !p->mb && p->Lkw == p->L && p->n_kseg == p->n_seg && !desc->measure_only) ? 1 : 0;
+    p->fuse_kw = (!p->resamp && !p->mb && p->Lkw == p->L && p->n_kseg == p->n_seg && !desc->measure_only &&
+                  !p->sc) ? 1 : 0;
     for (int c = 0; c < n_chunks && p->fuse_kw; c++) {
         const bool span_last = (c == n_chunks - 1) || (chunks[c + 1].track != chunks[c].track);
         if (!span_last && (p->chunks[c].n % p->L) != 0) p->fuse_kw = 0;
@@ -1129,6 +1136,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         for (const SpanDev &sp : p->spans) p->any_empty_span |= sp.nkseg == 0 ? 1 : 0;
     }
     if (desc->tanh_lut) UP(p->d_lut, desc->tanh_lut, 65536);
+    if (p->sc && desc->eq_in_lut) UP(p->d_in_lut, desc->eq_in_lut, 65536);
     if (desc->tanh_lut && desc->analog_on) {
         // numpy's float32 tanh is odd: lut[32768 - k] == -lut[32768 + k] bit for bit (sign
         // of zero included) for every k; then tanh(s) = sign(s) * half[|s|] with half[k] =
@@ -1211,7 +1219,8 @@ void amx_plan_free(amx_plan *p) {
                     p->d_bounds, p->d_tailpow, p->d_lut, p->d_energies, p->d_carryP,
                     p->d_esegs, p->d_eseg0, p->d_neseg, p->d_pcnt, p->d_ppart,
                     p->lim.seg_state, p->lim.cnt, p->d_obase, p->d_oph, p->d_bank,
-                    p->d_qh, p->d_qt, p->d_slow, p->d_lut_half, p->d_fcnt, p->d_bankn, p->d_owt};
+                    p->d_qh, p->d_qt, p->d_slow, p->d_lut_half, p->d_fcnt, p->d_bankn, p->d_owt,
+                    p->d_in_lut};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     if (p->up_fork) (void)hipEventDestroy(p->up_fork);
@@ -1285,7 +1294,8 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
             d_in = reinterpret_cast<const float *>(dup);
         }
         HIPCHK(amx::launch_front1(l, p->D, (p->cd.chin == 2 && !p->cd.in_s16) ? 2 : 1,
-                                  p->cd.analog_on != 0, d_in, p->d_lut, a16, p->d_G, e));
+                                  p->cd.analog_on != 0, d_in, p->sc ? p->d_in_lut : p->d_lut, a16, p->d_G, e,
+                                  p->sc != 0));
         break;
     case AMX_STAGE_SCAN_EQ:
         if (p->D > 0)
@@ -1294,7 +1304,10 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     case AMX_STAGE_FRONT2:
         if (p->mb)
             HIPCHK(amx::launch_front2(l, p->mask, a16, s, p16, 0, p->d_Gx, ex, nullptr, nullptr,
-                                      nullptr));
+                                      nullptr, p->sc != 0, p->d_in_lut));
+        else if (p->sc)
+            HIPCHK(amx::launch_front2(l, p->mask, a16, s, d_out, 1, nullptr, nullptr, nullptr,
+                                      nullptr, nullptr, true, p->d_in_lut));
         else if (p->fuse_kw)
             HIPCHK(amx::launch_front2(l, p->mask, a16, s, d_out, 1, nullptr, nullptr, p->d_Gkw,
                                       wsp<double>(d_ws, p->o_ekw), wsp<uint32_t>(d_ws, p->o_pk)));
@@ -1756,7 +1769,7 @@ int amx_loudnorm_192k(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, co
 int amx_pcm_to_s16(const void *d_raw, int64_t frames, int32_t channels, int32_t format,
                    int16_t *d_out, void *stream) {
     if (frames < 0 || (frames > 0 && (!d_raw || !d_out))) return fail(AMX_EINVAL, "null argument");
-    if (channels != 1 && channels != 2) return fail(AMX_EINVAL, "channels must be 1 or 2");
+    if (channels < 1 || channels > 8) return fail(AMX_EINVAL, "channels must be 1..8");
     if (format < AMX_PCM_U8 || format > AMX_PCM_F64BE) return fail(AMX_EINVAL, "bad PCM format %d", format);
     HIPCHK(amx::launch_pcm_to_s16(d_raw, frames, channels, format, d_out, (hipStream_t)stream));
     return AMX_OK;
@@ -1765,6 +1778,12 @@ int amx_pcm_to_s16(const void *d_raw, int64_t frames, int32_t channels, int32_t 
 int amx_plan_set_gate(amx_plan *p, const int32_t *d_gate) {
     if (!p) return fail(AMX_EINVAL, "null plan");
     p->gate = d_gate;
+    return AMX_OK;
+}
+
+int amx_plan_set_limiter_trace(amx_plan *p, double *d_att) {
+    if (!p) return fail(AMX_EINVAL, "null plan");
+    p->lim_att = d_att;
     return AMX_OK;
 }
 
@@ -2021,9 +2040,233 @@ int amx_finalize(amx_plan *p, const amx_final_desc *fd, const int16_t *d_x,
         if (rc) return rc;
     }
     p->lim.gate = p->gate;
+    p->lim.att = p->lim_att;
     HIPCHK(amx::launch_final(p->d_spans, p->n_tracks, p->max_span, d_x, d_halo, halo, d_gains, d_ctl,
                              fast ? 1 : 0, p->cd.fs, fd->level_in, level, fd->level_out, fd->limit,
                              fd->release_ms / 1000.0, bs, d_lim_state, sd, fd->from_rest, p->lim, d_y, st));
+    return AMX_OK;
+}
+
+}  // extern "C"
+
+// ==================================================================================
+// More than two channels (round 6).  audio_segment_to_float_array only reshapes a
+// stereo chunk (:252), so a 3..8-channel chunk goes through the chain as ONE
+// interleaved 1-D stream: analog character (its shelves along the stream, :264-265),
+// EQ (:274, float64 result), no width (:268), the crossover along the stream (:303);
+// pydub's compressor and overlay then work on frames of C samples (:306-309).
+//   pa (analog on): a stream chain (stream in L of int16 pairs) whose "EQ" is the
+//      analog character's two shelves, the input through the float32 tanh table;
+//   pb: the stream chain of the EQ (and the crossover bands when multiband);
+//   pc (multiband): a stereo plan over the chunks' real frames whose envelope kernels
+//      (k_env0 + fix-up) run on the C-sample r that k_mc_rms forms from pb's bands;
+//      k_mc_gain_overlay writes the C-channel output.
+struct amx_mc_plan {
+    int C = 0, mb = 0, in_s16 = 0;
+    amx_plan *pa = nullptr, *pb = nullptr, *pc = nullptr;
+    int64_t M = 0;                 // stream samples the pack covers
+    int64_t out_frames = 0;
+    size_t o_pack = 0, o_outa = 0, o_outb = 0, o_wa = 0, o_wb = 0, o_wc = 0, ws_bytes = 0;
+};
+
+extern "C" {
+
+void amx_mc_plan_free(amx_mc_plan *m) {
+    if (!m) return;
+    amx_plan_free(m->pa);
+    amx_plan_free(m->pb);
+    amx_plan_free(m->pc);
+    delete m;
+}
+
+int amx_mc_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t n_chunks, int32_t seg_frames,
+                       amx_mc_plan **out) {
+    if (!desc || !out || n_chunks < 0 || (n_chunks > 0 && !chunks)) return fail(AMX_EINVAL, "null argument");
+    *out = nullptr;
+    const int C = desc->channels_in;
+    if (C < 3 || C > 8) return fail(AMX_EINVAL, "amx_mc_plan_create: %d channels (3..8; 1 or 2: amx_plan_create)", C);
+    if (desc->analog_on && !desc->tanh_lut)
+        return fail(AMX_EINVAL, "analog character needs the float32 tanh table (tanh_lut)");
+    amx_mc_plan *m = new (std::nothrow) amx_mc_plan();
+    if (!m) return fail(AMX_ENOMEM, "out of memory");
+    m->C = C;
+    m->mb = desc->multiband_on ? 1 : 0;
+    m->in_s16 = desc->input_s16 ? 1 : 0;
+    std::vector<amx_chunk> sch((size_t)n_chunks), ach((size_t)n_chunks);
+    int64_t in_end = 0, acc = 0, sum_n = 0;
+    for (int32_t k = 0; k < n_chunks; k++) {
+        if (chunks[k].frames < 0 || chunks[k].in_offset < 0) {
+            delete m;
+            return fail(AMX_EINVAL, "chunk %d: negative offset or length", k);
+        }
+        sch[k] = chunks[k];
+        sch[k].in_offset = chunks[k].in_offset * C;
+        sch[k].frames = chunks[k].frames * C;
+        ach[k] = sch[k];
+        ach[k].in_offset = acc;                       // pb reads pa's output, chunks back to back
+        acc += sch[k].frames;
+        in_end = std::max(in_end, chunks[k].in_offset + chunks[k].frames);
+        sum_n += chunks[k].frames;
+    }
+    m->M = in_end * C;
+    // the stream chains: int16 pairs, the stream in L
+    amx_chain_desc ds = *desc;
+    ds.channels_in = 2;
+    ds.input_s16 = 1;
+    ds.analog_on = 0;
+    ds.tanh_lut = nullptr;
+    ds.width_on = 0;
+    ds.measure_only = 0;
+    ds.stream_chain = 1;
+    ds.eq_in_lut = nullptr;
+    int rc = AMX_OK;
+    if (desc->analog_on) {
+        // x = tanh(float32 s / 32768 * drive) (the table), then low shelf 120 Hz with g =
+        // 10^(cf/20) and high shelf 12 kHz with 10^(1.5 cf/20), both gains > 0: the EQ's
+        // positive-gain shelf form x + (y - x)(g - 1) at stages 0 and 3 (:264-265, :288)
+        amx_chain_desc da = ds;
+        da.multiband_on = 0;
+        for (int s = 0; s < 4; s++) { da.eq_kind[s] = 0; da.eq_gain_db[s] = 0.0; da.eq_gain[s] = 1.0; }
+        da.eq_kind[0] = 1;
+        da.eq_gain[0] = desc->analog_lo_gain;
+        da.eq_gain_db[0] = 20.0 * std::log10(desc->analog_lo_gain);
+        da.eq_kind[3] = 1;
+        da.eq_gain[3] = desc->analog_hi_gain;
+        da.eq_gain_db[3] = 20.0 * std::log10(desc->analog_hi_gain);
+        for (int k = 0; k < 6; k++) {
+            da.eq_coef[0][k] = desc->analog_lo_ba[k];
+            da.eq_coef[3][k] = desc->analog_hi_ba[k];
+        }
+        if (!(da.eq_gain_db[0] > 0.0 && da.eq_gain_db[3] > 0.0)) {
+            delete m;
+            return fail(AMX_EINVAL, "analog character gains must be > 1");
+        }
+        da.eq_in_lut = desc->tanh_lut;
+        rc = amx_plan_create(&da, sch.data(), n_chunks, nullptr, nullptr, seg_frames, &m->pa);
+        if (rc) { amx_mc_plan_free(m); return rc; }
+    }
+    rc = amx_plan_create(&ds, desc->analog_on ? ach.data() : sch.data(), n_chunks, nullptr, nullptr, seg_frames,
+                         &m->pb);
+    if (rc) { amx_mc_plan_free(m); return rc; }
+    if (m->mb) {
+        amx_chain_desc dc = *desc;
+        dc.channels_in = 2;
+        dc.input_s16 = 1;
+        dc.analog_on = 0;
+        dc.tanh_lut = nullptr;
+        dc.width_on = 0;
+        dc.measure_only = 0;
+        dc.stream_chain = 0;
+        dc.eq_in_lut = nullptr;
+        for (int s = 0; s < 4; s++) { dc.eq_kind[s] = 0; dc.eq_gain_db[s] = 0.0; dc.eq_gain[s] = 1.0; }
+        rc = amx_plan_create(&dc, chunks, n_chunks, nullptr, nullptr, seg_frames, &m->pc);
+        if (rc) { amx_mc_plan_free(m); return rc; }
+        m->out_frames = m->pc->out_frames;
+    } else {
+        m->out_frames = sum_n;
+    }
+    size_t off = 0;
+    auto take = [&](size_t bytes) { const size_t at = off; off += (bytes + 255) / 256 * 256; return at; };
+    m->o_pack = take((size_t)std::max<int64_t>(m->M, 1) * 4);
+    if (m->pa) m->o_outa = take((size_t)std::max<int64_t>(m->pa->out_frames, 1) * 4);
+    if (!m->mb) m->o_outb = take((size_t)std::max<int64_t>(m->pb->out_frames, 1) * 4);
+    if (m->pa) m->o_wa = take(m->pa->ws_bytes);
+    m->o_wb = take(m->pb->ws_bytes);
+    if (m->pc) m->o_wc = take(m->pc->ws_bytes);
+    m->ws_bytes = off;
+    *out = m;
+    return AMX_OK;
+}
+
+int amx_mc_plan_get_info(const amx_mc_plan *m, int64_t *workspace_bytes, int64_t *out_frames) {
+    if (!m || !workspace_bytes || !out_frames) return fail(AMX_EINVAL, "null argument");
+    *workspace_bytes = (int64_t)m->ws_bytes;
+    *out_frames = m->out_frames;
+    return AMX_OK;
+}
+
+int amx_mc_run_chunks(amx_mc_plan *m, const void *d_in, int16_t *d_out, void *d_ws, void *stream) {
+    if (!m || (m->M > 0 && (!d_in || !d_out || !d_ws))) return fail(AMX_EINVAL, "null argument");
+    if (m->M == 0) return AMX_OK;
+    hipStream_t st = (hipStream_t)stream;
+    char *w = reinterpret_cast<char *>(d_ws);
+    uint32_t *pack = reinterpret_cast<uint32_t *>(w + m->o_pack);
+    HIPCHK(amx::launch_mc_pack(d_in, m->M, m->in_s16, pack, st));
+    const float *src = reinterpret_cast<const float *>(pack);
+    if (m->pa) {
+        int16_t *outa = reinterpret_cast<int16_t *>(w + m->o_outa);
+        int rc = amx_run_chunks(m->pa, src, outa, w + m->o_wa, stream);
+        if (rc) return rc;
+        src = reinterpret_cast<const float *>(outa);
+    }
+    amx_plan *pb = m->pb;
+    void *wb = w + m->o_wb;
+    if (!m->mb) {
+        int16_t *outb = reinterpret_cast<int16_t *>(w + m->o_outb);
+        int rc = amx_run_chunks(pb, src, outb, wb, stream);
+        if (rc) return rc;
+        HIPCHK(amx::launch_mc_unpack(reinterpret_cast<const uint32_t *>(outb), m->out_frames * m->C, d_out, st));
+        return AMX_OK;
+    }
+    // the stream's EQ and crossover bands (pb), then the compressor on C-sample frames
+    for (int s = AMX_STAGE_FRONT1; s <= AMX_STAGE_XOVER; s++) {
+        int rc = amx_run_stage(pb, s, src, d_out, wb, stream);
+        if (rc) return rc;
+    }
+    amx_plan *pc = m->pc;
+    void *wc = w + m->o_wc;
+    amx::DynLaunch dl{pc->d_cd,    pc->d_chunks, pc->n_chunks, pc->d_esegs, pc->n_es,
+                      pc->d_eseg0, pc->d_neseg,  pc->nloc,     pc->max_chunk_n, pc->cd.look,
+                      pc->warm,    pc->Le,       pc->cd.env_rcp, pc->d_tabs, st,
+                      pc->env_wg,  pc->env_pin};
+    const int16_t *bands = wsp<int16_t>(wb, pb->o_bands);
+    uint16_t *mframe = wsp<uint16_t>(wc, pc->o_m);
+    int *bact = wsp<int>(wc, pc->o_eflags) + AMX_ENV_BACT;
+    HIPCHK(amx::launch_mc_rms(dl, pb->d_chunks, bands, pb->nloc, m->C, mframe, bact));
+    for (int s : {AMX_STAGE_ENV, AMX_STAGE_FIX}) {
+        int rc = amx_run_stage(pc, s, reinterpret_cast<const float *>(d_in), d_out, wc, stream);
+        if (rc) return rc;
+    }
+    HIPCHK(amx::launch_mc_gain_overlay(dl, pb->d_chunks, mframe, wsp<double>(wc, pc->o_gain), bands, pb->nloc,
+                                       m->C, pc->max_chunk_out, pc->d_n1, bact, d_out));
+    return AMX_OK;
+}
+
+int amx_mc_split_pairs(const int16_t *d_y, int64_t frames, int32_t channels, int16_t *d_pairs, void *stream) {
+    if (frames > 0 && (!d_y || !d_pairs)) return fail(AMX_EINVAL, "null argument");
+    HIPCHK(amx::launch_mc_split_pairs(d_y, frames, channels, d_pairs, (hipStream_t)stream));
+    return AMX_OK;
+}
+
+int amx_mc_loudness_combine(const double *d_hops, int64_t max_hops, const double *d_peak, int32_t channels,
+                            double *d_hops1, double *d_peak1, void *stream) {
+    if (!d_hops || !d_peak || !d_hops1 || !d_peak1 || max_hops <= 0) return fail(AMX_EINVAL, "null argument");
+    HIPCHK(amx::launch_mc_loudness_combine(d_hops, max_hops, d_peak, channels, d_hops1, d_peak1,
+                                           (hipStream_t)stream));
+    return AMX_OK;
+}
+
+int amx_mc_peak_pick(const int16_t *d_y, int64_t frames, int32_t channels, const double *d_gain, int16_t *d_syn,
+                     void *stream) {
+    if (frames > 0 && (!d_y || !d_gain || !d_syn)) return fail(AMX_EINVAL, "null argument");
+    if (channels < 1 || channels > 8) return fail(AMX_EINVAL, "%d channels", channels);
+    HIPCHK(amx::launch_mc_peak_pick(d_y, frames, channels, d_gain, d_syn, (hipStream_t)stream));
+    return AMX_OK;
+}
+
+int amx_mc_limiter_out(const amx_plan *p, const amx_final_desc *fd, const int16_t *d_y, int32_t channels,
+                       const double *d_gains, const int32_t *d_ctl, const double *d_att, int16_t *d_out,
+                       void *stream) {
+    if (!p || !fd || !d_gains || !d_ctl || (p->out_frames > 0 && (!d_y || !d_att || !d_out)))
+        return fail(AMX_EINVAL, "null argument");
+    if (channels < 1 || channels > 8) return fail(AMX_EINVAL, "%d channels", channels);
+    if (p->n_tracks != 1 || p->spans[0].tframe0 != 0) return fail(AMX_EINVAL, "one whole track per plan");
+    int32_t bs = 0, halo = 0;
+    int64_t sd = 0;
+    if (int rc = amx_limiter_geometry(p, fd, &bs, &halo, &sd)) return rc;
+    const double level = fd->auto_level ? 1 / fd->limit : 1;
+    HIPCHK(amx::launch_mc_limiter_out(d_y, p->out_frames, channels, halo, d_gains, d_ctl, d_att, fd->level_in,
+                                      level, fd->level_out, fd->limit, d_out, (hipStream_t)stream));
     return AMX_OK;
 }
 

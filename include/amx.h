@@ -101,6 +101,18 @@ typedef struct amx_chain_desc {
      * values, these only move work between the speculative and the fix-up passes */
     int32_t env_warm_frames;      /* speculative warm-up per envelope segment (rounded up to 128); <0 -> 2304 */
     int32_t env_rounds;           /* parallel fix-up rounds before the in-order walk (0..16); <0 -> 2 */
+    /* (ABI 4) a chain over ONE interleaved 1-D stream: the sub-plans amx_mc_plan_create
+     * builds for a file with more than two channels (audio_segment_to_float_array only
+     * reshapes stereo, :252).  The stream is the L channel of a pseudo-stereo int16
+     * buffer (R = 0).  stream_chain = 1: the EQ result is clipped and scaled in float64
+     * when a stage ran (the 1-D branch of :273-275 keeps float64), in float32 when none
+     * did; width, analog and mono input are refused.  eq_in_lut (nullable): the input
+     * sample s enters the EQ as eq_in_lut[s + 32768] instead of s / 32768 (the analog
+     * character of a stream: float32 tanh, then its two shelves ALONG the stream, run
+     * as EQ stages 0 and 3). */
+    int32_t stream_chain;
+    int32_t pad_sc_;
+    const float *eq_in_lut;
 } amx_chain_desc;
 
 /* One ~30 s chunk of one track (the ffmpeg segment split, :178). */
@@ -192,8 +204,9 @@ AMX_API int amx_run_stage(amx_plan *plan, int32_t stage, const float *d_in, int1
 /* Input decode (the s16 conversion of ffmpeg's segment split, :178, + pydub's
  * set_channels(2), :190): d_raw holds `frames` interleaved frames of `channels` (1 or
  * 2) samples in `format`; d_out [frames][2] int16 receives what the split's s16 WAV
- * chunks hold, mono duplicated to L = R.  Asynchronous on the stream.  A float32
- * file needs no call: amx_run_chunks quantises it (input_s16 = 0). */
+ * chunks hold, mono duplicated to L = R.  (ABI 4) channels 3..8: d_out is int16
+ * [frames][channels], no duplication (the input of amx_mc_run_chunks).  Asynchronous on
+ * the stream.  A float32 file needs no call: amx_run_chunks quantises it (input_s16 = 0). */
 #define AMX_PCM_U8 0      /* (v - 0x80) << 8 */
 #define AMX_PCM_S16 1     /* v */
 #define AMX_PCM_S24 2     /* 3-byte little-endian; v >> 8 */
@@ -455,6 +468,52 @@ AMX_API int amx_kw_carry_rows(amx_plan *plan, const double *d_rows, int32_t worl
 AMX_API int amx_finalize(amx_plan *plan, const amx_final_desc *fd, const int16_t *d_x,
                  const double *d_gains, const int32_t *d_ctl, int32_t fast, const int16_t *d_halo,
                  int16_t *d_y, double *d_lim_state, void *d_ws, void *stream);
+
+/* (ABI 4) The general limiter also writes every output frame's gain att (the value
+ * its dst = delayed sample x att uses; 1 on idle stretches) to d_att [out_frames]
+ * doubles, or stops (NULL).  The idle path (AMX_CTL_FAST) writes nothing: att = 1. */
+AMX_API int amx_plan_set_limiter_trace(amx_plan *plan, double *d_att);
+
+/* ---------------------------------------------------------------------------------
+ * (ABI 4) Files with more than two channels (3..8).  The reference keeps such a chunk
+ * as ONE interleaved 1-D stream (:252): analog character, EQ and crossover run along
+ * it (:264-265, :274, :303), width leaves it alone (:268), pydub's compressor and
+ * overlay work on frames of C samples (:306-309); ffmpeg's loudnorm measures the C
+ * channels with libebur128's default channel map, and the alimiter's gain follows the
+ * largest |sample| of each frame (:223).  The chain runs as pseudo-stereo sub-plans
+ * (the stream in L) plus C-channel compressor kernels. */
+typedef struct amx_mc_plan amx_mc_plan;
+/* desc: the settings as for amx_plan_create, with channels_in = C (3..8) and
+ * input_s16 saying what d_in holds (int16 or float32 [frames][C]); chunks in frames of
+ * the C-channel input.  Replaces :185-214 for such a file. */
+AMX_API int amx_mc_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t n_chunks,
+                               int32_t seg_frames, amx_mc_plan **out);
+AMX_API void amx_mc_plan_free(amx_mc_plan *plan);
+/* workspace bytes for amx_mc_run_chunks, output frames (all chunks) */
+AMX_API int amx_mc_plan_get_info(const amx_mc_plan *plan, int64_t *workspace_bytes, int64_t *out_frames);
+/* the chunk chains of every chunk -> d_out int16 [out_frames][C] (the concat, :211) */
+AMX_API int amx_mc_run_chunks(amx_mc_plan *plan, const void *d_in, int16_t *d_out, void *d_ws, void *stream);
+/* loudnorm's measurement of a C-channel track, from a stereo measure plan run over the
+ * channel pairs (0,1), (2,3), ... as tracks (the last pair of an odd C padded with a
+ * silent channel): d_pairs int16 [ceil(C/2)][frames][2] from d_y int16 [frames][C] */
+AMX_API int amx_mc_split_pairs(const int16_t *d_y, int64_t frames, int32_t channels, int16_t *d_pairs,
+                               void *stream);
+/* the pairs' hop energies [ceil(C/2)][max_hops][2] and peaks [ceil(C/2)][4] -> one
+ * track's [max_hops][2] (sum over channels with libebur128's weights: 1 for L R C, 1.41
+ * for the surrounds, 0 for unused channels; the second column 0) and peaks [4] (max) */
+AMX_API int amx_mc_loudness_combine(const double *d_hops, int64_t max_hops, const double *d_peak,
+                                    int32_t channels, double *d_hops1, double *d_peak1, void *stream);
+/* the alimiter's peak signal: per frame the sample of the channel whose gained |value|
+ * (d_gain[0]: loudnorm's linear gain, <= 0 none) is largest, in both channels of d_syn
+ * int16 [frames][2] -- the limiter's state only ever sees per-frame peaks */
+AMX_API int amx_mc_peak_pick(const int16_t *d_y, int64_t frames, int32_t channels, const double *d_gain,
+                             int16_t *d_syn, void *stream);
+/* the C-channel alimiter output from the peak signal's run (amx_finalize on a stereo
+ * plan over d_syn with amx_plan_set_limiter_trace): out = limiter_out(gained sample
+ * B - 1 frames earlier x att) per channel; d_ctl's AMX_CTL_FAST bit: att = 1 */
+AMX_API int amx_mc_limiter_out(const amx_plan *plan, const amx_final_desc *fd, const int16_t *d_y,
+                               int32_t channels, const double *d_gains, const int32_t *d_ctl,
+                               const double *d_att, int16_t *d_out, void *stream);
 
 #ifdef __cplusplus
 }

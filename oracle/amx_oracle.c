@@ -572,13 +572,29 @@ typedef struct {
     double v[8][5];
     uint64_t *hist, *st_hist;
     double peak[8];
+    double w[8];          /* channel weights of libebur128's default channel map */
     int64_t nb;
 } Ebur;
+
+/* libebur128 ebur128_init_channel_map (FFmpeg's copy; af_loudnorm sets no map of its
+ * own): 4 channels L R Ls Rs, 5 channels L R C Ls Rs, otherwise L R C unused Ls Rs and
+ * every later channel unused.  A block's energy skips unused channels and weights the
+ * surrounds (Mp110 / Mm110) by 1.41 (ebur128_calc_gating_block).  Stereo: 1, 1. */
+EXPORT void orc_ebur128_weights(int channels, double *w) {
+    for (int c = 0; c < channels && c < 8; c++) {
+        double v;
+        if (channels == 4) v = c < 2 ? 1.0 : 1.41;
+        else if (channels == 5) v = c < 3 ? 1.0 : 1.41;
+        else v = c < 3 ? 1.0 : (c == 3 ? 0.0 : (c < 6 ? 1.41 : 0.0));
+        w[c] = v;
+    }
+}
 
 static void ebur_init(Ebur *e, int fs, int channels, uint64_t *hist, uint64_t *st_hist) {
     orc_ebur128_tables(NULL, NULL);
     memset(e, 0, sizeof *e);
     e->channels = channels;
+    orc_ebur128_weights(channels, e->w);
     orc_kweight_coefs(fs, e->b, e->a);
     e->h100 = (size_t)((fs + 5) / 10);
     e->ring_frames = (size_t)fs * 3000 / 1000;
@@ -618,6 +634,7 @@ static double ebur_block_energy(const Ebur *e, size_t fpb) {
     const int ch = e->channels;
     double sum = 0.0;
     for (int c = 0; c < ch; c++) {
+        if (e->w[c] == 0.0) continue;                 /* FF_EBUR128_UNUSED */
         double cs = 0.0;
         if (e->idx < fpb * ch) {
             for (size_t i = 0; i < e->idx / ch; ++i) cs += e->ring[i * ch + c] * e->ring[i * ch + c];
@@ -626,6 +643,7 @@ static double ebur_block_energy(const Ebur *e, size_t fpb) {
         } else {
             for (size_t i = e->idx / ch - fpb; i < e->idx / ch; ++i) cs += e->ring[i * ch + c] * e->ring[i * ch + c];
         }
+        if (e->w[c] != 1.0) cs *= e->w[c];            /* the surrounds' 1.41 */
         sum += cs;
     }
     return sum / (double)fpb;
@@ -1095,6 +1113,14 @@ EXPORT void orc_quantize(const float *x, int64_t n, int channels, int16_t *out) 
             long q = lrintf(v);
             out[2 * i + c] = (int16_t)(q > 32767 ? 32767 : (q < -32768 ? -32768 : q));
         }
+    }
+}
+
+/* A.1 for every sample of a C > 2 channel file (no duplication): n_samples values */
+EXPORT void orc_quantize_flat(const float *x, int64_t n_samples, int16_t *out) {
+    for (int64_t i = 0; i < n_samples; i++) {
+        long q = lrintf(x[i] * 32768.0f);
+        out[i] = (int16_t)(q > 32767 ? 32767 : (q < -32768 ? -32768 : q));
     }
 }
 

@@ -278,6 +278,10 @@ def quantize(x_f32):
     x = np.ascontiguousarray(x_f32, np.float32)
     if x.ndim == 1:
         x = x.reshape(-1, 1)
+    if x.shape[1] > 2:                    # the file's own C channels, no duplication
+        out = np.empty(x.shape, np.int16)
+        lib().orc_quantize_flat(_p(x, _f32p), _i64(x.size), _p(out, _i16p))
+        return out
     out = np.empty((x.shape[0], 2), np.int16)
     lib().orc_quantize(_p(x, _f32p), _i64(x.shape[0]), ctypes.c_int(x.shape[1]), _p(out, _i16p))
     return out
@@ -483,14 +487,17 @@ def pipeline(x, fs, settings, chunks):
     """Whole process_audio_with_ffmpeg_pipeline (:171-226) on CPU.
 
     x: int16 [n, C] (already the ffmpeg s16 conversion) ; chunks: [(start, n)].
-    Returns (int16 output [n', 2], info dict)."""
+    Returns (int16 output [n', max(C, 2)], info dict).  C > 2: chunk_mc per chunk,
+    libebur128's channel weights in the measurement, the C-channel alimiter."""
     x = np.asarray(x)
     if x.ndim == 1:
         x = x.reshape(-1, 1)
     if x.shape[1] == 1:
         x = np.repeat(x, 2, axis=1)
-    outs = [chunk(x[s:s + n], fs, settings) for s, n in chunks]
-    cat = np.concatenate(outs, axis=0) if outs else np.zeros((0, 2), np.int16)
+    C = x.shape[1]
+    body = chunk if C == 2 else chunk_mc           # C > 2: the 1-D stream chain (:252)
+    outs = [body(x[s:s + n], fs, settings) for s, n in chunks]
+    cat = np.concatenate(outs, axis=0) if outs else np.zeros((0, C), np.int16)
     info = {"concat": cat}
     y = cat
     lufs = settings.get("lufs")
