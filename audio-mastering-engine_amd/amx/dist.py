@@ -599,9 +599,9 @@ class ShardedTrack:
         self._wd = None
         if any(kbs[q] >= kbs[q + 1] for q in range(world)) or kbs[world - 1] > kf.value:
             return None
-        xs, us, ys, wsb, ctl = [], [], [], [], []
+        xs, us, ys, wsb, ctl, doff = [], [], [], [], [], []
         for q in range(world):
-            win = (ctypes.c_int64 * 7)()
+            win = (ctypes.c_int64 * 9)()
             b = ctypes.c_int64()
             capi.check(L.amx_loudnorm_192k_shard_window(plan.h, 0, kbs[q], kbs[q + 1], win, ctypes.byref(b)),
                        "amx_loudnorm_192k_shard_window")
@@ -610,6 +610,7 @@ class ShardedTrack:
             ys.append((win[4], win[5]))
             wsb.append(b.value)
             ctl.append(win[6])
+            doff.append((win[7], win[8]))
         before = [max(0, F[q] - xs[q][0]) for q in range(world)]
         after = [max(0, xs[q][1] - F[q + 1]) for q in range(world)]
         if any(before[q] > (self.span_frames[q - 1] if q > 0 else 0) for q in range(world)) or \
@@ -620,6 +621,8 @@ class ShardedTrack:
         Hb, Ha = max(before), max(after)
         wd = {"plan": plan, "keep": keep, "K": K.value, "kb": kbs[r], "ke": kbs[r + 1], "x": xs[r], "u": us[r],
               "y": ys, "F": F, "Hb": Hb, "Ha": Ha, "ctl": ctl[r], "rec_doubles": rd.value,
+              "d_off": doff[r][0], "T": doff[r][1],
+              "qbuf": torch.zeros(3 + max(1, doff[r][1]), dtype=torch.float64, device=dev),
               "ws2": torch.empty(max(1, wsb[r]), dtype=torch.uint8, device=dev),
               "xwin": torch.zeros((max(1, xs[r][1] - xs[r][0]), 2), dtype=torch.int16, device=dev),
               "summ": torch.zeros(16, dtype=torch.float64, device=dev),
@@ -670,8 +673,10 @@ class ShardedTrack:
         (amx_loudnorm_192k_shard, windowed): part 0 (the 192 kHz stream over the u
         window, every frame's statistics from the all-reduced hop energies), part 1
         (gains, the fill pre-pass, the segments from guessed states), then the walks in
-        rank order with the one-record hand-off.  False: the parallel form cannot run
-        this track (a quiet start, a walk fallback) -- every rank takes the same branch."""
+        rank order with the one-record hand-off.  A quiet start runs split first
+        (_quiet_start: rank 0's frames in order up to the hand-over).  False: the parallel
+        form cannot run this track (a walk fallback, a start still quiet past rank 0's
+        segments) -- every rank takes the same branch."""
         import ctypes
         from . import capi
         L = capi.load()
@@ -689,7 +694,10 @@ class ShardedTrack:
 
         ctl = wd["ws2"][wd["ctl"]:wd["ctl"] + 4].view(torch.int32)
         part(0)
-        if int(ctl.item()) != 0:
+        c0 = int(ctl.item())
+        if c0 == 1 and not self._quiet_start(wd, part):
+            return False
+        if c0 not in (0, 1):
             return False
         part(1)
         if rank > 0:
@@ -706,6 +714,41 @@ class ShardedTrack:
         (f,), st = _staged(self.group, flag)
         dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
         return int(f.item()) == 0
+
+    def _quiet_start(self, wd, part):
+        """A track whose first 3 s are below measured_thresh (control word 1 on every rank,
+        the same hop energies): af_loudnorm's gains there follow its own output (a feedback
+        loop, k_ln_dyn frame by frame).  Rank 0 holds the track's start: it runs those frames
+        in order up to the hand-over segment (amx_ln_shard part 3) and broadcasts the control
+        words and the deltas written so far; every rank then runs its own segments as for a
+        loud start (rank 0 from the hand-over record).  False -- the track is still quiet past
+        rank 0's last segment, or a rank's first segment would precede the hand-over: the
+        replicated form, on every rank alike (the words come from the broadcast)."""
+        w = wd["ws2"]
+        ctl = w[wd["ctl"]:wd["ctl"] + 24].view(torch.int32)
+        T, d_off = int(wd["T"]), int(wd["d_off"])
+        D = w[d_off:d_off + 8 * T].view(torch.float64)
+        q = wd["qbuf"]
+        if self.rank == 0:
+            part(3)
+            q[0:3].copy_(ctl[torch.tensor([0, 4, 5], device=ctl.device)].to(torch.float64))
+            q[3:3 + T].copy_(D)
+        (b,), st = _staged(self.group, q)
+        dist.broadcast(b, src=0, group=self.group)
+        if st:
+            q.copy_(b)
+        words = [int(v) for v in q[0:3].tolist()]
+        if words[0] != 4:             # (the same words on every rank: one branch for all)
+            return False
+        # part 3 hands over at a segment below rank 0's last (amx_ln_shard.part 3), so every
+        # other rank's segments start after it
+        if self.rank > 0:
+            ctl[0] = 4
+            ctl[4] = words[1]
+            ctl[5] = words[2]
+            t0 = max(0, words[2] - 1)
+            D[:t0].copy_(q[3:3 + t0])
+        return True
 
     def _dynamic_windowed(self, wd):
         """the reference's two loudnorm passes in dynamic mode (:229 / :240) and the

@@ -294,6 +294,10 @@ struct LnArgs {
     // starts at frame 1 + k lp_Fs, k <= lp_J
     double *lp_D, *lp_recG;
     int lp_Fs, lp_J;
+    // (chunk-sharded quiet start, amx_ln_shard.part 3) the first INNER frame this kernel may
+    // not run: rank 0 holds the frames before it; a track still quiet there is left to
+    // the replicated form (lp_ctl[0] stays 1).  INT_MAX otherwise.
+    int lp_tstop;
 };
 // af_loudnorm dynamic mode in parallel form (amx_loudnorm.hip):
 // per-frame statistics and gains from pass 1's hop energies, then the true-peak

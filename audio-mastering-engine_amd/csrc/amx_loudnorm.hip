@@ -808,6 +808,7 @@ __global__ void __launch_bounds__(LN_NT) k_ln_dyn(LnArgs a0, int phase) {
     // ---- INNER frames (100 ms)
     while (Pin < n) {
         const int t_in = (int)((Pin - LN_FIRST) / LN_FR);     // this INNER frame
+        if (phase == 0 && t_in >= a0.lp_tstop) return;        // (a shard: past rank 0's frames)
         const int nb = (int)(n - Pin < LN_FR ? n - Pin : LN_FR);
         const uint64_t t_fill = clock64();
         const double gain = gauss(index + 10 < 30 ? index + 10 : index + 10 - 30);
@@ -2230,8 +2231,12 @@ hipError_t launch_loudnorm_shard(const LnArgs &ln, const LpArgs &lp, const uint3
         e = launch_zero(lp.match, sizeof(int) * (size_t)(lp.K + 1), st);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_lp_seg, dim3(lp.P), dim3(LP_NT), 0, st, lp);
-    } else {
+    } else if (part == 2) {
         hipLaunchKernelGGL(k_lp_walk, dim3(1), dim3(LP_NT), 0, st, lp);
+    } else {
+        // part 3 (rank 0 of a quiet start): the frames in order from the track start until
+        // the hand-over segment (k_ln_dyn phase 0, bounded by ln.lp_tstop)
+        hipLaunchKernelGGL(k_ln_dyn, dim3(1), dim3(LN_NT), 0, st, ln, 0);
     }
     return hipGetLastError();
 }

@@ -1638,6 +1638,7 @@ int ln_args(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const double
     a.lp_recG = q.recG;
     a.lp_Fs = q.Fs;
     a.lp_J = q.J;
+    a.lp_tstop = INT_MAX;
     q.kb = 0;
     q.ke = q.K;
     // k_lp_fill + the skipping scan + the sparse emit (AMX_LP_FILL=0: the dense form, for
@@ -1671,13 +1672,14 @@ int amx_loudnorm_192k_shard(amx_plan *p, int32_t track, const amx_loudnorm_desc 
                             const double *d_offset_i, const amx_ln_shard *sh, const int16_t *d_out,
                             const double *d_hops, int64_t max_hops, const double *d_peak, int16_t *d_y192,
                             double *d_summary, void *d_ws2, void *stream) {
-    if (!sh || sh->part < 0 || sh->part > 2) return fail(AMX_EINVAL, "bad shard");
+    if (!sh || sh->part < 0 || sh->part > 3) return fail(AMX_EINVAL, "bad shard");
+    if (sh->part == 3 && sh->kb != 0) return fail(AMX_EINVAL, "part 3 (a quiet start) runs on the first segments' rank");
     amx::LnArgs a;
     amx::LpArgs q;
     int64_t n192 = 0;
     if (!p || track < 0 || track >= p->n_tracks) return fail(AMX_EINVAL, "bad argument");
     if (int rc = ln_frames(p, track, &n192)) return rc;
-    int64_t win[7] = {0, 0, sh->u_lo, sh->u_hi, 0, 0, 0};
+    int64_t win[9] = {0, 0, sh->u_lo, sh->u_hi, 0, 0, 0, 0, 0};
     if (sh->windowed || sh->u_lo < 0) {
         int64_t wsb = 0;
         if (int rc = amx_loudnorm_192k_shard_window(p, track, sh->kb, sh->ke, win, &wsb)) return rc;
@@ -1692,6 +1694,9 @@ int amx_loudnorm_192k_shard(amx_plan *p, int32_t track, const amx_loudnorm_desc 
     if (sh->part == 2 && sh->kb > 0 && !sh->d_rec_in) return fail(AMX_EINVAL, "segment %d needs the true state", sh->kb);
     q.kb = sh->kb;
     q.ke = sh->ke;
+    // part 3: a hand-over at segment k needs the INNER frames < k Fs; the last segment this
+    // rank may hand over at is ke - 1 (a later lift: the replicated form)
+    if (sh->part == 3) a.lp_tstop = sh->ke - 1 > 0 ? (sh->ke - 1) * q.Fs : 0;
     q.rec_in = sh->kb > 0 ? sh->d_rec_in : nullptr;
     q.rec_out = sh->ke < q.K ? sh->d_rec_out : nullptr;
     const SpanDev &sp = p->spans[track];
@@ -1737,6 +1742,8 @@ int amx_loudnorm_192k_shard_window(const amx_plan *p, int32_t track, int32_t kb,
     win[5] = ke < lo.K ? ln_seg_base(lo, n192, ke) : n192;
     const LnLayout lw = ln_layout(n192, u_hi - u_lo, ke - kb);
     win[6] = lw.o_ctl;
+    win[7] = lw.o_D;       // (ABI 4) the INNER frames' deltas, T doubles (a quiet start's hand-over)
+    win[8] = lw.T;
     *ws_bytes = lw.total;
     return AMX_OK;
 }

@@ -346,7 +346,14 @@ AMX_API int amx_loudnorm_192k_ex(amx_plan *plan, int32_t track, const amx_loudno
  * frame).  Outputs: d_y192 frames [start(kb), start(ke)) (whole-track positions).
  * Replaces no single reference line: the reference runs the filter on one process. */
 typedef struct amx_ln_shard {
-    /* windowed != 0: the rank holds only windows of the track (amx_loudnorm_192k_shard_window):
+    /* part 0: the 192 kHz stream over the window + every frame's statistics (control word 0:
+     * the parallel form runs, 1: the track starts quietly or is under 3 s); 1: deltas,
+     * gains, the fill pre-pass, segments [kb, ke) from guessed states; 2: the walk from the
+     * true state at kb; (ABI 4) 3, on the rank with kb == 0 after part 0 said 1: a quiet
+     * start's frames in order from the track start until the hand-over segment (control
+     * words 4 / ho_k / ho_f, the deltas before ho_f written), or word 1 still when the track
+     * stays quiet past segment ke - 1 -- the other ranks take the words and deltas from it.
+     * windowed != 0: the rank holds only windows of the track (amx_loudnorm_192k_shard_window):
      * d_out = track frames [x_lo, x_hi), d_y192 = 192 kHz positions [y_lo, y_hi), d_ws2 of
      * the window's size with the stream u over [u_lo, u_hi) only (u_lo / u_hi ignored) */
     int32_t part, kb, ke, windowed;
@@ -364,7 +371,8 @@ AMX_API int amx_loudnorm_192k_shard(amx_plan *plan, int32_t track, const amx_lou
  * [x_lo, x_hi) its resampler reads (its own span plus halos of the neighbours' spans),
  * win[2..3] = the 192 kHz positions [u_lo, u_hi) its segments read, win[4..5] = the output
  * positions [y_lo, y_hi) they emit, win[6] = the byte offset in that d_ws2 of the int32
- * control words; *ws_bytes = the d_ws2 size of the window (the whole-track records stay;
+ * control words; (ABI 4: win holds 9) win[7] = the byte offset of the INNER frames' deltas
+ * (win[8] = T doubles); *ws_bytes = the d_ws2 size of the window (the whole-track records stay;
  * the stream and the limiter waves are the window's).  Per-rank memory and traffic then
  * scale as 1 / ranks. */
 AMX_API int amx_loudnorm_192k_shard_window(const amx_plan *plan, int32_t track, int32_t kb, int32_t ke,

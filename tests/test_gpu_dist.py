@@ -41,9 +41,11 @@ CASES = {
     # resampler form, each rank upsampling only what its segments read
     "dynamic_44k1": dict(bass_boost=1.0, lufs=-14.0),
     # a quiet 6 s intro: the filter starts below measured_thresh (above_threshold 0), a
-    # feedback loop the parallel form does not split -- every rank runs both filter runs
-    # whole, the 192 kHz measurement and alimiter still over the ranks' runs
+    # feedback loop: rank 0 runs those frames in order up to the hand-over segment and
+    # broadcasts the control words and deltas, then every rank runs its own windows
     "dynamic_quiet": dict(bass_boost=1.0, lufs=-14.0),
+    # quiet past rank 0's segments (62 s of 75): the split hand-over cannot run there
+    "dynamic_quiet_long": dict(bass_boost=1.0, lufs=-14.0),
 }
 ENV = {"dynamic_nowarm": {"AMX_LN_SEG": "1", "AMX_LN_WARM": "0"}}
 RATE = {"c3_lufs_44k1": 44100, "dynamic_44k1": 44100}
@@ -52,7 +54,7 @@ RATE = {"c3_lufs_44k1": 44100, "dynamic_44k1": 44100}
 # input gain per case: the loud case drives 0.1 % of the frames over the limit, so the final
 # alimiter (limit 0.98) must engage and the ranks hand its state along
 GAIN = {"c3_lufs": 1.0, "loud_limiter": 1.3, "square_limiter": 1.0, "c3_lufs_44k1": 1.0, "dynamic": 1.0,
-        "dynamic_nowarm": 1.0, "dynamic_44k1": 1.0, "dynamic_quiet": 1.0}
+        "dynamic_nowarm": 1.0, "dynamic_44k1": 1.0, "dynamic_quiet": 1.0, "dynamic_quiet_long": 1.0}
 
 
 def _track(seconds, case):
@@ -68,6 +70,8 @@ def _track(seconds, case):
             x[k:k + 50] += rng.uniform(-0.9, 0.9, (50, 2))
         if case == "dynamic_quiet":
             x[:int(6 * fs)] *= 0.0005
+        if case == "dynamic_quiet_long":
+            x[:int(62 * fs)] *= 0.0005
         return np.clip(x, -1.0, 1.0).astype(np.float32)
     return (synth.mix_like(n, fs, 2, seed=3) * np.float32(GAIN[case])).astype(np.float32)
 
@@ -153,7 +157,9 @@ def test_two_ranks_match_one(gpu, case):
     if case.startswith("dynamic"):
         # both filter runs on the ranks' windows, with the limiter-state hand-off (a quiet
         # start: the whole filter on every rank)
-        want = "replicated" if case == "dynamic_quiet" else "windowed"
+        # a quiet start runs split (rank 0 in order up to the hand-over);
+        # one still quiet past rank 0's segments takes the replicated form
+        want = "replicated" if case == "dynamic_quiet_long" else "windowed"
         assert forms == [want] * 2, forms
     # the loud case must exercise the rank-to-rank sequential limiter
     if not case.startswith("dynamic"):

@@ -570,16 +570,16 @@ def test_shard_windows_vs_oracle(gpu, oracle_mod, monkeypatch, ranks, seg, warm,
     dev = job.device
     wins, bufs = [], []
     for kb, ke in ranges:
-        win, b = (ctypes.c_int64 * 7)(), ctypes.c_int64()
+        win, b = (ctypes.c_int64 * 9)(), ctypes.c_int64()
         capi.check(L.amx_loudnorm_192k_shard_window(job.plan.h, 0, kb, ke, win, ctypes.byref(b)), "window")
-        x0, x1, u0, u1, y0, y1, ctl_off = list(win)
+        x0, x1, u0, u1, y0, y1, ctl_off = list(win)[:7]
         assert 0 <= x0 < x1 <= n and 0 <= u0 < u1 <= n192 and u0 <= y0 < y1 <= u1
         xw = torch.from_numpy(np.ascontiguousarray(x16[x0:x1])).to(dev)
         bufs.append((xw, torch.empty(b.value, dtype=torch.uint8, device=dev),
                      torch.empty((y1 - y0, 2), dtype=torch.int16, device=dev)))
         wins.append((x0, x1, u0, u1, y0, y1, ctl_off))
     # a window of no segments is refused
-    w0, b0 = (ctypes.c_int64 * 7)(), ctypes.c_int64()
+    w0, b0 = (ctypes.c_int64 * 9)(), ctypes.c_int64()
     assert L.amx_loudnorm_192k_shard_window(job.plan.h, 0, 3, 3, w0, ctypes.byref(b0)) != 0
     recs = [torch.zeros(rd.value, dtype=torch.float64, device=dev) for _ in range(ranks)]
     for offset in (0.0, 9.0):
