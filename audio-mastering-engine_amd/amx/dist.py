@@ -940,7 +940,10 @@ class ShardedTrack:
         """One step from the captured graph(s).  Pipelined (N > 1 over RCCL): enqueues
         the step on the next slot, then resolves the previous step (its decision word,
         and the rare hand-off / dynamic path on its own slot); returns this step's
-        output buffer, final after the next replay() or flush()."""
+        linear output buffer.  That buffer is final only after the next replay() or
+        flush(), and only if the step stayed linear: a step that turns out dynamic has its
+        192 kHz output in what flush() returns -- callers that keep a
+        step's output take it from flush() (or the next replay()'s _last_out)."""
         if not self.xchg:
             self._last_out = self._one_rank_dynamic(self.job.replay())
             return self._last_out

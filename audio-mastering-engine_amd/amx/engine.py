@@ -47,10 +47,12 @@ def ln_output_bound(n192):
     """The largest |sample| / 32768 of loudnorm's dynamic-mode output (int16 at 192 kHz):
     its true-peak limiter clamps every sample to the ceiling 10^(TP / 20) (af_loudnorm's
     final clamp), and the WAV muxer rounds to s16.  None for a track under 3 s, which
-    takes the linear path (output = input x offset, unclamped)."""
+    takes the linear path (output = input x offset, unclamped).  AMX_LN_MEASURED_BOUND=1:
+    None always (the 192 kHz alimiter's input is measured: A/B checks;
+    tests/test_gpu_dynamic.py::test_dynamic_output_within_ceiling checks the bound)."""
     import math
-    if n192 < 576000:                   # frame_size(192000, 3000): the linear fallback
-        return None
+    if n192 < 576000 or os.environ.get("AMX_LN_MEASURED_BOUND") == "1":
+        return None                     # (< 3 s: frame_size(192000, 3000), the linear fallback)
     c = 10.0 ** (LOUDNORM_TP / 20.0)
     return min(math.floor(c * 32768.0 + 0.5), 32767) / 32768.0
 

@@ -345,6 +345,37 @@ def test_filter_300s_vs_oracle(gpu, oracle_mod):
         _cmp(y, ref, "loudnorm filter 300 s %s" % ("pass 2" if measured else "pass 1"))
 
 
+@pytest.mark.parametrize("seconds,intro,fs", [(12.0, 0.0, 48000), (30.0, 4.0, 44100), (9.0, 0.0, 96000)])
+def test_dynamic_output_within_ceiling(gpu, oracle_mod, monkeypatch, seconds, intro, fs):
+    """the 192 kHz alimiter's input bound is af_loudnorm's ceiling
+    (engine.ln_output_bound) instead of a measurement -- exact only if EVERY sample of the
+    filter's output, the FIRST frame, a quiet start's frames and the FINAL flush included,
+    stays within it after s16 rounding.  Checked on the filter's whole 192 kHz output of
+    both passes, and the final output equals the measured path's (AMX_LN_MEASURED_BOUND=1)"""
+    import torch
+    from amx.engine import MasteringJob, ln_output_bound
+    x = _dynamic_signal(seconds, fs, 23, intro)
+    settings = dict(bass_boost=1.0, lufs=-14.0)
+    outs = {}
+    for measured in ("0", "1"):
+        monkeypatch.setenv("AMX_LN_MEASURED_BOUND", measured)
+        job = MasteringJob(fs, 2, settings, [x.shape[0]], quantum=512)
+        job.run(torch.from_numpy(x).cuda())
+        rep = job.fetch_report(raise_dynamic=False)
+        assert rep["modes"] == ["dynamic"], rep
+        y, info = job.dynamic_track(0, rep["stats"][0])
+        n192, job2 = job._j192[0][1], job._j192[1]
+        filt = job2.out[:n192].cpu().numpy()          # pass 2's filter output (the alimiter's input)
+        outs[measured] = y.cpu().numpy()
+        bound = ln_output_bound(n192) if measured == "0" else None
+        if measured == "0":
+            assert bound is not None
+            lim = int(round(bound * 32768))
+            assert int(np.abs(filt.astype(np.int32)).max()) <= lim, (np.abs(filt.astype(np.int32)).max(), lim)
+        job.close()
+    np.testing.assert_array_equal(outs["0"], outs["1"])
+
+
 @pytest.mark.parametrize("seconds,intro,fs", [(12.0, 0.0, 48000), (2.0, 0.0, 48000), (8.0, 3.5, 48000),
                                               (9.0, 0.0, 22050)])
 def test_master_audio_dynamic(gpu, oracle_mod, seconds, intro, fs):
