@@ -13,6 +13,14 @@
 // coalesced dword traffic, recursion reads from LDS.
 #include "amx_dev.hpp"
 
+// AMX_VT_LATE (the segment kernels' tile movers: front1s_run, k_gemv16, vt_fetch): a
+// prefetched tile is masked when it is put into LDS, not right after its load -- a select
+// beside the load made the compiler wait for the prefetch at once -- and the prefetch is
+// unconditional (past the last tile it re-reads the current one)
+#ifndef AMX_VT_LATE
+#define AMX_VT_LATE 1
+#endif
+
 namespace amx {
 
 #define AMX_HALF_LUT 32769   // entries of the odd tanh table's half (tanh(s) = sign(s) half[|s|])
@@ -144,14 +152,20 @@ __device__ __forceinline__ void front1s_run(const ChainDev &cd, const float *__r
     uint4 R[4], RG;
     auto fetch = [&](int k) {
         const int tt = threadIdx.x;
+#if AMX_VT_LATE
+        RG = *reinterpret_cast<const uint4 *>(G + (int64_t)k * D + 2 * (tt < GQ ? tt : 0));
+#else
         RG = tt < GQ ? *reinterpret_cast<const uint4 *>(G + (int64_t)k * D + 2 * tt)
                      : make_uint4(0u, 0u, 0u, 0u);
+#endif
 #pragma unroll
         for (int m = 0; m < 4; m++) {
             if constexpr (PART) {
                 const bool ok = k + 2 * c4 < ilen[m];          // frames k + 2 c4, +1
                 R[m] = *reinterpret_cast<const uint4 *>(ip[m] + (ok ? 2 * k : -4 * c4));
+#if !AMX_VT_LATE
                 if (!ok) R[m] = make_uint4(0u, 0u, 0u, 0u);
+#endif
             } else {
                 R[m] = *reinterpret_cast<const uint4 *>(ip[m] + 2 * k);
             }
@@ -162,13 +176,23 @@ __device__ __forceinline__ void front1s_run(const ChainDev &cd, const float *__r
     for (int k = 0; k < L; k += AMX_TF) {
 #pragma unroll
         for (int m = 0; m < 4; m++) {
+            uint4 v = R[m];
+#if AMX_VT_LATE
+            if constexpr (PART) {                               // (AMX_VT_LATE: masked here)
+                if (!(k + 2 * c4 < ilen[m])) v = make_uint4(0u, 0u, 0u, 0u);
+            }
+#endif
             uint32_t *w = s_in + (rg + 32 * m) * AMX_F1_PITCH + 4 * c4;
-            *reinterpret_cast<uint2 *>(w) = make_uint2(R[m].x, R[m].y);
-            *reinterpret_cast<uint2 *>(w + 2) = make_uint2(R[m].z, R[m].w);
+            *reinterpret_cast<uint2 *>(w) = make_uint2(v.x, v.y);
+            *reinterpret_cast<uint2 *>(w + 2) = make_uint2(v.z, v.w);
         }
         if (threadIdx.x < GQ) reinterpret_cast<uint4 *>(sG)[threadIdx.x] = RG;
         __syncthreads();
+#if AMX_VT_LATE
+        fetch(k + AMX_TF < L ? k + AMX_TF : k);
+#else
         if (k + AMX_TF < L) fetch(k + AMX_TF);
+#endif
         if constexpr (AN) {
             // The analog stage couples the channels, so a lane takes whole frames: the
             // two lanes of a pair take every other frame (f = 2 i + half), both
@@ -302,6 +326,9 @@ __global__ void __launch_bounds__(AMX_BLOCK, 4) k_front1s(const ChainDev *__rest
 // every pair bit for bit), so the 32 769-entry half table (128 KB) sits in the LDS of one
 // 1024-thread workgroup per CU (4 waves per SIMD), loaded once; the workgroups then
 // stride over every chunk's 4-frame groups.
+#ifndef AMX_AN_DEPTH
+#define AMX_AN_DEPTH 3     // input blocks held in registers (2: one block ahead)
+#endif
 __device__ __forceinline__ void analog_load8(const float *src, int64_t f, int64_t n, bool vin, float (&x)[8]) {
     if (f + 4 <= n && vin) {
         const float4 u0 = *reinterpret_cast<const float4 *>(src);
@@ -323,11 +350,12 @@ __global__ void __launch_bounds__(1024) k_analog_h(const ChainDev *__restrict__ 
                                                    const ChunkDev *__restrict__ chunks, int n_chunks,
                                                    const float *__restrict__ in,
                                                    const float *__restrict__ lut_half,
-                                                   uint32_t *__restrict__ a16) {
+                                                   uint32_t *__restrict__ a16, int64_t n_blocks) {
     __shared__ float s_tab[AMX_HALF_LUT];
     for (int i = threadIdx.x; i < AMX_HALF_LUT; i += 1024) s_tab[i] = lut_half[i];
     __syncthreads();
     const ChainDev &cd = *cdp;
+#if AMX_AN_DEPTH < 3
     auto work = [&](const ChunkDev &ch, const float (&x)[8], int64_t ff) {
         float t[8];
 #pragma unroll
@@ -354,9 +382,111 @@ __global__ void __launch_bounds__(1024) k_analog_h(const ChainDev *__restrict__ 
                 if (ff + i < ch.n) dst[i] = o[i];
         }
     };
+#endif
     constexpr int64_t BF = 1024 * 4;                   // frames per block
     int c = 0;
     int64_t cb0 = 0;                                    // first block of chunk c
+#if AMX_AN_DEPTH >= 3
+    // Three register sets: the next two blocks' input (64 KB per CU) is in flight while
+    // one is computed; one block ahead (32 KB per CU) held the kernel at ~3.6 TB/s.  For
+    // the loads to stay in flight, every pass through the loop issues at least the
+    // steady state's memory operations in the same order (the counter the waits use is
+    // in order, and a path with fewer operations after a load makes the compiler wait
+    // for everything):
+    //  - the chunk list is read through the constant address space (scalar loads, their
+    //    own counter) -- as vector loads, each chunk change waited out every load;
+    //  - a lane's quad is clamped to its chunk's last quad, so every lane of a block
+    //    stores one 16-B quad: lanes past the end recompute the last quad from the same
+    //    inputs and store the same bytes; frames past n read as 0 and land in the row's
+    //    padding (rows are 16-frame aligned, amx_plan.cpp), whose content nobody reads;
+    //  - a refill past the last block reloads its set's previous (valid) block, unused.
+    struct Ck { int64_t in_off, loc_off, n; };
+    auto kload = [&](int cix) -> Ck {                   // scalar loads (constant space)
+        typedef const __attribute__((address_space(4))) int64_t *K64;
+        const K64 q = (K64)(chunks + cix);
+        return Ck{q[0], q[1], q[3]};                    // in_off, loc_off, n (ChunkDev order)
+    };
+    const bool inv = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+    auto load_q = [&](const Ck &cc, int64_t f, float (&x)[8]) {
+        const float *src = in + (cc.in_off + f) * 2;
+        if (inv && (cc.in_off & 1) == 0 && f + 4 <= cc.n) {        // 16-B aligned whole quad
+            const float4 u0 = *reinterpret_cast<const float4 *>(src);
+            const float4 u1 = *reinterpret_cast<const float4 *>(src + 4);
+            x[0] = u0.x; x[1] = u0.y; x[2] = u0.z; x[3] = u0.w;
+            x[4] = u1.x; x[5] = u1.y; x[6] = u1.z; x[7] = u1.w;
+        } else {                                                    // dwords, clamped
+            const float *rowp = in + cc.in_off * 2;
+#pragma unroll
+            for (int e = 0; e < 8; e++) {               // (masked in work_q: no wait here)
+                const int64_t fr = f + e / 2;
+                x[e] = rowp[(fr < cc.n ? fr : cc.n - 1) * 2 + (e & 1)];
+            }
+        }
+    };
+    auto work_q = [&](const Ck &cc, const float (&x)[8], int64_t f) {
+        float t[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            const int q = f + e / 2 < cc.n ? (int)q_f32_to_s16_ffmpeg(x[e]) : 0;
+            const float v = s_tab[abs(q)];
+            t[e] = __int_as_float(__float_as_int(v) | (q & (int)0x80000000));
+        }
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            int16_t l, r;
+            analog_shelves(cd, t[2 * i], t[2 * i + 1], l, r);
+            o[i] = pack2(l, r);
+        }
+        *reinterpret_cast<uint4 *>(a16 + cc.loc_off + f) = make_uint4(o[0], o[1], o[2], o[3]);
+    };
+    Ck ck = kload(0);
+    int64_t nbk = (ck.n + BF - 1) / BF;
+    auto seek_k = [&](int64_t b) -> bool {                // workgroup-uniform
+        while (b >= cb0 + nbk) {
+            cb0 += nbk;
+            if (++c >= n_chunks) return false;
+            ck = kload(c);
+            nbk = (ck.n + BF - 1) / BF;
+        }
+        return true;
+    };
+    // this workgroup's blocks: k = 0 .. K-1 are job blocks blockIdx.x + k gridDim.x
+    const int64_t K = n_blocks > (int64_t)blockIdx.x ? (n_blocks - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+    if (K == 0) return;
+    int64_t kn = 0;                                     // the next block to issue
+    auto issue = [&](float (&x)[8], Ck &cc, int64_t &f) {
+        if (kn < K) {                                   // (scalar work only: the same
+            const int64_t b = (int64_t)blockIdx.x + kn * gridDim.x;   //  vector memory ops
+            seek_k(b);                                  //  on both sides)
+            cc = ck;
+            const int64_t fq = (b - cb0) * BF + threadIdx.x * 4;
+            const int64_t ql = (cc.n - 1) / 4 * 4;
+            f = fq < ql ? fq : ql;
+        }
+        kn++;
+        load_q(cc, f, x);
+    };
+    float xa[8], xb[8], xc[8];
+    Ck ca = ck, cb = ck, cc = ck;
+    int64_t fa = 0, fb = 0, fc = 0;
+    issue(xa, ca, fa);
+    cb = ca; fb = fa; cc = ca; fc = fa;
+    issue(xb, cb, fb);
+    issue(xc, cc, fc);
+    // one exit, and every iteration issues the same memory operations in the same order
+    int64_t k = 0;
+    for (; k + 3 <= K; k += 3) {
+        work_q(ca, xa, fa);
+        issue(xa, ca, fa);
+        work_q(cb, xb, fb);
+        issue(xb, cb, fb);
+        work_q(cc, xc, fc);
+        issue(xc, cc, fc);
+    }
+    if (k < K) work_q(ca, xa, fa);
+    if (k + 1 < K) work_q(cb, xb, fb);
+#else
     ChunkDev ch = chunks[0];
     int64_t nb = (ch.n + BF - 1) / BF;
     auto seek = [&](int64_t b) -> bool {                // workgroup-uniform
@@ -395,6 +525,7 @@ __global__ void __launch_bounds__(1024) k_analog_h(const ChainDev *__restrict__ 
         cc = cn2;
         f = fn2;
     }
+#endif
 }
 
 // EQ pass 1 over the s16 stereo chain input a16 (after k_analog_h): the GEMV of
@@ -438,16 +569,24 @@ __global__ void __launch_bounds__(AMX_BLOCK, 4) k_gemv16(const ChainDev *__restr
         ilen[m] = rl[(t >> 2) + 64 * m];
     }
     uint4 R[2], RG;
+    // (AMX_VT_LATE, as vt_fetch / vt_put: the loads alone in fetch, the masks at the put,
+    // an unconditional fetch -- so the next tile's loads stay in flight over this tile)
     auto fetch = [&](int k) {
+#if AMX_VT_LATE
+        RG = *reinterpret_cast<const uint4 *>(G + (int64_t)k * D + 2 * (t < GQ ? t : 0));
+#else
         RG = t < GQ ? *reinterpret_cast<const uint4 *>(G + (int64_t)k * D + 2 * t) : make_uint4(0u, 0u, 0u, 0u);
+#endif
 #pragma unroll
         for (int m = 0; m < 2; m++) {
             const int n = k + c4;
             uint4 v = *reinterpret_cast<const uint4 *>(ip[m] + (n < ilen[m] ? k : 0));
+#if !AMX_VT_LATE
             v.x = n < ilen[m] ? v.x : 0u;
             v.y = n + 1 < ilen[m] ? v.y : 0u;
             v.z = n + 2 < ilen[m] ? v.z : 0u;
             v.w = n + 3 < ilen[m] ? v.w : 0u;
+#endif
             R[m] = v;
         }
     };
@@ -458,11 +597,24 @@ __global__ void __launch_bounds__(AMX_BLOCK, 4) k_gemv16(const ChainDev *__restr
     const uint32_t *rp = s_in + row * AMX_G16_PITCH;
     for (int k = 0; k < L; k += AMX_TF) {
 #pragma unroll
-        for (int m = 0; m < 2; m++)
-            *reinterpret_cast<uint4 *>(s_in + ((t >> 2) + 64 * m) * AMX_G16_PITCH + c4) = R[m];
+        for (int m = 0; m < 2; m++) {
+            uint4 v = R[m];
+#if AMX_VT_LATE
+            const int n = k + c4;
+            v.x = n < ilen[m] ? v.x : 0u;
+            v.y = n + 1 < ilen[m] ? v.y : 0u;
+            v.z = n + 2 < ilen[m] ? v.z : 0u;
+            v.w = n + 3 < ilen[m] ? v.w : 0u;
+#endif
+            *reinterpret_cast<uint4 *>(s_in + ((t >> 2) + 64 * m) * AMX_G16_PITCH + c4) = v;
+        }
         if (t < GQ) reinterpret_cast<uint4 *>(sG)[t] = RG;
         __syncthreads();
+#if AMX_VT_LATE
+        fetch(k + AMX_TF < L ? k + AMX_TF : k);
+#else
         if (k + AMX_TF < L) fetch(k + AMX_TF);
+#endif
 #pragma unroll 1
         for (int f = 0; f < AMX_TF; f++) {
             const uint32_t w = rp[f];
@@ -511,6 +663,11 @@ struct VRows {
     int len[2];           // frames in the row (an invalid row: 0)
 };
 
+// AMX_VT_LATE: the frames past a row's length are zeroed when the tile is put into LDS,
+// not right after its load -- a select beside the load made the compiler wait for the
+// prefetched tile at once (vmcnt(0) right after the fetch: no overlap with the tile's
+// compute); and the fetch is unconditional (the last one re-reads the current tile), so
+// every pass through the tile loop issues the same memory operations
 __device__ __forceinline__ void vt_fetch(vt4 (&R)[2], const uint32_t *__restrict__ src, const VRows &vr,
                                          int k) {
     const int c4 = 4 * (threadIdx.x & 3);
@@ -519,16 +676,38 @@ __device__ __forceinline__ void vt_fetch(vt4 (&R)[2], const uint32_t *__restrict
         const int n = k + c4;
         const bool ok = n < vr.len[i];
         vt4 v = *reinterpret_cast<const vt4 *>(src + vr.base[i] + (ok ? n : 0));
+#if !AMX_VT_LATE
 #pragma unroll
         for (int e = 0; e < 4; e++) v[e] = n + e < vr.len[i] ? v[e] : 0u;
+#endif
         R[i] = v;
     }
 }
 
-__device__ __forceinline__ void vt_put(uint32_t *lds, const vt4 (&R)[2]) {
+// the tile of frames k .. k + AMX_TF - 1 (vt_fetch's R) into LDS
+__device__ __forceinline__ void vt_put(uint32_t *lds, const vt4 (&R)[2], const VRows &vr, int k) {
     const int r0 = (threadIdx.x & 63) >> 2, c4 = 4 * (threadIdx.x & 3);
-    *reinterpret_cast<vt4 *>(lds + r0 * AMX_VT_PITCH + c4) = R[0];
-    *reinterpret_cast<vt4 *>(lds + (r0 + 16) * AMX_VT_PITCH + c4) = R[1];
+    vt4 v0 = R[0], v1 = R[1];
+#if AMX_VT_LATE
+    const int n = k + c4;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        v0[e] = n + e < vr.len[0] ? v0[e] : 0u;
+        v1[e] = n + e < vr.len[1] ? v1[e] : 0u;
+    }
+#endif
+    *reinterpret_cast<vt4 *>(lds + r0 * AMX_VT_PITCH + c4) = v0;
+    *reinterpret_cast<vt4 *>(lds + (r0 + 16) * AMX_VT_PITCH + c4) = v1;
+}
+
+// the next tile's fetch: unconditional with AMX_VT_LATE (past the last tile it re-reads tile k)
+__device__ __forceinline__ void vt_next(vt4 (&R)[2], const uint32_t *__restrict__ src, const VRows &vr,
+                                        int k, int L) {
+#if AMX_VT_LATE
+    vt_fetch(R, src, vr, k + AMX_TF < L ? k + AMX_TF : k);
+#else
+    if (k + AMX_TF < L) vt_fetch(R, src, vr, k + AMX_TF);
+#endif
 }
 
 __device__ __forceinline__ void vt_store(const uint32_t *lds, uint32_t *__restrict__ dst, const VRows &vr,
@@ -626,9 +805,9 @@ __global__ void __launch_bounds__(AMX_BLOCK, (MB || KW) ? 4 : 5) k_front2(const 
     vt4 R[2];
     vt_fetch(R, a16, vin, 0);
     for (int k = 0; k < L; k += AMX_TF) {
-        vt_put(s_in, R);
+        vt_put(s_in, R, vin, k);
         amx_wave_sync();
-        if (k + AMX_TF < L) vt_fetch(R, a16, vin, k + AMX_TF);
+        vt_next(R, a16, vin, k, L);
         const uint32_t *rp = s_in + row * AMX_VT_PITCH;
         uint32_t *op = s_out + row * AMX_VT_PITCH;
 #pragma unroll 1
@@ -762,9 +941,9 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_xover2(const ChainDev *__restrict
     vt4 R[2];
     vt_fetch(R, p16, vr, 0);
     for (int k = 0; k < L; k += AMX_TF) {
-        vt_put(si, R);
+        vt_put(si, R, vr, k);
         amx_wave_sync();
-        if (k + AMX_TF < L) vt_fetch(R, p16, vr, k + AMX_TF);
+        vt_next(R, p16, vr, k, L);
         uint32_t xin[AMX_TF];
 #pragma unroll
         for (int q = 0; q < AMX_TF / 4; q++) {
@@ -829,11 +1008,10 @@ static hipError_t front1s_t(const Launch &l, const uint32_t *in, const float *lu
         if (l.f1_mode == AMX_F1_SPLIT && l.lut_half) {
             // analog as an elementwise pass (the half table in LDS), then the GEMV over its
             // s16 output; else (a tanh table that is not odd) k_front1s with the full table
-            const int64_t quads = (l.max_chunk_n + 3) / 4;
-            const int64_t wgs = (quads * (int64_t)l.n_chunks + 1023) / 1024;
+            const int64_t wgs = l.an_blocks;
             const dim3 gh((unsigned)(wgs < cu_count() ? (wgs > 0 ? wgs : 1) : cu_count()));
             hipLaunchKernelGGL(k_analog_h, gh, dim3(1024), 0, l.stream, l.cd, l.chunks, l.n_chunks,
-                               reinterpret_cast<const float *>(in), l.lut_half, a16);
+                               reinterpret_cast<const float *>(in), l.lut_half, a16, l.an_blocks);
             if constexpr (D > 0) {
                 hipLaunchKernelGGL((k_gemv16<D>), dim3((unsigned)((l.n_seg + rows - 1) / rows)), dim3(AMX_BLOCK), 0,
                                    l.stream, l.cd, l.chunks, l.segs, l.n_seg, l.L, a16, G, e);
