@@ -4,7 +4,8 @@ the N > 1 path runs -- K-filter tails and carry, hop partials, all-reduced loudn
 the limiter halo and, when the limiter can engage, the rank-to-rank sequential
 limiter -- and the concatenated rank outputs must equal the one-rank run of the
 same track bit for bit (the chunking, loudness decision and limiter are all
-track-level, so sharding must not change a sample)."""
+track-level, so sharding must not change a sample), and the C oracle's whole
+pipeline on the same input."""
 import datetime
 import gc
 import os
@@ -173,6 +174,18 @@ def test_two_ranks_match_one(gpu, case):
         return
     assert diff.max() == 0, "max |diff| %d LSB at %s (limiter fast path %s)" % (
         diff.max(), np.argmax(diff.max(axis=1)), fast[0])
+    # and against the oracle's whole pipeline (the N = 2 linear cases were
+    # checked against the one-rank GPU run only); the same bound as the one-GPU
+    # pipeline tests (tests/test_gpu_parity.py)
+    import oracle
+    from amx.chunking import chunk_bounds
+    fs = RATE.get(case, FS)
+    yo, oinfo = oracle.pipeline(oracle.quantize(x), fs, CASES[case], chunk_bounds(x.shape[0], fs, 512))
+    assert yo.shape == y2.shape, (yo.shape, y2.shape)
+    do = np.abs(y2.astype(np.int32) - yo.astype(np.int32))
+    exact = float((do == 0).mean())
+    print("%s over 2 ranks vs the oracle: max |diff| %d LSB, exact %.7f" % (case, do.max(), exact))
+    assert do.max() <= 3 and exact >= 0.9999, (int(do.max()), exact)
 
 
 @pytest.mark.parametrize("case", ["c3_lufs", "square_limiter"])
