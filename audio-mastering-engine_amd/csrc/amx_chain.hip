@@ -326,6 +326,9 @@ __global__ void __launch_bounds__(AMX_BLOCK, 4) k_front1s(const ChainDev *__rest
 // every pair bit for bit), so the 32 769-entry half table (128 KB) sits in the LDS of one
 // 1024-thread workgroup per CU (4 waves per SIMD), loaded once; the workgroups then
 // stride over every chunk's 4-frame groups.
+#ifndef AMX_AN_VEC
+#define AMX_AN_VEC 1       // k_analog_h<true> where the plan allows it (0: always the general form)
+#endif
 #ifndef AMX_AN_DEPTH
 #define AMX_AN_DEPTH 3     // input blocks held in registers (2: one block ahead)
 #endif
@@ -346,6 +349,11 @@ __device__ __forceinline__ void analog_load8(const float *src, int64_t f, int64_
 // workgroup), so a chunk's last, partial round of blocks does not leave most workgroups
 // idle before the next chunk starts (C3: 352 blocks per chunk over 256 workgroups;
 // striding chunk by chunk measured 52.6 against 49.4 us)
+// VEC (the host checks: every chunk starts at an even input frame, holds >= 4 frames, and
+// the input is 16-B aligned): the loop moves whole quads only -- 16-B loads, no masks and
+// no second load path, so the compiler keeps two blocks in flight over the third's
+// compute -- and a chunk's last n % 4 frames are done after the loop, a lane each.
+template <bool VEC>
 __global__ void __launch_bounds__(1024) k_analog_h(const ChainDev *__restrict__ cdp,
                                                    const ChunkDev *__restrict__ chunks, int n_chunks,
                                                    const float *__restrict__ in,
@@ -409,7 +417,7 @@ __global__ void __launch_bounds__(1024) k_analog_h(const ChainDev *__restrict__ 
     const bool inv = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
     auto load_q = [&](const Ck &cc, int64_t f, float (&x)[8]) {
         const float *src = in + (cc.in_off + f) * 2;
-        if (inv && (cc.in_off & 1) == 0 && f + 4 <= cc.n) {        // 16-B aligned whole quad
+        if (VEC || (inv && (cc.in_off & 1) == 0 && f + 4 <= cc.n)) {        // 16-B aligned whole quad
             const float4 u0 = *reinterpret_cast<const float4 *>(src);
             const float4 u1 = *reinterpret_cast<const float4 *>(src + 4);
             x[0] = u0.x; x[1] = u0.y; x[2] = u0.z; x[3] = u0.w;
@@ -427,7 +435,7 @@ __global__ void __launch_bounds__(1024) k_analog_h(const ChainDev *__restrict__ 
         float t[8];
 #pragma unroll
         for (int e = 0; e < 8; e++) {
-            const int q = f + e / 2 < cc.n ? (int)q_f32_to_s16_ffmpeg(x[e]) : 0;
+            const int q = VEC || f + e / 2 < cc.n ? (int)q_f32_to_s16_ffmpeg(x[e]) : 0;
             const float v = s_tab[abs(q)];
             t[e] = __int_as_float(__float_as_int(v) | (q & (int)0x80000000));
         }
@@ -461,7 +469,7 @@ __global__ void __launch_bounds__(1024) k_analog_h(const ChainDev *__restrict__ 
             seek_k(b);                                  //  on both sides)
             cc = ck;
             const int64_t fq = (b - cb0) * BF + threadIdx.x * 4;
-            const int64_t ql = (cc.n - 1) / 4 * 4;
+            const int64_t ql = VEC ? (cc.n / 4 - 1) * 4 : (cc.n - 1) / 4 * 4;   // (VEC: whole quads)
             f = fq < ql ? fq : ql;
         }
         kn++;
@@ -486,6 +494,27 @@ __global__ void __launch_bounds__(1024) k_analog_h(const ChainDev *__restrict__ 
     }
     if (k < K) work_q(ca, xa, fa);
     if (k + 1 < K) work_q(cb, xb, fb);
+    if constexpr (VEC) {
+        // the chunks' last n % 4 frames, a lane each
+        for (int cix = blockIdx.x; cix < n_chunks; cix += gridDim.x) {
+            const Ck q = kload(cix);
+            const int r = (int)(q.n & 3);
+            if ((int)threadIdx.x < r) {
+                const int64_t fr = q.n - r + threadIdx.x;
+                const float *src = in + (q.in_off + fr) * 2;
+                float t2[2];
+#pragma unroll
+                for (int e = 0; e < 2; e++) {
+                    const int qq = (int)q_f32_to_s16_ffmpeg(src[e]);
+                    const float v = s_tab[abs(qq)];
+                    t2[e] = __int_as_float(__float_as_int(v) | (qq & (int)0x80000000));
+                }
+                int16_t l, rr;
+                analog_shelves(cd, t2[0], t2[1], l, rr);
+                a16[q.loc_off + fr] = pack2(l, rr);
+            }
+        }
+    }
 #else
     ChunkDev ch = chunks[0];
     int64_t nb = (ch.n + BF - 1) / BF;
@@ -1010,8 +1039,13 @@ static hipError_t front1s_t(const Launch &l, const uint32_t *in, const float *lu
             // s16 output; else (a tanh table that is not odd) k_front1s with the full table
             const int64_t wgs = l.an_blocks;
             const dim3 gh((unsigned)(wgs < cu_count() ? (wgs > 0 ? wgs : 1) : cu_count()));
-            hipLaunchKernelGGL(k_analog_h, gh, dim3(1024), 0, l.stream, l.cd, l.chunks, l.n_chunks,
-                               reinterpret_cast<const float *>(in), l.lut_half, a16, l.an_blocks);
+            const bool vec = AMX_AN_VEC && l.an_vec && (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+            if (vec)
+                hipLaunchKernelGGL(k_analog_h<true>, gh, dim3(1024), 0, l.stream, l.cd, l.chunks, l.n_chunks,
+                                   reinterpret_cast<const float *>(in), l.lut_half, a16, l.an_blocks);
+            else
+                hipLaunchKernelGGL(k_analog_h<false>, gh, dim3(1024), 0, l.stream, l.cd, l.chunks, l.n_chunks,
+                                   reinterpret_cast<const float *>(in), l.lut_half, a16, l.an_blocks);
             if constexpr (D > 0) {
                 hipLaunchKernelGGL((k_gemv16<D>), dim3((unsigned)((l.n_seg + rows - 1) / rows)), dim3(AMX_BLOCK), 0,
                                    l.stream, l.cd, l.chunks, l.segs, l.n_seg, l.L, a16, G, e);

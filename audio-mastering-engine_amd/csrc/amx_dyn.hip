@@ -73,13 +73,18 @@ __device__ __forceinline__ uint32_t rms_floor(uint64_t S, uint32_t cnt, double r
     return cnt ? (r > 32768u ? 32768u : r) : 0u;
 }
 
-template <int LP>
+// AMX_RMS_N256: the tile of the LP = 256 form (48 / 44.1 kHz).  Measured (round 6,
+// profiles/r06m_rms_analog_ab.txt): 2048 frames (17 KB of prefix sums, 8 workgroups per
+// CU, 12.5 % halo) 1-2 us slower at C3 than 4096 (4 per CU, 6 % halo)
+#ifndef AMX_RMS_N256
+#define AMX_RMS_N256 4096
+#endif
+template <int LP, int N>
 __global__ void __launch_bounds__(AMX_BLOCK) k_rms(const ChainDev *__restrict__ cdp,
                                                    const ChunkDev *__restrict__ chunks,
                                                    const uint32_t *__restrict__ bands,
                                                    uint16_t *__restrict__ mi, int64_t nloc,
                                                    int *bact) {
-    constexpr int N = AMX_RMS_N;
     constexpr int F = N - LP;                          // frames out per workgroup
     constexpr int PER = N / AMX_BLOCK;                 // 16 slots per thread
     constexpr int VEC = PER / 4;                       // as 4 16-B loads
@@ -1249,10 +1254,11 @@ hipError_t launch_mc_gain_overlay(const DynLaunch &d, const ChunkDev *schunks, c
 // ---------------------------------------------------------------- launchers
 template <int LP>
 static void rms_t(const DynLaunch &d, const int16_t *bands, uint16_t *m, int *bact) {
-    constexpr int F = AMX_RMS_N - LP;
+    constexpr int N = LP == 256 ? AMX_RMS_N256 : AMX_RMS_N;
+    constexpr int F = N - LP;
     dim3 g((unsigned)((d.max_chunk_n + F - 1) / F), (unsigned)d.n_chunks, 3);
     if (empty(g)) return;
-    hipLaunchKernelGGL(k_rms<LP>, g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks,
+    hipLaunchKernelGGL((k_rms<LP, N>), g, dim3(AMX_BLOCK), 0, d.st, d.cd, d.chunks,
                        reinterpret_cast<const uint32_t *>(bands), m, d.nloc, bact);
 }
 

@@ -157,6 +157,7 @@ struct Launch {
     int f1_mode = AMX_F1_SPLIT;        // float32 stereo + analog: which pass-1 form (amx_chain.hip)
     int64_t max_chunk_n = 0;           // frames of the longest chunk (elementwise grids)
     int64_t an_blocks = 0;             // k_analog_h's 4096-frame blocks over all chunks
+    int an_vec = 0;                    // every chunk: even in_off and >= 4 frames (k_analog_h<true>)
 };
 struct ScanPlan {
     int D, n_blk, K;

@@ -314,6 +314,7 @@ struct amx_plan {
     int64_t max_nkseg = 0;
     int64_t nloc = 0, out_frames = 0, max_chunk_out = 0, max_span = 0, max_chunk_n = 0;
     int64_t an_blocks = 0;      // k_analog_h's 4096-frame blocks over all chunks
+    int an_vec = 1;             // k_analog_h<true>: every chunk at an even input frame, >= 4 frames
     int64_t in_frames = 0;  // input frames the chunks read (max in_offset + frames)
     int64_t max_hops = 1;   // 100 ms hops of the longest track's measurement stream
     int mono16 = 0;         // mono int16 input: duplicated to stereo into ws o_dup first
@@ -793,6 +794,7 @@ int amx_plan_create(const amx_chain_desc *desc, const amx_chunk *chunks, int32_t
         p->max_chunk_out = n2 > p->max_chunk_out ? n2 : p->max_chunk_out;
         p->max_chunk_n = ch.n > p->max_chunk_n ? ch.n : p->max_chunk_n;
         p->an_blocks += (ch.n + 4095) / 4096;
+        if (ch.n > 0 && ((ch.in_off & 1) != 0 || ch.n < 4)) p->an_vec = 0;
         loc += (ch.n + 15) / 16 * 16;   // chunk rows of per-frame scratch start 16-frame aligned
         outo += n2;
     }
@@ -1267,7 +1269,7 @@ int amx_run_stage(amx_plan *p, int32_t stage, const float *d_in, int16_t *d_out,
     if (p->n_seg == 0) return AMX_OK;
     hipStream_t st = (hipStream_t)stream;
     amx::Launch l{p->d_cd, p->d_chunks, p->d_segs, p->n_chunks, p->n_seg, p->L, st, p->d_lut_half,
-                  p->f1_mode, p->max_chunk_n, p->an_blocks};
+                  p->f1_mode, p->max_chunk_n, p->an_blocks, p->an_vec};
     int16_t *a16 = wsp<int16_t>(d_ws, p->o_a16);
     double *e = wsp<double>(d_ws, p->o_e), *s = wsp<double>(d_ws, p->o_s);
     int16_t *p16 = p->mb ? wsp<int16_t>(d_ws, p->o_p16) : nullptr;
