@@ -352,6 +352,9 @@ struct LpArgs {
     // k_lp_fill writes every position's unlimited output first, lp_detect skips blocks
     // below the ceiling and k_lp_seg emits only the multiplied slots
     double *bm;
+    // [n / 64 + 2] the same bound for FINAL's frames: the largest |u G_T offset| per 64
+    // positions from S0 (FINAL refills the whole ring with those values); NULL with bm
+    double *bmF;
 };
 // the 192 kHz resampler's geometry (amx_plan.cpp swr_*): output j sits at phase
 // position j dst / src (units of 1 / pc input frame); lin: interpolate rows ph, ph + 1

@@ -1475,8 +1475,12 @@ __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, in
     const double ceiling = a.ceiling;
     double pv0 = 0.0, pv1 = 0.0;               // n = 0 never qualifies (n > 0)
     double *st0 = W.st, *st1 = W.st + LP_STW;
-    const bool skip = a.bm != nullptr && !W.f.fin;
-    // outside FINAL the positions of consecutive slots from slot0 are consecutive
+    // the slots' bound: bm outside FINAL, bmF in FINAL (its frames hold u G_T offset fills,
+    // multiplied by envelope gains <= 1, and 0 past the track: blocks from n on bound 0)
+    const double *bmx = W.f.fin ? a.bmF : a.bm;
+    const bool skip = bmx != nullptr;
+    const int64_t nbx = W.f.fin ? (a.n + 63) >> 6 : INT64_MAX;
+    // the positions of consecutive slots from slot0 are consecutive
     const int64_t pos0 = lp_pos(W.f, slot0);
     unsigned long long mask[LP_NW];
 #pragma unroll
@@ -1492,9 +1496,10 @@ __device__ __forceinline__ int lp_detect(const LpArgs &a, LpWave &W, int smp, in
                 bool may = false;
                 if (g0 < count) {
                     const int64_t p = pos0 + g0;
-                    double mx = a.bm[p >> 6];
+                    auto bnd = [&](int64_t bi) -> double { return bi < nbx ? bmx[bi] : 0.0; };
+                    double mx = bnd(p >> 6);
 #pragma unroll
-                    for (int k = 1; k <= LP_NT / 64; k++) mx = fmax(mx, a.bm[(p + 64 * k - 1) >> 6]);
+                    for (int k = 1; k <= LP_NT / 64; k++) mx = fmax(mx, bnd((p + 64 * k - 1) >> 6));
                     may = mx * (1.0 + 1e-9) > ceiling;
                 }
                 lp_vote(W, may, mask);
@@ -1919,7 +1924,7 @@ __global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t
          b += ((int64_t)gridDim.x * 256) >> 4) {
         const int64_t p0 = 64 * b + 4 * (lane & 15);
         const bool whole = p0 >= u_lo && p0 + 4 <= u_hi && p0 + 4 <= a.n;
-        double mx = 0.0;
+        double mx = 0.0, mxF = 0.0;
         if (whole) {
             const float4 xa = u4[p0 >> 1], xb = u4[(p0 >> 1) + 1];     // positions p0 .. p0 + 3
             const float xs[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
@@ -1952,6 +1957,7 @@ __global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t
                 if (pos >= a.S0) {                     // FINAL emits it: u G_T offset
                     o0 = ((double)xs[2 * k] * gT) * off;
                     o1 = ((double)xs[2 * k + 1] * gT) * off;
+                    mxF = fmax(mxF, fmax(fabs(o0), fabs(o1)));
                 }
                 if (fabs(o0) > ceiling) o0 = ceiling * (o0 < 0 ? -1 : 1);
                 if (fabs(o1) > ceiling) o1 = ceiling * (o1 < 0 ? -1 : 1);
@@ -1968,6 +1974,7 @@ __global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t
             // a block edge of the window or the track: any position outside holds no fill
             // (+inf: the scan never skips such a block); inside ones one at a time
             mx = HUGE_VAL;
+            mxF = HUGE_VAL;
             const float2 *u = reinterpret_cast<const float2 *>(a.u);
             for (int k = 0; k < 4; k++) {
                 const int64_t pos = p0 + k;
@@ -1992,8 +1999,14 @@ __global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t
             }
         }
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) mx = fmax(mx, __shfl_xor(mx, o));
-        if ((lane & 15) == 0) a.bm[b] = mx;
+        for (int o = 1; o < 16; o <<= 1) {
+            mx = fmax(mx, __shfl_xor(mx, o));
+            mxF = fmax(mxF, __shfl_xor(mxF, o));
+        }
+        if ((lane & 15) == 0) {
+            a.bm[b] = mx;
+            if (a.bmF) a.bmF[b] = mxF;
+        }
     }
 }
 

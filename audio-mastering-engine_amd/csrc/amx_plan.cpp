@@ -1400,6 +1400,7 @@ struct LnLayout {
     int T = 0, nb_last = 0, Fs = 4, Wf = 3, J = 0, M = 0, K = 0, P = 0;
     int64_t o_u = 0, o_ring = 0, o_ctl = 0, o_dctl = 0, o_v = 0, o_hold = 0, o_D = 0, o_G = 0, o_ramp = 0;
     int64_t o_recG = 0, o_recE = 0, o_wrec = 0, o_cnt = 0, o_match = 0, o_rings = 0, o_wring = 0, o_bm = 0;
+    int64_t o_bmF = 0;
     int64_t total = 0;
 };
 // INNER frames, segments of Fs frames each warmed up Wf frames (AMX_LN_WARM, default 2)
@@ -1447,6 +1448,7 @@ LnLayout ln_layout(int64_t n192, int64_t u_frames = -1, int p_cap = -1) {
     l.o_rings = take((int64_t)l.P * AMX_LN_RING * 2 * sizeof(double));
     l.o_wring = take((int64_t)AMX_LN_RING * 2 * sizeof(double));
     l.o_bm = take((n192 / 64 + 2) * (int64_t)sizeof(double));
+    l.o_bmF = take((n192 / 64 + 2) * (int64_t)sizeof(double));
     l.total = o;
     return l;
 }
@@ -1649,6 +1651,9 @@ int ln_args(amx_plan *p, int32_t track, const amx_loudnorm_desc *d, const double
     // A/B measurements)
     const char *fe = std::getenv("AMX_LP_FILL");
     q.bm = (fe && std::atoi(fe) == 0) ? nullptr : reinterpret_cast<double *>(w + lo.o_bm);
+    // FINAL's bound (AMX_LP_FINAL_SKIP=0: FINAL's frames scan every group, for A/B)
+    const char *fs = std::getenv("AMX_LP_FINAL_SKIP");
+    q.bmF = (q.bm && !(fs && std::atoi(fs) == 0)) ? reinterpret_cast<double *>(w + lo.o_bmF) : nullptr;
     return AMX_OK;
 }
 }  // namespace
