@@ -1409,7 +1409,13 @@ __device__ __forceinline__ void lp_refill(const LpArgs &a, LpWave &W, int phi) {
 
 // multiply k slots from e0 by env(i) (af_loudnorm's envelope loops).  The k slots are
 // distinct, so the values of 4 groups of LP_NT are loaded before any of them is written
-// (one memory round trip per 4 LP_NT slots)
+// (one memory round trip per 4 LP_NT slots), and no pass reads a slot another pass
+// writes: the ring is synchronised once, after the last pass (AMX_LP_ENV_SYNC1; a sync
+// per pass drained every pass's stores before the next one's loads -- a release's 19 200
+// slots paid 19 store drains and barriers)
+#ifndef AMX_LP_ENV_SYNC1
+#define AMX_LP_ENV_SYNC1 1
+#endif
 template <class F>
 __device__ __forceinline__ void lp_env(const LpArgs &a, LpWave &W, int e0, int k, F env) {
     for (int i00 = 0; i00 < k; i00 += 4 * LP_NT) {
@@ -1434,8 +1440,13 @@ __device__ __forceinline__ void lp_env(const LpArgs &a, LpWave &W, int e0, int k
                 atomicOr(&W.flags[s[p] >> 5], 1u << (s[p] & 31));
             }
         }
+#if !AMX_LP_ENV_SYNC1
         lp_sync_ring();
+#endif
     }
+#if AMX_LP_ENV_SYNC1
+    if (k > 0) lp_sync_ring();
+#endif
 }
 
 __device__ __forceinline__ int lp_env_end(int e0, int k) {
