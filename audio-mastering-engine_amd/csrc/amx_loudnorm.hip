@@ -65,6 +65,10 @@ __device__ __forceinline__ float ln_dot(const float *w, const float *__restrict_
 }
 
 typedef float ln_f2 __attribute__((ext_vector_type(2)));
+typedef unsigned lp_u4 __attribute__((ext_vector_type(4)));
+#ifndef AMX_LP_HANDOFF
+#define AMX_LP_HANDOFF 1     // k_lp_seg's boundary records: sc1 stores + one acquire (0: __threadfence form)
+#endif
 
 // ln_dot with the 8 chains as 4 packed pairs (v_pk_fma_f32 / v_pk_add_f32): the same
 // operations lane by lane, the first term a fused multiply-add onto 0 as in ln_dot
@@ -1817,6 +1821,41 @@ __device__ __forceinline__ void lp_snapshot(const LpArgs &a, const LpWave &W, do
         out |= m != 0u;
     }
     const bool dirty = lp_first(W, out) >= 0;
+#if AMX_LP_HANDOFF
+    // the record goes out write-through (sc1, 16-B buffer stores): k_lp_seg's other
+    // workgroups read it in this launch (lp_arrive), on any XCD, with no release fence.
+    // The window's values are loaded half at a time before they are stored (two memory
+    // round trips; all at once spilled).
+    static_assert(LP_WIN % LP_NT == 0, "record window");
+    constexpr int NS = LP_WIN / LP_NT;
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rec, 0, LP_REC * (int)sizeof(double), 0x00020000);
+    if (lane < 4) {                       // scalars 0..7, two per lane
+        const double sc[8] = {(double)W.mode, (double)W.env_cnt, (double)W.env_index, (double)W.attack_length,
+                              W.gr0, W.gr1, (double)W.f.phi, dirty ? 1.0 : 0.0};
+        const double2 pr = make_double2(lane == 0 ? sc[0] : lane == 1 ? sc[2] : lane == 2 ? sc[4] : sc[6],
+                                        lane == 0 ? sc[1] : lane == 1 ? sc[3] : lane == 2 ? sc[5] : sc[7]);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(lp_u4, pr), rr, lane * 16, 0, 16);
+    }
+    constexpr int NH = NS / 2;
+#pragma unroll 1
+    for (int h = 0; h < 2; h++) {
+        double2 v[NH];
+#pragma unroll
+        for (int q = 0; q < NH; q++) {
+            int s = w0 + lane + (h * NH + q) * LP_NT;
+            if (s >= LP_RS) s -= LP_RS;
+#ifdef AMX_LPV_NOSNAP          // measurement variant: the window's values not loaded (wrong output)
+            v[q] = make_double2(0.0, 0.0);
+#else
+            v[q] = lp_val(a, W, s);
+#endif
+        }
+#pragma unroll
+        for (int q = 0; q < NH; q++)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(lp_u4, v[q]), rr,
+                                                   (16 + 2 * (lane + (h * NH + q) * LP_NT)) * (int)sizeof(double), 0, 16);
+    }
+#else
     if (lane == 0) {
         rec[0] = W.mode;
         rec[1] = W.env_cnt;
@@ -1838,6 +1877,7 @@ __device__ __forceinline__ void lp_snapshot(const LpArgs &a, const LpWave &W, do
         rec[16 + 2 * j] = v.x;
         rec[17 + 2 * j] = v.y;
     }
+#endif
 }
 
 // the same state back into a wave (every window slot flagged with its recorded value)
@@ -1873,7 +1913,23 @@ __device__ __forceinline__ bool lp_same(const LpWave &W, const double *A, const 
     bool diff = A[LP_DIRTY] != 0.0 || B[LP_DIRTY] != 0.0 || (int)A[0] != (int)B[0];
     if ((int)A[0] != LO_OUT || (int)B[0] != LO_OUT)
         for (int q = 0; q < 6; q++) diff |= !lp_bits_eq(A[q], B[q]);
+#if AMX_LP_HANDOFF
+    // every load issued before any compare (one round trip, not one per pass)
+    constexpr int NC = 2 * LP_WIN / LP_NT, NH = NC / 2;
+#pragma unroll 1
+    for (int h = 0; h < 2; h++) {
+        double x[NH], y[NH];
+#pragma unroll
+        for (int q = 0; q < NH; q++) {
+            x[q] = A[16 + threadIdx.x + (h * NH + q) * LP_NT];
+            y[q] = B[16 + threadIdx.x + (h * NH + q) * LP_NT];
+        }
+#pragma unroll
+        for (int q = 0; q < NH; q++) diff |= !lp_bits_eq(x[q], y[q]);
+    }
+#else
     for (int j = threadIdx.x; j < 2 * LP_WIN; j += LP_NT) diff |= !lp_bits_eq(A[16 + j], B[16 + j]);
+#endif
     return lp_first(W, diff) < 0;
 }
 
@@ -1882,6 +1938,27 @@ __device__ __forceinline__ bool lp_same(const LpWave &W, const double *A, const 
 // (every wave's record stores are released -- its own fence -- before lane 0 counts
 // the arrival; the count is broadcast through LDS)
 __device__ __forceinline__ void lp_arrive(const LpArgs &a, const LpWave &W, int j) {
+#if AMX_LP_HANDOFF
+    // the hand-off of DESIGN.md §3.7 / the guide's R1 form: the records were stored sc1
+    // (lp_snapshot); every wave drains its stores, then one relaxed agent-scope count;
+    // the second arriver acquires once (one lane's fence, its wait, the barrier) and reads
+    // both records with plain loads.  __threadfence() here wrote back the whole L2 at
+    // every arrival (2 per segment: the median segment spent ~180 us in snapshots and
+    // arrivals, profiles/r06t_seg_times.txt)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        W.sv[0] = (unsigned long long)__hip_atomic_fetch_add(&a.cnt[j], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int old = (int)(unsigned)W.sv[0];
+    if (old == 1) {
+        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const bool same = lp_same(W, a.recE + (int64_t)(j - 1) * LP_REC, a.recG + (int64_t)j * LP_REC);
+        if (threadIdx.x == 0) a.match[j] = same ? 1 : 0;
+    }
+#else
     __threadfence();
     __syncthreads();
     if (threadIdx.x == 0) W.sv[0] = (unsigned long long)(unsigned)atomicAdd(&a.cnt[j], 1);
@@ -1892,6 +1969,7 @@ __device__ __forceinline__ void lp_arrive(const LpArgs &a, const LpWave &W, int 
         const bool same = lp_same(W, a.recE + (int64_t)(j - 1) * LP_REC, a.recG + (int64_t)j * LP_REC);
         if (threadIdx.x == 0) a.match[j] = same ? 1 : 0;
     }
+#endif
 }
 
 __device__ __forceinline__ void lp_wave_init(const LpArgs &a, LpWave &W, double2 *ring, unsigned *flags,
