@@ -494,16 +494,23 @@ __device__ void lim_run(Lim &L, int64_t f, int64_t fend, bool idle) {
     }
 }
 
+// The segment records are read by the walker, another workgroup of this launch on any
+// XCD: stored write-through (agent-scope atomic stores, sc1) so the hand-off needs no
+// release fence (limiter_block: drain, relaxed count, one acquire in the walker)
+__device__ __forceinline__ void lim_st(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ void lim_store(const Lim &L, double *E, int64_t f_end, bool with_ring) {
     const int lane = threadIdx.x & 63;
     if (lane == 0) {
-        E[0] = L.att; E[1] = L.delta; E[2] = lim_pos(L, f_end); E[3] = L.nextiter; E[4] = L.nextlen;
-        E[5] = 1.0;
+        lim_st(E + 0, L.att); lim_st(E + 1, L.delta); lim_st(E + 2, (double)lim_pos(L, f_end));
+        lim_st(E + 3, (double)L.nextiter); lim_st(E + 4, (double)L.nextlen);
+        lim_st(E + 5, 1.0);
     }
     for (int k = lane; k < L.bs; k += 64) {
-        if (with_ring) E[8 + k] = L.buffer[k];
-        E[8 + L.bs + k] = L.nextdelta[k];
-        E[8 + 2 * L.bs + k] = L.nextposd[k];
+        if (with_ring) lim_st(E + 8 + k, L.buffer[k]);
+        lim_st(E + 8 + L.bs + k, L.nextdelta[k]);
+        lim_st(E + 8 + 2 * L.bs + k, L.nextposd[k]);
     }
 }
 __device__ void lim_load(Lim &L, const double *E) {
@@ -580,13 +587,15 @@ __device__ void limiter_block(const LimArgs &a, int bx, int nbx, double *lim_lds
         amx_wave_sync();
     }
 
-    // 2. the last block of the track walks
-    __threadfence();
+    // 2. the last block of the track walks (one wave per block: its drain, then the count;
+    // the walker acquires once before it reads the other blocks' records)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned old = 0;
-    if (lane == 0) old = atomicAdd(a.cnt + t, 1u);
+    if (lane == 0) old = __hip_atomic_fetch_add(a.cnt + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = __shfl(old, 0);
     if (old != (unsigned)nbx - 1) return;
-    __threadfence();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) a.cnt[t] = 0u;
     lim_init_span(L, S);                               // ring content before the span
     bool in_lds = false;                               // true end of segment k-1 is in L

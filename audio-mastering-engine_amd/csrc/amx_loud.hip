@@ -431,15 +431,20 @@ __global__ void __launch_bounds__(AMX_PEAK_THREADS) k_peak_reduce(const SpanDev 
         for (int w = 0; w < AMX_PEAK_THREADS / 64; w++)
             for (int c = 0; c < 4; c++) mm[c] = max(mm[c], red[c][w]);
         int *pt = part + ((int64_t)t * gridDim.x + blockIdx.x) * 4;
-        for (int c = 0; c < 4; c++) pt[c] = mm[c];
-        __threadfence();
-        last = atomicAdd(cnt + t, 1u) == (unsigned)(nb - 1);
+        // the hand-off of DESIGN.md §3.7: write-through (agent-scope atomic) stores of the
+        // slot, drained, then one relaxed agent-scope count; the last block acquires once.
+        // (__threadfence() in every block wrote back the XCD's whole L2)
+        for (int c = 0; c < 4; c++) __hip_atomic_store(pt + c, mm[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = __hip_atomic_fetch_add(cnt + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nb - 1);
     }
     __syncthreads();
     if (last) {
         // the slots in parallel (a thread per slot and channel word, then the block's max),
         // not one thread's chain of dependent volatile loads
-        __threadfence();
+        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         int v = 0;
         for (int k = threadIdx.x; k < 4 * nb; k += AMX_PEAK_THREADS) {
             const volatile int *q = part + (int64_t)t * gridDim.x * 4 + k;
