@@ -93,16 +93,30 @@ __device__ __forceinline__ float ln_dot2(const float *w, const float *__restrict
 // then every frame's L outputs with the bank rows as wave-uniform operands (k_ln_upsample's
 // generic form pays two 64-bit divisions and a per-lane bank row for every output).
 #define LN_UPF 4
+// Stores (round 6): a thread's 4 frames are 32 L contiguous bytes, so the lanes' own
+// stores had a 32 L-byte stride (one 16-B piece per 128-B line per instruction at 48 kHz:
+// the writes, 461 MB for a 5-min track, ran at ~2.4 TB/s).  A workgroup whose 256 x 4
+// frames are all in range stages its outputs in LDS and writes them as one contiguous
+// block, 16 B per lane per instruction (AMX_LN_UPS_LDS; the others store directly).
+#ifndef AMX_LN_UPS_LDS
+#define AMX_LN_UPS_LDS 1
+#endif
 template <int L>
 __global__ void __launch_bounds__(AMX_BLOCK) k_ln_up_static(const uint32_t *__restrict__ x, int64_t n_in,
                                                             const float *__restrict__ bank, int64_t j0, int64_t j1,
                                                             float *__restrict__ u, const int32_t *__restrict__ gate) {
     if (AMX_LN_GATED(gate)) return;
     constexpr int NW = LN_TAPS + LN_UPF - 1;
+    constexpr bool STAGE = AMX_LN_UPS_LDS && (L % 2 == 0);
+    constexpr int TF = 2 * L * LN_UPF;                 // floats a thread produces
+    __shared__ __attribute__((aligned(16))) float s_o[STAGE ? AMX_BLOCK * TF : 4];
     const int64_t f0 = j0 / L, f1 = (j1 + L - 1) / L;
     const int64_t nblk = (f1 - f0 + LN_UPF - 1) / LN_UPF;
-    for (int64_t bi = (int64_t)blockIdx.x * AMX_BLOCK + threadIdx.x; bi < nblk; bi += (int64_t)gridDim.x * AMX_BLOCK) {
-        const int64_t fb = f0 + bi * LN_UPF;          // this thread's first frame
+    // workgroup-uniform iterations (the staged stores need the barriers)
+    for (int64_t b0 = (int64_t)blockIdx.x * AMX_BLOCK; b0 < nblk; b0 += (int64_t)gridDim.x * AMX_BLOCK) {
+        const int64_t bi = b0 + threadIdx.x;
+        const bool act = bi < nblk;
+        const int64_t fb = f0 + (act ? bi : b0) * LN_UPF;   // this thread's first frame
         float w0[NW], w1[NW];
         const int64_t g = fb - LN_C;
         static_assert(LN_UPF == 4 && LN_C % 4 == 3, "the 16-B window loads start one frame early");
@@ -134,10 +148,13 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_ln_up_static(const uint32_t *__re
                 w1[i] = (float)hi16(v) * (1.0f / 32768.0f);
             }
         }
+        // the whole workgroup's outputs in range: frames f0 + 4 b0 .. + 4 * AMX_BLOCK
+        const int64_t fw = f0 + b0 * LN_UPF;
+        const bool whole = STAGE && b0 + AMX_BLOCK <= nblk && fw * L >= j0 &&
+                           (fw + (int64_t)AMX_BLOCK * LN_UPF) * L <= j1 && fw + (int64_t)AMX_BLOCK * LN_UPF <= f1;
 #pragma unroll
         for (int k = 0; k < LN_UPF; k++) {
             const int64_t f = fb + k;
-            if (f >= f1) break;
             float o[2 * L];
 #pragma unroll
             for (int ph = 0; ph < L; ph++) {
@@ -145,6 +162,16 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_ln_up_static(const uint32_t *__re
                 o[2 * ph] = ln_dot2(w0 + k, h);
                 o[2 * ph + 1] = ln_dot2(w1 + k, h);
             }
+            if constexpr (STAGE) {
+                if (whole) {
+#pragma unroll
+                    for (int q = 0; q < L / 2; q++)
+                        *reinterpret_cast<float4 *>(s_o + threadIdx.x * TF + k * 2 * L + 4 * q) =
+                            make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+                    continue;
+                }
+            }
+            if (!act || f >= f1) continue;
             bool done = false;
             if constexpr (L % 2 == 0) {
                 // the frame's L outputs are 8 L contiguous bytes: 16-B stores when all are
@@ -163,6 +190,16 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_ln_up_static(const uint32_t *__re
                     const int64_t j = f * L + ph;
                     if (j >= j0 && j < j1) *reinterpret_cast<float2 *>(u + 2 * j) = make_float2(o[2 * ph], o[2 * ph + 1]);
                 }
+            }
+        }
+        if constexpr (STAGE) {
+            if (whole) {                                     // workgroup-uniform
+                __syncthreads();
+                float4 *dst = reinterpret_cast<float4 *>(u + 2 * fw * L);
+                const float4 *src = reinterpret_cast<const float4 *>(s_o);
+#pragma unroll
+                for (int q = 0; q < TF / 4; q++) dst[q * AMX_BLOCK + threadIdx.x] = src[q * AMX_BLOCK + threadIdx.x];
+                __syncthreads();                             // s_o is rewritten next pass
             }
         }
     }
