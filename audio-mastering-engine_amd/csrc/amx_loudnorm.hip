@@ -2064,6 +2064,10 @@ __global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t
                 i = (int)(q - (int64_t)t * LP_FR);
             }
             uint32_t o[4];
+            // the four positions' (frame, index) pairs, then every gain-row load issued
+            // before any is used (a load under the last frame's branch made the compiler
+            // wait at the join: eight dependent round trips per quad)
+            int tk[4], ik[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const int64_t pos = p0 + k;
@@ -2071,10 +2075,24 @@ __global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t
                     i = 0;
                     t++;
                 }
-                const int tc = t < a.T - 1 ? t : a.T - 1;
-                double r = a.ramp[i];
-                if (!(t < a.T - 1 || a.nb_last == LP_FR)) r = (double)i / (double)a.nb_last;
-                const double g0 = a.G[tc], g1 = a.G[tc + 1];
+                tk[k] = t;
+                ik[k] = i;
+            }
+            double rk[4], g0k[4], g1k[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int tc = tk[k] < a.T - 1 ? tk[k] : a.T - 1;
+                rk[k] = a.ramp[ik[k]];
+                g0k[k] = a.G[tc];
+                g1k[k] = a.G[tc + 1];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int64_t pos = p0 + k;
+                const int t = tk[k], i = ik[k];
+                const double rl = (double)i / (double)a.nb_last;       // (the partial last frame's ramp)
+                const double r = (t < a.T - 1 || a.nb_last == LP_FR) ? rk[k] : rl;
+                const double g0 = g0k[k], g1 = g1k[k];
                 const double gi = g0 + (r * (g1 - g0));
                 const double g = pos < LP_RS ? d0 : gi;
                 const double v0 = ((double)xs[2 * k] * g) * off, v1 = ((double)xs[2 * k + 1] * g) * off;
