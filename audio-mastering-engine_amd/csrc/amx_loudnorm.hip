@@ -315,6 +315,12 @@ __device__ __forceinline__ int16_t ln_s16(double v) {            // av_clip_int1
     return (int16_t)(r > 32767.0 ? 32767 : (r < -32768.0 ? -32768 : (int)r));
 }
 
+// ln_s16 with the clamp as fmax / fmin (two fp64 operations instead of two compares and
+// four selects; the same value for every non-NaN v)
+__device__ __forceinline__ int16_t ln_s16_lim(double v) {
+    return (int16_t)(int)fmin(fmax(rint(v * 32768.0), -32768.0), 32767.0);
+}
+
 __device__ __forceinline__ int ln_w(int i) { return i < LN_RSZ ? i : i - LN_RSZ; }
 __device__ __forceinline__ int ln_wrap(int i) {
     while (i >= LN_RSZ) i -= LN_RSZ;
@@ -2030,6 +2036,9 @@ __device__ __forceinline__ void lp_wave_init(const LpArgs &a, LpWave &W, double2
 // outside [u_lo, u_hi) or past the track.  The fill is lp_val's expression term for
 // term: u (gain ramp) offset for INNER positions, u d0 offset below the ring's first
 // fill, u G_T offset for the positions FINAL emits.  One wave per 64-position block.
+#ifndef AMX_LPF_GRID
+#define AMX_LPF_GRID 65536
+#endif
 __global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t y_hi, int64_t u_lo, int64_t u_hi) {
     if ((a.ctl[0] != 0 && a.ctl[0] != 4) || a.T < 1) return;
     if (a.ctl[0] == 4) {
@@ -2045,6 +2054,7 @@ __global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t
     const int64_t b_lo = u_lo >> 6, b_hi = (u_hi + 63) >> 6;
     uint32_t *y = reinterpret_cast<uint32_t *>(a.y);
     const float4 *u4 = reinterpret_cast<const float4 *>(a.u);
+    const double2 *ramp2 = reinterpret_cast<const double2 *>(a.ramp);      // (16-B aligned: lp_fill)
     const bool small = a.n < ((int64_t)1 << 31);          // wave-uniform: 32-bit quotients
     for (int64_t b = b_lo + (((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4); b < b_hi;
          b += ((int64_t)gridDim.x * 256) >> 4) {
@@ -2054,6 +2064,9 @@ __global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t
         if (whole) {
             const float4 xa = u4[p0 >> 1], xb = u4[(p0 >> 1) + 1];     // positions p0 .. p0 + 3
             const float xs[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+            // p0, LP_RS and LP_FR are multiples of 4, so the quad's positions lie in one
+            // frame t at ramp indices i .. i + 3 (below LP_RS all four take d0): one pair of
+            // gain rows and one 32-B ramp piece per quad, every load issued before any use
             const int64_t q = p0 - LP_RS > 0 ? p0 - LP_RS : 0;
             int t, i;
             if (small) {
@@ -2063,56 +2076,54 @@ __global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t
                 t = (int)(q / LP_FR);
                 i = (int)(q - (int64_t)t * LP_FR);
             }
-            uint32_t o[4];
-            // the four positions' (frame, index) pairs, then every gain-row load issued
-            // before any is used (a load under the last frame's branch made the compiler
-            // wait at the join: eight dependent round trips per quad)
-            int tk[4], ik[4];
+            const int tc = t < a.T - 1 ? t : a.T - 1;
+            const double2 ra = ramp2[i >> 1], rb = ramp2[(i >> 1) + 1];
+            const double g0 = a.G[tc], g1 = a.G[tc + 1];
+            double rk[4] = {ra.x, ra.y, rb.x, rb.y};
+            if (!(t < a.T - 1 || a.nb_last == LP_FR)) {            // the partial last frame's ramp
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int64_t pos = p0 + k;
-                if (k > 0 && pos - LP_RS > 0 && ++i == LP_FR) {            // (positions <= LP_RS: q 0)
-                    i = 0;
-                    t++;
-                }
-                tk[k] = t;
-                ik[k] = i;
+                for (int k = 0; k < 4; k++) rk[k] = (double)(i + k) / (double)a.nb_last;
             }
-            double rk[4], g0k[4], g1k[4];
+            // below LP_RS the gain is d0: as d0 + r * 0, which is d0 exactly (a positive gain)
+            const bool below = p0 < LP_RS;
+            const double gb = below ? d0 : g0, dg = below ? 0.0 : g1 - g0;
+            double o[8];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const int tc = tk[k] < a.T - 1 ? tk[k] : a.T - 1;
-                rk[k] = a.ramp[ik[k]];
-                g0k[k] = a.G[tc];
-                g1k[k] = a.G[tc + 1];
+                const double g = gb + (rk[k] * dg);
+                o[2 * k] = ((double)xs[2 * k] * g) * off;
+                o[2 * k + 1] = ((double)xs[2 * k + 1] * g) * off;
+                mx = fmax(mx, fmax(fabs(o[2 * k]), fabs(o[2 * k + 1])));
             }
+            if (p0 + 3 >= a.S0) {                      // FINAL emits these: u G_T offset
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    if (p0 + k >= a.S0) {
+                        o[2 * k] = ((double)xs[2 * k] * gT) * off;
+                        o[2 * k + 1] = ((double)xs[2 * k + 1] * gT) * off;
+                        mxF = fmax(mxF, fmax(fabs(o[2 * k]), fabs(o[2 * k + 1])));
+                    }
+                }
+            }
+            uint32_t ow[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const int64_t pos = p0 + k;
-                const int t = tk[k], i = ik[k];
-                const double rl = (double)i / (double)a.nb_last;       // (the partial last frame's ramp)
-                const double r = (t < a.T - 1 || a.nb_last == LP_FR) ? rk[k] : rl;
-                const double g0 = g0k[k], g1 = g1k[k];
-                const double gi = g0 + (r * (g1 - g0));
-                const double g = pos < LP_RS ? d0 : gi;
-                const double v0 = ((double)xs[2 * k] * g) * off, v1 = ((double)xs[2 * k + 1] * g) * off;
-                mx = fmax(mx, fmax(fabs(v0), fabs(v1)));
-                double o0 = v0, o1 = v1;
-                if (pos >= a.S0) {                     // FINAL emits it: u G_T offset
-                    o0 = ((double)xs[2 * k] * gT) * off;
-                    o1 = ((double)xs[2 * k + 1] * gT) * off;
-                    mxF = fmax(mxF, fmax(fabs(o0), fabs(o1)));
+                int16_t h[2];
+#pragma unroll
+                for (int c = 0; c < 2; c++) {
+                    double v = o[2 * k + c];
+                    // (ceiling * +-1 is +-ceiling exactly: the sign copied instead)
+                    if (fabs(v) > ceiling) v = copysign(ceiling, v);
+                    h[c] = ln_s16_lim(v);
                 }
-                if (fabs(o0) > ceiling) o0 = ceiling * (o0 < 0 ? -1 : 1);
-                if (fabs(o1) > ceiling) o1 = ceiling * (o1 < 0 ? -1 : 1);
-                o[k] = pack2(ln_s16(o0), ln_s16(o1));
+                ow[k] = pack2(h[0], h[1]);
             }
             if (p0 >= y_lo && p0 + 4 <= y_hi) {
-                *reinterpret_cast<uint4 *>(y + p0) = make_uint4(o[0], o[1], o[2], o[3]);
+                *reinterpret_cast<uint4 *>(y + p0) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
             } else {
 #pragma unroll
                 for (int k = 0; k < 4; k++)
-                    if (p0 + k >= y_lo && p0 + k < y_hi) y[p0 + k] = o[k];
+                    if (p0 + k >= y_lo && p0 + k < y_hi) y[p0 + k] = ow[k];
             }
         } else {
             // a block edge of the window or the track: any position outside holds no fill
@@ -2306,14 +2317,20 @@ __global__ void __launch_bounds__(LP_NT) k_lp_walk(LpArgs a) {
     }
 }
 
-static void lp_fill(const LpArgs &lp, int64_t y_lo, int64_t y_hi, int64_t u_lo, int64_t u_hi, hipStream_t st) {
+static_assert(LP_RS % 4 == 0 && LP_FR % 4 == 0, "k_lp_fill: a quad of positions lies in one frame");
+static hipError_t lp_fill(const LpArgs &lp, int64_t y_lo, int64_t y_hi, int64_t u_lo, int64_t u_hi,
+                          hipStream_t st) {
+    // (the ramp's 32-B pieces: the plan's scratch is 256-B aligned)
+    if (reinterpret_cast<uintptr_t>(lp.ramp) % 16 != 0) return hipErrorInvalidValue;
     const int64_t blocks = ((u_hi + 63) >> 6) - (u_lo >> 6);
-    if (blocks <= 0) return;
-    // grid-stride over at most 4096 workgroups (a gated track's launch returns at once);
-    // a workgroup covers 16 blocks
+    if (blocks <= 0) return hipSuccess;
+    // grid-stride over at most AMX_LPF_GRID workgroups (a gated track's launch returns at
+    // once); a workgroup covers 16 blocks.  65 536 rather than 4 096: 5 us less per launch
+    // at C3 (profiles/r06ac_lp_fill_ab.txt)
     const int64_t g = (blocks + 15) / 16;
-    hipLaunchKernelGGL(k_lp_fill, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, lp, y_lo, y_hi, u_lo,
+    hipLaunchKernelGGL(k_lp_fill, dim3((unsigned)(g < AMX_LPF_GRID ? g : AMX_LPF_GRID)), dim3(256), 0, st, lp, y_lo, y_hi, u_lo,
                        u_hi);
+    return hipSuccess;
 }
 
 static void ln_upsample(const uint32_t *x, int64_t n_in, const SwrDev &r, int64_t j0, int64_t j1, float *u,
@@ -2354,8 +2371,9 @@ hipError_t launch_loudnorm(const LnArgs &ln, const LpArgs &lp, const uint32_t *x
     hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
     const int gb = max((lp.T + 1 + 255) / 256, (LP_FR + 255) / 256);
     hipLaunchKernelGGL(k_lp_gains, dim3(gb), dim3(256), 0, st, lp);
-    if (lp.bm) lp_fill(lp, 0, ln.n192, 0, ln.n192, st);
-    hipError_t e = launch_zero(lp.cnt, sizeof(int) * (size_t)(lp.K + 1), st);
+    hipError_t e = lp.bm ? lp_fill(lp, 0, ln.n192, 0, ln.n192, st) : hipSuccess;
+    if (e != hipSuccess) return e;
+    e = launch_zero(lp.cnt, sizeof(int) * (size_t)(lp.K + 1), st);
     if (e != hipSuccess) return e;
     e = launch_zero(lp.match, sizeof(int) * (size_t)(lp.K + 1), st);
     if (e != hipSuccess) return e;
@@ -2382,8 +2400,9 @@ hipError_t launch_loudnorm_shard(const LnArgs &ln, const LpArgs &lp, const uint3
         hipLaunchKernelGGL(k_lp_dscan, dim3(1), dim3(1024), 0, st, lp);
         const int gb = max((lp.T + 1 + 255) / 256, (LP_FR + 255) / 256);
         hipLaunchKernelGGL(k_lp_gains, dim3(gb), dim3(256), 0, st, lp);
-        if (lp.bm) lp_fill(lp, y_lo, y_hi, u_lo, u_hi, st);
-        hipError_t e = launch_zero(lp.cnt, sizeof(int) * (size_t)(lp.K + 1), st);
+        hipError_t e = lp.bm ? lp_fill(lp, y_lo, y_hi, u_lo, u_hi, st) : hipSuccess;
+        if (e != hipSuccess) return e;
+        e = launch_zero(lp.cnt, sizeof(int) * (size_t)(lp.K + 1), st);
         if (e != hipSuccess) return e;
         e = launch_zero(lp.match, sizeof(int) * (size_t)(lp.K + 1), st);
         if (e != hipSuccess) return e;

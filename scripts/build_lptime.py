@@ -13,7 +13,7 @@ OLD = """        if (k < kh) continue;
         const int ak = lp_seg_start(a, k), bk = k + 1 < a.K ? lp_seg_start(a, k + 1) : NF;"""
 NEW = """        if (k < kh) continue;
         const uint64_t tq0 = __builtin_amdgcn_s_memrealtime();
-        uint64_t tq2 = tq0, tq3 = tq0, tq4 = tq0;
+        uint64_t tf[7] = {0, 0, 0, 0, 0, 0, 0};
         const int ak = lp_seg_start(a, k), bk = k + 1 < a.K ? lp_seg_start(a, k + 1) : NF;"""
 OLD3 = """                if (phi == ak) {
                     lp_snapshot(a, W, a.recG + (int64_t)k * LP_REC);
@@ -22,17 +22,13 @@ OLD3 = """                if (phi == ak) {
                 lp_call(a, W, phi >= ak ? (a.bm ? 1 : 2) : 0);
             }"""
 NEW3 = """                if (phi == ak) {
-                    __syncthreads();
-                    tq2 = __builtin_amdgcn_s_memrealtime();
                     lp_snapshot(a, W, a.recG + (int64_t)k * LP_REC);
                     if (k > kh) lp_arrive(a, W, k);
-                    __syncthreads();
-                    tq3 = __builtin_amdgcn_s_memrealtime();
                 }
                 lp_call(a, W, phi >= ak ? (a.bm ? 1 : 2) : 0);
-            }
-            __syncthreads();
-            tq4 = __builtin_amdgcn_s_memrealtime();"""
+                __syncthreads();
+                if (phi - w < 7) tf[phi - w] = __builtin_amdgcn_s_memrealtime();
+            }"""
 OLD2 = """            lp_snapshot(a, W, a.recE + (int64_t)k * LP_REC);
             lp_arrive(a, W, k + 1);
         }
@@ -46,9 +42,7 @@ NEW2 = """            lp_snapshot(a, W, a.recE + (int64_t)k * LP_REC);
         if (threadIdx.x == 0) {
             a.recG[(int64_t)k * LP_REC + 8] = (double)tq0;
             a.recG[(int64_t)k * LP_REC + 9] = (double)tq1;
-            a.recG[(int64_t)k * LP_REC + 10] = (double)tq2;
-            a.recG[(int64_t)k * LP_REC + 11] = (double)tq3;
-            a.recG[(int64_t)k * LP_REC + 12] = (double)tq4;
+            for (int q = 0; q < 6; q++) a.recG[(int64_t)k * LP_REC + 10 + q] = (double)tf[q];
         }
     }
 }"""

@@ -40,18 +40,17 @@ def main():
     base = t0[ok].min()
     print("segments %d (K %d, Fs %d), kernel span %.1f us" % (ok.sum(), geo["K"], geo["Fs"], (t1[ok].max() - base) * 10e-3))
     print("segment time us: median %.1f p90 %.1f p99 %.1f max %.1f" % tuple(np.percentile(dt, [50, 90, 99, 100])))
-    t2, t3, t4 = rec[:, 10][ok], rec[:, 11][ok], rec[:, 12][ok]
-    warm = (t2 - t0[ok]) * 10e-3
-    snap = (t3 - t2) * 10e-3
-    body = (t4 - t3) * 10e-3
-    tail = (t1[ok] - t4) * 10e-3
-    for name, v in (("warm-up frames", warm), ("snapshot + arrive at the start", snap),
-                    ("the segment's frames", body), ("end: refill, snapshot, arrive", tail)):
-        print("  %-32s median %6.1f p90 %6.1f max %6.1f us" % ((name,) + tuple(np.percentile(v, [50, 90, 100]))))
+    tf = rec[:, 10:16][ok]
     order = np.argsort(-dt)[:15]
     for i in order:
-        print("  k %4d  start %7.1f  dt %7.1f us  warm %6.1f snap %6.1f body %6.1f tail %6.1f" % (
-            ks[i], (t0[ok][i] - base) * 10e-3, dt[i], warm[i], snap[i], body[i], tail[i]))
+        prev = t0[ok][i]
+        fr = []
+        for q in range(6):
+            if tf[i, q] > 0:
+                fr.append((tf[i, q] - prev) * 10e-3)
+                prev = tf[i, q]
+        print("  k %4d  dt %7.1f us  frames (warm-up 2, then the segment's):" % (ks[i], dt[i]),
+              " ".join("%6.1f" % v for v in fr), " tail %6.1f" % ((t1[ok][i] - prev) * 10e-3))
 
 
 if __name__ == "__main__":
