@@ -72,7 +72,8 @@ typedef unsigned lp_u4 __attribute__((ext_vector_type(4)));
 
 // ln_dot with the 8 chains as 4 packed pairs (v_pk_fma_f32 / v_pk_add_f32): the same
 // operations lane by lane, the first term a fused multiply-add onto 0 as in ln_dot
-__device__ __forceinline__ float ln_dot2(const float *w, const float *__restrict__ h) {
+template <class P>
+__device__ __forceinline__ float ln_dot2(const float *w, P h) {
     ln_f2 acc4[4];
 #pragma unroll
     for (int k = 0; k < 8; k += 2) {
@@ -101,6 +102,9 @@ __device__ __forceinline__ float ln_dot2(const float *w, const float *__restrict
 #ifndef AMX_LN_UPS_LDS
 #define AMX_LN_UPS_LDS 1
 #endif
+#ifndef AMX_LN_UPS_PH
+#define AMX_LN_UPS_PH 1
+#endif
 template <int L>
 __global__ void __launch_bounds__(AMX_BLOCK) k_ln_up_static(const uint32_t *__restrict__ x, int64_t n_in,
                                                             const float *__restrict__ bank, int64_t j0, int64_t j1,
@@ -110,6 +114,8 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_ln_up_static(const uint32_t *__re
     constexpr bool STAGE = AMX_LN_UPS_LDS && (L % 2 == 0);
     constexpr int TF = 2 * L * LN_UPF;                 // floats a thread produces
     __shared__ __attribute__((aligned(16))) float s_o[STAGE ? AMX_BLOCK * TF : 4];
+
+
     const int64_t f0 = j0 / L, f1 = (j1 + L - 1) / L;
     const int64_t nblk = (f1 - f0 + LN_UPF - 1) / LN_UPF;
     // workgroup-uniform iterations (the staged stores need the barriers)
@@ -152,15 +158,32 @@ __global__ void __launch_bounds__(AMX_BLOCK) k_ln_up_static(const uint32_t *__re
         const int64_t fw = f0 + b0 * LN_UPF;
         const bool whole = STAGE && b0 + AMX_BLOCK <= nblk && fw * L >= j0 &&
                            (fw + (int64_t)AMX_BLOCK * LN_UPF) * L <= j1 && fw + (int64_t)AMX_BLOCK * LN_UPF <= f1;
+#if AMX_LN_UPS_PH
+        // a (frame, phase)'s 32 bank taps are scalar operands loaded just before its two
+        // dots: the load address depends on the previous dot's result, so the compiler
+        // cannot hoist every frame's and phase's taps together (all 32 L at once: 128 SGPRs
+        // at L = 4, spilled to VGPR lanes, 332 v_readlane per pass beside 512 v_pk_fma)
+        typedef const __attribute__((address_space(4))) float *ConstF;
+        float dep = 0.0f;
+#endif
 #pragma unroll
         for (int k = 0; k < LN_UPF; k++) {
             const int64_t f = fb + k;
             float o[2 * L];
 #pragma unroll
             for (int ph = 0; ph < L; ph++) {
+#if AMX_LN_UPS_PH
+                uint64_t bp = reinterpret_cast<uint64_t>(bank + ph * LN_TAPS);
+                asm volatile("" : "+s"(bp) : "v"(dep));
+                const ConstF h = (ConstF)bp;
+#else
                 const float *h = bank + ph * LN_TAPS;
+#endif
                 o[2 * ph] = ln_dot2(w0 + k, h);
                 o[2 * ph + 1] = ln_dot2(w1 + k, h);
+#if AMX_LN_UPS_PH
+                dep = o[2 * ph + 1];
+#endif
             }
             if constexpr (STAGE) {
                 if (whole) {
@@ -2111,9 +2134,9 @@ __global__ void __launch_bounds__(256) k_lp_fill(LpArgs a, int64_t y_lo, int64_t
                 int16_t h[2];
 #pragma unroll
                 for (int c = 0; c < 2; c++) {
-                    double v = o[2 * k + c];
-                    // (ceiling * +-1 is +-ceiling exactly: the sign copied instead)
-                    if (fabs(v) > ceiling) v = copysign(ceiling, v);
+                    // |v| > ceiling -> ceiling * sign (+-ceiling exactly) as one fmax / fmin
+                    // pair (an in-range v, -0 included, passes unchanged)
+                    const double v = fmin(fmax(o[2 * k + c], -ceiling), ceiling);
                     h[c] = ln_s16_lim(v);
                 }
                 ow[k] = pack2(h[0], h[1]);
