@@ -1486,13 +1486,16 @@ __device__ __forceinline__ void lp_refill(const LpArgs &a, LpWave &W, int phi) {
 #ifndef AMX_LP_ENV_SYNC1
 #define AMX_LP_ENV_SYNC1 1
 #endif
+#ifndef AMX_LP_EG
+#define AMX_LP_EG 4              // groups of LP_NT slots per envelope pass (one memory round trip)
+#endif
 template <class F>
 __device__ __forceinline__ void lp_env(const LpArgs &a, LpWave &W, int e0, int k, F env) {
-    for (int i00 = 0; i00 < k; i00 += 4 * LP_NT) {
-        double2 v[4];
-        int s[4];
+    for (int i00 = 0; i00 < k; i00 += AMX_LP_EG * LP_NT) {
+        double2 v[AMX_LP_EG];
+        int s[AMX_LP_EG];
 #pragma unroll
-        for (int p = 0; p < 4; p++) {
+        for (int p = 0; p < AMX_LP_EG; p++) {
             const int i = i00 + LP_NT * p + (int)threadIdx.x;
             int ss = e0 + i;
             if (ss >= LP_RS) ss -= LP_RS;
@@ -1500,7 +1503,7 @@ __device__ __forceinline__ void lp_env(const LpArgs &a, LpWave &W, int e0, int k
             v[p] = lp_val(a, W, ss);                       // (i >= k: read, unused)
         }
 #pragma unroll
-        for (int p = 0; p < 4; p++) {
+        for (int p = 0; p < AMX_LP_EG; p++) {
             const int i = i00 + LP_NT * p + (int)threadIdx.x;
             if (i < k) {
                 const double g = env(i);
