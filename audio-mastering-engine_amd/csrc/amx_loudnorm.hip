@@ -1724,9 +1724,69 @@ __device__ __forceinline__ unsigned lp_range_bits(int w, int lo, int len) {
 }
 
 // the output of the frame where k_lp_fill already wrote every position's unlimited
-// value: only the slots the limiter multiplied differ -- their ring values, clamped, s16
-// (a frame with many of them emits densely)
+// value: only the slots the limiter multiplied differ -- their ring values, clamped, s16.
+// AMX_LP_EMIT_RANGE (default): the frame positions from the first to the last flagged
+// one, a lane per position and AMX_LP_EM groups of LP_NT per pass, each lane loading its
+// ring slot unconditionally (slot 0 when unflagged) and storing only a flagged one -- one
+// memory round trip per pass.  The per-word form below walked a word's set bits with a
+// load each: a burst frame's thousands of flagged slots cost ~50 us of dependent loads
+#ifndef AMX_LP_EMIT_RANGE
+#define AMX_LP_EMIT_RANGE 1
+#endif
+#ifndef AMX_LP_EM
+#define AMX_LP_EM 8
+#endif
+__device__ __forceinline__ void lp_emit_range(const LpArgs &a, const LpWave &W) {
+    const int nb = W.f.nb, lbi = W.f.lbi;
+    // the first and last flagged frame positions (i = slot - lbi mod LP_RS, i < nb).  The
+    // frame's range (nb <= LP_FR, far below LP_RS - 32) never holds both ends of itself in
+    // one word, so i rises with the slot inside a masked word: its lowest and highest set
+    // bits give its extremes
+    int lo = nb, hi = -1;
+    for (int w = threadIdx.x; w < LP_FW; w += LP_NT) {
+        const unsigned m = W.flags[w] & lp_range_bits(w, lbi, nb);
+        if (m) {
+            int i0 = 32 * w + __ffs(m) - 1 - lbi, i1 = 32 * w + 31 - __clz(m) - lbi;
+            if (i0 < 0) i0 += LP_RS;
+            if (i1 < 0) i1 += LP_RS;
+            lo = min(lo, i0);
+            hi = max(hi, i1);
+        }
+    }
+    lo = -(int)lp_wg_max(W, -(double)lo);
+    hi = (int)lp_wg_max(W, (double)hi);
+    if (hi < lo) return;
+    const double ceiling = a.ceiling;
+    uint32_t *y = reinterpret_cast<uint32_t *>(a.y);
+    for (int i00 = lo; i00 <= hi; i00 += AMX_LP_EM * LP_NT) {
+        double2 v[AMX_LP_EM];
+        bool fl[AMX_LP_EM];
+#pragma unroll
+        for (int p = 0; p < AMX_LP_EM; p++) {
+            const int i = i00 + LP_NT * p + (int)threadIdx.x;
+            int sl = lbi + i;
+            if (sl >= LP_RS) sl -= LP_RS;
+            fl[p] = i <= hi && lp_flag(W, sl < LP_RS ? sl : 0);
+            v[p] = W.ring[fl[p] ? sl : 0];
+        }
+#pragma unroll
+        for (int p = 0; p < AMX_LP_EM; p++) {
+            if (fl[p]) {
+                const int i = i00 + LP_NT * p + (int)threadIdx.x;
+                double o0 = v[p].x, o1 = v[p].y;
+                if (fabs(o0) > ceiling) o0 = ceiling * (o0 < 0 ? -1 : 1);
+                if (fabs(o1) > ceiling) o1 = ceiling * (o1 < 0 ? -1 : 1);
+                y[W.f.base + i] = pack2(ln_s16(o0), ln_s16(o1));
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ void lp_emit_sparse(const LpArgs &a, const LpWave &W) {
+#if AMX_LP_EMIT_RANGE
+    lp_emit_range(a, W);
+    return;
+#endif
     const int nb = W.f.nb, lbi = W.f.lbi;
     int cnt = 0;
     for (int w = threadIdx.x; w < LP_FW; w += LP_NT) cnt += __popc(W.flags[w] & lp_range_bits(w, lbi, nb));
